@@ -1,0 +1,69 @@
+// gsm_internal.h -- host-side launchers for the gfx950 kernels (gsm_kernels.hip) and
+// the radix sort (gsm_sort.hip).  Every launcher only enqueues on `stream`.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+#include "gsm_types.h"
+
+namespace gsm {
+
+// Scalars the projection/assignment kernels read (kernel argument, by value).
+struct ProjectArgs {
+    CameraUniforms cam;
+    TileBinningParams bin;
+    uint32_t rowBegin, rowEnd;  // slab of tile rows; full frame = [0, tilesY)
+    uint32_t count;
+    uint32_t maxAssignments;
+};
+
+// Device buffers of one renderer (the GlobalViewResources analogue, GlobalResources.swift:6-362).
+struct DeviceArena {
+    GaussianRenderData* renderData = nullptr;  // [maxG]
+    short4* bounds = nullptr;                  // [maxG]
+    BlendRecordA* recA = nullptr;              // [maxG]
+    uint32_t* recB = nullptr;                  // [maxG]
+    uint32_t* tileCounts = nullptr;            // [maxG]
+    uint32_t* blockSums = nullptr;             // [ceil(maxG/256) + 1]
+    TileAssignmentHeader* header = nullptr;    // [1]
+    uint32_t* keys[2] = {nullptr, nullptr};    // [cap] ping-pong
+    uint32_t* vals[2] = {nullptr, nullptr};    // [cap]
+    uint32_t* keysKeep = nullptr;              // [cap] unsorted copy (profiling/debug only)
+    uint32_t* valsKeep = nullptr;
+    uint32_t* radixHist = nullptr;             // [256 * radixGrid]
+    uint32_t* radixBinTotals = nullptr;        // [256]
+    GaussianHeader* headers = nullptr;         // [tileCount]
+    uint32_t* tileQueue = nullptr;             // [1] blend work counter
+    uint16_t* expTable = nullptr;              // [65536]
+    float2* sincosTable = nullptr;             // [65536]
+};
+
+constexpr int kProjectBlock = 256;
+constexpr int kRadixBlock = 256;
+constexpr int kRadixItems = 8;  // keys per thread per chunk
+constexpr int kRadixChunk = kRadixBlock * kRadixItems;
+
+// project + cull + SH + tile count + per-block count sums (GlobalShaders.metal:19-123, 563-616)
+void launch_project(bool halfInput, uint32_t shDegree, const void* world, const void* harmonics,
+                    const ProjectArgs& args, const DeviceArena& A, hipStream_t stream);
+// exclusive scan of the per-block sums, total + clamp into the header (GlobalShaders.metal:685-712)
+void launch_scan_blocks(uint32_t numBlocks, const ProjectArgs& args, const DeviceArena& A,
+                        hipStream_t stream);
+// duplicate-with-keys (GlobalShaders.metal:623-678 fused with :266-295)
+void launch_scatter(const ProjectArgs& args, const DeviceArena& A, hipStream_t stream);
+// per-tile binary search headers (GlobalShaders.metal:304-363), tiles of rows [rowBegin,rowEnd)
+void launch_headers(const uint32_t* sortedKeys, const FrameGeometry& geo, const DeviceArena& A,
+                    hipStream_t stream);
+// front-to-back fp16 blend + clear (GlobalShaders.metal:140-154, 1030-1187)
+void launch_blend(const uint32_t* sortedVals, const FrameGeometry& geo, const DeviceArena& A,
+                  void* color, size_t colorPitch, void* depth, size_t depthPitch, int numCUs,
+                  hipStream_t stream);
+
+// Stable LSD radix sort of (key, value) pairs; n read from device memory *nPtr.
+// Returns the index (0/1) of the ping-pong buffer holding the result.
+int radix_sort_pairs(uint32_t* keys[2], uint32_t* vals[2], const uint32_t* nPtr, uint32_t capacity,
+                     int firstDigit, int numDigits, uint32_t* hist, uint32_t* binTotals,
+                     hipStream_t stream);
+uint32_t radix_grid_for_capacity(uint32_t capacity);
+
+}  // namespace gsm

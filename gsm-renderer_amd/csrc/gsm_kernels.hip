@@ -1,0 +1,974 @@
+// gsm_kernels.hip -- gfx950 kernels of the GlobalRenderer frame (except the sort).
+//
+// Reference: Sources/Renderer/GlobalRenderer/GlobalShaders.metal and
+// Sources/Renderer/Shared/GaussianShared.h (paths relative to the reference root).
+// Numeric contract: DESIGN.md (built with -ffp-contract=off, IEEE div/sqrt).
+#include <hip/hip_runtime.h>
+
+#include "gsm_detmath.h"
+#include "gsm_internal.h"
+#include "gsm_types.h"
+
+namespace gsm {
+
+typedef _Float16 h1;
+typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ float hbits_to_f(uint16_t b) { return (float)__builtin_bit_cast(h1, b); }
+__device__ __forceinline__ uint16_t f_to_hbits(float f) { return __builtin_bit_cast(uint16_t, (h1)f); }
+
+__device__ __forceinline__ float clampf(float v, float lo, float hi) {
+    return __builtin_fminf(__builtin_fmaxf(v, lo), hi);
+}
+
+// ---------------------------------------------------------------------------
+// small column-major matrix helpers (simd / Metal layout)
+// ---------------------------------------------------------------------------
+struct M3 {
+    float m[3][3];  // m[col][row]
+};
+
+__device__ __forceinline__ M3 m3_mul(const M3& A, const M3& B) {
+    M3 R;
+#pragma unroll
+    for (int c = 0; c < 3; ++c)
+#pragma unroll
+        for (int r = 0; r < 3; ++r) {
+            float acc = A.m[0][r] * B.m[c][0];
+            acc = acc + A.m[1][r] * B.m[c][1];
+            acc = acc + A.m[2][r] * B.m[c][2];
+            R.m[c][r] = acc;
+        }
+    return R;
+}
+
+// float4x4 * float4 (column-major): sum_j col_j * v_j left to right.
+__device__ __forceinline__ void m4_mul_v(const float* M, const float v[4], float out[4]) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        float acc = M[0 * 4 + i] * v[0];
+        acc = acc + M[1 * 4 + i] * v[1];
+        acc = acc + M[2 * 4 + i] * v[2];
+        acc = acc + M[3 * 4 + i] * v[3];
+        out[i] = acc;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// GaussianShared.h pieces
+// ---------------------------------------------------------------------------
+struct Cov2 {
+    float a, b, c, d;  // col0 = (a, b), col1 = (c, d)
+};
+
+// conicFromThetaSigmas (GaussianShared.h:490-510) for a quantised angle.
+struct Conic {
+    float A, B, C;
+};
+__device__ __forceinline__ Conic conic_from_quant(const float2* __restrict__ sincos, uint16_t thq,
+                                                  float sigma1, float sigma2) {
+    float2 sc = sincos[thq];
+    float s = sc.x, c = sc.y;
+    float sig1 = __builtin_fmaxf(sigma1, 1e-4f);
+    float sig2 = __builtin_fmaxf(sigma2, 1e-4f);
+    float iv1 = 1.0f / (sig1 * sig1);
+    float iv2 = 1.0f / (sig2 * sig2);
+    float cc = c * c, ss = s * s, cs = c * s;
+    Conic k;
+    k.A = cc * iv1 + ss * iv2;
+    k.B = cs * (iv1 - iv2);
+    k.C = ss * iv1 + cc * iv2;
+    return k;
+}
+
+// gaussianComputePower (GaussianShared.h:595-597).
+__device__ __forceinline__ float compute_power(float opacity) {
+    const float LN2 = 0.693147180559945f;
+    return LN2 * 8.0f + LN2 * det_log2f(__builtin_fmaxf(opacity, 1e-6f));
+}
+
+// gaussianSegmentIntersectEllipse .. intersectsTile (GaussianShared.h:599-653).
+__device__ __forceinline__ bool seg_ellipse(float a, float b, float c, float d, float l, float r) {
+    float delta = b * b - 4.0f * a * c;
+    float t1 = (l - d) * (2.0f * a) + b;
+    float t2 = (r - d) * (2.0f * a) + b;
+    return delta >= 0.0f && (t1 <= 0.0f || t1 * t1 <= delta) && (t2 >= 0.0f || t2 * t2 <= delta);
+}
+__device__ __forceinline__ bool intersects_tile(int tx, int ty, float cx, float cy, const Conic& k,
+                                                float w) {
+    const int pminx = tx * (int)kTileWidth, pminy = ty * (int)kTileHeight;
+    const int pmaxx = pminx + (int)kTileWidth - 1, pmaxy = pminy + (int)kTileHeight - 1;
+    if (cx >= (float)pminx && cx <= (float)pmaxx && cy >= (float)pminy && cy <= (float)pmaxy)
+        return true;
+    float dx = (cx * 2.0f < (float)(pminx + pmaxx)) ? cx - (float)pminx : cx - (float)pmaxx;
+    if (seg_ellipse(k.C, -2.0f * k.B * dx, k.A * dx * dx - w, cy, (float)pminy, (float)pmaxy))
+        return true;
+    float dy = (cy * 2.0f < (float)(pminy + pmaxy)) ? cy - (float)pminy : cy - (float)pmaxy;
+    if (seg_ellipse(k.A, -2.0f * k.B * dy, k.C * dy * dy - w, cx, (float)pminx, (float)pmaxx))
+        return true;
+    return false;
+}
+
+constexpr float SH_C0 = 0.28209479177387814f;
+constexpr float SH_C1 = 0.4886025119029199f;
+constexpr float SH_C2_0 = 1.0925484305920792f;
+constexpr float SH_C2_1 = -1.0925484305920792f;
+constexpr float SH_C2_2 = 0.31539156525252005f;
+constexpr float SH_C2_3 = -1.0925484305920792f;
+constexpr float SH_C2_4 = 0.5462742152960396f;
+constexpr float SH_C3_0 = -0.5900435899266435f;
+constexpr float SH_C3_1 = 2.890611442640554f;
+constexpr float SH_C3_2 = -0.4570457994644658f;
+constexpr float SH_C3_3 = 0.3731763325901154f;
+constexpr float SH_C3_4 = -0.4570457994644658f;
+constexpr float SH_C3_5 = 1.445305721320277f;
+constexpr float SH_C3_6 = -0.5900435899266435f;
+
+template <bool HALF>
+__device__ __forceinline__ float load_harm(const void* __restrict__ h, size_t i) {
+    if constexpr (HALF) {
+        return hbits_to_f(((const uint16_t*)h)[i]);
+    } else {
+        return ((const float*)h)[i];
+    }
+}
+
+// computeSHColor (GaussianShared.h:38-116) specialised by degree like the
+// SH_DEGREE function constant (GlobalProjectCullEncoder.swift:19-45).
+template <bool HALF, int DEG>
+__device__ __forceinline__ void sh_color(const void* __restrict__ harm, uint32_t gid,
+                                         const float pos[3], const float cam[3], uint32_t shk,
+                                         float col[3]) {
+    if (DEG == 0 || shk == 0) {
+        const size_t base = (size_t)gid * 3u;
+        col[0] = load_harm<HALF>(harm, base) * SH_C0;
+        col[1] = load_harm<HALF>(harm, base + 1) * SH_C0;
+        col[2] = load_harm<HALF>(harm, base + 2) * SH_C0;
+        return;
+    }
+    constexpr int K = DEG == 1 ? 4 : (DEG == 2 ? 9 : 16);
+    float d0 = cam[0] - pos[0], d1 = cam[1] - pos[1], d2 = cam[2] - pos[2];
+    float dd = d0 * d0 + d1 * d1;
+    dd = dd + d2 * d2;
+    float n = __builtin_sqrtf(dd);
+    float x = d0 / n, y = d1 / n, z = d2 / n;
+    float xx = x * x, yy = y * y, zz = z * z;
+    float xy = x * y, yz = y * z, xz = x * z;
+    float b[16];
+    b[0] = SH_C0;
+    b[1] = (-SH_C1) * y;
+    b[2] = SH_C1 * z;
+    b[3] = (-SH_C1) * x;
+    if constexpr (DEG >= 2) {
+        b[4] = SH_C2_0 * xy;
+        b[5] = SH_C2_1 * yz;
+        b[6] = SH_C2_2 * ((2.0f * zz - xx) - yy);
+        b[7] = SH_C2_3 * xz;
+        b[8] = SH_C2_4 * (xx - yy);
+    }
+    if constexpr (DEG >= 3) {
+        b[9] = (SH_C3_0 * y) * (3.0f * xx - yy);
+        b[10] = (SH_C3_1 * xy) * z;
+        b[11] = (SH_C3_2 * y) * ((4.0f * zz - xx) - yy);
+        b[12] = (SH_C3_3 * z) * ((2.0f * zz - 3.0f * xx) - 3.0f * yy);
+        b[13] = (SH_C3_4 * x) * ((4.0f * zz - xx) - yy);
+        b[14] = (SH_C3_5 * z) * (xx - yy);
+        b[15] = (SH_C3_6 * x) * (xx - 3.0f * yy);
+    }
+    const size_t base = (size_t)gid * (size_t)K * 3u;
+    float cr = 0.0f, cg = 0.0f, cb = 0.0f;
+    if constexpr (HALF && DEG == 3) {
+        // 96 B per gaussian, 16-B aligned: six dwordx4 loads.
+        const uint4* p = (const uint4*)((const uint16_t*)harm + base);
+        uint16_t hv[48];
+#pragma unroll
+        for (int q = 0; q < 6; ++q) {
+            uint4 v = p[q];
+            uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                hv[q * 8 + 2 * t] = (uint16_t)(w[t] & 0xFFFFu);
+                hv[q * 8 + 2 * t + 1] = (uint16_t)(w[t] >> 16);
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            cr = cr + hbits_to_f(hv[i]) * b[i];
+            cg = cg + hbits_to_f(hv[16 + i]) * b[i];
+            cb = cb + hbits_to_f(hv[32 + i]) * b[i];
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < K; ++i) {
+            cr = cr + load_harm<HALF>(harm, base + i) * b[i];
+            cg = cg + load_harm<HALF>(harm, base + K + i) * b[i];
+            cb = cb + load_harm<HALF>(harm, base + 2 * K + i) * b[i];
+        }
+    }
+    col[0] = cr;
+    col[1] = cg;
+    col[2] = cb;
+}
+
+// srgbToLinearChannel (GaussianShared.h:118-121).
+__device__ __forceinline__ float srgb_to_linear(float c) {
+    c = clampf(c, 0.0f, 1.0f);
+    return (c <= 0.04045f) ? (c / 12.92f) : det_powrf((c + 0.055f) / 1.055f, 2.4f);
+}
+
+__device__ __forceinline__ float fmod_pi(float t) {
+    // fmod(t, pi_f) for |t| < 2 pi_f (atan2 range): exact by Sterbenz.
+    float a = __builtin_fabsf(t);
+    if (a >= kPiF) {
+        float r = a - kPiF;
+        return __builtin_copysignf(r, t);
+    }
+    return t;
+}
+
+template <int BLOCK>
+__device__ __forceinline__ uint32_t block_reduce_add(uint32_t v, uint32_t* lds) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    if (lane == 0) lds[wave] = v;
+    __syncthreads();
+    uint32_t s = 0;
+#pragma unroll
+    for (int w = 0; w < BLOCK / 64; ++w) s += lds[w];
+    return s;
+}
+
+// Inclusive scan inside a wave of 64 lanes.
+__device__ __forceinline__ uint32_t wave_inclusive_scan(uint32_t v) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        uint32_t t = __shfl_up(v, o, 64);
+        if (lane >= o) v += t;
+    }
+    return v;
+}
+// Exclusive scan over a block; returns the block total in *total.
+template <int BLOCK>
+__device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t v, uint32_t* lds, uint32_t* total) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint32_t inc = wave_inclusive_scan(v);
+    if (lane == 63) lds[wave] = inc;
+    __syncthreads();
+    uint32_t off = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < BLOCK / 64; ++w) {
+        uint32_t s = lds[w];
+        if (w < wave) off += s;
+        tot += s;
+    }
+    __syncthreads();
+    *total = tot;
+    return off + inc - v;
+}
+
+// ---------------------------------------------------------------------------
+// 1. project + cull + SH colour + tile count  (globalProjectCull, GlobalShaders.metal:19-123;
+//    tileCountIndirectKernel, :563-616)
+// ---------------------------------------------------------------------------
+template <bool HALF, int DEG>
+__global__ __launch_bounds__(kProjectBlock) void k_project(
+    const void* __restrict__ world, const void* __restrict__ harm, ProjectArgs P,
+    GaussianRenderData* __restrict__ outRD, short4* __restrict__ outBounds,
+    BlendRecordA* __restrict__ outA, uint32_t* __restrict__ outB, uint32_t* __restrict__ counts,
+    uint32_t* __restrict__ blockSums, const float2* __restrict__ sincos) {
+    __shared__ uint32_t lds[kProjectBlock / 64];
+    const uint32_t gid = blockIdx.x * kProjectBlock + threadIdx.x;
+    uint32_t ntiles = 0;
+    if (gid < P.count) {
+        const CameraUniforms& cam = P.cam;
+        float pos[3], scale[3], rot[4], opacity;
+        if constexpr (HALF) {
+            const uint4* wp = (const uint4*)((const PackedWorldGaussianHalf*)world + gid);
+            uint4 w0 = wp[0], w1 = wp[1];
+            pos[0] = __builtin_bit_cast(float, w0.x);
+            pos[1] = __builtin_bit_cast(float, w0.y);
+            pos[2] = __builtin_bit_cast(float, w0.z);
+            opacity = hbits_to_f((uint16_t)(w0.w & 0xFFFFu));
+            scale[0] = hbits_to_f((uint16_t)(w0.w >> 16));
+            scale[1] = hbits_to_f((uint16_t)(w1.x & 0xFFFFu));
+            scale[2] = hbits_to_f((uint16_t)(w1.x >> 16));
+            rot[0] = hbits_to_f((uint16_t)(w1.y & 0xFFFFu));
+            rot[1] = hbits_to_f((uint16_t)(w1.y >> 16));
+            rot[2] = hbits_to_f((uint16_t)(w1.z & 0xFFFFu));
+            rot[3] = hbits_to_f((uint16_t)(w1.z >> 16));
+        } else {
+            const float4* wp = (const float4*)((const PackedWorldGaussian*)world + gid);
+            float4 w0 = wp[0], w1 = wp[1], w2 = wp[2];
+            pos[0] = w0.x; pos[1] = w0.y; pos[2] = w0.z; opacity = w0.w;
+            scale[0] = w1.x; scale[1] = w1.y; scale[2] = w1.z;
+            rot[0] = w2.x; rot[1] = w2.y; rot[2] = w2.z; rot[3] = w2.w;
+        }
+        bool vis = true;
+        // cullByScale (GaussianShared.h:719-722)
+        if (__builtin_fmaxf(scale[0], __builtin_fmaxf(scale[1], scale[2])) < 0.0005f) vis = false;
+        float vp[4], clip[4];
+        if (vis) {
+            const float p4[4] = {pos[0], pos[1], pos[2], 1.0f};
+            m4_mul_v(cam.view, p4, vp);
+            m4_mul_v(cam.proj, vp, clip);
+            if (!(clip[3] > cam.nearPlane)) vis = false;  // isInFrontOfCameraClipW
+        }
+        float sx = 0.f, sy = 0.f;
+        if (vis) {
+            float ndcx = clip[0] / clip[3], ndcy = clip[1] / clip[3];
+            sx = ((ndcx + 1.0f) * cam.width - 1.0f) * 0.5f;  // ndcToScreenCentered
+            sy = ((ndcy + 1.0f) * cam.height - 1.0f) * 0.5f;
+            if (opacity < P.bin.alphaThreshold) vis = false;
+        }
+        Cov2 cov;
+        float theta = 0.f, s1 = 0.f, s2 = 0.f;
+        if (vis) {
+            // normalizeQuaternion (GaussianShared.h:289-295), applied twice (:64 and :308)
+            float q[4] = {rot[0], rot[1], rot[2], rot[3]};
+#pragma unroll
+            for (int pass = 0; pass < 2; ++pass) {
+                float d = q[0] * q[0] + q[1] * q[1];
+                d = d + q[2] * q[2];
+                d = d + q[3] * q[3];
+                float nrm = __builtin_sqrtf(__builtin_fmaxf(d, 1e-8f));
+                if (nrm < 1e-8f) {
+                    q[0] = 1.0f; q[1] = 0.0f; q[2] = 0.0f; q[3] = 0.0f;
+                } else {
+                    q[0] = q[0] / nrm; q[1] = q[1] / nrm; q[2] = q[2] / nrm; q[3] = q[3] / nrm;
+                }
+            }
+            // quaternionToMatrix (GaussianShared.h:297-305)
+            float x = q[0], y = q[1], z = q[2], r = q[3];
+            float xx = x * x, yy = y * y, zz = z * z, xy = x * y, xz = x * z, yz = y * z;
+            M3 R;
+            R.m[0][0] = 1.0f - 2.0f * (yy + zz); R.m[1][0] = 2.0f * (xy - r * z); R.m[2][0] = 2.0f * (xz + r * y);
+            R.m[0][1] = 2.0f * (xy + r * z); R.m[1][1] = 1.0f - 2.0f * (xx + zz); R.m[2][1] = 2.0f * (yz - r * x);
+            R.m[0][2] = 2.0f * (xz - r * y); R.m[1][2] = 2.0f * (yz + r * x); R.m[2][2] = 1.0f - 2.0f * (xx + yy);
+            // buildCovariance3D (GaussianShared.h:307-324)
+            float RS[3][3];
+#pragma unroll
+            for (int c = 0; c < 3; ++c)
+#pragma unroll
+                for (int rr = 0; rr < 3; ++rr) RS[c][rr] = R.m[c][rr] * scale[c];
+            M3 C3;
+#pragma unroll
+            for (int c = 0; c < 3; ++c)
+#pragma unroll
+                for (int rr = 0; rr < 3; ++rr)
+                    C3.m[c][rr] = (RS[0][c] * RS[0][rr] + RS[1][c] * RS[1][rr]) + RS[2][c] * RS[2][rr];
+            // projectCovariance2D (GaussianShared.h:326-375)
+            M3 W;
+#pragma unroll
+            for (int c = 0; c < 3; ++c)
+#pragma unroll
+                for (int rr = 0; rr < 3; ++rr) W.m[c][rr] = cam.view[c * 4 + rr];
+            float absZ = __builtin_fabsf(vp[2]);
+            float signZ = (vp[2] >= 0.0f) ? 1.0f : -1.0f;
+            float safeAbsZ = __builtin_fmaxf(absZ, 1e-4f);
+            float invAbsZ = 1.0f / safeAbsZ;
+            float invAbsZ2 = invAbsZ * invAbsZ;
+            float p00 = cam.proj[0], p11 = cam.proj[5];
+            float limX = 1.3f * (1.0f / __builtin_fmaxf(__builtin_fabsf(p00), 1e-4f));
+            float limY = 1.3f * (1.0f / __builtin_fmaxf(__builtin_fabsf(p11), 1e-4f));
+            float xCl = clampf(vp[0] * invAbsZ, -limX, limX) * safeAbsZ;
+            float yCl = clampf(vp[1] * invAbsZ, -limY, limY) * safeAbsZ;
+            float focalX = cam.width * __builtin_fabsf(p00) * 0.5f;
+            float focalY = cam.height * __builtin_fabsf(p11) * 0.5f;
+            M3 J;
+            J.m[0][0] = focalX * invAbsZ; J.m[0][1] = 0.0f; J.m[0][2] = 0.0f;
+            J.m[1][0] = 0.0f; J.m[1][1] = focalY * invAbsZ; J.m[1][2] = 0.0f;
+            J.m[2][0] = -focalX * xCl * signZ * invAbsZ2;
+            J.m[2][1] = -focalY * yCl * signZ * invAbsZ2;
+            J.m[2][2] = 0.0f;
+            M3 T = m3_mul(J, W);
+            M3 M1 = m3_mul(T, C3);
+            M3 Tt;
+#pragma unroll
+            for (int c = 0; c < 3; ++c)
+#pragma unroll
+                for (int rr = 0; rr < 3; ++rr) Tt.m[c][rr] = T.m[rr][c];
+            M3 F = m3_mul(M1, Tt);
+            cov.a = F.m[0][0] + 0.3f;
+            cov.b = F.m[0][1];
+            cov.c = F.m[1][0];
+            cov.d = F.m[1][1] + 0.3f;
+            // stabilizeCovariance2D (GaussianShared.h:655-714)
+            {
+                const float kMinVar = 1e-4f, kMinDet = 1e-8f;
+                float maxCond = 256.0f * 256.0f;
+                float maxDim = __builtin_fmaxf(cam.width, cam.height);
+                float maxEig = (maxDim * 2.0f) / 3.0f;
+                maxEig = maxEig * maxEig;
+                float a = cov.a, b = 0.5f * (cov.b + cov.c), d = cov.d;
+                if (!__builtin_isfinite(a) || !__builtin_isfinite(b) || !__builtin_isfinite(d)) {
+                    cov.a = 1.0f; cov.b = 0.0f; cov.c = 0.0f; cov.d = 1.0f;
+                } else {
+                    a = __builtin_fmaxf(a, kMinVar);
+                    d = __builtin_fmaxf(d, kMinVar);
+                    float det = a * d - b * b;
+                    if (!__builtin_isfinite(det) || det < kMinDet) {
+                        float bump = (kMinDet - det) + kMinVar;
+                        a = a + bump;
+                        d = d + bump;
+                        det = a * d - b * b;
+                    }
+                    float mid = 0.5f * (a + d);
+                    float sq = __builtin_sqrtf(__builtin_fmaxf(mid * mid - det, 0.0f));
+                    float l1 = mid + sq;
+                    float l2 = __builtin_fmaxf(mid - sq, kMinVar);
+                    float v1x, v1y;
+                    if (__builtin_fabsf(b) > 1e-8f) {
+                        float vx = b, vy = l1 - a;
+                        float dn = __builtin_fmaxf(__builtin_sqrtf(vx * vx + vy * vy), 1e-8f);
+                        v1x = vx / dn;
+                        v1y = vy / dn;
+                    } else if (a >= d) {
+                        v1x = 1.0f; v1y = 0.0f;
+                    } else {
+                        v1x = 0.0f; v1y = 1.0f;
+                    }
+                    float v2x = v1y, v2y = -v1x;
+                    l1 = __builtin_fminf(l1, maxEig);
+                    l2 = __builtin_fmaxf(l2, l1 / maxCond);
+                    cov.a = l1 * (v1x * v1x) + l2 * (v2x * v2x);
+                    cov.b = l1 * (v1x * v1y) + l2 * (v2x * v2y);
+                    cov.c = l1 * (v1y * v1x) + l2 * (v2y * v2x);
+                    cov.d = l1 * (v1y * v1y) + l2 * (v2y * v2y);
+                }
+            }
+            // covarianceToThetaSigmas (GaussianShared.h:446-488)
+            {
+                float a = cov.a, b = 0.5f * (cov.b + cov.c), d = cov.d;
+                bool ok = __builtin_isfinite(a) && __builtin_isfinite(b) && __builtin_isfinite(d);
+                if (ok) {
+                    a = __builtin_fmaxf(a, 1e-8f);
+                    d = __builtin_fmaxf(d, 1e-8f);
+                    float det = a * d - b * b;
+                    ok = __builtin_isfinite(det) && det > 0.0f;
+                    if (ok) {
+                        float mid = 0.5f * (a + d);
+                        float sq = __builtin_sqrtf(__builtin_fmaxf(mid * mid - det, 0.0f));
+                        float l1 = __builtin_fmaxf(mid + sq, 1e-8f);
+                        float l2 = __builtin_fmaxf(mid - sq, 1e-8f);
+                        float v1x, v1y;
+                        if (__builtin_fabsf(b) > 1e-8f) {
+                            float tx = b, ty = l1 - a;
+                            float nn = __builtin_sqrtf(tx * tx + ty * ty);
+                            v1x = tx / nn;
+                            v1y = ty / nn;
+                        } else if (a >= d) {
+                            v1x = 1.0f; v1y = 0.0f;
+                        } else {
+                            v1x = 0.0f; v1y = 1.0f;
+                        }
+                        float th = det_atan2f(v1y, v1x);
+                        th = fmod_pi(th);
+                        if (th < 0.0f) th = th + kPiF;
+                        if (th >= kPiF) th = th - kPiF;
+                        theta = th;
+                        s1 = __builtin_sqrtf(l1);
+                        s2 = __builtin_sqrtf(l2);
+                        ok = __builtin_isfinite(th) && __builtin_isfinite(s1) && __builtin_isfinite(s2);
+                    }
+                }
+                if (!ok) vis = false;
+            }
+        }
+        if (vis) {
+            float radius = 3.0f * __builtin_fmaxf(s1, s2);
+            if (radius < 0.5f) vis = false;  // cullByRadius
+        }
+        if (vis && P.bin.totalInkThreshold > 0.0f) {  // cullByTotalInkFromCov
+            float a = cov.a, b = 0.5f * (cov.b + cov.c), d = cov.d;
+            float det = a * d - b * b;
+            float ink = opacity * 6.283185f * __builtin_sqrtf(__builtin_fmaxf(det, 1e-12f));
+            float adjFar = cam.farPlane * 0.02f;
+            float s = clampf((adjFar - clip[3]) / (adjFar - cam.nearPlane), 0.0f, 1.0f);
+            float depthFactor = 1.0f - s * s;
+            if (ink < depthFactor * P.bin.totalInkThreshold) vis = false;
+        }
+        float ex = 0.f, ey = 0.f;
+        if (vis) {  // computeOBBExtents (GaussianShared.h:402-427)
+            float a = cov.a, b = cov.b, d = cov.d;
+            float det = a * d - b * b;
+            float mid = 0.5f * (a + d);
+            float sq = __builtin_sqrtf(__builtin_fmaxf(mid * mid - det, 1e-6f));
+            float l1 = mid + sq;
+            float l2 = __builtin_fmaxf(mid - sq, 1e-6f);
+            float e1 = 3.0f * __builtin_sqrtf(__builtin_fmaxf(l1, 1e-6f));
+            float e2 = 3.0f * __builtin_sqrtf(__builtin_fmaxf(l2, 1e-6f));
+            float v1x, v1y;
+            if (__builtin_fabsf(b) > 1e-6f) {
+                float vx = b, vy = l1 - a;
+                float dn = __builtin_fmaxf(__builtin_sqrtf(vx * vx + vy * vy), 1e-6f);
+                v1x = vx / dn;
+                v1y = vy / dn;
+            } else if (a >= d) {
+                v1x = 1.0f; v1y = 0.0f;
+            } else {
+                v1x = 0.0f; v1y = 1.0f;
+            }
+            ex = __builtin_fabsf(v1x) * e1 + __builtin_fabsf(v1y) * e2;
+            ey = __builtin_fabsf(v1y) * e1 + __builtin_fabsf(v1x) * e2;
+            // cullByScreenBounds (GaussianShared.h:771-781)
+            if (sx + ex < 0.0f || sx - ex > cam.width || sy + ey < 0.0f || sy - ey > cam.height)
+                vis = false;
+        }
+        if (!vis) {
+            outBounds[gid] = make_short4(0, -1, 0, -1);
+        } else {
+            float col[3];
+            sh_color<HALF, DEG>(harm, gid, pos, cam.cameraCenter, cam.shComponents, col);
+            col[0] = __builtin_fmaxf(col[0] + 0.5f, 0.0f);
+            col[1] = __builtin_fmaxf(col[1] + 0.5f, 0.0f);
+            col[2] = __builtin_fmaxf(col[2] + 0.5f, 0.0f);
+            if (cam.inputIsSRGB > 0.5f) {
+                col[0] = srgb_to_linear(col[0]);
+                col[1] = srgb_to_linear(col[1]);
+                col[2] = srgb_to_linear(col[2]);
+            }
+            // pack GaussianRenderData (GlobalShaders.metal:106-117), packThetaPi (GaussianShared.h:434-440)
+            float th = fmod_pi(theta);
+            if (th < 0.0f) th = th + kPiF;
+            float u = th * (65535.0f / kPiF);
+            uint16_t thq = (uint16_t)clampf(u + 0.5f, 0.0f, 65535.0f);
+            uint16_t hmx = f_to_hbits(sx), hmy = f_to_hbits(sy);
+            uint16_t hs1 = f_to_hbits(s1), hs2 = f_to_hbits(s2), hd = f_to_hbits(clip[3]);
+            uint32_t cR = (uint32_t)(uint8_t)clampf(col[0] * 255.0f, 0.0f, 255.0f);
+            uint32_t cG = (uint32_t)(uint8_t)clampf(col[1] * 255.0f, 0.0f, 255.0f);
+            uint32_t cB = (uint32_t)(uint8_t)clampf(col[2] * 255.0f, 0.0f, 255.0f);
+            uint32_t cO = (uint32_t)(uint8_t)clampf(opacity * 255.0f, 0.0f, 255.0f);
+            uint4 rdw;
+            rdw.x = (uint32_t)hmx | ((uint32_t)hmy << 16);
+            rdw.y = (uint32_t)thq | ((uint32_t)hs1 << 16);
+            rdw.z = (uint32_t)hs2 | ((uint32_t)hd << 16);
+            rdw.w = cR | (cG << 8) | (cB << 16) | (cO << 24);
+            *(uint4*)(outRD + gid) = rdw;
+
+            // computeTileBounds (GaussianShared.h:791-828)
+            float maxW = cam.width - 1.0f, maxH = cam.height - 1.0f;
+            float xmin = clampf(sx - ex, 0.0f, maxW), xmax = clampf(sx + ex, 0.0f, maxW);
+            float ymin = clampf(sy - ey, 0.0f, maxH), ymax = clampf(sy + ey, 0.0f, maxH);
+            int minTX = (int)__builtin_floorf(xmin / (float)kTileWidth);
+            int maxTX = (int)__builtin_ceilf(xmax / (float)kTileWidth) - 1;
+            int minTY = (int)__builtin_floorf(ymin / (float)kTileHeight);
+            int maxTY = (int)__builtin_ceilf(ymax / (float)kTileHeight) - 1;
+            minTX = max(minTX, 0);
+            minTY = max(minTY, 0);
+            maxTX = min(maxTX, (int)P.bin.tilesX - 1);
+            maxTY = min(maxTY, (int)P.bin.tilesY - 1);
+            outBounds[gid] = make_short4((short)minTX, (short)maxTX, (short)minTY, (short)maxTY);
+
+            // per-gaussian values of globalRender (GlobalShaders.metal:1094-1105; getColor/getOpacity :9-15)
+            float cmx = hbits_to_f(hmx), cmy = hbits_to_f(hmy);
+            Conic k = conic_from_quant(sincos, thq, hbits_to_f(hs1), hbits_to_f(hs2));
+            uint16_t hcxx = f_to_hbits(k.A), hcyy = f_to_hbits(k.C), hcxy2 = f_to_hbits(2.0f * k.B);
+            uint16_t hop = f_to_hbits((float)cO / 255.0f);
+            uint16_t hr = f_to_hbits((float)cR / 255.0f), hg = f_to_hbits((float)cG / 255.0f);
+            uint16_t hb = f_to_hbits((float)cB / 255.0f);
+            BlendRecordA ra;
+            ra.x = rdw.x;
+            ra.y = (uint32_t)hcxx | ((uint32_t)hcyy << 16);
+            ra.z = (uint32_t)hcxy2 | ((uint32_t)hop << 16);
+            ra.w = (uint32_t)hr | ((uint32_t)hg << 16);
+            outA[gid] = ra;
+            outB[gid] = (uint32_t)hb | ((uint32_t)hd << 16);
+
+            // tileCountIndirectKernel (GlobalShaders.metal:563-616), rows limited to the slab
+            float alpha = (float)cO;
+            if (alpha >= 1e-4f && minTX <= maxTX && minTY <= maxTY) {
+                float w = 2.0f * compute_power(alpha);
+                int ty0 = max(minTY, (int)P.rowBegin), ty1 = min(maxTY, (int)P.rowEnd - 1);
+                for (int ty = ty0; ty <= ty1; ++ty)
+                    for (int tx = minTX; tx <= maxTX; ++tx)
+                        if (intersects_tile(tx, ty, cmx, cmy, k, w)) ntiles++;
+            }
+        }
+        counts[gid] = ntiles;
+    }
+    uint32_t s = block_reduce_add<kProjectBlock>(ntiles, lds);
+    if (threadIdx.x == 0) blockSums[blockIdx.x] = s;
+}
+
+// ---------------------------------------------------------------------------
+// 2. exclusive scan of block sums (single workgroup) + clamp
+//    (prefix sum: TwoPassTileAssignEncoder.swift:91-196; clamp GlobalShaders.metal:694-712)
+// ---------------------------------------------------------------------------
+constexpr int kScanThreads = 1024;
+__global__ __launch_bounds__(kScanThreads) void k_scan_blocks(uint32_t* __restrict__ sums,
+                                                              uint32_t nb, uint32_t maxAssignments,
+                                                              TileAssignmentHeader* __restrict__ hdr) {
+    __shared__ uint32_t lds[kScanThreads / 64];
+    const uint32_t per = (nb + kScanThreads - 1) / kScanThreads;
+    const uint32_t b0 = threadIdx.x * per;
+    uint64_t local = 0;
+    for (uint32_t i = 0; i < per; ++i) {
+        uint32_t idx = b0 + i;
+        if (idx < nb) local += sums[idx];
+    }
+    uint32_t loc32 = local > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)local;
+    uint32_t total;
+    uint32_t off = block_exclusive_scan<kScanThreads>(loc32, lds, &total);
+    uint32_t run = off;
+    for (uint32_t i = 0; i < per; ++i) {
+        uint32_t idx = b0 + i;
+        if (idx < nb) {
+            uint32_t v = sums[idx];
+            sums[idx] = run;
+            run += v;
+        }
+    }
+    if (threadIdx.x == 0) {
+        uint32_t tot = total;
+        uint32_t ovf = 0;
+        if (tot > maxAssignments) {
+            tot = maxAssignments;
+            ovf = 1;
+        }
+        hdr->totalAssignments = tot;
+        hdr->maxCapacity = maxAssignments;
+        hdr->paddedCount = ((tot + 1023u) / 1024u) * 1024u;
+        hdr->overflow = ovf;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// 3. duplicate with keys (tileScatterIndirectKernel GlobalShaders.metal:623-678 +
+//    computeSortKeysKernel :266-295): key = tile<<16 | (fp16 depth ^ 0x8000), value = gid
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kProjectBlock) void k_scatter(
+    ProjectArgs P, const GaussianRenderData* __restrict__ rd, const short4* __restrict__ bounds,
+    const uint32_t* __restrict__ counts, const uint32_t* __restrict__ blockOffsets,
+    uint32_t* __restrict__ keys, uint32_t* __restrict__ vals, const float2* __restrict__ sincos) {
+    __shared__ uint32_t lds[kProjectBlock / 64];
+    const uint32_t gid = blockIdx.x * kProjectBlock + threadIdx.x;
+    uint32_t c = (gid < P.count) ? counts[gid] : 0u;
+    uint32_t total;
+    uint32_t off = block_exclusive_scan<kProjectBlock>(c, lds, &total);
+    if (c == 0) return;
+    uint64_t wp = (uint64_t)blockOffsets[blockIdx.x] + off;
+    if (wp >= P.maxAssignments) return;
+    const short4 r = bounds[gid];
+    uint4 rdw = *(const uint4*)(rd + gid);
+    uint16_t hmx = (uint16_t)(rdw.x & 0xFFFFu), hmy = (uint16_t)(rdw.x >> 16);
+    uint16_t thq = (uint16_t)(rdw.y & 0xFFFFu), hs1 = (uint16_t)(rdw.y >> 16);
+    uint16_t hs2 = (uint16_t)(rdw.z & 0xFFFFu), hd = (uint16_t)(rdw.z >> 16);
+    uint32_t opac = rdw.w >> 24;
+    float cx = hbits_to_f(hmx), cy = hbits_to_f(hmy);
+    Conic k = conic_from_quant(sincos, thq, hbits_to_f(hs1), hbits_to_f(hs2));
+    float w = 2.0f * compute_power((float)opac);
+    const uint32_t dbits = ((uint32_t)hd ^ 0x8000u) & 0xFFFFu;
+    int ty0 = max((int)r.z, (int)P.rowBegin), ty1 = min((int)r.w, (int)P.rowEnd - 1);
+    for (int ty = ty0; ty <= ty1; ++ty)
+        for (int tx = (int)r.x; tx <= (int)r.y; ++tx)
+            if (intersects_tile(tx, ty, cx, cy, k, w)) {
+                if (wp < P.maxAssignments) {
+                    uint32_t tile = (uint32_t)(ty * (int)P.bin.tilesX + tx);
+                    keys[wp] = (tile << 16) | dbits;
+                    vals[wp] = gid;
+                    wp++;
+                }
+            }
+}
+
+// ---------------------------------------------------------------------------
+// 4. headers (buildHeadersFromSortedKernel, GlobalShaders.metal:304-356)
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_headers(const uint32_t* __restrict__ sortedKeys,
+                                                 const TileAssignmentHeader* __restrict__ hdr,
+                                                 uint32_t tileBegin, uint32_t tileEnd,
+                                                 GaussianHeader* __restrict__ headers) {
+    const uint32_t tile = tileBegin + blockIdx.x * 256 + threadIdx.x;
+    if (tile >= tileEnd) return;
+    const uint32_t total = hdr->totalAssignments;
+    GaussianHeader h;
+    if (total == 0) {
+        h.offset = 0;
+        h.count = 0;
+    } else {
+        uint32_t l = 0, r = total;
+        while (l < r) {
+            uint32_t mid = (l + r) >> 1;
+            if ((sortedKeys[mid] >> 16) < tile) l = mid + 1;
+            else r = mid;
+        }
+        uint32_t s = l;
+        r = total;
+        while (l < r) {
+            uint32_t mid = (l + r) >> 1;
+            if ((sortedKeys[mid] >> 16) <= tile) l = mid + 1;
+            else r = mid;
+        }
+        h.offset = s;
+        h.count = l > s ? l - s : 0u;
+    }
+    headers[tile] = h;
+}
+
+// ---------------------------------------------------------------------------
+// 5. blend (globalRender, GlobalShaders.metal:1030-1187) + clear (:140-154)
+//
+// Persistent: one 1024-thread workgroup per CU holds the 128 KiB fp16 exp table
+// in LDS; each of its 16 waves pulls 32x16 tiles from a device counter.  A wave is
+// one tile: lane = 4x2 pixel group at (lx*4, ly*2) exactly like the reference's
+// 8x8 threadgroup, so the per-thread saturation break is preserved.
+// ---------------------------------------------------------------------------
+constexpr int kBlendThreads = 1024;
+
+__device__ __forceinline__ h2 as_h2(uint32_t u) { return __builtin_bit_cast(h2, u); }
+__device__ __forceinline__ uint32_t as_u32(h2 v) { return __builtin_bit_cast(uint32_t, v); }
+__device__ __forceinline__ h2 splat_lo(h2 v) { return h2{v.x, v.x}; }
+__device__ __forceinline__ h2 splat_hi(h2 v) { return h2{v.y, v.y}; }
+
+__device__ __forceinline__ h2 lookup2(const uint16_t* tbl, h2 p) {
+    uint32_t pb = as_u32(p);
+    uint32_t lo = tbl[pb & 0xFFFFu];
+    uint32_t hi = tbl[pb >> 16];
+    return as_h2(lo | (hi << 16));
+}
+
+__global__ __launch_bounds__(kBlendThreads) void k_blend(
+    const GaussianHeader* __restrict__ headers, const uint32_t* __restrict__ sortedVals,
+    const BlendRecordA* __restrict__ recA, const uint32_t* __restrict__ recB,
+    const uint16_t* __restrict__ expTable, uint32_t* __restrict__ queue, uint32_t tileBegin,
+    uint32_t numTiles, uint32_t tilesX, uint32_t W, uint32_t H, uint8_t* __restrict__ color,
+    size_t colorPitch, uint8_t* __restrict__ depth, size_t depthPitch, int vecStores) {
+    __shared__ uint16_t tbl[65536];
+    {
+        const uint4* src = (const uint4*)expTable;
+        uint4* dst = (uint4*)tbl;
+        for (int i = threadIdx.x; i < 65536 * 2 / 16; i += kBlendThreads) dst[i] = src[i];
+    }
+    __syncthreads();
+
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t lx = lane & 7, ly = lane >> 3;
+    const h2 ONE = {(h1)1.0f, (h1)1.0f};
+    const h2 ZERO = {(h1)0.0f, (h1)0.0f};
+    const h1 thr = (h1)(1.0f / 255.0f);  // half(1.0h/255.0h)
+    const h1 c099 = (h1)0.99;            // 0.99h
+    const h2 C099 = {c099, c099};
+
+    for (;;) {
+        uint32_t qi = 0;
+        if (lane == 0) qi = atomicAdd(queue, 1u);
+        qi = __builtin_amdgcn_readfirstlane(qi);
+        if (qi >= numTiles) break;
+        const uint32_t tile = tileBegin + qi;
+        const uint32_t tileX = tile % tilesX, tileY = tile / tilesX;
+        const uint32_t baseX = tileX * kTileWidth + lx * 4, baseY = tileY * kTileHeight + ly * 2;
+        const GaussianHeader hdr = headers[tile];
+        const uint32_t start = __builtin_amdgcn_readfirstlane(hdr.offset);
+        const uint32_t count = __builtin_amdgcn_readfirstlane(hdr.count);
+
+        h2 T0a = ONE, T0b = ONE, T1a = ONE, T1b = ONE;  // row 0: px 0-1, 2-3; row 1
+        h2 R0a = ZERO, R0b = ZERO, R1a = ZERO, R1b = ZERO;
+        h2 G0a = ZERO, G0b = ZERO, G1a = ZERO, G1b = ZERO;
+        h2 B0a = ZERO, B0b = ZERO, B1a = ZERO, B1b = ZERO;
+        h2 D0a = ZERO, D0b = ZERO, D1a = ZERO, D1b = ZERO;
+
+        if (count > 0) {
+            const h2 Xa = {(h1)(float)(baseX + 0), (h1)(float)(baseX + 1)};
+            const h2 Xb = {(h1)(float)(baseX + 2), (h1)(float)(baseX + 3)};
+            const h2 Yv = {(h1)(float)(baseY + 0), (h1)(float)(baseY + 1)};
+            bool alive = true;
+            uint4 curA = make_uint4(0, 0, 0, 0);
+            uint32_t curB = 0;
+            if (lane < count) {
+                uint32_t g = sortedVals[start + lane];
+                curA = *(const uint4*)(recA + g);
+                curB = recB[g];
+            }
+            for (uint32_t base = 0; base < count; base += 64) {
+                uint4 nxtA = make_uint4(0, 0, 0, 0);
+                uint32_t nxtB = 0;
+                if (base + 64 + lane < count) {
+                    uint32_t g = sortedVals[start + base + 64 + lane];
+                    nxtA = *(const uint4*)(recA + g);
+                    nxtB = recB[g];
+                }
+                const uint32_t nb = min(64u, count - base);
+                bool done = false;
+                for (uint32_t j = 0; j < nb; ++j) {
+                    // early exit when the thread's 8 pixels are saturated (GlobalShaders.metal:1086-1088)
+                    if (alive) {
+                        h2 m = __builtin_elementwise_max(__builtin_elementwise_max(T0a, T0b),
+                                                         __builtin_elementwise_max(T1a, T1b));
+                        h1 mm = __builtin_elementwise_max(m.x, m.y);
+                        if (mm < thr) alive = false;
+                    }
+                    if (__ballot(alive) == 0) {
+                        done = true;
+                        break;
+                    }
+                    const uint32_t r0 = __builtin_amdgcn_readlane(curA.x, j);
+                    const uint32_t r1 = __builtin_amdgcn_readlane(curA.y, j);
+                    const uint32_t r2 = __builtin_amdgcn_readlane(curA.z, j);
+                    const uint32_t r3 = __builtin_amdgcn_readlane(curA.w, j);
+                    const uint32_t r4 = __builtin_amdgcn_readlane(curB, j);
+                    bool nz = false;
+                    h2 a0a, a0b, a1a, a1b;
+                    if (alive) {
+                        const h2 mean = as_h2(r0), cc = as_h2(r1), oc = as_h2(r2);
+                        const h2 MX = splat_lo(mean), MY = splat_hi(mean);
+                        const h2 CXX = splat_lo(cc), CYY = splat_hi(cc);
+                        const h2 CXY = splat_lo(oc), OP = splat_hi(oc);
+                        const h2 dxa = Xa - MX, dxb = Xb - MX, dy = Yv - MY;
+                        const h2 sxa = (dxa * dxa) * CXX, sxb = (dxb * dxb) * CXX;
+                        const h2 sy = (dy * dy) * CYY;
+                        const h2 dy0 = splat_lo(dy), dy1 = splat_hi(dy);
+                        const h2 sy0 = splat_lo(sy), sy1 = splat_hi(sy);
+                        // p = ((dx*dx)*cxx + (dy*dy)*cyy) + (dx*dy)*cxy2  (GlobalShaders.metal:1115-1122)
+                        const h2 p0a = (sxa + sy0) + (dxa * dy0) * CXY;
+                        const h2 p0b = (sxb + sy0) + (dxb * dy0) * CXY;
+                        const h2 p1a = (sxa + sy1) + (dxa * dy1) * CXY;
+                        const h2 p1b = (sxb + sy1) + (dxb * dy1) * CXY;
+                        // a = min(opacity * exp(-0.5h * p), 0.99h)  (GlobalShaders.metal:1124-1131)
+                        a0a = __builtin_elementwise_min(OP * lookup2(tbl, p0a), C099);
+                        a0b = __builtin_elementwise_min(OP * lookup2(tbl, p0b), C099);
+                        a1a = __builtin_elementwise_min(OP * lookup2(tbl, p1a), C099);
+                        a1b = __builtin_elementwise_min(OP * lookup2(tbl, p1b), C099);
+                        nz = ((as_u32(a0a) | as_u32(a0b) | as_u32(a1a) | as_u32(a1b)) & 0x7FFF7FFFu) != 0;
+                    }
+                    // all-zero alphas change nothing (GlobalShaders.metal:1135); skip wave-wide
+                    if (__ballot(nz) == 0) continue;
+                    if (alive) {
+                        const h2 rg = as_h2(r3), bd = as_h2(r4);
+                        const h2 CR = splat_lo(rg), CG = splat_hi(rg);
+                        const h2 CB = splat_lo(bd), CD = splat_hi(bd);
+                        // (GlobalShaders.metal:1137-1149)
+                        h2 w;
+                        w = a0a * T0a; R0a = R0a + CR * w; G0a = G0a + CG * w; B0a = B0a + CB * w; D0a = D0a + CD * w; T0a = T0a * (ONE - a0a);
+                        w = a0b * T0b; R0b = R0b + CR * w; G0b = G0b + CG * w; B0b = B0b + CB * w; D0b = D0b + CD * w; T0b = T0b * (ONE - a0b);
+                        w = a1a * T1a; R1a = R1a + CR * w; G1a = G1a + CG * w; B1a = B1a + CB * w; D1a = D1a + CD * w; T1a = T1a * (ONE - a1a);
+                        w = a1b * T1b; R1b = R1b + CR * w; G1b = G1b + CG * w; B1b = B1b + CB * w; D1b = D1b + CD * w; T1b = T1b * (ONE - a1b);
+                    }
+                }
+                if (done) break;
+                curA = nxtA;
+                curB = nxtB;
+            }
+        }
+
+        // write (GlobalShaders.metal:1152-1186); inactive tiles get the clear colour (0,0,0,1)
+        h2 A0a, A0b, A1a, A1b;
+        if (count > 0) {
+            A0a = ONE - T0a; A0b = ONE - T0b; A1a = ONE - T1a; A1b = ONE - T1b;
+        } else {
+            A0a = ONE; A0b = ONE; A1a = ONE; A1b = ONE;
+        }
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const uint32_t y = baseY + j;
+            if (y >= H) continue;
+            const h2 Ra = j ? R1a : R0a, Rb = j ? R1b : R0b;
+            const h2 Ga = j ? G1a : G0a, Gb = j ? G1b : G0b;
+            const h2 Ba = j ? B1a : B0a, Bb = j ? B1b : B0b;
+            const h2 Aa = j ? A1a : A0a, Ab = j ? A1b : A0b;
+            const h2 Da = j ? D1a : D0a, Db = j ? D1b : D0b;
+            uint32_t px[4][2];
+            const h2 Rv[2] = {Ra, Rb}, Gv[2] = {Ga, Gb}, Bv[2] = {Ba, Bb}, Av[2] = {Aa, Ab};
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int hh = i >> 1, e = i & 1;
+                h1 r = e ? Rv[hh].y : Rv[hh].x, g = e ? Gv[hh].y : Gv[hh].x;
+                h1 b = e ? Bv[hh].y : Bv[hh].x, a = e ? Av[hh].y : Av[hh].x;
+                px[i][0] = (uint32_t)__builtin_bit_cast(uint16_t, r) | ((uint32_t)__builtin_bit_cast(uint16_t, g) << 16);
+                px[i][1] = (uint32_t)__builtin_bit_cast(uint16_t, b) | ((uint32_t)__builtin_bit_cast(uint16_t, a) << 16);
+            }
+            uint8_t* crow = color + (size_t)y * colorPitch;
+            uint8_t* drow = depth ? depth + (size_t)y * depthPitch : nullptr;
+            if (vecStores && baseX + 3 < W) {
+                uint4* cp = (uint4*)(crow + (size_t)baseX * 8);
+                cp[0] = make_uint4(px[0][0], px[0][1], px[1][0], px[1][1]);
+                cp[1] = make_uint4(px[2][0], px[2][1], px[3][0], px[3][1]);
+                if (drow) *(uint2*)(drow + (size_t)baseX * 2) = make_uint2(as_u32(Da), as_u32(Db));
+            } else {
+                const uint32_t dv[2] = {as_u32(Da), as_u32(Db)};
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const uint32_t x = baseX + i;
+                    if (x >= W) continue;
+                    uint32_t* cp = (uint32_t*)(crow + (size_t)x * 8);
+                    cp[0] = px[i][0];
+                    cp[1] = px[i][1];
+                    if (drow) {
+                        uint16_t dh = (uint16_t)((dv[i >> 1] >> ((i & 1) * 16)) & 0xFFFFu);
+                        *(uint16_t*)(drow + (size_t)x * 2) = dh;
+                    }
+                }
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// launchers
+// ---------------------------------------------------------------------------
+template <bool HALF>
+static void launch_project_t(uint32_t deg, const void* world, const void* harm, const ProjectArgs& a,
+                             const DeviceArena& A, hipStream_t s) {
+    const uint32_t blocks = (a.count + kProjectBlock - 1) / kProjectBlock;
+    if (blocks == 0) return;
+#define GSM_LAUNCH_PROJ(D)                                                                     \
+    hipLaunchKernelGGL((k_project<HALF, D>), dim3(blocks), dim3(kProjectBlock), 0, s, world,   \
+                       harm, a, A.renderData, A.bounds, A.recA, A.recB, A.tileCounts,          \
+                       A.blockSums, A.sincosTable)
+    switch (deg) {
+        case 0: GSM_LAUNCH_PROJ(0); break;
+        case 1: GSM_LAUNCH_PROJ(1); break;
+        case 2: GSM_LAUNCH_PROJ(2); break;
+        default: GSM_LAUNCH_PROJ(3); break;
+    }
+#undef GSM_LAUNCH_PROJ
+}
+
+void launch_project(bool halfInput, uint32_t deg, const void* world, const void* harm,
+                    const ProjectArgs& a, const DeviceArena& A, hipStream_t s) {
+    if (halfInput) launch_project_t<true>(deg, world, harm, a, A, s);
+    else launch_project_t<false>(deg, world, harm, a, A, s);
+}
+
+void launch_scan_blocks(uint32_t nb, const ProjectArgs& a, const DeviceArena& A, hipStream_t s) {
+    hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(kScanThreads), 0, s, A.blockSums, nb,
+                       a.maxAssignments, A.header);
+}
+
+void launch_scatter(const ProjectArgs& a, const DeviceArena& A, hipStream_t s) {
+    const uint32_t blocks = (a.count + kProjectBlock - 1) / kProjectBlock;
+    if (blocks == 0) return;
+    hipLaunchKernelGGL(k_scatter, dim3(blocks), dim3(kProjectBlock), 0, s, a, A.renderData, A.bounds,
+                       A.tileCounts, A.blockSums, A.keys[0], A.vals[0], A.sincosTable);
+}
+
+void launch_headers(const uint32_t* sortedKeys, const FrameGeometry& g, const DeviceArena& A,
+                    hipStream_t s) {
+    const uint32_t t0 = g.rowBegin * g.tilesX, t1 = g.rowEnd * g.tilesX;
+    if (t1 <= t0) return;
+    const uint32_t blocks = (t1 - t0 + 255) / 256;
+    hipLaunchKernelGGL(k_headers, dim3(blocks), dim3(256), 0, s, sortedKeys, A.header, t0, t1,
+                       A.headers);
+}
+
+void launch_blend(const uint32_t* sortedVals, const FrameGeometry& g, const DeviceArena& A, void* color,
+                  size_t colorPitch, void* depth, size_t depthPitch, int numCUs, hipStream_t s) {
+    const uint32_t t0 = g.rowBegin * g.tilesX, t1 = g.rowEnd * g.tilesX;
+    if (t1 <= t0) return;
+    const int vec = ((((uintptr_t)color) & 15u) == 0 && (colorPitch & 15u) == 0 &&
+                     (depth == nullptr || ((((uintptr_t)depth) & 7u) == 0 && (depthPitch & 7u) == 0)))
+                        ? 1
+                        : 0;
+    hipMemsetAsync(A.tileQueue, 0, sizeof(uint32_t), s);
+    uint32_t numTiles = t1 - t0;
+    uint32_t grid = (uint32_t)numCUs;
+    uint32_t maxUseful = (numTiles + (kBlendThreads / 64) - 1) / (kBlendThreads / 64);
+    if (grid > maxUseful) grid = maxUseful;
+    if (grid == 0) grid = 1;
+    hipLaunchKernelGGL(k_blend, dim3(grid), dim3(kBlendThreads), 0, s, A.headers, sortedVals, A.recA,
+                       A.recB, A.expTable, A.tileQueue, t0, numTiles, g.tilesX, g.width, g.height,
+                       (uint8_t*)color, colorPitch, (uint8_t*)depth, depthPitch, vec);
+}
+
+}  // namespace gsm

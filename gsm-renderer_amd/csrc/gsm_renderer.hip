@@ -1,0 +1,370 @@
+// gsm_renderer.hip -- host orchestration of one GlobalRenderer frame on MI355X.
+//
+// The C++ analogue of GlobalRenderer.swift (frame orchestration, :110-572) and
+// GlobalResources.swift (up-front scratch arena, :58-361).  One HIP stream replaces
+// the Metal command buffer; every grid size is a host constant (capacity-sized) and
+// data-dependent counts are read on the device, so a frame is enqueue-only and can
+// be captured into a hipGraph.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <vector>
+
+#include "../../include/gsm_debug.h"
+#include "../../include/gsm_renderer.h"
+#include "gsm_detmath.h"
+#include "gsm_internal.h"
+#include "gsm_renderer_impl.h"
+
+namespace gsm {
+
+static size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
+
+GlobalRenderer::~GlobalRenderer() { release(); }
+
+void GlobalRenderer::release() {
+    if (device_ >= 0) hipSetDevice(device_);
+    for (void* p : allocations_) hipFree(p);
+    allocations_.clear();
+    for (auto& e : events_)
+        if (e) hipEventDestroy(e);
+    events_.clear();
+}
+
+gsm_status GlobalRenderer::alloc(void** p, size_t bytes) {
+    *p = nullptr;
+    if (bytes == 0) bytes = 16;
+    if (hipMalloc(p, bytes) != hipSuccess) {
+        *p = nullptr;
+        return GSM_ERR_FAILED_TO_ALLOCATE_BUFFER;
+    }
+    allocations_.push_back(*p);
+    return GSM_OK;
+}
+
+gsm_status GlobalRenderer::create(const gsm_renderer_config& cfg, int hipDevice, GlobalRenderer** out) {
+    *out = nullptr;
+    // GlobalRenderer.init guard (GlobalRenderer.swift:111-113)
+    if (cfg.max_gaussians > kMaxSupportedGaussians) return GSM_ERR_INVALID_GAUSSIAN_COUNT;
+    if (cfg.precision != GSM_PRECISION_FLOAT32 && cfg.precision != GSM_PRECISION_FLOAT16)
+        return GSM_ERR_INVALID_ARGUMENT;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
+        (void)hipGetLastError();
+        return GSM_ERR_DEVICE_NOT_AVAILABLE;
+    }
+    int dev = hipDevice;
+    if (dev < 0) {
+        if (hipGetDevice(&dev) != hipSuccess) return GSM_ERR_DEVICE_NOT_AVAILABLE;
+    }
+    if (dev >= ndev) return GSM_ERR_DEVICE_NOT_AVAILABLE;
+    if (hipSetDevice(dev) != hipSuccess) return GSM_ERR_DEVICE_NOT_AVAILABLE;
+
+    GlobalRenderer* r = new (std::nothrow) GlobalRenderer();
+    if (!r) return GSM_ERR_FAILED_TO_ALLOCATE_BUFFER;
+    r->device_ = dev;
+    r->config_ = cfg;
+    // RendererLimits (GlobalRenderer.swift:6-23)
+    r->maxGaussians_ = cfg.max_gaussians ? cfg.max_gaussians : 1u;
+    r->maxWidth_ = cfg.max_width ? cfg.max_width : 1u;
+    r->maxHeight_ = cfg.max_height ? cfg.max_height : 1u;
+    r->tilesX_ = (r->maxWidth_ + kTileWidth - 1) / kTileWidth;
+    r->tilesY_ = (r->maxHeight_ + kTileHeight - 1) / kTileHeight;
+    r->tileCount_ = r->tilesX_ * r->tilesY_;
+    if (r->tileCount_ > 65536u) {  // 16-bit tile field of the sort key (GlobalShaders.metal:288)
+        delete r;
+        return GSM_ERR_INVALID_TILE_COUNT;
+    }
+    r->rowBegin_ = 0;
+    r->rowEnd_ = r->tilesY_;
+    const uint64_t cap64 = 4ull * r->maxGaussians_;  // GlobalResources.swift:79
+    r->maxAssignments_ = (uint32_t)(cap64 > 0xFFFFFFF0ull ? 0xFFFFFFF0ull : cap64);
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, dev) != hipSuccess) {
+        delete r;
+        return GSM_ERR_DEVICE_NOT_AVAILABLE;
+    }
+    r->numCUs_ = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+
+    const size_t G = r->maxGaussians_;
+    const size_t cap = r->maxAssignments_;
+    const size_t nb = (G + kProjectBlock - 1) / kProjectBlock;
+    const uint32_t rgrid = radix_grid_for_capacity(r->maxAssignments_);
+    DeviceArena& A = r->arena_;
+    gsm_status st = GSM_OK;
+#define GSM_ALLOC(ptr, bytes)                                              \
+    do {                                                                   \
+        if (st == GSM_OK) st = r->alloc((void**)&(ptr), align_up((bytes), 256)); \
+    } while (0)
+    GSM_ALLOC(A.renderData, G * sizeof(GaussianRenderData));
+    GSM_ALLOC(A.bounds, G * sizeof(short4));
+    GSM_ALLOC(A.recA, G * sizeof(BlendRecordA));
+    GSM_ALLOC(A.recB, G * sizeof(uint32_t));
+    GSM_ALLOC(A.tileCounts, G * sizeof(uint32_t));
+    GSM_ALLOC(A.blockSums, (nb + 1) * sizeof(uint32_t));
+    GSM_ALLOC(A.header, sizeof(TileAssignmentHeader));
+    GSM_ALLOC(A.keys[0], cap * sizeof(uint32_t));
+    GSM_ALLOC(A.keys[1], cap * sizeof(uint32_t));
+    GSM_ALLOC(A.vals[0], cap * sizeof(uint32_t));
+    GSM_ALLOC(A.vals[1], cap * sizeof(uint32_t));
+    GSM_ALLOC(A.radixHist, (size_t)256 * rgrid * sizeof(uint32_t));
+    GSM_ALLOC(A.radixBinTotals, 256 * sizeof(uint32_t));
+    GSM_ALLOC(A.headers, (size_t)r->tileCount_ * sizeof(GaussianHeader));
+    GSM_ALLOC(A.tileQueue, sizeof(uint32_t));
+    GSM_ALLOC(A.expTable, 65536 * sizeof(uint16_t));
+    GSM_ALLOC(A.sincosTable, 65536 * sizeof(float2));
+#undef GSM_ALLOC
+    if (st != GSM_OK) {
+        delete r;
+        return st;
+    }
+    // numeric-contract tables (gsm_detmath.h)
+    std::vector<uint16_t> expt(65536);
+    for (uint32_t i = 0; i < 65536; ++i) expt[i] = blend_exp_table_entry((uint16_t)i);
+    std::vector<float2> sc(65536);
+    for (uint32_t i = 0; i < 65536; ++i) det_sincos_table_entry(i, &sc[i].x, &sc[i].y);
+    if (hipMemcpy(A.expTable, expt.data(), 65536 * sizeof(uint16_t), hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(A.sincosTable, sc.data(), 65536 * sizeof(float2), hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemset(A.header, 0, sizeof(TileAssignmentHeader)) != hipSuccess ||
+        hipMemset(A.headers, 0, (size_t)r->tileCount_ * sizeof(GaussianHeader)) != hipSuccess) {
+        delete r;
+        return GSM_ERR_FAILED_TO_ALLOCATE_BUFFER;
+    }
+    *out = r;
+    return GSM_OK;
+}
+
+int GlobalRenderer::sortPassCount() const {
+    // RadixSortEncoder.swift:52-63: depth bytes (2) + bytes of (tileCount-1), max 4.
+    int tileBytes = 1;
+    uint32_t remaining = tileCount_ > 0 ? tileCount_ - 1 : 0;
+    while (remaining >= 256) {
+        tileBytes++;
+        remaining >>= 8;
+    }
+    int p = 2 + tileBytes;
+    return p > 4 ? 4 : p;
+}
+
+gsm_status GlobalRenderer::render(hipStream_t s, const gsm_gaussian_input& in,
+                                  const gsm_camera_params& camp, uint32_t width, uint32_t height,
+                                  void* color, size_t colorPitch, void* depth, size_t depthPitch) {
+    // validateLimits (GlobalRenderer.swift:372-376) -- errors instead of a silent skip
+    if (in.gaussian_count > maxGaussians_) return GSM_ERR_INVALID_GAUSSIAN_COUNT;
+    if (width == 0 || height == 0 || width > maxWidth_ || height > maxHeight_)
+        return GSM_ERR_INVALID_DIMENSIONS;
+    if (!color) return GSM_ERR_MISSING_REQUIRED_BUFFER;
+    if (in.gaussian_count > 0 && (!in.gaussians || !in.harmonics)) return GSM_ERR_MISSING_REQUIRED_BUFFER;
+    if (colorPitch < (size_t)width * 8) return GSM_ERR_INVALID_BUFFER_SIZE;
+    if (depth && depthPitch < (size_t)width * 2) return GSM_ERR_INVALID_BUFFER_SIZE;
+    if (hipSetDevice(device_) != hipSuccess) return GSM_ERR_DEVICE_NOT_AVAILABLE;
+
+    ProjectArgs a;
+    std::memset(&a, 0, sizeof(a));
+    // CameraUniforms(from: camera, ...) (KernelTypes.swift:107-123)
+    std::memcpy(a.cam.view, camp.view, sizeof(a.cam.view));
+    std::memcpy(a.cam.proj, camp.proj, sizeof(a.cam.proj));
+    std::memcpy(a.cam.cameraCenter, camp.position, sizeof(a.cam.cameraCenter));
+    a.cam.pixelFactor = 1.0f;
+    a.cam.focalX = camp.focal_x;
+    a.cam.focalY = camp.focal_y;
+    a.cam.width = (float)width;
+    a.cam.height = (float)height;
+    a.cam.nearPlane = camp.near_plane;
+    a.cam.farPlane = camp.far_plane;
+    a.cam.shComponents = in.sh_components;
+    a.cam.gaussianCount = in.gaussian_count;
+    a.cam.inputIsSRGB = config_.gaussian_color_space == GSM_COLOR_SPACE_SRGB ? 1.0f : 0.0f;
+    // buildBinningParams (GlobalRenderer.swift:38-51)
+    a.bin.gaussianCount = in.gaussian_count;
+    a.bin.tilesX = tilesX_;
+    a.bin.tilesY = tilesY_;
+    a.bin.tileWidth = kTileWidth;
+    a.bin.tileHeight = kTileHeight;
+    a.bin.surfaceWidth = maxWidth_;
+    a.bin.surfaceHeight = maxHeight_;
+    a.bin.maxCapacity = in.gaussian_count;
+    a.bin.alphaThreshold = 0.005f;
+    a.bin.totalInkThreshold = 2.0f;
+    a.rowBegin = rowBegin_;
+    a.rowEnd = rowEnd_;
+    a.count = in.gaussian_count;
+    a.maxAssignments = maxAssignments_;
+
+    // GlobalProjectCullEncoder.swift:19-26 SH_DEGREE selection
+    const uint32_t k = in.sh_components;
+    const uint32_t deg = k <= 1 ? 0u : (k <= 4 ? 1u : (k <= 9 ? 2u : 3u));
+    const bool prof = (profiling_ & 1) != 0;
+    const bool keep = (profiling_ & 2) != 0;
+    const uint32_t nb = (in.gaussian_count + kProjectBlock - 1) / kProjectBlock;
+    lastCount_ = in.gaussian_count;
+    lastWidth_ = width;
+    lastHeight_ = height;
+
+    hipEvent_t* ev = prof ? frameEvents(profFrames_) : nullptr;
+    if (prof) hipEventRecord(ev[0], s);
+    launch_project(config_.precision == GSM_PRECISION_FLOAT16, deg, in.gaussians, in.harmonics, a,
+                   arena_, s);
+    if (prof) hipEventRecord(ev[1], s);
+    launch_scan_blocks(nb, a, arena_, s);
+    if (prof) hipEventRecord(ev[2], s);
+    launch_scatter(a, arena_, s);
+    if (keep) {  // preserve the unsorted assignment arrays for readback
+        hipMemcpyAsync(arena_.keysKeep, arena_.keys[0], (size_t)maxAssignments_ * 4, hipMemcpyDeviceToDevice, s);
+        hipMemcpyAsync(arena_.valsKeep, arena_.vals[0], (size_t)maxAssignments_ * 4, hipMemcpyDeviceToDevice, s);
+    }
+    if (prof) hipEventRecord(ev[3], s);
+    uint32_t* kb[2] = {arena_.keys[0], arena_.keys[1]};
+    uint32_t* vb[2] = {arena_.vals[0], arena_.vals[1]};
+    const int res = radix_sort_pairs(kb, vb, &arena_.header->totalAssignments, maxAssignments_, 0,
+                                     sortPassCount(), arena_.radixHist, arena_.radixBinTotals, s);
+    sortedKeys_ = kb[res];
+    sortedVals_ = vb[res];
+    unsortedKeys_ = keep ? arena_.keysKeep : nullptr;
+    unsortedVals_ = keep ? arena_.valsKeep : nullptr;
+    if (prof) hipEventRecord(ev[4], s);
+    FrameGeometry g;
+    g.tilesX = tilesX_;
+    g.tilesY = tilesY_;
+    g.tileCount = tileCount_;
+    g.rowBegin = rowBegin_;
+    g.rowEnd = rowEnd_;
+    g.width = width;
+    g.height = height;
+    g.maxAssignments = maxAssignments_;
+    launch_headers(sortedKeys_, g, arena_, s);
+    if (prof) hipEventRecord(ev[5], s);
+    launch_blend(sortedVals_, g, arena_, color, colorPitch, depth, depthPitch, numCUs_, s);
+    if (prof) hipEventRecord(ev[6], s);
+    if (prof) profFrames_++;
+    haveTimes_ = profFrames_ > 0;
+    if (hipGetLastError() != hipSuccess) return GSM_ERR_RENDER_FAILED;
+    return GSM_OK;
+}
+
+gsm_status GlobalRenderer::stageTimes(float* ms, int n) {
+    // Average of every profiled frame still in the ring (the last kEventRing frames).
+    if (!haveTimes_ || profFrames_ == 0) return GSM_ERR_RENDER_FAILED;
+    hipSetDevice(device_);
+    if (hipEventSynchronize(frameEvents(profFrames_ - 1)[GSM_STAGE_COUNT]) != hipSuccess)
+        return GSM_ERR_RENDER_FAILED;
+    const uint32_t frames = profFrames_ < (uint32_t)kEventRing ? profFrames_ : (uint32_t)kEventRing;
+    const uint32_t first = profFrames_ - frames;
+    for (int i = 0; i < n && i < GSM_STAGE_COUNT; ++i) {
+        double acc = 0.0;
+        for (uint32_t f = first; f < profFrames_; ++f) {
+            float t = 0.f;
+            hipEvent_t* ev = frameEvents(f);
+            if (hipEventElapsedTime(&t, ev[i], ev[i + 1]) != hipSuccess) return GSM_ERR_RENDER_FAILED;
+            acc += t;
+        }
+        ms[i] = (float)(acc / frames);
+    }
+    return GSM_OK;
+}
+
+gsm_status GlobalRenderer::lastGpuTime(double* seconds) {
+    if (!haveTimes_ || profFrames_ == 0) return GSM_ERR_RENDER_FAILED;
+    hipSetDevice(device_);
+    hipEvent_t* ev = frameEvents(profFrames_ - 1);
+    if (hipEventSynchronize(ev[GSM_STAGE_COUNT]) != hipSuccess) return GSM_ERR_RENDER_FAILED;
+    float t = 0.f;
+    if (hipEventElapsedTime(&t, ev[0], ev[GSM_STAGE_COUNT]) != hipSuccess) return GSM_ERR_RENDER_FAILED;
+    *seconds = (double)t * 1e-3;
+    return GSM_OK;
+}
+
+gsm_status GlobalRenderer::counters(gsm_debug_counters* out) {
+    hipSetDevice(device_);
+    TileAssignmentHeader h;
+    if (hipMemcpy(&h, arena_.header, sizeof(h), hipMemcpyDeviceToHost) != hipSuccess)
+        return GSM_ERR_RENDER_FAILED;
+    out->total_assignments = h.totalAssignments;
+    out->max_capacity = h.maxCapacity;
+    out->padded_count = h.paddedCount;
+    out->overflow = h.overflow;
+    out->tiles_x = tilesX_;
+    out->tiles_y = tilesY_;
+    out->tile_count = tileCount_;
+    out->gaussian_count = lastCount_;
+    return GSM_OK;
+}
+
+gsm_status GlobalRenderer::debugCopy(int which, void* dst, size_t bytes, size_t* needed) {
+    hipSetDevice(device_);
+    gsm_debug_counters c;
+    gsm_status st = counters(&c);
+    if (st != GSM_OK) return st;
+    const size_t n = lastCount_, tot = c.total_assignments;
+    const void* src = nullptr;
+    size_t full = 0;
+    std::vector<short4> tmpBounds;
+    switch (which) {
+        case GSM_BUF_RENDER_DATA: src = arena_.renderData; full = n * 16; break;
+        case GSM_BUF_BOUNDS: full = n * 16; break;
+        case GSM_BUF_TILE_COUNTS: src = arena_.tileCounts; full = n * 4; break;
+        case GSM_BUF_KEYS: src = unsortedKeys_; full = tot * 4; break;
+        case GSM_BUF_VALUES: src = unsortedVals_; full = tot * 4; break;
+        case GSM_BUF_SORTED_KEYS: src = sortedKeys_; full = tot * 4; break;
+        case GSM_BUF_SORTED_VALUES: src = sortedVals_; full = tot * 4; break;
+        case GSM_BUF_HEADERS: src = arena_.headers; full = (size_t)tileCount_ * 8; break;
+        case GSM_BUF_EXP_TABLE: src = arena_.expTable; full = 65536 * 2; break;
+        default: return GSM_ERR_INVALID_ARGUMENT;
+    }
+    if (needed) *needed = full;
+    if (!dst || bytes == 0) return GSM_OK;
+    size_t cpy = bytes < full ? bytes : full;
+    if (which == GSM_BUF_BOUNDS) {
+        tmpBounds.resize(n ? n : 1);
+        if (n && hipMemcpy(tmpBounds.data(), arena_.bounds, n * sizeof(short4), hipMemcpyDeviceToHost) != hipSuccess)
+            return GSM_ERR_RENDER_FAILED;
+        std::vector<int32_t> b(n * 4);
+        for (size_t i = 0; i < n; ++i) {
+            b[4 * i + 0] = tmpBounds[i].x;
+            b[4 * i + 1] = tmpBounds[i].y;
+            b[4 * i + 2] = tmpBounds[i].z;
+            b[4 * i + 3] = tmpBounds[i].w;
+        }
+        std::memcpy(dst, b.data(), cpy);
+        return GSM_OK;
+    }
+    if (!src) return full == 0 ? GSM_OK : GSM_ERR_MISSING_REQUIRED_BUFFER;
+    if (cpy && hipMemcpy(dst, src, cpy, hipMemcpyDeviceToHost) != hipSuccess) return GSM_ERR_RENDER_FAILED;
+    return GSM_OK;
+}
+
+gsm_status GlobalRenderer::setTileRows(uint32_t b, uint32_t e) {
+    if (b == 0 && e == 0) {
+        rowBegin_ = 0;
+        rowEnd_ = tilesY_;
+        return GSM_OK;
+    }
+    if (b >= e || e > tilesY_) return GSM_ERR_INVALID_ARGUMENT;
+    rowBegin_ = b;
+    rowEnd_ = e;
+    return GSM_OK;
+}
+
+}  // namespace gsm
+
+namespace gsm {
+gsm_status GlobalRenderer::setProfiling(int flags) {
+    hipSetDevice(device_);
+    if ((flags & 2) && !arena_.keysKeep) {
+        gsm_status st = alloc((void**)&arena_.keysKeep, (size_t)maxAssignments_ * 4);
+        if (st == GSM_OK) st = alloc((void**)&arena_.valsKeep, (size_t)maxAssignments_ * 4);
+        if (st != GSM_OK) return st;
+    }
+    if ((flags & 1) && events_.empty()) {
+        events_.assign((size_t)kEventRing * (GSM_STAGE_COUNT + 1), nullptr);
+        for (auto& e : events_)
+            if (hipEventCreate(&e) != hipSuccess) return GSM_ERR_ENCODER_CREATION_FAILED;
+    }
+    profiling_ = flags;
+    profFrames_ = 0;  // restart the averaging window
+    haveTimes_ = false;
+    return GSM_OK;
+}
+}  // namespace gsm

@@ -1,0 +1,65 @@
+// gsm_renderer_impl.h -- C++ GlobalRenderer behind the C ABI (include/gsm_renderer.h).
+// Mirrors the reference class GlobalRenderer (GlobalRenderer.swift:72-572).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <vector>
+
+#include "../../include/gsm_debug.h"
+#include "../../include/gsm_renderer.h"
+#include "gsm_internal.h"
+
+namespace gsm {
+
+class GlobalRenderer {
+   public:
+    // GlobalRenderer.init(device:config:) (GlobalRenderer.swift:110-193)
+    static gsm_status create(const gsm_renderer_config& cfg, int hipDevice, GlobalRenderer** out);
+    ~GlobalRenderer();
+
+    // GlobalRenderer.render (GlobalRenderer.swift:201-238)
+    gsm_status render(hipStream_t stream, const gsm_gaussian_input& input,
+                      const gsm_camera_params& camera, uint32_t width, uint32_t height, void* color,
+                      size_t colorPitch, void* depth, size_t depthPitch);
+
+    gsm_status counters(gsm_debug_counters* out);
+    gsm_status debugCopy(int which, void* dst, size_t bytes, size_t* needed);
+    gsm_status setProfiling(int flags);  // bit0: stage events, bit1: keep unsorted keys
+    gsm_status stageTimes(float* ms, int n);
+    gsm_status lastGpuTime(double* seconds);
+    gsm_status setTileRows(uint32_t begin, uint32_t end);
+    int device() const { return device_; }
+
+   private:
+    GlobalRenderer() = default;
+    gsm_status alloc(void** p, size_t bytes);
+    void release();
+    int sortPassCount() const;
+
+    int device_ = -1;
+    int numCUs_ = 256;
+    gsm_renderer_config config_{};
+    uint32_t maxGaussians_ = 1, maxWidth_ = 1, maxHeight_ = 1;
+    uint32_t tilesX_ = 1, tilesY_ = 1, tileCount_ = 1;
+    uint32_t rowBegin_ = 0, rowEnd_ = 1;
+    uint32_t maxAssignments_ = 4;
+    DeviceArena arena_;
+    std::vector<void*> allocations_;
+    static constexpr int kEventRing = 128;  // frames of stage events kept for averaging
+    std::vector<hipEvent_t> events_;       // [kEventRing][GSM_STAGE_COUNT + 1]
+    uint32_t profFrames_ = 0;
+    hipEvent_t* frameEvents(uint32_t frame) { return &events_[(frame % kEventRing) * (GSM_STAGE_COUNT + 1)]; }
+    int profiling_ = 0;
+    bool haveTimes_ = false;
+    uint32_t lastCount_ = 0, lastWidth_ = 0, lastHeight_ = 0;
+    const uint32_t* sortedKeys_ = nullptr;
+    const uint32_t* sortedVals_ = nullptr;
+    const uint32_t* unsortedKeys_ = nullptr;
+    const uint32_t* unsortedVals_ = nullptr;
+};
+
+}  // namespace gsm
+
+struct gsm_renderer {
+    gsm::GlobalRenderer* impl;
+};

@@ -1,0 +1,77 @@
+/*
+ * gsm_debug.h -- introspection, stage profiling, multi-GPU slab control and
+ * stand-alone sort for libgsm_amd.so.
+ *
+ * The reference exposes its intermediate buffers to its own tests through
+ * `@testable import Renderer` (Tests/RendererTests/GlobalUnitTests.swift:2) and
+ * per-view resources (GlobalResources.swift:6-362); these entry points are the
+ * C-ABI equivalent used by the parity tests and the benchmark.  All readbacks
+ * are synchronous host copies: call them after the frame's stream work is done.
+ */
+#ifndef GSM_DEBUG_H
+#define GSM_DEBUG_H
+
+#include "gsm_renderer.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* TileAssignmentHeader (BridgingTypes.h:99-104) + derived frame counters. */
+typedef struct {
+    uint32_t total_assignments; /* after the clamp to max_capacity */
+    uint32_t max_capacity;      /* 4 * max_gaussians */
+    uint32_t padded_count;      /* roundup(total, 1024) (GlobalShaders.metal:711-712) */
+    uint32_t overflow;          /* 1 when the clamp fired (GlobalShaders.metal:697-701) */
+    uint32_t tiles_x, tiles_y, tile_count;
+    uint32_t gaussian_count;    /* of the last frame */
+} gsm_debug_counters;
+
+/* Buffers that can be copied back (reference resource named in brackets). */
+typedef enum {
+    GSM_BUF_RENDER_DATA = 0,   /* GaussianRenderData[count], 16 B each [interleavedGaussians] */
+    GSM_BUF_BOUNDS = 1,        /* int32[count][4] minTX,maxTX,minTY,maxTY [boundsCache] */
+    GSM_BUF_TILE_COUNTS = 2,   /* uint32[count] tiles per gaussian [coverageBuffer] */
+    GSM_BUF_KEYS = 3,          /* uint32[total] unsorted sort keys [sortKeys before sort] */
+    GSM_BUF_VALUES = 4,        /* int32[total] unsorted gaussian ids [tileIndices] */
+    GSM_BUF_SORTED_KEYS = 5,   /* uint32[total] [sortKeys after sort] */
+    GSM_BUF_SORTED_VALUES = 6, /* int32[total] [sortedIndices] */
+    GSM_BUF_HEADERS = 7,       /* GaussianHeader[tile_count] {offset,count} [orderedHeaders] */
+    GSM_BUF_EXP_TABLE = 8      /* uint16[65536] blend exp table indexed by fp16 quad-form bits */
+} gsm_buffer_id;
+
+gsm_status gsm_global_debug_counters(gsm_renderer *renderer, gsm_debug_counters *out);
+/* Copies up to `bytes` of buffer `which` into host memory; *needed receives the full size. */
+gsm_status gsm_global_debug_copy(gsm_renderer *renderer, int which, void *host_dst, size_t bytes,
+                                 size_t *needed);
+/* When enabled, every stage is bracketed by HIP events on the frame's stream and
+ * keeps the unsorted keys (GSM_BUF_KEYS/VALUES) for readback. */
+gsm_status gsm_global_set_profiling(gsm_renderer *renderer, int enable);
+
+enum {
+    GSM_STAGE_PROJECT = 0, /* project + cull + SH + tile count */
+    GSM_STAGE_SCAN = 1,    /* prefix scan of tile counts */
+    GSM_STAGE_SCATTER = 2, /* duplicate-with-keys */
+    GSM_STAGE_SORT = 3,    /* radix sort */
+    GSM_STAGE_HEADERS = 4, /* tile headers */
+    GSM_STAGE_BLEND = 5,   /* clear + front-to-back blend */
+    GSM_STAGE_COUNT = 6
+};
+/* Milliseconds of each stage of the last profiled frame (after stream sync). */
+gsm_status gsm_global_stage_times(gsm_renderer *renderer, float *ms, int n);
+
+/* Multi-GPU screen-slab partition: restrict tile assignment,
+ * sort, headers and blend to tile rows [row_begin, row_end).  Pixels outside the
+ * slab are not written.  (0, 0) restores the full frame. */
+gsm_status gsm_global_set_tile_rows(gsm_renderer *renderer, uint32_t row_begin, uint32_t row_end);
+
+/* Stable LSD radix sort of n (uint32 key, uint32 value) pairs in device memory,
+ * in place, `key_bits` low key bits significant (the RadixSortEncoder unit-test
+ * surface, GlobalUnitTests.swift:23-178).  Allocates its scratch; synchronises
+ * `stream` before returning. */
+gsm_status gsm_sort_pairs_u32(void *keys, void *values, uint32_t n, uint32_t key_bits, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,87 @@
+"""C-ABI surface of libgsm_amd.so: loads, exports every declared symbol, struct layouts
+match the headers, and the host-side validation that needs no GPU."""
+import ctypes as C
+import os
+import re
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADERS = [os.path.join(ROOT, "include", h) for h in ("gsm_renderer.h", "gsm_debug.h")]
+
+
+def declared_functions():
+    names = set()
+    for h in HEADERS:
+        src = open(h).read()
+        src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+        for m in re.finditer(r"\b(gsm_[a-z0-9_]+)\s*\(", src):
+            names.add(m.group(1))
+    return sorted(names)
+
+
+def test_library_exports_every_declared_symbol(gsm):
+    L = gsm._lib()
+    missing = [n for n in declared_functions() if not hasattr(L, n)]
+    assert not missing, missing
+    assert set(declared_functions()) == set(gsm._SIGNATURES), "binding must cover the headers"
+    out = subprocess.run(["nm", "-D", "--defined-only", gsm.library_path()], capture_output=True,
+                         text=True, check=True).stdout
+    exported = set(re.findall(r" T (gsm_[a-z0-9_]+)", out))
+    assert set(declared_functions()) <= exported
+
+
+def test_struct_sizes_match_headers(gsm, tmp_path):
+    prog = tmp_path / "sizes.c"
+    prog.write_text('#include "gsm_debug.h"\n#include <stdio.h>\n'
+                    'int main(void){printf("%zu %zu %zu %zu\\n", sizeof(gsm_renderer_config),'
+                    ' sizeof(gsm_gaussian_input), sizeof(gsm_camera_params),'
+                    ' sizeof(gsm_debug_counters));return 0;}\n')
+    exe = tmp_path / "sizes"
+    subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(prog), "-o", str(exe)], check=True)
+    sizes = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True,
+                                            check=True).stdout.split()]
+    assert sizes == [C.sizeof(gsm._Config), C.sizeof(gsm._Input), C.sizeof(gsm._Camera),
+                     C.sizeof(gsm._Counters)]
+
+
+def test_status_strings_and_defaults(gsm):
+    L = gsm._lib()
+    assert L.gsm_abi_version() == 1
+    for s in gsm.Status:
+        assert L.gsm_status_string(int(s))
+    cfg = gsm._Config()
+    L.gsm_renderer_config_default(C.byref(cfg))
+    # RendererConfig() defaults (GaussianRendererProtocol.swift:211-219)
+    assert (cfg.max_gaussians, cfg.max_width, cfg.max_height) == (6_000_000, 1920, 1080)
+    assert cfg.precision == gsm.RenderPrecision.FLOAT16
+    assert cfg.gaussian_color_space == gsm.GaussianColorSpace.SRGB
+    cam = gsm._Camera()
+    L.gsm_camera_params_init(C.byref(cam), None, None, None, 1.0, 2.0)
+    assert abs(cam.near_plane - 0.1) < 1e-7 and cam.far_plane == 10.0
+
+
+def test_create_rejects_too_many_gaussians_without_touching_the_gpu(gsm):
+    # GlobalRenderer.init guard: maxGaussians <= 30_000_000 (GlobalRenderer.swift:111-113)
+    with pytest.raises(gsm.RendererError) as e:
+        gsm.GlobalRenderer(config=gsm.RendererConfig(max_gaussians=30_000_001))
+    assert e.value.status == gsm.Status.INVALID_GAUSSIAN_COUNT
+
+
+def test_create_without_device_reports_device_not_available(gsm):
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is visible")
+    with pytest.raises(gsm.RendererError) as e:
+        gsm.GlobalRenderer(config=gsm.RendererConfig(max_gaussians=1000))
+    assert e.value.status == gsm.Status.DEVICE_NOT_AVAILABLE
+
+
+def test_null_handle_arguments(gsm):
+    L = gsm._lib()
+    assert L.gsm_global_render(None, None, None, None, 1, 1, None, 0, None, 0) == gsm.Status.INVALID_ARGUMENT
+    assert L.gsm_global_render_stereo(None, None, None, None, None, 1, 1, None, 0, None, 0) == \
+        gsm.Status.INVALID_ARGUMENT
+    assert L.gsm_global_debug_read_total_assignments(None) == 0
+    L.gsm_global_destroy(None)

@@ -1,0 +1,271 @@
+"""GPU parity: the HIP path (through the C ABI) against the C oracle, bit-exact.
+
+Every intermediate of the reference's frame is compared: GaussianRenderData of the
+visible gaussians, tile bounds, per-gaussian tile counts, unsorted and sorted keys /
+indices, tile headers, and the rgba16f colour + r16f depth targets
+(north star: headers/permutation bit-exact, colour within 1 fp16 ULP -- we require 0).
+"""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+from golden import make_golden as MG  # noqa: E402
+
+
+def to_dev(torch, arr):
+    a = np.ascontiguousarray(arr)
+    if a.size == 0:
+        return torch.zeros(16, dtype=torch.uint8, device="cuda")
+    return torch.from_numpy(a.view(np.uint8).reshape(-1).copy()).cuda()
+
+
+def gpu_render(gsm, torch, case, renderer=None, color_fill=None, keep=True, depth=True):
+    w, h = case["width"], case["height"]
+    maxw, maxh = case.get("max_width", w), case.get("max_height", h)
+    prec = 1 if case["world"].dtype.itemsize == 32 else 0
+    own = renderer is None
+    if own:
+        cfg = gsm.RendererConfig(max_gaussians=case["max_gaussians"], max_width=maxw, max_height=maxh,
+                                 precision=prec, gaussian_color_space=case.get("color_space", 0))
+        renderer = gsm.GlobalRenderer(config=cfg)
+    renderer.set_profiling(stage_events=True, keep_unsorted=keep)
+    world = to_dev(torch, case["world"])
+    harm = to_dev(torch, case["harm"])
+    n = len(case["world"]) if case.get("count") is None else case["count"]
+    color = torch.empty((h, w, 4), dtype=torch.float16, device="cuda")
+    if color_fill is not None:
+        color.fill_(color_fill)
+    else:
+        color.fill_(float("nan"))
+    dep = torch.full((h, w), float("nan"), dtype=torch.float16, device="cuda") if depth else None
+    inp = gsm.GaussianInput(world, harm, n, case["sh"])
+    cam = gsm.CameraParams.from_dict(case["cam"])
+    renderer.render(color, dep, inp, cam, w, h)
+    torch.cuda.synchronize()
+    out = {
+        "color": color.view(torch.int16).cpu().numpy().view(np.uint16),
+        "depth": dep.view(torch.int16).cpu().numpy().view(np.uint16) if depth else None,
+        "counters": renderer.counters(),
+        "render_data": renderer.copy_buffer(gsm.BufferId.RENDER_DATA),
+        "bounds": renderer.copy_buffer(gsm.BufferId.BOUNDS),
+        "tile_counts": renderer.copy_buffer(gsm.BufferId.TILE_COUNTS),
+        "sorted_keys": renderer.copy_buffer(gsm.BufferId.SORTED_KEYS),
+        "sorted_values": renderer.copy_buffer(gsm.BufferId.SORTED_VALUES),
+        "headers": renderer.copy_buffer(gsm.BufferId.HEADERS),
+        "stage_ms": renderer.stage_times_ms(),
+        "renderer": renderer,
+    }
+    if keep:
+        out["keys"] = renderer.copy_buffer(gsm.BufferId.KEYS)
+        out["values"] = renderer.copy_buffer(gsm.BufferId.VALUES)
+    return out
+
+
+def oracle_render(oracle, case):
+    return oracle.render(case["world"], case["harm"], case["sh"], case["cam"], case["width"],
+                         case["height"], max_gaussians=case["max_gaussians"],
+                         max_width=case.get("max_width"), max_height=case.get("max_height"),
+                         color_space=case.get("color_space", 0), count=case.get("count"))
+
+
+def first_diff(a, b):
+    a = np.asarray(a).reshape(-1)
+    b = np.asarray(b).reshape(-1)
+    if a.shape != b.shape:
+        return f"shape {a.shape} vs {b.shape}"
+    idx = np.nonzero(a != b)[0]
+    return f"{idx.size} diffs, first at {idx[:5].tolist()}: gpu {a[idx[:5]].tolist()} oracle {b[idx[:5]].tolist()}"
+
+
+def assert_frame_equal(g, r, stages=True):
+    c = g["counters"]
+    assert c["total_assignments"] == r["total_assignments"]
+    assert c["overflow"] == r["overflow"]
+    if stages:
+        vis = r["mask"].astype(bool)
+        gv = g["render_data"][vis].view(np.uint8)
+        rv = r["render_data"][vis].view(np.uint8)
+        assert np.array_equal(gv, rv), "render data: " + first_diff(gv, rv)
+        assert np.array_equal(g["bounds"], r["bounds"]), "bounds: " + first_diff(g["bounds"], r["bounds"])
+        assert np.array_equal(g["tile_counts"], r["tile_counts"]), \
+            "tile counts: " + first_diff(g["tile_counts"], r["tile_counts"])
+        if "keys" in g:
+            assert np.array_equal(g["keys"], r["keys"]), "keys: " + first_diff(g["keys"], r["keys"])
+            assert np.array_equal(g["values"], r["values"]), "values: " + first_diff(g["values"], r["values"])
+        assert np.array_equal(g["sorted_keys"], r["sorted_keys"]), \
+            "sorted keys: " + first_diff(g["sorted_keys"], r["sorted_keys"])
+        assert np.array_equal(g["sorted_values"], r["sorted_values"]), \
+            "sorted values: " + first_diff(g["sorted_values"], r["sorted_values"])
+        assert np.array_equal(g["headers"], r["headers"]), "headers: " + first_diff(g["headers"], r["headers"])
+    assert np.array_equal(g["color"], r["color"]), "color: " + first_diff(g["color"], r["color"])
+    if g["depth"] is not None:
+        assert np.array_equal(g["depth"], r["depth"]), "depth: " + first_diff(g["depth"], r["depth"])
+
+
+@pytest.mark.parametrize("name", MG.CASES)
+def test_golden_cases_bit_exact(gsm, cuda, oracle, name):
+    case = MG.scene(name)
+    r = oracle_render(oracle, case)
+    g = gpu_render(gsm, cuda, case)
+    assert_frame_equal(g, r)
+    g["renderer"].close()
+
+
+def test_blend_exp_table_is_correctly_rounded(gsm, cuda):
+    r = gsm.GlobalRenderer(config=gsm.RendererConfig(max_gaussians=16, max_width=64, max_height=32))
+    tbl = r.copy_buffer(gsm.BufferId.EXP_TABLE)
+    gold = np.load(os.path.join(HERE, "golden", "exp_h_table.npy"))
+    # entry p = exp_h(fp16(-0.5 * p))
+    p = np.arange(65536, dtype=np.uint32).astype(np.uint16).view(np.float16).astype(np.float32)
+    arg = (np.float32(-0.5) * p).astype(np.float16).view(np.uint16)
+    np.testing.assert_array_equal(tbl, gold[arg])
+    r.close()
+
+
+@pytest.mark.parametrize("seed,count,tiles", [(42, 1024, 10), (123, 50_000, 100)])
+def test_radix_sort_kats(gsm, cuda, seed, count, tiles):
+    """GlobalUnitTests.testRadixSortCorrectness / testRadixSortLargeScale on the HIP sort."""
+    keys = np.load(os.path.join(HERE, "golden", f"radix_kat_seed{seed}.npz"))["keys"]
+    assert keys.size == count
+    k = cuda.from_numpy(keys.view(np.int32).copy()).cuda()
+    v = cuda.arange(count, dtype=cuda.int32, device="cuda")
+    gsm.sort_pairs_u32(k, v)
+    ks = k.cpu().numpy().view(np.uint32)
+    vs = v.cpu().numpy()
+    assert np.all(ks[:-1] <= ks[1:])
+    np.testing.assert_array_equal(ks, np.sort(keys))
+    np.testing.assert_array_equal(vs, np.argsort(keys, kind="stable"))
+
+
+def test_radix_sort_random_large(gsm, cuda):
+    rng = np.random.default_rng(5)
+    for n, bits in [(1, 32), (2047, 32), (2049, 16), (3_000_001, 32)]:
+        keys = rng.integers(0, 2 ** bits, n, dtype=np.uint64).astype(np.uint32)
+        keys[: n // 3] = keys[0]  # heavy duplicates: stability matters
+        k = cuda.from_numpy(keys.view(np.int32).copy()).cuda()
+        v = cuda.arange(n, dtype=cuda.int32, device="cuda")
+        gsm.sort_pairs_u32(k, v, key_bits=bits)
+        np.testing.assert_array_equal(k.cpu().numpy().view(np.uint32), np.sort(keys, kind="stable"))
+        np.testing.assert_array_equal(v.cpu().numpy(), np.argsort(keys, kind="stable"))
+
+
+def _synth(n, w, h, sh, prec, seed, **kw):
+    from gsm_amd import scenes
+    world, harm, cam = scenes.gen_scene(n, w, h, sh, prec, seed=seed, **kw)
+    return dict(world=world, harm=harm, sh=sh, cam=cam, width=w, height=h, max_gaussians=max(n, 1))
+
+
+def test_empty_frame_is_clear(gsm, cuda, oracle):
+    case = _synth(64, 320, 180, 1, 0, 1)
+    case["count"] = 0
+    g = gpu_render(gsm, cuda, case)
+    r = oracle_render(oracle, case)
+    assert r["total_assignments"] == 0
+    assert_frame_equal(g, r, stages=False)
+    col = g["color"].view(np.float16)
+    assert np.all(col[..., :3] == 0) and np.all(col[..., 3] == 1)
+    assert np.all(g["headers"] == 0)
+
+
+def test_edge_cases(gsm, cuda, oracle):
+    from gsm_amd.types import WORLD32
+    w = np.zeros(5, WORLD32)
+    w["rot"][:, 3] = 1.0
+    # 0: huge gaussian covering the screen; 1: behind the camera; 2: tiny (scale cull);
+    # 3: transparent (alpha cull); 4: off-screen
+    w[0]["px"], w[0]["py"], w[0]["pz"], w[0]["opacity"] = 0.0, 0.0, 2.0, 0.9
+    w[0]["sx"], w[0]["sy"], w[0]["sz"] = 1.5, 0.4, 0.2
+    w[0]["rot"] = [0.2, 0.1, 0.3, 0.9]
+    w[1]["pz"], w[1]["opacity"], w[1]["sx"], w[1]["sy"], w[1]["sz"] = -2.0, 0.9, 0.1, 0.1, 0.1
+    w[2]["pz"], w[2]["opacity"], w[2]["sx"], w[2]["sy"], w[2]["sz"] = 3.0, 0.9, 1e-4, 1e-4, 1e-4
+    w[3]["pz"], w[3]["opacity"], w[3]["sx"], w[3]["sy"], w[3]["sz"] = 3.0, 0.001, 0.1, 0.1, 0.1
+    w[4]["px"], w[4]["pz"], w[4]["opacity"], w[4]["sx"], w[4]["sy"], w[4]["sz"] = 50.0, 3.0, 0.9, .1, .1, .1
+    harm = np.tile(np.array([0.3, -0.2, 0.8], np.float32), 5)
+    cam = oracle.make_camera(640, 360)
+    case = dict(world=w, harm=harm, sh=1, cam=cam, width=640, height=360, max_gaussians=5)
+    r = oracle_render(oracle, case)
+    assert list(r["mask"]) == [1, 0, 0, 0, 0]
+    g = gpu_render(gsm, cuda, case)
+    assert_frame_equal(g, r)
+
+
+def test_frame_smaller_than_max_and_reuse(gsm, cuda, oracle):
+    """width/height < maxWidth/maxHeight (tile grid from the max dims, GlobalRenderer.swift:25-51),
+    then a second, different frame on the same renderer (no stale state)."""
+    a = _synth(20_000, 600, 300, 16, 1, 11)
+    a.update(max_width=640, max_height=360, max_gaussians=30_000)
+    ra = oracle_render(oracle, a)
+    ga = gpu_render(gsm, cuda, a)
+    assert_frame_equal(ga, ra)
+    b = _synth(25_000, 640, 360, 9, 1, 12)
+    b.update(max_width=640, max_height=360, max_gaussians=30_000)
+    rb = oracle_render(oracle, b)
+    gb = gpu_render(gsm, cuda, b, renderer=ga["renderer"])
+    assert_frame_equal(gb, rb)
+    ga["renderer"].close()
+
+
+def test_null_depth_and_determinism(gsm, cuda, oracle):
+    case = _synth(30_000, 640, 360, 16, 1, 21)
+    r = oracle_render(oracle, case)
+    g1 = gpu_render(gsm, cuda, case, depth=False, keep=False)
+    assert_frame_equal(g1, r)
+    g2 = gpu_render(gsm, cuda, case, renderer=g1["renderer"], depth=False, keep=False)
+    assert np.array_equal(g1["color"], g2["color"])
+    g1["renderer"].close()
+
+
+def test_tile_row_slabs_compose_to_full_frame(gsm, cuda, oracle):
+    """Multi-GPU slab partition: rows [b, e) rendered alone equal the full frame there."""
+    case = _synth(30_000, 640, 360, 16, 1, 31)
+    r = oracle_render(oracle, case)
+    tiles_y = r["tiles_y"]
+    cfg = gsm.RendererConfig(max_gaussians=30_000, max_width=640, max_height=360, precision=1,
+                             gaussian_color_space=0)
+    rend = gsm.GlobalRenderer(config=cfg)
+    composed = np.zeros_like(r["color"])
+    bounds = [0, 7, 15, tiles_y]
+    for b, e in zip(bounds[:-1], bounds[1:]):
+        rend.set_tile_rows(b, e)
+        g = gpu_render(gsm, cuda, case, renderer=rend, color_fill=-7.0, keep=False)
+        y0, y1 = b * 16, min(e * 16, 360)
+        composed[y0:y1] = g["color"][y0:y1]
+        outside = np.concatenate([g["color"][:y0].reshape(-1), g["color"][y1:].reshape(-1)])
+        assert np.all(outside.view(np.float16) == -7.0), "slab wrote outside its rows"
+    assert np.array_equal(composed, r["color"])
+    rend.close()
+
+
+def test_stereo_is_unsupported_like_the_reference(gsm, cuda):
+    rend = gsm.GlobalRenderer(config=gsm.RendererConfig(max_gaussians=16, max_width=64, max_height=32))
+    x = cuda.zeros(16, dtype=cuda.uint8, device="cuda")
+    cam = gsm.CameraParams(np.eye(4, dtype=np.float32).reshape(-1), np.eye(4, dtype=np.float32).reshape(-1))
+    with pytest.raises(gsm.RendererError) as e:
+        rend.render_stereo(x, None, gsm.GaussianInput(x, x, 0, 0), cam, cam, 32, 32)
+    assert e.value.status == gsm.Status.UNSUPPORTED
+    with pytest.raises(gsm.RendererError) as e:
+        rend.render(x, None, gsm.GaussianInput(x, x, 17, 0), cam, 32, 32)
+    assert e.value.status == gsm.Status.INVALID_GAUSSIAN_COUNT
+    with pytest.raises(gsm.RendererError) as e:
+        rend.render(x, None, gsm.GaussianInput(x, x, 1, 0), cam, 65, 32)
+    assert e.value.status == gsm.Status.INVALID_DIMENSIONS
+    rend.close()
+
+
+@pytest.mark.parametrize("cfg_name", ["cfg2_1m_sh3_1080p_f16"])
+def test_full_size_config_bit_exact(gsm, cuda, oracle, cfg_name):
+    """BASELINE configs[1] (1M, SH3, 1920x1080, fp16) end to end against the oracle."""
+    from gsm_amd import scenes
+    c = scenes.CONFIGS[cfg_name]
+    case = _synth(c["count"], c["width"], c["height"], c["sh"], c["precision"], 42)
+    r = oracle_render(oracle, case)
+    g = gpu_render(gsm, cuda, case, keep=False)
+    assert r["overflow"] == 0
+    assert_frame_equal(g, r)
+    g["renderer"].close()

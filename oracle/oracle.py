@@ -166,6 +166,8 @@ def render(world: np.ndarray, harmonics: np.ndarray, sh_components: int, camera:
            count: int | None = None) -> dict:
     """Render one frame with the oracle; returns every intermediate as numpy arrays."""
     L = lib()
+    if nthreads <= 0:  # the GPU box exports OMP_NUM_THREADS=16 (its CPU share per GPU)
+        nthreads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
     if precision is None:
         precision = 1 if world.dtype == WORLD16 else 0
     n = len(world) if count is None else count

@@ -847,7 +847,8 @@ static void blend_tiles(void *vctx, uint32_t lo, uint32_t hi) {
                 for (int j = 0; j < 2; ++j) posy[j] = og_f2h((float)(baseY + (uint32_t)j));
                 uint16_t T[8], C[8][3], D[8];
                 for (int q = 0; q < 8; ++q) { T[q] = H_ONE; C[q][0] = C[q][1] = C[q][2] = H_ZERO; D[q] = H_ZERO; }
-                for (uint32_t i = 0; i < count; ++i) {
+                uint32_t i = 0;
+                for (; i < count; ++i) {
                     uint16_t m0 = hmax(hmax(T[0], T[1]), hmax(T[2], T[3]));
                     uint16_t m1 = hmax(hmax(T[4], T[5]), hmax(T[6], T[7]));
                     if (H(hmax(m0, m1)) < H(thr)) break;
@@ -879,6 +880,7 @@ static void blend_tiles(void *vctx, uint32_t lo, uint32_t hi) {
                         T[q] = hmul(T[q], hsub(H_ONE, a[q]));
                     }
                 }
+                f->group_iters[(size_t)tile * 64 + ly * 8 + lx] = i;
                 for (int j = 0; j < 2; ++j)
                     for (int ii = 0; ii < 4; ++ii) {
                         uint32_t x = baseX + (uint32_t)ii, y = baseY + (uint32_t)j;
@@ -920,7 +922,7 @@ void og_frame_free(og_frame *f) {
     if (!f) return;
     free(f->render_data); free(f->bounds); free(f->mask); free(f->tile_counts);
     free(f->keys); free(f->values); free(f->sorted_keys); free(f->sorted_values);
-    free(f->headers); free(f->color); free(f->depth);
+    free(f->headers); free(f->color); free(f->depth); free(f->group_iters);
     free(f);
 }
 
@@ -958,11 +960,12 @@ int og_render(const og_config *cfg, const void *gaussians, const void *harmonics
     f->headers = (uint32_t *)calloc((size_t)f->tile_count * 2, sizeof(uint32_t));
     f->color = (uint16_t *)calloc((size_t)width * height * 4, sizeof(uint16_t));
     f->depth = (uint16_t *)calloc((size_t)width * height, sizeof(uint16_t));
+    f->group_iters = (uint32_t *)calloc((size_t)f->tile_count * 64, sizeof(uint32_t));
     uint32_t *offsets = (uint32_t *)calloc(n, sizeof(uint32_t));
     conic3 *conic = (conic3 *)calloc(n, sizeof(conic3));
     float *power = (float *)calloc(n, sizeof(float));
     if (!f->render_data || !f->bounds || !f->mask || !f->tile_counts || !f->headers || !f->color ||
-        !f->depth || !offsets || !conic || !power) {
+        !f->depth || !f->group_iters || !offsets || !conic || !power) {
         free(offsets); free(conic); free(power);
         og_frame_free(f);
         return OG_ERR_OUT_OF_MEMORY;

@@ -93,6 +93,7 @@ typedef struct {
     uint32_t *headers;           /* [tile_count*2] {offset,count} */
     uint16_t *color;             /* [height*width*4] rgba16f bits */
     uint16_t *depth;             /* [height*width]   r16f bits */
+    uint32_t *group_iters;       /* [tile_count*64] entries each 4x2 thread group processed before its break */
     double t_project, t_assign, t_sort, t_headers, t_blend; /* seconds */
 } og_frame;
 

@@ -47,6 +47,7 @@ class OgFrame(C.Structure):
                 ("tile_counts", C.c_void_p), ("keys", C.c_void_p), ("values", C.c_void_p),
                 ("sorted_keys", C.c_void_p), ("sorted_values", C.c_void_p),
                 ("headers", C.c_void_p), ("color", C.c_void_p), ("depth", C.c_void_p),
+                ("group_iters", C.c_void_p),
                 ("t_project", C.c_double), ("t_assign", C.c_double), ("t_sort", C.c_double),
                 ("t_headers", C.c_double), ("t_blend", C.c_double)]
 
@@ -200,6 +201,7 @@ def render(world: np.ndarray, harmonics: np.ndarray, sh_components: int, camera:
             "headers": _arr(f.headers, np.uint32, f.tile_count * 2).reshape(-1, 2),
             "color": _arr(f.color, np.uint16, width * height * 4).reshape(height, width, 4),
             "depth": _arr(f.depth, np.uint16, width * height).reshape(height, width),
+            "group_iters": _arr(f.group_iters, np.uint32, f.tile_count * 64).reshape(-1, 8, 8),
             "times": {"project": f.t_project, "assign": f.t_assign, "sort": f.t_sort,
                       "headers": f.t_headers, "blend": f.t_blend},
         }

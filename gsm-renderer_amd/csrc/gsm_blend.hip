@@ -1,0 +1,453 @@
+// gsm_blend.hip -- the GlobalRenderer's blend stage on gfx950: clear + front-to-back
+// alpha blending of every tile's depth-sorted list (globalRender, GlobalShaders.metal:1030-1187;
+// clear: :140-154), plus the load-balancing schedule of its work units.
+//
+// Persistent workgroups: one workgroup per CU holds the 128 KiB fp16 exp table in LDS and its
+// waves pull work units (parts of tiles) from a device counter.  Bit-exact with the oracle: the
+// per-thread saturation break of the reference (one 4x2 pixel group) is evaluated per group on
+// every list entry.  Numeric contract: DESIGN.md.
+#include <hip/hip_runtime.h>
+
+#include <cstdlib>
+
+#include "gsm_internal.h"
+#include "gsm_types.h"
+
+namespace gsm {
+
+typedef _Float16 h1;
+typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ h2 as_h2(uint32_t u) { return __builtin_bit_cast(h2, u); }
+__device__ __forceinline__ uint32_t as_u32(h2 v) { return __builtin_bit_cast(uint32_t, v); }
+__device__ __forceinline__ h2 splat_lo(h2 v) { return h2{v.x, v.x}; }
+__device__ __forceinline__ h2 splat_hi(h2 v) { return h2{v.y, v.y}; }
+
+// exp table lookup for a packed pair of quadratic forms: the table is indexed by the fp16 bits
+// of p and holds fp16(exp(fp16(-0.5 * p))), correctly rounded (gsm_detmath.h)
+__device__ __forceinline__ h2 lookup2(const uint16_t* tbl, h2 p) {
+    const uint32_t pb = as_u32(p);
+    const uint32_t lo = tbl[pb & 0xFFFFu];
+    const uint32_t hi = tbl[pb >> 16];
+    return as_h2(lo | (hi << 16));
+}
+
+// max over the 4 lanes of a quad: DPP quad_perm [1,0,3,2] then [2,3,0,1]
+__device__ __forceinline__ uint32_t quad_max_u32(uint32_t v) {
+    const uint32_t a = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);
+    v = v > a ? v : a;
+    const uint32_t b = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);
+    return v > b ? v : b;
+}
+
+// ---------------------------------------------------------------------------
+// k_blend_px: one wave per blend unit, P pixel pairs per lane.
+//   P = 1: 16x8 quadrant of a tile (4 units per tile), a 4x2 group spans 4 lanes
+//   P = 2: 16x16 half tile (2 units per tile), a group spans 2 lanes (rows)
+//   P = 4: the 32x16 tile, a lane is one reference thread (4x2 pixels)
+// More pairs per lane give every list entry's uniform work (5 readlanes, the dy terms of
+// the quadratic form) to more pixels and P independent T chains per lane; fewer give
+// shorter walks (a unit walks until its slowest group breaks).  The list is walked in
+// groups of U = 4/P entries through a three-stage software pipeline (stage 1: next group's
+// p and table reads; stage 2: blend this group; stage 3: next group's alphas).
+// ---------------------------------------------------------------------------
+template <int NT, int P>
+__global__ __launch_bounds__(NT) void k_blend_px(
+    const GaussianHeader* __restrict__ headers, const uint32_t* __restrict__ sortedVals,
+    const BlendRecordA* __restrict__ recA, const uint32_t* __restrict__ recB,
+    const uint16_t* __restrict__ expTable, uint32_t* __restrict__ queue, uint32_t tileBegin,
+    uint32_t numTiles, uint32_t tilesX, uint32_t W, uint32_t H, uint8_t* __restrict__ color,
+    size_t colorPitch, uint8_t* __restrict__ depth, size_t depthPitch, int flags,
+    const uint32_t* __restrict__ order, uint16_t* __restrict__ unitCost,
+    unsigned long long* __restrict__ trace) {
+    static_assert(P == 1 || P == 2 || P == 4, "pairs per lane");
+    constexpr uint32_t U = 4 / P;        // entries per pipeline group
+    constexpr uint32_t NG = 64 / U;      // groups per 64-entry batch
+    constexpr uint32_t EXITG = 16 / U;   // exit test every 16 entries
+    constexpr uint32_t UPT = 4 / P;      // units per tile
+    constexpr uint32_t NW = NT / 64;
+    constexpr uint32_t UNROLL = P == 4 ? 1 : NG;  // P = 4: 64 one-entry groups stay a loop
+    const bool vecStores = (flags & 1) != 0;
+    const bool agePrio = (flags & 2) != 0;
+    __shared__ __attribute__((aligned(16))) uint16_t tbl[65536];
+    {
+        const uint4* src = (const uint4*)expTable;
+        uint4* dst = (uint4*)tbl;
+        for (int i = threadIdx.x; i < 65536 * 2 / 16; i += NT) dst[i] = src[i];
+    }
+    __syncthreads();
+
+    const uint32_t lane = threadIdx.x & 63;
+    // pixel pair k of this lane sits at (px[k], py[k]) and (px[k] + 1, py[k]) inside the unit
+    uint32_t offX[P], offY[P];
+    if (P == 1) {
+        const uint32_t grp = lane >> 2;
+        offX[0] = (grp & 3u) * 4u + (lane & 1u) * 2u;
+        offY[0] = (grp >> 2) * 2u + ((lane >> 1) & 1u);
+    } else if (P == 2) {
+        const uint32_t grp = lane >> 1;
+        offX[0] = (grp & 3u) * 4u;
+        offX[P - 1] = offX[0] + 2u;
+        offY[0] = offY[P - 1] = (grp >> 2) * 2u + (lane & 1u);
+    } else {
+        offX[0] = offX[2 % P] = (lane & 7u) * 4u;
+        offX[1 % P] = offX[3 % P] = (lane & 7u) * 4u + 2u;
+        offY[0] = offY[1 % P] = (lane >> 3) * 2u;
+        offY[2 % P] = offY[3 % P] = (lane >> 3) * 2u + 1u;
+    }
+    const h2 ONE = {(h1)1.0f, (h1)1.0f};
+    const h2 ZERO = {(h1)0.0f, (h1)0.0f};
+    const uint32_t thrBits = (uint32_t)__builtin_bit_cast(uint16_t, (h1)(1.0f / 255.0f));
+    const h1 c099 = (h1)0.99;
+    const h2 C099 = {c099, c099};
+    const uint32_t numUnits = numTiles * UPT;
+    const uint32_t gridWaves = gridDim.x * NW;
+
+    uint32_t qi = blockIdx.x * NW + (threadIdx.x >> 6);  // first unit static, then the queue
+    while (qi < numUnits) {
+        uint32_t u = order ? __builtin_amdgcn_readfirstlane(order[qi]) : qi;
+        if (u >= numUnits) u = qi;  // a schedule is a permutation of [0, numUnits); never trust it further
+        const uint32_t tile = tileBegin + u / UPT, part = u % UPT;
+        const uint32_t tileX = tile % tilesX, tileY = tile / tilesX;
+        const uint32_t ux = tileX * kTileWidth + (P == 4 ? 0u : (part & 1u) * 16u);
+        const uint32_t uy = tileY * kTileHeight + (P == 1 ? (part >> 1) * 8u : 0u);
+        const GaussianHeader hdr = headers[tile];
+        const uint32_t start = __builtin_amdgcn_readfirstlane(hdr.offset);
+        const uint32_t count = __builtin_amdgcn_readfirstlane(hdr.count);
+        unsigned long long tStart = 0;
+        if (trace) tStart = __builtin_amdgcn_s_memrealtime();
+        uint32_t nproc = 0;
+        uint32_t nextQ = 0;
+
+        h2 T[P], R[P], G[P], B[P], D[P];
+#pragma unroll
+        for (int k = 0; k < P; ++k) {
+            T[k] = ONE;
+            R[k] = G[k] = B[k] = D[k] = ZERO;
+        }
+        if (count > 0) {
+            h2 X[P], Yv;  // Yv: the lane's (up to) two rows
+#pragma unroll
+            for (int k = 0; k < P; ++k) X[k] = h2{(h1)(float)(ux + offX[k]), (h1)(float)(ux + offX[k] + 1u)};
+            Yv = h2{(h1)(float)(uy + offY[0]), (h1)(float)(uy + offY[P - 1])};
+            const uint32_t* lst = sortedVals + start;
+            // Batch registers: lane l of bA/bB holds list entry b0 + l, nA/nB entry b0 + 64 + l,
+            // mA/mB entry b0 + 128 + l, nI the index of entry b0 + 192 + l.  Loads are
+            // unpredicated (clamped index) and issued one batch ahead of their first use, so
+            // the group loop never waits on memory (a predicated load would merge with the old
+            // register value and force a copy -- and a vmcnt wait -- into the loop).  Lanes past
+            // the list end hold a neutral record: mean = unit origin, conic = 0, opacity = 0
+            // gives p = 0, alpha = 0 exactly, which leaves T, C and the break state unchanged.
+            const uint32_t last = count - 1u;
+            const uint4 pad = make_uint4(as_u32(h2{(h1)(float)ux, (h1)(float)uy}), 0u, 0u, 0u);
+            const uint32_t gi0 = lst[min(lane, last)];
+            const uint32_t gi1 = lst[min(64u + lane, last)];
+            const uint32_t gi2 = lst[min(128u + lane, last)];
+            uint4 bA = *(const uint4*)(recA + gi0);
+            uint32_t bB = recB[gi0];
+            uint4 nA = *(const uint4*)(recA + gi1);
+            uint32_t nB = recB[gi1];
+            uint4 mA = *(const uint4*)(recA + gi2);
+            uint32_t mB = recB[gi2];
+            uint32_t nI = lst[min(192u + lane, last)];
+            if (lane == 0) nextQ = atomicAdd(queue, 1u);
+            if (lane >= count) {
+                bA = pad;
+                bB = 0u;
+            }
+            if (64u + lane >= count) {
+                nA = pad;
+                nB = 0u;
+            }
+
+            h2 ac[U][P], om[U][P];
+            uint32_t rgc[U], bdc[U], rgn[U], bdn[U], opn[U];
+            uint32_t eln[U][P], ehn[U][P];
+            bool alive = true;
+            // p = ((dx*dx)*cxx + (dy*dy)*cyy) + (dx*dy)*cxy2 (GlobalShaders.metal:1115-1122);
+            // the dy terms are shared by the pairs of a row
+            auto quadform = [&](uint32_t r0, uint32_t r1, uint32_t r2, h2 (&pq)[P]) {
+                const h2 mean = as_h2(r0), cc = as_h2(r1), oc = as_h2(r2);
+                const h2 dyv = Yv - splat_hi(mean);
+                const h2 dyy = (dyv * dyv) * splat_hi(cc);
+#pragma unroll
+                for (int k = 0; k < P; ++k) {
+                    const h2 dx = X[k] - splat_lo(mean);
+                    const bool r2nd = (P == 4) && (k >= 2);
+                    const h2 dy = r2nd ? splat_hi(dyv) : splat_lo(dyv);
+                    const h2 yy = r2nd ? splat_hi(dyy) : splat_lo(dyy);
+                    pq[k] = ((dx * dx) * splat_lo(cc) + yy) + (dx * dy) * splat_lo(oc);
+                }
+            };
+            // prime group 0
+#pragma unroll
+            for (uint32_t k = 0; k < U; ++k) {
+                const uint32_t r2 = __builtin_amdgcn_readlane(bA.z, k);
+                h2 pq[P];
+                quadform(__builtin_amdgcn_readlane(bA.x, k), __builtin_amdgcn_readlane(bA.y, k), r2, pq);
+                rgc[k] = __builtin_amdgcn_readlane(bA.w, k);
+                bdc[k] = __builtin_amdgcn_readlane(bB, k);
+#pragma unroll
+                for (int q = 0; q < P; ++q) {
+                    // a = min(opacity * exp(-0.5h * p), 0.99h) (GlobalShaders.metal:1124-1131)
+                    ac[k][q] = __builtin_elementwise_min(splat_hi(as_h2(r2)) * lookup2(tbl, pq[q]), C099);
+                    om[k][q] = ONE - ac[k][q];
+                }
+            }
+            for (uint32_t b0 = 0;; b0 += 64u) {
+#pragma unroll UNROLL
+                for (uint32_t gi = 0; gi < NG; ++gi) {
+                    // stage 1: the next group's table words go in flight (independent of T)
+                    {
+                        const bool nb = gi + 1 == NG;
+                        const uint32_t sx = nb ? nA.x : bA.x, sy = nb ? nA.y : bA.y;
+                        const uint32_t sz = nb ? nA.z : bA.z, sw = nb ? nA.w : bA.w;
+                        const uint32_t sb = nb ? nB : bB;
+#pragma unroll
+                        for (uint32_t k = 0; k < U; ++k) {
+                            const uint32_t j = ((gi + 1) * U + k) & 63u;
+                            h2 pq[P];
+                            opn[k] = __builtin_amdgcn_readlane(sz, j);
+                            quadform(__builtin_amdgcn_readlane(sx, j), __builtin_amdgcn_readlane(sy, j), opn[k], pq);
+                            rgn[k] = __builtin_amdgcn_readlane(sw, j);
+                            bdn[k] = __builtin_amdgcn_readlane(sb, j);
+#pragma unroll
+                            for (int q = 0; q < P; ++q) {
+                                const uint32_t pb = as_u32(pq[q]);
+                                eln[k][q] = tbl[pb & 0xFFFFu];
+                                ehn[k][q] = tbl[pb >> 16];
+                            }
+                        }
+                    }
+                    // stage 2: blend the current group
+#pragma unroll
+                    for (uint32_t k = 0; k < U; ++k) {
+                        // group break (GlobalShaders.metal:1086-1088): max T of the 4x2 group
+                        h2 tm = T[0];
+#pragma unroll
+                        for (int q = 1; q < P; ++q) tm = __builtin_elementwise_max(tm, T[q]);
+                        const uint32_t tb = as_u32(tm);
+                        uint32_t gm = max(tb & 0xFFFFu, tb >> 16);
+                        if (P == 1) gm = quad_max_u32(gm);
+                        if (P == 2) {
+                            const uint32_t o = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)gm, 0xB1, 0xF, 0xF, false);
+                            gm = max(gm, o);
+                        }
+                        alive = alive && !(gm < thrBits);  // T >= 0: fp16 order == bit order
+                        const h2 rgv = as_h2(rgc[k]), bdv = as_h2(bdc[k]);
+#pragma unroll
+                        for (int q = 0; q < P; ++q) {
+                            // a dead lane keeps T and blends nothing (alpha 0 would give C + c*0 == C)
+                            const h2 Tn = T[q] * om[k][q];
+                            const h2 aT = ac[k][q] * T[q];  // (GlobalShaders.metal:1137-1149)
+                            const h2 w = alive ? aT : ZERO;
+                            T[q] = alive ? Tn : T[q];
+                            R[q] = R[q] + splat_lo(rgv) * w;
+                            G[q] = G[q] + splat_hi(rgv) * w;
+                            B[q] = B[q] + splat_lo(bdv) * w;
+                            D[q] = D[q] + splat_hi(bdv) * w;
+                        }
+                    }
+                    const uint32_t g1 = b0 + (gi + 1) * U;
+                    // late exits are harmless: neutral records past the end, dead lanes blend nothing
+                    if ((gi + 1) % EXITG == 0 && (g1 >= count || __ballot(alive) == 0)) {
+                        nproc = g1;
+                        goto unit_done;
+                    }
+                    // stage 3: the next group's alphas
+#pragma unroll
+                    for (uint32_t k = 0; k < U; ++k) {
+#pragma unroll
+                        for (int q = 0; q < P; ++q) {
+                            const h2 ek = as_h2(eln[k][q] | (ehn[k][q] << 16));
+                            ac[k][q] = __builtin_elementwise_min(splat_hi(as_h2(opn[k])) * ek, C099);
+                            om[k][q] = ONE - ac[k][q];
+                        }
+                        rgc[k] = rgn[k];
+                        bdc[k] = bdn[k];
+                    }
+                }
+                if (agePrio) {
+                    if (b0 == 0) __builtin_amdgcn_s_setprio(1);
+                    else if (b0 == 128u) __builtin_amdgcn_s_setprio(2);
+                    else if (b0 == 320u) __builtin_amdgcn_s_setprio(3);
+                }
+                bA = nA;
+                bB = nB;
+                const bool mv = b0 + 128u + lane < count;
+                nA = mv ? mA : pad;
+                nB = mv ? mB : 0u;
+                mA = *(const uint4*)(recA + nI);
+                mB = recB[nI];
+                nI = lst[min(b0 + 256u + lane, last)];
+            }
+        unit_done:;
+        } else {
+            if (lane == 0) nextQ = atomicAdd(queue, 1u);
+        }
+        // write (GlobalShaders.metal:1152-1186); empty tiles keep the clear colour (0,0,0,1)
+#pragma unroll
+        for (int q = 0; q < P; ++q) {
+            const uint32_t px = ux + offX[q], py = uy + offY[q];
+            const h2 Av = (count > 0) ? (ONE - T[q]) : ONE;
+            if (py < H) {
+                uint8_t* crow = color + (size_t)py * colorPitch;
+                // integer packing (extracting .y of a half2 via __builtin_bit_cast miscompiled)
+                const uint32_t ur = as_u32(R[q]), ug = as_u32(G[q]), ub = as_u32(B[q]), ua = as_u32(Av);
+                const uint32_t p0a = (ur & 0xFFFFu) | (ug << 16);
+                const uint32_t p0b = (ub & 0xFFFFu) | (ua << 16);
+                const uint32_t p1a = (ur >> 16) | (ug & 0xFFFF0000u);
+                const uint32_t p1b = (ub >> 16) | (ua & 0xFFFF0000u);
+                const uint32_t ud = as_u32(D[q]);
+                if (vecStores && px + 1 < W) {
+                    *(uint4*)(crow + (size_t)px * 8) = make_uint4(p0a, p0b, p1a, p1b);
+                    if (depth) *(uint32_t*)(depth + (size_t)py * depthPitch + (size_t)px * 2) = ud;
+                } else {
+                    if (px < W) {
+                        uint32_t* c0 = (uint32_t*)(crow + (size_t)px * 8);
+                        c0[0] = p0a;
+                        c0[1] = p0b;
+                        if (depth) *(uint16_t*)(depth + (size_t)py * depthPitch + (size_t)px * 2) = (uint16_t)(ud & 0xFFFFu);
+                    }
+                    if (px + 1 < W) {
+                        uint32_t* c1 = (uint32_t*)(crow + (size_t)(px + 1) * 8);
+                        c1[0] = p1a;
+                        c1[1] = p1b;
+                        if (depth) *(uint16_t*)(depth + (size_t)py * depthPitch + (size_t)(px + 1) * 2) = (uint16_t)(ud >> 16);
+                    }
+                }
+            }
+        }
+        if (lane == 0) unitCost[u] = (uint16_t)min(nproc, 65535u);
+        if (trace && lane == 0) {
+            unsigned long long* t = trace + (size_t)u * 4;
+            t[0] = tStart;
+            t[1] = __builtin_amdgcn_s_memrealtime();
+            t[2] = ((unsigned long long)count << 32) | nproc;
+            t[3] = ((unsigned long long)__builtin_amdgcn_s_getreg(20 | (31 << 11)) << 32) |
+                   (unsigned long long)__builtin_amdgcn_s_getreg(4 | (31 << 11));
+        }
+        if (agePrio) __builtin_amdgcn_s_setprio(0);
+        qi = __builtin_amdgcn_readfirstlane(nextQ) + gridWaves;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Blend schedule: a stable sort of the units into 8 linear buckets of last frame's walk length
+// (longest bucket first; index order, i.e. tile locality, kept inside a bucket), one workgroup.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(1024) void k_unit_order(const uint16_t* __restrict__ cost,
+                                                     uint32_t* __restrict__ order, uint32_t n) {
+    constexpr uint32_t NB = 8, NWV = 16;
+    __shared__ uint32_t wmax[NWV];
+    __shared__ uint32_t cnt[NWV][NB];
+    const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
+    // pass 1: the longest walk
+    uint32_t m = 0;
+    for (uint32_t i = t; i < n; i += 1024) m = max(m, (uint32_t)cost[i]);
+    for (int off = 32; off > 0; off >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, off));
+    if (lane == 0) wmax[w] = m;
+    __syncthreads();
+    uint32_t mx = 0;
+    for (uint32_t k = 0; k < NWV; ++k) mx = max(mx, wmax[k]);
+    const uint32_t den = mx + 1u;
+    // pass 2: per-wave bucket counts over a contiguous range of units
+    const uint32_t per = ((n + NWV - 1) / NWV + 63u) & ~63u;
+    const uint32_t lo = min(n, w * per), hi = min(n, lo + per);
+    uint32_t myCnt = 0;  // lane b < NB counts bucket b
+    for (uint32_t c = lo; c < hi; c += 64) {
+        const uint32_t i = c + lane;
+        const uint32_t bk = i < hi ? (NB - 1u) - min(NB - 1u, (uint32_t)cost[i] * NB / den) : NB;
+        for (uint32_t b2 = 0; b2 < NB; ++b2) {
+            const uint32_t pc = (uint32_t)__popcll(__ballot(bk == b2));
+            if (lane == b2) myCnt += pc;
+        }
+    }
+    if (lane < NB) cnt[w][lane] = myCnt;
+    __syncthreads();
+    // bases: bucket-major (bk 0 = longest), then wave order -> stable
+    uint32_t base = 0;  // lane b < NB: where this wave's bucket-b units start
+    if (lane < NB) {
+        for (uint32_t b2 = 0; b2 < lane; ++b2)
+            for (uint32_t k = 0; k < NWV; ++k) base += cnt[k][b2];
+        for (uint32_t k = 0; k < w; ++k) base += cnt[k][lane];
+    }
+    // pass 3: scatter in index order
+    for (uint32_t c = lo; c < hi; c += 64) {
+        const uint32_t i = c + lane;
+        const uint32_t bk = i < hi ? (NB - 1u) - min(NB - 1u, (uint32_t)cost[i] * NB / den) : NB;
+        for (uint32_t b2 = 0; b2 < NB; ++b2) {
+            const uint64_t msk = __ballot(bk == b2);
+            const uint32_t bb = (uint32_t)__shfl((int)base, (int)b2);
+            if (bk == b2) order[bb + (uint32_t)__popcll(msk & ((1ull << lane) - 1ull))] = i;
+            if (lane == b2) base += (uint32_t)__popcll(msk);
+        }
+    }
+}
+
+
+int blend_pairs_per_lane() {
+    const char* v = getenv("GSM_BLEND_PAIRS");
+    const int p = v ? atoi(v) : 2;
+    return (p == 1 || p == 2 || p == 4) ? p : 2;
+}
+
+uint32_t blend_units_per_tile() { return 4u / (uint32_t)blend_pairs_per_lane(); }
+
+static int blend_waves_per_wg() {
+    const char* v = getenv("GSM_BLEND_WAVES");
+    const int w = v ? atoi(v) : 8;
+    return (w == 8 || w == 16) ? w : 8;
+}
+
+bool blend_schedule_enabled(uint32_t numTiles, int numCUs) {
+    const char* v = getenv("GSM_BLEND_SCHED");  // 0 = index order, 1 = cost order, else auto
+    if (v && v[0] == '0') return false;
+    if (v && v[0] == '1') return true;
+    // Ordering by last frame's walks pays where units are few per wave slot (balance), and
+    // costs L2 locality where they are many (at 4K the index order's tile neighbourhoods win).
+    const uint64_t slots = (uint64_t)numCUs * (uint64_t)blend_waves_per_wg();
+    return (uint64_t)numTiles * blend_units_per_tile() < 8u * slots;
+}
+
+void launch_unit_order(uint32_t numUnits, const DeviceArena& A, hipStream_t s) {
+    hipLaunchKernelGGL(k_unit_order, dim3(1), dim3(1024), 0, s, A.unitCost, A.unitOrder, numUnits);
+}
+
+void launch_blend(const uint32_t* sortedVals, const FrameGeometry& g, const DeviceArena& A, void* color,
+                  size_t colorPitch, void* depth, size_t depthPitch, int numCUs, bool costOrder,
+                  hipStream_t s) {
+    const uint32_t t0 = g.rowBegin * g.tilesX, t1 = g.rowEnd * g.tilesX;
+    if (t1 <= t0) return;
+    const uint32_t numTiles = t1 - t0;
+    const int vec = ((((uintptr_t)color) & 15u) == 0 && (colorPitch & 15u) == 0 &&
+                     (depth == nullptr || ((((uintptr_t)depth) & 7u) == 0 && (depthPitch & 7u) == 0)))
+                        ? 1
+                        : 0;
+    const char* pv = getenv("GSM_BLEND_PRIO");  // age-raised wave priority (default on)
+    const int flags = vec | ((pv && pv[0] == '0') ? 0 : 2);
+    hipMemsetAsync(A.tileQueue, 0, sizeof(uint32_t), s);
+    const int P = blend_pairs_per_lane();
+    const int waves = blend_waves_per_wg();
+    const uint32_t units = numTiles * (4u / (uint32_t)P);
+    uint32_t grid = (units + (uint32_t)waves - 1) / (uint32_t)waves;
+    if (grid > (uint32_t)numCUs) grid = (uint32_t)numCUs;
+#define GSM_LAUNCH_PX(NTH, PP)                                                                      \
+    hipLaunchKernelGGL((k_blend_px<NTH, PP>), dim3(grid), dim3(NTH), 0, s, A.headers, sortedVals,   \
+                       A.recA, A.recB, A.expTable, A.tileQueue, t0, numTiles, g.tilesX, g.width,    \
+                       g.height, (uint8_t*)color, colorPitch, (uint8_t*)depth, depthPitch, flags,    \
+                       costOrder ? A.unitOrder : nullptr, A.unitCost, A.blendTrace)
+#define GSM_LAUNCH_P(NTH)                    \
+    if (P == 1) GSM_LAUNCH_PX(NTH, 1);       \
+    else if (P == 4) GSM_LAUNCH_PX(NTH, 4);  \
+    else GSM_LAUNCH_PX(NTH, 2)
+    if (waves == 16) {
+        GSM_LAUNCH_P(1024);
+    } else {
+        GSM_LAUNCH_P(512);
+    }
+#undef GSM_LAUNCH_P
+#undef GSM_LAUNCH_PX
+}
+
+}  // namespace gsm

@@ -30,10 +30,13 @@ struct DeviceArena {
     uint32_t* vals[2] = {nullptr, nullptr};    // [cap]
     uint32_t* keysKeep = nullptr;              // [cap] unsorted copy (profiling/debug only)
     uint32_t* valsKeep = nullptr;
+    unsigned long long* blendTrace = nullptr;  // [4 * tiles * 4] (profiling bit 2 only)
     uint32_t* radixHist = nullptr;             // [256 * radixGrid]
     uint32_t* radixBinTotals = nullptr;        // [256]
     GaussianHeader* headers = nullptr;         // [tileCount]
     uint32_t* tileQueue = nullptr;             // [1] blend work counter
+    uint16_t* unitCost = nullptr;              // [4 * tileCount] list entries each blend unit walked
+    uint32_t* unitOrder = nullptr;             // [4 * tileCount] blend units, longest last-frame walk first
     uint16_t* expTable = nullptr;              // [65536]
     float2* sincosTable = nullptr;             // [65536]
 };
@@ -57,7 +60,15 @@ void launch_headers(const uint32_t* sortedKeys, const FrameGeometry& geo, const 
 // front-to-back fp16 blend + clear (GlobalShaders.metal:140-154, 1030-1187)
 void launch_blend(const uint32_t* sortedVals, const FrameGeometry& geo, const DeviceArena& A,
                   void* color, size_t colorPitch, void* depth, size_t depthPitch, int numCUs,
-                  hipStream_t stream);
+                  bool costOrder, hipStream_t stream);
+// orders the blend units by the walk lengths the previous frame measured (longest first), so
+// the dynamic queue hands out long units before short ones
+void launch_unit_order(uint32_t numUnits, const DeviceArena& A, hipStream_t stream);
+// blend kernel shape: pixel pairs per lane (0 = quadrant kernel) and blend units per tile
+int blend_pairs_per_lane();
+uint32_t blend_units_per_tile();
+// whether the blend follows last frame's cost order (few units per wave slot) or index order
+bool blend_schedule_enabled(uint32_t numTiles, int numCUs);
 
 // Stable LSD radix sort of (key, value) pairs; n read from device memory *nPtr.
 // Returns the index (0/1) of the ping-pong buffer holding the result.

@@ -5,6 +5,8 @@
 // Numeric contract: DESIGN.md (built with -ffp-contract=off, IEEE div/sqrt).
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "gsm_detmath.h"
 #include "gsm_internal.h"
 #include "gsm_types.h"
@@ -708,203 +710,6 @@ __global__ __launch_bounds__(256) void k_headers(const uint32_t* __restrict__ so
 }
 
 // ---------------------------------------------------------------------------
-// 5. blend (globalRender, GlobalShaders.metal:1030-1187) + clear (:140-154)
-//
-// Persistent: one 1024-thread workgroup per CU holds the 128 KiB fp16 exp table
-// in LDS; each of its 16 waves pulls 32x16 tiles from a device counter.  A wave is
-// one tile: lane = 4x2 pixel group at (lx*4, ly*2) exactly like the reference's
-// 8x8 threadgroup, so the per-thread saturation break is preserved.
-// ---------------------------------------------------------------------------
-constexpr int kBlendThreads = 1024;
-
-__device__ __forceinline__ h2 as_h2(uint32_t u) { return __builtin_bit_cast(h2, u); }
-__device__ __forceinline__ uint32_t as_u32(h2 v) { return __builtin_bit_cast(uint32_t, v); }
-__device__ __forceinline__ h2 splat_lo(h2 v) { return h2{v.x, v.x}; }
-__device__ __forceinline__ h2 splat_hi(h2 v) { return h2{v.y, v.y}; }
-
-__device__ __forceinline__ h2 lookup2(const uint16_t* tbl, h2 p) {
-    uint32_t pb = as_u32(p);
-    uint32_t lo = tbl[pb & 0xFFFFu];
-    uint32_t hi = tbl[pb >> 16];
-    return as_h2(lo | (hi << 16));
-}
-
-__global__ __launch_bounds__(kBlendThreads) void k_blend(
-    const GaussianHeader* __restrict__ headers, const uint32_t* __restrict__ sortedVals,
-    const BlendRecordA* __restrict__ recA, const uint32_t* __restrict__ recB,
-    const uint16_t* __restrict__ expTable, uint32_t* __restrict__ queue, uint32_t tileBegin,
-    uint32_t numTiles, uint32_t tilesX, uint32_t W, uint32_t H, uint8_t* __restrict__ color,
-    size_t colorPitch, uint8_t* __restrict__ depth, size_t depthPitch, int vecStores) {
-    __shared__ uint16_t tbl[65536];
-    {
-        const uint4* src = (const uint4*)expTable;
-        uint4* dst = (uint4*)tbl;
-        for (int i = threadIdx.x; i < 65536 * 2 / 16; i += kBlendThreads) dst[i] = src[i];
-    }
-    __syncthreads();
-
-    const uint32_t lane = threadIdx.x & 63;
-    const uint32_t lx = lane & 7, ly = lane >> 3;
-    const h2 ONE = {(h1)1.0f, (h1)1.0f};
-    const h2 ZERO = {(h1)0.0f, (h1)0.0f};
-    const h1 thr = (h1)(1.0f / 255.0f);  // half(1.0h/255.0h)
-    const h1 c099 = (h1)0.99;            // 0.99h
-    const h2 C099 = {c099, c099};
-
-    for (;;) {
-        uint32_t qi = 0;
-        if (lane == 0) qi = atomicAdd(queue, 1u);
-        qi = __builtin_amdgcn_readfirstlane(qi);
-        if (qi >= numTiles) break;
-        const uint32_t tile = tileBegin + qi;
-        const uint32_t tileX = tile % tilesX, tileY = tile / tilesX;
-        const uint32_t baseX = tileX * kTileWidth + lx * 4, baseY = tileY * kTileHeight + ly * 2;
-        const GaussianHeader hdr = headers[tile];
-        const uint32_t start = __builtin_amdgcn_readfirstlane(hdr.offset);
-        const uint32_t count = __builtin_amdgcn_readfirstlane(hdr.count);
-
-        h2 T0a = ONE, T0b = ONE, T1a = ONE, T1b = ONE;  // row 0: px 0-1, 2-3; row 1
-        h2 R0a = ZERO, R0b = ZERO, R1a = ZERO, R1b = ZERO;
-        h2 G0a = ZERO, G0b = ZERO, G1a = ZERO, G1b = ZERO;
-        h2 B0a = ZERO, B0b = ZERO, B1a = ZERO, B1b = ZERO;
-        h2 D0a = ZERO, D0b = ZERO, D1a = ZERO, D1b = ZERO;
-
-        if (count > 0) {
-            const h2 Xa = {(h1)(float)(baseX + 0), (h1)(float)(baseX + 1)};
-            const h2 Xb = {(h1)(float)(baseX + 2), (h1)(float)(baseX + 3)};
-            const h2 Yv = {(h1)(float)(baseY + 0), (h1)(float)(baseY + 1)};
-            bool alive = true;
-            uint4 curA = make_uint4(0, 0, 0, 0);
-            uint32_t curB = 0;
-            if (lane < count) {
-                uint32_t g = sortedVals[start + lane];
-                curA = *(const uint4*)(recA + g);
-                curB = recB[g];
-            }
-            for (uint32_t base = 0; base < count; base += 64) {
-                uint4 nxtA = make_uint4(0, 0, 0, 0);
-                uint32_t nxtB = 0;
-                if (base + 64 + lane < count) {
-                    uint32_t g = sortedVals[start + base + 64 + lane];
-                    nxtA = *(const uint4*)(recA + g);
-                    nxtB = recB[g];
-                }
-                const uint32_t nb = min(64u, count - base);
-                bool done = false;
-                for (uint32_t j = 0; j < nb; ++j) {
-                    // early exit when the thread's 8 pixels are saturated (GlobalShaders.metal:1086-1088)
-                    if (alive) {
-                        h2 m = __builtin_elementwise_max(__builtin_elementwise_max(T0a, T0b),
-                                                         __builtin_elementwise_max(T1a, T1b));
-                        h1 mm = __builtin_elementwise_max(m.x, m.y);
-                        if (mm < thr) alive = false;
-                    }
-                    if (__ballot(alive) == 0) {
-                        done = true;
-                        break;
-                    }
-                    const uint32_t r0 = __builtin_amdgcn_readlane(curA.x, j);
-                    const uint32_t r1 = __builtin_amdgcn_readlane(curA.y, j);
-                    const uint32_t r2 = __builtin_amdgcn_readlane(curA.z, j);
-                    const uint32_t r3 = __builtin_amdgcn_readlane(curA.w, j);
-                    const uint32_t r4 = __builtin_amdgcn_readlane(curB, j);
-                    bool nz = false;
-                    h2 a0a, a0b, a1a, a1b;
-                    if (alive) {
-                        const h2 mean = as_h2(r0), cc = as_h2(r1), oc = as_h2(r2);
-                        const h2 MX = splat_lo(mean), MY = splat_hi(mean);
-                        const h2 CXX = splat_lo(cc), CYY = splat_hi(cc);
-                        const h2 CXY = splat_lo(oc), OP = splat_hi(oc);
-                        const h2 dxa = Xa - MX, dxb = Xb - MX, dy = Yv - MY;
-                        const h2 sxa = (dxa * dxa) * CXX, sxb = (dxb * dxb) * CXX;
-                        const h2 sy = (dy * dy) * CYY;
-                        const h2 dy0 = splat_lo(dy), dy1 = splat_hi(dy);
-                        const h2 sy0 = splat_lo(sy), sy1 = splat_hi(sy);
-                        // p = ((dx*dx)*cxx + (dy*dy)*cyy) + (dx*dy)*cxy2  (GlobalShaders.metal:1115-1122)
-                        const h2 p0a = (sxa + sy0) + (dxa * dy0) * CXY;
-                        const h2 p0b = (sxb + sy0) + (dxb * dy0) * CXY;
-                        const h2 p1a = (sxa + sy1) + (dxa * dy1) * CXY;
-                        const h2 p1b = (sxb + sy1) + (dxb * dy1) * CXY;
-                        // a = min(opacity * exp(-0.5h * p), 0.99h)  (GlobalShaders.metal:1124-1131)
-                        a0a = __builtin_elementwise_min(OP * lookup2(tbl, p0a), C099);
-                        a0b = __builtin_elementwise_min(OP * lookup2(tbl, p0b), C099);
-                        a1a = __builtin_elementwise_min(OP * lookup2(tbl, p1a), C099);
-                        a1b = __builtin_elementwise_min(OP * lookup2(tbl, p1b), C099);
-                        nz = ((as_u32(a0a) | as_u32(a0b) | as_u32(a1a) | as_u32(a1b)) & 0x7FFF7FFFu) != 0;
-                    }
-                    // all-zero alphas change nothing (GlobalShaders.metal:1135); skip wave-wide
-                    if (__ballot(nz) == 0) continue;
-                    if (alive) {
-                        const h2 rg = as_h2(r3), bd = as_h2(r4);
-                        const h2 CR = splat_lo(rg), CG = splat_hi(rg);
-                        const h2 CB = splat_lo(bd), CD = splat_hi(bd);
-                        // (GlobalShaders.metal:1137-1149)
-                        h2 w;
-                        w = a0a * T0a; R0a = R0a + CR * w; G0a = G0a + CG * w; B0a = B0a + CB * w; D0a = D0a + CD * w; T0a = T0a * (ONE - a0a);
-                        w = a0b * T0b; R0b = R0b + CR * w; G0b = G0b + CG * w; B0b = B0b + CB * w; D0b = D0b + CD * w; T0b = T0b * (ONE - a0b);
-                        w = a1a * T1a; R1a = R1a + CR * w; G1a = G1a + CG * w; B1a = B1a + CB * w; D1a = D1a + CD * w; T1a = T1a * (ONE - a1a);
-                        w = a1b * T1b; R1b = R1b + CR * w; G1b = G1b + CG * w; B1b = B1b + CB * w; D1b = D1b + CD * w; T1b = T1b * (ONE - a1b);
-                    }
-                }
-                if (done) break;
-                curA = nxtA;
-                curB = nxtB;
-            }
-        }
-
-        // write (GlobalShaders.metal:1152-1186); inactive tiles get the clear colour (0,0,0,1)
-        h2 A0a, A0b, A1a, A1b;
-        if (count > 0) {
-            A0a = ONE - T0a; A0b = ONE - T0b; A1a = ONE - T1a; A1b = ONE - T1b;
-        } else {
-            A0a = ONE; A0b = ONE; A1a = ONE; A1b = ONE;
-        }
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            const uint32_t y = baseY + j;
-            if (y >= H) continue;
-            const h2 Ra = j ? R1a : R0a, Rb = j ? R1b : R0b;
-            const h2 Ga = j ? G1a : G0a, Gb = j ? G1b : G0b;
-            const h2 Ba = j ? B1a : B0a, Bb = j ? B1b : B0b;
-            const h2 Aa = j ? A1a : A0a, Ab = j ? A1b : A0b;
-            const h2 Da = j ? D1a : D0a, Db = j ? D1b : D0b;
-            uint32_t px[4][2];
-            const h2 Rv[2] = {Ra, Rb}, Gv[2] = {Ga, Gb}, Bv[2] = {Ba, Bb}, Av[2] = {Aa, Ab};
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const int hh = i >> 1, e = i & 1;
-                h1 r = e ? Rv[hh].y : Rv[hh].x, g = e ? Gv[hh].y : Gv[hh].x;
-                h1 b = e ? Bv[hh].y : Bv[hh].x, a = e ? Av[hh].y : Av[hh].x;
-                px[i][0] = (uint32_t)__builtin_bit_cast(uint16_t, r) | ((uint32_t)__builtin_bit_cast(uint16_t, g) << 16);
-                px[i][1] = (uint32_t)__builtin_bit_cast(uint16_t, b) | ((uint32_t)__builtin_bit_cast(uint16_t, a) << 16);
-            }
-            uint8_t* crow = color + (size_t)y * colorPitch;
-            uint8_t* drow = depth ? depth + (size_t)y * depthPitch : nullptr;
-            if (vecStores && baseX + 3 < W) {
-                uint4* cp = (uint4*)(crow + (size_t)baseX * 8);
-                cp[0] = make_uint4(px[0][0], px[0][1], px[1][0], px[1][1]);
-                cp[1] = make_uint4(px[2][0], px[2][1], px[3][0], px[3][1]);
-                if (drow) *(uint2*)(drow + (size_t)baseX * 2) = make_uint2(as_u32(Da), as_u32(Db));
-            } else {
-                const uint32_t dv[2] = {as_u32(Da), as_u32(Db)};
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const uint32_t x = baseX + i;
-                    if (x >= W) continue;
-                    uint32_t* cp = (uint32_t*)(crow + (size_t)x * 8);
-                    cp[0] = px[i][0];
-                    cp[1] = px[i][1];
-                    if (drow) {
-                        uint16_t dh = (uint16_t)((dv[i >> 1] >> ((i & 1) * 16)) & 0xFFFFu);
-                        *(uint16_t*)(drow + (size_t)x * 2) = dh;
-                    }
-                }
-            }
-        }
-    }
-}
-
-// ---------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------
 template <bool HALF>
@@ -950,25 +755,6 @@ void launch_headers(const uint32_t* sortedKeys, const FrameGeometry& g, const De
     const uint32_t blocks = (t1 - t0 + 255) / 256;
     hipLaunchKernelGGL(k_headers, dim3(blocks), dim3(256), 0, s, sortedKeys, A.header, t0, t1,
                        A.headers);
-}
-
-void launch_blend(const uint32_t* sortedVals, const FrameGeometry& g, const DeviceArena& A, void* color,
-                  size_t colorPitch, void* depth, size_t depthPitch, int numCUs, hipStream_t s) {
-    const uint32_t t0 = g.rowBegin * g.tilesX, t1 = g.rowEnd * g.tilesX;
-    if (t1 <= t0) return;
-    const int vec = ((((uintptr_t)color) & 15u) == 0 && (colorPitch & 15u) == 0 &&
-                     (depth == nullptr || ((((uintptr_t)depth) & 7u) == 0 && (depthPitch & 7u) == 0)))
-                        ? 1
-                        : 0;
-    hipMemsetAsync(A.tileQueue, 0, sizeof(uint32_t), s);
-    uint32_t numTiles = t1 - t0;
-    uint32_t grid = (uint32_t)numCUs;
-    uint32_t maxUseful = (numTiles + (kBlendThreads / 64) - 1) / (kBlendThreads / 64);
-    if (grid > maxUseful) grid = maxUseful;
-    if (grid == 0) grid = 1;
-    hipLaunchKernelGGL(k_blend, dim3(grid), dim3(kBlendThreads), 0, s, A.headers, sortedVals, A.recA,
-                       A.recB, A.expTable, A.tileQueue, t0, numTiles, g.tilesX, g.width, g.height,
-                       (uint8_t*)color, colorPitch, (uint8_t*)depth, depthPitch, vec);
 }
 
 }  // namespace gsm

@@ -31,6 +31,11 @@ void GlobalRenderer::release() {
     for (auto& e : events_)
         if (e) hipEventDestroy(e);
     events_.clear();
+    if (evFrame_) hipEventDestroy(evFrame_);
+    if (evOrder_) hipEventDestroy(evOrder_);
+    if (side_) hipStreamDestroy(side_);
+    evFrame_ = evOrder_ = nullptr;
+    side_ = nullptr;
 }
 
 gsm_status GlobalRenderer::alloc(void** p, size_t bytes) {
@@ -113,6 +118,8 @@ gsm_status GlobalRenderer::create(const gsm_renderer_config& cfg, int hipDevice,
     GSM_ALLOC(A.radixBinTotals, 256 * sizeof(uint32_t));
     GSM_ALLOC(A.headers, (size_t)r->tileCount_ * sizeof(GaussianHeader));
     GSM_ALLOC(A.tileQueue, sizeof(uint32_t));
+    GSM_ALLOC(A.unitCost, (size_t)r->tileCount_ * 4 * sizeof(uint16_t));
+    GSM_ALLOC(A.unitOrder, (size_t)r->tileCount_ * 4 * sizeof(uint32_t));
     GSM_ALLOC(A.expTable, 65536 * sizeof(uint16_t));
     GSM_ALLOC(A.sincosTable, 65536 * sizeof(float2));
 #undef GSM_ALLOC
@@ -128,7 +135,8 @@ gsm_status GlobalRenderer::create(const gsm_renderer_config& cfg, int hipDevice,
     if (hipMemcpy(A.expTable, expt.data(), 65536 * sizeof(uint16_t), hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(A.sincosTable, sc.data(), 65536 * sizeof(float2), hipMemcpyHostToDevice) != hipSuccess ||
         hipMemset(A.header, 0, sizeof(TileAssignmentHeader)) != hipSuccess ||
-        hipMemset(A.headers, 0, (size_t)r->tileCount_ * sizeof(GaussianHeader)) != hipSuccess) {
+        hipMemset(A.headers, 0, (size_t)r->tileCount_ * sizeof(GaussianHeader)) != hipSuccess ||
+        hipMemset(A.unitCost, 0, (size_t)r->tileCount_ * 4 * sizeof(uint16_t)) != hipSuccess) {
         delete r;
         return GSM_ERR_FAILED_TO_ALLOCATE_BUFFER;
     }
@@ -203,6 +211,32 @@ gsm_status GlobalRenderer::render(hipStream_t s, const gsm_gaussian_input& in,
     lastWidth_ = width;
     lastHeight_ = height;
 
+    // Blend schedule: the units ordered by the walk lengths the previous frame of the same
+    // geometry measured (the image does not depend on the order, only the load balance does).
+    // The ordering kernel only needs those costs, so it runs on a side stream beside this
+    // frame's projection and sort.
+    const uint32_t upt = blend_units_per_tile();
+    const uint32_t units = (rowEnd_ - rowBegin_) * tilesX_ * upt;
+    const uint64_t key = ((uint64_t)upt << 60) ^ ((uint64_t)width << 40) ^ ((uint64_t)height << 20) ^
+                         ((uint64_t)rowBegin_ << 10) ^ rowEnd_;
+    if (key != schedKey_) {
+        hipMemsetAsync(arena_.unitCost, 0, (size_t)units * sizeof(uint16_t), s);
+        schedKey_ = key;
+    }
+    bool costOrder = units > 0 && blend_schedule_enabled((rowEnd_ - rowBegin_) * tilesX_, numCUs_);
+    if (costOrder && !side_) {
+        if (hipStreamCreateWithFlags(&side_, hipStreamNonBlocking) != hipSuccess ||
+            hipEventCreateWithFlags(&evFrame_, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&evOrder_, hipEventDisableTiming) != hipSuccess)
+            return GSM_ERR_ENCODER_CREATION_FAILED;
+    }
+    if (costOrder) {
+        hipEventRecord(evFrame_, s);  // after the previous frame's blend wrote the costs
+        hipStreamWaitEvent(side_, evFrame_, 0);
+        launch_unit_order(units, arena_, side_);
+        hipEventRecord(evOrder_, side_);
+    }
+
     hipEvent_t* ev = prof ? frameEvents(profFrames_) : nullptr;
     if (prof) hipEventRecord(ev[0], s);
     launch_project(config_.precision == GSM_PRECISION_FLOAT16, deg, in.gaussians, in.harmonics, a,
@@ -235,8 +269,10 @@ gsm_status GlobalRenderer::render(hipStream_t s, const gsm_gaussian_input& in,
     g.height = height;
     g.maxAssignments = maxAssignments_;
     launch_headers(sortedKeys_, g, arena_, s);
+    arena_.blendTrace = (profiling_ & 4) ? traceBuf_ : nullptr;
     if (prof) hipEventRecord(ev[5], s);
-    launch_blend(sortedVals_, g, arena_, color, colorPitch, depth, depthPitch, numCUs_, s);
+    if (costOrder) hipStreamWaitEvent(s, evOrder_, 0);
+    launch_blend(sortedVals_, g, arena_, color, colorPitch, depth, depthPitch, numCUs_, costOrder, s);
     if (prof) hipEventRecord(ev[6], s);
     if (prof) profFrames_++;
     haveTimes_ = profFrames_ > 0;
@@ -311,6 +347,7 @@ gsm_status GlobalRenderer::debugCopy(int which, void* dst, size_t bytes, size_t*
         case GSM_BUF_SORTED_VALUES: src = sortedVals_; full = tot * 4; break;
         case GSM_BUF_HEADERS: src = arena_.headers; full = (size_t)tileCount_ * 8; break;
         case GSM_BUF_EXP_TABLE: src = arena_.expTable; full = 65536 * 2; break;
+        case GSM_BUF_BLEND_TRACE: src = (profiling_ & 4) ? traceBuf_ : nullptr; full = (size_t)tileCount_ * 4 * 4 * 8; break;
         default: return GSM_ERR_INVALID_ARGUMENT;
     }
     if (needed) *needed = full;
@@ -355,6 +392,10 @@ gsm_status GlobalRenderer::setProfiling(int flags) {
     if ((flags & 2) && !arena_.keysKeep) {
         gsm_status st = alloc((void**)&arena_.keysKeep, (size_t)maxAssignments_ * 4);
         if (st == GSM_OK) st = alloc((void**)&arena_.valsKeep, (size_t)maxAssignments_ * 4);
+        if (st != GSM_OK) return st;
+    }
+    if ((flags & 4) && !traceBuf_) {
+        gsm_status st = alloc((void**)&traceBuf_, (size_t)tileCount_ * 4 * 4 * 8);
         if (st != GSM_OK) return st;
     }
     if ((flags & 1) && events_.empty()) {

@@ -77,6 +77,7 @@ class BufferId(enum.IntEnum):  # include/gsm_debug.h gsm_buffer_id
     SORTED_VALUES = 6
     HEADERS = 7
     EXP_TABLE = 8
+    BLEND_TRACE = 9
 
 
 STAGES = ("project", "scan", "scatter", "sort", "headers", "blend")
@@ -300,8 +301,9 @@ class GlobalRenderer:
         return float(s.value) if st == 0 else None
 
     # -- introspection (include/gsm_debug.h) --
-    def set_profiling(self, stage_events: bool = True, keep_unsorted: bool = False):
-        flags = (1 if stage_events else 0) | (2 if keep_unsorted else 0)
+    def set_profiling(self, stage_events: bool = True, keep_unsorted: bool = False,
+                      blend_trace: bool = False):
+        flags = (1 if stage_events else 0) | (2 if keep_unsorted else 0) | (4 if blend_trace else 0)
         _check(_lib().gsm_global_set_profiling(self._h, flags), "gsm_global_set_profiling")
 
     def stage_times_ms(self) -> dict:
@@ -336,6 +338,8 @@ class GlobalRenderer:
             return raw.view(np.int32)
         if which == BufferId.HEADERS:
             return raw.view(np.uint32).reshape(-1, 2)
+        if which == BufferId.BLEND_TRACE:
+            return raw.view(np.uint64).reshape(-1, 4)
         if which == BufferId.EXP_TABLE:
             return raw.view(np.uint16)
         return raw

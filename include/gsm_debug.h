@@ -37,15 +37,18 @@ typedef enum {
     GSM_BUF_SORTED_KEYS = 5,   /* uint32[total] [sortKeys after sort] */
     GSM_BUF_SORTED_VALUES = 6, /* int32[total] [sortedIndices] */
     GSM_BUF_HEADERS = 7,       /* GaussianHeader[tile_count] {offset,count} [orderedHeaders] */
-    GSM_BUF_EXP_TABLE = 8      /* uint16[65536] blend exp table indexed by fp16 quad-form bits */
+    GSM_BUF_EXP_TABLE = 8,     /* uint16[65536] blend exp table indexed by fp16 quad-form bits */
+    GSM_BUF_BLEND_TRACE = 9    /* uint64[blend units][4] {start, end (100 MHz ticks), count<<32 | entries
+                                  walked, XCC_ID<<32 | HW_ID} of the last profiled frame (bit 2) */
 } gsm_buffer_id;
 
 gsm_status gsm_global_debug_counters(gsm_renderer *renderer, gsm_debug_counters *out);
 /* Copies up to `bytes` of buffer `which` into host memory; *needed receives the full size. */
 gsm_status gsm_global_debug_copy(gsm_renderer *renderer, int which, void *host_dst, size_t bytes,
                                  size_t *needed);
-/* When enabled, every stage is bracketed by HIP events on the frame's stream and
- * keeps the unsorted keys (GSM_BUF_KEYS/VALUES) for readback. */
+/* `enable` is a bit set: bit 0 brackets every stage by HIP events on the frame's stream,
+ * bit 1 keeps the unsorted keys (GSM_BUF_KEYS/VALUES) for readback, bit 2 records a
+ * per-unit blend trace (GSM_BUF_BLEND_TRACE).  Bits 1-2 cost time and memory. */
 gsm_status gsm_global_set_profiling(gsm_renderer *renderer, int enable);
 
 enum {

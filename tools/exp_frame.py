@@ -42,12 +42,13 @@ def main():
         k, vals = v.split("=")
         variants = [(f"{name} {k}={x}".strip(), {**env, k: x}) for name, env in variants
                     for x in vals.split(",")]
+    varied = {k for _, env in variants for k in env}
     results = {name: [] for name, _ in variants}
     ref = None
     for rnd in range(args.rounds):
         for name, env in variants:
             for k in list(os.environ):
-                if k.startswith("GSM_") and k.endswith("_DYN"):
+                if k in varied:
                     del os.environ[k]
             os.environ.update(env)
             for _ in range(3):

@@ -53,7 +53,7 @@ __device__ __forceinline__ uint32_t quad_max_u32(uint32_t v) {
 // ---------------------------------------------------------------------------
 template <int NT, int P>
 __global__ __launch_bounds__(NT) void k_blend_px(
-    const GaussianHeader* __restrict__ headers, const uint32_t* __restrict__ sortedVals,
+    const uint32_t* __restrict__ tileStart, const uint32_t* __restrict__ sortedVals,
     const BlendRecordA* __restrict__ recA, const uint32_t* __restrict__ recB,
     const uint16_t* __restrict__ expTable, uint32_t* __restrict__ queue, uint32_t tileBegin,
     uint32_t numTiles, uint32_t tilesX, uint32_t W, uint32_t H, uint8_t* __restrict__ color,
@@ -111,9 +111,8 @@ __global__ __launch_bounds__(NT) void k_blend_px(
         const uint32_t tileX = tile % tilesX, tileY = tile / tilesX;
         const uint32_t ux = tileX * kTileWidth + (P == 4 ? 0u : (part & 1u) * 16u);
         const uint32_t uy = tileY * kTileHeight + (P == 1 ? (part >> 1) * 8u : 0u);
-        const GaussianHeader hdr = headers[tile];
-        const uint32_t start = __builtin_amdgcn_readfirstlane(hdr.offset);
-        const uint32_t count = __builtin_amdgcn_readfirstlane(hdr.count);
+        const uint32_t start = __builtin_amdgcn_readfirstlane(tileStart[tile]);
+        const uint32_t count = __builtin_amdgcn_readfirstlane(tileStart[tile + 1]) - start;
         unsigned long long tStart = 0;
         if (trace) tStart = __builtin_amdgcn_s_memrealtime();
         uint32_t nproc = 0;
@@ -433,7 +432,7 @@ void launch_blend(const uint32_t* sortedVals, const FrameGeometry& g, const Devi
     uint32_t grid = (units + (uint32_t)waves - 1) / (uint32_t)waves;
     if (grid > (uint32_t)numCUs) grid = (uint32_t)numCUs;
 #define GSM_LAUNCH_PX(NTH, PP)                                                                      \
-    hipLaunchKernelGGL((k_blend_px<NTH, PP>), dim3(grid), dim3(NTH), 0, s, A.headers, sortedVals,   \
+    hipLaunchKernelGGL((k_blend_px<NTH, PP>), dim3(grid), dim3(NTH), 0, s, A.tileStart, sortedVals, \
                        A.recA, A.recB, A.expTable, A.tileQueue, t0, numTiles, g.tilesX, g.width,    \
                        g.height, (uint8_t*)color, colorPitch, (uint8_t*)depth, depthPitch, flags,    \
                        costOrder ? A.unitOrder : nullptr, A.unitCost, A.blendTrace)

@@ -33,7 +33,7 @@ struct DeviceArena {
     unsigned long long* blendTrace = nullptr;  // [4 * tiles * 4] (profiling bit 2 only)
     uint32_t* radixHist = nullptr;             // [256 * radixGrid]
     uint32_t* radixBinTotals = nullptr;        // [256]
-    GaussianHeader* headers = nullptr;         // [tileCount]
+    uint32_t* tileStart = nullptr;             // [tileCount + 1] first sorted entry of each tile
     uint32_t* tileQueue = nullptr;             // [1] blend work counter
     uint16_t* unitCost = nullptr;              // [4 * tileCount] list entries each blend unit walked
     uint32_t* unitOrder = nullptr;             // [4 * tileCount] blend units, longest last-frame walk first
@@ -43,7 +43,7 @@ struct DeviceArena {
 
 constexpr int kProjectBlock = 256;
 constexpr int kRadixBlock = 256;
-constexpr int kRadixItems = 8;  // keys per thread per chunk
+constexpr int kRadixItems = 16;  // keys per thread per chunk (4096-key chunks)
 constexpr int kRadixChunk = kRadixBlock * kRadixItems;
 
 // project + cull + SH + tile count + per-block count sums (GlobalShaders.metal:19-123, 563-616)

@@ -677,84 +677,53 @@ __global__ __launch_bounds__(kProjectBlock) void k_scatter(
 
 // ---------------------------------------------------------------------------
 // 4. headers (buildHeadersFromSortedKernel, GlobalShaders.metal:304-356)
+//
+// The reference binary-searches every tile (offset = lower_bound, count = upper - lower).
+// Here one pass over the sorted keys finds the run boundaries instead: at position i with
+// tile(i-1) < tile(i), every tile t in (tile(i-1), tile(i)] starts at i, which also gives
+// empty tiles their lower_bound.  tileStart[t+1] - tileStart[t] is the count; the
+// {offset, count} layout of the reference is produced on readback.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_headers(const uint32_t* __restrict__ sortedKeys,
-                                                 const TileAssignmentHeader* __restrict__ hdr,
-                                                 uint32_t tileBegin, uint32_t tileEnd,
-                                                 GaussianHeader* __restrict__ headers) {
-    const uint32_t tile = tileBegin + blockIdx.x * 256 + threadIdx.x;
-    if (tile >= tileEnd) return;
+__global__ __launch_bounds__(256) void k_tile_starts(const uint32_t* __restrict__ sortedKeys,
+                                                     const TileAssignmentHeader* __restrict__ hdr,
+                                                     uint32_t tileBegin, uint32_t tileEnd,
+                                                     uint32_t* __restrict__ tileStart) {
     const uint32_t total = hdr->totalAssignments;
-    GaussianHeader h;
-    if (total == 0) {
-        h.offset = 0;
-        h.count = 0;
-    } else {
-        uint32_t l = 0, r = total;
-        while (l < r) {
-            uint32_t mid = (l + r) >> 1;
-            if ((sortedKeys[mid] >> 16) < tile) l = mid + 1;
-            else r = mid;
+    const uint32_t stride = gridDim.x * 256u * 4u;
+    // 4 consecutive positions per thread and step (one 16-byte load plus the key before them)
+    for (uint32_t i0 = (blockIdx.x * 256u + threadIdx.x) * 4u; i0 <= total; i0 += stride) {
+        uint32_t k[5];
+        k[0] = i0 == 0 ? 0u : sortedKeys[i0 - 1];
+        if (i0 + 4u <= total) {
+            const uint4 q = *(const uint4*)(sortedKeys + i0);
+            k[1] = q.x;
+            k[2] = q.y;
+            k[3] = q.z;
+            k[4] = q.w;
+        } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) k[j + 1] = i0 + j < total ? sortedKeys[i0 + j] : 0u;
         }
-        uint32_t s = l;
-        r = total;
-        while (l < r) {
-            uint32_t mid = (l + r) >> 1;
-            if ((sortedKeys[mid] >> 16) <= tile) l = mid + 1;
-            else r = mid;
+#pragma unroll
+        for (uint32_t j = 0; j < 4; ++j) {
+            const uint32_t i = i0 + j;
+            if (i > total) break;
+            // keys hold slab tiles only (tile count and scatter are limited to [tileBegin, tileEnd))
+            const uint32_t prev = i == 0 ? tileBegin - 1u : (k[j] >> 16);
+            const uint32_t cur = i == total ? tileEnd : min(k[j + 1] >> 16, tileEnd);
+            for (uint32_t t = prev + 1u; t <= cur; ++t) tileStart[t] = i;
         }
-        h.offset = s;
-        h.count = l > s ? l - s : 0u;
     }
-    headers[tile] = h;
-}
-
-// ---------------------------------------------------------------------------
-// launchers
-// ---------------------------------------------------------------------------
-template <bool HALF>
-static void launch_project_t(uint32_t deg, const void* world, const void* harm, const ProjectArgs& a,
-                             const DeviceArena& A, hipStream_t s) {
-    const uint32_t blocks = (a.count + kProjectBlock - 1) / kProjectBlock;
-    if (blocks == 0) return;
-#define GSM_LAUNCH_PROJ(D)                                                                     \
-    hipLaunchKernelGGL((k_project<HALF, D>), dim3(blocks), dim3(kProjectBlock), 0, s, world,   \
-                       harm, a, A.renderData, A.bounds, A.recA, A.recB, A.tileCounts,          \
-                       A.blockSums, A.sincosTable)
-    switch (deg) {
-        case 0: GSM_LAUNCH_PROJ(0); break;
-        case 1: GSM_LAUNCH_PROJ(1); break;
-        case 2: GSM_LAUNCH_PROJ(2); break;
-        default: GSM_LAUNCH_PROJ(3); break;
-    }
-#undef GSM_LAUNCH_PROJ
-}
-
-void launch_project(bool halfInput, uint32_t deg, const void* world, const void* harm,
-                    const ProjectArgs& a, const DeviceArena& A, hipStream_t s) {
-    if (halfInput) launch_project_t<true>(deg, world, harm, a, A, s);
-    else launch_project_t<false>(deg, world, harm, a, A, s);
-}
-
-void launch_scan_blocks(uint32_t nb, const ProjectArgs& a, const DeviceArena& A, hipStream_t s) {
-    hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(kScanThreads), 0, s, A.blockSums, nb,
-                       a.maxAssignments, A.header);
-}
-
-void launch_scatter(const ProjectArgs& a, const DeviceArena& A, hipStream_t s) {
-    const uint32_t blocks = (a.count + kProjectBlock - 1) / kProjectBlock;
-    if (blocks == 0) return;
-    hipLaunchKernelGGL(k_scatter, dim3(blocks), dim3(kProjectBlock), 0, s, a, A.renderData, A.bounds,
-                       A.tileCounts, A.blockSums, A.keys[0], A.vals[0], A.sincosTable);
 }
 
 void launch_headers(const uint32_t* sortedKeys, const FrameGeometry& g, const DeviceArena& A,
                     hipStream_t s) {
     const uint32_t t0 = g.rowBegin * g.tilesX, t1 = g.rowEnd * g.tilesX;
     if (t1 <= t0) return;
-    const uint32_t blocks = (t1 - t0 + 255) / 256;
-    hipLaunchKernelGGL(k_headers, dim3(blocks), dim3(256), 0, s, sortedKeys, A.header, t0, t1,
-                       A.headers);
+    uint32_t blocks = (g.maxAssignments + 1u + 1023u) / 1024u;  // grid-stride over the device-side total
+    if (blocks > 4096u) blocks = 4096u;
+    hipLaunchKernelGGL(k_tile_starts, dim3(blocks), dim3(256), 0, s, sortedKeys, A.header, t0, t1,
+                       A.tileStart);
 }
 
 }  // namespace gsm

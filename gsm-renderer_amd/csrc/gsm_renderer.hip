@@ -116,7 +116,7 @@ gsm_status GlobalRenderer::create(const gsm_renderer_config& cfg, int hipDevice,
     GSM_ALLOC(A.vals[1], cap * sizeof(uint32_t));
     GSM_ALLOC(A.radixHist, (size_t)256 * rgrid * sizeof(uint32_t));
     GSM_ALLOC(A.radixBinTotals, 256 * sizeof(uint32_t));
-    GSM_ALLOC(A.headers, (size_t)r->tileCount_ * sizeof(GaussianHeader));
+    GSM_ALLOC(A.tileStart, ((size_t)r->tileCount_ + 1) * sizeof(uint32_t));
     GSM_ALLOC(A.tileQueue, sizeof(uint32_t));
     GSM_ALLOC(A.unitCost, (size_t)r->tileCount_ * 4 * sizeof(uint16_t));
     GSM_ALLOC(A.unitOrder, (size_t)r->tileCount_ * 4 * sizeof(uint32_t));
@@ -135,7 +135,7 @@ gsm_status GlobalRenderer::create(const gsm_renderer_config& cfg, int hipDevice,
     if (hipMemcpy(A.expTable, expt.data(), 65536 * sizeof(uint16_t), hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(A.sincosTable, sc.data(), 65536 * sizeof(float2), hipMemcpyHostToDevice) != hipSuccess ||
         hipMemset(A.header, 0, sizeof(TileAssignmentHeader)) != hipSuccess ||
-        hipMemset(A.headers, 0, (size_t)r->tileCount_ * sizeof(GaussianHeader)) != hipSuccess ||
+        hipMemset(A.tileStart, 0, ((size_t)r->tileCount_ + 1) * sizeof(uint32_t)) != hipSuccess ||
         hipMemset(A.unitCost, 0, (size_t)r->tileCount_ * 4 * sizeof(uint16_t)) != hipSuccess) {
         delete r;
         return GSM_ERR_FAILED_TO_ALLOCATE_BUFFER;
@@ -345,7 +345,7 @@ gsm_status GlobalRenderer::debugCopy(int which, void* dst, size_t bytes, size_t*
         case GSM_BUF_VALUES: src = unsortedVals_; full = tot * 4; break;
         case GSM_BUF_SORTED_KEYS: src = sortedKeys_; full = tot * 4; break;
         case GSM_BUF_SORTED_VALUES: src = sortedVals_; full = tot * 4; break;
-        case GSM_BUF_HEADERS: src = arena_.headers; full = (size_t)tileCount_ * 8; break;
+        case GSM_BUF_HEADERS: full = (size_t)tileCount_ * 8; break;
         case GSM_BUF_EXP_TABLE: src = arena_.expTable; full = 65536 * 2; break;
         case GSM_BUF_BLEND_TRACE: src = (profiling_ & 4) ? traceBuf_ : nullptr; full = (size_t)tileCount_ * 4 * 4 * 8; break;
         default: return GSM_ERR_INVALID_ARGUMENT;
@@ -365,6 +365,18 @@ gsm_status GlobalRenderer::debugCopy(int which, void* dst, size_t bytes, size_t*
             b[4 * i + 3] = tmpBounds[i].w;
         }
         std::memcpy(dst, b.data(), cpy);
+        return GSM_OK;
+    }
+    if (which == GSM_BUF_HEADERS) {  // {offset = lower_bound, count} per tile, as the reference
+        std::vector<uint32_t> ts((size_t)tileCount_ + 1);
+        if (hipMemcpy(ts.data(), arena_.tileStart, ts.size() * 4, hipMemcpyDeviceToHost) != hipSuccess)
+            return GSM_ERR_RENDER_FAILED;
+        std::vector<uint32_t> h((size_t)tileCount_ * 2);
+        for (uint32_t t = 0; t < tileCount_; ++t) {
+            h[2 * t] = ts[t];
+            h[2 * t + 1] = ts[t + 1] >= ts[t] ? ts[t + 1] - ts[t] : 0u;
+        }
+        std::memcpy(dst, h.data(), cpy);
         return GSM_OK;
     }
     if (!src) return full == 0 ? GSM_OK : GSM_ERR_MISSING_REQUIRED_BUFFER;

@@ -46,18 +46,30 @@ __global__ __launch_bounds__(kRadixBlock) void k_radix_upsweep(const uint32_t* _
                                                                uint32_t shift,
                                                                uint32_t* __restrict__ hist) {
     __shared__ uint32_t cnt[kWaves][256];
-    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint32_t wave = threadIdx.x >> 6;
     for (int i = threadIdx.x; i < kWaves * 256; i += kRadixBlock) (&cnt[0][0])[i] = 0;
     __syncthreads();
     uint32_t begin, end;
     block_range(*nPtr, gridDim.x, blockIdx.x, &begin, &end);
-    const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-    for (uint32_t base = begin + wave * 64; base < end; base += kRadixBlock) {
-        const uint32_t idx = base + lane;
-        const bool valid = idx < end;
-        const uint32_t d = valid ? (keys[idx] >> shift) & 0xFFu : 0u;
-        const uint64_t peers = match_digit(d, valid);
-        if (valid && (peers & lt) == 0) cnt[wave][d] += (uint32_t)__popcll(peers);
+    // a chunk's keys are all loaded before any is counted (16 loads in flight per thread);
+    // order does not matter for a histogram, so they come as 16-byte vectors
+    for (uint32_t cbase = begin; cbase < end; cbase += kRadixChunk) {
+        uint4 q[kRadixItems / 4];
+#pragma unroll
+        for (int i = 0; i < kRadixItems / 4; ++i) {
+            const uint32_t idx = cbase + (uint32_t)(i * kRadixBlock + threadIdx.x) * 4u;
+            q[i] = idx + 3u < end ? *(const uint4*)(keys + idx)
+                                  : make_uint4(idx < end ? keys[idx] : 0u, idx + 1u < end ? keys[idx + 1u] : 0u,
+                                               idx + 2u < end ? keys[idx + 2u] : 0u, 0u);
+        }
+#pragma unroll
+        for (int i = 0; i < kRadixItems / 4; ++i) {
+            const uint32_t idx = cbase + (uint32_t)(i * kRadixBlock + threadIdx.x) * 4u;
+            const uint32_t kk[4] = {q[i].x, q[i].y, q[i].z, q[i].w};
+#pragma unroll
+            for (int c = 0; c < 4; ++c)  // per-wave LDS counters: one ds_add per key
+                if (idx + (uint32_t)c < end) atomicAdd(&cnt[wave][(kk[c] >> shift) & 0xFFu], 1u);
+        }
     }
     __syncthreads();
     for (int d = threadIdx.x; d < 256; d += kRadixBlock) {
@@ -69,21 +81,22 @@ __global__ __launch_bounds__(kRadixBlock) void k_radix_upsweep(const uint32_t* _
 }
 
 // One workgroup per digit: exclusive scan of hist[d][0..grid) in place, digit total out.
+// grid <= 1024, so every thread holds at most 4 entries in registers (one read, one write).
 __global__ __launch_bounds__(256) void k_radix_scan(uint32_t* __restrict__ hist, uint32_t grid,
                                                     uint32_t* __restrict__ binTotals) {
     __shared__ uint32_t part[4];
     const uint32_t d = blockIdx.x;
     uint32_t* row = hist + (size_t)d * grid;
-    const uint32_t per = (grid + 255) / 256;
-    const uint32_t b0 = threadIdx.x * per;
-    uint32_t local = 0;
-    for (uint32_t i = 0; i < per; ++i)
-        if (b0 + i < grid) local += row[b0 + i];
+    const uint32_t b0 = threadIdx.x * 4u;
+    uint32_t v[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[i] = b0 + i < grid ? row[b0 + i] : 0u;
+    const uint32_t local = v[0] + v[1] + v[2] + v[3];
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     uint32_t inc = local;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
-        uint32_t t = __shfl_up(inc, o, 64);
+        const uint32_t t = __shfl_up(inc, o, 64);
         if (lane >= (uint32_t)o) inc += t;
     }
     if (lane == 63) part[wave] = inc;
@@ -95,11 +108,11 @@ __global__ __launch_bounds__(256) void k_radix_scan(uint32_t* __restrict__ hist,
         tot += part[w];
     }
     uint32_t run = off + inc - local;
-    for (uint32_t i = 0; i < per; ++i)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
         if (b0 + i < grid) {
-            uint32_t v = row[b0 + i];
             row[b0 + i] = run;
-            run += v;
+            run += v[i];
         }
     if (threadIdx.x == 0) binTotals[d] = tot;
 }
@@ -146,7 +159,7 @@ __global__ __launch_bounds__(kRadixBlock) void k_radix_downsweep(
     const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     for (uint32_t cbase = begin; cbase < end; cbase += kRadixChunk) {
         uint32_t k[kRadixItems], v[kRadixItems], rank[kRadixItems];
-        // wave w owns elements [cbase + w*512, +512): item j at + j*64 + lane (index order)
+        // wave w owns elements [cbase + w*64*items, +64*items): item j at + j*64 + lane (index order)
 #pragma unroll
         for (int j = 0; j < kRadixItems; ++j) {
             const uint32_t idx = cbase + wave * (64 * kRadixItems) + j * 64 + lane;
@@ -218,6 +231,7 @@ __global__ __launch_bounds__(kRadixBlock) void k_radix_downsweep(
 }
 
 uint32_t radix_grid_for_capacity(uint32_t capacity) {
+    // <= 1024 blocks: k_radix_scan holds a digit's column in 4 registers per thread
     uint32_t g = (capacity + kRadixChunk - 1) / kRadixChunk;
     if (g > 1024) g = 1024;
     if (g < 1) g = 1;

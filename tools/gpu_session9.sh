@@ -1,0 +1,10 @@
+set -u
+cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out
+timeout -k 10 600 python -m pytest tests -m gpu -q -x > gpurun_out/pytest_gpu.log 2>&1; rc=$?; tail -3 gpurun_out/pytest_gpu.log; echo pytest rc=$rc
+[ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
+timeout -k 10 300 python tools/exp_frame.py > gpurun_out/exp9.log 2>&1; rc=$?; grep variant gpurun_out/exp9.log; echo exp rc=$rc
+[ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python tools/exp_frame.py --config cfg3_5m_sh3_4k_f16 --rounds 2 --frames 10 > gpurun_out/exp9_4k.log 2>&1; rc=$?; grep variant gpurun_out/exp9_4k.log; echo exp4k rc=$rc
+[ $rc -eq 0 ] || exit $rc
+cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/prof9 -o run -- python $GRAFT_REPO_ROOT/tools/exp_frame.py --rounds 1 --frames 20 > $GRAFT_REPO_ROOT/gpurun_out/prof9.log 2>&1; echo prof rc=$?

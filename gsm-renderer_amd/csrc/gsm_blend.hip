@@ -17,6 +17,7 @@ namespace gsm {
 
 typedef _Float16 h1;
 typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ h2 as_h2(uint32_t u) { return __builtin_bit_cast(h2, u); }
 __device__ __forceinline__ uint32_t as_u32(h2 v) { return __builtin_bit_cast(uint32_t, v); }
@@ -51,7 +52,7 @@ __device__ __forceinline__ uint32_t quad_max_u32(uint32_t v) {
 // groups of U = 4/P entries through a three-stage software pipeline (stage 1: next group's
 // p and table reads; stage 2: blend this group; stage 3: next group's alphas).
 // ---------------------------------------------------------------------------
-template <int NT, int P>
+template <int NT, int P, bool EXECM>
 __global__ __launch_bounds__(NT) void k_blend_px(
     const uint32_t* __restrict__ tileStart, const uint32_t* __restrict__ sortedVals,
     const BlendRecordA* __restrict__ recA, const uint32_t* __restrict__ recB,
@@ -76,6 +77,8 @@ __global__ __launch_bounds__(NT) void k_blend_px(
         for (int i = threadIdx.x; i < 65536 * 2 / 16; i += NT) dst[i] = src[i];
     }
     __syncthreads();
+    // the inline-asm table reads address the LDS from 0: the table is this kernel's only LDS
+    if ((uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint16_t*)tbl != 0u) __builtin_trap();
 
     const uint32_t lane = threadIdx.x & 63;
     // pixel pair k of this lane sits at (px[k], py[k]) and (px[k] + 1, py[k]) inside the unit
@@ -161,7 +164,7 @@ __global__ __launch_bounds__(NT) void k_blend_px(
 
             h2 ac[U][P], om[U][P];
             uint32_t rgc[U], bdc[U], rgn[U], bdn[U], opn[U];
-            uint32_t eln[U][P], ehn[U][P];
+            h2 en[U][P];  // next group's exp table values
             bool alive = true;
             // p = ((dx*dx)*cxx + (dy*dy)*cyy) + (dx*dy)*cxy2 (GlobalShaders.metal:1115-1122);
             // the dy terms are shared by the pairs of a row
@@ -212,9 +215,17 @@ __global__ __launch_bounds__(NT) void k_blend_px(
                             bdn[k] = __builtin_amdgcn_readlane(sb, j);
 #pragma unroll
                             for (int q = 0; q < P; ++q) {
+                                // both halves land in one register (ds_read_u16_d16 / _d16_hi);
+                                // the compiler does not count these reads: stage 3 waits for them
                                 const uint32_t pb = as_u32(pq[q]);
-                                eln[k][q] = tbl[pb & 0xFFFFu];
-                                ehn[k][q] = tbl[pb >> 16];
+                                uint32_t alo;  // (pb & 0xffff) * 2 in one SDWA op (the table sits at LDS 0)
+                                asm("v_lshlrev_b32_sdwa %0, 1, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0"
+                                    : "=v"(alo) : "v"(pb));
+                                const uint32_t ahi = (pb >> 16) << 1;
+                                uint32_t e;
+                                asm volatile("ds_read_u16_d16 %0, %1" : "=v"(e) : "v"(alo));
+                                asm volatile("ds_read_u16_d16_hi %0, %1" : "+v"(e) : "v"(ahi));
+                                en[k][q] = as_h2(e);
                             }
                         }
                     }
@@ -222,10 +233,12 @@ __global__ __launch_bounds__(NT) void k_blend_px(
 #pragma unroll
                     for (uint32_t k = 0; k < U; ++k) {
                         // group break (GlobalShaders.metal:1086-1088): max T of the 4x2 group
-                        h2 tm = T[0];
+                        // T >= 0, so the u16 bit patterns order like the values (v_pk_max_u16,
+                        // no canonicalising of the fp16 inputs)
+                        u16x2 tm = __builtin_bit_cast(u16x2, T[0]);
 #pragma unroll
-                        for (int q = 1; q < P; ++q) tm = __builtin_elementwise_max(tm, T[q]);
-                        const uint32_t tb = as_u32(tm);
+                        for (int q = 1; q < P; ++q) tm = __builtin_elementwise_max(tm, __builtin_bit_cast(u16x2, T[q]));
+                        const uint32_t tb = __builtin_bit_cast(uint32_t, tm);
                         uint32_t gm = max(tb & 0xFFFFu, tb >> 16);
                         if (P == 1) gm = quad_max_u32(gm);
                         if (P == 2) {
@@ -234,17 +247,31 @@ __global__ __launch_bounds__(NT) void k_blend_px(
                         }
                         alive = alive && !(gm < thrBits);  // T >= 0: fp16 order == bit order
                         const h2 rgv = as_h2(rgc[k]), bdv = as_h2(bdc[k]);
+                        // a dead lane keeps T and C (alpha 0 would give the same bits: C + c*0 == C,
+                        // T*1 == T): EXECM runs the updates under an EXEC mask of the live lanes,
+                        // otherwise w and T are selected per lane
+                        if (!EXECM) {
 #pragma unroll
-                        for (int q = 0; q < P; ++q) {
-                            // a dead lane keeps T and blends nothing (alpha 0 would give C + c*0 == C)
-                            const h2 Tn = T[q] * om[k][q];
-                            const h2 aT = ac[k][q] * T[q];  // (GlobalShaders.metal:1137-1149)
-                            const h2 w = alive ? aT : ZERO;
-                            T[q] = alive ? Tn : T[q];
-                            R[q] = R[q] + splat_lo(rgv) * w;
-                            G[q] = G[q] + splat_hi(rgv) * w;
-                            B[q] = B[q] + splat_lo(bdv) * w;
-                            D[q] = D[q] + splat_hi(bdv) * w;
+                            for (int q = 0; q < P; ++q) {
+                                const h2 Tn = T[q] * om[k][q];
+                                const h2 aT = ac[k][q] * T[q];  // (GlobalShaders.metal:1137-1149)
+                                const h2 w = alive ? aT : ZERO;
+                                T[q] = alive ? Tn : T[q];
+                                R[q] = R[q] + splat_lo(rgv) * w;
+                                G[q] = G[q] + splat_hi(rgv) * w;
+                                B[q] = B[q] + splat_lo(bdv) * w;
+                                D[q] = D[q] + splat_hi(bdv) * w;
+                            }
+                        } else if (alive) {
+#pragma unroll
+                            for (int q = 0; q < P; ++q) {
+                                const h2 w = ac[k][q] * T[q];  // (GlobalShaders.metal:1137-1149)
+                                T[q] = T[q] * om[k][q];
+                                R[q] = R[q] + splat_lo(rgv) * w;
+                                G[q] = G[q] + splat_hi(rgv) * w;
+                                B[q] = B[q] + splat_lo(bdv) * w;
+                                D[q] = D[q] + splat_hi(bdv) * w;
+                            }
                         }
                     }
                     const uint32_t g1 = b0 + (gi + 1) * U;
@@ -254,12 +281,16 @@ __global__ __launch_bounds__(NT) void k_blend_px(
                         goto unit_done;
                     }
                     // stage 3: the next group's alphas
+                    if (U * P == 4) {  // the table reads of stage 1 have landed (tied to their registers)
+                        uint32_t* e = (uint32_t*)&en[0][0];
+                        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(e[0]), "+v"(e[1 % (U * P)]), "+v"(e[2 % (U * P)]),
+                                     "+v"(e[3 % (U * P)]));
+                    }
 #pragma unroll
                     for (uint32_t k = 0; k < U; ++k) {
 #pragma unroll
                         for (int q = 0; q < P; ++q) {
-                            const h2 ek = as_h2(eln[k][q] | (ehn[k][q] << 16));
-                            ac[k][q] = __builtin_elementwise_min(splat_hi(as_h2(opn[k])) * ek, C099);
+                            ac[k][q] = __builtin_elementwise_min(splat_hi(as_h2(opn[k])) * en[k][q], C099);
                             om[k][q] = ONE - ac[k][q];
                         }
                         rgc[k] = rgn[k];
@@ -428,11 +459,16 @@ void launch_blend(const uint32_t* sortedVals, const FrameGeometry& g, const Devi
     hipMemsetAsync(A.tileQueue, 0, sizeof(uint32_t), s);
     const int P = blend_pairs_per_lane();
     const int waves = blend_waves_per_wg();
+    const char* ev = getenv("GSM_BLEND_EXECM");  // dead lanes: EXEC mask (default) or selects
+    const bool execm = !(ev && ev[0] == '0');
     const uint32_t units = numTiles * (4u / (uint32_t)P);
     uint32_t grid = (units + (uint32_t)waves - 1) / (uint32_t)waves;
     if (grid > (uint32_t)numCUs) grid = (uint32_t)numCUs;
 #define GSM_LAUNCH_PX(NTH, PP)                                                                      \
-    hipLaunchKernelGGL((k_blend_px<NTH, PP>), dim3(grid), dim3(NTH), 0, s, A.tileStart, sortedVals, \
+    if (execm) GSM_LAUNCH_PXE(NTH, PP, true);                                                         \
+    else GSM_LAUNCH_PXE(NTH, PP, false)
+#define GSM_LAUNCH_PXE(NTH, PP, EM)                                                                 \
+    hipLaunchKernelGGL((k_blend_px<NTH, PP, EM>), dim3(grid), dim3(NTH), 0, s, A.tileStart, sortedVals, \
                        A.recA, A.recB, A.expTable, A.tileQueue, t0, numTiles, g.tilesX, g.width,    \
                        g.height, (uint8_t*)color, colorPitch, (uint8_t*)depth, depthPitch, flags,    \
                        costOrder ? A.unitOrder : nullptr, A.unitCost, A.blendTrace)
@@ -447,6 +483,7 @@ void launch_blend(const uint32_t* sortedVals, const FrameGeometry& g, const Devi
     }
 #undef GSM_LAUNCH_P
 #undef GSM_LAUNCH_PX
+#undef GSM_LAUNCH_PXE
 }
 
 }  // namespace gsm

@@ -716,6 +716,45 @@ __global__ __launch_bounds__(256) void k_tile_starts(const uint32_t* __restrict_
     }
 }
 
+// ---------------------------------------------------------------------------
+// launchers
+// ---------------------------------------------------------------------------
+template <bool HALF>
+static void launch_project_t(uint32_t deg, const void* world, const void* harm, const ProjectArgs& a,
+                             const DeviceArena& A, hipStream_t s) {
+    const uint32_t blocks = (a.count + kProjectBlock - 1) / kProjectBlock;
+    if (blocks == 0) return;
+#define GSM_LAUNCH_PROJ(D)                                                                     \
+    hipLaunchKernelGGL((k_project<HALF, D>), dim3(blocks), dim3(kProjectBlock), 0, s, world,   \
+                       harm, a, A.renderData, A.bounds, A.recA, A.recB, A.tileCounts,          \
+                       A.blockSums, A.sincosTable)
+    switch (deg) {
+        case 0: GSM_LAUNCH_PROJ(0); break;
+        case 1: GSM_LAUNCH_PROJ(1); break;
+        case 2: GSM_LAUNCH_PROJ(2); break;
+        default: GSM_LAUNCH_PROJ(3); break;
+    }
+#undef GSM_LAUNCH_PROJ
+}
+
+void launch_project(bool halfInput, uint32_t deg, const void* world, const void* harm,
+                    const ProjectArgs& a, const DeviceArena& A, hipStream_t s) {
+    if (halfInput) launch_project_t<true>(deg, world, harm, a, A, s);
+    else launch_project_t<false>(deg, world, harm, a, A, s);
+}
+
+void launch_scan_blocks(uint32_t nb, const ProjectArgs& a, const DeviceArena& A, hipStream_t s) {
+    hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(kScanThreads), 0, s, A.blockSums, nb,
+                       a.maxAssignments, A.header);
+}
+
+void launch_scatter(const ProjectArgs& a, const DeviceArena& A, hipStream_t s) {
+    const uint32_t blocks = (a.count + kProjectBlock - 1) / kProjectBlock;
+    if (blocks == 0) return;
+    hipLaunchKernelGGL(k_scatter, dim3(blocks), dim3(kProjectBlock), 0, s, a, A.renderData, A.bounds,
+                       A.tileCounts, A.blockSums, A.keys[0], A.vals[0], A.sincosTable);
+}
+
 void launch_headers(const uint32_t* sortedKeys, const FrameGeometry& g, const DeviceArena& A,
                     hipStream_t s) {
     const uint32_t t0 = g.rowBegin * g.tilesX, t1 = g.rowEnd * g.tilesX;

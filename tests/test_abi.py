@@ -32,6 +32,14 @@ def test_library_exports_every_declared_symbol(gsm):
     assert set(declared_functions()) <= exported
 
 
+def test_library_has_no_unresolved_internal_symbols(gsm):
+    """Every gsm:: function the library calls is defined in it (a lazily bound ctypes load
+    would only fail at the first call, on the GPU box)."""
+    out = subprocess.run(["nm", "-DC", "--undefined-only", gsm.library_path()], capture_output=True,
+                         text=True, check=True).stdout
+    assert not [l for l in out.splitlines() if "gsm::" in l or " gsm_" in l], out
+
+
 def test_struct_sizes_match_headers(gsm, tmp_path):
     prog = tmp_path / "sizes.c"
     prog.write_text('#include "gsm_debug.h"\n#include <stdio.h>\n'

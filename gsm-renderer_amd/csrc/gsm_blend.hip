@@ -77,8 +77,6 @@ __global__ __launch_bounds__(NT) void k_blend_px(
         for (int i = threadIdx.x; i < 65536 * 2 / 16; i += NT) dst[i] = src[i];
     }
     __syncthreads();
-    // the inline-asm table reads address the LDS from 0: the table is this kernel's only LDS
-    if ((uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint16_t*)tbl != 0u) __builtin_trap();
 
     const uint32_t lane = threadIdx.x & 63;
     // pixel pair k of this lane sits at (px[k], py[k]) and (px[k] + 1, py[k]) inside the unit
@@ -164,7 +162,7 @@ __global__ __launch_bounds__(NT) void k_blend_px(
 
             h2 ac[U][P], om[U][P];
             uint32_t rgc[U], bdc[U], rgn[U], bdn[U], opn[U];
-            h2 en[U][P];  // next group's exp table values
+            uint32_t eln[U][P], ehn[U][P];  // next group's exp table words
             bool alive = true;
             // p = ((dx*dx)*cxx + (dy*dy)*cyy) + (dx*dy)*cxy2 (GlobalShaders.metal:1115-1122);
             // the dy terms are shared by the pairs of a row
@@ -215,17 +213,11 @@ __global__ __launch_bounds__(NT) void k_blend_px(
                             bdn[k] = __builtin_amdgcn_readlane(sb, j);
 #pragma unroll
                             for (int q = 0; q < P; ++q) {
-                                // both halves land in one register (ds_read_u16_d16 / _d16_hi);
-                                // the compiler does not count these reads: stage 3 waits for them
+                                // raw table words: first used in stage 3, after the current
+                                // group's blend, so the LDS latency hides behind it
                                 const uint32_t pb = as_u32(pq[q]);
-                                uint32_t alo;  // (pb & 0xffff) * 2 in one SDWA op (the table sits at LDS 0)
-                                asm("v_lshlrev_b32_sdwa %0, 1, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0"
-                                    : "=v"(alo) : "v"(pb));
-                                const uint32_t ahi = (pb >> 16) << 1;
-                                uint32_t e;
-                                asm volatile("ds_read_u16_d16 %0, %1" : "=v"(e) : "v"(alo));
-                                asm volatile("ds_read_u16_d16_hi %0, %1" : "+v"(e) : "v"(ahi));
-                                en[k][q] = as_h2(e);
+                                eln[k][q] = tbl[pb & 0xFFFFu];
+                                ehn[k][q] = tbl[pb >> 16];
                             }
                         }
                     }
@@ -281,16 +273,12 @@ __global__ __launch_bounds__(NT) void k_blend_px(
                         goto unit_done;
                     }
                     // stage 3: the next group's alphas
-                    if (U * P == 4) {  // the table reads of stage 1 have landed (tied to their registers)
-                        uint32_t* e = (uint32_t*)&en[0][0];
-                        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(e[0]), "+v"(e[1 % (U * P)]), "+v"(e[2 % (U * P)]),
-                                     "+v"(e[3 % (U * P)]));
-                    }
 #pragma unroll
                     for (uint32_t k = 0; k < U; ++k) {
 #pragma unroll
                         for (int q = 0; q < P; ++q) {
-                            ac[k][q] = __builtin_elementwise_min(splat_hi(as_h2(opn[k])) * en[k][q], C099);
+                            const h2 ek = as_h2(eln[k][q] | (ehn[k][q] << 16));
+                            ac[k][q] = __builtin_elementwise_min(splat_hi(as_h2(opn[k])) * ek, C099);
                             om[k][q] = ONE - ac[k][q];
                         }
                         rgc[k] = rgn[k];

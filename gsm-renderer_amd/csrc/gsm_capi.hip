@@ -6,6 +6,7 @@
 #include <new>
 
 #include "../../include/gsm_debug.h"
+#include "../../include/gsm_multigpu.h"
 #include "../../include/gsm_renderer.h"
 #include "gsm_internal.h"
 #include "gsm_renderer_impl.h"
@@ -93,6 +94,24 @@ gsm_status gsm_global_render(gsm_renderer* r, void* stream, const gsm_gaussian_i
     if (!r || !r->impl || !input || !camera) return GSM_ERR_INVALID_ARGUMENT;
     return r->impl->render((hipStream_t)stream, *input, *camera, width, height, color, color_pitch,
                            depth, depth_pitch);
+}
+
+gsm_status gsm_global_project_partition(gsm_renderer* r, void* stream, const gsm_gaussian_input* input,
+                                        const gsm_camera_params* camera, uint32_t width, uint32_t height,
+                                        uint32_t first, uint32_t count, const uint32_t* slab_rows,
+                                        uint32_t num_slabs, void* send, uint64_t send_capacity,
+                                        uint32_t* send_counts) {
+    if (!r || !r->impl || !input || !camera) return GSM_ERR_INVALID_ARGUMENT;
+    return r->impl->projectPartition((hipStream_t)stream, *input, *camera, width, height, first, count,
+                                     slab_rows, num_slabs, send, send_capacity, send_counts);
+}
+
+gsm_status gsm_global_render_records(gsm_renderer* r, void* stream, const void* records, uint32_t count,
+                                     uint32_t width, uint32_t height, void* color, size_t color_pitch,
+                                     void* depth, size_t depth_pitch) {
+    if (!r || !r->impl) return GSM_ERR_INVALID_ARGUMENT;
+    return r->impl->renderRecords((hipStream_t)stream, records, count, width, height, color, color_pitch,
+                                  depth, depth_pitch);
 }
 
 gsm_status gsm_global_render_stereo(gsm_renderer* r, void*, const gsm_gaussian_input*,

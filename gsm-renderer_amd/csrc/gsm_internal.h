@@ -17,6 +17,28 @@ struct ProjectArgs {
     uint32_t maxAssignments;
 };
 
+// Multi-GPU partition: tile-row boundaries of the slabs, and the 48-byte
+// record a slab owner receives per gaussian (GaussianRenderData + blend record + tile rect).
+constexpr uint32_t kMaxSlabs = 16;
+struct SlabTable {
+    uint32_t rows[kMaxSlabs + 1];
+    uint32_t n;
+};
+struct SplatRecord {
+    uint4 rd;         // GaussianRenderData
+    BlendRecordA ra;  // mean, conic, opacity, r, g
+    short4 bounds;    // tile rect
+    uint32_t rb;      // b, depth
+    uint32_t pad;
+};
+static_assert(sizeof(SplatRecord) == 48, "SplatRecord must be 48 B");
+struct PartitionBuffers {
+    SplatRecord* records = nullptr;     // [maxG] projected records of the rank's range
+    uint32_t* masks = nullptr;          // [maxG] slabs each gaussian meets
+    uint32_t* blockSlabCounts = nullptr;  // [kMaxSlabs * blocks]
+    uint32_t* slabBase = nullptr;       // [kMaxSlabs]
+};
+
 // Device buffers of one renderer (the GlobalViewResources analogue, GlobalResources.swift:6-362).
 struct DeviceArena {
     GaussianRenderData* renderData = nullptr;  // [maxG]
@@ -50,6 +72,15 @@ constexpr int kRadixChunk = kRadixBlock * kRadixItems;
 void launch_project(bool halfInput, uint32_t shDegree, const void* world, const void* harmonics,
                     const ProjectArgs& args, const DeviceArena& A, hipStream_t stream);
 // exclusive scan of the per-block sums, total + clamp into the header (GlobalShaders.metal:685-712)
+// project gaussians [0, a.count) of world/harm (already offset to the rank's range) and pack
+// the records of each slab's gaussians into `send` (slab-major, ascending id), counts to sendCounts
+void launch_partition(bool halfInput, uint32_t shDegree, const void* world, const void* harmonics,
+                      const ProjectArgs& args, const SlabTable& slabs, const PartitionBuffers& B,
+                      const float2* sincos, void* send, uint64_t capacity, uint32_t* sendCounts,
+                      hipStream_t stream);
+// received records -> per-gaussian arrays + tile counts of the renderer's rows (replaces project)
+void launch_records_in(const void* records, const ProjectArgs& args, const DeviceArena& A,
+                       hipStream_t stream);
 void launch_scan_blocks(uint32_t numBlocks, const ProjectArgs& args, const DeviceArena& A,
                         hipStream_t stream);
 // duplicate-with-keys (GlobalShaders.metal:623-678 fused with :266-295)

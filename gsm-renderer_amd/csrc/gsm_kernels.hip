@@ -274,16 +274,28 @@ __device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t v, uint32_t* l
 // 1. project + cull + SH colour + tile count  (globalProjectCull, GlobalShaders.metal:19-123;
 //    tileCountIndirectKernel, :563-616)
 // ---------------------------------------------------------------------------
+// Per-gaussian projection (globalProjectCull, GlobalShaders.metal:19-123, and the per-gaussian
+// values of globalRender): everything one gaussian contributes before tile assignment.
+struct ProjOut {
+    uint4 rd;          // GaussianRenderData
+    BlendRecordA ra;   // blend record (mean, conic, opacity, r, g)
+    uint32_t rb;       // blend record (b, depth)
+    short4 bounds;     // tile rect, (0,-1,0,-1) when culled
+    float cmx, cmy, w; // fp16-rounded mean, intersection level
+    Conic k;
+    bool vis, countable;
+};
+
 template <bool HALF, int DEG>
-__global__ __launch_bounds__(kProjectBlock) void k_project(
-    const void* __restrict__ world, const void* __restrict__ harm, ProjectArgs P,
-    GaussianRenderData* __restrict__ outRD, short4* __restrict__ outBounds,
-    BlendRecordA* __restrict__ outA, uint32_t* __restrict__ outB, uint32_t* __restrict__ counts,
-    uint32_t* __restrict__ blockSums, const float2* __restrict__ sincos) {
-    __shared__ uint32_t lds[kProjectBlock / 64];
-    const uint32_t gid = blockIdx.x * kProjectBlock + threadIdx.x;
-    uint32_t ntiles = 0;
-    if (gid < P.count) {
+__device__ __forceinline__ ProjOut project_gaussian(const void* __restrict__ world,
+                                                    const void* __restrict__ harm, uint32_t gid,
+                                                    const ProjectArgs& P,
+                                                    const float2* __restrict__ sincos) {
+    ProjOut o;
+    o.vis = false;
+    o.countable = false;
+    o.bounds = make_short4(0, -1, 0, -1);
+    {
         const CameraUniforms& cam = P.cam;
         float pos[3], scale[3], rot[4], opacity;
         if constexpr (HALF) {
@@ -518,9 +530,7 @@ __global__ __launch_bounds__(kProjectBlock) void k_project(
             if (sx + ex < 0.0f || sx - ex > cam.width || sy + ey < 0.0f || sy - ey > cam.height)
                 vis = false;
         }
-        if (!vis) {
-            outBounds[gid] = make_short4(0, -1, 0, -1);
-        } else {
+        if (vis) {
             float col[3];
             sh_color<HALF, DEG>(harm, gid, pos, cam.cameraCenter, cam.shComponents, col);
             col[0] = __builtin_fmaxf(col[0] + 0.5f, 0.0f);
@@ -547,7 +557,7 @@ __global__ __launch_bounds__(kProjectBlock) void k_project(
             rdw.y = (uint32_t)thq | ((uint32_t)hs1 << 16);
             rdw.z = (uint32_t)hs2 | ((uint32_t)hd << 16);
             rdw.w = cR | (cG << 8) | (cB << 16) | (cO << 24);
-            *(uint4*)(outRD + gid) = rdw;
+            o.rd = rdw;
 
             // computeTileBounds (GaussianShared.h:791-828)
             float maxW = cam.width - 1.0f, maxH = cam.height - 1.0f;
@@ -561,7 +571,7 @@ __global__ __launch_bounds__(kProjectBlock) void k_project(
             minTY = max(minTY, 0);
             maxTX = min(maxTX, (int)P.bin.tilesX - 1);
             maxTY = min(maxTY, (int)P.bin.tilesY - 1);
-            outBounds[gid] = make_short4((short)minTX, (short)maxTX, (short)minTY, (short)maxTY);
+            o.bounds = make_short4((short)minTX, (short)maxTX, (short)minTY, (short)maxTY);
 
             // per-gaussian values of globalRender (GlobalShaders.metal:1094-1105; getColor/getOpacity :9-15)
             float cmx = hbits_to_f(hmx), cmy = hbits_to_f(hmy);
@@ -575,19 +585,196 @@ __global__ __launch_bounds__(kProjectBlock) void k_project(
             ra.y = (uint32_t)hcxx | ((uint32_t)hcyy << 16);
             ra.z = (uint32_t)hcxy2 | ((uint32_t)hop << 16);
             ra.w = (uint32_t)hr | ((uint32_t)hg << 16);
-            outA[gid] = ra;
-            outB[gid] = (uint32_t)hb | ((uint32_t)hd << 16);
+            o.ra = ra;
+            o.rb = (uint32_t)hb | ((uint32_t)hd << 16);
+            o.vis = true;
+            o.cmx = cmx;
+            o.cmy = cmy;
+            o.k = k;
 
-            // tileCountIndirectKernel (GlobalShaders.metal:563-616), rows limited to the slab
-            float alpha = (float)cO;
-            if (alpha >= 1e-4f && minTX <= maxTX && minTY <= maxTY) {
-                float w = 2.0f * compute_power(alpha);
-                int ty0 = max(minTY, (int)P.rowBegin), ty1 = min(maxTY, (int)P.rowEnd - 1);
-                for (int ty = ty0; ty <= ty1; ++ty)
-                    for (int tx = minTX; tx <= maxTX; ++tx)
-                        if (intersects_tile(tx, ty, cmx, cmy, k, w)) ntiles++;
-            }
+            // tileCountIndirectKernel (GlobalShaders.metal:563-616): alpha is the u8 opacity
+            const float alpha = (float)cO;
+            o.countable = alpha >= 1e-4f && minTX <= maxTX && minTY <= maxTY;
+            o.w = o.countable ? 2.0f * compute_power(alpha) : 0.0f;
         }
+    }
+    return o;
+}
+
+// tiles of a projected gaussian's rect in rows [rowBegin, rowEnd) that its ellipse meets
+__device__ __forceinline__ uint32_t count_tiles(const ProjOut& o, int rowBegin, int rowEnd) {
+    uint32_t n = 0;
+    if (!o.countable) return 0;
+    const int ty0 = max((int)o.bounds.z, rowBegin), ty1 = min((int)o.bounds.w, rowEnd - 1);
+    for (int ty = ty0; ty <= ty1; ++ty)
+        for (int tx = (int)o.bounds.x; tx <= (int)o.bounds.y; ++tx)
+            if (intersects_tile(tx, ty, o.cmx, o.cmy, o.k, o.w)) n++;
+    return n;
+}
+
+template <bool HALF, int DEG>
+__global__ __launch_bounds__(kProjectBlock) void k_project(
+    const void* __restrict__ world, const void* __restrict__ harm, ProjectArgs P,
+    GaussianRenderData* __restrict__ outRD, short4* __restrict__ outBounds,
+    BlendRecordA* __restrict__ outA, uint32_t* __restrict__ outB, uint32_t* __restrict__ counts,
+    uint32_t* __restrict__ blockSums, const float2* __restrict__ sincos) {
+    __shared__ uint32_t lds[kProjectBlock / 64];
+    const uint32_t gid = blockIdx.x * kProjectBlock + threadIdx.x;
+    uint32_t ntiles = 0;
+    if (gid < P.count) {
+        const ProjOut o = project_gaussian<HALF, DEG>(world, harm, gid, P, sincos);
+        outBounds[gid] = o.bounds;
+        if (o.vis) {
+            *(uint4*)(outRD + gid) = o.rd;
+            outA[gid] = o.ra;
+            outB[gid] = o.rb;
+            ntiles = count_tiles(o, (int)P.rowBegin, (int)P.rowEnd);  // rows limited to the slab
+        }
+        counts[gid] = ntiles;
+    }
+    uint32_t s = block_reduce_add<kProjectBlock>(ntiles, lds);
+    if (threadIdx.x == 0) blockSums[blockIdx.x] = s;
+}
+
+// ---------------------------------------------------------------------------
+// 1b. multi-GPU partition: a rank projects its range of gaussians once,
+//     keeps every projected gaussian whose ellipse meets a tile of slab s, and packs its
+//     48-byte splat record into slab s's segment of the send buffer in ascending id order.
+//     The slab owner rebuilds keys from the records (k_records_in + the usual scatter), so a
+//     record crosses the fabric once per (gaussian, slab), not once per tile.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ bool meets_rows(const ProjOut& o, int rowBegin, int rowEnd) {
+    if (!o.countable) return false;
+    const int ty0 = max((int)o.bounds.z, rowBegin), ty1 = min((int)o.bounds.w, rowEnd - 1);
+    for (int ty = ty0; ty <= ty1; ++ty)
+        for (int tx = (int)o.bounds.x; tx <= (int)o.bounds.y; ++tx)
+            if (intersects_tile(tx, ty, o.cmx, o.cmy, o.k, o.w)) return true;
+    return false;
+}
+
+template <bool HALF, int DEG>
+__global__ __launch_bounds__(kProjectBlock) void k_project_part(
+    const void* __restrict__ world, const void* __restrict__ harm, ProjectArgs P, SlabTable slabs,
+    SplatRecord* __restrict__ records, uint32_t* __restrict__ masks,
+    uint32_t* __restrict__ blockSlabCounts, const float2* __restrict__ sincos) {
+    __shared__ uint32_t wcnt[kProjectBlock / 64][kMaxSlabs];
+    const uint32_t gid = blockIdx.x * kProjectBlock + threadIdx.x;
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint32_t mask = 0;
+    if (gid < P.count) {
+        const ProjOut o = project_gaussian<HALF, DEG>(world, harm, gid, P, sincos);
+        if (o.vis) {
+            SplatRecord r;
+            r.rd = o.rd;
+            r.ra = o.ra;
+            r.bounds = o.bounds;
+            r.rb = o.rb;
+            r.pad = 0u;
+            records[gid] = r;
+            for (uint32_t sl = 0; sl < slabs.n; ++sl)
+                if (meets_rows(o, (int)slabs.rows[sl], (int)slabs.rows[sl + 1])) mask |= 1u << sl;
+        }
+        masks[gid] = mask;
+    }
+    for (uint32_t sl = 0; sl < slabs.n; ++sl) {
+        const uint32_t c = (uint32_t)__popcll(__ballot((mask >> sl) & 1u));
+        if (lane == 0) wcnt[wave][sl] = c;
+    }
+    __syncthreads();
+    if (threadIdx.x < slabs.n) {
+        uint32_t t = 0;
+#pragma unroll
+        for (int w = 0; w < kProjectBlock / 64; ++w) t += wcnt[w][threadIdx.x];
+        blockSlabCounts[(size_t)threadIdx.x * gridDim.x + blockIdx.x] = t;
+    }
+}
+
+// one workgroup: per slab, exclusive scan of its block counts (in place), then the slab bases;
+// sendCounts[s] = records for slab s, slabBase[s] = its first record in the send buffer
+__global__ __launch_bounds__(1024) void k_part_scan(uint32_t* __restrict__ blockSlabCounts,
+                                                    uint32_t numBlocks, uint32_t numSlabs,
+                                                    uint32_t* __restrict__ sendCounts,
+                                                    uint32_t* __restrict__ slabBase) {
+    __shared__ uint32_t lds[1024 / 64];
+    __shared__ uint32_t totals[kMaxSlabs];
+    for (uint32_t sl = 0; sl < numSlabs; ++sl) {
+        uint32_t* row = blockSlabCounts + (size_t)sl * numBlocks;
+        uint32_t carry = 0;
+        for (uint32_t base = 0; base < numBlocks; base += 1024) {
+            const uint32_t i = base + threadIdx.x;
+            const uint32_t v = i < numBlocks ? row[i] : 0u;
+            uint32_t tot;
+            const uint32_t ex = block_exclusive_scan<1024>(v, lds, &tot);
+            if (i < numBlocks) row[i] = carry + ex;
+            carry += tot;
+            __syncthreads();
+        }
+        if (threadIdx.x == 0) totals[sl] = carry;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t run = 0;
+        for (uint32_t sl = 0; sl < numSlabs; ++sl) {
+            slabBase[sl] = run;
+            sendCounts[sl] = totals[sl];
+            run += totals[sl];
+        }
+    }
+}
+
+__global__ __launch_bounds__(kProjectBlock) void k_part_pack(
+    const SplatRecord* __restrict__ records, const uint32_t* __restrict__ masks, uint32_t count,
+    uint32_t numSlabs, const uint32_t* __restrict__ blockSlabOffsets,
+    const uint32_t* __restrict__ slabBase, SplatRecord* __restrict__ send, uint64_t capacity) {
+    __shared__ uint32_t wcnt[kProjectBlock / 64][kMaxSlabs];
+    const uint32_t gid = blockIdx.x * kProjectBlock + threadIdx.x;
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint32_t mask = gid < count ? masks[gid] : 0u;
+    const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    uint32_t rank[kMaxSlabs];
+    for (uint32_t sl = 0; sl < numSlabs; ++sl) {
+        const uint64_t b = __ballot((mask >> sl) & 1u);
+        rank[sl] = (uint32_t)__popcll(b & lt);
+        if (lane == 0) wcnt[wave][sl] = (uint32_t)__popcll(b);
+    }
+    __syncthreads();
+    if (!mask) return;
+    const SplatRecord r = records[gid];
+    for (uint32_t sl = 0; sl < numSlabs; ++sl) {
+        if (!((mask >> sl) & 1u)) continue;
+        uint32_t before = 0;
+        for (uint32_t w = 0; w < wave; ++w) before += wcnt[w][sl];
+        const uint64_t pos = (uint64_t)slabBase[sl] + blockSlabOffsets[(size_t)sl * gridDim.x + blockIdx.x] +
+                             before + rank[sl];
+        if (pos < capacity) send[pos] = r;
+    }
+}
+
+// slab owner: received records -> the renderer's per-gaussian arrays + tile counts for its rows
+__global__ __launch_bounds__(kProjectBlock) void k_records_in(
+    const SplatRecord* __restrict__ in, ProjectArgs P, GaussianRenderData* __restrict__ outRD,
+    short4* __restrict__ outBounds, BlendRecordA* __restrict__ outA, uint32_t* __restrict__ outB,
+    uint32_t* __restrict__ counts, uint32_t* __restrict__ blockSums, const float2* __restrict__ sincos) {
+    __shared__ uint32_t lds[kProjectBlock / 64];
+    const uint32_t gid = blockIdx.x * kProjectBlock + threadIdx.x;
+    uint32_t ntiles = 0;
+    if (gid < P.count) {
+        const SplatRecord r = in[gid];
+        *(uint4*)(outRD + gid) = r.rd;
+        outBounds[gid] = r.bounds;
+        outA[gid] = r.ra;
+        outB[gid] = r.rb;
+        // the values k_project had in registers, rebuilt from the record exactly as k_scatter does
+        ProjOut o;
+        o.bounds = r.bounds;
+        o.cmx = hbits_to_f((uint16_t)(r.rd.x & 0xFFFFu));
+        o.cmy = hbits_to_f((uint16_t)(r.rd.x >> 16));
+        o.k = conic_from_quant(sincos, (uint16_t)(r.rd.y & 0xFFFFu), hbits_to_f((uint16_t)(r.rd.y >> 16)),
+                               hbits_to_f((uint16_t)(r.rd.z & 0xFFFFu)));
+        const float alpha = (float)(r.rd.w >> 24);
+        o.countable = alpha >= 1e-4f && r.bounds.x <= r.bounds.y && r.bounds.z <= r.bounds.w;
+        o.w = o.countable ? 2.0f * compute_power(alpha) : 0.0f;
+        ntiles = count_tiles(o, (int)P.rowBegin, (int)P.rowEnd);
         counts[gid] = ntiles;
     }
     uint32_t s = block_reduce_add<kProjectBlock>(ntiles, lds);
@@ -741,6 +928,47 @@ void launch_project(bool halfInput, uint32_t deg, const void* world, const void*
                     const ProjectArgs& a, const DeviceArena& A, hipStream_t s) {
     if (halfInput) launch_project_t<true>(deg, world, harm, a, A, s);
     else launch_project_t<false>(deg, world, harm, a, A, s);
+}
+
+template <bool HALF>
+static void launch_project_part_t(uint32_t deg, const void* world, const void* harm, const ProjectArgs& a,
+                                  const SlabTable& slabs, const PartitionBuffers& B, const float2* sincos,
+                                  hipStream_t s) {
+    const uint32_t blocks = (a.count + kProjectBlock - 1) / kProjectBlock;
+#define GSM_LAUNCH_PPART(D)                                                                        \
+    hipLaunchKernelGGL((k_project_part<HALF, D>), dim3(blocks), dim3(kProjectBlock), 0, s, world,  \
+                       harm, a, slabs, B.records, B.masks, B.blockSlabCounts, sincos)
+    switch (deg) {
+        case 0: GSM_LAUNCH_PPART(0); break;
+        case 1: GSM_LAUNCH_PPART(1); break;
+        case 2: GSM_LAUNCH_PPART(2); break;
+        default: GSM_LAUNCH_PPART(3); break;
+    }
+#undef GSM_LAUNCH_PPART
+}
+
+void launch_partition(bool halfInput, uint32_t deg, const void* world, const void* harm,
+                      const ProjectArgs& a, const SlabTable& slabs, const PartitionBuffers& B,
+                      const float2* sincos, void* send, uint64_t capacity, uint32_t* sendCounts,
+                      hipStream_t s) {
+    const uint32_t blocks = (a.count + kProjectBlock - 1) / kProjectBlock;
+    if (blocks == 0) {
+        hipMemsetAsync(sendCounts, 0, slabs.n * sizeof(uint32_t), s);
+        return;
+    }
+    if (halfInput) launch_project_part_t<true>(deg, world, harm, a, slabs, B, sincos, s);
+    else launch_project_part_t<false>(deg, world, harm, a, slabs, B, sincos, s);
+    hipLaunchKernelGGL(k_part_scan, dim3(1), dim3(1024), 0, s, B.blockSlabCounts, blocks, slabs.n,
+                       sendCounts, B.slabBase);
+    hipLaunchKernelGGL(k_part_pack, dim3(blocks), dim3(kProjectBlock), 0, s, B.records, B.masks, a.count,
+                       slabs.n, B.blockSlabCounts, B.slabBase, (SplatRecord*)send, capacity);
+}
+
+void launch_records_in(const void* records, const ProjectArgs& a, const DeviceArena& A, hipStream_t s) {
+    const uint32_t blocks = (a.count + kProjectBlock - 1) / kProjectBlock;
+    if (blocks == 0) return;
+    hipLaunchKernelGGL(k_records_in, dim3(blocks), dim3(kProjectBlock), 0, s, (const SplatRecord*)records, a,
+                       A.renderData, A.bounds, A.recA, A.recB, A.tileCounts, A.blockSums, A.sincosTable);
 }
 
 void launch_scan_blocks(uint32_t nb, const ProjectArgs& a, const DeviceArena& A, hipStream_t s) {

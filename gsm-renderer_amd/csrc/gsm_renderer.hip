@@ -156,19 +156,8 @@ int GlobalRenderer::sortPassCount() const {
     return p > 4 ? 4 : p;
 }
 
-gsm_status GlobalRenderer::render(hipStream_t s, const gsm_gaussian_input& in,
-                                  const gsm_camera_params& camp, uint32_t width, uint32_t height,
-                                  void* color, size_t colorPitch, void* depth, size_t depthPitch) {
-    // validateLimits (GlobalRenderer.swift:372-376) -- errors instead of a silent skip
-    if (in.gaussian_count > maxGaussians_) return GSM_ERR_INVALID_GAUSSIAN_COUNT;
-    if (width == 0 || height == 0 || width > maxWidth_ || height > maxHeight_)
-        return GSM_ERR_INVALID_DIMENSIONS;
-    if (!color) return GSM_ERR_MISSING_REQUIRED_BUFFER;
-    if (in.gaussian_count > 0 && (!in.gaussians || !in.harmonics)) return GSM_ERR_MISSING_REQUIRED_BUFFER;
-    if (colorPitch < (size_t)width * 8) return GSM_ERR_INVALID_BUFFER_SIZE;
-    if (depth && depthPitch < (size_t)width * 2) return GSM_ERR_INVALID_BUFFER_SIZE;
-    if (hipSetDevice(device_) != hipSuccess) return GSM_ERR_DEVICE_NOT_AVAILABLE;
-
+ProjectArgs GlobalRenderer::frameArgs(const gsm_camera_params& camp, uint32_t width, uint32_t height,
+                                      uint32_t count, uint32_t shComponents) const {
     ProjectArgs a;
     std::memset(&a, 0, sizeof(a));
     // CameraUniforms(from: camera, ...) (KernelTypes.swift:107-123)
@@ -182,35 +171,126 @@ gsm_status GlobalRenderer::render(hipStream_t s, const gsm_gaussian_input& in,
     a.cam.height = (float)height;
     a.cam.nearPlane = camp.near_plane;
     a.cam.farPlane = camp.far_plane;
-    a.cam.shComponents = in.sh_components;
-    a.cam.gaussianCount = in.gaussian_count;
+    a.cam.shComponents = shComponents;
+    a.cam.gaussianCount = count;
     a.cam.inputIsSRGB = config_.gaussian_color_space == GSM_COLOR_SPACE_SRGB ? 1.0f : 0.0f;
     // buildBinningParams (GlobalRenderer.swift:38-51)
-    a.bin.gaussianCount = in.gaussian_count;
+    a.bin.gaussianCount = count;
     a.bin.tilesX = tilesX_;
     a.bin.tilesY = tilesY_;
     a.bin.tileWidth = kTileWidth;
     a.bin.tileHeight = kTileHeight;
     a.bin.surfaceWidth = maxWidth_;
     a.bin.surfaceHeight = maxHeight_;
-    a.bin.maxCapacity = in.gaussian_count;
+    a.bin.maxCapacity = count;
     a.bin.alphaThreshold = 0.005f;
     a.bin.totalInkThreshold = 2.0f;
     a.rowBegin = rowBegin_;
     a.rowEnd = rowEnd_;
-    a.count = in.gaussian_count;
+    a.count = count;
     a.maxAssignments = maxAssignments_;
 
+    return a;
+}
+
+gsm_status GlobalRenderer::validateFrame(uint32_t count, bool inputMissing, uint32_t width, uint32_t height,
+                                         const void* color, size_t colorPitch, const void* depth,
+                                         size_t depthPitch) const {
+    // validateLimits (GlobalRenderer.swift:372-376) -- errors instead of a silent skip
+    if (count > maxGaussians_) return GSM_ERR_INVALID_GAUSSIAN_COUNT;
+    if (width == 0 || height == 0 || width > maxWidth_ || height > maxHeight_)
+        return GSM_ERR_INVALID_DIMENSIONS;
+    if (!color) return GSM_ERR_MISSING_REQUIRED_BUFFER;
+    if (count > 0 && inputMissing) return GSM_ERR_MISSING_REQUIRED_BUFFER;
+    if (colorPitch < (size_t)width * 8) return GSM_ERR_INVALID_BUFFER_SIZE;
+    if (depth && depthPitch < (size_t)width * 2) return GSM_ERR_INVALID_BUFFER_SIZE;
+    if (hipSetDevice(device_) != hipSuccess) return GSM_ERR_DEVICE_NOT_AVAILABLE;
+    return GSM_OK;
+}
+
+gsm_status GlobalRenderer::render(hipStream_t s, const gsm_gaussian_input& in,
+                                  const gsm_camera_params& camp, uint32_t width, uint32_t height,
+                                  void* color, size_t colorPitch, void* depth, size_t depthPitch) {
+    gsm_status st = validateFrame(in.gaussian_count, !in.gaussians || !in.harmonics, width, height, color,
+                                  colorPitch, depth, depthPitch);
+    if (st != GSM_OK) return st;
+    const ProjectArgs a = frameArgs(camp, width, height, in.gaussian_count, in.sh_components);
     // GlobalProjectCullEncoder.swift:19-26 SH_DEGREE selection
     const uint32_t k = in.sh_components;
     const uint32_t deg = k <= 1 ? 0u : (k <= 4 ? 1u : (k <= 9 ? 2u : 3u));
+    const bool half = config_.precision == GSM_PRECISION_FLOAT16;
+    return runFrame(s, a, width, height, color, colorPitch, depth, depthPitch,
+                    [&](const ProjectArgs& pa) { launch_project(half, deg, in.gaussians, in.harmonics, pa, arena_, s); });
+}
+
+gsm_status GlobalRenderer::renderRecords(hipStream_t s, const void* records, uint32_t count, uint32_t width,
+                                         uint32_t height, void* color, size_t colorPitch, void* depth,
+                                         size_t depthPitch) {
+    gsm_status st = validateFrame(count, !records, width, height, color, colorPitch, depth, depthPitch);
+    if (st != GSM_OK) return st;
+    gsm_camera_params cam;
+    std::memset(&cam, 0, sizeof(cam));
+    const ProjectArgs a = frameArgs(cam, width, height, count, 1);
+    return runFrame(s, a, width, height, color, colorPitch, depth, depthPitch,
+                    [&](const ProjectArgs& pa) { launch_records_in(records, pa, arena_, s); });
+}
+
+gsm_status GlobalRenderer::projectPartition(hipStream_t s, const gsm_gaussian_input& in,
+                                            const gsm_camera_params& camp, uint32_t width, uint32_t height,
+                                            uint32_t first, uint32_t count, const uint32_t* slabRows,
+                                            uint32_t numSlabs, void* send, uint64_t capacity,
+                                            uint32_t* sendCounts) {
+    if ((uint64_t)first + count > in.gaussian_count || count > maxGaussians_)
+        return GSM_ERR_INVALID_GAUSSIAN_COUNT;
+    if (width == 0 || height == 0 || width > maxWidth_ || height > maxHeight_)
+        return GSM_ERR_INVALID_DIMENSIONS;
+    if (!slabRows || numSlabs == 0 || numSlabs > kMaxSlabs) return GSM_ERR_INVALID_ARGUMENT;
+    if (!sendCounts || (count > 0 && (!send || !in.gaussians || !in.harmonics)))
+        return GSM_ERR_MISSING_REQUIRED_BUFFER;
+    SlabTable slabs;
+    std::memset(&slabs, 0, sizeof(slabs));
+    slabs.n = numSlabs;
+    for (uint32_t i = 0; i <= numSlabs; ++i) {
+        if (slabRows[i] > tilesY_ || (i > 0 && slabRows[i] < slabRows[i - 1])) return GSM_ERR_INVALID_ARGUMENT;
+        slabs.rows[i] = slabRows[i];
+    }
+    if (hipSetDevice(device_) != hipSuccess) return GSM_ERR_DEVICE_NOT_AVAILABLE;
+    if (!part_.records) {  // lazily: only ranks of a partitioned frame need these
+        const size_t blocks = ((size_t)maxGaussians_ + kProjectBlock - 1) / kProjectBlock;
+        gsm_status st = alloc((void**)&part_.records, (size_t)maxGaussians_ * sizeof(SplatRecord));
+        if (st == GSM_OK) st = alloc((void**)&part_.masks, (size_t)maxGaussians_ * 4);
+        if (st == GSM_OK) st = alloc((void**)&part_.blockSlabCounts, kMaxSlabs * (blocks + 1) * 4);
+        if (st == GSM_OK) st = alloc((void**)&part_.slabBase, kMaxSlabs * 4);
+        if (st != GSM_OK) {
+            part_ = PartitionBuffers();
+            return st;
+        }
+    }
+    const bool half = config_.precision == GSM_PRECISION_FLOAT16;
+    ProjectArgs a = frameArgs(camp, width, height, count, in.sh_components);
+    a.rowBegin = 0;
+    a.rowEnd = tilesY_;
+    const size_t ws = half ? sizeof(PackedWorldGaussianHalf) : sizeof(PackedWorldGaussian);
+    const size_t hs = (size_t)in.sh_components * 3 * (half ? 2 : 4);
+    const char* world = (const char*)in.gaussians + (size_t)first * ws;
+    const char* harm = (const char*)in.harmonics + (size_t)first * hs;
+    const uint32_t k = in.sh_components;
+    const uint32_t deg = k <= 1 ? 0u : (k <= 4 ? 1u : (k <= 9 ? 2u : 3u));
+    launch_partition(half, deg, world, harm, a, slabs, part_, arena_.sincosTable, send, capacity, sendCounts, s);
+    if (hipGetLastError() != hipSuccess) return GSM_ERR_RENDER_FAILED;
+    return GSM_OK;
+}
+
+template <class Front>
+gsm_status GlobalRenderer::runFrame(hipStream_t s, const ProjectArgs& a, uint32_t width, uint32_t height,
+                                    void* color, size_t colorPitch, void* depth, size_t depthPitch,
+                                    Front&& front) {
     const bool prof = (profiling_ & 1) != 0;
     const bool keep = (profiling_ & 2) != 0;
-    const uint32_t nb = (in.gaussian_count + kProjectBlock - 1) / kProjectBlock;
-    lastCount_ = in.gaussian_count;
+    const uint32_t nb = (a.count + kProjectBlock - 1) / kProjectBlock;
+    lastCount_ = a.count;
     lastWidth_ = width;
     lastHeight_ = height;
-
     // Blend schedule: the units ordered by the walk lengths the previous frame of the same
     // geometry measured (the image does not depend on the order, only the load balance does).
     // The ordering kernel only needs those costs, so it runs on a side stream beside this
@@ -239,8 +319,7 @@ gsm_status GlobalRenderer::render(hipStream_t s, const gsm_gaussian_input& in,
 
     hipEvent_t* ev = prof ? frameEvents(profFrames_) : nullptr;
     if (prof) hipEventRecord(ev[0], s);
-    launch_project(config_.precision == GSM_PRECISION_FLOAT16, deg, in.gaussians, in.harmonics, a,
-                   arena_, s);
+    front(a);
     if (prof) hipEventRecord(ev[1], s);
     launch_scan_blocks(nb, a, arena_, s);
     if (prof) hipEventRecord(ev[2], s);

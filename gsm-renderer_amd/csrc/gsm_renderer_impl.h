@@ -22,6 +22,15 @@ class GlobalRenderer {
                       const gsm_camera_params& camera, uint32_t width, uint32_t height, void* color,
                       size_t colorPitch, void* depth, size_t depthPitch);
 
+    // multi-GPU partition: project ids [first, first+count) and pack the splat
+    // records of every tile-row slab they meet; render a slab from the records it received
+    gsm_status projectPartition(hipStream_t stream, const gsm_gaussian_input& input,
+                                const gsm_camera_params& camera, uint32_t width, uint32_t height,
+                                uint32_t first, uint32_t count, const uint32_t* slabRows, uint32_t numSlabs,
+                                void* send, uint64_t capacity, uint32_t* sendCounts);
+    gsm_status renderRecords(hipStream_t stream, const void* records, uint32_t count, uint32_t width,
+                             uint32_t height, void* color, size_t colorPitch, void* depth, size_t depthPitch);
+
     gsm_status counters(gsm_debug_counters* out);
     gsm_status debugCopy(int which, void* dst, size_t bytes, size_t* needed);
     gsm_status setProfiling(int flags);  // bit0: stage events, bit1: keep unsorted keys
@@ -33,6 +42,15 @@ class GlobalRenderer {
    private:
     GlobalRenderer() = default;
     gsm_status alloc(void** p, size_t bytes);
+    ProjectArgs frameArgs(const gsm_camera_params& camera, uint32_t width, uint32_t height, uint32_t count,
+                          uint32_t shComponents) const;
+    gsm_status validateFrame(uint32_t count, bool inputMissing, uint32_t width, uint32_t height,
+                             const void* color, size_t colorPitch, const void* depth, size_t depthPitch) const;
+    // scan, scatter, sort, headers and blend after `front` filled the per-gaussian arrays
+    template <class Front>
+    gsm_status runFrame(hipStream_t s, const ProjectArgs& a, uint32_t width, uint32_t height, void* color,
+                        size_t colorPitch, void* depth, size_t depthPitch, Front&& front);
+    PartitionBuffers part_;
     void release();
     int sortPassCount() const;
 

@@ -185,7 +185,17 @@ _SIGNATURES = {
     "gsm_global_stage_times": ([C.c_void_p, C.POINTER(C.c_float), C.c_int], C.c_int),
     "gsm_global_set_tile_rows": ([C.c_void_p, C.c_uint32, C.c_uint32], C.c_int),
     "gsm_sort_pairs_u32": ([C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p], C.c_int),
+    # include/gsm_multigpu.h
+    "gsm_global_project_partition": ([C.c_void_p, C.c_void_p, C.POINTER(_Input), C.POINTER(_Camera),
+                                      C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32,
+                                      C.POINTER(C.c_uint32), C.c_uint32, C.c_void_p, C.c_uint64,
+                                      C.c_void_p], C.c_int),
+    "gsm_global_render_records": ([C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32,
+                                   C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t], C.c_int),
 }
+
+SPLAT_RECORD_BYTES = 48  # include/gsm_multigpu.h GSM_SPLAT_RECORD_BYTES
+MAX_SLABS = 16
 
 
 def _lib():
@@ -280,6 +290,32 @@ class GlobalRenderer:
                                       int(width), int(height), _ptr(color_texture), cp,
                                       _ptr(depth_texture), dp)
         _check(st, "gsm_global_render")
+
+    def project_partition(self, input: GaussianInput, camera: CameraParams, width: int, height: int,
+                          first: int, count: int, slab_rows, send, send_capacity: int, send_counts,
+                          stream=None):
+        """gsm_global_project_partition: records of ids [first, first+count) per tile-row slab
+        (slab_rows: num_slabs + 1 boundaries) into `send` (device, send_capacity records);
+        `send_counts` (device, uint32 per slab) receives the record count of every slab."""
+        inp = _Input(_ptr(input.gaussians), _ptr(input.harmonics), int(input.gaussian_count),
+                     int(input.sh_components))
+        cam = _camera_struct(camera)
+        rows = (C.c_uint32 * len(slab_rows))(*[int(x) for x in slab_rows])
+        st = _lib().gsm_global_project_partition(self._h, _stream_handle(stream), C.byref(inp), C.byref(cam),
+                                                 int(width), int(height), int(first), int(count), rows,
+                                                 len(slab_rows) - 1, _ptr(send), int(send_capacity),
+                                                 _ptr(send_counts))
+        _check(st, "gsm_global_project_partition")
+
+    def render_records(self, color_texture, depth_texture, records, count: int, width: int, height: int,
+                       stream=None, color_pitch: Optional[int] = None, depth_pitch: Optional[int] = None):
+        """gsm_global_render_records: this renderer's tile rows from `count` received records."""
+        cp = color_pitch if color_pitch is not None else int(width) * 8
+        dp = depth_pitch if depth_pitch is not None else int(width) * 2
+        st = _lib().gsm_global_render_records(self._h, _stream_handle(stream), _ptr(records), int(count),
+                                              int(width), int(height), _ptr(color_texture), cp,
+                                              _ptr(depth_texture), dp)
+        _check(st, "gsm_global_render_records")
 
     def render_stereo(self, color_texture, depth_texture, input: GaussianInput, left: CameraParams,
                       right: CameraParams, width: int, height: int, stream=None):

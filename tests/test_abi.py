@@ -8,7 +8,7 @@ import subprocess
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-HEADERS = [os.path.join(ROOT, "include", h) for h in ("gsm_renderer.h", "gsm_debug.h")]
+HEADERS = [os.path.join(ROOT, "include", h) for h in ("gsm_renderer.h", "gsm_debug.h", "gsm_multigpu.h")]
 
 
 def declared_functions():

@@ -6,9 +6,13 @@ radix sort -> tile headers -> front-to-back fp16 blend) over one synthetic scene
 resident in HBM.  Default workload = BASELINE.json configs[1]: 1M gaussians, SH3,
 1920x1080, PackedWorldGaussianHalf (fp16).
 
-N>1 (torch.distributed.run, one rank per GPU, RCCL): every rank projects all
-gaussians and renders its band of tile rows (gsm_amd.slabs); the bands are gathered on
-rank 0 inside the timed step.  The frame is fixed as N grows -> "scaling": "strong".
+N>1 (torch.distributed.run, one rank per GPU, RCCL over xGMI), --multi:
+  alltoall (default): rank r projects ids [r*N/n, (r+1)*N/n) once and packs a
+      48-byte record per (gaussian, slab it meets); all_to_all of the counts and of the
+      records (gsm_amd.exchange); every rank renders its band of tile rows from the records;
+  replicas: every rank projects all gaussians and keeps its band's assignments.
+Either way the bands are gathered on rank 0 inside the timed step.  The frame is fixed as N
+grows -> "scaling": "strong".
 
 Prints ONE JSON line on rank 0 (contract in the task statement), including
 "roofline" for the dominant kernel (the blend) and "cpu_baseline" (the C oracle
@@ -40,6 +44,8 @@ def parse():
     p.add_argument("--cpu-threads", type=int, default=16)
     p.add_argument("--parity", type=int, default=1, help="compare the frame with the oracle")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
+    p.add_argument("--multi", choices=("alltoall", "replicas"), default="alltoall",
+                   help="N>1 partition: all-to-all of projected records (8e) or projection replicas")
     return p.parse_args()
 
 
@@ -49,15 +55,22 @@ def main():
     import torch.distributed as dist
 
     import gsm_amd
-    from gsm_amd import scenes, slabs
+    from gsm_amd import exchange, scenes, slabs
 
     world_size = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    # BENCH_DIST_BACKEND=gloo rehearses the N>1 protocol with several ranks on one GPU (CPU-staged
+    # collectives; timings meaningless).  The driver's multi-GPU runs use RCCL ("nccl").
+    backend = os.environ.get("BENCH_DIST_BACKEND", "nccl")
+    gpu = local_rank % max(1, torch.cuda.device_count()) if backend == "gloo" else local_rank
     if world_size > 1:
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-    dev = torch.device("cuda", local_rank if world_size > 1 else 0)
+        torch.cuda.set_device(gpu)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
+        else:
+            dist.init_process_group(backend)
+    dev = torch.device("cuda", gpu if world_size > 1 else 0)
     torch.cuda.set_device(dev)
 
     c = scenes.CONFIGS[args.config]
@@ -85,10 +98,30 @@ def main():
     cam = gsm_amd.CameraParams.from_dict(cam_d)
     stream = torch.cuda.current_stream(dev)
 
+    alltoall = world_size > 1 and args.multi == "alltoall"
+    if alltoall:
+        first, cnt = exchange.id_range(n, world_size, rank)
+        rows = exchange.slab_rows(tiles_y, H, world_size)
+        send_cap = max(cnt, 1) * world_size
+        send = torch.empty(send_cap * exchange.RECORD_BYTES, dtype=torch.uint8, device=dev)
+        send_counts = torch.zeros(world_size, dtype=torch.int32, device=dev)
+        recv = torch.empty(max(n, 1) * exchange.RECORD_BYTES, dtype=torch.uint8, device=dev)
+
     def step():
-        renderer.render(cptr, dptr, inp, cam, W, H, stream=stream, color_pitch=pitch_c, depth_pitch=pitch_d)
+        if alltoall:
+            renderer.project_partition(inp, cam, W, H, first, cnt, rows, send, send_cap, send_counts,
+                                       stream=stream)
+            nrec = exchange.exchange(send, send_counts, recv, staged=backend != "nccl")
+            renderer.render_records(cptr, dptr, recv, nrec, W, H, stream=stream, color_pitch=pitch_c,
+                                    depth_pitch=pitch_d)
+        else:
+            renderer.render(cptr, dptr, inp, cam, W, H, stream=stream, color_pitch=pitch_c, depth_pitch=pitch_d)
         if world_size > 1:
-            dist.gather(color, gather_list=gather, dst=0)
+            if backend == "nccl":
+                dist.gather(color, gather_list=gather, dst=0)
+            else:  # rehearsal: gloo collectives take host tensors
+                gl = [g.cpu() for g in gather] if gather else None
+                dist.gather(color.cpu(), gather_list=gl, dst=0)
 
     for _ in range(args.warmup):
         step()
@@ -175,7 +208,9 @@ def main():
                                f"{W}x{H} {'fp16 PackedWorldGaussianHalf' if prec else 'fp32 PackedWorldGaussian'}",
                    "gaussians": n, "width": W, "height": H, "sh_components": sh,
                    "assignments": A, "tiles": T,
-                   "parallelism": "tile-row slabs" if world_size > 1 else "single GPU"},
+                   "parallelism": (f"dp{world_size} tile-row slabs, "
+                                   + ("all-to-all of projected records" if alltoall else "projection replicas"))
+                                  if world_size > 1 else "single GPU"},
         "roofline": {"bound": "hbm", "kernel": "k_blend", "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "algorithmic_bytes": b_blend, "avg_launch_ms": stage_ms["blend"],

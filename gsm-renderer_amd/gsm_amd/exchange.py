@@ -37,17 +37,23 @@ def slab_rows(tiles_y: int, height: int, world_size: int) -> List[int]:
     return [s.row_begin for s in ss] + [ss[-1].row_end]
 
 
-def exchange(send, send_counts, recv, group=None) -> int:
+def exchange(send, send_counts, recv, group=None, staged: bool = False) -> int:
     """all_to_all of per-slab record counts, then of the records themselves.
 
     send: byte tensor holding the slab-major records of this rank; send_counts: int32
     tensor, one count per destination rank; recv: byte tensor large enough for every
     record this rank receives.  Returns the number of records received (they sit at the
     front of `recv` in source-rank order).  Works for any torch.distributed backend that
-    implements all_to_all_single (nccl = RCCL on ROCm, gloo)."""
+    implements all_to_all_single (nccl = RCCL on ROCm, gloo).  staged=True moves device
+    tensors through host memory (gloo rehearsal of a multi-GPU run)."""
     import torch
     import torch.distributed as dist
 
+    if staged and send.is_cuda:
+        hr = torch.empty(recv.numel(), dtype=torch.uint8)
+        got = exchange(send.cpu(), send_counts.cpu(), hr, group=group)
+        recv[: got * RECORD_BYTES].copy_(hr[: got * RECORD_BYTES])
+        return got
     recv_counts = torch.empty_like(send_counts)
     dist.all_to_all_single(recv_counts, send_counts, group=group)
     sc = [int(x) for x in send_counts.tolist()]

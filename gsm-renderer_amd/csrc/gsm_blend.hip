@@ -351,6 +351,205 @@ __global__ __launch_bounds__(NT) void k_blend_px(
 }
 
 // ---------------------------------------------------------------------------
+// k_blend_lanes: group-granular blend.  The unit of work is one reference thread's 4x2 pixel
+// group (item = tile * 64 + group); a wave holds 32 of them, two lanes per group (one pixel
+// row each, two pixel pairs per lane).  Every group walks its tile's list only until its own
+// saturation break (GlobalShaders.metal:1086-1088), and the moment a group finishes its two
+// lanes take the next item, so no lane waits for a slower group of the same unit.  Records
+// are gathered per lane (no broadcast): entry cur's record and entry cur+1's index are
+// loaded one iteration ahead (ping-pong registers, unrolled by two so no load result is
+// copied in a loop phi).  Items are handed out a tile at a time per wave (one atomic per
+// tile; the first tile of every wave is static).
+// ---------------------------------------------------------------------------
+template <int NT>
+__global__ __launch_bounds__(NT) void k_blend_lanes(
+    const uint32_t* __restrict__ tileStart, const uint32_t* __restrict__ sortedVals,
+    const BlendRecordA* __restrict__ recA, const uint32_t* __restrict__ recB,
+    const uint16_t* __restrict__ expTable, uint32_t* __restrict__ queue, uint32_t tileBegin,
+    uint32_t numTiles, uint32_t tilesX, uint32_t W, uint32_t H, uint8_t* __restrict__ color,
+    size_t colorPitch, uint8_t* __restrict__ depth, size_t depthPitch, int flags) {
+    constexpr uint32_t NW = NT / 64;
+    const bool vecStores = (flags & 1) != 0;
+    __shared__ __attribute__((aligned(16))) uint16_t tbl[65536];
+    {
+        const uint4* src = (const uint4*)expTable;
+        uint4* dst = (uint4*)tbl;
+        for (int i = threadIdx.x; i < 65536 * 2 / 16; i += NT) dst[i] = src[i];
+    }
+    __syncthreads();
+
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t rowInGroup = lane & 1u;
+    const uint64_t slotBit = 1ull << (lane & ~1u);  // the even lane of this lane's slot
+    const h2 ONE = {(h1)1.0f, (h1)1.0f};
+    const h2 ZERO = {(h1)0.0f, (h1)0.0f};
+    const uint32_t thrBits = (uint32_t)__builtin_bit_cast(uint16_t, (h1)(1.0f / 255.0f));
+    const h1 c099 = (h1)0.99;
+    const h2 C099 = {c099, c099};
+    const uint32_t gridWaves = gridDim.x * NW;
+
+    // Wave-uniform tile stream: the tile being handed out and `left` of its 64 groups still to
+    // give.  The first tile of every wave is static; later ones come from the queue (a wave
+    // fetches a tile ~2 (1080p) to ~8 (4K) times, so the fetch latency is not hidden).
+    auto tile_bounds = [&](uint32_t t, uint32_t& s0, uint32_t& s1) {
+        if (t < numTiles) {
+            s0 = __builtin_amdgcn_readfirstlane(tileStart[tileBegin + t]);
+            s1 = __builtin_amdgcn_readfirstlane(tileStart[tileBegin + t + 1]);
+        } else {
+            s0 = s1 = 0;
+        }
+    };
+    uint32_t curTile = blockIdx.x * NW + (threadIdx.x >> 6);
+    uint32_t cs0, cs1;
+    tile_bounds(curTile, cs0, cs1);
+    uint32_t nextItem = 0, left = curTile < numTiles ? 64u : 0u;
+    bool exhausted = curTile >= numTiles;
+
+    // per-lane slot state
+    bool act = false;
+    uint32_t cur = 0, end = 0, wait = 0, outX = 0, outY = 0;
+    bool hasList = false;
+    h2 T[2], R[2], G[2], B[2], D[2], X[2], Y = ZERO;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        T[q] = ONE;
+        R[q] = G[q] = B[q] = D[q] = X[q] = ZERO;
+    }
+    // pipeline registers in two sets: the record of entry cur and the index of entry cur+1
+    uint4 ra0 = make_uint4(0, 0, 0, 0), ra1 = make_uint4(0, 0, 0, 0);
+    uint32_t rb0 = 0, rb1 = 0, ix0 = 0, ix1 = 0;
+
+    auto refill = [&]() {
+        uint64_t freeM = __ballot(!act) & 0x5555555555555555ull;  // one bit per free slot
+        while (freeM && !exhausted) {
+            if (left == 0) {  // next tile from the queue
+                uint32_t t = 0;
+                if (lane == 0) t = atomicAdd(queue, 1u);
+                curTile = __builtin_amdgcn_readfirstlane(t) + gridWaves;
+                if (curTile >= numTiles) {
+                    exhausted = true;
+                    break;
+                }
+                tile_bounds(curTile, cs0, cs1);
+                nextItem = 0;
+                left = 64;
+            }
+            const uint32_t nFree = (uint32_t)__popcll(freeM);
+            const uint32_t take = nFree < left ? nFree : left;
+            const uint32_t rank = (uint32_t)__popcll(freeM & (slotBit - 1ull));
+            if ((freeM & slotBit) && rank < take) {
+                const uint32_t g = nextItem + rank;  // group of the tile: reference thread (g&7, g>>3)
+                const uint32_t tile = tileBegin + curTile;
+                const uint32_t tx = tile % tilesX, ty = tile / tilesX;
+                cur = cs0;
+                end = cs1;
+                hasList = cs1 > cs0;
+                wait = 2;  // two iterations fill the pipeline
+                act = true;
+                outX = tx * kTileWidth + (g & 7u) * 4u;
+                outY = ty * kTileHeight + (g >> 3) * 2u + rowInGroup;
+                X[0] = h2{(h1)(float)outX, (h1)(float)(outX + 1u)};
+                X[1] = h2{(h1)(float)(outX + 2u), (h1)(float)(outX + 3u)};
+                Y = h2{(h1)(float)outY, (h1)(float)outY};
+#pragma unroll
+                for (int q = 0; q < 2; ++q) {
+                    T[q] = ONE;
+                    R[q] = G[q] = B[q] = D[q] = ZERO;
+                }
+            }
+            for (uint32_t k = 0; k < take; ++k) freeM &= freeM - 1ull;  // drop the served slots
+            nextItem += take;
+            left -= take;
+        }
+    };
+
+    auto finish = [&]() {  // the group's 8 pixels (GlobalShaders.metal:1152-1186)
+        if (outY < H) {
+            uint8_t* crow = color + (size_t)outY * colorPitch;
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+                const uint32_t px = outX + 2u * (uint32_t)q;
+                // empty tiles keep the clear colour (0,0,0,1) (GlobalShaders.metal:140-154)
+                const h2 Av = hasList ? (ONE - T[q]) : ONE;
+                const uint32_t ur = as_u32(R[q]), ug = as_u32(G[q]), ub = as_u32(B[q]), ua = as_u32(Av);
+                const uint32_t p0a = (ur & 0xFFFFu) | (ug << 16);
+                const uint32_t p0b = (ub & 0xFFFFu) | (ua << 16);
+                const uint32_t p1a = (ur >> 16) | (ug & 0xFFFF0000u);
+                const uint32_t p1b = (ub >> 16) | (ua & 0xFFFF0000u);
+                const uint32_t ud = as_u32(D[q]);
+                if (vecStores && px + 1 < W) {
+                    *(uint4*)(crow + (size_t)px * 8) = make_uint4(p0a, p0b, p1a, p1b);
+                    if (depth) *(uint32_t*)(depth + (size_t)outY * depthPitch + (size_t)px * 2) = ud;
+                } else {
+                    if (px < W) {
+                        uint32_t* c0 = (uint32_t*)(crow + (size_t)px * 8);
+                        c0[0] = p0a;
+                        c0[1] = p0b;
+                        if (depth) *(uint16_t*)(depth + (size_t)outY * depthPitch + (size_t)px * 2) = (uint16_t)(ud & 0xFFFFu);
+                    }
+                    if (px + 1 < W) {
+                        uint32_t* c1 = (uint32_t*)(crow + (size_t)(px + 1) * 8);
+                        c1[0] = p1a;
+                        c1[1] = p1b;
+                        if (depth) *(uint16_t*)(depth + (size_t)outY * depthPitch + (size_t)(px + 1) * 2) = (uint16_t)(ud >> 16);
+                    }
+                }
+            }
+        }
+        act = false;
+    };
+
+    // One list entry per slot: first the loads of the next entry (record of cur+1 through the
+    // index in `ix`, index of cur+2; unpredicated and clamped to the tile's list -- or to entry 0,
+    // which the renderer keeps a valid gaussian id), then the blend of entry cur from (ra, rb).
+    auto step = [&](const uint4 ra, const uint32_t rb, const uint32_t ix, uint4& na, uint32_t& nb, uint32_t& nx) {
+        na = *(const uint4*)(recA + ix);
+        nb = recB[ix];
+        const uint32_t ahead = wait == 2 ? 0u : (wait == 1 ? 1u : 2u);
+        nx = sortedVals[end > cur + ahead ? cur + ahead : (end > 0 ? end - 1u : 0u)];
+        if (act && wait == 0) {
+            // group break (GlobalShaders.metal:1086-1088): max T over the group's 8 pixels
+            const u16x2 tm = __builtin_elementwise_max(__builtin_bit_cast(u16x2, T[0]), __builtin_bit_cast(u16x2, T[1]));
+            const uint32_t tb = __builtin_bit_cast(uint32_t, tm);
+            uint32_t gm = max(tb & 0xFFFFu, tb >> 16);
+            const uint32_t o = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)gm, 0xB1, 0xF, 0xF, false);
+            gm = max(gm, o);  // the other row of the group (partner lane, same slot)
+            if (gm < thrBits || cur >= end) {
+                finish();
+            } else {
+                const h2 mean = as_h2(ra.x), cc = as_h2(ra.y), oc = as_h2(ra.z), rgv = as_h2(ra.w), bdv = as_h2(rb);
+                const h2 dyv = Y - splat_hi(mean);
+                const h2 dyy = (dyv * dyv) * splat_hi(cc);
+#pragma unroll
+                for (int q = 0; q < 2; ++q) {
+                    const h2 dx = X[q] - splat_lo(mean);
+                    // p = ((dx*dx)*cxx + (dy*dy)*cyy) + (dx*dy)*cxy2 (GlobalShaders.metal:1115-1122)
+                    const h2 pq = ((dx * dx) * splat_lo(cc) + dyy) + (dx * dyv) * splat_lo(oc);
+                    // a = min(opacity * exp(-0.5h * p), 0.99h) (GlobalShaders.metal:1124-1131)
+                    const h2 a = __builtin_elementwise_min(splat_hi(oc) * lookup2(tbl, pq), C099);
+                    const h2 w = a * T[q];  // (GlobalShaders.metal:1137-1149)
+                    T[q] = T[q] * (ONE - a);
+                    R[q] = R[q] + splat_lo(rgv) * w;
+                    G[q] = G[q] + splat_hi(rgv) * w;
+                    B[q] = B[q] + splat_lo(bdv) * w;
+                    D[q] = D[q] + splat_hi(bdv) * w;
+                }
+                cur++;
+            }
+        } else if (act) {
+            wait--;
+        }
+    };
+
+    refill();
+    while (__ballot(act) != 0) {
+        step(ra0, rb0, ix0, ra1, rb1, ix1);
+        step(ra1, rb1, ix1, ra0, rb0, ix0);
+        refill();
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Blend schedule: a stable sort of the units into 8 linear buckets of last frame's walk length
 // (longest bucket first; index order, i.e. tile locality, kept inside a bucket), one workgroup.
 // ---------------------------------------------------------------------------
@@ -412,10 +611,13 @@ int blend_pairs_per_lane() {
 
 uint32_t blend_units_per_tile() { return 4u / (uint32_t)blend_pairs_per_lane(); }
 
-static int blend_waves_per_wg() {
+static int blend_waves_per_wg(uint32_t numTiles, int numCUs) {
     const char* v = getenv("GSM_BLEND_WAVES");
-    const int w = v ? atoi(v) : 8;
-    return (w == 8 || w == 16) ? w : 8;
+    if (v && (atoi(v) == 8 || atoi(v) == 16)) return atoi(v);
+    // 16 waves per CU hide more latency once every wave slot gets >= 6 units (4K: 16200 tiles);
+    // with fewer units per slot the tail dominates and 8 waves finish first (1080p)
+    const uint64_t units = (uint64_t)numTiles * blend_units_per_tile();
+    return units >= 6ull * (uint64_t)numCUs * 16u ? 16 : 8;
 }
 
 bool blend_schedule_enabled(uint32_t numTiles, int numCUs) {
@@ -423,9 +625,10 @@ bool blend_schedule_enabled(uint32_t numTiles, int numCUs) {
     if (v && v[0] == '0') return false;
     if (v && v[0] == '1') return true;
     // Ordering by last frame's walks pays where units are few per wave slot (balance), and
-    // costs L2 locality where they are many (at 4K the index order's tile neighbourhoods win).
-    const uint64_t slots = (uint64_t)numCUs * (uint64_t)blend_waves_per_wg();
-    return (uint64_t)numTiles * blend_units_per_tile() < 8u * slots;
+    // costs L2 locality where they are many (at 4K the index order's tile neighbourhoods win):
+    // on below 4 units per slot.
+    const uint64_t slots = (uint64_t)numCUs * (uint64_t)blend_waves_per_wg(numTiles, numCUs);
+    return (uint64_t)numTiles * blend_units_per_tile() < 4u * slots;
 }
 
 void launch_unit_order(uint32_t numUnits, const DeviceArena& A, hipStream_t s) {
@@ -446,9 +649,23 @@ void launch_blend(const uint32_t* sortedVals, const FrameGeometry& g, const Devi
     const int flags = vec | ((pv && pv[0] == '0') ? 0 : 2);
     hipMemsetAsync(A.tileQueue, 0, sizeof(uint32_t), s);
     const int P = blend_pairs_per_lane();
-    const int waves = blend_waves_per_wg();
+    const int waves = blend_waves_per_wg(numTiles, numCUs);
     const char* ev = getenv("GSM_BLEND_EXECM");  // dead lanes: EXEC mask (default) or selects
     const bool execm = !(ev && ev[0] == '0');
+    const char* lv = getenv("GSM_BLEND_LANES");  // group-granular k_blend_lanes
+    if (lv && lv[0] == '1') {
+        uint32_t lgrid = (numTiles + (uint32_t)waves - 1) / (uint32_t)waves;
+        if (lgrid > (uint32_t)numCUs) lgrid = (uint32_t)numCUs;
+        if (waves == 16)
+            hipLaunchKernelGGL((k_blend_lanes<1024>), dim3(lgrid), dim3(1024), 0, s, A.tileStart, sortedVals, A.recA,
+                               A.recB, A.expTable, A.tileQueue, t0, numTiles, g.tilesX, g.width, g.height,
+                               (uint8_t*)color, colorPitch, (uint8_t*)depth, depthPitch, flags);
+        else
+            hipLaunchKernelGGL((k_blend_lanes<512>), dim3(lgrid), dim3(512), 0, s, A.tileStart, sortedVals, A.recA,
+                               A.recB, A.expTable, A.tileQueue, t0, numTiles, g.tilesX, g.width, g.height,
+                               (uint8_t*)color, colorPitch, (uint8_t*)depth, depthPitch, flags);
+        return;
+    }
     const uint32_t units = numTiles * (4u / (uint32_t)P);
     uint32_t grid = (units + (uint32_t)waves - 1) / (uint32_t)waves;
     if (grid > (uint32_t)numCUs) grid = (uint32_t)numCUs;

@@ -136,7 +136,11 @@ gsm_status GlobalRenderer::create(const gsm_renderer_config& cfg, int hipDevice,
         hipMemcpy(A.sincosTable, sc.data(), 65536 * sizeof(float2), hipMemcpyHostToDevice) != hipSuccess ||
         hipMemset(A.header, 0, sizeof(TileAssignmentHeader)) != hipSuccess ||
         hipMemset(A.tileStart, 0, ((size_t)r->tileCount_ + 1) * sizeof(uint32_t)) != hipSuccess ||
-        hipMemset(A.unitCost, 0, (size_t)r->tileCount_ * 4 * sizeof(uint16_t)) != hipSuccess) {
+        hipMemset(A.unitCost, 0, (size_t)r->tileCount_ * 4 * sizeof(uint16_t)) != hipSuccess ||
+        // every entry of the value buffers is a valid gaussian id at all times (the blend's
+        // clamped, unpredicated gathers may read entry 0 of an empty frame)
+        hipMemset(A.vals[0], 0, cap * sizeof(uint32_t)) != hipSuccess ||
+        hipMemset(A.vals[1], 0, cap * sizeof(uint32_t)) != hipSuccess) {
         delete r;
         return GSM_ERR_FAILED_TO_ALLOCATE_BUFFER;
     }
@@ -331,13 +335,6 @@ gsm_status GlobalRenderer::runFrame(hipStream_t s, const ProjectArgs& a, uint32_
     if (prof) hipEventRecord(ev[3], s);
     uint32_t* kb[2] = {arena_.keys[0], arena_.keys[1]};
     uint32_t* vb[2] = {arena_.vals[0], arena_.vals[1]};
-    const int res = radix_sort_pairs(kb, vb, &arena_.header->totalAssignments, maxAssignments_, 0,
-                                     sortPassCount(), arena_.radixHist, arena_.radixBinTotals, s);
-    sortedKeys_ = kb[res];
-    sortedVals_ = vb[res];
-    unsortedKeys_ = keep ? arena_.keysKeep : nullptr;
-    unsortedVals_ = keep ? arena_.valsKeep : nullptr;
-    if (prof) hipEventRecord(ev[4], s);
     FrameGeometry g;
     g.tilesX = tilesX_;
     g.tilesY = tilesY_;
@@ -347,7 +344,28 @@ gsm_status GlobalRenderer::runFrame(hipStream_t s, const ProjectArgs& a, uint32_
     g.width = width;
     g.height = height;
     g.maxAssignments = maxAssignments_;
-    launch_headers(sortedKeys_, g, arena_, s);
+    const char* segv = getenv("GSM_SORT_SEGMENTED");  // experiment: tile digits + per-tile depth sort
+    const bool segmented = segv && segv[0] == '1';
+    if (segmented) {
+        // tile digits only (stable: runs stay in assignment order), tile starts from the runs,
+        // then every tile's run sorted by depth in one workgroup
+        const int res = radix_sort_pairs(kb, vb, &arena_.header->totalAssignments, maxAssignments_, 2,
+                                         sortPassCount() - 2, arena_.radixHist, arena_.radixBinTotals, s);
+        launch_headers(kb[res], g, arena_, s);
+        tile_depth_sort(kb[res], vb[res], kb[res ^ 1], vb[res ^ 1], arena_.tileStart, rowBegin_ * tilesX_,
+                        (rowEnd_ - rowBegin_) * tilesX_, s);
+        sortedKeys_ = kb[res ^ 1];
+        sortedVals_ = vb[res ^ 1];
+    } else {
+        const int res = radix_sort_pairs(kb, vb, &arena_.header->totalAssignments, maxAssignments_, 0,
+                                         sortPassCount(), arena_.radixHist, arena_.radixBinTotals, s);
+        sortedKeys_ = kb[res];
+        sortedVals_ = vb[res];
+    }
+    unsortedKeys_ = keep ? arena_.keysKeep : nullptr;
+    unsortedVals_ = keep ? arena_.valsKeep : nullptr;
+    if (prof) hipEventRecord(ev[4], s);
+    if (!segmented) launch_headers(sortedKeys_, g, arena_, s);  // else done inside the sort
     arena_.blendTrace = (profiling_ & 4) ? traceBuf_ : nullptr;
     if (prof) hipEventRecord(ev[5], s);
     if (costOrder) hipStreamWaitEvent(s, evOrder_, 0);

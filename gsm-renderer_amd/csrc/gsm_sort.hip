@@ -256,3 +256,120 @@ int radix_sort_pairs(uint32_t* keys[2], uint32_t* vals[2], const uint32_t* nPtr,
 }
 
 }  // namespace gsm
+
+namespace gsm {
+
+// ---------------------------------------------------------------------------
+// Frame sort, second half: after the tile-digit passes the keys are grouped by tile, each
+// tile's run in assignment order; one workgroup per tile then sorts its run stably by the
+// 16-bit depth key.  Stable by construction: the LDS path sorts (depth << 16 | position)
+// with a bitonic network; runs longer than the LDS capacity take two LSD byte passes over
+// global memory within the workgroup.  The result equals the reference's 4-pass LSD sort of
+// (tile << 16 | depth) keys (SURVEY.md 8(a) determinism contract).
+// ---------------------------------------------------------------------------
+constexpr uint32_t kSegThreads = 256;
+constexpr uint32_t kSegCap = 8192;  // entries per tile sorted in LDS (32 KiB)
+
+__device__ void seg_radix_pass(const uint32_t* __restrict__ kin, const uint32_t* __restrict__ vin,
+                               uint32_t* __restrict__ kout, uint32_t* __restrict__ vout, uint32_t n,
+                               uint32_t shift, uint32_t* hist, uint32_t* wcnt) {
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    for (uint32_t i = tid; i < 256; i += kSegThreads) hist[i] = 0;
+    __syncthreads();
+    for (uint32_t i = tid; i < n; i += kSegThreads) atomicAdd(&hist[(kin[i] >> shift) & 0xFFu], 1u);
+    __syncthreads();
+    if (tid == 0) {  // exclusive scan of the 256 digit counts
+        uint32_t run = 0;
+        for (int d = 0; d < 256; ++d) {
+            const uint32_t c = hist[d];
+            hist[d] = run;
+            run += c;
+        }
+    }
+    __syncthreads();
+    const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    for (uint32_t base = 0; base < n; base += kSegThreads) {  // chunks in order: stable
+        const uint32_t i = base + tid;
+        const bool valid = i < n;
+        const uint32_t k = valid ? kin[i] : 0u, v = valid ? vin[i] : 0u;
+        const uint32_t d = (k >> shift) & 0xFFu;
+        const uint64_t peers = match_digit(d, valid);
+        for (uint32_t j = tid; j < 4 * 256; j += kSegThreads) wcnt[j] = 0;
+        __syncthreads();
+        if (valid && (peers & lt) == 0) wcnt[wave * 256 + d] = (uint32_t)__popcll(peers);
+        __syncthreads();
+        if (valid) {
+            uint32_t before = 0;
+            for (uint32_t w = 0; w < wave; ++w) before += wcnt[w * 256 + d];
+            const uint32_t pos = hist[d] + before + (uint32_t)__popcll(peers & lt);
+            kout[pos] = k;
+            vout[pos] = v;
+        }
+        __syncthreads();
+        for (uint32_t j = tid; j < 256; j += kSegThreads)
+            hist[j] += wcnt[j] + wcnt[256 + j] + wcnt[512 + j] + wcnt[768 + j];
+        __syncthreads();
+    }
+}
+
+__global__ __launch_bounds__(kSegThreads) void k_tile_depth_sort(
+    uint32_t* __restrict__ keysIn, uint32_t* __restrict__ valsIn, uint32_t* __restrict__ keysOut,
+    uint32_t* __restrict__ valsOut, const uint32_t* __restrict__ tileStart, uint32_t tileBegin) {
+    __shared__ uint32_t sk[kSegCap];
+    const uint32_t t = tileBegin + blockIdx.x;
+    const uint32_t start = tileStart[t];
+    const uint32_t n = tileStart[t + 1] - start;
+    if (n == 0) return;
+    const uint32_t tid = threadIdx.x;
+    uint32_t* kin = keysIn + start;
+    uint32_t* vin = valsIn + start;
+    uint32_t* kout = keysOut + start;
+    uint32_t* vout = valsOut + start;
+    if (n <= kSegCap) {
+        uint32_t np = 1;
+        while (np < n) np <<= 1;
+        for (uint32_t i = tid; i < np; i += kSegThreads)
+            sk[i] = i < n ? ((kin[i] & 0xFFFFu) << 16) | i : 0xFFFFFFFFu;
+        __syncthreads();
+        for (uint32_t k = 2; k <= np; k <<= 1)
+            for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+                for (uint32_t i = tid; i < np; i += kSegThreads) {
+                    const uint32_t ixj = i ^ j;
+                    if (ixj > i) {
+                        const uint32_t a = sk[i], b = sk[ixj];
+                        if ((a > b) == ((i & k) == 0)) {
+                            sk[i] = b;
+                            sk[ixj] = a;
+                        }
+                    }
+                }
+                __syncthreads();
+            }
+        const uint32_t tileBits = t << 16;
+        for (uint32_t i = tid; i < n; i += kSegThreads) {
+            const uint32_t c = sk[i];
+            kout[i] = tileBits | (c >> 16);
+            vout[i] = vin[c & 0xFFFFu];
+        }
+    } else {  // long run: low then high depth byte through global memory, then back to out
+        uint32_t* hist = sk;
+        uint32_t* wcnt = sk + 256;
+        seg_radix_pass(kin, vin, kout, vout, n, 0, hist, wcnt);
+        __syncthreads();
+        seg_radix_pass(kout, vout, kin, vin, n, 8, hist, wcnt);
+        __syncthreads();
+        for (uint32_t i = tid; i < n; i += kSegThreads) {
+            kout[i] = kin[i];
+            vout[i] = vin[i];
+        }
+    }
+}
+
+void tile_depth_sort(uint32_t* keysIn, uint32_t* valsIn, uint32_t* keysOut, uint32_t* valsOut,
+                     const uint32_t* tileStart, uint32_t tileBegin, uint32_t numTiles, hipStream_t s) {
+    if (numTiles == 0) return;
+    hipLaunchKernelGGL(k_tile_depth_sort, dim3(numTiles), dim3(kSegThreads), 0, s, keysIn, valsIn, keysOut,
+                       valsOut, tileStart, tileBegin);
+}
+
+}  // namespace gsm

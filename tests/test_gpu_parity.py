@@ -295,6 +295,18 @@ def test_partitioned_frame_matches_single_gpu(gsm, cuda, oracle, world, n, w, h,
         rend.close()
 
 
+def test_crowded_tiles_take_the_long_run_sort(gsm, cuda, oracle):
+    """Tiles whose list exceeds the per-tile LDS sort (8192 entries) go through the
+    workgroup's two global LSD passes; the frame must still match the oracle bit for bit."""
+    case = _synth(40_000, 320, 180, 4, 1, 5, spread=0.002, scale_px=0.8)
+    r = oracle_render(oracle, case)
+    hdr = r["headers"].reshape(-1, 2)
+    assert hdr[:, 1].max() > 8192, "scene must crowd a tile past the LDS capacity"
+    g = gpu_render(gsm, cuda, case)
+    assert_frame_equal(g, r)
+    g["renderer"].close()
+
+
 def test_stereo_is_unsupported_like_the_reference(gsm, cuda):
     rend = gsm.GlobalRenderer(config=gsm.RendererConfig(max_gaussians=16, max_width=64, max_height=32))
     x = cuda.zeros(16, dtype=cuda.uint8, device="cuda")

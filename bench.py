@@ -75,6 +75,9 @@ def main():
 
     c = scenes.CONFIGS[args.config]
     n, W, H, sh, prec = c["count"], c["width"], c["height"], c["sh"], c["precision"]
+    stereo = c.get("stereo")  # config 5: W is per eye, the target is 2W wide
+    if stereo and world_size > 1:
+        raise SystemExit("the stereo config runs on one GPU")
     world_np, harm_np, cam_d = scenes.gen_scene(n, W, H, sh, prec, seed=42)
     world = torch.from_numpy(world_np.view(np.uint8).reshape(-1).copy()).to(dev)
     harm = torch.from_numpy(harm_np.view(np.uint8).reshape(-1).copy()).to(dev)
@@ -87,10 +90,11 @@ def main():
     all_sl = slabs.all_slabs(tiles_y, H, world_size)
     if world_size > 1:
         renderer.set_tile_rows(slab.row_begin, slab.row_end)
-    pitch_c, pitch_d = W * 8, W * 2
+    TW = 2 * W if stereo else W  # target width
+    pitch_c, pitch_d = TW * 8, TW * 2
     # band buffers; the renderer addresses absolute rows, so hand it base - y0 * pitch
-    color = torch.zeros((slab.rows_padded, W, 4), dtype=torch.float16, device=dev)
-    depth = torch.zeros((slab.rows_padded, W), dtype=torch.float16, device=dev)
+    color = torch.zeros((slab.rows_padded, TW, 4), dtype=torch.float16, device=dev)
+    depth = torch.zeros((slab.rows_padded, TW), dtype=torch.float16, device=dev)
     cptr = color.data_ptr() - slab.y0 * pitch_c
     dptr = depth.data_ptr() - slab.y0 * pitch_d
     gather = [torch.empty_like(color) for _ in range(world_size)] if (world_size > 1 and rank == 0) else None
@@ -107,8 +111,15 @@ def main():
         send_counts = torch.zeros(world_size, dtype=torch.int32, device=dev)
         recv = torch.empty(max(n, 1) * exchange.RECORD_BYTES, dtype=torch.uint8, device=dev)
 
+    if stereo:
+        cam_l = gsm_amd.CameraParams.from_dict(scenes.make_camera(W, H, -stereo))
+        cam_r = gsm_amd.CameraParams.from_dict(scenes.make_camera(W, H, stereo))
+
     def step():
-        if alltoall:
+        if stereo:
+            renderer.render_stereo_sbs(cptr, dptr, inp, cam_l, cam_r, W, H, stream=stream,
+                                       color_pitch=pitch_c, depth_pitch=pitch_d)
+        elif alltoall:
             renderer.project_partition(inp, cam, W, H, first, cnt, rows, send, send_cap, send_counts,
                                        stream=stream)
             nrec = exchange.exchange(send, send_counts, recv, staged=backend != "nccl")
@@ -173,23 +184,25 @@ def main():
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import oracle as O  # CPU baseline + parity checker only
         threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+        views = [scenes.make_camera(W, H, -stereo), scenes.make_camera(W, H, stereo)] if stereo else [cam_d]
         times = []
-        ref = None
+        refs = None
         reps = 3 if args.cpu_baseline else 1
-        for _ in range(reps):
+        for _ in range(reps):  # one frame = every view (both eyes for config 5)
             t = time.perf_counter()
-            ref = O.render(world_np, harm_np, sh, cam_d, W, H, max_gaussians=n, nthreads=threads)
+            refs = [O.render(world_np, harm_np, sh, cv, W, H, max_gaussians=n, nthreads=threads) for cv in views]
             times.append(time.perf_counter() - t)
         if args.parity:
             got = color[:H].view(torch.int16).cpu().numpy().view(np.uint16)
-            parity = bool(np.array_equal(got, ref["color"])) and \
-                int(ref["total_assignments"]) == A
+            parity = all(bool(np.array_equal(got[:, v * W:(v + 1) * W], r["color"])) for v, r in enumerate(refs)) \
+                and int(refs[-1]["total_assignments"]) == A
         if args.cpu_baseline:
             med = float(np.median(times))
             cpu = {"value": 1.0 / med, "unit": "frames/s", "cores": threads, "kind": "port",
-                   "sample": f"{reps} full frames of {args.config} (1M gaussians, 1920x1080) with the "
-                             f"C oracle (oracle/gsm_oracle.c, pthreads), median {med:.2f} s/frame",
-                   "stages_s": {k: round(v, 4) for k, v in ref["times"].items()}}
+                   "sample": f"{reps} full frames of {args.config} ({n} gaussians, {len(views)} view(s) of "
+                             f"{W}x{H}) with the C oracle (oracle/gsm_oracle.c, pthreads), median "
+                             f"{med:.2f} s/frame",
+                   "stages_s": {k: round(v, 4) for k, v in refs[-1]["times"].items()}}
 
     out = {
         "metric": "frames/sec @ N Gaussians × W×H (1/2/4/8 GPU); sort Gkeys/s; blend HBM GB/s",
@@ -205,7 +218,8 @@ def main():
         "dtype": "fp16",
         "data": "synthetic",
         "config": {"workload": f"{args.config}: {n} gaussians SH{ {1: 0, 4: 1, 9: 2, 16: 3}[sh] } "
-                               f"{W}x{H} {'fp16 PackedWorldGaussianHalf' if prec else 'fp32 PackedWorldGaussian'}",
+                               f"{'2x' if stereo else ''}{W}x{H}{' side-by-side stereo' if stereo else ''} "
+                               f"{'fp16 PackedWorldGaussianHalf' if prec else 'fp32 PackedWorldGaussian'}",
                    "gaussians": n, "width": W, "height": H, "sh_components": sh,
                    "assignments": A, "tiles": T,
                    "parallelism": (f"dp{world_size} tile-row slabs, "

@@ -647,7 +647,7 @@ void launch_blend(const uint32_t* sortedVals, const FrameGeometry& g, const Devi
                         : 0;
     const char* pv = getenv("GSM_BLEND_PRIO");  // age-raised wave priority (default on)
     const int flags = vec | ((pv && pv[0] == '0') ? 0 : 2);
-    hipMemsetAsync(A.tileQueue, 0, sizeof(uint32_t), s);
+    // A.tileQueue was zeroed by k_scan_blocks earlier in the frame
     const int P = blend_pairs_per_lane();
     const int waves = blend_waves_per_wg(numTiles, numCUs);
     const char* ev = getenv("GSM_BLEND_EXECM");  // dead lanes: EXEC mask (default) or selects

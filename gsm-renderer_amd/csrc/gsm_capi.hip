@@ -114,6 +114,21 @@ gsm_status gsm_global_render_records(gsm_renderer* r, void* stream, const void* 
                                   depth, depth_pitch);
 }
 
+gsm_status gsm_global_render_stereo_sbs(gsm_renderer* r, void* stream, const gsm_gaussian_input* input,
+                                        const gsm_camera_params* left, const gsm_camera_params* right,
+                                        uint32_t width_per_eye, uint32_t height, void* color, size_t color_pitch,
+                                        void* depth, size_t depth_pitch) {
+    if (!r || !r->impl || !input || !left || !right) return GSM_ERR_INVALID_ARGUMENT;
+    if (!color) return GSM_ERR_MISSING_REQUIRED_BUFFER;
+    gsm_status st = r->impl->render((hipStream_t)stream, *input, *left, width_per_eye, height, color,
+                                    color_pitch, depth, depth_pitch);
+    if (st != GSM_OK) return st;
+    char* rc = (char*)color + (size_t)width_per_eye * 8;
+    char* rd = depth ? (char*)depth + (size_t)width_per_eye * 2 : nullptr;
+    return r->impl->render((hipStream_t)stream, *input, *right, width_per_eye, height, rc, color_pitch, rd,
+                           depth_pitch);
+}
+
 gsm_status gsm_global_render_stereo(gsm_renderer* r, void*, const gsm_gaussian_input*,
                                     const gsm_camera_params*, const gsm_camera_params*, uint32_t,
                                     uint32_t, void*, size_t, void*, size_t) {

@@ -788,7 +788,8 @@ __global__ __launch_bounds__(kProjectBlock) void k_records_in(
 constexpr int kScanThreads = 1024;
 __global__ __launch_bounds__(kScanThreads) void k_scan_blocks(uint32_t* __restrict__ sums,
                                                               uint32_t nb, uint32_t maxAssignments,
-                                                              TileAssignmentHeader* __restrict__ hdr) {
+                                                              TileAssignmentHeader* __restrict__ hdr,
+                                                              uint32_t* __restrict__ blendQueue) {
     __shared__ uint32_t lds[kScanThreads / 64];
     const uint32_t per = (nb + kScanThreads - 1) / kScanThreads;
     const uint32_t b0 = threadIdx.x * per;
@@ -820,6 +821,7 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_blocks(uint32_t* __restri
         hdr->maxCapacity = maxAssignments;
         hdr->paddedCount = ((tot + 1023u) / 1024u) * 1024u;
         hdr->overflow = ovf;
+        *blendQueue = 0;  // the blend's work counter for this frame (saves a memset launch)
     }
 }
 
@@ -973,7 +975,7 @@ void launch_records_in(const void* records, const ProjectArgs& a, const DeviceAr
 
 void launch_scan_blocks(uint32_t nb, const ProjectArgs& a, const DeviceArena& A, hipStream_t s) {
     hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(kScanThreads), 0, s, A.blockSums, nb,
-                       a.maxAssignments, A.header);
+                       a.maxAssignments, A.header, A.tileQueue);
 }
 
 void launch_scatter(const ProjectArgs& a, const DeviceArena& A, hipStream_t s) {

@@ -176,6 +176,9 @@ _SIGNATURES = {
     "gsm_global_render_stereo": ([C.c_void_p, C.c_void_p, C.POINTER(_Input), C.POINTER(_Camera),
                                   C.POINTER(_Camera), C.c_uint32, C.c_uint32, C.c_void_p, C.c_size_t,
                                   C.c_void_p, C.c_size_t], C.c_int),
+    "gsm_global_render_stereo_sbs": ([C.c_void_p, C.c_void_p, C.POINTER(_Input), C.POINTER(_Camera),
+                                      C.POINTER(_Camera), C.c_uint32, C.c_uint32, C.c_void_p, C.c_size_t,
+                                      C.c_void_p, C.c_size_t], C.c_int),
     "gsm_global_debug_read_total_assignments": ([C.c_void_p], C.c_uint32),
     "gsm_global_last_gpu_time": ([C.c_void_p, C.POINTER(C.c_double)], C.c_int),
     "gsm_global_debug_counters": ([C.c_void_p, C.POINTER(_Counters)], C.c_int),
@@ -326,6 +329,20 @@ class GlobalRenderer:
                                              C.byref(cr), int(width), int(height), _ptr(color_texture),
                                              int(width) * 16, _ptr(depth_texture), int(width) * 4)
         _check(st, "gsm_global_render_stereo")
+
+    def render_stereo_sbs(self, color_texture, depth_texture, input: GaussianInput, left: CameraParams,
+                          right: CameraParams, width_per_eye: int, height: int, stream=None,
+                          color_pitch: Optional[int] = None, depth_pitch: Optional[int] = None):
+        """gsm_global_render_stereo_sbs: both eyes into one side-by-side target (config 5)."""
+        inp = _Input(_ptr(input.gaussians), _ptr(input.harmonics), int(input.gaussian_count),
+                     int(input.sh_components))
+        cl, cr = _camera_struct(left), _camera_struct(right)
+        cp = color_pitch if color_pitch is not None else 2 * int(width_per_eye) * 8
+        dp = depth_pitch if depth_pitch is not None else 2 * int(width_per_eye) * 2
+        st = _lib().gsm_global_render_stereo_sbs(self._h, _stream_handle(stream), C.byref(inp), C.byref(cl),
+                                                 C.byref(cr), int(width_per_eye), int(height),
+                                                 _ptr(color_texture), cp, _ptr(depth_texture), dp)
+        _check(st, "gsm_global_render_stereo_sbs")
 
     def debug_read_total_assignments(self) -> int:
         return int(_lib().gsm_global_debug_read_total_assignments(self._h))

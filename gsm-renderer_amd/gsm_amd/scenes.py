@@ -92,4 +92,7 @@ CONFIGS = {
     "cfg1_50k_sh0_640x360_f32": dict(count=50_000, width=640, height=360, sh=1, precision=0),
     "cfg2_1m_sh3_1080p_f16": dict(count=1_000_000, width=1920, height=1080, sh=16, precision=1),
     "cfg3_5m_sh3_4k_f16": dict(count=5_000_000, width=3840, height=2160, sh=16, precision=1),
+    # config 5: two eyes of 1440x1600 side by side (width = per eye), +-32 mm x offsets
+    "cfg5_1m_sh2_stereo_2x1440x1600_f16": dict(count=1_000_000, width=1440, height=1600, sh=9, precision=1,
+                                               stereo=0.032),
 }

@@ -120,6 +120,19 @@ gsm_status gsm_global_render_stereo(gsm_renderer *renderer, void *stream,
                                     size_t color_pitch_bytes, void *depth_r16f,
                                     size_t depth_pitch_bytes);
 
+/* Config 5: both eyes of a stereo pair through the Global
+ * path into one side-by-side target -- left eye in columns [0, width_per_eye), right eye in
+ * [width_per_eye, 2 * width_per_eye) of rows of color_pitch bytes.  Each half equals
+ * gsm_global_render of that eye (the two views are independent Global frames; the
+ * DepthFirst renderer's shared-colour stereo semantics are not reproduced).  width_per_eye
+ * is bounded by config.max_width. */
+gsm_status gsm_global_render_stereo_sbs(gsm_renderer *renderer, void *stream,
+                                        const gsm_gaussian_input *input,
+                                        const gsm_camera_params *left, const gsm_camera_params *right,
+                                        uint32_t width_per_eye, uint32_t height, void *color_rgba16f,
+                                        size_t color_pitch_bytes, void *depth_r16f,
+                                        size_t depth_pitch_bytes);
+
 /* GlobalRenderer.debugReadTotalAssignments() (GlobalRenderer.swift:196-199): reads
  * the GPU counter; call after the frame's stream work has completed. */
 uint32_t gsm_global_debug_read_total_assignments(gsm_renderer *renderer);

@@ -307,6 +307,32 @@ def test_crowded_tiles_take_the_long_run_sort(gsm, cuda, oracle):
     g["renderer"].close()
 
 
+def test_stereo_side_by_side_halves_equal_mono_frames(gsm, cuda, oracle):
+    """Config 5 shape (SH2, two eyes side by side, +-32 mm): each half of the
+    gsm_global_render_stereo_sbs target equals the oracle frame of that eye, bit for bit."""
+    from gsm_amd import scenes
+    n, w, h = 30_000, 360, 400
+    world, harm, _ = scenes.gen_scene(n, w, h, 9, 1, seed=11)
+    cams = [scenes.make_camera(w, h, -0.032), scenes.make_camera(w, h, 0.032)]
+    refs = [oracle_render(oracle, dict(world=world, harm=harm, sh=9, cam=c, width=w, height=h,
+                                      max_gaussians=n)) for c in cams]
+    rend = gsm.GlobalRenderer(config=gsm.RendererConfig(max_gaussians=n, max_width=w, max_height=h, precision=1,
+                                                        gaussian_color_space=0))
+    color = cuda.full((h, 2 * w, 4), float("nan"), dtype=cuda.float16, device="cuda")
+    depth = cuda.full((h, 2 * w), float("nan"), dtype=cuda.float16, device="cuda")
+    inp = gsm.GaussianInput(to_dev(cuda, world), to_dev(cuda, harm), n, 9)
+    rend.render_stereo_sbs(color, depth, inp, gsm.CameraParams.from_dict(cams[0]),
+                           gsm.CameraParams.from_dict(cams[1]), w, h)
+    cuda.cuda.synchronize()
+    c = color.view(cuda.int16).cpu().numpy().view(np.uint16)
+    d = depth.view(cuda.int16).cpu().numpy().view(np.uint16)
+    for eye, r in enumerate(refs):
+        assert np.array_equal(c[:, eye * w:(eye + 1) * w], r["color"]), f"eye {eye}"
+        assert np.array_equal(d[:, eye * w:(eye + 1) * w], r["depth"]), f"eye {eye} depth"
+    assert not np.array_equal(refs[0]["color"], refs[1]["color"])  # the eyes do differ
+    rend.close()
+
+
 def test_stereo_is_unsupported_like_the_reference(gsm, cuda):
     rend = gsm.GlobalRenderer(config=gsm.RendererConfig(max_gaussians=16, max_width=64, max_height=32))
     x = cuda.zeros(16, dtype=cuda.uint8, device="cuda")

@@ -621,14 +621,12 @@ static int blend_waves_per_wg(uint32_t numTiles, int numCUs) {
 }
 
 bool blend_schedule_enabled(uint32_t numTiles, int numCUs) {
-    const char* v = getenv("GSM_BLEND_SCHED");  // 0 = index order, 1 = cost order, else auto
-    if (v && v[0] == '0') return false;
-    if (v && v[0] == '1') return true;
-    // Ordering by last frame's walks pays where units are few per wave slot (balance), and
-    // costs L2 locality where they are many (at 4K the index order's tile neighbourhoods win):
-    // on below 4 units per slot.
-    const uint64_t slots = (uint64_t)numCUs * (uint64_t)blend_waves_per_wg(numTiles, numCUs);
-    return (uint64_t)numTiles * blend_units_per_tile() < 4u * slots;
+    (void)numTiles;
+    (void)numCUs;
+    const char* v = getenv("GSM_BLEND_SCHED");  // 0 = index order; default: last frame's cost order
+    // Measured (events, µs): 1080p 8 waves 293 -> 248 with the order; 4K 16 waves 703 -> 660.
+    // (At 4K with 8 waves the order cost 4 % of L2 locality, but 4K runs 16 waves.)
+    return !(v && v[0] == '0');
 }
 
 void launch_unit_order(uint32_t numUnits, const DeviceArena& A, hipStream_t s) {

@@ -44,8 +44,8 @@ def main():
     st = r.stage_times_ms()
     tr = r.copy_buffer(gsm_amd.BufferId.BLEND_TRACE).astype(np.int64)
     hd = r.copy_buffer(gsm_amd.BufferId.HEADERS)
-    units = hd.shape[0] * 4
-    tr = tr[:units]
+    tr = tr[tr[:, 1] > 0]  # units of this frame (2 per tile at the default pairs-per-lane)
+    units = tr.shape[0]
     t0 = tr[:, 0].min()
     start = (tr[:, 0] - t0) * 10.0  # 100 MHz ticks -> ns
     end = (tr[:, 1] - t0) * 10.0

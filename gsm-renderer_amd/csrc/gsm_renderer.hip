@@ -289,7 +289,8 @@ template <class Front>
 gsm_status GlobalRenderer::runFrame(hipStream_t s, const ProjectArgs& a, uint32_t width, uint32_t height,
                                     void* color, size_t colorPitch, void* depth, size_t depthPitch,
                                     Front&& front) {
-    const bool prof = (profiling_ & 1) != 0;
+    const bool prof = (profiling_ & 1) != 0;         // every stage bracketed by events
+    const bool blendOnly = !prof && (profiling_ & 8) != 0;  // only the blend (2 events per frame)
     const bool keep = (profiling_ & 2) != 0;
     const uint32_t nb = (a.count + kProjectBlock - 1) / kProjectBlock;
     lastCount_ = a.count;
@@ -321,7 +322,7 @@ gsm_status GlobalRenderer::runFrame(hipStream_t s, const ProjectArgs& a, uint32_
         hipEventRecord(evOrder_, side_);
     }
 
-    hipEvent_t* ev = prof ? frameEvents(profFrames_) : nullptr;
+    hipEvent_t* ev = (prof || blendOnly) ? frameEvents(profFrames_) : nullptr;
     if (prof) hipEventRecord(ev[0], s);
     front(a);
     if (prof) hipEventRecord(ev[1], s);
@@ -367,11 +368,11 @@ gsm_status GlobalRenderer::runFrame(hipStream_t s, const ProjectArgs& a, uint32_
     if (prof) hipEventRecord(ev[4], s);
     if (!segmented) launch_headers(sortedKeys_, g, arena_, s);  // else done inside the sort
     arena_.blendTrace = (profiling_ & 4) ? traceBuf_ : nullptr;
-    if (prof) hipEventRecord(ev[5], s);
     if (costOrder) hipStreamWaitEvent(s, evOrder_, 0);
+    if (prof || blendOnly) hipEventRecord(ev[5], s);
     launch_blend(sortedVals_, g, arena_, color, colorPitch, depth, depthPitch, numCUs_, costOrder, s);
-    if (prof) hipEventRecord(ev[6], s);
-    if (prof) profFrames_++;
+    if (prof || blendOnly) hipEventRecord(ev[6], s);
+    if (prof || blendOnly) profFrames_++;
     haveTimes_ = profFrames_ > 0;
     if (hipGetLastError() != hipSuccess) return GSM_ERR_RENDER_FAILED;
     return GSM_OK;
@@ -385,7 +386,12 @@ gsm_status GlobalRenderer::stageTimes(float* ms, int n) {
         return GSM_ERR_RENDER_FAILED;
     const uint32_t frames = profFrames_ < (uint32_t)kEventRing ? profFrames_ : (uint32_t)kEventRing;
     const uint32_t first = profFrames_ - frames;
+    const bool blendOnly = (profiling_ & 1) == 0;  // bit 3: only the blend's pair of events exists
     for (int i = 0; i < n && i < GSM_STAGE_COUNT; ++i) {
+        if (blendOnly && i != GSM_STAGE_BLEND) {
+            ms[i] = 0.0f;
+            continue;
+        }
         double acc = 0.0;
         for (uint32_t f = first; f < profFrames_; ++f) {
             float t = 0.f;
@@ -399,7 +405,8 @@ gsm_status GlobalRenderer::stageTimes(float* ms, int n) {
 }
 
 gsm_status GlobalRenderer::lastGpuTime(double* seconds) {
-    if (!haveTimes_ || profFrames_ == 0) return GSM_ERR_RENDER_FAILED;
+    // the whole-frame span needs ev[0], which only the every-stage mode records
+    if (!haveTimes_ || profFrames_ == 0 || (profiling_ & 1) == 0) return GSM_ERR_RENDER_FAILED;
     hipSetDevice(device_);
     hipEvent_t* ev = frameEvents(profFrames_ - 1);
     if (hipEventSynchronize(ev[GSM_STAGE_COUNT]) != hipSuccess) return GSM_ERR_RENDER_FAILED;
@@ -507,7 +514,7 @@ gsm_status GlobalRenderer::setProfiling(int flags) {
         gsm_status st = alloc((void**)&traceBuf_, (size_t)tileCount_ * 4 * 4 * 8);
         if (st != GSM_OK) return st;
     }
-    if ((flags & 1) && events_.empty()) {
+    if ((flags & 9) && events_.empty()) {  // bit 0 (every stage) or bit 3 (blend only)
         events_.assign((size_t)kEventRing * (GSM_STAGE_COUNT + 1), nullptr);
         for (auto& e : events_)
             if (hipEventCreate(&e) != hipSuccess) return GSM_ERR_ENCODER_CREATION_FAILED;

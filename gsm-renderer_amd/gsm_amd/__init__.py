@@ -355,8 +355,9 @@ class GlobalRenderer:
 
     # -- introspection (include/gsm_debug.h) --
     def set_profiling(self, stage_events: bool = True, keep_unsorted: bool = False,
-                      blend_trace: bool = False):
-        flags = (1 if stage_events else 0) | (2 if keep_unsorted else 0) | (4 if blend_trace else 0)
+                      blend_trace: bool = False, blend_events: bool = False):
+        flags = (1 if stage_events else 0) | (2 if keep_unsorted else 0) | (4 if blend_trace else 0) | \
+            (8 if blend_events else 0)
         _check(_lib().gsm_global_set_profiling(self._h, flags), "gsm_global_set_profiling")
 
     def stage_times_ms(self) -> dict:

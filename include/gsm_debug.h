@@ -48,7 +48,8 @@ gsm_status gsm_global_debug_copy(gsm_renderer *renderer, int which, void *host_d
                                  size_t *needed);
 /* `enable` is a bit set: bit 0 brackets every stage by HIP events on the frame's stream,
  * bit 1 keeps the unsorted keys (GSM_BUF_KEYS/VALUES) for readback, bit 2 records a
- * per-unit blend trace (GSM_BUF_BLEND_TRACE).  Bits 1-2 cost time and memory. */
+ * per-unit blend trace (GSM_BUF_BLEND_TRACE), bit 3 (without bit 0) brackets only the blend
+ * (two events per frame; the other stages then report 0).  Every event costs frame time. */
 gsm_status gsm_global_set_profiling(gsm_renderer *renderer, int enable);
 
 enum {

@@ -345,13 +345,17 @@ gsm_status GlobalRenderer::runFrame(hipStream_t s, const ProjectArgs& a, uint32_
     g.width = width;
     g.height = height;
     g.maxAssignments = maxAssignments_;
-    const char* segv = getenv("GSM_SORT_SEGMENTED");  // experiment: tile digits + per-tile depth sort
-    const bool segmented = segv && segv[0] == '1';
-    if (segmented) {
-        // tile digits only (stable: runs stay in assignment order), tile starts from the runs,
-        // then every tile's run sorted by depth in one workgroup
-        const int res = radix_sort_pairs(kb, vb, &arena_.header->totalAssignments, maxAssignments_, 2,
-                                         sortPassCount() - 2, arena_.radixHist, arena_.radixBinTotals, s);
+    // Frame sort.  Default: a stable LSD sort by the tile field only
+    // (ceil(tileBits / 8) passes), tile starts from the runs, then each tile's run sorted
+    // stably by depth by one wave in LDS -- the same order as the reference's 4-pass sort of
+    // (tile << 16 | depth) keys.  GSM_SORT=radix4 keeps the 4 full 8-bit passes (A/B).
+    const char* sv = getenv("GSM_SORT");
+    const bool fullRadix = sv && std::strcmp(sv, "radix4") == 0;
+    if (!fullRadix) {
+        uint32_t tileBits = 1;
+        while (tileBits < 16 && (tileCount_ - 1u) >> tileBits) tileBits++;
+        const int res = radix_sort_bits(kb, vb, &arena_.header->totalAssignments, maxAssignments_, 16, tileBits,
+                                        arena_.radixHist, arena_.radixBinTotals, s);
         launch_headers(kb[res], g, arena_, s);
         tile_depth_sort(kb[res], vb[res], kb[res ^ 1], vb[res ^ 1], arena_.tileStart, rowBegin_ * tilesX_,
                         (rowEnd_ - rowBegin_) * tilesX_, s);
@@ -366,7 +370,7 @@ gsm_status GlobalRenderer::runFrame(hipStream_t s, const ProjectArgs& a, uint32_
     unsortedKeys_ = keep ? arena_.keysKeep : nullptr;
     unsortedVals_ = keep ? arena_.valsKeep : nullptr;
     if (prof) hipEventRecord(ev[4], s);
-    if (!segmented) launch_headers(sortedKeys_, g, arena_, s);  // else done inside the sort
+    if (fullRadix) launch_headers(sortedKeys_, g, arena_, s);  // else done inside the sort
     arena_.blendTrace = (profiling_ & 4) ? traceBuf_ : nullptr;
     if (costOrder) hipStreamWaitEvent(s, evOrder_, 0);
     if (prof || blendOnly) hipEventRecord(ev[5], s);

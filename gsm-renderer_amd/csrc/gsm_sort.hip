@@ -1,11 +1,12 @@
-// gsm_sort.hip -- stable LSD radix sort of (uint32 key, uint32 value) pairs for gfx950.
+// gsm_sort.hip -- stable LSD radix sort of (uint32 key, uint32 value) pairs for gfx950, and the
+// frame sort built from it.
 //
 // Replaces the reference's 5-kernel-per-digit Metal radix sort
 // (RadixSortEncoder.swift:41-214, GlobalShaders.metal:768-1028) with a
-// reduce-then-scan design for wave64:
-//   upsweep   : per-block 256-bin digit histogram (wave-aggregated LDS counters)
+// reduce-then-scan design for wave64, digits of BITS <= 8 bits:
+//   upsweep   : per-block 2^BITS-bin digit histogram (wave-aggregated LDS counters)
 //   scan      : one workgroup per digit scans its column over blocks
-//   downsweep : per 2048-key chunk, wave64 ballot-match ranking (8 ballots), LDS
+//   downsweep : per 4096-key chunk, wave64 ballot-match ranking (BITS ballots), LDS
 //               staging in digit order, coalesced run writes
 // The element count is read on the device (no host round trip, graph-capturable);
 // every block owns a contiguous range, so the sort is stable like the reference's.
@@ -29,11 +30,12 @@ __device__ __forceinline__ void block_range(uint32_t n, uint32_t grid, uint32_t 
     *end = (uint32_t)ee;
 }
 
-// 64-bit mask of the active lanes whose 8-bit digit equals this lane's.
+// 64-bit mask of the active lanes whose BITS-bit digit equals this lane's.
+template <int BITS>
 __device__ __forceinline__ uint64_t match_digit(uint32_t d, bool valid) {
     uint64_t peers = __ballot(valid);
 #pragma unroll
-    for (int bit = 0; bit < 8; ++bit) {
+    for (int bit = 0; bit < BITS; ++bit) {
         const bool set = (d >> bit) & 1u;
         const uint64_t m = __ballot(set);
         peers &= set ? m : ~m;
@@ -41,13 +43,15 @@ __device__ __forceinline__ uint64_t match_digit(uint32_t d, bool valid) {
     return peers;
 }
 
+template <int BITS>
 __global__ __launch_bounds__(kRadixBlock) void k_radix_upsweep(const uint32_t* __restrict__ keys,
                                                                const uint32_t* __restrict__ nPtr,
                                                                uint32_t shift,
                                                                uint32_t* __restrict__ hist) {
-    __shared__ uint32_t cnt[kWaves][256];
+    constexpr uint32_t R = 1u << BITS;
+    __shared__ uint32_t cnt[kWaves][R];
     const uint32_t wave = threadIdx.x >> 6;
-    for (int i = threadIdx.x; i < kWaves * 256; i += kRadixBlock) (&cnt[0][0])[i] = 0;
+    for (int i = threadIdx.x; i < kWaves * (int)R; i += kRadixBlock) (&cnt[0][0])[i] = 0;
     __syncthreads();
     uint32_t begin, end;
     block_range(*nPtr, gridDim.x, blockIdx.x, &begin, &end);
@@ -68,11 +72,11 @@ __global__ __launch_bounds__(kRadixBlock) void k_radix_upsweep(const uint32_t* _
             const uint32_t kk[4] = {q[i].x, q[i].y, q[i].z, q[i].w};
 #pragma unroll
             for (int c = 0; c < 4; ++c)  // per-wave LDS counters: one ds_add per key
-                if (idx + (uint32_t)c < end) atomicAdd(&cnt[wave][(kk[c] >> shift) & 0xFFu], 1u);
+                if (idx + (uint32_t)c < end) atomicAdd(&cnt[wave][(kk[c] >> shift) & (R - 1u)], 1u);
         }
     }
     __syncthreads();
-    for (int d = threadIdx.x; d < 256; d += kRadixBlock) {
+    for (uint32_t d = threadIdx.x; d < R; d += kRadixBlock) {
         uint32_t s = 0;
 #pragma unroll
         for (int w = 0; w < kWaves; ++w) s += cnt[w][d];
@@ -117,10 +121,13 @@ __global__ __launch_bounds__(256) void k_radix_scan(uint32_t* __restrict__ hist,
     if (threadIdx.x == 0) binTotals[d] = tot;
 }
 
+// Digits >= 2^BITS do not exist: their counters stay 0 (thread tid owns digit tid of 256).
+template <int BITS>
 __global__ __launch_bounds__(kRadixBlock) void k_radix_downsweep(
     const uint32_t* __restrict__ keysIn, const uint32_t* __restrict__ valsIn,
     uint32_t* __restrict__ keysOut, uint32_t* __restrict__ valsOut, const uint32_t* __restrict__ nPtr,
     uint32_t shift, const uint32_t* __restrict__ hist, const uint32_t* __restrict__ binTotals) {
+    constexpr uint32_t R = 1u << BITS;
     __shared__ uint32_t binBase[256];
     __shared__ uint32_t localStart[256];
     __shared__ uint32_t chunkTotal[256];
@@ -137,7 +144,7 @@ __global__ __launch_bounds__(kRadixBlock) void k_radix_downsweep(
 
     // global base of every digit for this block: exclusive scan over digits + block column offset
     {
-        const uint32_t t = binTotals[tid];
+        const uint32_t t = tid < R ? binTotals[tid] : 0u;
         uint32_t inc = t;
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) {
@@ -150,7 +157,7 @@ __global__ __launch_bounds__(kRadixBlock) void k_radix_downsweep(
 #pragma unroll
         for (int w = 0; w < kWaves; ++w)
             if ((uint32_t)w < wave) off += part[w];
-        binBase[tid] = off + inc - t + hist[(size_t)tid * gridDim.x + blockIdx.x];
+        binBase[tid] = off + inc - t + (tid < R ? hist[(size_t)tid * gridDim.x + blockIdx.x] : 0u);
 #pragma unroll
         for (int w = 0; w < kWaves; ++w) waveCnt[w][tid] = 0;
         __syncthreads();
@@ -171,8 +178,8 @@ __global__ __launch_bounds__(kRadixBlock) void k_radix_downsweep(
         for (int j = 0; j < kRadixItems; ++j) {
             const uint32_t idx = cbase + wave * (64 * kRadixItems) + j * 64 + lane;
             const bool valid = idx < end;
-            const uint32_t d = (k[j] >> shift) & 0xFFu;
-            const uint64_t peers = match_digit(d, valid);
+            const uint32_t d = (k[j] >> shift) & (R - 1u);
+            const uint64_t peers = match_digit<BITS>(d, valid);
             const uint32_t before = valid ? waveCnt[wave][d] : 0u;
             rank[j] = before + (uint32_t)__popcll(peers & lt);
             if (valid && (peers & lt) == 0) waveCnt[wave][d] = before + (uint32_t)__popcll(peers);
@@ -207,7 +214,7 @@ __global__ __launch_bounds__(kRadixBlock) void k_radix_downsweep(
         for (int j = 0; j < kRadixItems; ++j) {
             const uint32_t idx = cbase + wave * (64 * kRadixItems) + j * 64 + lane;
             if (idx < end) {
-                const uint32_t d = (k[j] >> shift) & 0xFFu;
+                const uint32_t d = (k[j] >> shift) & (R - 1u);
                 const uint32_t pos = localStart[d] + waveCnt[wave][d] + rank[j];
                 sKeys[pos] = k[j];
                 sVals[pos] = v[j];
@@ -217,7 +224,7 @@ __global__ __launch_bounds__(kRadixBlock) void k_radix_downsweep(
         const uint32_t cn = min((uint32_t)kRadixChunk, end - cbase);
         for (uint32_t p = tid; p < cn; p += kRadixBlock) {
             const uint32_t key = sKeys[p];
-            const uint32_t d = (key >> shift) & 0xFFu;
+            const uint32_t d = (key >> shift) & (R - 1u);
             const uint32_t dst = binBase[d] + (p - localStart[d]);
             keysOut[dst] = key;
             valsOut[dst] = sVals[p];
@@ -238,18 +245,50 @@ uint32_t radix_grid_for_capacity(uint32_t capacity) {
     return g;
 }
 
+static void radix_pass(uint32_t* kin, uint32_t* vin, uint32_t* kout, uint32_t* vout, const uint32_t* nPtr,
+                       uint32_t grid, uint32_t shift, int bits, uint32_t* hist, uint32_t* binTotals,
+                       hipStream_t s) {
+#define GSM_RADIX_PASS(B)                                                                                   \
+    hipLaunchKernelGGL(k_radix_upsweep<B>, dim3(grid), dim3(kRadixBlock), 0, s, kin, nPtr, shift, hist);    \
+    hipLaunchKernelGGL(k_radix_scan, dim3(1u << B), dim3(256), 0, s, hist, grid, binTotals);               \
+    hipLaunchKernelGGL(k_radix_downsweep<B>, dim3(grid), dim3(kRadixBlock), 0, s, kin, vin, kout, vout, nPtr, \
+                       shift, hist, binTotals)
+    switch (bits) {
+        case 4: GSM_RADIX_PASS(4); break;
+        case 5: GSM_RADIX_PASS(5); break;
+        case 6: GSM_RADIX_PASS(6); break;
+        case 7: GSM_RADIX_PASS(7); break;
+        default: GSM_RADIX_PASS(8); break;
+    }
+#undef GSM_RADIX_PASS
+}
+
 int radix_sort_pairs(uint32_t* keys[2], uint32_t* vals[2], const uint32_t* nPtr, uint32_t capacity,
                      int firstDigit, int numDigits, uint32_t* hist, uint32_t* binTotals,
                      hipStream_t s) {
     const uint32_t grid = radix_grid_for_capacity(capacity);
     int cur = 0;
     for (int dgt = firstDigit; dgt < firstDigit + numDigits; ++dgt) {
-        const uint32_t shift = (uint32_t)dgt * 8u;
-        hipLaunchKernelGGL(k_radix_upsweep, dim3(grid), dim3(kRadixBlock), 0, s, keys[cur], nPtr,
-                           shift, hist);
-        hipLaunchKernelGGL(k_radix_scan, dim3(256), dim3(256), 0, s, hist, grid, binTotals);
-        hipLaunchKernelGGL(k_radix_downsweep, dim3(grid), dim3(kRadixBlock), 0, s, keys[cur],
-                           vals[cur], keys[cur ^ 1], vals[cur ^ 1], nPtr, shift, hist, binTotals);
+        radix_pass(keys[cur], vals[cur], keys[cur ^ 1], vals[cur ^ 1], nPtr, grid, (uint32_t)dgt * 8u, 8, hist,
+                   binTotals, s);
+        cur ^= 1;
+    }
+    return cur;
+}
+
+int radix_sort_bits(uint32_t* keys[2], uint32_t* vals[2], const uint32_t* nPtr, uint32_t capacity,
+                    uint32_t shift, uint32_t bits, uint32_t* hist, uint32_t* binTotals, hipStream_t s) {
+    const uint32_t grid = radix_grid_for_capacity(capacity);
+    const uint32_t passes = (bits + 7) / 8;
+    int cur = 0;
+    uint32_t done = 0;
+    for (uint32_t p = 0; p < passes; ++p) {
+        // near-equal digit widths; a digit wider than the bits left reads zero bits above the field
+        uint32_t b = (bits - done + (passes - p) - 1) / (passes - p);
+        if (b < 4) b = 4;
+        radix_pass(keys[cur], vals[cur], keys[cur ^ 1], vals[cur ^ 1], nPtr, grid, shift + done, (int)b, hist,
+                   binTotals, s);
+        done += b;
         cur ^= 1;
     }
     return cur;
@@ -260,107 +299,176 @@ int radix_sort_pairs(uint32_t* keys[2], uint32_t* vals[2], const uint32_t* nPtr,
 namespace gsm {
 
 // ---------------------------------------------------------------------------
-// Frame sort, second half: after the tile-digit passes the keys are grouped by tile, each
-// tile's run in assignment order; one workgroup per tile then sorts its run stably by the
-// 16-bit depth key.  Stable by construction: the LDS path sorts (depth << 16 | position)
-// with a bitonic network; runs longer than the LDS capacity take two LSD byte passes over
-// global memory within the workgroup.  The result equals the reference's 4-pass LSD sort of
-// (tile << 16 | depth) keys (SURVEY.md 8(a) determinism contract).
-// ---------------------------------------------------------------------------
-constexpr uint32_t kSegThreads = 256;
-constexpr uint32_t kSegCap = 8192;  // entries per tile sorted in LDS (32 KiB)
+// Frame sort, second half.  After the tile-digit passes the assignments are grouped by tile,
+// each tile's run in assignment order (ascending gaussian id, SURVEY.md 8(a) determinism
+// contract); sorting every run stably by its 16-bit depth key then gives exactly the
+// reference's 4-pass LSD order of (tile << 16 | depth) keys (RadixSortEncoder.swift:41-101).
+//
+// k_tile_sort: one workgroup per tile, runs of up to kTsCap entries held 8 per thread.  Two
+// 8-bit LSD passes over the depth key.  Wave w owns a contiguous segment of the run and ranks
+// its items in order against per-wave LDS digit counters (ballot match, no barrier inside the
+// segment); one scan over (digit, wave) then turns the local ranks into positions -- the
+// downsweep of the global sort with a single chunk, so the order is stable.  Pass 1 scatters
+// (depth << 16 | position-in-run) words into LDS; pass 2 scatters the rebuilt keys and the
+// values gathered by the position field into the output run.  Longer runs (rare) take the
+// same passes through global memory in chunks of 256.
+constexpr uint32_t kTsThreads = 256;
+constexpr uint32_t kTsItems = 8;
+constexpr uint32_t kTsCap = kTsThreads * kTsItems;  // 2048 entries per tile in LDS
 
-__device__ void seg_radix_pass(const uint32_t* __restrict__ kin, const uint32_t* __restrict__ vin,
-                               uint32_t* __restrict__ kout, uint32_t* __restrict__ vout, uint32_t n,
-                               uint32_t shift, uint32_t* hist, uint32_t* wcnt) {
-    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    for (uint32_t i = tid; i < 256; i += kSegThreads) hist[i] = 0;
+// Lanes of one wave hand LDS words to each other below.  The hardware keeps a wave's LDS
+// operations in order, but the language does not: without this (no instruction) the compiler
+// may forward a lane's own earlier store past another lane's update.
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Thread tid owns digit tid: exclusive scan over (digit, wave) of the counts in wcnt, in place.
+__device__ __forceinline__ void ts_offsets(uint32_t (*wcnt)[256], uint32_t* part) {
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+    const uint32_t c0 = wcnt[0][tid], c1 = wcnt[1][tid], c2 = wcnt[2][tid], c3 = wcnt[3][tid];
+    const uint32_t tot = c0 + c1 + c2 + c3;
+    uint32_t inc = tot;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t t = __shfl_up(inc, o, 64);
+        if (lane >= (uint32_t)o) inc += t;
+    }
+    if (lane == 63) part[wave] = inc;
     __syncthreads();
-    for (uint32_t i = tid; i < n; i += kSegThreads) atomicAdd(&hist[(kin[i] >> shift) & 0xFFu], 1u);
+    uint32_t off = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < 4; ++w)
+        if (w < wave) off += part[w];
+    const uint32_t e = off + inc - tot;
+    wcnt[0][tid] = e;
+    wcnt[1][tid] = e + c0;
+    wcnt[2][tid] = e + c0 + c1;
+    wcnt[3][tid] = e + c0 + c1 + c2;
     __syncthreads();
-    if (tid == 0) {  // exclusive scan of the 256 digit counts
-        uint32_t run = 0;
-        for (int d = 0; d < 256; ++d) {
-            const uint32_t c = hist[d];
-            hist[d] = run;
-            run += c;
+}
+
+// one pass: pos[j] = destination of item j (items of wave w at seg + j*64 + lane)
+__device__ __forceinline__ void ts_rank_pass(const uint32_t (&x)[kTsItems], uint32_t (&pos)[kTsItems], uint32_t E,
+                                             uint32_t seg, uint32_t n, uint32_t shift, uint32_t (*wcnt)[256],
+                                             uint32_t* part) {
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+    const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    uint32_t* cnt = wcnt[wave];
+#pragma unroll
+    for (uint32_t j = 0; j < kTsItems; ++j) {
+        if (j < E) {
+            const bool valid = seg + j * 64u + lane < n;
+            const uint32_t d = (x[j] >> shift) & 0xFFu;
+            const uint64_t peers = match_digit<8>(d, valid);
+            const uint32_t before = cnt[d];
+            if (valid && (peers & lt) == 0) cnt[d] = before + (uint32_t)__popcll(peers);
+            wave_sync();
+            pos[j] = before + (uint32_t)__popcll(peers & lt);
         }
     }
     __syncthreads();
+    ts_offsets(wcnt, part);
+#pragma unroll
+    for (uint32_t j = 0; j < kTsItems; ++j)
+        if (j < E) pos[j] += cnt[(x[j] >> shift) & 0xFFu];
+}
+
+// one stable 8-bit LSD pass of a run of n (key, value) pairs by the workgroup, in -> out (global)
+__device__ void ts_pass_global(const uint32_t* __restrict__ kin, const uint32_t* __restrict__ vin,
+                               uint32_t* __restrict__ kout, uint32_t* __restrict__ vout, uint32_t n,
+                               uint32_t shift, uint32_t (*wcnt)[256], uint32_t* part, uint32_t* carry) {
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
     const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-    for (uint32_t base = 0; base < n; base += kSegThreads) {  // chunks in order: stable
-        const uint32_t i = base + tid;
+    // digit starts over the whole run
+#pragma unroll
+    for (uint32_t w = 0; w < 4; ++w) wcnt[w][tid] = 0;
+    __syncthreads();
+    for (uint32_t i = tid; i < n; i += kTsThreads) atomicAdd(&wcnt[0][(kin[i] >> shift) & 0xFFu], 1u);
+    __syncthreads();
+    ts_offsets(wcnt, part);
+    carry[tid] = wcnt[0][tid];
+    __syncthreads();
+    for (uint32_t b = 0; b < n; b += kTsThreads) {  // chunks of 256 in order: stable
+        const uint32_t i = b + tid;
         const bool valid = i < n;
         const uint32_t k = valid ? kin[i] : 0u, v = valid ? vin[i] : 0u;
         const uint32_t d = (k >> shift) & 0xFFu;
-        const uint64_t peers = match_digit(d, valid);
-        for (uint32_t j = tid; j < 4 * 256; j += kSegThreads) wcnt[j] = 0;
+        const uint64_t peers = match_digit<8>(d, valid);
+#pragma unroll
+        for (uint32_t w = 0; w < 4; ++w) wcnt[w][tid] = 0;
         __syncthreads();
-        if (valid && (peers & lt) == 0) wcnt[wave * 256 + d] = (uint32_t)__popcll(peers);
+        if (valid && (peers & lt) == 0) wcnt[wave][d] = (uint32_t)__popcll(peers);
         __syncthreads();
         if (valid) {
-            uint32_t before = 0;
-            for (uint32_t w = 0; w < wave; ++w) before += wcnt[w * 256 + d];
-            const uint32_t pos = hist[d] + before + (uint32_t)__popcll(peers & lt);
-            kout[pos] = k;
-            vout[pos] = v;
+            uint32_t before = carry[d];
+            for (uint32_t w = 0; w < wave; ++w) before += wcnt[w][d];
+            const uint32_t p = before + (uint32_t)__popcll(peers & lt);
+            kout[p] = k;
+            vout[p] = v;
         }
         __syncthreads();
-        for (uint32_t j = tid; j < 256; j += kSegThreads)
-            hist[j] += wcnt[j] + wcnt[256 + j] + wcnt[512 + j] + wcnt[768 + j];
+        carry[tid] += wcnt[0][tid] + wcnt[1][tid] + wcnt[2][tid] + wcnt[3][tid];
         __syncthreads();
     }
 }
 
-__global__ __launch_bounds__(kSegThreads) void k_tile_depth_sort(
+__global__ __launch_bounds__(kTsThreads) void k_tile_sort(
     uint32_t* __restrict__ keysIn, uint32_t* __restrict__ valsIn, uint32_t* __restrict__ keysOut,
     uint32_t* __restrict__ valsOut, const uint32_t* __restrict__ tileStart, uint32_t tileBegin) {
-    __shared__ uint32_t sk[kSegCap];
+    __shared__ __attribute__((aligned(16))) uint32_t buf[kTsCap];
+    __shared__ __attribute__((aligned(16))) uint32_t wcnt[4][256];
+    __shared__ uint32_t part[4];
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
     const uint32_t t = tileBegin + blockIdx.x;
     const uint32_t start = tileStart[t];
     const uint32_t n = tileStart[t + 1] - start;
-    if (n == 0) return;
-    const uint32_t tid = threadIdx.x;
-    uint32_t* kin = keysIn + start;
-    uint32_t* vin = valsIn + start;
+    if (n == 0) return;  // uniform: the whole workgroup leaves
+    if (n > kTsCap) {  // rare: the same two passes streamed through global memory
+        ts_pass_global(keysIn + start, valsIn + start, keysOut + start, valsOut + start, n, 0, wcnt, part, buf);
+        ts_pass_global(keysOut + start, valsOut + start, keysIn + start, valsIn + start, n, 8, wcnt, part, buf);
+        for (uint32_t i = tid; i < n; i += kTsThreads) {
+            keysOut[start + i] = keysIn[start + i];
+            valsOut[start + i] = valsIn[start + i];
+        }
+        return;
+    }
+    const uint32_t* kin = keysIn + start;
+    const uint32_t* vin = valsIn + start;
+    const uint32_t E = (n + kTsThreads - 1) / kTsThreads;  // items per thread
+    const uint32_t seg = wave * 64u * E;                    // this wave's segment of the run
+    uint32_t x[kTsItems], pos[kTsItems];
+    // all of the run's keys in flight at once; word = depth << 16 | position in the run
+#pragma unroll
+    for (uint32_t j = 0; j < kTsItems; ++j) {
+        const uint32_t i = seg + j * 64u + lane;
+        x[j] = (j < E && i < n) ? ((kin[i] & 0xFFFFu) << 16) | i : 0u;
+    }
+#pragma unroll
+    for (uint32_t w = 0; w < 4; ++w) wcnt[w][tid] = 0;
+    __syncthreads();
+    ts_rank_pass(x, pos, E, seg, n, 16, wcnt, part);  // low depth byte
+#pragma unroll
+    for (uint32_t j = 0; j < kTsItems; ++j)
+        if (j < E && seg + j * 64u + lane < n) buf[pos[j]] = x[j];
+    __syncthreads();
+#pragma unroll
+    for (uint32_t j = 0; j < kTsItems; ++j)
+        if (j < E) x[j] = seg + j * 64u + lane < n ? buf[seg + j * 64u + lane] : 0u;
+#pragma unroll
+    for (uint32_t w = 0; w < 4; ++w) wcnt[w][tid] = 0;
+    __syncthreads();
+    ts_rank_pass(x, pos, E, seg, n, 24, wcnt, part);  // high depth byte
     uint32_t* kout = keysOut + start;
     uint32_t* vout = valsOut + start;
-    if (n <= kSegCap) {
-        uint32_t np = 1;
-        while (np < n) np <<= 1;
-        for (uint32_t i = tid; i < np; i += kSegThreads)
-            sk[i] = i < n ? ((kin[i] & 0xFFFFu) << 16) | i : 0xFFFFFFFFu;
-        __syncthreads();
-        for (uint32_t k = 2; k <= np; k <<= 1)
-            for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-                for (uint32_t i = tid; i < np; i += kSegThreads) {
-                    const uint32_t ixj = i ^ j;
-                    if (ixj > i) {
-                        const uint32_t a = sk[i], b = sk[ixj];
-                        if ((a > b) == ((i & k) == 0)) {
-                            sk[i] = b;
-                            sk[ixj] = a;
-                        }
-                    }
-                }
-                __syncthreads();
-            }
-        const uint32_t tileBits = t << 16;
-        for (uint32_t i = tid; i < n; i += kSegThreads) {
-            const uint32_t c = sk[i];
-            kout[i] = tileBits | (c >> 16);
-            vout[i] = vin[c & 0xFFFFu];
-        }
-    } else {  // long run: low then high depth byte through global memory, then back to out
-        uint32_t* hist = sk;
-        uint32_t* wcnt = sk + 256;
-        seg_radix_pass(kin, vin, kout, vout, n, 0, hist, wcnt);
-        __syncthreads();
-        seg_radix_pass(kout, vout, kin, vin, n, 8, hist, wcnt);
-        __syncthreads();
-        for (uint32_t i = tid; i < n; i += kSegThreads) {
-            kout[i] = kin[i];
-            vout[i] = vin[i];
+    const uint32_t tileBits = t << 16;
+#pragma unroll
+    for (uint32_t j = 0; j < kTsItems; ++j) {
+        if (j < E && seg + j * 64u + lane < n) {
+            kout[pos[j]] = tileBits | (x[j] >> 16);
+            vout[pos[j]] = vin[x[j] & 0xFFFFu];
         }
     }
 }
@@ -368,8 +476,8 @@ __global__ __launch_bounds__(kSegThreads) void k_tile_depth_sort(
 void tile_depth_sort(uint32_t* keysIn, uint32_t* valsIn, uint32_t* keysOut, uint32_t* valsOut,
                      const uint32_t* tileStart, uint32_t tileBegin, uint32_t numTiles, hipStream_t s) {
     if (numTiles == 0) return;
-    hipLaunchKernelGGL(k_tile_depth_sort, dim3(numTiles), dim3(kSegThreads), 0, s, keysIn, valsIn, keysOut,
-                       valsOut, tileStart, tileBegin);
+    hipLaunchKernelGGL(k_tile_sort, dim3(numTiles), dim3(kTsThreads), 0, s, keysIn, valsIn, keysOut, valsOut,
+                       tileStart, tileBegin);
 }
 
 }  // namespace gsm

@@ -296,8 +296,8 @@ def test_partitioned_frame_matches_single_gpu(gsm, cuda, oracle, world, n, w, h,
 
 
 def test_crowded_tiles_take_the_long_run_sort(gsm, cuda, oracle):
-    """Tiles whose list exceeds the per-tile LDS sort (8192 entries) go through the
-    workgroup's two global LSD passes; the frame must still match the oracle bit for bit."""
+    """Tiles whose list exceeds the per-tile LDS sort (2048 entries per wave) go through the
+    wave's two global LSD passes; the frame must still match the oracle bit for bit."""
     case = _synth(40_000, 320, 180, 4, 1, 5, spread=0.002, scale_px=0.8)
     r = oracle_render(oracle, case)
     hdr = r["headers"].reshape(-1, 2)

@@ -162,7 +162,7 @@ __global__ __launch_bounds__(NT) void k_blend_px(
 
             h2 ac[U][P], om[U][P];
             uint32_t rgc[U], bdc[U], rgn[U], bdn[U], opn[U];
-            uint32_t eln[U][P], ehn[U][P];  // next group's exp table words
+            u16x2 en[U][P];  // next group's exp table words (d16 loads into both halves)
             bool alive = true;
             // p = ((dx*dx)*cxx + (dy*dy)*cyy) + (dx*dy)*cxy2 (GlobalShaders.metal:1115-1122);
             // the dy terms are shared by the pairs of a row
@@ -216,8 +216,8 @@ __global__ __launch_bounds__(NT) void k_blend_px(
                                 // raw table words: first used in stage 3, after the current
                                 // group's blend, so the LDS latency hides behind it
                                 const uint32_t pb = as_u32(pq[q]);
-                                eln[k][q] = tbl[pb & 0xFFFFu];
-                                ehn[k][q] = tbl[pb >> 16];
+                                en[k][q].x = tbl[pb & 0xFFFFu];
+                                en[k][q].y = tbl[pb >> 16];
                             }
                         }
                     }
@@ -277,7 +277,7 @@ __global__ __launch_bounds__(NT) void k_blend_px(
                     for (uint32_t k = 0; k < U; ++k) {
 #pragma unroll
                         for (int q = 0; q < P; ++q) {
-                            const h2 ek = as_h2(eln[k][q] | (ehn[k][q] << 16));
+                            const h2 ek = __builtin_bit_cast(h2, en[k][q]);
                             ac[k][q] = __builtin_elementwise_min(splat_hi(as_h2(opn[k])) * ek, C099);
                             om[k][q] = ONE - ac[k][q];
                         }

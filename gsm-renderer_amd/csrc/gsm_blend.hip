@@ -52,7 +52,7 @@ __device__ __forceinline__ uint32_t quad_max_u32(uint32_t v) {
 // groups of U = 4/P entries through a three-stage software pipeline (stage 1: next group's
 // p and table reads; stage 2: blend this group; stage 3: next group's alphas).
 // ---------------------------------------------------------------------------
-template <int NT, int P, bool EXECM>
+template <int NT, int P, bool EXECM, int EXPT = 0>
 __global__ __launch_bounds__(NT) void k_blend_px(
     const uint32_t* __restrict__ tileStart, const uint32_t* __restrict__ sortedVals,
     const BlendRecordA* __restrict__ recA, const uint32_t* __restrict__ recB,
@@ -216,8 +216,12 @@ __global__ __launch_bounds__(NT) void k_blend_px(
                                 // raw table words: first used in stage 3, after the current
                                 // group's blend, so the LDS latency hides behind it
                                 const uint32_t pb = as_u32(pq[q]);
-                                en[k][q].x = tbl[pb & 0xFFFFu];
-                                en[k][q].y = tbl[pb >> 16];
+                                if (EXPT == 1) {  // timing experiment: no table reads (wrong image)
+                                    en[k][q] = __builtin_bit_cast(u16x2, pb ^ 0x55555555u);
+                                } else {
+                                    en[k][q].x = tbl[pb & 0xFFFFu];
+                                    en[k][q].y = tbl[pb >> 16];
+                                }
                             }
                         }
                     }
@@ -237,7 +241,7 @@ __global__ __launch_bounds__(NT) void k_blend_px(
                             const uint32_t o = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)gm, 0xB1, 0xF, 0xF, false);
                             gm = max(gm, o);
                         }
-                        alive = alive && !(gm < thrBits);  // T >= 0: fp16 order == bit order
+                        alive = alive && (EXPT == 2 || !(gm < thrBits));  // T >= 0: fp16 order == bit order
                         const h2 rgv = as_h2(rgc[k]), bdv = as_h2(bdc[k]);
                         // a dead lane keeps T and C (alpha 0 would give the same bits: C + c*0 == C,
                         // T*1 == T): EXECM runs the updates under an EXEC mask of the live lanes,
@@ -668,10 +672,10 @@ void launch_blend(const uint32_t* sortedVals, const FrameGeometry& g, const Devi
     uint32_t grid = (units + (uint32_t)waves - 1) / (uint32_t)waves;
     if (grid > (uint32_t)numCUs) grid = (uint32_t)numCUs;
 #define GSM_LAUNCH_PX(NTH, PP)                                                                      \
-    if (execm) GSM_LAUNCH_PXE(NTH, PP, true);                                                         \
-    else GSM_LAUNCH_PXE(NTH, PP, false)
-#define GSM_LAUNCH_PXE(NTH, PP, EM)                                                                 \
-    hipLaunchKernelGGL((k_blend_px<NTH, PP, EM>), dim3(grid), dim3(NTH), 0, s, A.tileStart, sortedVals, \
+    if (execm) GSM_LAUNCH_PXE(NTH, PP, true, 0);                                                      \
+    else GSM_LAUNCH_PXE(NTH, PP, false, 0)
+#define GSM_LAUNCH_PXE(NTH, PP, EM, X)                                                              \
+    hipLaunchKernelGGL((k_blend_px<NTH, PP, EM, X>), dim3(grid), dim3(NTH), 0, s, A.tileStart, sortedVals, \
                        A.recA, A.recB, A.expTable, A.tileQueue, t0, numTiles, g.tilesX, g.width,    \
                        g.height, (uint8_t*)color, colorPitch, (uint8_t*)depth, depthPitch, flags,    \
                        costOrder ? A.unitOrder : nullptr, A.unitCost, A.blendTrace)
@@ -679,6 +683,12 @@ void launch_blend(const uint32_t* sortedVals, const FrameGeometry& g, const Devi
     if (P == 1) GSM_LAUNCH_PX(NTH, 1);       \
     else if (P == 4) GSM_LAUNCH_PX(NTH, 4);  \
     else GSM_LAUNCH_PX(NTH, 2)
+    const char* xv = getenv("GSM_BLEND_EXPT");  // timing experiments (wrong images): 1 no table, 2 no break
+    if (xv && (xv[0] == '1' || xv[0] == '2') && P == 2 && waves == 8 && execm) {
+        if (xv[0] == '1') GSM_LAUNCH_PXE(512, 2, true, 1);
+        else GSM_LAUNCH_PXE(512, 2, true, 2);
+        return;
+    }
     if (waves == 16) {
         GSM_LAUNCH_P(1024);
     } else {

@@ -15,6 +15,10 @@ struct ProjectArgs {
     uint32_t rowBegin, rowEnd;  // slab of tile rows; full frame = [0, tilesY)
     uint32_t count;
     uint32_t maxAssignments;
+    // per-frame constants of projectCovariance2D / stabilizeCovariance2D / computeDepthFactor,
+    // evaluated once on the host with the same IEEE fp32 operations the kernels would repeat
+    // per gaussian (GaussianShared.h:326-375, 655-714, 275-278)
+    float limX, limY, focalX, focalY, maxEig, adjFar, adjDen;
 };
 
 // Multi-GPU partition: tile-row boundaries of the slabs, and the 48-byte

@@ -286,11 +286,20 @@ struct ProjOut {
     bool vis, countable;
 };
 
+// fp16(float(c) / 255) for c = 0..255 (getColor/getOpacity, GlobalShaders.metal:9-15), one
+// entry per thread of the block; callers use it after the barrier
+static_assert(kProjectBlock == 256, "one div255 entry per thread");
+__device__ __forceinline__ void fill_div255(uint16_t* div255) {
+    div255[threadIdx.x] = f_to_hbits((float)threadIdx.x / 255.0f);
+    __syncthreads();
+}
+
 template <bool HALF, int DEG>
 __device__ __forceinline__ ProjOut project_gaussian(const void* __restrict__ world,
                                                     const void* __restrict__ harm, uint32_t gid,
                                                     const ProjectArgs& P,
-                                                    const float2* __restrict__ sincos) {
+                                                    const float2* __restrict__ sincos,
+                                                    const uint16_t* div255) {
     ProjOut o;
     o.vis = false;
     o.countable = false;
@@ -383,13 +392,10 @@ __device__ __forceinline__ ProjOut project_gaussian(const void* __restrict__ wor
             float safeAbsZ = __builtin_fmaxf(absZ, 1e-4f);
             float invAbsZ = 1.0f / safeAbsZ;
             float invAbsZ2 = invAbsZ * invAbsZ;
-            float p00 = cam.proj[0], p11 = cam.proj[5];
-            float limX = 1.3f * (1.0f / __builtin_fmaxf(__builtin_fabsf(p00), 1e-4f));
-            float limY = 1.3f * (1.0f / __builtin_fmaxf(__builtin_fabsf(p11), 1e-4f));
+            const float limX = P.limX, limY = P.limY;  // host-evaluated, same operations
             float xCl = clampf(vp[0] * invAbsZ, -limX, limX) * safeAbsZ;
             float yCl = clampf(vp[1] * invAbsZ, -limY, limY) * safeAbsZ;
-            float focalX = cam.width * __builtin_fabsf(p00) * 0.5f;
-            float focalY = cam.height * __builtin_fabsf(p11) * 0.5f;
+            const float focalX = P.focalX, focalY = P.focalY;
             M3 J;
             J.m[0][0] = focalX * invAbsZ; J.m[0][1] = 0.0f; J.m[0][2] = 0.0f;
             J.m[1][0] = 0.0f; J.m[1][1] = focalY * invAbsZ; J.m[1][2] = 0.0f;
@@ -411,10 +417,7 @@ __device__ __forceinline__ ProjOut project_gaussian(const void* __restrict__ wor
             // stabilizeCovariance2D (GaussianShared.h:655-714)
             {
                 const float kMinVar = 1e-4f, kMinDet = 1e-8f;
-                float maxCond = 256.0f * 256.0f;
-                float maxDim = __builtin_fmaxf(cam.width, cam.height);
-                float maxEig = (maxDim * 2.0f) / 3.0f;
-                maxEig = maxEig * maxEig;
+                const float maxEig = P.maxEig;  // ((max(W, H) * 2) / 3)^2, host-evaluated
                 float a = cov.a, b = 0.5f * (cov.b + cov.c), d = cov.d;
                 if (!__builtin_isfinite(a) || !__builtin_isfinite(b) || !__builtin_isfinite(d)) {
                     cov.a = 1.0f; cov.b = 0.0f; cov.c = 0.0f; cov.d = 1.0f;
@@ -445,7 +448,7 @@ __device__ __forceinline__ ProjOut project_gaussian(const void* __restrict__ wor
                     }
                     float v2x = v1y, v2y = -v1x;
                     l1 = __builtin_fminf(l1, maxEig);
-                    l2 = __builtin_fmaxf(l2, l1 / maxCond);
+                    l2 = __builtin_fmaxf(l2, l1 * (1.0f / 65536.0f));  // l1 / 256^2: exact power of two
                     cov.a = l1 * (v1x * v1x) + l2 * (v2x * v2x);
                     cov.b = l1 * (v1x * v1y) + l2 * (v2x * v2y);
                     cov.c = l1 * (v1y * v1x) + l2 * (v2y * v2x);
@@ -498,8 +501,7 @@ __device__ __forceinline__ ProjOut project_gaussian(const void* __restrict__ wor
             float a = cov.a, b = 0.5f * (cov.b + cov.c), d = cov.d;
             float det = a * d - b * b;
             float ink = opacity * 6.283185f * __builtin_sqrtf(__builtin_fmaxf(det, 1e-12f));
-            float adjFar = cam.farPlane * 0.02f;
-            float s = clampf((adjFar - clip[3]) / (adjFar - cam.nearPlane), 0.0f, 1.0f);
+            float s = clampf((P.adjFar - clip[3]) / P.adjDen, 0.0f, 1.0f);
             float depthFactor = 1.0f - s * s;
             if (ink < depthFactor * P.bin.totalInkThreshold) vis = false;
         }
@@ -563,10 +565,12 @@ __device__ __forceinline__ ProjOut project_gaussian(const void* __restrict__ wor
             float maxW = cam.width - 1.0f, maxH = cam.height - 1.0f;
             float xmin = clampf(sx - ex, 0.0f, maxW), xmax = clampf(sx + ex, 0.0f, maxW);
             float ymin = clampf(sy - ey, 0.0f, maxH), ymax = clampf(sy + ey, 0.0f, maxH);
-            int minTX = (int)__builtin_floorf(xmin / (float)kTileWidth);
-            int maxTX = (int)__builtin_ceilf(xmax / (float)kTileWidth) - 1;
-            int minTY = (int)__builtin_floorf(ymin / (float)kTileHeight);
-            int maxTY = (int)__builtin_ceilf(ymax / (float)kTileHeight) - 1;
+            // x / 32 and y / 16: division by a power of two equals the product with its inverse
+            static_assert(kTileWidth == 32 && kTileHeight == 16, "tile size");
+            int minTX = (int)__builtin_floorf(xmin * (1.0f / 32.0f));
+            int maxTX = (int)__builtin_ceilf(xmax * (1.0f / 32.0f)) - 1;
+            int minTY = (int)__builtin_floorf(ymin * (1.0f / 16.0f));
+            int maxTY = (int)__builtin_ceilf(ymax * (1.0f / 16.0f)) - 1;
             minTX = max(minTX, 0);
             minTY = max(minTY, 0);
             maxTX = min(maxTX, (int)P.bin.tilesX - 1);
@@ -577,9 +581,10 @@ __device__ __forceinline__ ProjOut project_gaussian(const void* __restrict__ wor
             float cmx = hbits_to_f(hmx), cmy = hbits_to_f(hmy);
             Conic k = conic_from_quant(sincos, thq, hbits_to_f(hs1), hbits_to_f(hs2));
             uint16_t hcxx = f_to_hbits(k.A), hcyy = f_to_hbits(k.C), hcxy2 = f_to_hbits(2.0f * k.B);
-            uint16_t hop = f_to_hbits((float)cO / 255.0f);
-            uint16_t hr = f_to_hbits((float)cR / 255.0f), hg = f_to_hbits((float)cG / 255.0f);
-            uint16_t hb = f_to_hbits((float)cB / 255.0f);
+            // fp16(float(c) / 255) for the u8 channels: the block's 256-entry table
+            uint16_t hop = div255[cO];
+            uint16_t hr = div255[cR], hg = div255[cG];
+            uint16_t hb = div255[cB];
             BlendRecordA ra;
             ra.x = rdw.x;
             ra.y = (uint32_t)hcxx | ((uint32_t)hcyy << 16);
@@ -619,10 +624,12 @@ __global__ __launch_bounds__(kProjectBlock) void k_project(
     BlendRecordA* __restrict__ outA, uint32_t* __restrict__ outB, uint32_t* __restrict__ counts,
     uint32_t* __restrict__ blockSums, const float2* __restrict__ sincos) {
     __shared__ uint32_t lds[kProjectBlock / 64];
+    __shared__ uint16_t div255[256];
+    fill_div255(div255);
     const uint32_t gid = blockIdx.x * kProjectBlock + threadIdx.x;
     uint32_t ntiles = 0;
     if (gid < P.count) {
-        const ProjOut o = project_gaussian<HALF, DEG>(world, harm, gid, P, sincos);
+        const ProjOut o = project_gaussian<HALF, DEG>(world, harm, gid, P, sincos, div255);
         outBounds[gid] = o.bounds;
         if (o.vis) {
             *(uint4*)(outRD + gid) = o.rd;
@@ -658,11 +665,13 @@ __global__ __launch_bounds__(kProjectBlock) void k_project_part(
     SplatRecord* __restrict__ records, uint32_t* __restrict__ masks,
     uint32_t* __restrict__ blockSlabCounts, const float2* __restrict__ sincos) {
     __shared__ uint32_t wcnt[kProjectBlock / 64][kMaxSlabs];
+    __shared__ uint16_t div255[256];
+    fill_div255(div255);
     const uint32_t gid = blockIdx.x * kProjectBlock + threadIdx.x;
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     uint32_t mask = 0;
     if (gid < P.count) {
-        const ProjOut o = project_gaussian<HALF, DEG>(world, harm, gid, P, sincos);
+        const ProjOut o = project_gaussian<HALF, DEG>(world, harm, gid, P, sincos, div255);
         if (o.vis) {
             SplatRecord r;
             r.rd = o.rd;

@@ -7,6 +7,7 @@
 // be captured into a hipGraph.
 #include <hip/hip_runtime.h>
 
+#include <cmath>
 #include <cstdio>
 #include <cstring>
 #include <new>
@@ -193,6 +194,17 @@ ProjectArgs GlobalRenderer::frameArgs(const gsm_camera_params& camp, uint32_t wi
     a.rowEnd = rowEnd_;
     a.count = count;
     a.maxAssignments = maxAssignments_;
+    // uniform terms of the projection, same operation order as the per-gaussian code
+    const float p00 = a.cam.proj[0], p11 = a.cam.proj[5];
+    a.limX = 1.3f * (1.0f / std::fmax(std::fabs(p00), 1e-4f));
+    a.limY = 1.3f * (1.0f / std::fmax(std::fabs(p11), 1e-4f));
+    a.focalX = a.cam.width * std::fabs(p00) * 0.5f;
+    a.focalY = a.cam.height * std::fabs(p11) * 0.5f;
+    const float maxDim = std::fmax(a.cam.width, a.cam.height);
+    const float maxEig = (maxDim * 2.0f) / 3.0f;
+    a.maxEig = maxEig * maxEig;
+    a.adjFar = a.cam.farPlane * 0.02f;
+    a.adjDen = a.adjFar - a.cam.nearPlane;
 
     return a;
 }

@@ -50,6 +50,7 @@ struct DeviceArena {
     BlendRecordA* recA = nullptr;              // [maxG]
     uint32_t* recB = nullptr;                  // [maxG]
     uint32_t* tileCounts = nullptr;            // [maxG]
+    uint32_t* tileMasks = nullptr;             // [maxG] tile tests of rects <= 32 tiles, scan order
     uint32_t* blockSums = nullptr;             // [ceil(maxG/256) + 1]
     TileAssignmentHeader* header = nullptr;    // [1]
     uint32_t* keys[2] = {nullptr, nullptr};    // [cap] ping-pong

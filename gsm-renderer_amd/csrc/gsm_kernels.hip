@@ -607,13 +607,23 @@ __device__ __forceinline__ ProjOut project_gaussian(const void* __restrict__ wor
 }
 
 // tiles of a projected gaussian's rect in rows [rowBegin, rowEnd) that its ellipse meets
-__device__ __forceinline__ uint32_t count_tiles(const ProjOut& o, int rowBegin, int rowEnd) {
-    uint32_t n = 0;
+// (tileCountIndirectKernel, GlobalShaders.metal:563-616).  For rects of at most 32 tiles the
+// answers are also returned as a bit mask in scan order (bit (ty - ty0) * width + (tx - tx0)),
+// so the scatter reuses them instead of repeating the tests.
+constexpr int kMaskTiles = 32;
+__device__ __forceinline__ uint32_t count_tiles(const ProjOut& o, int rowBegin, int rowEnd, uint32_t* maskOut) {
+    uint32_t n = 0, mask = 0;
+    *maskOut = 0;
     if (!o.countable) return 0;
     const int ty0 = max((int)o.bounds.z, rowBegin), ty1 = min((int)o.bounds.w, rowEnd - 1);
+    uint32_t bit = 0;
     for (int ty = ty0; ty <= ty1; ++ty)
-        for (int tx = (int)o.bounds.x; tx <= (int)o.bounds.y; ++tx)
-            if (intersects_tile(tx, ty, o.cmx, o.cmy, o.k, o.w)) n++;
+        for (int tx = (int)o.bounds.x; tx <= (int)o.bounds.y; ++tx, ++bit)
+            if (intersects_tile(tx, ty, o.cmx, o.cmy, o.k, o.w)) {
+                n++;
+                if (bit < (uint32_t)kMaskTiles) mask |= 1u << bit;
+            }
+    *maskOut = mask;
     return n;
 }
 
@@ -622,7 +632,7 @@ __global__ __launch_bounds__(kProjectBlock) void k_project(
     const void* __restrict__ world, const void* __restrict__ harm, ProjectArgs P,
     GaussianRenderData* __restrict__ outRD, short4* __restrict__ outBounds,
     BlendRecordA* __restrict__ outA, uint32_t* __restrict__ outB, uint32_t* __restrict__ counts,
-    uint32_t* __restrict__ blockSums, const float2* __restrict__ sincos) {
+    uint32_t* __restrict__ masks, uint32_t* __restrict__ blockSums, const float2* __restrict__ sincos) {
     __shared__ uint32_t lds[kProjectBlock / 64];
     __shared__ uint16_t div255[256];
     fill_div255(div255);
@@ -635,7 +645,9 @@ __global__ __launch_bounds__(kProjectBlock) void k_project(
             *(uint4*)(outRD + gid) = o.rd;
             outA[gid] = o.ra;
             outB[gid] = o.rb;
-            ntiles = count_tiles(o, (int)P.rowBegin, (int)P.rowEnd);  // rows limited to the slab
+            uint32_t mask;
+            ntiles = count_tiles(o, (int)P.rowBegin, (int)P.rowEnd, &mask);  // rows limited to the slab
+            masks[gid] = mask;
         }
         counts[gid] = ntiles;
     }
@@ -763,7 +775,8 @@ __global__ __launch_bounds__(kProjectBlock) void k_part_pack(
 __global__ __launch_bounds__(kProjectBlock) void k_records_in(
     const SplatRecord* __restrict__ in, ProjectArgs P, GaussianRenderData* __restrict__ outRD,
     short4* __restrict__ outBounds, BlendRecordA* __restrict__ outA, uint32_t* __restrict__ outB,
-    uint32_t* __restrict__ counts, uint32_t* __restrict__ blockSums, const float2* __restrict__ sincos) {
+    uint32_t* __restrict__ counts, uint32_t* __restrict__ masks, uint32_t* __restrict__ blockSums,
+    const float2* __restrict__ sincos) {
     __shared__ uint32_t lds[kProjectBlock / 64];
     const uint32_t gid = blockIdx.x * kProjectBlock + threadIdx.x;
     uint32_t ntiles = 0;
@@ -783,8 +796,10 @@ __global__ __launch_bounds__(kProjectBlock) void k_records_in(
         const float alpha = (float)(r.rd.w >> 24);
         o.countable = alpha >= 1e-4f && r.bounds.x <= r.bounds.y && r.bounds.z <= r.bounds.w;
         o.w = o.countable ? 2.0f * compute_power(alpha) : 0.0f;
-        ntiles = count_tiles(o, (int)P.rowBegin, (int)P.rowEnd);
+        uint32_t mask;
+        ntiles = count_tiles(o, (int)P.rowBegin, (int)P.rowEnd, &mask);
         counts[gid] = ntiles;
+        masks[gid] = mask;
     }
     uint32_t s = block_reduce_add<kProjectBlock>(ntiles, lds);
     if (threadIdx.x == 0) blockSums[blockIdx.x] = s;
@@ -840,8 +855,9 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_blocks(uint32_t* __restri
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(kProjectBlock) void k_scatter(
     ProjectArgs P, const GaussianRenderData* __restrict__ rd, const short4* __restrict__ bounds,
-    const uint32_t* __restrict__ counts, const uint32_t* __restrict__ blockOffsets,
-    uint32_t* __restrict__ keys, uint32_t* __restrict__ vals, const float2* __restrict__ sincos) {
+    const uint32_t* __restrict__ counts, const uint32_t* __restrict__ masks,
+    const uint32_t* __restrict__ blockOffsets, uint32_t* __restrict__ keys, uint32_t* __restrict__ vals,
+    const float2* __restrict__ sincos) {
     __shared__ uint32_t lds[kProjectBlock / 64];
     const uint32_t gid = blockIdx.x * kProjectBlock + threadIdx.x;
     uint32_t c = (gid < P.count) ? counts[gid] : 0u;
@@ -851,16 +867,35 @@ __global__ __launch_bounds__(kProjectBlock) void k_scatter(
     uint64_t wp = (uint64_t)blockOffsets[blockIdx.x] + off;
     if (wp >= P.maxAssignments) return;
     const short4 r = bounds[gid];
+    const uint32_t rdz = ((const uint4*)(rd + gid))->z;
+    const uint32_t dbits = ((rdz >> 16) ^ 0x8000u) & 0xFFFFu;
+    const int ty0 = max((int)r.z, (int)P.rowBegin), ty1 = min((int)r.w, (int)P.rowEnd - 1);
+    const int rw = (int)r.y - (int)r.x + 1;
+    if ((ty1 - ty0 + 1) * rw <= kMaskTiles) {
+        // the projection's answers, in its scan order (ty-major, tx-minor)
+        uint32_t mask = masks[gid];
+        uint32_t bit = 0;
+        for (int ty = ty0; ty <= ty1 && mask; ++ty)
+            for (int tx = (int)r.x; tx <= (int)r.y; ++tx, ++bit)
+                if ((mask >> bit) & 1u) {
+                    mask &= ~(1u << bit);
+                    if (wp < P.maxAssignments) {
+                        keys[wp] = ((uint32_t)(ty * (int)P.bin.tilesX + tx) << 16) | dbits;
+                        vals[wp] = gid;
+                        wp++;
+                    }
+                }
+        return;
+    }
+    // large rects: repeat the tests (tileScatterIndirectKernel, GlobalShaders.metal:623-678)
     uint4 rdw = *(const uint4*)(rd + gid);
     uint16_t hmx = (uint16_t)(rdw.x & 0xFFFFu), hmy = (uint16_t)(rdw.x >> 16);
     uint16_t thq = (uint16_t)(rdw.y & 0xFFFFu), hs1 = (uint16_t)(rdw.y >> 16);
-    uint16_t hs2 = (uint16_t)(rdw.z & 0xFFFFu), hd = (uint16_t)(rdw.z >> 16);
+    uint16_t hs2 = (uint16_t)(rdw.z & 0xFFFFu);
     uint32_t opac = rdw.w >> 24;
     float cx = hbits_to_f(hmx), cy = hbits_to_f(hmy);
     Conic k = conic_from_quant(sincos, thq, hbits_to_f(hs1), hbits_to_f(hs2));
     float w = 2.0f * compute_power((float)opac);
-    const uint32_t dbits = ((uint32_t)hd ^ 0x8000u) & 0xFFFFu;
-    int ty0 = max((int)r.z, (int)P.rowBegin), ty1 = min((int)r.w, (int)P.rowEnd - 1);
     for (int ty = ty0; ty <= ty1; ++ty)
         for (int tx = (int)r.x; tx <= (int)r.y; ++tx)
             if (intersects_tile(tx, ty, cx, cy, k, w)) {
@@ -873,15 +908,6 @@ __global__ __launch_bounds__(kProjectBlock) void k_scatter(
             }
 }
 
-// ---------------------------------------------------------------------------
-// 4. headers (buildHeadersFromSortedKernel, GlobalShaders.metal:304-356)
-//
-// The reference binary-searches every tile (offset = lower_bound, count = upper - lower).
-// Here one pass over the sorted keys finds the run boundaries instead: at position i with
-// tile(i-1) < tile(i), every tile t in (tile(i-1), tile(i)] starts at i, which also gives
-// empty tiles their lower_bound.  tileStart[t+1] - tileStart[t] is the count; the
-// {offset, count} layout of the reference is produced on readback.
-// ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_tile_starts(const uint32_t* __restrict__ sortedKeys,
                                                      const TileAssignmentHeader* __restrict__ hdr,
                                                      uint32_t tileBegin, uint32_t tileEnd,
@@ -924,7 +950,7 @@ static void launch_project_t(uint32_t deg, const void* world, const void* harm, 
     if (blocks == 0) return;
 #define GSM_LAUNCH_PROJ(D)                                                                     \
     hipLaunchKernelGGL((k_project<HALF, D>), dim3(blocks), dim3(kProjectBlock), 0, s, world,   \
-                       harm, a, A.renderData, A.bounds, A.recA, A.recB, A.tileCounts,          \
+                       harm, a, A.renderData, A.bounds, A.recA, A.recB, A.tileCounts, A.tileMasks, \
                        A.blockSums, A.sincosTable)
     switch (deg) {
         case 0: GSM_LAUNCH_PROJ(0); break;
@@ -979,7 +1005,8 @@ void launch_records_in(const void* records, const ProjectArgs& a, const DeviceAr
     const uint32_t blocks = (a.count + kProjectBlock - 1) / kProjectBlock;
     if (blocks == 0) return;
     hipLaunchKernelGGL(k_records_in, dim3(blocks), dim3(kProjectBlock), 0, s, (const SplatRecord*)records, a,
-                       A.renderData, A.bounds, A.recA, A.recB, A.tileCounts, A.blockSums, A.sincosTable);
+                       A.renderData, A.bounds, A.recA, A.recB, A.tileCounts, A.tileMasks, A.blockSums,
+                       A.sincosTable);
 }
 
 void launch_scan_blocks(uint32_t nb, const ProjectArgs& a, const DeviceArena& A, hipStream_t s) {
@@ -991,7 +1018,7 @@ void launch_scatter(const ProjectArgs& a, const DeviceArena& A, hipStream_t s) {
     const uint32_t blocks = (a.count + kProjectBlock - 1) / kProjectBlock;
     if (blocks == 0) return;
     hipLaunchKernelGGL(k_scatter, dim3(blocks), dim3(kProjectBlock), 0, s, a, A.renderData, A.bounds,
-                       A.tileCounts, A.blockSums, A.keys[0], A.vals[0], A.sincosTable);
+                       A.tileCounts, A.tileMasks, A.blockSums, A.keys[0], A.vals[0], A.sincosTable);
 }
 
 void launch_headers(const uint32_t* sortedKeys, const FrameGeometry& g, const DeviceArena& A,

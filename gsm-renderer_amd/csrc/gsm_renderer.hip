@@ -109,6 +109,7 @@ gsm_status GlobalRenderer::create(const gsm_renderer_config& cfg, int hipDevice,
     GSM_ALLOC(A.recA, G * sizeof(BlendRecordA));
     GSM_ALLOC(A.recB, G * sizeof(uint32_t));
     GSM_ALLOC(A.tileCounts, G * sizeof(uint32_t));
+    GSM_ALLOC(A.tileMasks, G * sizeof(uint32_t));
     GSM_ALLOC(A.blockSums, (nb + 1) * sizeof(uint32_t));
     GSM_ALLOC(A.header, sizeof(TileAssignmentHeader));
     GSM_ALLOC(A.keys[0], cap * sizeof(uint32_t));

@@ -104,7 +104,16 @@ __global__ __launch_bounds__(NT) void k_blend_px(
     const uint32_t numUnits = numTiles * UPT;
     const uint32_t gridWaves = gridDim.x * NW;
 
-    uint32_t qi = blockIdx.x * NW + (threadIdx.x >> 6);  // first unit static, then the queue
+    // First unit static, then the queue.  With the schedule on (flags bit 2), the first half of
+    // every workgroup's waves (one per SIMD) take the gridDim.x * NW/2 longest units and run
+    // them at the top priority, so each SIMD pairs one long walk with one shorter one and the
+    // long walk issues nearly as fast as a wave alone (the makespan is the longest walk's).
+    const uint32_t wv = threadIdx.x >> 6;
+    const bool split = (flags & 4) != 0;
+    uint32_t qi = !split ? blockIdx.x * NW + wv
+                         : (wv < NW / 2 ? blockIdx.x * (NW / 2) + wv
+                                        : gridDim.x * (NW / 2) + blockIdx.x * (NW / 2) + (wv - NW / 2));
+    bool topPrio = split && wv < NW / 2;
     while (qi < numUnits) {
         uint32_t u = order ? __builtin_amdgcn_readfirstlane(order[qi]) : qi;
         if (u >= numUnits) u = qi;  // a schedule is a permutation of [0, numUnits); never trust it further
@@ -289,10 +298,12 @@ __global__ __launch_bounds__(NT) void k_blend_px(
                         bdc[k] = bdn[k];
                     }
                 }
-                if (agePrio) {
+                if (topPrio) {
+                    if (b0 == 0) __builtin_amdgcn_s_setprio(3);
+                } else if (agePrio) {
                     if (b0 == 0) __builtin_amdgcn_s_setprio(1);
                     else if (b0 == 128u) __builtin_amdgcn_s_setprio(2);
-                    else if (b0 == 320u) __builtin_amdgcn_s_setprio(3);
+                    else if (b0 == 320u && !split) __builtin_amdgcn_s_setprio(3);
                 }
                 bA = nA;
                 bB = nB;
@@ -349,7 +360,8 @@ __global__ __launch_bounds__(NT) void k_blend_px(
             t[3] = ((unsigned long long)__builtin_amdgcn_s_getreg(20 | (31 << 11)) << 32) |
                    (unsigned long long)__builtin_amdgcn_s_getreg(4 | (31 << 11));
         }
-        if (agePrio) __builtin_amdgcn_s_setprio(0);
+        if (agePrio || topPrio) __builtin_amdgcn_s_setprio(0);
+        topPrio = false;
         qi = __builtin_amdgcn_readfirstlane(nextQ) + gridWaves;
     }
 }
@@ -554,55 +566,83 @@ __global__ __launch_bounds__(NT) void k_blend_lanes(
 }
 
 // ---------------------------------------------------------------------------
-// Blend schedule: a stable sort of the units into 8 linear buckets of last frame's walk length
-// (longest bucket first; index order, i.e. tile locality, kept inside a bucket), one workgroup.
+// Blend schedule: the units in descending order of the walk each made in the previous frame
+// (longest-processing-time-first list scheduling on the persistent waves), as a stable
+// counting sort into 256 buckets of walk length (bucket width = max walk / 256, so the order
+// is exact to ~1 % of the longest walk; index order, i.e. tile locality, inside a bucket).
+// One workgroup of 1024 threads: histogram, scan, then a stable ranked scatter in chunks of
+// 1024 units (wave ballot match + per-wave bucket counters).
 // ---------------------------------------------------------------------------
+constexpr uint32_t kUoBuckets = 256, kUoWaves = 16;
+
+__device__ __forceinline__ uint64_t uo_match8(uint32_t d, bool valid) {
+    uint64_t peers = __ballot(valid);
+#pragma unroll
+    for (int bit = 0; bit < 8; ++bit) {
+        const bool set = (d >> bit) & 1u;
+        const uint64_t m = __ballot(set);
+        peers &= set ? m : ~m;
+    }
+    return peers;
+}
+
 __global__ __launch_bounds__(1024) void k_unit_order(const uint16_t* __restrict__ cost,
                                                      uint32_t* __restrict__ order, uint32_t n) {
-    constexpr uint32_t NB = 8, NWV = 16;
-    __shared__ uint32_t wmax[NWV];
-    __shared__ uint32_t cnt[NWV][NB];
+    __shared__ uint32_t wmax[kUoWaves];
+    __shared__ uint32_t base[kUoBuckets];
+    __shared__ uint32_t wcnt[kUoWaves][kUoBuckets];
     const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
     // pass 1: the longest walk
     uint32_t m = 0;
     for (uint32_t i = t; i < n; i += 1024) m = max(m, (uint32_t)cost[i]);
     for (int off = 32; off > 0; off >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, off));
     if (lane == 0) wmax[w] = m;
+    if (t < kUoBuckets) base[t] = 0;
     __syncthreads();
     uint32_t mx = 0;
-    for (uint32_t k = 0; k < NWV; ++k) mx = max(mx, wmax[k]);
+    for (uint32_t k = 0; k < kUoWaves; ++k) mx = max(mx, wmax[k]);
     const uint32_t den = mx + 1u;
-    // pass 2: per-wave bucket counts over a contiguous range of units
-    const uint32_t per = ((n + NWV - 1) / NWV + 63u) & ~63u;
-    const uint32_t lo = min(n, w * per), hi = min(n, lo + per);
-    uint32_t myCnt = 0;  // lane b < NB counts bucket b
-    for (uint32_t c = lo; c < hi; c += 64) {
-        const uint32_t i = c + lane;
-        const uint32_t bk = i < hi ? (NB - 1u) - min(NB - 1u, (uint32_t)cost[i] * NB / den) : NB;
-        for (uint32_t b2 = 0; b2 < NB; ++b2) {
-            const uint32_t pc = (uint32_t)__popcll(__ballot(bk == b2));
-            if (lane == b2) myCnt += pc;
-        }
-    }
-    if (lane < NB) cnt[w][lane] = myCnt;
+    auto bucket = [&](uint32_t i) {  // 0 = longest walks
+        return (kUoBuckets - 1u) - min(kUoBuckets - 1u, (uint32_t)cost[i] * kUoBuckets / den);
+    };
+    // pass 2: bucket sizes, then their exclusive scan (bucket-major = descending walk)
+    for (uint32_t i = t; i < n; i += 1024) atomicAdd(&base[bucket(i)], 1u);
     __syncthreads();
-    // bases: bucket-major (bk 0 = longest), then wave order -> stable
-    uint32_t base = 0;  // lane b < NB: where this wave's bucket-b units start
-    if (lane < NB) {
-        for (uint32_t b2 = 0; b2 < lane; ++b2)
-            for (uint32_t k = 0; k < NWV; ++k) base += cnt[k][b2];
-        for (uint32_t k = 0; k < w; ++k) base += cnt[k][lane];
-    }
-    // pass 3: scatter in index order
-    for (uint32_t c = lo; c < hi; c += 64) {
-        const uint32_t i = c + lane;
-        const uint32_t bk = i < hi ? (NB - 1u) - min(NB - 1u, (uint32_t)cost[i] * NB / den) : NB;
-        for (uint32_t b2 = 0; b2 < NB; ++b2) {
-            const uint64_t msk = __ballot(bk == b2);
-            const uint32_t bb = (uint32_t)__shfl((int)base, (int)b2);
-            if (bk == b2) order[bb + (uint32_t)__popcll(msk & ((1ull << lane) - 1ull))] = i;
-            if (lane == b2) base += (uint32_t)__popcll(msk);
+    if (w == 0) {
+        const uint4 c = *(const uint4*)(base + lane * 4u);
+        const uint32_t local = c.x + c.y + c.z + c.w;
+        uint32_t inc = local;
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t v = __shfl_up(inc, o, 64);
+            if (lane >= (uint32_t)o) inc += v;
         }
+        const uint32_t e = inc - local;
+        *(uint4*)(base + lane * 4u) = make_uint4(e, e + c.x, e + c.x + c.y, e + c.x + c.y + c.z);
+    }
+    __syncthreads();
+    // pass 3: stable scatter, chunks of 1024 units in index order
+    const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    for (uint32_t c0 = 0; c0 < n; c0 += 1024) {
+        const uint32_t i = c0 + t;
+        const bool valid = i < n;
+        const uint32_t bk = valid ? bucket(i) : 0u;
+        const uint64_t peers = uo_match8(bk, valid);
+        for (uint32_t k = t; k < kUoWaves * kUoBuckets; k += 1024) (&wcnt[0][0])[k] = 0;
+        __syncthreads();
+        if (valid && (peers & lt) == 0) wcnt[w][bk] = (uint32_t)__popcll(peers);
+        __syncthreads();
+        if (valid) {
+            uint32_t before = base[bk];
+            for (uint32_t k = 0; k < w; ++k) before += wcnt[k][bk];
+            order[before + (uint32_t)__popcll(peers & lt)] = i;
+        }
+        __syncthreads();
+        if (t < kUoBuckets) {
+            uint32_t add = 0;
+            for (uint32_t k = 0; k < kUoWaves; ++k) add += wcnt[k][t];
+            base[t] += add;
+        }
+        __syncthreads();
     }
 }
 
@@ -648,7 +688,8 @@ void launch_blend(const uint32_t* sortedVals, const FrameGeometry& g, const Devi
                         ? 1
                         : 0;
     const char* pv = getenv("GSM_BLEND_PRIO");  // age-raised wave priority (default on)
-    const int flags = vec | ((pv && pv[0] == '0') ? 0 : 2);
+    const char* sp = getenv("GSM_BLEND_SPLIT");  // long units on half the waves at top priority
+    const int flags = vec | ((pv && pv[0] == '0') ? 0 : 2) | ((costOrder && !(sp && sp[0] == '0')) ? 4 : 0);
     // A.tileQueue was zeroed by k_scan_blocks earlier in the frame
     const int P = blend_pairs_per_lane();
     const int waves = blend_waves_per_wg(numTiles, numCUs);

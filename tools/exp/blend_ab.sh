@@ -1,0 +1,15 @@
+set -u
+cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out; export TMPDIR=/tmp
+run() {  # label env...
+  local label=$1; shift
+  env "$@" timeout -k 10 120 python bench.py --steps 30 --warmup 5 --cpu-baseline 0 --parity 0 ${BENCH_ARGS:-} > gpurun_out/ab_$label.log 2>&1 || { echo "$label failed"; tail -3 gpurun_out/ab_$label.log; return 1; }
+  python -c "import json;d=json.loads(open('gpurun_out/ab_$label.log').read().strip().splitlines()[-1]);print('$label',round(d['value'],1),'blend',round(d['stages_ms']['blend_timed_region']*1000,1))"
+}
+run base X=1 || exit 1
+run w16 GSM_BLEND_WAVES=16 || exit 1
+run p1w8 GSM_BLEND_PAIRS=1 || exit 1
+run p1w16 GSM_BLEND_PAIRS=1 GSM_BLEND_WAVES=16 || exit 1
+run p4w8 GSM_BLEND_PAIRS=4 || exit 1
+run p4w16 GSM_BLEND_PAIRS=4 GSM_BLEND_WAVES=16 || exit 1
+run nosched GSM_BLEND_SCHED=0 || exit 1
+run noprio GSM_BLEND_PRIO=0 || exit 1

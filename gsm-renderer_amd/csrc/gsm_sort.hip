@@ -43,6 +43,27 @@ __device__ __forceinline__ uint64_t match_digit(uint32_t d, bool valid) {
     return peers;
 }
 
+// Stable rank of a lane's digit among the earlier lanes of its wave with the same digit, from
+// one LDS atomic: gfx950 serves the lanes of one ds_add_rtn_u32 that hit the same address in
+// lane order (tools/exp/lds_atomic_order.hip: 15M same-address lane pairs, every one in lane
+// order; the GPU parity tests re-check the sorts bit for bit).  Returns the counter's old value;
+// the counter ends at the count.  kBallotRank selects the ballot-match form instead (8 ballots
+// per digit) for A/B measurement.
+constexpr bool kBallotRank = false;
+template <int BITS>
+__device__ __forceinline__ uint32_t wave_rank(uint32_t* cnt, uint32_t d, bool valid, uint64_t lt) {
+    if constexpr (kBallotRank) {
+        const uint64_t peers = match_digit<BITS>(d, valid);
+        const uint32_t before = cnt[d];
+        if (valid && (peers & lt) == 0) cnt[d] = before + (uint32_t)__popcll(peers);
+        return before + (uint32_t)__popcll(peers & lt);
+    } else {
+        uint32_t r = 0;
+        if (valid) r = atomicAdd(&cnt[d], 1u);
+        return r;
+    }
+}
+
 template <int BITS>
 __global__ __launch_bounds__(kRadixBlock) void k_radix_upsweep(const uint32_t* __restrict__ keys,
                                                                const uint32_t* __restrict__ nPtr,
@@ -179,10 +200,7 @@ __global__ __launch_bounds__(kRadixBlock) void k_radix_downsweep(
             const uint32_t idx = cbase + wave * (64 * kRadixItems) + j * 64 + lane;
             const bool valid = idx < end;
             const uint32_t d = (k[j] >> shift) & (R - 1u);
-            const uint64_t peers = match_digit<BITS>(d, valid);
-            const uint32_t before = valid ? waveCnt[wave][d] : 0u;
-            rank[j] = before + (uint32_t)__popcll(peers & lt);
-            if (valid && (peers & lt) == 0) waveCnt[wave][d] = before + (uint32_t)__popcll(peers);
+            rank[j] = wave_rank<BITS>(waveCnt[wave], d, valid, lt);
         }
         __syncthreads();
         // per digit: offsets of each wave, chunk total, then exclusive scan over digits
@@ -362,11 +380,8 @@ __device__ __forceinline__ void ts_rank_pass(const uint32_t (&x)[kTsItems], uint
         if (j < E) {
             const bool valid = seg + j * 64u + lane < n;
             const uint32_t d = (x[j] >> shift) & 0xFFu;
-            const uint64_t peers = match_digit<8>(d, valid);
-            const uint32_t before = cnt[d];
-            if (valid && (peers & lt) == 0) cnt[d] = before + (uint32_t)__popcll(peers);
+            pos[j] = wave_rank<8>(cnt, d, valid, lt);
             wave_sync();
-            pos[j] = before + (uint32_t)__popcll(peers & lt);
         }
     }
     __syncthreads();
@@ -396,16 +411,15 @@ __device__ void ts_pass_global(const uint32_t* __restrict__ kin, const uint32_t*
         const bool valid = i < n;
         const uint32_t k = valid ? kin[i] : 0u, v = valid ? vin[i] : 0u;
         const uint32_t d = (k >> shift) & 0xFFu;
-        const uint64_t peers = match_digit<8>(d, valid);
 #pragma unroll
         for (uint32_t w = 0; w < 4; ++w) wcnt[w][tid] = 0;
         __syncthreads();
-        if (valid && (peers & lt) == 0) wcnt[wave][d] = (uint32_t)__popcll(peers);
+        const uint32_t r = wave_rank<8>(wcnt[wave], d, valid, lt);
         __syncthreads();
         if (valid) {
             uint32_t before = carry[d];
             for (uint32_t w = 0; w < wave; ++w) before += wcnt[w][d];
-            const uint32_t p = before + (uint32_t)__popcll(peers & lt);
+            const uint32_t p = before + r;
             kout[p] = k;
             vout[p] = v;
         }

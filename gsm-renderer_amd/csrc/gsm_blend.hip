@@ -52,7 +52,15 @@ __device__ __forceinline__ uint32_t quad_max_u32(uint32_t v) {
 // groups of U = 4/P entries through a three-stage software pipeline (stage 1: next group's
 // p and table reads; stage 2: blend this group; stage 3: next group's alphas).
 // ---------------------------------------------------------------------------
-template <int NT, int P, bool EXECM, int EXPT = 0>
+// Lanes of one wave hand LDS words to each other: the compiler must not forward a lane's own
+// store past them (no instruction; the hardware keeps a wave's LDS operations in order).
+__device__ __forceinline__ void blend_wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <int NT, int P, bool EXECM, int EXPT = 0, bool COMPACT = false>
 __global__ __launch_bounds__(NT) void k_blend_px(
     const uint32_t* __restrict__ tileStart, const uint32_t* __restrict__ sortedVals,
     const BlendRecordA* __restrict__ recA, const uint32_t* __restrict__ recB,
@@ -62,15 +70,16 @@ __global__ __launch_bounds__(NT) void k_blend_px(
     const uint32_t* __restrict__ order, uint16_t* __restrict__ unitCost,
     unsigned long long* __restrict__ trace) {
     static_assert(P == 1 || P == 2 || P == 4, "pairs per lane");
+    static_assert(!COMPACT || (P == 2 && EXECM), "compaction: half tiles, EXEC-masked updates");
     constexpr uint32_t U = 4 / P;        // entries per pipeline group
     constexpr uint32_t NG = 64 / U;      // groups per 64-entry batch
     constexpr uint32_t EXITG = 16 / U;   // exit test every 16 entries
     constexpr uint32_t UPT = 4 / P;      // units per tile
     constexpr uint32_t NW = NT / 64;
     constexpr uint32_t UNROLL = P == 4 ? 1 : NG;  // P = 4: 64 one-entry groups stay a loop
-    const bool vecStores = (flags & 1) != 0;
     const bool agePrio = (flags & 2) != 0;
     __shared__ __attribute__((aligned(16))) uint16_t tbl[65536];
+    __shared__ uint32_t cscr[NW][16];  // compaction: the alive groups of each wave, in order
     {
         const uint4* src = (const uint4*)expTable;
         uint4* dst = (uint4*)tbl;
@@ -79,6 +88,35 @@ __global__ __launch_bounds__(NT) void k_blend_px(
     __syncthreads();
 
     const uint32_t lane = threadIdx.x & 63;
+    // write (GlobalShaders.metal:1152-1186): one pixel pair (px, py), (px + 1, py)
+    auto write_pair = [&](uint32_t px, uint32_t py, h2 Av, h2 Rq, h2 Gq, h2 Bq, h2 Dq) {
+        if (py >= H) return;
+        uint8_t* crow = color + (size_t)py * colorPitch;
+        // integer packing (extracting .y of a half2 via __builtin_bit_cast miscompiled)
+        const uint32_t ur = as_u32(Rq), ug = as_u32(Gq), ub = as_u32(Bq), ua = as_u32(Av);
+        const uint32_t p0a = (ur & 0xFFFFu) | (ug << 16);
+        const uint32_t p0b = (ub & 0xFFFFu) | (ua << 16);
+        const uint32_t p1a = (ur >> 16) | (ug & 0xFFFF0000u);
+        const uint32_t p1b = (ub >> 16) | (ua & 0xFFFF0000u);
+        const uint32_t ud = as_u32(Dq);
+        if ((flags & 1) && px + 1 < W) {
+            *(uint4*)(crow + (size_t)px * 8) = make_uint4(p0a, p0b, p1a, p1b);
+            if (depth) *(uint32_t*)(depth + (size_t)py * depthPitch + (size_t)px * 2) = ud;
+        } else {
+            if (px < W) {
+                uint32_t* c0 = (uint32_t*)(crow + (size_t)px * 8);
+                c0[0] = p0a;
+                c0[1] = p0b;
+                if (depth) *(uint16_t*)(depth + (size_t)py * depthPitch + (size_t)px * 2) = (uint16_t)(ud & 0xFFFFu);
+            }
+            if (px + 1 < W) {
+                uint32_t* c1 = (uint32_t*)(crow + (size_t)(px + 1) * 8);
+                c1[0] = p1a;
+                c1[1] = p1b;
+                if (depth) *(uint16_t*)(depth + (size_t)py * depthPitch + (size_t)(px + 1) * 2) = (uint16_t)(ud >> 16);
+            }
+        }
+    };
     // pixel pair k of this lane sits at (px[k], py[k]) and (px[k] + 1, py[k]) inside the unit
     uint32_t offX[P], offY[P];
     if (P == 1) {
@@ -110,10 +148,11 @@ __global__ __launch_bounds__(NT) void k_blend_px(
     // long walk issues nearly as fast as a wave alone (the makespan is the longest walk's).
     const uint32_t wv = threadIdx.x >> 6;
     const bool split = (flags & 4) != 0;
+    constexpr uint32_t NTOP = 4;  // one top-priority wave per SIMD
     uint32_t qi = !split ? blockIdx.x * NW + wv
-                         : (wv < NW / 2 ? blockIdx.x * (NW / 2) + wv
-                                        : gridDim.x * (NW / 2) + blockIdx.x * (NW / 2) + (wv - NW / 2));
-    bool topPrio = split && wv < NW / 2;
+                         : (wv < NTOP ? blockIdx.x * NTOP + wv
+                                      : gridDim.x * NTOP + blockIdx.x * (NW - NTOP) + (wv - NTOP));
+    bool topPrio = split && wv < NTOP;
     while (qi < numUnits) {
         uint32_t u = order ? __builtin_amdgcn_readfirstlane(order[qi]) : qi;
         if (u >= numUnits) u = qi;  // a schedule is a permutation of [0, numUnits); never trust it further
@@ -126,6 +165,7 @@ __global__ __launch_bounds__(NT) void k_blend_px(
         unsigned long long tStart = 0;
         if (trace) tStart = __builtin_amdgcn_s_memrealtime();
         uint32_t nproc = 0;
+        uint32_t ncomp = 0;  // entry at which the unit moved to one pair per lane (trace only)
         uint32_t nextQ = 0;
 
         h2 T[P], R[P], G[P], B[P], D[P];
@@ -173,6 +213,7 @@ __global__ __launch_bounds__(NT) void k_blend_px(
             uint32_t rgc[U], bdc[U], rgn[U], bdn[U], opn[U];
             u16x2 en[U][P];  // next group's exp table words (d16 loads into both halves)
             bool alive = true;
+            uint32_t eC = 0, b0C = 0;  // compaction: next entry, its batch base
             // p = ((dx*dx)*cxx + (dy*dy)*cyy) + (dx*dy)*cxy2 (GlobalShaders.metal:1115-1122);
             // the dy terms are shared by the pairs of a row
             auto quadform = [&](uint32_t r0, uint32_t r1, uint32_t r2, h2 (&pq)[P]) {
@@ -281,9 +322,18 @@ __global__ __launch_bounds__(NT) void k_blend_px(
                     }
                     const uint32_t g1 = b0 + (gi + 1) * U;
                     // late exits are harmless: neutral records past the end, dead lanes blend nothing
-                    if ((gi + 1) % EXITG == 0 && (g1 >= count || __ballot(alive) == 0)) {
-                        nproc = g1;
-                        goto unit_done;
+                    if ((gi + 1) % EXITG == 0) {
+                        const uint64_t am = __ballot(alive);
+                        if (g1 >= count || am == 0) {
+                            nproc = g1;
+                            goto unit_done;
+                        }
+                        // at most 16 of the 32 groups alive: continue them one pixel pair per lane
+                        if (COMPACT && __popcll(am & 0x5555555555555555ull) <= 16) {
+                            eC = g1;
+                            b0C = b0;
+                            goto compact_phase;
+                        }
                     }
                     // stage 3: the next group's alphas
 #pragma unroll
@@ -314,51 +364,146 @@ __global__ __launch_bounds__(NT) void k_blend_px(
                 mB = recB[nI];
                 nI = lst[min(b0 + 256u + lane, last)];
             }
+        compact_phase:
+            if constexpr (COMPACT) {
+                // Groups that broke keep their pixels: written now, in the half-tile layout.
+                if (!alive) {
+#pragma unroll
+                    for (int q = 0; q < P; ++q)
+                        write_pair(ux + offX[q], uy + offY[q], ONE - T[q], R[q], G[q], B[q], D[q]);
+                }
+                // The alive groups (<= 16) move to one pixel pair per lane: group g' of the new
+                // layout owns lanes 4g'..4g'+3 (pair k of row r at lane 4g' + 2r + k), so its
+                // break is again a quad max.  State comes over by ds_bpermute from lane 2g + r.
+                const uint64_t am = __ballot(alive) & 0x5555555555555555ull;
+                const uint32_t ng = (uint32_t)__popcll(am);
+                if (alive && (lane & 1u) == 0) cscr[wv][__popcll(am & ((1ull << lane) - 1ull))] = lane >> 1;
+                blend_wave_sync();
+                const uint32_t gp = lane >> 2, kk = lane & 1u, rr = (lane >> 1) & 1u;
+                const bool valid1 = gp < ng;
+                const uint32_t sg = cscr[wv][valid1 ? gp : 0u];
+                const int srcAddr = (int)((2u * sg + rr) * 4u);
+                auto pick = [&](h2 v0, h2 v1) {
+                    const uint32_t a0 = (uint32_t)__builtin_amdgcn_ds_bpermute(srcAddr, (int)as_u32(v0));
+                    const uint32_t a1 = (uint32_t)__builtin_amdgcn_ds_bpermute(srcAddr, (int)as_u32(v1));
+                    return as_h2(kk ? a1 : a0);
+                };
+                h2 T1 = pick(T[0], T[1]), R1 = pick(R[0], R[1]), G1 = pick(G[0], G[1]);
+                h2 B1 = pick(B[0], B[1]), D1 = pick(D[0], D[1]);
+                const uint32_t px1 = ux + (sg & 3u) * 4u + 2u * kk, py1 = uy + (sg >> 2) * 2u + rr;
+                const h2 X1 = h2{(h1)(float)px1, (h1)(float)(px1 + 1u)};
+                const h2 Y1 = h2{(h1)(float)py1, (h1)(float)py1};
+                bool alive1 = valid1;
+                // the same per-pixel operations as the half-tile walk (quadform above)
+                auto quad1 = [&](uint32_t r0, uint32_t r1, uint32_t r2) {
+                    const h2 mean = as_h2(r0), cc = as_h2(r1), oc = as_h2(r2);
+                    const h2 dyv = Y1 - splat_hi(mean);
+                    const h2 dyy = (dyv * dyv) * splat_hi(cc);
+                    const h2 dx = X1 - splat_lo(mean);
+                    return ((dx * dx) * splat_lo(cc) + splat_lo(dyy)) + (dx * splat_lo(dyv)) * splat_lo(oc);
+                };
+                auto rotate = [&](uint32_t base) {  // batches move one 64-entry step (as above)
+                    bA = nA;
+                    bB = nB;
+                    const bool mv = base + 128u + lane < count;
+                    nA = mv ? mA : pad;
+                    nB = mv ? mB : 0u;
+                    mA = *(const uint4*)(recA + nI);
+                    mB = recB[nI];
+                    nI = lst[min(base + 256u + lane, last)];
+                };
+                uint32_t e = eC, bb = b0C;
+                ncomp = eC;
+                if (e - bb == 64u) {
+                    rotate(bb);
+                    bb += 64u;
+                }
+                constexpr uint32_t U1 = 4;  // entries per pipeline group
+                h2 ac1[U1], om1[U1];
+                uint32_t rgc1[U1], bdc1[U1], rgn1[U1], bdn1[U1], opn1[U1];
+                u16x2 en1[U1];
+#pragma unroll
+                for (uint32_t k = 0; k < U1; ++k) {  // prime the group at e
+                    const uint32_t j = e - bb + k;
+                    const uint32_t r2 = __builtin_amdgcn_readlane(bA.z, j);
+                    const h2 pq = quad1(__builtin_amdgcn_readlane(bA.x, j), __builtin_amdgcn_readlane(bA.y, j), r2);
+                    rgc1[k] = __builtin_amdgcn_readlane(bA.w, j);
+                    bdc1[k] = __builtin_amdgcn_readlane(bB, j);
+                    ac1[k] = __builtin_elementwise_min(splat_hi(as_h2(r2)) * lookup2(tbl, pq), C099);
+                    om1[k] = ONE - ac1[k];
+                }
+                for (;;) {
+                    // stage 1: the next group's records and table words
+                    {
+                        const uint32_t jn = e + U1 - bb;  // 4..64
+                        const bool nb = jn >= 64u;
+                        const uint32_t sx = nb ? nA.x : bA.x, sy = nb ? nA.y : bA.y;
+                        const uint32_t sz = nb ? nA.z : bA.z, sw = nb ? nA.w : bA.w;
+                        const uint32_t sb = nb ? nB : bB;
+#pragma unroll
+                        for (uint32_t k = 0; k < U1; ++k) {
+                            const uint32_t j = (jn + k) & 63u;
+                            opn1[k] = __builtin_amdgcn_readlane(sz, j);
+                            const h2 pq = quad1(__builtin_amdgcn_readlane(sx, j), __builtin_amdgcn_readlane(sy, j), opn1[k]);
+                            rgn1[k] = __builtin_amdgcn_readlane(sw, j);
+                            bdn1[k] = __builtin_amdgcn_readlane(sb, j);
+                            const uint32_t pb = as_u32(pq);
+                            en1[k].x = tbl[pb & 0xFFFFu];
+                            en1[k].y = tbl[pb >> 16];
+                        }
+                    }
+                    // stage 2: blend the current group
+#pragma unroll
+                    for (uint32_t k = 0; k < U1; ++k) {
+                        const uint32_t tb = as_u32(T1);
+                        const uint32_t gm = quad_max_u32(max(tb & 0xFFFFu, tb >> 16));
+                        alive1 = alive1 && !(gm < thrBits);
+                        if (alive1) {
+                            const h2 rgv = as_h2(rgc1[k]), bdv = as_h2(bdc1[k]);
+                            const h2 w = ac1[k] * T1;  // (GlobalShaders.metal:1137-1149)
+                            T1 = T1 * om1[k];
+                            R1 = R1 + splat_lo(rgv) * w;
+                            G1 = G1 + splat_hi(rgv) * w;
+                            B1 = B1 + splat_lo(bdv) * w;
+                            D1 = D1 + splat_hi(bdv) * w;
+                        }
+                    }
+                    e += U1;
+                    if ((e & 15u) == 0 && (e >= count || __ballot(alive1) == 0)) break;
+                    // stage 3: the next group's alphas
+#pragma unroll
+                    for (uint32_t k = 0; k < U1; ++k) {
+                        const h2 ek = __builtin_bit_cast(h2, en1[k]);
+                        ac1[k] = __builtin_elementwise_min(splat_hi(as_h2(opn1[k])) * ek, C099);
+                        om1[k] = ONE - ac1[k];
+                        rgc1[k] = rgn1[k];
+                        bdc1[k] = bdn1[k];
+                    }
+                    if (e - bb == 64u) {
+                        rotate(bb);
+                        bb += 64u;
+                    }
+                }
+                nproc = e;
+                if (valid1) write_pair(px1, py1, ONE - T1, R1, G1, B1, D1);
+                goto unit_end;
+            }
         unit_done:;
         } else {
             if (lane == 0) nextQ = atomicAdd(queue, 1u);
         }
         // write (GlobalShaders.metal:1152-1186); empty tiles keep the clear colour (0,0,0,1)
 #pragma unroll
-        for (int q = 0; q < P; ++q) {
-            const uint32_t px = ux + offX[q], py = uy + offY[q];
-            const h2 Av = (count > 0) ? (ONE - T[q]) : ONE;
-            if (py < H) {
-                uint8_t* crow = color + (size_t)py * colorPitch;
-                // integer packing (extracting .y of a half2 via __builtin_bit_cast miscompiled)
-                const uint32_t ur = as_u32(R[q]), ug = as_u32(G[q]), ub = as_u32(B[q]), ua = as_u32(Av);
-                const uint32_t p0a = (ur & 0xFFFFu) | (ug << 16);
-                const uint32_t p0b = (ub & 0xFFFFu) | (ua << 16);
-                const uint32_t p1a = (ur >> 16) | (ug & 0xFFFF0000u);
-                const uint32_t p1b = (ub >> 16) | (ua & 0xFFFF0000u);
-                const uint32_t ud = as_u32(D[q]);
-                if (vecStores && px + 1 < W) {
-                    *(uint4*)(crow + (size_t)px * 8) = make_uint4(p0a, p0b, p1a, p1b);
-                    if (depth) *(uint32_t*)(depth + (size_t)py * depthPitch + (size_t)px * 2) = ud;
-                } else {
-                    if (px < W) {
-                        uint32_t* c0 = (uint32_t*)(crow + (size_t)px * 8);
-                        c0[0] = p0a;
-                        c0[1] = p0b;
-                        if (depth) *(uint16_t*)(depth + (size_t)py * depthPitch + (size_t)px * 2) = (uint16_t)(ud & 0xFFFFu);
-                    }
-                    if (px + 1 < W) {
-                        uint32_t* c1 = (uint32_t*)(crow + (size_t)(px + 1) * 8);
-                        c1[0] = p1a;
-                        c1[1] = p1b;
-                        if (depth) *(uint16_t*)(depth + (size_t)py * depthPitch + (size_t)(px + 1) * 2) = (uint16_t)(ud >> 16);
-                    }
-                }
-            }
-        }
+        for (int q = 0; q < P; ++q)
+            write_pair(ux + offX[q], uy + offY[q], (count > 0) ? (ONE - T[q]) : ONE, R[q], G[q], B[q], D[q]);
+    unit_end:
         if (lane == 0) unitCost[u] = (uint16_t)min(nproc, 65535u);
         if (trace && lane == 0) {
             unsigned long long* t = trace + (size_t)u * 4;
             t[0] = tStart;
             t[1] = __builtin_amdgcn_s_memrealtime();
             t[2] = ((unsigned long long)count << 32) | nproc;
-            t[3] = ((unsigned long long)__builtin_amdgcn_s_getreg(20 | (31 << 11)) << 32) |
-                   (unsigned long long)__builtin_amdgcn_s_getreg(4 | (31 << 11));
+            t[3] = ((unsigned long long)ncomp << 32) | (unsigned long long)__builtin_amdgcn_s_getreg(4 | (31 << 11));
         }
         if (agePrio || topPrio) __builtin_amdgcn_s_setprio(0);
         topPrio = false;
@@ -657,7 +802,7 @@ uint32_t blend_units_per_tile() { return 4u / (uint32_t)blend_pairs_per_lane(); 
 
 static int blend_waves_per_wg(uint32_t numTiles, int numCUs) {
     const char* v = getenv("GSM_BLEND_WAVES");
-    if (v && (atoi(v) == 8 || atoi(v) == 16)) return atoi(v);
+    if (v && (atoi(v) == 8 || atoi(v) == 12 || atoi(v) == 16)) return atoi(v);
     // 16 waves per CU hide more latency once every wave slot gets >= 6 units (4K: 16200 tiles);
     // with fewer units per slot the tail dominates and 8 waves finish first (1080p)
     const uint64_t units = (uint64_t)numTiles * blend_units_per_tile();
@@ -728,6 +873,24 @@ void launch_blend(const uint32_t* sortedVals, const FrameGeometry& g, const Devi
     if (xv && (xv[0] == '1' || xv[0] == '2') && P == 2 && waves == 8 && execm) {
         if (xv[0] == '1') GSM_LAUNCH_PXE(512, 2, true, 1);
         else GSM_LAUNCH_PXE(512, 2, true, 2);
+        return;
+    }
+    const char* cv = getenv("GSM_BLEND_COMPACT");  // groups move to 1 pair per lane when <= 16 alive
+    if (P == 2 && execm && !(cv && cv[0] == '0')) {
+        if (waves == 12) hipLaunchKernelGGL((k_blend_px<768, 2, true, 0, true>), dim3(grid), dim3(768), 0, s,
+                                            A.tileStart, sortedVals, A.recA, A.recB, A.expTable, A.tileQueue, t0,
+                                            numTiles, g.tilesX, g.width, g.height, (uint8_t*)color, colorPitch,
+                                            (uint8_t*)depth, depthPitch, flags, costOrder ? A.unitOrder : nullptr,
+                                            A.unitCost, A.blendTrace);
+        else if (waves == 16) hipLaunchKernelGGL((k_blend_px<1024, 2, true, 0, true>), dim3(grid), dim3(1024), 0, s,
+                                            A.tileStart, sortedVals, A.recA, A.recB, A.expTable, A.tileQueue, t0,
+                                            numTiles, g.tilesX, g.width, g.height, (uint8_t*)color, colorPitch,
+                                            (uint8_t*)depth, depthPitch, flags, costOrder ? A.unitOrder : nullptr,
+                                            A.unitCost, A.blendTrace);
+        else hipLaunchKernelGGL((k_blend_px<512, 2, true, 0, true>), dim3(grid), dim3(512), 0, s, A.tileStart,
+                                sortedVals, A.recA, A.recB, A.expTable, A.tileQueue, t0, numTiles, g.tilesX,
+                                g.width, g.height, (uint8_t*)color, colorPitch, (uint8_t*)depth, depthPitch, flags,
+                                costOrder ? A.unitOrder : nullptr, A.unitCost, A.blendTrace);
         return;
     }
     if (waves == 16) {

@@ -32,6 +32,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "gsm-renderer_amd"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec); measured copy ceiling ~6290
+VALU_PEAK_GIPS = 1024 * 2.4 / 4  # wave64 packed-fp16 VALU instructions per ns, whole chip
 
 
 def parse():
@@ -43,7 +44,8 @@ def parse():
     p.add_argument("--cpu-baseline", type=int, default=1, help="time the C oracle (rank 0, N=1)")
     p.add_argument("--cpu-threads", type=int, default=16)
     p.add_argument("--parity", type=int, default=1, help="compare the frame with the oracle")
-    p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
+    p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"),
+                   help="blend HBM bytes and VALU instructions per launch (tools/traffic.py)")
     p.add_argument("--multi", choices=("alltoall", "replicas"), default="alltoall",
                    help="N>1 partition: all-to-all of projected records (8e) or projection replicas")
     return p.parse_args()
@@ -179,10 +181,13 @@ def main():
     t_blend = blend_ms_timed * 1e-3
     achieved = b_blend / t_blend / 1e9 if t_blend > 0 else 0.0
     traffic = None
+    valu_insts = None
     if os.path.exists(args.traffic_json):
         try:
             with open(args.traffic_json) as f:
-                traffic = json.load(f).get("blend_hbm_bytes_per_launch")
+                tj = json.load(f)
+            traffic = tj.get("blend_hbm_bytes_per_launch")
+            valu_insts = tj.get("blend_valu_insts_per_launch")
         except Exception:
             traffic = None
     sort_gkeys = A / (stage_ms["sort"] * 1e-3) / 1e9 if stage_ms["sort"] > 0 else 0.0
@@ -239,6 +244,16 @@ def main():
                      "algorithmic_bytes": b_blend, "avg_launch_ms": blend_ms_timed,
                      "note": "blend is VALU/LDS-bound (fp16 math per pixel per entry); HBM fraction "
                              "reported per the metric"},
+        # the blend's real bound: packed-fp16 VALU issue.  Peak = 1024 SIMDs x one wave64
+        # v_pk_* instruction per 4 cycles x 2.4 GHz (measured issue cost of v_pk_mul_f16 with
+        # >= 2 waves per SIMD: tools/exp/valu_lat.hip); instructions per launch from the
+        # SQ_INSTS_VALU PMC pass of tools/gpu_round.sh (config 2 only).
+        "roofline_valu": ({"bound": "valu", "kernel": "k_blend", "unit": "G wave-instr/s",
+                           "achieved": valu_insts / t_blend / 1e9, "peak": VALU_PEAK_GIPS,
+                           "frac": valu_insts / t_blend / 1e9 / VALU_PEAK_GIPS,
+                           "insts_per_launch": valu_insts}
+                          if (valu_insts and t_blend > 0 and args.config == "cfg2_1m_sh3_1080p_f16"
+                              and world_size == 1) else None),
         "cpu_baseline": cpu,
         "stages_ms": stage_ms,
         "sort_gkeys_per_s": sort_gkeys,

@@ -30,6 +30,8 @@ for k, cs in acc.items():
         "write_size_kb": round(w, 1),
         "correction": "FETCH_SIZE x2 (gfx950 counts half of wide reads), WRITE_SIZE exact",
         "blend_hbm_bytes_per_launch": int(round((2 * f + w) * 1024)),
+        "blend_valu_insts_per_launch": (int(round(sum(cs["SQ_INSTS_VALU"]) / len(cs["SQ_INSTS_VALU"])))
+                                        if "SQ_INSTS_VALU" in cs else None),
         "note": "includes each workgroup's 128 KiB exp-table load and the re-reads of a tile's list by "
                 "both half-tile units; Infinity-Cache hits are counted by these fabric counters",
     }

@@ -186,8 +186,9 @@ def main():
         try:
             with open(args.traffic_json) as f:
                 tj = json.load(f)
-            traffic = tj.get("blend_hbm_bytes_per_launch")
-            valu_insts = tj.get("blend_valu_insts_per_launch")
+            if tj.get("config") == args.config and world_size == 1:  # measured on this workload only
+                traffic = tj.get("blend_hbm_bytes_per_launch")
+                valu_insts = tj.get("blend_valu_insts_per_launch")
         except Exception:
             traffic = None
     sort_gkeys = A / (stage_ms["sort"] * 1e-3) / 1e9 if stage_ms["sort"] > 0 else 0.0
@@ -252,8 +253,7 @@ def main():
                            "achieved": valu_insts / t_blend / 1e9, "peak": VALU_PEAK_GIPS,
                            "frac": valu_insts / t_blend / 1e9 / VALU_PEAK_GIPS,
                            "insts_per_launch": valu_insts}
-                          if (valu_insts and t_blend > 0 and args.config == "cfg2_1m_sh3_1080p_f16"
-                              and world_size == 1) else None),
+                          if (valu_insts and t_blend > 0) else None),
         "cpu_baseline": cpu,
         "stages_ms": stage_ms,
         "sort_gkeys_per_s": sort_gkeys,

@@ -17,11 +17,6 @@ step() {  # name timeout cmd...   (stdout+stderr -> $OUT/name.log; crash/timeout
 }
 step pytest_gpu 600 python -u -m pytest tests -m gpu -v --timeout 120 --timeout-method thread
 step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
-step bench_cfg2 600 python bench.py
-step bench_cfg3 600 python bench.py --config cfg3_5m_sh3_4k_f16 --steps 30 --warmup 3
-step bench_cfg5 600 python bench.py --config cfg5_1m_sh2_stereo_2x1440x1600_f16 --steps 30 --warmup 3
-step kernel_trace 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/kt -o run -- \
-     python bench.py --steps 50 --warmup 5 --cpu-baseline 0 --parity 0
 CMD="python bench.py --steps 10 --warmup 3 --cpu-baseline 0 --parity 0"
 i=0
 for set in "FETCH_SIZE" "WRITE_SIZE" \
@@ -33,4 +28,9 @@ done
 python tools/pmc_summary.py $OUT/pmc > $OUT/pmc_summary.txt
 python tools/traffic.py $OUT/pmc > $OUT/traffic.json
 cat $OUT/traffic.json
+step bench_cfg2 600 python bench.py --traffic-json $OUT/traffic.json
+step bench_cfg3 600 python bench.py --traffic-json $OUT/traffic.json --config cfg3_5m_sh3_4k_f16 --steps 30 --warmup 3
+step bench_cfg5 600 python bench.py --traffic-json $OUT/traffic.json --config cfg5_1m_sh2_stereo_2x1440x1600_f16 --steps 30 --warmup 3
+step kernel_trace 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/kt -o run -- \
+     python bench.py --traffic-json $OUT/traffic.json --steps 50 --warmup 5 --cpu-baseline 0 --parity 0
 echo "=== done"

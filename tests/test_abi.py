@@ -9,11 +9,12 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HEADERS = [os.path.join(ROOT, "include", h) for h in ("gsm_renderer.h", "gsm_debug.h", "gsm_multigpu.h")]
+PLY_HEADER = os.path.join(ROOT, "include", "gsm_ply.h")
 
 
-def declared_functions():
+def declared_functions(headers=HEADERS):
     names = set()
-    for h in HEADERS:
+    for h in headers:
         src = open(h).read()
         src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
         for m in re.finditer(r"\b(gsm_[a-z0-9_]+)\s*\(", src):
@@ -30,6 +31,15 @@ def test_library_exports_every_declared_symbol(gsm):
                          text=True, check=True).stdout
     exported = set(re.findall(r" T (gsm_[a-z0-9_]+)", out))
     assert set(declared_functions()) <= exported
+
+
+def test_ply_header_symbols_exported_and_bound(gsm):
+    from gsm_amd import ply
+    names = set(declared_functions([PLY_HEADER]))
+    assert names == set(ply._SIG), "the ply binding must cover include/gsm_ply.h"
+    out = subprocess.run(["nm", "-D", "--defined-only", gsm.library_path()], capture_output=True,
+                         text=True, check=True).stdout
+    assert names <= set(re.findall(r" T (gsm_[a-z0-9_]+)", out))
 
 
 def test_library_has_no_unresolved_internal_symbols(gsm):

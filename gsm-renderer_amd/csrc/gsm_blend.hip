@@ -60,6 +60,7 @@ __device__ __forceinline__ void blend_wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+constexpr bool kBlendU4 = false;  // 4-entry groups at P = 2 (measured: no gain)
 template <int NT, int P, bool EXECM, int EXPT = 0, bool COMPACT = false>
 __global__ __launch_bounds__(NT) void k_blend_px(
     const uint32_t* __restrict__ tileStart, const uint32_t* __restrict__ sortedVals,
@@ -71,7 +72,7 @@ __global__ __launch_bounds__(NT) void k_blend_px(
     unsigned long long* __restrict__ trace) {
     static_assert(P == 1 || P == 2 || P == 4, "pairs per lane");
     static_assert(!COMPACT || (P == 2 && EXECM), "compaction: half tiles, EXEC-masked updates");
-    constexpr uint32_t U = 4 / P;        // entries per pipeline group
+    constexpr uint32_t U = (P == 2 && kBlendU4) ? 4 : 4 / P;  // entries per pipeline group
     constexpr uint32_t NG = 64 / U;      // groups per 64-entry batch
     constexpr uint32_t EXITG = 16 / U;   // exit test every 16 entries
     constexpr uint32_t UPT = 4 / P;      // units per tile

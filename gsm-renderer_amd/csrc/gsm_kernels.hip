@@ -815,25 +815,47 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_blocks(uint32_t* __restri
                                                               TileAssignmentHeader* __restrict__ hdr,
                                                               uint32_t* __restrict__ blendQueue) {
     __shared__ uint32_t lds[kScanThreads / 64];
-    const uint32_t per = (nb + kScanThreads - 1) / kScanThreads;
-    const uint32_t b0 = threadIdx.x * per;
-    uint64_t local = 0;
-    for (uint32_t i = 0; i < per; ++i) {
-        uint32_t idx = b0 + i;
-        if (idx < nb) local += sums[idx];
-    }
-    uint32_t loc32 = local > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)local;
-    uint32_t total;
-    uint32_t off = block_exclusive_scan<kScanThreads>(loc32, lds, &total);
-    uint32_t run = off;
-    for (uint32_t i = 0; i < per; ++i) {
-        uint32_t idx = b0 + i;
-        if (idx < nb) {
-            uint32_t v = sums[idx];
-            sums[idx] = run;
-            run += v;
+    // rows of 4 * kScanThreads block sums, kScanRows rows in flight: thread t holds sums
+    // [row * 4096 + 4t, +4) as one 16-byte load, so every load of a pass is issued before the
+    // first scan (the sums are read once and written once)
+    constexpr uint32_t kRow = 4u * kScanThreads, kScanRows = 8;
+    const uint32_t t4 = threadIdx.x * 4u;
+    uint64_t carry = 0;
+    for (uint32_t base = 0; base < nb; base += kScanRows * kRow) {
+        uint4 v[kScanRows];
+#pragma unroll
+        for (uint32_t r = 0; r < kScanRows; ++r) {
+            const uint32_t i = base + r * kRow + t4;
+            v[r] = i + 3u < nb ? *(const uint4*)(sums + i)
+                               : make_uint4(i < nb ? sums[i] : 0u, i + 1u < nb ? sums[i + 1u] : 0u,
+                                            i + 2u < nb ? sums[i + 2u] : 0u, 0u);
+        }
+#pragma unroll
+        for (uint32_t r = 0; r < kScanRows; ++r) {
+            const uint32_t row0 = base + r * kRow;
+            if (row0 >= nb) break;
+            uint32_t tot;
+            const uint32_t off = block_exclusive_scan<kScanThreads>(v[r].x + v[r].y + v[r].z + v[r].w, lds, &tot);
+            uint64_t run = carry + off;
+            const uint32_t in[4] = {v[r].x, v[r].y, v[r].z, v[r].w};
+            uint32_t o[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                o[j] = run > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)run;
+                run += in[j];
+            }
+            const uint32_t i = row0 + t4;
+            if (i + 3u < nb) {
+                *(uint4*)(sums + i) = make_uint4(o[0], o[1], o[2], o[3]);
+            } else {
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    if (i + (uint32_t)j < nb) sums[i + j] = o[j];
+            }
+            carry += tot;
         }
     }
+    const uint32_t total = carry > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)carry;
     if (threadIdx.x == 0) {
         uint32_t tot = total;
         uint32_t ovf = 0;

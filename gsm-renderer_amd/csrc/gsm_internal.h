@@ -101,8 +101,8 @@ void launch_blend(const uint32_t* sortedVals, const FrameGeometry& geo, const De
 // the dynamic queue hands out long units before short ones
 void launch_unit_order(uint32_t numUnits, const DeviceArena& A, hipStream_t stream);
 // blend kernel shape: pixel pairs per lane (0 = quadrant kernel) and blend units per tile
-int blend_pairs_per_lane();
-uint32_t blend_units_per_tile();
+int blend_pairs_per_lane(uint32_t numTiles, int numCUs);
+uint32_t blend_units_per_tile(uint32_t numTiles, int numCUs);
 // whether the blend follows last frame's cost order (few units per wave slot) or index order
 bool blend_schedule_enabled(uint32_t numTiles, int numCUs);
 

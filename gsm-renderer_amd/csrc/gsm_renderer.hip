@@ -313,7 +313,7 @@ gsm_status GlobalRenderer::runFrame(hipStream_t s, const ProjectArgs& a, uint32_
     // geometry measured (the image does not depend on the order, only the load balance does).
     // The ordering kernel only needs those costs, so it runs on a side stream beside this
     // frame's projection and sort.
-    const uint32_t upt = blend_units_per_tile();
+    const uint32_t upt = blend_units_per_tile((rowEnd_ - rowBegin_) * tilesX_, numCUs_);
     const uint32_t units = (rowEnd_ - rowBegin_) * tilesX_ * upt;
     const uint64_t key = ((uint64_t)upt << 60) ^ ((uint64_t)width << 40) ^ ((uint64_t)height << 20) ^
                          ((uint64_t)rowBegin_ << 10) ^ rowEnd_;

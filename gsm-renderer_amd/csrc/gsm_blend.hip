@@ -10,6 +10,8 @@
 
 #include <cstdlib>
 
+#include "../../include/gsm_renderer.h"
+#include "gsm_detmath.h"
 #include "gsm_internal.h"
 #include "gsm_types.h"
 
@@ -20,6 +22,11 @@ typedef _Float16 h2 __attribute__((ext_vector_type(2)));
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ h2 as_h2(uint32_t u) { return __builtin_bit_cast(h2, u); }
+__device__ __forceinline__ float h_bits_to_f(uint16_t b) { return (float)__builtin_bit_cast(h1, b); }
+// linear -> sRGB encode of a [0, 1] value (include/gsm_renderer.h), powr of the numeric contract
+__device__ __forceinline__ float srgb_encode(float c) {
+    return c <= 0.0031308f ? c * 12.92f : 1.055f * det_powrf(c, 1.0f / 2.4f) - 0.055f;
+}
 __device__ __forceinline__ uint32_t as_u32(h2 v) { return __builtin_bit_cast(uint32_t, v); }
 __device__ __forceinline__ h2 splat_lo(h2 v) { return h2{v.x, v.x}; }
 __device__ __forceinline__ h2 splat_hi(h2 v) { return h2{v.y, v.y}; }
@@ -89,32 +96,71 @@ __global__ __launch_bounds__(NT) void k_blend_px(
     __syncthreads();
 
     const uint32_t lane = threadIdx.x & 63;
-    // write (GlobalShaders.metal:1152-1186): one pixel pair (px, py), (px + 1, py)
+    // write (GlobalShaders.metal:1152-1186): one pixel pair (px, py), (px + 1, py) in the target's
+    // format (flags bits 4-7, gsm_color_format; conversion rules in include/gsm_renderer.h)
+    const int colorFmt = (flags >> 4) & 15;
     auto write_pair = [&](uint32_t px, uint32_t py, h2 Av, h2 Rq, h2 Gq, h2 Bq, h2 Dq) {
         if (py >= H) return;
         uint8_t* crow = color + (size_t)py * colorPitch;
         // integer packing (extracting .y of a half2 via __builtin_bit_cast miscompiled)
         const uint32_t ur = as_u32(Rq), ug = as_u32(Gq), ub = as_u32(Bq), ua = as_u32(Av);
-        const uint32_t p0a = (ur & 0xFFFFu) | (ug << 16);
-        const uint32_t p0b = (ub & 0xFFFFu) | (ua << 16);
-        const uint32_t p1a = (ur >> 16) | (ug & 0xFFFF0000u);
-        const uint32_t p1b = (ub >> 16) | (ua & 0xFFFF0000u);
         const uint32_t ud = as_u32(Dq);
-        if ((flags & 1) && px + 1 < W) {
-            *(uint4*)(crow + (size_t)px * 8) = make_uint4(p0a, p0b, p1a, p1b);
-            if (depth) *(uint32_t*)(depth + (size_t)py * depthPitch + (size_t)px * 2) = ud;
-        } else {
-            if (px < W) {
-                uint32_t* c0 = (uint32_t*)(crow + (size_t)px * 8);
-                c0[0] = p0a;
-                c0[1] = p0b;
-                if (depth) *(uint16_t*)(depth + (size_t)py * depthPitch + (size_t)px * 2) = (uint16_t)(ud & 0xFFFFu);
+        if (colorFmt == GSM_COLOR_FORMAT_RGBA16F) {
+            const uint32_t p0a = (ur & 0xFFFFu) | (ug << 16);
+            const uint32_t p0b = (ub & 0xFFFFu) | (ua << 16);
+            const uint32_t p1a = (ur >> 16) | (ug & 0xFFFF0000u);
+            const uint32_t p1b = (ub >> 16) | (ua & 0xFFFF0000u);
+            if ((flags & 1) && px + 1 < W) {
+                *(uint4*)(crow + (size_t)px * 8) = make_uint4(p0a, p0b, p1a, p1b);
+            } else {
+                if (px < W) {  // 4-byte stores: any 4-byte aligned pitch
+                    ((uint32_t*)(crow + (size_t)px * 8))[0] = p0a;
+                    ((uint32_t*)(crow + (size_t)px * 8))[1] = p0b;
+                }
+                if (px + 1 < W) {
+                    ((uint32_t*)(crow + (size_t)(px + 1) * 8))[0] = p1a;
+                    ((uint32_t*)(crow + (size_t)(px + 1) * 8))[1] = p1b;
+                }
             }
-            if (px + 1 < W) {
-                uint32_t* c1 = (uint32_t*)(crow + (size_t)(px + 1) * 8);
-                c1[0] = p1a;
-                c1[1] = p1b;
-                if (depth) *(uint16_t*)(depth + (size_t)py * depthPitch + (size_t)(px + 1) * 2) = (uint16_t)(ud >> 16);
+        } else {
+#pragma unroll
+            for (uint32_t i = 0; i < 2; ++i) {
+                if (px + i >= W) break;
+                const uint32_t sh = 16u * i;
+                float c[4] = {h_bits_to_f((uint16_t)(ur >> sh)), h_bits_to_f((uint16_t)(ug >> sh)),
+                              h_bits_to_f((uint16_t)(ub >> sh)), h_bits_to_f((uint16_t)(ua >> sh))};
+                if (colorFmt == GSM_COLOR_FORMAT_RGBA32F) {
+                    float* o = (float*)(crow + (size_t)(px + i) * 16);
+                    if (flags & 1) {
+                        *(float4*)o = make_float4(c[0], c[1], c[2], c[3]);
+                    } else {
+                        o[0] = c[0];
+                        o[1] = c[1];
+                        o[2] = c[2];
+                        o[3] = c[3];
+                    }
+                    continue;
+                }
+                const bool srgb = colorFmt == GSM_COLOR_FORMAT_RGBA8_UNORM_SRGB ||
+                                  colorFmt == GSM_COLOR_FORMAT_BGRA8_UNORM_SRGB;
+                uint32_t u8[4];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    float x = __builtin_fminf(__builtin_fmaxf(c[k], 0.0f), 1.0f);
+                    if (srgb && k < 3) x = srgb_encode(x);
+                    u8[k] = (uint32_t)__builtin_rintf(x * 255.0f);
+                }
+                const bool bgra = colorFmt >= GSM_COLOR_FORMAT_BGRA8_UNORM;
+                const uint32_t px32 = (bgra ? u8[2] : u8[0]) | (u8[1] << 8) | ((bgra ? u8[0] : u8[2]) << 16) | (u8[3] << 24);
+                *(uint32_t*)(crow + (size_t)(px + i) * 4) = px32;
+            }
+        }
+        if (depth) {
+            if ((flags & 1) && px + 1 < W) {
+                *(uint32_t*)(depth + (size_t)py * depthPitch + (size_t)px * 2) = ud;
+            } else {
+                if (px < W) *(uint16_t*)(depth + (size_t)py * depthPitch + (size_t)px * 2) = (uint16_t)(ud & 0xFFFFu);
+                if (px + 1 < W) *(uint16_t*)(depth + (size_t)py * depthPitch + (size_t)(px + 1) * 2) = (uint16_t)(ud >> 16);
             }
         }
     };
@@ -830,7 +876,7 @@ void launch_unit_order(uint32_t numUnits, const DeviceArena& A, hipStream_t s) {
 }
 
 void launch_blend(const uint32_t* sortedVals, const FrameGeometry& g, const DeviceArena& A, void* color,
-                  size_t colorPitch, void* depth, size_t depthPitch, int numCUs, bool costOrder,
+                  size_t colorPitch, void* depth, size_t depthPitch, int numCUs, bool costOrder, int colorFormat,
                   hipStream_t s) {
     const uint32_t t0 = g.rowBegin * g.tilesX, t1 = g.rowEnd * g.tilesX;
     if (t1 <= t0) return;
@@ -841,7 +887,8 @@ void launch_blend(const uint32_t* sortedVals, const FrameGeometry& g, const Devi
                         : 0;
     const char* pv = getenv("GSM_BLEND_PRIO");  // age-raised wave priority (default on)
     const char* sp = getenv("GSM_BLEND_SPLIT");  // long units on half the waves at top priority
-    const int flags = vec | ((pv && pv[0] == '0') ? 0 : 2) | ((costOrder && !(sp && sp[0] == '0')) ? 4 : 0);
+    const int flags = vec | ((pv && pv[0] == '0') ? 0 : 2) | ((costOrder && !(sp && sp[0] == '0')) ? 4 : 0) |
+                      ((colorFormat & 15) << 4);
     // A.tileQueue was zeroed by k_scan_blocks earlier in the frame
     const int P = blend_pairs_per_lane(numTiles, numCUs);
     const int waves = blend_waves_per_wg(numTiles, numCUs);

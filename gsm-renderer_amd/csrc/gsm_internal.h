@@ -96,7 +96,7 @@ void launch_headers(const uint32_t* sortedKeys, const FrameGeometry& geo, const 
 // front-to-back fp16 blend + clear (GlobalShaders.metal:140-154, 1030-1187)
 void launch_blend(const uint32_t* sortedVals, const FrameGeometry& geo, const DeviceArena& A,
                   void* color, size_t colorPitch, void* depth, size_t depthPitch, int numCUs,
-                  bool costOrder, hipStream_t stream);
+                  bool costOrder, int colorFormat, hipStream_t stream);
 // orders the blend units by the walk lengths the previous frame measured (longest first), so
 // the dynamic queue hands out long units before short ones
 void launch_unit_order(uint32_t numUnits, const DeviceArena& A, hipStream_t stream);

@@ -56,6 +56,7 @@ gsm_status GlobalRenderer::create(const gsm_renderer_config& cfg, int hipDevice,
     if (cfg.max_gaussians > kMaxSupportedGaussians) return GSM_ERR_INVALID_GAUSSIAN_COUNT;
     if (cfg.precision != GSM_PRECISION_FLOAT32 && cfg.precision != GSM_PRECISION_FLOAT16)
         return GSM_ERR_INVALID_ARGUMENT;
+    if (cfg.color_format > GSM_COLOR_FORMAT_BGRA8_UNORM_SRGB) return GSM_ERR_INVALID_ARGUMENT;
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
         (void)hipGetLastError();
@@ -219,7 +220,12 @@ gsm_status GlobalRenderer::validateFrame(uint32_t count, bool inputMissing, uint
         return GSM_ERR_INVALID_DIMENSIONS;
     if (!color) return GSM_ERR_MISSING_REQUIRED_BUFFER;
     if (count > 0 && inputMissing) return GSM_ERR_MISSING_REQUIRED_BUFFER;
-    if (colorPitch < (size_t)width * 8) return GSM_ERR_INVALID_BUFFER_SIZE;
+    const size_t bpp = config_.color_format == GSM_COLOR_FORMAT_RGBA16F ? 8
+                       : (config_.color_format == GSM_COLOR_FORMAT_RGBA32F ? 16 : 4);
+    if (colorPitch < (size_t)width * bpp) return GSM_ERR_INVALID_BUFFER_SIZE;
+    // the blend stores at least 4-byte words of colour and 2-byte depth values
+    if ((((uintptr_t)color) & 3u) || (colorPitch & 3u)) return GSM_ERR_INVALID_BUFFER_SIZE;
+    if (depth && ((((uintptr_t)depth) & 1u) || (depthPitch & 1u))) return GSM_ERR_INVALID_BUFFER_SIZE;
     if (depth && depthPitch < (size_t)width * 2) return GSM_ERR_INVALID_BUFFER_SIZE;
     if (hipSetDevice(device_) != hipSuccess) return GSM_ERR_DEVICE_NOT_AVAILABLE;
     return GSM_OK;
@@ -387,7 +393,8 @@ gsm_status GlobalRenderer::runFrame(hipStream_t s, const ProjectArgs& a, uint32_
     arena_.blendTrace = (profiling_ & 4) ? traceBuf_ : nullptr;
     if (costOrder) hipStreamWaitEvent(s, evOrder_, 0);
     if (prof || blendOnly) hipEventRecord(ev[5], s);
-    launch_blend(sortedVals_, g, arena_, color, colorPitch, depth, depthPitch, numCUs_, costOrder, s);
+    launch_blend(sortedVals_, g, arena_, color, colorPitch, depth, depthPitch, numCUs_, costOrder,
+                 (int)config_.color_format, s);
     if (prof || blendOnly) hipEventRecord(ev[6], s);
     if (prof || blendOnly) profFrames_++;
     haveTimes_ = profFrames_ > 0;

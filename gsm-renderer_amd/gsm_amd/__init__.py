@@ -67,6 +67,21 @@ class GaussianColorSpace(enum.IntEnum):  # GaussianRendererProtocol.swift:196-20
     SRGB = 1
 
 
+class ColorFormat(enum.IntEnum):
+    """Colour target pixel format (RendererConfig.colorFormat, GaussianRendererProtocol.swift:207;
+    include/gsm_renderer.h gsm_color_format has the conversion rules)."""
+    RGBA16F = 0
+    RGBA32F = 1
+    RGBA8_UNORM = 2
+    RGBA8_UNORM_SRGB = 3
+    BGRA8_UNORM = 4
+    BGRA8_UNORM_SRGB = 5
+
+    @property
+    def bytes_per_pixel(self) -> int:
+        return 8 if self == ColorFormat.RGBA16F else (16 if self == ColorFormat.RGBA32F else 4)
+
+
 class BufferId(enum.IntEnum):  # include/gsm_debug.h gsm_buffer_id
     RENDER_DATA = 0
     BOUNDS = 1
@@ -268,6 +283,7 @@ class GlobalRenderer:
         _check(L.gsm_global_create(C.byref(cfg), dev, C.byref(h)), "gsm_global_create")
         self._h = h
         self.device = dev
+        self._bpp = ColorFormat(int(config.color_format)).bytes_per_pixel
 
     def close(self):
         if getattr(self, "_h", None) and self._h.value:
@@ -287,7 +303,7 @@ class GlobalRenderer:
         inp = _Input(_ptr(input.gaussians), _ptr(input.harmonics), int(input.gaussian_count),
                      int(input.sh_components))
         cam = _camera_struct(camera)
-        cp = color_pitch if color_pitch is not None else int(width) * 8
+        cp = color_pitch if color_pitch is not None else int(width) * self._bpp
         dp = depth_pitch if depth_pitch is not None else int(width) * 2
         st = _lib().gsm_global_render(self._h, _stream_handle(stream), C.byref(inp), C.byref(cam),
                                       int(width), int(height), _ptr(color_texture), cp,
@@ -313,7 +329,7 @@ class GlobalRenderer:
     def render_records(self, color_texture, depth_texture, records, count: int, width: int, height: int,
                        stream=None, color_pitch: Optional[int] = None, depth_pitch: Optional[int] = None):
         """gsm_global_render_records: this renderer's tile rows from `count` received records."""
-        cp = color_pitch if color_pitch is not None else int(width) * 8
+        cp = color_pitch if color_pitch is not None else int(width) * self._bpp
         dp = depth_pitch if depth_pitch is not None else int(width) * 2
         st = _lib().gsm_global_render_records(self._h, _stream_handle(stream), _ptr(records), int(count),
                                               int(width), int(height), _ptr(color_texture), cp,
@@ -337,7 +353,7 @@ class GlobalRenderer:
         inp = _Input(_ptr(input.gaussians), _ptr(input.harmonics), int(input.gaussian_count),
                      int(input.sh_components))
         cl, cr = _camera_struct(left), _camera_struct(right)
-        cp = color_pitch if color_pitch is not None else 2 * int(width_per_eye) * 8
+        cp = color_pitch if color_pitch is not None else 2 * int(width_per_eye) * self._bpp
         dp = depth_pitch if depth_pitch is not None else 2 * int(width_per_eye) * 2
         st = _lib().gsm_global_render_stereo_sbs(self._h, _stream_handle(stream), C.byref(inp), C.byref(cl),
                                                  C.byref(cr), int(width_per_eye), int(height),

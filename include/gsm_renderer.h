@@ -48,14 +48,33 @@ typedef enum { GSM_PRECISION_FLOAT32 = 0, GSM_PRECISION_FLOAT16 = 1 } gsm_precis
 /* RendererConfig.GaussianColorSpace (GaussianRendererProtocol.swift:196-201). */
 typedef enum { GSM_COLOR_SPACE_LINEAR = 0, GSM_COLOR_SPACE_SRGB = 1 } gsm_color_space;
 
-/* RendererConfig (GaussianRendererProtocol.swift:195-228).  color_format and
- * back_to_front are accepted and ignored, as in the reference Global path. */
+/* Pixel format of the colour target (RendererConfig.colorFormat, GaussianRendererProtocol.swift:207;
+ * the reference's Global path writes half4 into whatever texture it is given and Metal converts
+ * on the write, GlobalShaders.metal:1155-1186).  With raw device pointers the format of the
+ * target is declared here.  Conversion of the blended fp16 value c (alpha = 1 - T):
+ *   RGBA16F: as is (8 B/px);  RGBA32F: exact widening (16 B/px);
+ *   *8_UNORM: u8 = RTNE(clamp(c, 0, 1) * 255), clamp by IEEE maxNum/minNum (NaN -> 0) (4 B/px);
+ *   *8_UNORM_SRGB: the same after the linear->sRGB encode of R, G, B:
+ *     c <= 0.0031308 ? 12.92 c : 1.055 powr(c, 1 / 2.4) - 0.055 (fp32, powr of the numeric contract).
+ * BGRA formats store B, G, R, A.  The Metal rounding of unorm / sRGB writes is not specified
+ * to the bit: parity for the 8-bit formats is against this definition. */
+typedef enum {
+    GSM_COLOR_FORMAT_RGBA16F = 0,
+    GSM_COLOR_FORMAT_RGBA32F = 1,
+    GSM_COLOR_FORMAT_RGBA8_UNORM = 2,
+    GSM_COLOR_FORMAT_RGBA8_UNORM_SRGB = 3,
+    GSM_COLOR_FORMAT_BGRA8_UNORM = 4,
+    GSM_COLOR_FORMAT_BGRA8_UNORM_SRGB = 5 /* the reference's RendererConfig default (.bgra8Unorm_srgb) */
+} gsm_color_format;
+
+/* RendererConfig (GaussianRendererProtocol.swift:195-228).  back_to_front is accepted and
+ * ignored, as in the reference Global path. */
 typedef struct {
     uint32_t max_gaussians;        /* default 6_000_000, <= 30_000_000 (GlobalRenderer.swift:73) */
     uint32_t max_width;            /* default 1920 */
     uint32_t max_height;           /* default 1080 */
     uint32_t precision;            /* gsm_precision, default FLOAT16 */
-    uint32_t color_format;         /* opaque pixel-format tag, ignored */
+    uint32_t color_format;         /* gsm_color_format of the colour target, default RGBA16F */
     uint32_t gaussian_color_space; /* gsm_color_space, default SRGB */
     uint32_t back_to_front;        /* ignored */
 } gsm_renderer_config;
@@ -102,8 +121,8 @@ void gsm_global_destroy(gsm_renderer *renderer);
 /* GlobalRenderer.render(commandBuffer:colorTexture:depthTexture:input:camera:width:height:)
  * (GlobalRenderer.swift:201-238; protocol GaussianRendererProtocol.swift:248-256).
  * Enqueue-only on `stream` (the analogue of encoding into the caller's command
- * buffer; the caller synchronises).  color: rgba16Float, height rows of
- * color_pitch bytes; depth: r16Float or NULL (the reference then renders into
+ * buffer; the caller synchronises).  color: config.color_format (rgba16Float by default),
+ * height rows of color_pitch bytes; depth: r16Float or NULL (the reference then renders into
  * its own internal depth texture, GlobalRenderer.swift:350).  Returns an error
  * where the reference silently skips the frame (GlobalRenderer.swift:295-299). */
 gsm_status gsm_global_render(gsm_renderer *renderer, void *stream, const gsm_gaussian_input *input,

@@ -1121,3 +1121,40 @@ void og_make_camera(uint32_t width, uint32_t height, og_camera *cam) {
     cam->near_plane = nearp;
     cam->far_plane = farp;
 }
+
+/* Metal's conversion of the half4 a texture write stores (GlobalShaders.metal:1155-1186) into the
+ * target's pixel format, as declared in include/gsm_renderer.h: unorm8 = RTNE(clamp * 255) with
+ * IEEE maxNum/minNum clamping (NaN -> 0); sRGB formats encode R, G, B first with
+ * c <= 0.0031308 ? 12.92 c : 1.055 powr(c, 1 / 2.4) - 0.055 (fp32, contract powr). */
+static float og_clamp01(float x) {
+    x = (x > 0.0f || x != x) ? (x != x ? 0.0f : x) : 0.0f; /* maxNum(x, 0) */
+    return x < 1.0f ? x : 1.0f;                               /* minNum(x, 1) */
+}
+static uint32_t og_unorm8(float x) { return (uint32_t)nearbyintf(x * 255.0f); }
+int og_convert_color(const uint16_t *src, size_t n, int format, void *dst) {
+    ensure_init();
+    if (format == 0) {
+        memcpy(dst, src, n * 8);
+        return 8;
+    }
+    for (size_t i = 0; i < n; ++i) {
+        float c[4];
+        for (int k = 0; k < 4; ++k) c[k] = g_h2f[src[4 * i + k]];
+        if (format == 1) {
+            memcpy((uint8_t *)dst + 16 * i, c, 16);
+            continue;
+        }
+        if (format < 2 || format > 5) return 0;
+        const int srgb = format == 3 || format == 5;
+        uint32_t u[4];
+        for (int k = 0; k < 4; ++k) {
+            float x = og_clamp01(c[k]);
+            if (srgb && k < 3) x = x <= 0.0031308f ? x * 12.92f : 1.055f * ogm_powrf(x, 1.0f / 2.4f) - 0.055f;
+            u[k] = og_unorm8(x);
+        }
+        const int bgra = format >= 4;
+        const uint32_t p = (bgra ? u[2] : u[0]) | (u[1] << 8) | ((bgra ? u[0] : u[2]) << 16) | (u[3] << 24);
+        memcpy((uint8_t *)dst + 4 * i, &p, 4);
+    }
+    return format == 1 ? 16 : 4;
+}

@@ -119,6 +119,11 @@ uint32_t og_sort_key(uint32_t tile, uint16_t depth_h);
 /* Stable LSD radix sort of (key,value) pairs, 8-bit digits (RadixSortEncoder.swift:41-101). */
 void og_radix_sort_pairs(uint32_t *keys, int32_t *values, uint32_t n);
 
+/* The colour target's pixel format (include/gsm_renderer.h gsm_color_format): converts n
+ * rgba16f pixels (the frame's colour) into dst -- 0 rgba16f copy, 1 rgba32f, 2 rgba8 unorm,
+ * 3 rgba8 unorm sRGB, 4 bgra8 unorm, 5 bgra8 unorm sRGB.  Returns bytes per pixel or 0. */
+int og_convert_color(const uint16_t *rgba16f, size_t n, int format, void *dst);
+
 /* fp16 helpers (round-to-nearest-even, IEEE binary16). */
 uint16_t og_f2h(float f);
 float og_h2f(uint16_t h);

@@ -93,6 +93,8 @@ def lib():
         for name in ("og_log2f", "og_exp2f"):
             getattr(L, name).argtypes = [C.c_float]
             getattr(L, name).restype = C.c_float
+        L.og_convert_color.argtypes = [C.c_void_p, C.c_size_t, C.c_int, C.c_void_p]
+        L.og_convert_color.restype = C.c_int
         L.og_srand48.argtypes = [C.c_long]
         L.og_drand48.restype = C.c_double
         L.og_gen_visible_gaussians.argtypes = [C.c_uint32, C.c_long, C.c_void_p, C.c_void_p]
@@ -144,6 +146,20 @@ def gen_grid_gaussians(count: int, seed: int = 42):
     harm = np.zeros(count * 3, np.float32)
     lib().og_gen_grid_gaussians(count, seed, world.ctypes.data, harm.ctypes.data)
     return world, harm
+
+
+def convert_color(color_u16: np.ndarray, fmt: int) -> np.ndarray:
+    """The frame's rgba16f colour (uint16 bits, [..., 4]) in target pixel format `fmt`
+    (include/gsm_renderer.h gsm_color_format): uint16 [..., 4], float32 [..., 4] or uint8 [..., 4]."""
+    src = np.ascontiguousarray(color_u16, np.uint16)
+    n = src.size // 4
+    shape = src.shape
+    if fmt == 0:
+        return src.copy()
+    out = np.zeros(shape, np.float32) if fmt == 1 else np.zeros(shape, np.uint8)
+    if lib().og_convert_color(src.ctypes.data, n, int(fmt), out.ctypes.data) == 0:
+        raise ValueError(f"unknown colour format {fmt}")
+    return out
 
 
 def radix_sort_pairs(keys: np.ndarray, values: np.ndarray):

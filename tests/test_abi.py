@@ -87,6 +87,14 @@ def test_create_rejects_too_many_gaussians_without_touching_the_gpu(gsm):
     assert e.value.status == gsm.Status.INVALID_GAUSSIAN_COUNT
 
 
+def test_create_rejects_unknown_color_format_without_touching_the_gpu(gsm):
+    # gsm_color_format: RGBA16F .. BGRA8_UNORM_SRGB (include/gsm_renderer.h)
+    with pytest.raises(gsm.RendererError) as e:
+        gsm.GlobalRenderer(config=gsm.RendererConfig(max_gaussians=1000, color_format=6))
+    assert e.value.status == gsm.Status.INVALID_ARGUMENT
+    assert [f.bytes_per_pixel for f in gsm.ColorFormat] == [8, 16, 4, 4, 4, 4]
+
+
 def test_create_without_device_reports_device_not_available(gsm):
     import torch
     if torch.cuda.is_available():

@@ -360,3 +360,33 @@ def test_full_size_config_bit_exact(gsm, cuda, oracle, cfg_name):
     assert r["overflow"] == 0
     assert_frame_equal(g, r)
     g["renderer"].close()
+
+
+@pytest.mark.parametrize("fmt", [1, 2, 3, 4, 5])
+def test_color_formats(gsm, cuda, oracle, fmt):
+    """The colour target in every gsm_color_format equals the oracle's rgba16f frame converted by
+    the declared rules (include/gsm_renderer.h; oracle.convert_color); depth stays r16f."""
+    case = _synth(20000, 320, 180, 9, 1, 21)
+    w, h = case["width"], case["height"]
+    ref = oracle_render(oracle, case)
+    want = oracle.convert_color(ref["color"], fmt)
+    r = gsm.GlobalRenderer(config=gsm.RendererConfig(max_gaussians=case["max_gaussians"], max_width=w,
+                                                      max_height=h, precision=1, color_format=fmt,
+                                                      gaussian_color_space=0))
+    dt = cuda.float32 if fmt == 1 else cuda.uint8
+    color = cuda.full((h, w, 4), 7, dtype=dt, device="cuda")
+    dep = cuda.full((h, w), float("nan"), dtype=cuda.float16, device="cuda")
+    inp = gsm.GaussianInput(to_dev(cuda, case["world"]), to_dev(cuda, case["harm"]), len(case["world"]), case["sh"])
+    r.render(color, dep, inp, gsm.CameraParams.from_dict(case["cam"]), w, h)
+    cuda.cuda.synchronize()
+    got = color.cpu().numpy()
+    if fmt == 1:
+        np.testing.assert_array_equal(got.view(np.uint32), want.view(np.uint32))
+    else:
+        np.testing.assert_array_equal(got, want)
+    np.testing.assert_array_equal(dep.view(cuda.int16).cpu().numpy().view(np.uint16), ref["depth"])
+    # an unaligned pitch is rejected, not written
+    with pytest.raises(gsm.RendererError):
+        r.render(color, dep, inp, gsm.CameraParams.from_dict(case["cam"]), w, h,
+                 color_pitch=w * gsm.ColorFormat(fmt).bytes_per_pixel + 2)
+    r.close()

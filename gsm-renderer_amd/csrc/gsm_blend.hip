@@ -68,6 +68,9 @@ __device__ __forceinline__ void blend_wave_sync() {
 }
 
 constexpr bool kBlendU4 = false;  // 4-entry groups at P = 2 (measured: no gain)
+// Records of the walk's current 64-entry batch staged in LDS and read back with uniform
+// addresses (one ds_read_b128 + one ds_read_b32 broadcast per entry) instead of 5 v_readlane.
+constexpr bool kLdsRecords = true;
 template <int NT, int P, bool EXECM, int EXPT = 0, bool COMPACT = false>
 __global__ __launch_bounds__(NT) void k_blend_px(
     const uint32_t* __restrict__ tileStart, const uint32_t* __restrict__ sortedVals,
@@ -88,6 +91,8 @@ __global__ __launch_bounds__(NT) void k_blend_px(
     const bool agePrio = (flags & 2) != 0;
     __shared__ __attribute__((aligned(16))) uint16_t tbl[65536];
     __shared__ uint32_t cscr[NW][16];  // compaction: the alive groups of each wave, in order
+    __shared__ __attribute__((aligned(16))) uint4 lrecA[kLdsRecords ? NW : 1][64];  // current batch records
+    __shared__ uint32_t lrecB[kLdsRecords ? NW : 1][64];
     {
         const uint4* src = (const uint4*)expTable;
         uint4* dst = (uint4*)tbl;
@@ -276,6 +281,11 @@ __global__ __launch_bounds__(NT) void k_blend_px(
                     pq[k] = ((dx * dx) * splat_lo(cc) + yy) + (dx * dy) * splat_lo(oc);
                 }
             };
+            if (kLdsRecords) {
+                lrecA[wv][lane] = bA;
+                lrecB[wv][lane] = bB;
+                blend_wave_sync();
+            }
             // prime group 0
 #pragma unroll
             for (uint32_t k = 0; k < U; ++k) {
@@ -297,6 +307,11 @@ __global__ __launch_bounds__(NT) void k_blend_px(
                     // stage 1: the next group's table words go in flight (independent of T)
                     {
                         const bool nb = gi + 1 == NG;
+                        if (kLdsRecords && nb) {  // every entry of this batch was read: stage the next one
+                            lrecA[wv][lane] = nA;
+                            lrecB[wv][lane] = nB;
+                            blend_wave_sync();
+                        }
                         const uint32_t sx = nb ? nA.x : bA.x, sy = nb ? nA.y : bA.y;
                         const uint32_t sz = nb ? nA.z : bA.z, sw = nb ? nA.w : bA.w;
                         const uint32_t sb = nb ? nB : bB;
@@ -304,10 +319,18 @@ __global__ __launch_bounds__(NT) void k_blend_px(
                         for (uint32_t k = 0; k < U; ++k) {
                             const uint32_t j = ((gi + 1) * U + k) & 63u;
                             h2 pq[P];
-                            opn[k] = __builtin_amdgcn_readlane(sz, j);
-                            quadform(__builtin_amdgcn_readlane(sx, j), __builtin_amdgcn_readlane(sy, j), opn[k], pq);
-                            rgn[k] = __builtin_amdgcn_readlane(sw, j);
-                            bdn[k] = __builtin_amdgcn_readlane(sb, j);
+                            if (kLdsRecords) {
+                                const uint4 ra = lrecA[wv][j];
+                                opn[k] = ra.z;
+                                quadform(ra.x, ra.y, ra.z, pq);
+                                rgn[k] = ra.w;
+                                bdn[k] = lrecB[wv][j];
+                            } else {
+                                opn[k] = __builtin_amdgcn_readlane(sz, j);
+                                quadform(__builtin_amdgcn_readlane(sx, j), __builtin_amdgcn_readlane(sy, j), opn[k], pq);
+                                rgn[k] = __builtin_amdgcn_readlane(sw, j);
+                                bdn[k] = __builtin_amdgcn_readlane(sb, j);
+                            }
 #pragma unroll
                             for (int q = 0; q < P; ++q) {
                                 // raw table words: first used in stage 3, after the current

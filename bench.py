@@ -46,6 +46,10 @@ def parse():
     p.add_argument("--parity", type=int, default=1, help="compare the frame with the oracle")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"),
                    help="blend HBM bytes and VALU instructions per launch (tools/traffic.py)")
+    p.add_argument("--stereo-path", choices=("depthfirst", "global"), default="depthfirst",
+                   help="stereo configs: DepthFirst semantics (SURVEY 8f rank 1) or two Global views")
+    p.add_argument("--df-max-gaussians", type=int, default=6_000_000,
+                   help="DepthFirst RendererConfig.maxGaussians (reference default 6M -> 24M instances)")
     p.add_argument("--multi", choices=("alltoall", "replicas"), default="alltoall",
                    help="N>1 partition: all-to-all of projected records (8e) or projection replicas")
     return p.parse_args()
@@ -83,6 +87,8 @@ def main():
     world_np, harm_np, cam_d = scenes.gen_scene(n, W, H, sh, prec, seed=42)
     world = torch.from_numpy(world_np.view(np.uint8).reshape(-1).copy()).to(dev)
     harm = torch.from_numpy(harm_np.view(np.uint8).reshape(-1).copy()).to(dev)
+    if stereo and args.stereo_path == "depthfirst":
+        return run_depthfirst(args, c, world_np, harm_np, world, harm, dev)
 
     cfg = gsm_amd.RendererConfig(max_gaussians=n, max_width=W, max_height=H, precision=prec,
                                  gaussian_color_space=gsm_amd.GaussianColorSpace.LINEAR)
@@ -264,6 +270,91 @@ def main():
     renderer.close()
     if world_size > 1:
         dist.destroy_process_group()
+
+
+def run_depthfirst(args, c, world_np, harm_np, world, harm, dev):
+    """Config 5 with DepthFirst stereo semantics (gsm_depthfirst_render_stereo_sbs): one frame =
+    both eyes side by side, projected once, 16x16 tiles blended for both eyes together."""
+    import torch
+
+    import gsm_amd
+    from gsm_amd import scenes
+    n, W, H, sh, prec, stereo = c["count"], c["width"], c["height"], c["sh"], c["precision"], c["stereo"]
+    cfg = gsm_amd.RendererConfig(max_gaussians=max(n, args.df_max_gaussians), max_width=W, max_height=H,
+                                 precision=prec, gaussian_color_space=gsm_amd.GaussianColorSpace.LINEAR)
+    renderer = gsm_amd.DepthFirstRenderer(device=dev.index, config=cfg)
+    color = torch.zeros((H, 2 * W, 4), dtype=torch.float16, device=dev)
+    inp = gsm_amd.GaussianInput(world, harm, n, sh)
+    cams = [scenes.make_camera(W, H, -stereo), scenes.make_camera(W, H, stereo)]
+    cam_l, cam_r = (gsm_amd.CameraParams.from_dict(x) for x in cams)
+    stream = torch.cuda.current_stream(dev)
+
+    def step():
+        renderer.render_stereo_sbs(color, inp, cam_l, cam_r, W, H, stream=stream)
+
+    for _ in range(args.warmup):
+        step()
+    renderer.set_profiling(stage_events=False, blend_events=True)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    blend_ms_timed = renderer.stage_times_ms()["blend"]
+    renderer.set_profiling(stage_events=True)
+    for _ in range(10):
+        step()
+    torch.cuda.synchronize()
+    stage_ms = renderer.stage_times_ms()
+    stage_ms["blend_timed_region"] = blend_ms_timed
+    cnt = renderer.counters()
+    ms_per_step = elapsed / args.steps * 1e3
+    A, T, P = cnt["total_instances"], cnt["tile_count"], 2 * W * H
+    # blend algorithmic bytes: 4 B id + 32 B StereoTiledRenderData per instance, rgba16f per
+    # pixel of both eyes, 8 B header per tile
+    b_blend = A * 36 + P * 8 + T * 8
+    t_blend = blend_ms_timed * 1e-3
+    achieved = b_blend / t_blend / 1e9 if t_blend > 0 else 0.0
+    parity, cpu = None, None
+    if args.parity or args.cpu_baseline:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle as O  # CPU baseline + parity checker only
+        threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+        times, ref = [], None
+        for _ in range(2 if args.cpu_baseline else 1):
+            t = time.perf_counter()
+            ref = O.df_render_stereo(world_np, harm_np, sh, cams[0], cams[1], W, H,
+                                     max_gaussians=max(n, args.df_max_gaussians), nthreads=threads)
+            times.append(time.perf_counter() - t)
+        if args.parity:
+            got = color.view(torch.int16).cpu().numpy().view(np.uint16)
+            parity = bool(np.array_equal(got, ref["color"])) and int(ref["total_instances"]) == A
+        if args.cpu_baseline:
+            med = float(np.median(times))
+            cpu = {"value": 1.0 / med, "unit": "frames/s", "cores": threads, "kind": "port",
+                   "sample": f"{len(times)} full DepthFirst stereo frames of {args.config} with the C oracle "
+                             f"(og_df_render_stereo, pthreads), median {med:.2f} s/frame",
+                   "stages_s": {k: round(v, 4) for k, v in ref["times"].items()}}
+    out = {
+        "metric": "frames/sec @ N Gaussians × W×H (1/2/4/8 GPU); sort Gkeys/s; blend HBM GB/s",
+        "value": 1e3 / ms_per_step, "unit": "frames/s", "n_gpus": 1, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "strong",
+        "vs_baseline": None, "dtype": "fp16", "data": "synthetic",
+        "config": {"workload": f"{args.config}: {n} gaussians SH{ {1: 0, 4: 1, 9: 2, 16: 3}[sh] } 2x{W}x{H} "
+                               f"side-by-side stereo, DepthFirst semantics (16x16 tiles, shared SH colour, "
+                               f"union bounds), fp16 PackedWorldGaussianHalf",
+                   "gaussians": n, "width": W, "height": H, "sh_components": sh, "instances": A,
+                   "visible": cnt["visible"], "tiles": T, "max_gaussians": cfg.max_gaussians,
+                   "parallelism": "single GPU"},
+        "roofline": {"bound": "hbm", "kernel": "k_df_blend", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "algorithmic_bytes": b_blend, "avg_launch_ms": blend_ms_timed,
+                     "note": "blend is VALU/LDS-bound (fp16 math per pixel, both eyes per entry)"},
+        "cpu_baseline": cpu, "stages_ms": stage_ms, "blend_gb_per_s": achieved, "parity_vs_oracle": parity,
+    }
+    print(json.dumps(out))
+    renderer.close()
 
 
 if __name__ == "__main__":

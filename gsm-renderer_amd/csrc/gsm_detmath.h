@@ -134,6 +134,36 @@ inline void det_sincos_table_entry(uint32_t q, float* s, float* c) {
     *s = (float)sd;
     *c = (float)cd;
 }
+// sin/cos of an unquantised fp32 angle in [0, pi] (conicFromThetaSigmas' fast::sincos for the
+// DepthFirst stereo projection's fp32 theta, DepthFirstShaders.metal:455,471): reflected about
+// pi/2, Horner polynomials in double with the Taylor coefficients +-1/n! (compile-time
+// correctly rounded), only * and + (no contraction), one rounding to fp32.  Evaluated per
+// gaussian on the GPU with IEEE double ops; oracle/gsm_oracle_math.h ogm_sincos_theta is the
+// same expression.
+GSM_HD void det_sincos_theta(float th, float* s, float* c) {
+    constexpr double S[11] = {1.0, -1.0 / 6.0, 1.0 / 120.0, -1.0 / 5040.0, 1.0 / 362880.0,
+                              -1.0 / 39916800.0, 1.0 / 6227020800.0, -1.0 / 1307674368000.0,
+                              1.0 / 355687428096000.0, -1.0 / 121645100408832000.0,
+                              1.0 / 51090942171709440000.0};
+    constexpr double K[11] = {1.0, -1.0 / 2.0, 1.0 / 24.0, -1.0 / 720.0, 1.0 / 40320.0,
+                              -1.0 / 3628800.0, 1.0 / 479001600.0, -1.0 / 87178291200.0,
+                              1.0 / 20922789888000.0, -1.0 / 6402373705728000.0,
+                              1.0 / 2432902008176640000.0};
+    const double half_pi = 1.5707963267948966192;
+    double x = (double)th, sg = 1.0;
+    if (!(x <= half_pi)) {
+        x = x - 2.0 * half_pi;
+        sg = -1.0;
+    }
+    double x2 = x * x, ps = S[10], pc = K[10];
+#pragma unroll
+    for (int i = 9; i >= 0; --i) {
+        ps = ps * x2 + S[i];
+        pc = pc * x2 + K[i];
+    }
+    *s = (float)(sg * (x * ps));
+    *c = (float)(sg * pc);
+}
 inline double det_exp_double(double x) {  // |x| <= 20
     double y = x / 64.0, term = 1.0, sum = 1.0;
     for (int k = 1; k < 24; ++k) {
@@ -192,6 +222,14 @@ inline uint16_t blend_exp_table_entry(uint16_t pb) {
     float p = half_bits_to_float(pb);
     uint16_t arg = float_to_half_bits(-0.5f * p);  // fp16 multiply: exact product, one rounding
     return det_exp_half_bits(arg);
+}
+// The DepthFirst stereo blend's alpha factor: p > r2Max = 9 gives alpha 0 without the exp
+// (DepthFirstShaders.metal:1898-1905); opacity * 0 = 0 and min(0, 0.99) = 0, so the cutoff
+// folds into the table.  NaN p compares false and keeps the exp entry.
+inline uint16_t stereo_exp_table_entry(uint16_t pb) {
+    const float p = half_bits_to_float(pb);
+    if (p > 9.0f) return 0;
+    return blend_exp_table_entry(pb);
 }
 
 }  // namespace gsm

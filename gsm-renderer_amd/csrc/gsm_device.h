@@ -1,0 +1,478 @@
+// gsm_device.h -- device helpers shared by the gfx950 kernels of the GlobalRenderer
+// (gsm_kernels.hip) and the DepthFirst stereo path (gsm_depthfirst.hip): fp16 bit casts,
+// column-major matrix products, the GaussianShared.h pieces and block/wave scans.
+// Numeric contract: DESIGN.md (built with -ffp-contract=off, IEEE div/sqrt).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "../../include/gsm_renderer.h"
+#include "gsm_detmath.h"
+#include "gsm_internal.h"
+#include "gsm_types.h"
+
+namespace gsm {
+
+typedef _Float16 h1;
+typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ float hbits_to_f(uint16_t b) { return (float)__builtin_bit_cast(h1, b); }
+__device__ __forceinline__ uint16_t f_to_hbits(float f) { return __builtin_bit_cast(uint16_t, (h1)f); }
+
+__device__ __forceinline__ float clampf(float v, float lo, float hi) {
+    return __builtin_fminf(__builtin_fmaxf(v, lo), hi);
+}
+
+// ---------------------------------------------------------------------------
+// small column-major matrix helpers (simd / Metal layout)
+// ---------------------------------------------------------------------------
+struct M3 {
+    float m[3][3];  // m[col][row]
+};
+
+__device__ __forceinline__ M3 m3_mul(const M3& A, const M3& B) {
+    M3 R;
+#pragma unroll
+    for (int c = 0; c < 3; ++c)
+#pragma unroll
+        for (int r = 0; r < 3; ++r) {
+            float acc = A.m[0][r] * B.m[c][0];
+            acc = acc + A.m[1][r] * B.m[c][1];
+            acc = acc + A.m[2][r] * B.m[c][2];
+            R.m[c][r] = acc;
+        }
+    return R;
+}
+
+// float4x4 * float4 (column-major): sum_j col_j * v_j left to right.
+__device__ __forceinline__ void m4_mul_v(const float* M, const float v[4], float out[4]) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        float acc = M[0 * 4 + i] * v[0];
+        acc = acc + M[1 * 4 + i] * v[1];
+        acc = acc + M[2 * 4 + i] * v[2];
+        acc = acc + M[3 * 4 + i] * v[3];
+        out[i] = acc;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// GaussianShared.h pieces
+// ---------------------------------------------------------------------------
+struct Cov2 {
+    float a, b, c, d;  // col0 = (a, b), col1 = (c, d)
+};
+
+// conicFromThetaSigmas (GaussianShared.h:490-510) for a quantised angle.
+struct Conic {
+    float A, B, C;
+};
+__device__ __forceinline__ Conic conic_from_quant(const float2* __restrict__ sincos, uint16_t thq,
+                                                  float sigma1, float sigma2) {
+    float2 sc = sincos[thq];
+    float s = sc.x, c = sc.y;
+    float sig1 = __builtin_fmaxf(sigma1, 1e-4f);
+    float sig2 = __builtin_fmaxf(sigma2, 1e-4f);
+    float iv1 = 1.0f / (sig1 * sig1);
+    float iv2 = 1.0f / (sig2 * sig2);
+    float cc = c * c, ss = s * s, cs = c * s;
+    Conic k;
+    k.A = cc * iv1 + ss * iv2;
+    k.B = cs * (iv1 - iv2);
+    k.C = ss * iv1 + cc * iv2;
+    return k;
+}
+
+// gaussianComputePower (GaussianShared.h:595-597).
+__device__ __forceinline__ float compute_power(float opacity) {
+    const float LN2 = 0.693147180559945f;
+    return LN2 * 8.0f + LN2 * det_log2f(__builtin_fmaxf(opacity, 1e-6f));
+}
+
+// gaussianSegmentIntersectEllipse .. intersectsTile (GaussianShared.h:599-653).
+__device__ __forceinline__ bool seg_ellipse(float a, float b, float c, float d, float l, float r) {
+    float delta = b * b - 4.0f * a * c;
+    float t1 = (l - d) * (2.0f * a) + b;
+    float t2 = (r - d) * (2.0f * a) + b;
+    return delta >= 0.0f && (t1 <= 0.0f || t1 * t1 <= delta) && (t2 >= 0.0f || t2 * t2 <= delta);
+}
+__device__ __forceinline__ bool intersects_tile(int tx, int ty, float cx, float cy, const Conic& k,
+                                                float w) {
+    const int pminx = tx * (int)kTileWidth, pminy = ty * (int)kTileHeight;
+    const int pmaxx = pminx + (int)kTileWidth - 1, pmaxy = pminy + (int)kTileHeight - 1;
+    if (cx >= (float)pminx && cx <= (float)pmaxx && cy >= (float)pminy && cy <= (float)pmaxy)
+        return true;
+    float dx = (cx * 2.0f < (float)(pminx + pmaxx)) ? cx - (float)pminx : cx - (float)pmaxx;
+    if (seg_ellipse(k.C, -2.0f * k.B * dx, k.A * dx * dx - w, cy, (float)pminy, (float)pmaxy))
+        return true;
+    float dy = (cy * 2.0f < (float)(pminy + pmaxy)) ? cy - (float)pminy : cy - (float)pmaxy;
+    if (seg_ellipse(k.A, -2.0f * k.B * dy, k.C * dy * dy - w, cx, (float)pminx, (float)pmaxx))
+        return true;
+    return false;
+}
+
+constexpr float SH_C0 = 0.28209479177387814f;
+constexpr float SH_C1 = 0.4886025119029199f;
+constexpr float SH_C2_0 = 1.0925484305920792f;
+constexpr float SH_C2_1 = -1.0925484305920792f;
+constexpr float SH_C2_2 = 0.31539156525252005f;
+constexpr float SH_C2_3 = -1.0925484305920792f;
+constexpr float SH_C2_4 = 0.5462742152960396f;
+constexpr float SH_C3_0 = -0.5900435899266435f;
+constexpr float SH_C3_1 = 2.890611442640554f;
+constexpr float SH_C3_2 = -0.4570457994644658f;
+constexpr float SH_C3_3 = 0.3731763325901154f;
+constexpr float SH_C3_4 = -0.4570457994644658f;
+constexpr float SH_C3_5 = 1.445305721320277f;
+constexpr float SH_C3_6 = -0.5900435899266435f;
+
+template <bool HALF>
+__device__ __forceinline__ float load_harm(const void* __restrict__ h, size_t i) {
+    if constexpr (HALF) {
+        return hbits_to_f(((const uint16_t*)h)[i]);
+    } else {
+        return ((const float*)h)[i];
+    }
+}
+
+// computeSHColor (GaussianShared.h:38-116) specialised by degree like the
+// SH_DEGREE function constant (GlobalProjectCullEncoder.swift:19-45).
+template <bool HALF, int DEG>
+__device__ __forceinline__ void sh_color(const void* __restrict__ harm, uint32_t gid,
+                                         const float pos[3], const float cam[3], uint32_t shk,
+                                         float col[3]) {
+    if (DEG == 0 || shk == 0) {
+        const size_t base = (size_t)gid * 3u;
+        col[0] = load_harm<HALF>(harm, base) * SH_C0;
+        col[1] = load_harm<HALF>(harm, base + 1) * SH_C0;
+        col[2] = load_harm<HALF>(harm, base + 2) * SH_C0;
+        return;
+    }
+    constexpr int K = DEG == 1 ? 4 : (DEG == 2 ? 9 : 16);
+    float d0 = cam[0] - pos[0], d1 = cam[1] - pos[1], d2 = cam[2] - pos[2];
+    float dd = d0 * d0 + d1 * d1;
+    dd = dd + d2 * d2;
+    float n = __builtin_sqrtf(dd);
+    float x = d0 / n, y = d1 / n, z = d2 / n;
+    float xx = x * x, yy = y * y, zz = z * z;
+    float xy = x * y, yz = y * z, xz = x * z;
+    float b[16];
+    b[0] = SH_C0;
+    b[1] = (-SH_C1) * y;
+    b[2] = SH_C1 * z;
+    b[3] = (-SH_C1) * x;
+    if constexpr (DEG >= 2) {
+        b[4] = SH_C2_0 * xy;
+        b[5] = SH_C2_1 * yz;
+        b[6] = SH_C2_2 * ((2.0f * zz - xx) - yy);
+        b[7] = SH_C2_3 * xz;
+        b[8] = SH_C2_4 * (xx - yy);
+    }
+    if constexpr (DEG >= 3) {
+        b[9] = (SH_C3_0 * y) * (3.0f * xx - yy);
+        b[10] = (SH_C3_1 * xy) * z;
+        b[11] = (SH_C3_2 * y) * ((4.0f * zz - xx) - yy);
+        b[12] = (SH_C3_3 * z) * ((2.0f * zz - 3.0f * xx) - 3.0f * yy);
+        b[13] = (SH_C3_4 * x) * ((4.0f * zz - xx) - yy);
+        b[14] = (SH_C3_5 * z) * (xx - yy);
+        b[15] = (SH_C3_6 * x) * (xx - 3.0f * yy);
+    }
+    const size_t base = (size_t)gid * (size_t)K * 3u;
+    float cr = 0.0f, cg = 0.0f, cb = 0.0f;
+    if constexpr (HALF && DEG == 3) {
+        // 96 B per gaussian, 16-B aligned: six dwordx4 loads.
+        const uint4* p = (const uint4*)((const uint16_t*)harm + base);
+        uint16_t hv[48];
+#pragma unroll
+        for (int q = 0; q < 6; ++q) {
+            uint4 v = p[q];
+            uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                hv[q * 8 + 2 * t] = (uint16_t)(w[t] & 0xFFFFu);
+                hv[q * 8 + 2 * t + 1] = (uint16_t)(w[t] >> 16);
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            cr = cr + hbits_to_f(hv[i]) * b[i];
+            cg = cg + hbits_to_f(hv[16 + i]) * b[i];
+            cb = cb + hbits_to_f(hv[32 + i]) * b[i];
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < K; ++i) {
+            cr = cr + load_harm<HALF>(harm, base + i) * b[i];
+            cg = cg + load_harm<HALF>(harm, base + K + i) * b[i];
+            cb = cb + load_harm<HALF>(harm, base + 2 * K + i) * b[i];
+        }
+    }
+    col[0] = cr;
+    col[1] = cg;
+    col[2] = cb;
+}
+
+// srgbToLinearChannel (GaussianShared.h:118-121).
+__device__ __forceinline__ float srgb_to_linear(float c) {
+    c = clampf(c, 0.0f, 1.0f);
+    return (c <= 0.04045f) ? (c / 12.92f) : det_powrf((c + 0.055f) / 1.055f, 2.4f);
+}
+
+__device__ __forceinline__ float fmod_pi(float t) {
+    // fmod(t, pi_f) for |t| < 2 pi_f (atan2 range): exact by Sterbenz.
+    float a = __builtin_fabsf(t);
+    if (a >= kPiF) {
+        float r = a - kPiF;
+        return __builtin_copysignf(r, t);
+    }
+    return t;
+}
+
+// normalizeQuaternion (GaussianShared.h:289-295) applied twice -- by the projection kernels
+// (GlobalShaders.metal:64, DepthFirstShaders.metal:393) and again inside buildCovariance3D
+// (GaussianShared.h:308) -- then quaternionToMatrix (:297-305) and R S S^T R^T (:307-324).
+__device__ __forceinline__ M3 build_cov3d(const float scale[3], const float rot[4]) {
+    float q[4] = {rot[0], rot[1], rot[2], rot[3]};
+#pragma unroll
+    for (int pass = 0; pass < 2; ++pass) {
+        float d = q[0] * q[0] + q[1] * q[1];
+        d = d + q[2] * q[2];
+        d = d + q[3] * q[3];
+        float nrm = __builtin_sqrtf(__builtin_fmaxf(d, 1e-8f));
+        if (nrm < 1e-8f) {
+            q[0] = 1.0f; q[1] = 0.0f; q[2] = 0.0f; q[3] = 0.0f;
+        } else {
+            q[0] = q[0] / nrm; q[1] = q[1] / nrm; q[2] = q[2] / nrm; q[3] = q[3] / nrm;
+        }
+    }
+    float x = q[0], y = q[1], z = q[2], r = q[3];
+    float xx = x * x, yy = y * y, zz = z * z, xy = x * y, xz = x * z, yz = y * z;
+    M3 R;
+    R.m[0][0] = 1.0f - 2.0f * (yy + zz); R.m[1][0] = 2.0f * (xy - r * z); R.m[2][0] = 2.0f * (xz + r * y);
+    R.m[0][1] = 2.0f * (xy + r * z); R.m[1][1] = 1.0f - 2.0f * (xx + zz); R.m[2][1] = 2.0f * (yz - r * x);
+    R.m[0][2] = 2.0f * (xz - r * y); R.m[1][2] = 2.0f * (yz + r * x); R.m[2][2] = 1.0f - 2.0f * (xx + yy);
+    float RS[3][3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c)
+#pragma unroll
+        for (int rr = 0; rr < 3; ++rr) RS[c][rr] = R.m[c][rr] * scale[c];
+    M3 C3;
+#pragma unroll
+    for (int c = 0; c < 3; ++c)
+#pragma unroll
+        for (int rr = 0; rr < 3; ++rr)
+            C3.m[c][rr] = (RS[0][c] * RS[0][rr] + RS[1][c] * RS[1][rr]) + RS[2][c] * RS[2][rr];
+    return C3;
+}
+
+// projectCovariance2D (GaussianShared.h:326-375) with its uniform terms (tan clamp limits and
+// focal lengths from the projection matrix and viewport) evaluated once per frame on the host.
+__device__ __forceinline__ Cov2 project_cov2d(const M3& C3, const float vp[3], const float* view, float limX,
+                                              float limY, float focalX, float focalY) {
+    M3 W;
+#pragma unroll
+    for (int c = 0; c < 3; ++c)
+#pragma unroll
+        for (int rr = 0; rr < 3; ++rr) W.m[c][rr] = view[c * 4 + rr];
+    float absZ = __builtin_fabsf(vp[2]);
+    float signZ = (vp[2] >= 0.0f) ? 1.0f : -1.0f;
+    float safeAbsZ = __builtin_fmaxf(absZ, 1e-4f);
+    float invAbsZ = 1.0f / safeAbsZ;
+    float invAbsZ2 = invAbsZ * invAbsZ;
+    float xCl = clampf(vp[0] * invAbsZ, -limX, limX) * safeAbsZ;
+    float yCl = clampf(vp[1] * invAbsZ, -limY, limY) * safeAbsZ;
+    M3 J;
+    J.m[0][0] = focalX * invAbsZ; J.m[0][1] = 0.0f; J.m[0][2] = 0.0f;
+    J.m[1][0] = 0.0f; J.m[1][1] = focalY * invAbsZ; J.m[1][2] = 0.0f;
+    J.m[2][0] = -focalX * xCl * signZ * invAbsZ2;
+    J.m[2][1] = -focalY * yCl * signZ * invAbsZ2;
+    J.m[2][2] = 0.0f;
+    M3 T = m3_mul(J, W);
+    M3 M1 = m3_mul(T, C3);
+    M3 Tt;
+#pragma unroll
+    for (int c = 0; c < 3; ++c)
+#pragma unroll
+        for (int rr = 0; rr < 3; ++rr) Tt.m[c][rr] = T.m[rr][c];
+    M3 F = m3_mul(M1, Tt);
+    Cov2 cov;
+    cov.a = F.m[0][0] + 0.3f;
+    cov.b = F.m[0][1];
+    cov.c = F.m[1][0];
+    cov.d = F.m[1][1] + 0.3f;
+    return cov;
+}
+
+// stabilizeCovariance2D (GaussianShared.h:655-714); maxEig = ((max(W, H) * 2) / 3)^2 from the host.
+__device__ __forceinline__ Cov2 stabilize_cov2d(Cov2 cov, float maxEig) {
+    const float kMinVar = 1e-4f, kMinDet = 1e-8f;
+    float a = cov.a, b = 0.5f * (cov.b + cov.c), d = cov.d;
+    if (!__builtin_isfinite(a) || !__builtin_isfinite(b) || !__builtin_isfinite(d)) {
+        cov.a = 1.0f; cov.b = 0.0f; cov.c = 0.0f; cov.d = 1.0f;
+        return cov;
+    }
+    a = __builtin_fmaxf(a, kMinVar);
+    d = __builtin_fmaxf(d, kMinVar);
+    float det = a * d - b * b;
+    if (!__builtin_isfinite(det) || det < kMinDet) {
+        float bump = (kMinDet - det) + kMinVar;
+        a = a + bump;
+        d = d + bump;
+        det = a * d - b * b;
+    }
+    float mid = 0.5f * (a + d);
+    float sq = __builtin_sqrtf(__builtin_fmaxf(mid * mid - det, 0.0f));
+    float l1 = mid + sq;
+    float l2 = __builtin_fmaxf(mid - sq, kMinVar);
+    float v1x, v1y;
+    if (__builtin_fabsf(b) > 1e-8f) {
+        float vx = b, vy = l1 - a;
+        float dn = __builtin_fmaxf(__builtin_sqrtf(vx * vx + vy * vy), 1e-8f);
+        v1x = vx / dn;
+        v1y = vy / dn;
+    } else if (a >= d) {
+        v1x = 1.0f; v1y = 0.0f;
+    } else {
+        v1x = 0.0f; v1y = 1.0f;
+    }
+    float v2x = v1y, v2y = -v1x;
+    l1 = __builtin_fminf(l1, maxEig);
+    l2 = __builtin_fmaxf(l2, l1 * (1.0f / 65536.0f));  // l1 / 256^2: exact power of two
+    cov.a = l1 * (v1x * v1x) + l2 * (v2x * v2x);
+    cov.b = l1 * (v1x * v1y) + l2 * (v2x * v2y);
+    cov.c = l1 * (v1y * v1x) + l2 * (v2y * v2x);
+    cov.d = l1 * (v1y * v1y) + l2 * (v2y * v2y);
+    return cov;
+}
+
+// covarianceToThetaSigmas (GaussianShared.h:446-488): theta in [0, pi), sigmas = sqrt(eigenvalues).
+__device__ __forceinline__ bool theta_sigmas(const Cov2& cov, float* theta, float* s1, float* s2) {
+    float a = cov.a, b = 0.5f * (cov.b + cov.c), d = cov.d;
+    if (!(__builtin_isfinite(a) && __builtin_isfinite(b) && __builtin_isfinite(d))) return false;
+    a = __builtin_fmaxf(a, 1e-8f);
+    d = __builtin_fmaxf(d, 1e-8f);
+    float det = a * d - b * b;
+    if (!(__builtin_isfinite(det) && det > 0.0f)) return false;
+    float mid = 0.5f * (a + d);
+    float sq = __builtin_sqrtf(__builtin_fmaxf(mid * mid - det, 0.0f));
+    float l1 = __builtin_fmaxf(mid + sq, 1e-8f);
+    float l2 = __builtin_fmaxf(mid - sq, 1e-8f);
+    float v1x, v1y;
+    if (__builtin_fabsf(b) > 1e-8f) {
+        float tx = b, ty = l1 - a;
+        float nn = __builtin_sqrtf(tx * tx + ty * ty);
+        v1x = tx / nn;
+        v1y = ty / nn;
+    } else if (a >= d) {
+        v1x = 1.0f; v1y = 0.0f;
+    } else {
+        v1x = 0.0f; v1y = 1.0f;
+    }
+    float th = det_atan2f(v1y, v1x);
+    th = fmod_pi(th);
+    if (th < 0.0f) th = th + kPiF;
+    if (th >= kPiF) th = th - kPiF;
+    *theta = th;
+    *s1 = __builtin_sqrtf(l1);
+    *s2 = __builtin_sqrtf(l2);
+    return __builtin_isfinite(th) && __builtin_isfinite(*s1) && __builtin_isfinite(*s2);
+}
+
+// computeOBBExtents (GaussianShared.h:402-427) at k = 3 sigma.
+__device__ __forceinline__ void obb_extents(const Cov2& cov, float* ex, float* ey) {
+    float a = cov.a, b = cov.b, d = cov.d;
+    float det = a * d - b * b;
+    float mid = 0.5f * (a + d);
+    float sq = __builtin_sqrtf(__builtin_fmaxf(mid * mid - det, 1e-6f));
+    float l1 = mid + sq;
+    float l2 = __builtin_fmaxf(mid - sq, 1e-6f);
+    float e1 = 3.0f * __builtin_sqrtf(__builtin_fmaxf(l1, 1e-6f));
+    float e2 = 3.0f * __builtin_sqrtf(__builtin_fmaxf(l2, 1e-6f));
+    float v1x, v1y;
+    if (__builtin_fabsf(b) > 1e-6f) {
+        float vx = b, vy = l1 - a;
+        float dn = __builtin_fmaxf(__builtin_sqrtf(vx * vx + vy * vy), 1e-6f);
+        v1x = vx / dn;
+        v1y = vy / dn;
+    } else if (a >= d) {
+        v1x = 1.0f; v1y = 0.0f;
+    } else {
+        v1x = 0.0f; v1y = 1.0f;
+    }
+    *ex = __builtin_fabsf(v1x) * e1 + __builtin_fabsf(v1y) * e2;
+    *ey = __builtin_fabsf(v1y) * e1 + __builtin_fabsf(v1x) * e2;
+}
+
+// Colour target store of one rgba16f pixel in config.color_format (include/gsm_renderer.h
+// conversion rules; oracle og_convert_color): rgba32f widens, the 8-bit formats clamp to
+// [0, 1], sRGB-encode rgb and round to nearest.
+__device__ __forceinline__ float srgb_encode_px(float c) {
+    return c <= 0.0031308f ? c * 12.92f : 1.055f * det_powrf(c, 1.0f / 2.4f) - 0.055f;
+}
+__device__ __forceinline__ void store_color_px(int fmt, char* dst, uint32_t rg, uint32_t ba) {
+    if (fmt == GSM_COLOR_FORMAT_RGBA16F) {  // 4-byte stores: any 4-byte aligned pitch
+        ((uint32_t*)dst)[0] = rg;
+        ((uint32_t*)dst)[1] = ba;
+        return;
+    }
+    float c[4] = {hbits_to_f((uint16_t)(rg & 0xFFFFu)), hbits_to_f((uint16_t)(rg >> 16)),
+                  hbits_to_f((uint16_t)(ba & 0xFFFFu)), hbits_to_f((uint16_t)(ba >> 16))};
+    if (fmt == GSM_COLOR_FORMAT_RGBA32F) {
+        float* o = (float*)dst;
+        o[0] = c[0]; o[1] = c[1]; o[2] = c[2]; o[3] = c[3];
+        return;
+    }
+    const bool srgb = fmt == GSM_COLOR_FORMAT_RGBA8_UNORM_SRGB || fmt == GSM_COLOR_FORMAT_BGRA8_UNORM_SRGB;
+    uint32_t u8[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        float x = clampf(c[k], 0.0f, 1.0f);
+        if (srgb && k < 3) x = srgb_encode_px(x);
+        u8[k] = (uint32_t)__builtin_rintf(x * 255.0f);
+    }
+    const bool bgra = fmt >= GSM_COLOR_FORMAT_BGRA8_UNORM;
+    *(uint32_t*)dst = (bgra ? u8[2] : u8[0]) | (u8[1] << 8) | ((bgra ? u8[0] : u8[2]) << 16) | (u8[3] << 24);
+}
+
+template <int BLOCK>
+__device__ __forceinline__ uint32_t block_reduce_add(uint32_t v, uint32_t* lds) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    if (lane == 0) lds[wave] = v;
+    __syncthreads();
+    uint32_t s = 0;
+#pragma unroll
+    for (int w = 0; w < BLOCK / 64; ++w) s += lds[w];
+    return s;
+}
+
+// Inclusive scan inside a wave of 64 lanes.
+__device__ __forceinline__ uint32_t wave_inclusive_scan(uint32_t v) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        uint32_t t = __shfl_up(v, o, 64);
+        if (lane >= o) v += t;
+    }
+    return v;
+}
+// Exclusive scan over a block; returns the block total in *total.
+template <int BLOCK>
+__device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t v, uint32_t* lds, uint32_t* total) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint32_t inc = wave_inclusive_scan(v);
+    if (lane == 63) lds[wave] = inc;
+    __syncthreads();
+    uint32_t off = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < BLOCK / 64; ++w) {
+        uint32_t s = lds[w];
+        if (w < wave) off += s;
+        tot += s;
+    }
+    __syncthreads();
+    *total = tot;
+    return off + inc - v;
+}
+
+}  // namespace gsm

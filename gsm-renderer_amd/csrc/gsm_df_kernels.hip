@@ -1,0 +1,549 @@
+// gsm_df_kernels.hip -- gfx950 kernels of the DepthFirst stereo side-by-side frame
+// (SURVEY.md 8(f) rank 1).  Reference: Sources/Renderer/DepthFirstRenderer/DepthFirstShaders.metal
+// and Sources/Renderer/Shared/GaussianShared.h; host order DepthFirstRenderer.swift:595-831.
+//
+// Frame: project both eyes once per gaussian (k_df_project) -> compact the visible ones with
+// their 32-bit depth keys (k_df_compact) -> stable LSD depth sort (gsm_sort.hip) -> per-gaussian
+// tile counts in depth order, scan, instance expansion of the union rect (k_df_icount,
+// k_df_instances) -> stable LSD sort by tile id -> tile ranges (k_df_ranges) -> one persistent
+// blend kernel that clears, composites both eyes per 16x16 tile and writes the two eyes side by
+// side with the copy pass's row flip (k_df_blend).
+// Numeric contract: DESIGN.md (built with -ffp-contract=off, IEEE div/sqrt); bit-exact with
+// oracle/gsm_oracle.c og_df_render_stereo.
+#include <hip/hip_runtime.h>
+
+#include "../../include/gsm_renderer.h"
+#include "gsm_detmath.h"
+#include "gsm_device.h"
+#include "gsm_df_internal.h"
+#include "gsm_internal.h"
+#include "gsm_types.h"
+
+namespace gsm {
+
+// ---------------------------------------------------------------------------
+// 1. projection of both eyes (depthFirstStereoProjectCullKernel, DepthFirstShaders.metal:341-499)
+// ---------------------------------------------------------------------------
+// EyeProjectionResult (DepthFirstShaders.metal:236-247)
+struct DfEyeOut {
+    bool visible;
+    float sx, sy, theta, s1, s2, detCov, depth;
+    int tb[4];
+};
+
+// projectToEye (DepthFirstShaders.metal:249-339).  wp: scene-transformed position; C3: the
+// covariance of the scene-scaled gaussian (the same for both eyes).
+__device__ __forceinline__ DfEyeOut df_project_eye(const DfEyeConst& E, const DfArgs& P, const float wp[4],
+                                                   const M3& C3) {
+    DfEyeOut r;
+    r.visible = false;
+    r.sx = r.sy = r.theta = r.s1 = r.s2 = r.detCov = 0.0f;
+    r.tb[0] = 0; r.tb[1] = -1; r.tb[2] = 0; r.tb[3] = -1;
+    float vp[4], clip[4];
+    m4_mul_v(E.view, wp, vp);
+    m4_mul_v(E.proj, vp, clip);
+    r.depth = clip[3];
+    if (!(clip[3] > P.nearPlane)) return r;  // isInFrontOfCameraClipW
+    if (r.depth > P.farPlane) return r;      // cullByFarPlane (GaussianShared.h:732-734)
+    const float ndcx = clip[0] / clip[3], ndcy = clip[1] / clip[3];
+    r.sx = (ndcx + 1.0f) * 0.5f * P.width;   // ndcToScreen (GaussianShared.h:150-155)
+    r.sy = (ndcy + 1.0f) * 0.5f * P.height;
+    Cov2 cov = project_cov2d(C3, vp, E.view, E.limX, E.limY, E.focalX, E.focalY);
+    cov = stabilize_cov2d(cov, P.maxEig);
+    float th, s1, s2;
+    if (!theta_sigmas(cov, &th, &s1, &s2)) return r;
+    r.theta = th;
+    r.s1 = s1;
+    r.s2 = s2;
+    {
+        const float a = cov.a, b = 0.5f * (cov.b + cov.c), d = cov.d;
+        r.detCov = __builtin_fmaxf(a * d - b * b, 0.0f);
+    }
+    if (3.0f * __builtin_fmaxf(s1, s2) < 0.5f) return r;  // cullByRadius
+    float ex, ey;
+    obb_extents(cov, &ex, &ey);
+    if (r.sx + ex < 0.0f || r.sx - ex > P.width || r.sy + ey < 0.0f || r.sy - ey > P.height) return r;
+    // computeTileBounds (GaussianShared.h:791-828) on 16x16 tiles: x / 16 == x * (1/16) exactly
+    const float maxW = P.width - 1.0f, maxH = P.height - 1.0f;
+    const float xmin = clampf(r.sx - ex, 0.0f, maxW), xmax = clampf(r.sx + ex, 0.0f, maxW);
+    const float ymin = clampf(r.sy - ey, 0.0f, maxH), ymax = clampf(r.sy + ey, 0.0f, maxH);
+    int minTX = (int)__builtin_floorf(xmin * (1.0f / 16.0f));
+    int maxTX = (int)__builtin_ceilf(xmax * (1.0f / 16.0f)) - 1;
+    int minTY = (int)__builtin_floorf(ymin * (1.0f / 16.0f));
+    int maxTY = (int)__builtin_ceilf(ymax * (1.0f / 16.0f)) - 1;
+    r.tb[0] = max(minTX, 0);
+    r.tb[1] = min(maxTX, (int)P.tilesX - 1);
+    r.tb[2] = max(minTY, 0);
+    r.tb[3] = min(maxTY, (int)P.tilesY - 1);
+    r.visible = true;
+    return r;
+}
+
+// float_to_sortable_uint (DepthFirstShaders.metal:33-37)
+__device__ __forceinline__ uint32_t df_sortable(float v) {
+    const uint32_t b = __builtin_bit_cast(uint32_t, v);
+    return b ^ ((b & 0x80000000u) ? 0xFFFFFFFFu : 0x80000000u);
+}
+
+// the six fp16 fields of one eye in StereoTiledRenderData (DepthFirstShaders.metal:452-480):
+// mean, conicFromThetaSigmas of the unquantised angle (GaussianShared.h:490-510; sin/cos of the
+// numeric contract, det_sincos_theta), depth; an eye the gaussian misses gets mean -1e10 (-inf)
+__device__ __forceinline__ void df_pack_eye(const DfEyeOut& e, uint32_t w[3]) {
+    if (!e.visible) {
+        const uint32_t hneg = f_to_hbits(-1e10f);
+        w[0] = hneg | (hneg << 16);
+        w[1] = 0;
+        w[2] = 0;
+        return;
+    }
+    float s, c;
+    det_sincos_theta(e.theta, &s, &c);
+    const float sig1 = __builtin_fmaxf(e.s1, 1e-4f), sig2 = __builtin_fmaxf(e.s2, 1e-4f);
+    const float iv1 = 1.0f / (sig1 * sig1), iv2 = 1.0f / (sig2 * sig2);
+    const float cc = c * c, ss = s * s, cs = c * s;
+    const float A = cc * iv1 + ss * iv2;
+    const float B = cs * (iv1 - iv2);
+    const float C = ss * iv1 + cc * iv2;
+    w[0] = (uint32_t)f_to_hbits(e.sx) | ((uint32_t)f_to_hbits(e.sy) << 16);
+    w[1] = (uint32_t)f_to_hbits(A) | ((uint32_t)f_to_hbits(C) << 16);
+    w[2] = (uint32_t)f_to_hbits(2.0f * B) | ((uint32_t)f_to_hbits(e.depth) << 16);
+}
+
+template <bool HALF, int DEG>
+__global__ __launch_bounds__(kDfBlock) void k_df_project(const void* __restrict__ world,
+                                                         const void* __restrict__ harm, DfArgs P,
+                                                         StereoTiledRenderData* __restrict__ outRD,
+                                                         short4* __restrict__ outBounds,
+                                                         uint32_t* __restrict__ touchedOut,
+                                                         uint32_t* __restrict__ depthKeys,
+                                                         uint32_t* __restrict__ blockSums) {
+    __shared__ uint32_t lds[kDfBlock / 64];
+    const uint32_t gid = blockIdx.x * kDfBlock + threadIdx.x;
+    uint32_t vis = 0;
+    if (gid < P.count) {
+        float pos[3], scale[3], rot[4], opacity;
+        if constexpr (HALF) {
+            const uint4* wq = (const uint4*)((const PackedWorldGaussianHalf*)world + gid);
+            const uint4 w0 = wq[0], w1 = wq[1];
+            pos[0] = __builtin_bit_cast(float, w0.x);
+            pos[1] = __builtin_bit_cast(float, w0.y);
+            pos[2] = __builtin_bit_cast(float, w0.z);
+            opacity = hbits_to_f((uint16_t)(w0.w & 0xFFFFu));
+            scale[0] = hbits_to_f((uint16_t)(w0.w >> 16));
+            scale[1] = hbits_to_f((uint16_t)(w1.x & 0xFFFFu));
+            scale[2] = hbits_to_f((uint16_t)(w1.x >> 16));
+            rot[0] = hbits_to_f((uint16_t)(w1.y & 0xFFFFu));
+            rot[1] = hbits_to_f((uint16_t)(w1.y >> 16));
+            rot[2] = hbits_to_f((uint16_t)(w1.z & 0xFFFFu));
+            rot[3] = hbits_to_f((uint16_t)(w1.z >> 16));
+        } else {
+            const float4* wq = (const float4*)((const PackedWorldGaussian*)world + gid);
+            const float4 w0 = wq[0], w1 = wq[1], w2 = wq[2];
+            pos[0] = w0.x; pos[1] = w0.y; pos[2] = w0.z; opacity = w0.w;
+            scale[0] = w1.x; scale[1] = w1.y; scale[2] = w1.z;
+            rot[0] = w2.x; rot[1] = w2.y; rot[2] = w2.z; rot[3] = w2.w;
+        }
+        // cullByScale (GaussianShared.h:719-722), alpha threshold (TileBinningParams 0.005)
+        bool ok = !(__builtin_fmaxf(scale[0], __builtin_fmaxf(scale[1], scale[2])) < 0.0005f) &&
+                  !(opacity < 0.005f);
+        DfEyeOut L, R;
+        L.visible = R.visible = false;
+        if (ok) {
+            const float p4[4] = {pos[0], pos[1], pos[2], 1.0f};
+            float wp[4];
+            m4_mul_v(P.scene, p4, wp);
+            const float ss[3] = {scale[0] * P.sceneScale, scale[1] * P.sceneScale, scale[2] * P.sceneScale};
+            const M3 C3 = build_cov3d(ss, rot);
+            L = df_project_eye(P.eye[0], P, wp, C3);
+            R = df_project_eye(P.eye[1], P, wp, C3);
+            ok = L.visible || R.visible;
+        }
+        float checkDepth = 0.0f;
+        if (ok) {
+            checkDepth = L.visible ? L.depth : R.depth;
+            if (L.visible && R.visible) checkDepth = (L.depth + R.depth) * 0.5f;
+            float detCov = L.visible ? L.detCov : R.detCov;
+            if (L.visible && R.visible) detCov = __builtin_fmaxf(L.detCov, R.detCov);
+            // cullByTotalInk (GaussianShared.h:739-751) + computeDepthFactor (:275-278)
+            const float ink = opacity * 6.283185f * __builtin_sqrtf(__builtin_fmaxf(detCov, 1e-12f));
+            const float s = clampf((P.adjFar - checkDepth) / P.adjDen, 0.0f, 1.0f);
+            const float depthFactor = 1.0f - s * s;
+            if (ink < depthFactor * 2.0f) ok = false;
+        }
+        int ub[4] = {0, -1, 0, -1};
+        uint32_t touched = 0;
+        if (ok) {
+            if (L.visible && R.visible) {
+                ub[0] = min(L.tb[0], R.tb[0]);
+                ub[1] = max(L.tb[1], R.tb[1]);
+                ub[2] = min(L.tb[2], R.tb[2]);
+                ub[3] = max(L.tb[3], R.tb[3]);
+            } else {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) ub[q] = L.visible ? L.tb[q] : R.tb[q];
+            }
+            const int ux = max(ub[1] - ub[0] + 1, 0), uy = max(ub[3] - ub[2] + 1, 0);
+            touched = (uint32_t)(ux * uy);
+            if (touched == 0) ok = false;
+        }
+        if (ok) {
+            float col[3];
+            sh_color<HALF, DEG>(harm, gid, pos, P.mid, P.shComponents, col);
+            col[0] = __builtin_fmaxf(col[0] + 0.5f, 0.0f);
+            col[1] = __builtin_fmaxf(col[1] + 0.5f, 0.0f);
+            col[2] = __builtin_fmaxf(col[2] + 0.5f, 0.0f);
+            if (P.inputIsSRGB > 0.5f) {
+                col[0] = srgb_to_linear(col[0]);
+                col[1] = srgb_to_linear(col[1]);
+                col[2] = srgb_to_linear(col[2]);
+            }
+            uint32_t wl[3], wr[3];
+            df_pack_eye(L, wl);
+            df_pack_eye(R, wr);
+            const uint32_t cR = (uint32_t)(uint8_t)clampf(col[0] * 255.0f, 0.0f, 255.0f);
+            const uint32_t cG = (uint32_t)(uint8_t)clampf(col[1] * 255.0f, 0.0f, 255.0f);
+            const uint32_t cB = (uint32_t)(uint8_t)clampf(col[2] * 255.0f, 0.0f, 255.0f);
+            const uint32_t cO = (uint32_t)(uint8_t)clampf(opacity * 255.0f, 0.0f, 255.0f);
+            uint4* o = (uint4*)(outRD + gid);
+            o[0] = make_uint4(wl[0], wl[1], wl[2], wr[0]);
+            o[1] = make_uint4(wr[1], wr[2], cR | (cG << 8) | (cB << 16) | (cO << 24),
+                              (uint32_t)f_to_hbits(checkDepth));
+            outBounds[gid] = make_short4((short)ub[0], (short)ub[1], (short)ub[2], (short)ub[3]);
+            touchedOut[gid] = touched;
+            depthKeys[gid] = df_sortable(checkDepth);
+            vis = 1;
+        } else {
+            outBounds[gid] = make_short4(0, -1, 0, -1);
+            touchedOut[gid] = 0;
+            depthKeys[gid] = 0xFFFFFFFFu;
+        }
+    }
+    const uint32_t s = block_reduce_add<kDfBlock>(vis, lds);
+    if (threadIdx.x == 0) blockSums[blockIdx.x] = s;
+}
+
+// ---------------------------------------------------------------------------
+// 2. compaction (visibilityScatterCompactKernel, DepthFirstShaders.metal:589-621): ascending id
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kDfBlock) void k_df_compact(uint32_t count, const uint32_t* __restrict__ touched,
+                                                         const uint32_t* __restrict__ depthKeys,
+                                                         const uint32_t* __restrict__ blockOffsets,
+                                                         uint32_t* __restrict__ keys, uint32_t* __restrict__ vals) {
+    __shared__ uint32_t lds[kDfBlock / 64];
+    const uint32_t gid = blockIdx.x * kDfBlock + threadIdx.x;
+    const uint32_t v = (gid < count && touched[gid] > 0u) ? 1u : 0u;
+    uint32_t total;
+    const uint32_t off = block_exclusive_scan<kDfBlock>(v, lds, &total);
+    if (v) {
+        const uint32_t o = blockOffsets[blockIdx.x] + off;
+        keys[o] = depthKeys[gid];
+        vals[o] = gid;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// 3. instances in depth order (applyDepthOrderingKernel :623-640, prefix sum, then
+//    createInstancesStereoKernel :790-826): gaussian i of the depth order writes its union rect's
+//    tiles ty-major, tx-minor from its exclusive offset while below maxInstances
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kDfBlock) void k_df_icount(const TileAssignmentHeader* __restrict__ visHdr,
+                                                        const uint32_t* __restrict__ order,
+                                                        const uint32_t* __restrict__ touched,
+                                                        uint32_t* __restrict__ sums) {
+    __shared__ uint32_t lds[kDfBlock / 64];
+    const uint32_t i = blockIdx.x * kDfBlock + threadIdx.x;
+    const uint32_t V = visHdr->totalAssignments;
+    const uint32_t c = i < V ? touched[order[i]] : 0u;
+    const uint32_t s = block_reduce_add<kDfBlock>(c, lds);
+    if (threadIdx.x == 0) sums[blockIdx.x] = s;
+}
+
+__global__ __launch_bounds__(kDfBlock) void k_df_instances(const TileAssignmentHeader* __restrict__ visHdr,
+                                                           const uint32_t* __restrict__ order,
+                                                           const uint32_t* __restrict__ touched,
+                                                           const short4* __restrict__ bounds,
+                                                           const uint32_t* __restrict__ blockOffsets,
+                                                           uint32_t maxInstances, uint32_t tilesX,
+                                                           uint32_t* __restrict__ tiles, uint32_t* __restrict__ gids) {
+    __shared__ uint32_t lds[kDfBlock / 64];
+    const uint32_t i = blockIdx.x * kDfBlock + threadIdx.x;
+    const uint32_t V = visHdr->totalAssignments;
+    const uint32_t g = i < V ? order[i] : 0u;
+    const uint32_t c = i < V ? touched[g] : 0u;
+    uint32_t total;
+    const uint32_t off = block_exclusive_scan<kDfBlock>(c, lds, &total);
+    if (c == 0) return;
+    uint64_t wp = (uint64_t)blockOffsets[blockIdx.x] + off;
+    const short4 r = bounds[g];
+    for (int ty = r.z; ty <= r.w; ++ty)
+        for (int tx = r.x; tx <= r.y; ++tx) {
+            if (wp >= maxInstances) return;
+            tiles[wp] = (uint32_t)(ty * (int)tilesX + tx) & 0xFFFFu;  // ushort tile id
+            gids[wp] = g;
+            wp++;
+        }
+}
+
+// ---------------------------------------------------------------------------
+// 4. tile ranges (extractTileRangesKernel, DepthFirstShaders.metal:1258-1313): two binary searches
+//    per tile; an empty tile's offset is its lower bound, an empty frame gives {0, 0}
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_df_ranges(const uint32_t* __restrict__ tiles,
+                                                   const TileAssignmentHeader* __restrict__ instHdr,
+                                                   uint32_t tileCount, uint2* __restrict__ headers) {
+    const uint32_t t = blockIdx.x * 256u + threadIdx.x;
+    if (t >= tileCount) return;
+    const uint32_t total = instHdr->totalAssignments;
+    if (total == 0) {
+        headers[t] = make_uint2(0u, 0u);
+        return;
+    }
+    uint32_t l = 0, r = total;
+    while (l < r) {
+        const uint32_t m = (l + r) >> 1;
+        if (tiles[m] < t) l = m + 1; else r = m;
+    }
+    const uint32_t s = l;
+    r = total;
+    while (l < r) {
+        const uint32_t m = (l + r) >> 1;
+        if (tiles[m] <= t) l = m + 1; else r = m;
+    }
+    headers[t] = make_uint2(s, l - s);
+}
+
+// ---------------------------------------------------------------------------
+// 5. blend (clearStereoRenderTextureKernel :1813-1823, depthFirstStereoRender :1825-1982) and the
+//    side-by-side copy (DepthFirstStereoCopyEncoder.swift:29-99, DepthFirstShaders.metal:1990-2018)
+//
+// Persistent workgroups, one per CU: the 128 KiB stereo alpha table sits in LDS and the waves
+// pull 16x16 tiles from a device counter.  A lane is one reference thread: a 2x2 pixel group of
+// both eyes, held as packed fp16 pairs (row 0 = {x, x+1}, row 1).  The tile's list is walked in
+// batches of kDfBatch records: lane pairs gather one 32-byte record (the u8 colour and opacity
+// turned into fp16 c/255 on the way) into the wave's LDS stage, then every entry is read back
+// as a uniform-address broadcast.  Per lane and entry the reference's control flow -- the
+// joint break when both eyes' max transmittance < 1/255, the per-eye test, the all-zero skip and
+// the r^2 > 9 cutoff -- is applied as data: an eye that is done, or a pixel past the cutoff
+// (folded into the table, stereo_exp_table_entry), gets alpha 0, which leaves its colour and
+// transmittance bit-identical (C + c * (0 * T) = C, T * (1 - 0) = T), and a dead lane stays
+// dead (T never grows).  The wave leaves the list once every lane is done.
+// ---------------------------------------------------------------------------
+constexpr uint32_t kDfBatch = 32;
+
+__device__ __forceinline__ void df_wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+__device__ __forceinline__ h2 df_h2(uint32_t u) { return __builtin_bit_cast(h2, u); }
+__device__ __forceinline__ uint32_t df_u32(h2 v) { return __builtin_bit_cast(uint32_t, v); }
+__device__ __forceinline__ h2 df_lo(h2 v) { return h2{v.x, v.x}; }
+__device__ __forceinline__ h2 df_hi(h2 v) { return h2{v.y, v.y}; }
+__device__ __forceinline__ h2 df_lookup2(const uint16_t* tbl, h2 p) {
+    const uint32_t pb = df_u32(p);
+    const uint32_t lo = tbl[pb & 0xFFFFu];
+    const uint32_t hi = tbl[pb >> 16];
+    return df_h2(lo | (hi << 16));
+}
+
+struct DfEyeState {
+    h2 T[2], Cr[2], Cg[2], Cb[2];  // [row]: {x, x + 1}
+};
+
+// one list entry for one eye of a lane (depthFirstStereoRender :1872-1913 / :1915-1956)
+__device__ __forceinline__ void df_blend_eye(DfEyeState& st, bool alive, h2 mean, h2 cc, h2 cxy, h2 opr, h2 gb,
+                                             h2 PX, h2 PY, const uint16_t* tbl) {
+    const h2 ONE = {(h1)1.0f, (h1)1.0f};
+    const h1 c099 = (h1)0.99;
+    const h2 C099 = {c099, c099};
+    const h2 dx = PX - df_lo(mean);
+    const h2 dy = PY - df_hi(mean);
+    const h2 ax = (dx * dx) * df_lo(cc);  // dx*dx*cxx for x, x+1
+    const h2 by = (dy * dy) * df_hi(cc);  // dy*dy*cyy for rows 0, 1
+    const h2 c2 = df_lo(cxy);
+    const h2 p0 = (ax + df_lo(by)) + (dx * df_lo(dy)) * c2;
+    const h2 p1 = (ax + df_hi(by)) + (dx * df_hi(dy)) * c2;
+    const h2 op = df_lo(opr);
+    h2 a0 = __builtin_elementwise_min(op * df_lookup2(tbl, p0), C099);
+    h2 a1 = __builtin_elementwise_min(op * df_lookup2(tbl, p1), C099);
+    if (!alive) {
+        a0 = df_h2(0u);
+        a1 = df_h2(0u);
+    }
+    const h2 w0 = a0 * st.T[0], w1 = a1 * st.T[1];
+    const h2 r = df_hi(opr), g = df_lo(gb), b = df_hi(gb);
+    st.Cr[0] = st.Cr[0] + r * w0;
+    st.Cr[1] = st.Cr[1] + r * w1;
+    st.Cg[0] = st.Cg[0] + g * w0;
+    st.Cg[1] = st.Cg[1] + g * w1;
+    st.Cb[0] = st.Cb[0] + b * w0;
+    st.Cb[1] = st.Cb[1] + b * w1;
+    st.T[0] = st.T[0] * (ONE - a0);
+    st.T[1] = st.T[1] * (ONE - a1);
+}
+
+// max transmittance of a lane's 4 pixels >= fp16(1/255); T >= 0, so fp16 order is bit order
+__device__ __forceinline__ bool df_alive(const DfEyeState& st, uint32_t thrBits) {
+    const uint32_t a = df_u32(st.T[0]), b = df_u32(st.T[1]);
+    const uint32_t m = max(max(a & 0xFFFFu, a >> 16), max(b & 0xFFFFu, b >> 16));
+    return m >= thrBits;
+}
+
+template <int NW>
+__global__ __launch_bounds__(NW * 64) void k_df_blend(const uint2* __restrict__ headers,
+                                                      const uint32_t* __restrict__ gids,
+                                                      const StereoTiledRenderData* __restrict__ rd,
+                                                      const uint16_t* __restrict__ expTable,
+                                                      uint32_t* __restrict__ queue, uint32_t tilesX,
+                                                      uint32_t tileCount, uint32_t W, uint32_t H,
+                                                      uint8_t* __restrict__ color, size_t pitch, int fmt) {
+    __shared__ __attribute__((aligned(16))) uint16_t tbl[65536];
+    __shared__ __attribute__((aligned(16))) uint4 stage[NW][kDfBatch * 2];
+    __shared__ uint16_t div255[256];
+    {
+        const uint4* src = (const uint4*)expTable;
+        uint4* dst = (uint4*)tbl;
+        for (int i = threadIdx.x; i < 65536 * 2 / 16; i += NW * 64) dst[i] = src[i];
+        if (threadIdx.x < 256) div255[threadIdx.x] = f_to_hbits((float)threadIdx.x / 255.0f);  // getColor
+    }
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    const uint32_t thrBits = (uint32_t)f_to_hbits(1.0f / 255.0f);  // half(1.0h / 255.0h)
+    const uint32_t bpp = fmt == GSM_COLOR_FORMAT_RGBA16F ? 8u : (fmt == GSM_COLOR_FORMAT_RGBA32F ? 16u : 4u);
+    const h2 ONE = {(h1)1.0f, (h1)1.0f};
+    uint4* stg = stage[wave];
+    for (;;) {
+        uint32_t t = 0;
+        if (lane == 0) t = atomicAdd(queue, 1u);
+        t = (uint32_t)__shfl((int)t, 0, 64);
+        if (t >= tileCount) break;
+        const uint2 hd = headers[t];
+        const uint32_t tileX = t % tilesX, tileY = t / tilesX;
+        const uint32_t bx = tileX * kDfTile + (lane & 7u) * 2u, by = tileY * kDfTile + (lane >> 3) * 2u;
+        const h2 PX = {(h1)(float)bx, (h1)(float)(bx + 1u)};
+        const h2 PY = {(h1)(float)by, (h1)(float)(by + 1u)};
+        DfEyeState E[2];
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+            E[e].T[0] = E[e].T[1] = ONE;
+            E[e].Cr[0] = E[e].Cr[1] = E[e].Cg[0] = E[e].Cg[1] = E[e].Cb[0] = E[e].Cb[1] = df_h2(0u);
+        }
+        bool done = false;
+        for (uint32_t b0 = 0; b0 < hd.y && !done; b0 += kDfBatch) {
+            const uint32_t n = min(kDfBatch, hd.y - b0);
+            const uint32_t rec = lane >> 1;
+            if (rec < n) {
+                const uint32_t g = gids[hd.x + b0 + rec];
+                uint4 v = ((const uint4*)(rd + g))[lane & 1u];
+                if (lane & 1u) {  // colorR, G, B, opacity (bytes 24..27) -> fp16 {op, r}, {g, b}
+                    const uint32_t c = v.z;
+                    v.z = (uint32_t)div255[c >> 24] | ((uint32_t)div255[c & 0xFFu] << 16);
+                    v.w = (uint32_t)div255[(c >> 8) & 0xFFu] | ((uint32_t)div255[(c >> 16) & 0xFFu] << 16);
+                }
+                stg[lane] = v;
+            }
+            df_wave_sync();
+            for (uint32_t j = 0; j < n; ++j) {
+                const bool aL = df_alive(E[0], thrBits), aR = df_alive(E[1], thrBits);
+                if (!__any(aL || aR)) {  // every lane has taken the reference's break
+                    done = true;
+                    break;
+                }
+                const uint4 s0 = stg[2 * j], s1 = stg[2 * j + 1];
+                const h2 opr = df_h2(s1.z), gb = df_h2(s1.w);
+                // gMean.x >= -60000.0h: the eye's mean is real (uniform over the wave)
+                const h2 mL = df_h2(s0.x), mR = df_h2(s0.w);
+                if ((float)mL.x >= -60000.0f)
+                    df_blend_eye(E[0], aL, mL, df_h2(s0.y), df_h2(s0.z), opr, gb, PX, PY, tbl);
+                if ((float)mR.x >= -60000.0f)
+                    df_blend_eye(E[1], aR, mR, df_h2(s1.x), df_h2(s1.y), opr, gb, PX, PY, tbl);
+            }
+            df_wave_sync();  // the stage is rewritten by the next batch
+        }
+        // (C, 1 - T) of eye e's pixel (x, y) lands in target row H - 1 - y, column e * W + x; a tile
+        // with an empty list is not an active tile and keeps the clear value (0, 0, 0, 1)
+        const uint32_t clearA = hd.y == 0 ? 0x3C003C00u : 0u;
+#pragma unroll
+        for (int e = 0; e < 2; ++e)
+#pragma unroll
+            for (int row = 0; row < 2; ++row) {
+                const uint32_t y = by + (uint32_t)row;
+                if (y >= H) continue;
+                uint8_t* trow = color + (size_t)(H - 1u - y) * pitch + (size_t)e * W * bpp;
+                const uint32_t ur = df_u32(E[e].Cr[row]), ug = df_u32(E[e].Cg[row]);
+                const uint32_t ub = df_u32(E[e].Cb[row]), ua = df_u32(ONE - E[e].T[row]) | clearA;
+                if (bx < W)
+                    store_color_px(fmt, (char*)(trow + (size_t)bx * bpp), (ur & 0xFFFFu) | (ug << 16),
+                                   (ub & 0xFFFFu) | (ua << 16));
+                if (bx + 1u < W)
+                    store_color_px(fmt, (char*)(trow + (size_t)(bx + 1u) * bpp), (ur >> 16) | (ug & 0xFFFF0000u),
+                                   (ub >> 16) | (ua & 0xFFFF0000u));
+            }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// launchers
+// ---------------------------------------------------------------------------
+template <bool HALF>
+static void df_launch_project_t(uint32_t deg, const void* world, const void* harm, const DfArgs& a,
+                                const DfArena& A, hipStream_t s) {
+    const uint32_t blocks = (a.count + kDfBlock - 1) / kDfBlock;
+    if (blocks == 0) return;
+#define GSM_DF_PROJ(D)                                                                                   \
+    hipLaunchKernelGGL((k_df_project<HALF, D>), dim3(blocks), dim3(kDfBlock), 0, s, world, harm, a,       \
+                       A.renderData, A.bounds, A.touched, A.depthKeys, A.blockSums)
+    switch (deg) {
+        case 0: GSM_DF_PROJ(0); break;
+        case 1: GSM_DF_PROJ(1); break;
+        case 2: GSM_DF_PROJ(2); break;
+        default: GSM_DF_PROJ(3); break;
+    }
+#undef GSM_DF_PROJ
+}
+
+void df_launch_project(bool halfInput, uint32_t deg, const void* world, const void* harm, const DfArgs& a,
+                       const DfArena& A, hipStream_t s) {
+    if (halfInput) df_launch_project_t<true>(deg, world, harm, a, A, s);
+    else df_launch_project_t<false>(deg, world, harm, a, A, s);
+}
+
+void df_launch_compact(const DfArgs& a, const DfArena& A, hipStream_t s) {
+    const uint32_t blocks = (a.count + kDfBlock - 1) / kDfBlock;
+    if (blocks == 0) return;
+    hipLaunchKernelGGL(k_df_compact, dim3(blocks), dim3(kDfBlock), 0, s, a.count, A.touched, A.depthKeys,
+                       A.blockSums, A.dkeys[0], A.dvals[0]);
+}
+
+void df_launch_instance_counts(const uint32_t* order, const DfArgs& a, const DfArena& A, hipStream_t s) {
+    const uint32_t blocks = (a.count + kDfBlock - 1) / kDfBlock;
+    if (blocks == 0) return;
+    hipLaunchKernelGGL(k_df_icount, dim3(blocks), dim3(kDfBlock), 0, s, A.visHdr, order, A.touched, A.instSums);
+}
+
+void df_launch_instances(const uint32_t* order, const DfArgs& a, const DfArena& A, hipStream_t s) {
+    const uint32_t blocks = (a.count + kDfBlock - 1) / kDfBlock;
+    if (blocks == 0) return;
+    hipLaunchKernelGGL(k_df_instances, dim3(blocks), dim3(kDfBlock), 0, s, A.visHdr, order, A.touched, A.bounds,
+                       A.instSums, a.maxInstances, a.tilesX, A.ikeys[0], A.ivals[0]);
+}
+
+void df_launch_ranges(const uint32_t* sortedTiles, const DfArgs& a, const DfArena& A, hipStream_t s) {
+    const uint32_t blocks = (a.tileCount + 255u) / 256u;
+    if (blocks == 0) return;
+    hipLaunchKernelGGL(k_df_ranges, dim3(blocks), dim3(256), 0, s, sortedTiles, A.instHdr, a.tileCount, A.headers);
+}
+
+constexpr int kDfBlendWaves = 16;
+void df_launch_blend(const uint32_t* sortedGids, const DfArgs& a, const DfArena& A, void* color, size_t pitch,
+                     int colorFormat, int numCUs, hipStream_t s) {
+    uint32_t grid = (uint32_t)(numCUs > 0 ? numCUs : 256);
+    const uint32_t need = (a.tileCount + kDfBlendWaves - 1) / kDfBlendWaves;
+    if (grid > need) grid = need;
+    if (grid == 0) return;
+    hipLaunchKernelGGL(k_df_blend<kDfBlendWaves>, dim3(grid), dim3(kDfBlendWaves * 64), 0, s, A.headers, sortedGids,
+                       A.renderData, A.expTable, A.queue, a.tilesX, a.tileCount, (uint32_t)a.width,
+                       (uint32_t)a.height, (uint8_t*)color, pitch, colorFormat);
+}
+
+}  // namespace gsm

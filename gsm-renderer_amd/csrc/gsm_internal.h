@@ -88,6 +88,10 @@ void launch_records_in(const void* records, const ProjectArgs& args, const Devic
                        hipStream_t stream);
 void launch_scan_blocks(uint32_t numBlocks, const ProjectArgs& args, const DeviceArena& A,
                         hipStream_t stream);
+// the same scan for any array of nb per-block sums: exclusive scan in place, the total clamped
+// to cap into hdr (overflow flag when it exceeds cap), *queue = 0
+void launch_scan_sums(uint32_t* sums, uint32_t nb, uint32_t cap, TileAssignmentHeader* hdr, uint32_t* queue,
+                      hipStream_t stream);
 // duplicate-with-keys (GlobalShaders.metal:623-678 fused with :266-295)
 void launch_scatter(const ProjectArgs& args, const DeviceArena& A, hipStream_t stream);
 // per-tile binary search headers (GlobalShaders.metal:304-363), tiles of rows [rowBegin,rowEnd)

@@ -106,6 +106,18 @@ struct BlendRecordA {
     uint32_t x, y, z, w;
 };
 
+// BridgingTypes.h:250-276 -- 32 B projected splat of the DepthFirst stereo path: per eye fp16
+// mean, conic (cxx, cyy, 2*cxy) and depth; shared u8 colour/opacity and fp16 centre depth.
+struct StereoTiledRenderData {
+    uint16_t leftMeanX, leftMeanY, leftCxx, leftCyy, leftCxy2, leftDepth;
+    uint16_t rightMeanX, rightMeanY, rightCxx, rightCyy, rightCxy2, rightDepth;
+    uint8_t colorR, colorG, colorB, opacity;
+    uint16_t centerDepth, pad0;
+};
+static_assert(sizeof(StereoTiledRenderData) == 32, "StereoTiledRenderData must be 32 B");
+static_assert(offsetof(StereoTiledRenderData, rightMeanX) == 12, "layout");
+static_assert(offsetof(StereoTiledRenderData, colorR) == 24, "layout");
+
 // Tile-slab bookkeeping for one frame.
 struct FrameGeometry {
     uint32_t tilesX, tilesY, tileCount;

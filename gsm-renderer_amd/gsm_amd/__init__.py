@@ -175,6 +175,12 @@ class _Counters(C.Structure):
                 ("tiles_y", C.c_uint32), ("tile_count", C.c_uint32), ("gaussian_count", C.c_uint32)]
 
 
+class _DfCounters(C.Structure):
+    _fields_ = [("gaussian_count", C.c_uint32), ("visible", C.c_uint32), ("total_instances", C.c_uint32),
+                ("max_instances", C.c_uint32), ("overflow", C.c_uint32), ("tiles_x", C.c_uint32),
+                ("tiles_y", C.c_uint32), ("tile_count", C.c_uint32)]
+
+
 _LIB = None
 
 # every function include/gsm_renderer.h and include/gsm_debug.h declare, with ctypes signature
@@ -210,6 +216,18 @@ _SIGNATURES = {
                                       C.c_void_p], C.c_int),
     "gsm_global_render_records": ([C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32,
                                    C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t], C.c_int),
+    # include/gsm_depthfirst.h
+    "gsm_depthfirst_create": ([C.POINTER(_Config), C.c_int, C.POINTER(C.c_void_p)], C.c_int),
+    "gsm_depthfirst_destroy": ([C.c_void_p], None),
+    "gsm_depthfirst_render_stereo_sbs": ([C.c_void_p, C.c_void_p, C.POINTER(_Input), C.POINTER(_Camera),
+                                          C.POINTER(_Camera), C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p,
+                                          C.c_size_t], C.c_int),
+    "gsm_depthfirst_debug_counters": ([C.c_void_p, C.POINTER(_DfCounters)], C.c_int),
+    "gsm_depthfirst_debug_copy": ([C.c_void_p, C.c_int, C.c_void_p, C.c_size_t, C.POINTER(C.c_size_t)],
+                                  C.c_int),
+    "gsm_depthfirst_set_profiling": ([C.c_void_p, C.c_int], C.c_int),
+    "gsm_depthfirst_stage_times": ([C.c_void_p, C.POINTER(C.c_float), C.c_int], C.c_int),
+    "gsm_depthfirst_last_gpu_time": ([C.c_void_p, C.POINTER(C.c_double)], C.c_int),
 }
 
 SPLAT_RECORD_BYTES = 48  # include/gsm_multigpu.h GSM_SPLAT_RECORD_BYTES
@@ -413,6 +431,113 @@ class GlobalRenderer:
         if which == BufferId.EXP_TABLE:
             return raw.view(np.uint16)
         return raw
+
+
+class DepthFirstBuffer(enum.IntEnum):  # include/gsm_depthfirst.h gsm_depthfirst_buffer
+    RENDER_DATA = 0
+    BOUNDS = 1
+    TOUCHED = 2
+    DEPTH_KEYS = 3
+    DEPTH_ORDER = 4
+    INSTANCE_TILES = 5
+    INSTANCE_GAUSSIANS = 6
+    HEADERS = 7
+
+
+DF_STAGES = ("project", "depth_sort", "instances", "tile_sort", "blend")  # gsm_depthfirst_stage
+
+# StereoTiledRenderData (BridgingTypes.h:250-276), 32 B
+STEREO_RENDER_DATA = np.dtype([(f, "<u2") for f in (
+    "leftMeanX", "leftMeanY", "leftCxx", "leftCyy", "leftCxy2", "leftDepth",
+    "rightMeanX", "rightMeanY", "rightCxx", "rightCyy", "rightCxy2", "rightDepth")] +
+    [("colorR", "u1"), ("colorG", "u1"), ("colorB", "u1"), ("opacity", "u1"),
+     ("centerDepth", "<u2"), ("pad0", "<u2")])
+
+
+class DepthFirstRenderer:
+    """DepthFirstRenderer (DepthFirstRenderer.swift:11-831) on one HIP device: the stereo
+    side-by-side path (renderStereo(target: .sideBySide), :205-223, 469-512).  The mono
+    render/renderStereo(.foveated) entry points of the reference are out of scope."""
+
+    def __init__(self, device: Optional[int] = None, config: RendererConfig = RendererConfig()):
+        L = _lib()
+        self.config = config
+        cfg = _Config(int(config.max_gaussians), int(config.max_width), int(config.max_height),
+                      int(config.precision), int(config.color_format),
+                      int(config.gaussian_color_space), int(bool(config.back_to_front)))
+        h = C.c_void_p()
+        dev = -1 if device is None else int(device)
+        _check(L.gsm_depthfirst_create(C.byref(cfg), dev, C.byref(h)), "gsm_depthfirst_create")
+        self._h = h
+        self.device = dev
+        self._bpp = ColorFormat(int(config.color_format)).bytes_per_pixel
+
+    def close(self):
+        if getattr(self, "_h", None) and self._h.value:
+            _lib().gsm_depthfirst_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def render_stereo_sbs(self, color_texture, input: GaussianInput, left: CameraParams, right: CameraParams,
+                          width_per_eye: int, height: int, scene_transform=None, stream=None,
+                          color_pitch: Optional[int] = None):
+        """Both eyes side by side into color_texture ([height, 2 * width_per_eye] of the
+        config's colour format), as the reference's copy pass leaves them (rows flipped)."""
+        inp = _Input(_ptr(input.gaussians), _ptr(input.harmonics), int(input.gaussian_count),
+                     int(input.sh_components))
+        cl, cr = _camera_struct(left), _camera_struct(right)
+        st_arr = None
+        if scene_transform is not None:
+            st_arr = (C.c_float * 16)(*[float(v) for v in np.asarray(scene_transform, np.float32).reshape(16)])
+        cp = color_pitch if color_pitch is not None else 2 * int(width_per_eye) * self._bpp
+        st = _lib().gsm_depthfirst_render_stereo_sbs(self._h, _stream_handle(stream), C.byref(inp), C.byref(cl),
+                                                     C.byref(cr), st_arr, int(width_per_eye), int(height),
+                                                     _ptr(color_texture), cp)
+        _check(st, "gsm_depthfirst_render_stereo_sbs")
+
+    @property
+    def last_gpu_time(self) -> Optional[float]:
+        s = C.c_double()
+        st = _lib().gsm_depthfirst_last_gpu_time(self._h, C.byref(s))
+        return float(s.value) if st == 0 else None
+
+    def set_profiling(self, stage_events: bool = True, blend_events: bool = False):
+        flags = (1 if stage_events else 0) | (8 if blend_events else 0)
+        _check(_lib().gsm_depthfirst_set_profiling(self._h, flags), "set_profiling")
+
+    def stage_times_ms(self) -> dict:
+        arr = (C.c_float * len(DF_STAGES))()
+        _check(_lib().gsm_depthfirst_stage_times(self._h, arr, len(DF_STAGES)), "gsm_depthfirst_stage_times")
+        return {k: float(v) for k, v in zip(DF_STAGES, arr)}
+
+    def counters(self) -> dict:
+        c = _DfCounters()
+        _check(_lib().gsm_depthfirst_debug_counters(self._h, C.byref(c)), "gsm_depthfirst_debug_counters")
+        return {name: int(getattr(c, name)) for name, _ in _DfCounters._fields_}
+
+    def copy_buffer(self, which: DepthFirstBuffer) -> np.ndarray:
+        L = _lib()
+        need = C.c_size_t()
+        _check(L.gsm_depthfirst_debug_copy(self._h, int(which), None, 0, C.byref(need)), "debug_copy")
+        n = int(need.value)
+        raw = np.zeros(max(n, 1), np.uint8)
+        if n:
+            _check(L.gsm_depthfirst_debug_copy(self._h, int(which), raw.ctypes.data, n, None), "debug_copy")
+        raw = raw[:n]
+        if which == DepthFirstBuffer.RENDER_DATA:
+            return raw.view(STEREO_RENDER_DATA)
+        if which == DepthFirstBuffer.BOUNDS:
+            return raw.view(np.int32).reshape(-1, 4)
+        if which == DepthFirstBuffer.HEADERS:
+            return raw.view(np.uint32).reshape(-1, 2)
+        if which in (DepthFirstBuffer.DEPTH_ORDER, DepthFirstBuffer.INSTANCE_GAUSSIANS):
+            return raw.view(np.int32)
+        return raw.view(np.uint32)
 
 
 def sort_pairs_u32(keys, values, key_bits: int = 32, stream=None):

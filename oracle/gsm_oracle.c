@@ -1158,3 +1158,445 @@ int og_convert_color(const uint16_t *src, size_t n, int format, void *dst) {
     }
     return format == 1 ? 16 : 4;
 }
+
+/* ================================================================== */
+/* DepthFirst stereo side-by-side              */
+/* Sources/Renderer/DepthFirstRenderer/DepthFirstRenderer.swift:469-831 */
+/* and DepthFirstShaders.metal (kernels cited per function).           */
+/* ================================================================== */
+
+/* float_to_sortable_uint (DepthFirstShaders.metal:33-37). */
+static inline uint32_t df_sortable(float v) {
+    uint32_t b = ogm_fbits(v);
+    return b ^ ((b & 0x80000000u) ? 0xFFFFFFFFu : 0x80000000u);
+}
+
+void og_sincos_theta(float th, float *s, float *c) { ogm_sincos_theta(th, s, c); }
+uint32_t og_float_to_sortable(float v) { return df_sortable(v); }
+
+/* conicFromThetaSigmas (GaussianShared.h:490-510) for an fp32 angle (sincos: numeric contract). */
+static inline conic3 conic_from_theta(float th, float sigma1, float sigma2) {
+    float s, c;
+    ogm_sincos_theta(th, &s, &c);
+    float sig1 = fmaxf(sigma1, 1e-4f);
+    float sig2 = fmaxf(sigma2, 1e-4f);
+    float iv1 = 1.0f / (sig1 * sig1);
+    float iv2 = 1.0f / (sig2 * sig2);
+    float cc = c * c, ss = s * s, cs = c * s;
+    conic3 o;
+    o.A = cc * iv1 + ss * iv2;
+    o.B = cs * (iv1 - iv2);
+    o.C = ss * iv1 + cc * iv2;
+    return o;
+}
+
+/* EyeProjectionResult (DepthFirstShaders.metal:236-247). */
+typedef struct {
+    int visible;
+    float sx, sy, theta, s1, s2, det_cov, depth;
+    int32_t tb[4];
+} df_eye;
+
+/* projectToEye (DepthFirstShaders.metal:249-339). */
+static df_eye df_project_eye(f3 pos, f3 scale, f4 quat, const float *scene, float scene_scale,
+                             const float *view, const float *proj, float W, float Hh, float nearp,
+                             float farp, int tiles_x, int tiles_y) {
+    df_eye e;
+    memset(&e, 0, sizeof(e));
+    e.tb[0] = 0; e.tb[1] = -1; e.tb[2] = 0; e.tb[3] = -1;
+    f4 p4 = {pos.x, pos.y, pos.z, 1.0f};
+    f4 wp = mat4_mul_vec(scene, p4);
+    f4 vp = mat4_mul_vec(view, wp);
+    f4 clip = mat4_mul_vec(proj, vp);
+    e.depth = clip.w;
+    if (!(clip.w > nearp)) return e;  /* isInFrontOfCameraClipW */
+    if (e.depth > farp) return e;     /* cullByFarPlane (GaussianShared.h:732-734) */
+    float ndcx = clip.x / clip.w, ndcy = clip.y / clip.w;
+    /* ndcToScreen (GaussianShared.h:150-155): no pixel-centre shift */
+    e.sx = (ndcx + 1.0f) * 0.5f * W;
+    e.sy = (ndcy + 1.0f) * 0.5f * Hh;
+    f3 ss = {scale.x * scene_scale, scale.y * scene_scale, scale.z * scene_scale};
+    m3 cov3d = build_cov3d(ss, quat);
+    f3 vp3 = {vp.x, vp.y, vp.z};
+    m2 cov2d = project_cov2d(&cov3d, vp3, view, proj, W, Hh);
+    cov2d = stabilize_cov2d(cov2d, W, Hh);
+    float th, s1, s2;
+    if (!cov_to_theta_sigmas(cov2d, &th, &s1, &s2)) return e;
+    e.theta = th; e.s1 = s1; e.s2 = s2;
+    float a = cov2d.c[0].x, b = 0.5f * (cov2d.c[0].y + cov2d.c[1].x), d = cov2d.c[1].y;
+    e.det_cov = fmaxf(a * d - b * b, 0.0f);
+    float radius = 3.0f * fmaxf(s1, s2);
+    if (radius < 0.5f) return e; /* cullByRadius */
+    f2 obb = obb_extents(cov2d, 3.0f);
+    if (e.sx + obb.x < 0.0f || e.sx - obb.x > W || e.sy + obb.y < 0.0f || e.sy - obb.y > Hh) return e;
+    /* computeTileBounds (GaussianShared.h:791-828), 16x16 tiles (DepthFirstRenderer.swift:8-9) */
+    float xmin = clampf(e.sx - obb.x, 0.0f, W - 1.0f), xmax = clampf(e.sx + obb.x, 0.0f, W - 1.0f);
+    float ymin = clampf(e.sy - obb.y, 0.0f, Hh - 1.0f), ymax = clampf(e.sy + obb.y, 0.0f, Hh - 1.0f);
+    int minTX = (int)floorf(xmin / 16.0f), maxTX = (int)ceilf(xmax / 16.0f) - 1;
+    int minTY = (int)floorf(ymin / 16.0f), maxTY = (int)ceilf(ymax / 16.0f) - 1;
+    if (minTX < 0) minTX = 0;
+    if (minTY < 0) minTY = 0;
+    if (maxTX > tiles_x - 1) maxTX = tiles_x - 1;
+    if (maxTY > tiles_y - 1) maxTY = tiles_y - 1;
+    e.tb[0] = minTX; e.tb[1] = maxTX; e.tb[2] = minTY; e.tb[3] = maxTY;
+    e.visible = 1;
+    return e;
+}
+
+typedef struct {
+    const og_config *cfg;
+    const void *gaussians, *harmonics;
+    uint32_t shk;
+    const og_camera *left, *right;
+    const float *scene;
+    float scene_scale;
+    float W, H;
+    int tiles_x, tiles_y;
+    og_df_frame *f;
+} df_ctx;
+
+static void df_mark_culled(og_df_frame *f, uint32_t gid) {
+    int32_t *b = f->bounds + 4 * (size_t)gid;
+    b[0] = 0; b[1] = -1; b[2] = 0; b[3] = -1;
+    f->touched[gid] = 0;
+    f->depth_keys[gid] = 0xFFFFFFFFu;
+}
+
+/* depthFirstStereoProjectCullKernel (DepthFirstShaders.metal:341-499). */
+static void df_project_range(void *vctx, uint32_t lo, uint32_t hi) {
+    df_ctx *X = (df_ctx *)vctx;
+    og_df_frame *f = X->f;
+    const int half_in = X->cfg->precision == 1;
+    const float nearp = X->left->near_plane, farp = X->left->far_plane; /* StereoCameraUniforms: left eye's */
+    const float alphaThreshold = 0.005f, totalInkThreshold = 2.0f;
+    const uint16_t hneg = og_f2h(-1e10f);
+    for (uint32_t gid = lo; gid < hi; ++gid) {
+        f3 pos, scale;
+        float opacity;
+        f4 rot;
+        if (half_in) {
+            const og_world16 *g = (const og_world16 *)X->gaussians + gid;
+            pos.x = g->px; pos.y = g->py; pos.z = g->pz;
+            scale.x = H(g->sx); scale.y = H(g->sy); scale.z = H(g->sz);
+            opacity = H(g->opacity);
+            rot.x = H(g->rx); rot.y = H(g->ry); rot.z = H(g->rz); rot.w = H(g->rw);
+        } else {
+            const og_world32 *g = (const og_world32 *)X->gaussians + gid;
+            pos.x = g->px; pos.y = g->py; pos.z = g->pz;
+            scale.x = g->sx; scale.y = g->sy; scale.z = g->sz;
+            opacity = g->opacity;
+            rot.x = g->rot[0]; rot.y = g->rot[1]; rot.z = g->rot[2]; rot.w = g->rot[3];
+        }
+        if (fmaxf(scale.x, fmaxf(scale.y, scale.z)) < 0.0005f) { df_mark_culled(f, gid); continue; }
+        if (opacity < alphaThreshold) { df_mark_culled(f, gid); continue; }
+        f4 quat = normalize_quat(rot);
+        df_eye L = df_project_eye(pos, scale, quat, X->scene, X->scene_scale, X->left->view, X->left->proj,
+                                  X->W, X->H, nearp, farp, X->tiles_x, X->tiles_y);
+        df_eye R = df_project_eye(pos, scale, quat, X->scene, X->scene_scale, X->right->view, X->right->proj,
+                                  X->W, X->H, nearp, farp, X->tiles_x, X->tiles_y);
+        if (!L.visible && !R.visible) { df_mark_culled(f, gid); continue; }
+        float checkDepth = L.visible ? L.depth : R.depth;
+        if (L.visible && R.visible) checkDepth = (L.depth + R.depth) * 0.5f;
+        float detCov = L.visible ? L.det_cov : R.det_cov;
+        if (L.visible && R.visible) detCov = fmaxf(L.det_cov, R.det_cov);
+        { /* cullByTotalInk (GaussianShared.h:739-751) + computeDepthFactor (:275-278) */
+            float ink = opacity * 6.283185f * sqrtf(fmaxf(detCov, 1e-12f));
+            float adjFar = farp * 0.02f;
+            float s = saturatef((adjFar - checkDepth) / (adjFar - nearp));
+            float depthFactor = 1.0f - s * s;
+            if (ink < depthFactor * totalInkThreshold) { df_mark_culled(f, gid); continue; }
+        }
+        f3 mid = {(X->left->position[0] + X->right->position[0]) * 0.5f,
+                  (X->left->position[1] + X->right->position[1]) * 0.5f,
+                  (X->left->position[2] + X->right->position[2]) * 0.5f};
+        f3 col = compute_sh_color(X->harmonics, half_in, gid, pos, mid, X->shk);
+        col.x = fmaxf(col.x + 0.5f, 0.0f);
+        col.y = fmaxf(col.y + 0.5f, 0.0f);
+        col.z = fmaxf(col.z + 0.5f, 0.0f);
+        if (X->cfg->color_space == 1) {
+            col.x = srgb_to_linear(col.x);
+            col.y = srgb_to_linear(col.y);
+            col.z = srgb_to_linear(col.z);
+        }
+        int32_t ub[4];
+        if (L.visible && R.visible) {
+            ub[0] = L.tb[0] < R.tb[0] ? L.tb[0] : R.tb[0];
+            ub[1] = L.tb[1] > R.tb[1] ? L.tb[1] : R.tb[1];
+            ub[2] = L.tb[2] < R.tb[2] ? L.tb[2] : R.tb[2];
+            ub[3] = L.tb[3] > R.tb[3] ? L.tb[3] : R.tb[3];
+        } else {
+            const int32_t *t = L.visible ? L.tb : R.tb;
+            ub[0] = t[0]; ub[1] = t[1]; ub[2] = t[2]; ub[3] = t[3];
+        }
+        int ux = ub[1] - ub[0] + 1, uy = ub[3] - ub[2] + 1;
+        if (ux < 0) ux = 0;
+        if (uy < 0) uy = 0;
+        uint32_t touched = (uint32_t)(ux * uy);
+        if (touched == 0) { df_mark_culled(f, gid); continue; }
+        og_stereo_render_data rd;
+        memset(&rd, 0, sizeof(rd));
+        const df_eye *eyes[2] = {&L, &R};
+        uint16_t *dst[2] = {&rd.leftMeanX, &rd.rightMeanX};
+        for (int e = 0; e < 2; ++e) {
+            uint16_t *o = dst[e]; /* meanX, meanY, cxx, cyy, cxy2, depth */
+            if (eyes[e]->visible) {
+                conic3 k = conic_from_theta(eyes[e]->theta, eyes[e]->s1, eyes[e]->s2);
+                o[0] = og_f2h(eyes[e]->sx);
+                o[1] = og_f2h(eyes[e]->sy);
+                o[2] = og_f2h(k.A);
+                o[3] = og_f2h(k.C);
+                o[4] = og_f2h(2.0f * k.B);
+                o[5] = og_f2h(eyes[e]->depth);
+            } else {
+                o[0] = hneg; o[1] = hneg; o[2] = 0; o[3] = 0; o[4] = 0; o[5] = 0;
+            }
+        }
+        rd.colorR = (uint8_t)clampf(col.x * 255.0f, 0.0f, 255.0f);
+        rd.colorG = (uint8_t)clampf(col.y * 255.0f, 0.0f, 255.0f);
+        rd.colorB = (uint8_t)clampf(col.z * 255.0f, 0.0f, 255.0f);
+        rd.opacity = (uint8_t)clampf(opacity * 255.0f, 0.0f, 255.0f);
+        rd.centerDepth = og_f2h(checkDepth);
+        f->render_data[gid] = rd;
+        int32_t *b = f->bounds + 4 * (size_t)gid;
+        b[0] = ub[0]; b[1] = ub[1]; b[2] = ub[2]; b[3] = ub[3];
+        f->touched[gid] = touched;
+        f->depth_keys[gid] = df_sortable(checkDepth);
+    }
+}
+
+/* depthFirstStereoRender (DepthFirstShaders.metal:1825-1982) for one active tile. */
+typedef struct { og_df_frame *f; uint32_t *active; } df_blend_ctx;
+
+static void df_blend_tiles(void *vctx, uint32_t lo, uint32_t hi) {
+    df_blend_ctx *B = (df_blend_ctx *)vctx;
+    og_df_frame *f = B->f;
+    const uint16_t ONE = 0x3C00u;
+    const uint16_t thr = og_f2h(1.0f / 255.0f); /* half(1.0h/255.0h) */
+    const uint16_t c099 = og_d2h(0.99);
+    const float r2max = 9.0f;                   /* half(9.0f) */
+    const uint32_t W = f->width, Hh = f->height;
+    for (uint32_t ai = lo; ai < hi; ++ai) {
+        uint32_t tile = B->active[ai];
+        uint32_t start = f->headers[2 * tile], count = f->headers[2 * tile + 1];
+        uint32_t tileX = tile % f->tiles_x, tileY = tile / f->tiles_x;
+        for (uint32_t ly = 0; ly < 8; ++ly)
+            for (uint32_t lx = 0; lx < 8; ++lx) {
+                uint32_t baseX = tileX * 16 + lx * 2, baseY = tileY * 16 + ly * 2;
+                /* pixel q = (q & 1, q >> 1): 00, 10, 01, 11 */
+                uint16_t px[4], py[4];
+                for (int q = 0; q < 4; ++q) {
+                    px[q] = og_f2h((float)(baseX + (uint32_t)(q & 1)));
+                    py[q] = og_f2h((float)(baseY + (uint32_t)(q >> 1)));
+                }
+                uint16_t T[2][4], C[2][4][3];
+                for (int e = 0; e < 2; ++e)
+                    for (int q = 0; q < 4; ++q) { T[e][q] = ONE; C[e][q][0] = C[e][q][1] = C[e][q][2] = 0; }
+                for (uint32_t i = 0; i < count; ++i) {
+                    uint16_t mt[2];
+                    for (int e = 0; e < 2; ++e) mt[e] = hmax(hmax(T[e][0], T[e][1]), hmax(T[e][2], T[e][3]));
+                    if (H(hmax(mt[0], mt[1])) < H(thr)) break;
+                    int32_t gi = f->inst_gids[start + i];
+                    if (gi < 0) continue;
+                    const og_stereo_render_data *g = &f->render_data[gi];
+                    uint16_t op = og_f2h(H(og_f2h((float)g->opacity)) / 255.0f);
+                    uint16_t gc[3] = {og_f2h(H(og_f2h((float)g->colorR)) / 255.0f),
+                                      og_f2h(H(og_f2h((float)g->colorG)) / 255.0f),
+                                      og_f2h(H(og_f2h((float)g->colorB)) / 255.0f)};
+                    for (int e = 0; e < 2; ++e) {
+                        if (!(H(mt[e]) >= H(thr))) continue;
+                        const uint16_t *ev = e == 0 ? &g->leftMeanX : &g->rightMeanX;
+                        if (!(H(ev[0]) >= -60000.0f)) continue;
+                        uint16_t p[4], a[4];
+                        int all_out = 1;
+                        for (int q = 0; q < 4; ++q) {
+                            uint16_t dx = hsub(px[q], ev[0]), dy = hsub(py[q], ev[1]);
+                            p[q] = hadd(hadd(hmul(hmul(dx, dx), ev[2]), hmul(hmul(dy, dy), ev[3])),
+                                        hmul(hmul(dx, dy), ev[4]));
+                            if (!(H(p[q]) > r2max)) all_out = 0;
+                        }
+                        int any = 0;
+                        for (int q = 0; q < 4; ++q) {
+                            a[q] = 0;
+                            if (!all_out && !(H(p[q]) > r2max))
+                                a[q] = hmin(hmul(op, g_exp_h[og_f2h(-0.5f * H(p[q]))]), c099);
+                            if (H(a[q]) != 0.0f) any = 1;
+                        }
+                        if (!any) continue;
+                        for (int q = 0; q < 4; ++q) {
+                            uint16_t w = hmul(a[q], T[e][q]);
+                            for (int ch = 0; ch < 3; ++ch) C[e][q][ch] = hadd(C[e][q][ch], hmul(gc[ch], w));
+                            T[e][q] = hmul(T[e][q], hsub(ONE, a[q]));
+                        }
+                    }
+                }
+                for (int e = 0; e < 2; ++e)
+                    for (int q = 0; q < 4; ++q) {
+                        uint32_t x = baseX + (uint32_t)(q & 1), y = baseY + (uint32_t)(q >> 1);
+                        if (x >= W || y >= Hh) continue;
+                        uint16_t *o = f->eye_color + 4 * ((size_t)e * W * Hh + (size_t)y * W + x);
+                        o[0] = C[e][q][0]; o[1] = C[e][q][1]; o[2] = C[e][q][2];
+                        o[3] = hsub(ONE, T[e][q]);
+                    }
+            }
+    }
+}
+
+void og_df_frame_free(og_df_frame *f) {
+    if (!f) return;
+    free(f->render_data); free(f->bounds); free(f->touched); free(f->depth_keys);
+    free(f->depth_order); free(f->inst_tiles); free(f->inst_gids); free(f->headers);
+    free(f->eye_color); free(f->color);
+    free(f);
+}
+
+/* DepthFirstRenderer.renderStereo(.sideBySide) -> renderStereoSideBySideRaster ->
+ * encodeStereoPipeline (DepthFirstRenderer.swift:205-223, 469-512, 595-831). */
+int og_df_render_stereo(const og_config *cfg, const void *gaussians, const void *harmonics,
+                        uint32_t count, uint32_t shk, const og_camera *left, const og_camera *right,
+                        const float *scene_transform, uint32_t width, uint32_t height, int nthreads,
+                        og_df_frame **out) {
+    ensure_init();
+    *out = NULL;
+    if (!cfg || !left || !right || (count > 0 && (!gaussians || !harmonics))) return OG_ERR_INVALID_ARGUMENT;
+    if (cfg->max_gaussians > 30000000u) return OG_ERR_INVALID_GAUSSIAN_COUNT; /* DepthFirstRenderer.swift:51-56 */
+    uint32_t maxG = cfg->max_gaussians ? cfg->max_gaussians : 1u;
+    if (count > maxG) return OG_ERR_INVALID_GAUSSIAN_COUNT; /* encodeStereoPipeline guard :607 */
+    uint32_t maxW = cfg->max_width ? cfg->max_width : 1u, maxH = cfg->max_height ? cfg->max_height : 1u;
+    if (width == 0 || height == 0 || width > maxW || height > maxH) return OG_ERR_INVALID_DIMENSIONS;
+    if (nthreads <= 0) nthreads = (int)sysconf(_SC_NPROCESSORS_ONLN);
+    if (nthreads < 1) nthreads = 1;
+    static const float identity[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
+    const float *scene = scene_transform ? scene_transform : identity;
+
+    og_df_frame *f = (og_df_frame *)calloc(1, sizeof(og_df_frame));
+    if (!f) return OG_ERR_OUT_OF_MEMORY;
+    f->count = count;
+    f->width = width;
+    f->height = height;
+    /* buildBinningParams(gaussianCount:width:height:) (GlobalRenderer.swift:54-70), 16x16 tiles */
+    f->tiles_x = (width + 15u) / 16u;
+    f->tiles_y = (height + 15u) / 16u;
+    f->tile_count = f->tiles_x * f->tiles_y;
+    f->max_instances = 4u * maxG; /* DepthFirstResources.swift:399 */
+    size_t n = count ? count : 1;
+    f->render_data = (og_stereo_render_data *)calloc(n, sizeof(og_stereo_render_data));
+    f->bounds = (int32_t *)calloc(n * 4, sizeof(int32_t));
+    f->touched = (uint32_t *)calloc(n, sizeof(uint32_t));
+    f->depth_keys = (uint32_t *)calloc(n, sizeof(uint32_t));
+    f->depth_order = (int32_t *)calloc(n, sizeof(int32_t));
+    f->headers = (uint32_t *)calloc((size_t)f->tile_count * 2, sizeof(uint32_t));
+    f->eye_color = (uint16_t *)calloc((size_t)2 * width * height * 4, sizeof(uint16_t));
+    f->color = (uint16_t *)calloc((size_t)2 * width * height * 4, sizeof(uint16_t));
+    if (!f->render_data || !f->bounds || !f->touched || !f->depth_keys || !f->depth_order || !f->headers ||
+        !f->eye_color || !f->color) {
+        og_df_frame_free(f);
+        return OG_ERR_OUT_OF_MEMORY;
+    }
+    df_ctx X;
+    memset(&X, 0, sizeof(X));
+    X.cfg = cfg; X.gaussians = gaussians; X.harmonics = harmonics; X.shk = shk;
+    X.left = left; X.right = right; X.scene = scene;
+    /* length(sceneTransform[0].xyz) (DepthFirstShaders.metal:293): sqrt(dot) */
+    {
+        float d = scene[0] * scene[0] + scene[1] * scene[1];
+        d = d + scene[2] * scene[2];
+        X.scene_scale = sqrtf(d);
+    }
+    X.W = (float)width; X.H = (float)height;
+    X.tiles_x = (int)f->tiles_x; X.tiles_y = (int)f->tiles_y;
+    X.f = f;
+    double t0 = now_s();
+    parallel_for(nthreads, count, df_project_range, &X);
+    double t1 = now_s();
+    /* visibilityScatterCompactKernel (DepthFirstShaders.metal:589-621): ascending gid */
+    uint32_t V = 0;
+    uint32_t *keys = (uint32_t *)malloc(sizeof(uint32_t) * n);
+    if (!keys) { og_df_frame_free(f); return OG_ERR_OUT_OF_MEMORY; }
+    for (uint32_t g = 0; g < count; ++g)
+        if (f->touched[g] > 0) { keys[V] = f->depth_keys[g]; f->depth_order[V] = (int32_t)g; V++; }
+    f->visible = V;
+    /* DepthRadixSortEncoder .bits32: 4 stable 8-bit LSD passes (DepthRadixSortEncoder.swift:14-22) */
+    og_radix_sort_pairs(keys, f->depth_order, V);
+    free(keys);
+    /* applyDepthOrderingKernel + prefix sum + createInstancesStereoKernel (:623-640, :790-826) */
+    uint64_t total = 0;
+    for (uint32_t i = 0; i < V; ++i) total += f->touched[f->depth_order[i]];
+    f->overflow = total > f->max_instances ? 1u : 0u; /* prepareDepthFirstDispatchKernel (:2191-2194) */
+    uint32_t tot = (uint32_t)(total > f->max_instances ? f->max_instances : total);
+    f->total_instances = tot;
+    size_t na = tot ? tot : 1;
+    uint32_t *tiles = (uint32_t *)malloc(sizeof(uint32_t) * na);
+    int32_t *gids = (int32_t *)malloc(sizeof(int32_t) * na);
+    f->inst_tiles = (uint32_t *)calloc(na, sizeof(uint32_t));
+    f->inst_gids = (int32_t *)calloc(na, sizeof(int32_t));
+    uint32_t *cnt = (uint32_t *)calloc((size_t)f->tile_count + 1, sizeof(uint32_t));
+    if (!tiles || !gids || !f->inst_tiles || !f->inst_gids || !cnt) {
+        free(tiles); free(gids); free(cnt);
+        og_df_frame_free(f);
+        return OG_ERR_OUT_OF_MEMORY;
+    }
+    uint64_t off = 0;
+    for (uint32_t i = 0; i < V; ++i) {
+        int32_t g = f->depth_order[i];
+        const int32_t *b = f->bounds + 4 * (size_t)g;
+        for (int ty = b[2]; ty <= b[3]; ++ty)
+            for (int tx = b[0]; tx <= b[1]; ++tx) {
+                if (off < f->max_instances) {
+                    tiles[off] = (uint32_t)(ty * (int)f->tiles_x + tx) & 0xFFFFu; /* ushort tile id */
+                    gids[off] = g;
+                }
+                off++;
+            }
+    }
+    /* TileSortEncoder: stable sort of the instances by tile id (a 16-bit LSD radix sort) */
+    for (uint32_t i = 0; i < tot; ++i) cnt[tiles[i] + 1]++;
+    for (uint32_t t = 0; t < f->tile_count; ++t) cnt[t + 1] += cnt[t];
+    for (uint32_t i = 0; i < tot; ++i) {
+        uint32_t p = cnt[tiles[i]]++;
+        f->inst_tiles[p] = tiles[i];
+        f->inst_gids[p] = gids[i];
+    }
+    free(tiles); free(gids); free(cnt);
+    double t2 = now_s();
+    /* extractTileRangesKernel (DepthFirstShaders.metal:1258-1313) */
+    uint32_t *active = (uint32_t *)calloc(f->tile_count ? f->tile_count : 1, sizeof(uint32_t));
+    if (!active) { og_df_frame_free(f); return OG_ERR_OUT_OF_MEMORY; }
+    uint32_t nact = 0;
+    for (uint32_t tile = 0; tile < f->tile_count; ++tile) {
+        if (tot == 0) { f->headers[2 * tile] = 0; f->headers[2 * tile + 1] = 0; continue; }
+        uint32_t l = 0, r = tot;
+        while (l < r) { uint32_t m = (l + r) >> 1; if (f->inst_tiles[m] < tile) l = m + 1; else r = m; }
+        uint32_t s = l;
+        l = s; r = tot;
+        while (l < r) { uint32_t m = (l + r) >> 1; if (f->inst_tiles[m] <= tile) l = m + 1; else r = m; }
+        f->headers[2 * tile] = s;
+        f->headers[2 * tile + 1] = l > s ? l - s : 0u;
+        if (l > s) active[nact++] = tile;
+    }
+    f->active_tiles = nact;
+    /* clearStereoRenderTextureKernel (:1813-1823): both slices (0,0,0,1) */
+    for (size_t i = 0; i < (size_t)2 * width * height; ++i) {
+        f->eye_color[4 * i] = 0; f->eye_color[4 * i + 1] = 0; f->eye_color[4 * i + 2] = 0;
+        f->eye_color[4 * i + 3] = 0x3C00u;
+    }
+    df_blend_ctx B = {f, active};
+    parallel_for_interleaved(nthreads, nact, df_blend_tiles, &B);
+    free(active);
+    /* DepthFirstStereoCopyEncoder (DepthFirstStereoCopyEncoder.swift:29-99): a full-screen
+     * triangle per eye viewport (left at x = 0, right at x = width, StereoConfiguration origin
+     * DepthFirstRenderer.swift:480-485) sampling slice `eye` at uv = clamp(uv, 0, 1) with the
+     * vertex uv (0,0) at NDC (-1,-1) (DepthFirstShaders.metal:1990-2018).  At pixel centres of a
+     * 1:1 viewport the linear filter lands on texel centres (weight 1), and the bottom NDC edge
+     * maps to texture row 0: target row y of eye e is slice e's row height-1-y. */
+    for (uint32_t e = 0; e < 2; ++e)
+        for (uint32_t y = 0; y < height; ++y)
+            memcpy(f->color + 4 * ((size_t)y * 2 * width + (size_t)e * width),
+                   f->eye_color + 4 * ((size_t)e * width * height + (size_t)(height - 1 - y) * width),
+                   (size_t)width * 8);
+    double t3 = now_s();
+    f->t_project = t1 - t0;
+    f->t_sort = t2 - t1;
+    f->t_blend = t3 - t2;
+    *out = f;
+    return OG_OK;
+}

@@ -146,6 +146,45 @@ void og_gen_grid_gaussians(uint32_t count, long seed, og_world32 *world, float *
 /* makeCameraParams (TestUtils.swift:74-94), OpenCV convention, identity view. */
 void og_make_camera(uint32_t width, uint32_t height, og_camera *cam);
 
+/* ---- DepthFirst stereo side-by-side ---------------------------- */
+/* BridgingTypes.h:250-276 StereoTiledRenderData (32 B).  fp16 fields as raw bits; an eye the
+ * gaussian is not visible in has mean = fp16(-1e10) = -inf and zero conic/depth. */
+typedef struct {
+    uint16_t leftMeanX, leftMeanY, leftCxx, leftCyy, leftCxy2, leftDepth;
+    uint16_t rightMeanX, rightMeanY, rightCxx, rightCyy, rightCxy2, rightDepth;
+    uint8_t colorR, colorG, colorB, opacity;
+    uint16_t centerDepth, pad0;
+} og_stereo_render_data;
+
+typedef struct {
+    uint32_t count, width, height; /* width, height: per eye */
+    uint32_t tiles_x, tiles_y, tile_count, max_instances;
+    uint32_t visible, total_instances, overflow, active_tiles;
+    og_stereo_render_data *render_data; /* [count]; culled entries zero-filled */
+    int32_t *bounds;      /* [count*4] union tile rect, (0,-1,0,-1) when culled */
+    uint32_t *touched;    /* [count] tiles of the union rect, 0 when culled */
+    uint32_t *depth_keys; /* [count] float_to_sortable_uint(centre depth), 0xFFFFFFFF when culled */
+    int32_t *depth_order; /* [visible] gaussian ids after the stable 32-bit depth sort */
+    uint32_t *inst_tiles; /* [total_instances] tile ids after the stable tile sort */
+    int32_t *inst_gids;   /* [total_instances] */
+    uint32_t *headers;    /* [tile_count*2] {offset, count} */
+    uint16_t *eye_color;  /* [2][height][width][4] the intermediate rgba16f slices (0 = left) */
+    uint16_t *color;      /* [height][2*width][4] the side-by-side target after the copy */
+    double t_project, t_sort, t_blend;
+} og_df_frame;
+
+/* DepthFirstRenderer.renderStereo(target: .sideBySide) (DepthFirstRenderer.swift:205-223,
+ * 469-512, 595-831).  scene_transform: 16 floats column-major (StereoConfiguration.sceneTransform,
+ * GaussianRendererProtocol.swift:106) or NULL for the identity the side-by-side path uses. */
+int og_df_render_stereo(const og_config *cfg, const void *gaussians, const void *harmonics,
+                        uint32_t count, uint32_t sh_components, const og_camera *left,
+                        const og_camera *right, const float *scene_transform, uint32_t width,
+                        uint32_t height, int nthreads, og_df_frame **out);
+void og_df_frame_free(og_df_frame *f);
+/* sin/cos of an fp32 angle (numeric contract) and float_to_sortable_uint. */
+void og_sincos_theta(float th, float *s, float *c);
+uint32_t og_float_to_sortable(float v);
+
 #ifdef __cplusplus
 }
 #endif

@@ -137,4 +137,34 @@ static inline double ogm_exp_d(double x) {
     return sum;
 }
 
+/* sin/cos of an unquantised fp32 angle th in [0, pi] (conicFromThetaSigmas' fast::sincos,
+ * GaussianShared.h:490-494, as the DepthFirst stereo projection calls it with the fp32 theta,
+ * DepthFirstShaders.metal:455,471).  Reflected about pi/2 like ogm_sincos_d, then Horner
+ * polynomials in double with the Taylor coefficients +-1/n! (compile-time correctly rounded
+ * doubles), only * and + (no contraction), one rounding to fp32.  The GPU evaluates the same
+ * expression (gsm_detmath.h det_sincos_theta) with IEEE double ops, so the bits agree. */
+static inline void ogm_sincos_theta(float th, float *s, float *c) {
+    static const double S[11] = {1.0, -1.0 / 6.0, 1.0 / 120.0, -1.0 / 5040.0, 1.0 / 362880.0,
+                                 -1.0 / 39916800.0, 1.0 / 6227020800.0, -1.0 / 1307674368000.0,
+                                 1.0 / 355687428096000.0, -1.0 / 121645100408832000.0,
+                                 1.0 / 51090942171709440000.0};
+    static const double K[11] = {1.0, -1.0 / 2.0, 1.0 / 24.0, -1.0 / 720.0, 1.0 / 40320.0,
+                                 -1.0 / 3628800.0, 1.0 / 479001600.0, -1.0 / 87178291200.0,
+                                 1.0 / 20922789888000.0, -1.0 / 6402373705728000.0,
+                                 1.0 / 2432902008176640000.0};
+    const double half_pi = 1.5707963267948966192;
+    double x = (double)th, sg = 1.0;
+    if (!(x <= half_pi)) {
+        x = x - 2.0 * half_pi;
+        sg = -1.0;
+    }
+    double x2 = x * x, ps = S[10], pc = K[10];
+    for (int i = 9; i >= 0; --i) {
+        ps = ps * x2 + S[i];
+        pc = pc * x2 + K[i];
+    }
+    *s = (float)(sg * (x * ps));
+    *c = (float)(sg * pc);
+}
+
 #endif

@@ -23,7 +23,13 @@ WORLD16 = np.dtype([("px", "<f4"), ("py", "<f4"), ("pz", "<f4"), ("opacity", "<u
 RENDER_DATA = np.dtype([("meanX", "<u2"), ("meanY", "<u2"), ("theta", "<u2"), ("sigma1", "<u2"),
                         ("sigma2", "<u2"), ("depth", "<u2"), ("colorR", "u1"), ("colorG", "u1"),
                         ("colorB", "u1"), ("opacity", "u1")])
+STEREO_RENDER_DATA = np.dtype([(f, "<u2") for f in (
+    "leftMeanX", "leftMeanY", "leftCxx", "leftCyy", "leftCxy2", "leftDepth",
+    "rightMeanX", "rightMeanY", "rightCxx", "rightCyy", "rightCxy2", "rightDepth")] +
+    [("colorR", "u1"), ("colorG", "u1"), ("colorB", "u1"), ("opacity", "u1"),
+     ("centerDepth", "<u2"), ("pad0", "<u2")])
 assert WORLD32.itemsize == 48 and WORLD16.itemsize == 32 and RENDER_DATA.itemsize == 16
+assert STEREO_RENDER_DATA.itemsize == 32
 
 
 class OgCamera(C.Structure):
@@ -50,6 +56,19 @@ class OgFrame(C.Structure):
                 ("group_iters", C.c_void_p),
                 ("t_project", C.c_double), ("t_assign", C.c_double), ("t_sort", C.c_double),
                 ("t_headers", C.c_double), ("t_blend", C.c_double)]
+
+
+class OgDfFrame(C.Structure):
+    _fields_ = [("count", C.c_uint32), ("width", C.c_uint32), ("height", C.c_uint32),
+                ("tiles_x", C.c_uint32), ("tiles_y", C.c_uint32), ("tile_count", C.c_uint32),
+                ("max_instances", C.c_uint32), ("visible", C.c_uint32),
+                ("total_instances", C.c_uint32), ("overflow", C.c_uint32),
+                ("active_tiles", C.c_uint32),
+                ("render_data", C.c_void_p), ("bounds", C.c_void_p), ("touched", C.c_void_p),
+                ("depth_keys", C.c_void_p), ("depth_order", C.c_void_p),
+                ("inst_tiles", C.c_void_p), ("inst_gids", C.c_void_p), ("headers", C.c_void_p),
+                ("eye_color", C.c_void_p), ("color", C.c_void_p),
+                ("t_project", C.c_double), ("t_sort", C.c_double), ("t_blend", C.c_double)]
 
 
 def build(force: bool = False) -> str:
@@ -100,6 +119,15 @@ def lib():
         L.og_gen_visible_gaussians.argtypes = [C.c_uint32, C.c_long, C.c_void_p, C.c_void_p]
         L.og_gen_grid_gaussians.argtypes = [C.c_uint32, C.c_long, C.c_void_p, C.c_void_p]
         L.og_make_camera.argtypes = [C.c_uint32, C.c_uint32, C.POINTER(OgCamera)]
+        L.og_df_render_stereo.argtypes = [C.POINTER(OgConfig), C.c_void_p, C.c_void_p, C.c_uint32,
+                                          C.c_uint32, C.POINTER(OgCamera), C.POINTER(OgCamera),
+                                          C.c_void_p, C.c_uint32, C.c_uint32, C.c_int,
+                                          C.POINTER(C.POINTER(OgDfFrame))]
+        L.og_df_render_stereo.restype = C.c_int
+        L.og_df_frame_free.argtypes = [C.POINTER(OgDfFrame)]
+        L.og_sincos_theta.argtypes = [C.c_float, C.POINTER(C.c_float), C.POINTER(C.c_float)]
+        L.og_float_to_sortable.argtypes = [C.c_float]
+        L.og_float_to_sortable.restype = C.c_uint32
         _lib = L
     return _lib
 
@@ -223,4 +251,67 @@ def render(world: np.ndarray, harmonics: np.ndarray, sh_components: int, camera:
         }
     finally:
         L.og_frame_free(out)
+    return res
+
+
+def _nthreads(nthreads: int) -> int:
+    if nthreads > 0:
+        return nthreads
+    return int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+
+
+def sincos_theta(theta: float):
+    s, c = C.c_float(), C.c_float()
+    lib().og_sincos_theta(float(theta), C.byref(s), C.byref(c))
+    return s.value, c.value
+
+
+def df_render_stereo(world: np.ndarray, harmonics: np.ndarray, sh_components: int, left: dict,
+                     right: dict, width: int, height: int, scene_transform=None,
+                     max_gaussians: int | None = None, max_width: int | None = None,
+                     max_height: int | None = None, precision: int | None = None,
+                     color_space: int = 0, nthreads: int = 0, count: int | None = None) -> dict:
+    """DepthFirst stereo side-by-side frame (og_df_render_stereo); width/height per eye.
+    "color" is the [height, 2*width, 4] side-by-side target, "eye_color" the two
+    intermediate slices [2, height, width, 4] before the copy's vertical flip."""
+    L = lib()
+    if precision is None:
+        precision = 1 if world.dtype == WORLD16 else 0
+    n = len(world) if count is None else count
+    cfg = OgConfig(max_gaussians if max_gaussians is not None else max(n, 1),
+                   max_width or width, max_height or height, precision, color_space)
+    cl, cr = dict_to_camera(left), dict_to_camera(right)
+    world = np.ascontiguousarray(world)
+    harmonics = np.ascontiguousarray(harmonics)
+    st = None
+    if scene_transform is not None:
+        st = np.ascontiguousarray(np.asarray(scene_transform, np.float32).reshape(16))
+    out = C.POINTER(OgDfFrame)()
+    rc = L.og_df_render_stereo(C.byref(cfg), world.ctypes.data if world.size else None,
+                               harmonics.ctypes.data if harmonics.size else None, n, sh_components,
+                               C.byref(cl), C.byref(cr), st.ctypes.data if st is not None else None,
+                               width, height, _nthreads(nthreads), C.byref(out))
+    if rc != 0:
+        return {"status": rc}
+    f = out.contents
+    try:
+        tot, V = f.total_instances, f.visible
+        res = {
+            "status": 0, "count": f.count, "tiles_x": f.tiles_x, "tiles_y": f.tiles_y,
+            "tile_count": f.tile_count, "max_instances": f.max_instances, "visible": V,
+            "total_instances": tot, "overflow": f.overflow, "active_tiles": f.active_tiles,
+            "render_data": _arr(f.render_data, STEREO_RENDER_DATA, f.count),
+            "bounds": _arr(f.bounds, np.int32, f.count * 4).reshape(-1, 4),
+            "touched": _arr(f.touched, np.uint32, f.count),
+            "depth_keys": _arr(f.depth_keys, np.uint32, f.count),
+            "depth_order": _arr(f.depth_order, np.int32, V),
+            "inst_tiles": _arr(f.inst_tiles, np.uint32, tot),
+            "inst_gids": _arr(f.inst_gids, np.int32, tot),
+            "headers": _arr(f.headers, np.uint32, f.tile_count * 2).reshape(-1, 2),
+            "eye_color": _arr(f.eye_color, np.uint16, 2 * width * height * 4).reshape(2, height, width, 4),
+            "color": _arr(f.color, np.uint16, 2 * width * height * 4).reshape(height, 2 * width, 4),
+            "times": {"project": f.t_project, "sort": f.t_sort, "blend": f.t_blend},
+        }
+    finally:
+        L.og_df_frame_free(out)
     return res

@@ -8,7 +8,8 @@ import subprocess
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-HEADERS = [os.path.join(ROOT, "include", h) for h in ("gsm_renderer.h", "gsm_debug.h", "gsm_multigpu.h")]
+HEADERS = [os.path.join(ROOT, "include", h) for h in ("gsm_renderer.h", "gsm_debug.h", "gsm_multigpu.h",
+                                                            "gsm_depthfirst.h")]
 PLY_HEADER = os.path.join(ROOT, "include", "gsm_ply.h")
 
 

@@ -12,6 +12,8 @@
 // oracle/gsm_oracle.c og_df_render_stereo.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "../../include/gsm_renderer.h"
 #include "gsm_detmath.h"
 #include "gsm_device.h"
@@ -339,33 +341,50 @@ __device__ __forceinline__ h2 df_h2(uint32_t u) { return __builtin_bit_cast(h2, 
 __device__ __forceinline__ uint32_t df_u32(h2 v) { return __builtin_bit_cast(uint32_t, v); }
 __device__ __forceinline__ h2 df_lo(h2 v) { return h2{v.x, v.x}; }
 __device__ __forceinline__ h2 df_hi(h2 v) { return h2{v.y, v.y}; }
-__device__ __forceinline__ h2 df_lookup2(const uint16_t* tbl, h2 p) {
-    const uint32_t pb = df_u32(p);
-    const uint32_t lo = tbl[pb & 0xFFFFu];
-    const uint32_t hi = tbl[pb >> 16];
-    return df_h2(lo | (hi << 16));
-}
+typedef unsigned short df_u16x2 __attribute__((ext_vector_type(2)));
 
 struct DfEyeState {
     h2 T[2], Cr[2], Cg[2], Cb[2];  // [row]: {x, x + 1}
 };
 
-// one list entry for one eye of a lane (depthFirstStereoRender :1872-1913 / :1915-1956)
-__device__ __forceinline__ void df_blend_eye(DfEyeState& st, bool alive, h2 mean, h2 cc, h2 cxy, h2 opr, h2 gb,
-                                             h2 PX, h2 PY, const uint16_t* tbl) {
+// p = ((dx*dx)*cxx + (dy*dy)*cyy) + (dx*dy)*cxy2 for the lane's 2x2 pixels of one eye
+// (DepthFirstShaders.metal:1881-1884); the x terms are shared by the rows, the y terms by the columns
+__device__ __forceinline__ void df_quadform(h2 mean, h2 cc, h2 cxy, h2 PX, h2 PY, h2& p0, h2& p1) {
+    const h2 dx = PX - df_lo(mean);
+    const h2 dy = PY - df_hi(mean);
+    const h2 ax = (dx * dx) * df_lo(cc);
+    const h2 by = (dy * dy) * df_hi(cc);
+    const h2 c2 = df_lo(cxy);
+    p0 = (ax + df_lo(by)) + (dx * df_lo(dy)) * c2;
+    p1 = (ax + df_hi(by)) + (dx * df_hi(dy)) * c2;
+}
+
+// every alpha of the 2x2 group is 0 when each p is in (9, +inf] (the r^2 cutoff; NaN and negative p
+// are not): (bits - 0x4881) mod 2^16 <= 0x7C00 - 0x4881
+__device__ __forceinline__ bool df_all_cut(h2 p0, h2 p1) {
+    const df_u16x2 k = {(unsigned short)0x4881u, (unsigned short)0x4881u};
+    const df_u16x2 d0 = __builtin_bit_cast(df_u16x2, p0) - k, d1 = __builtin_bit_cast(df_u16x2, p1) - k;
+    const df_u16x2 m = __builtin_elementwise_max(d0, d1);
+    return max((uint32_t)m.x, (uint32_t)m.y) <= 0x7C00u - 0x4881u;
+}
+
+// one list entry for one eye of a lane (depthFirstStereoRender :1872-1913 / :1915-1956) from the
+// quadratic forms: alpha = min(opacity * exp(-0.5 p), 0.99) with the r^2 cutoff folded into the
+// table, forced to 0 for a lane whose eye is done, then C += c * (a * T), T *= 1 - a
+__device__ __forceinline__ void df_blend_eye(DfEyeState& st, bool alive, h2 p0, h2 p1, h2 opr, h2 gb,
+                                             const uint16_t* tbl) {
     const h2 ONE = {(h1)1.0f, (h1)1.0f};
     const h1 c099 = (h1)0.99;
     const h2 C099 = {c099, c099};
-    const h2 dx = PX - df_lo(mean);
-    const h2 dy = PY - df_hi(mean);
-    const h2 ax = (dx * dx) * df_lo(cc);  // dx*dx*cxx for x, x+1
-    const h2 by = (dy * dy) * df_hi(cc);  // dy*dy*cyy for rows 0, 1
-    const h2 c2 = df_lo(cxy);
-    const h2 p0 = (ax + df_lo(by)) + (dx * df_lo(dy)) * c2;
-    const h2 p1 = (ax + df_hi(by)) + (dx * df_hi(dy)) * c2;
+    const uint32_t b0 = df_u32(p0), b1 = df_u32(p1);
+    df_u16x2 e0, e1;  // d16 loads straight into the halves
+    e0.x = tbl[b0 & 0xFFFFu];
+    e0.y = tbl[b0 >> 16];
+    e1.x = tbl[b1 & 0xFFFFu];
+    e1.y = tbl[b1 >> 16];
     const h2 op = df_lo(opr);
-    h2 a0 = __builtin_elementwise_min(op * df_lookup2(tbl, p0), C099);
-    h2 a1 = __builtin_elementwise_min(op * df_lookup2(tbl, p1), C099);
+    h2 a0 = __builtin_elementwise_min(op * __builtin_bit_cast(h2, e0), C099);
+    h2 a1 = __builtin_elementwise_min(op * __builtin_bit_cast(h2, e1), C099);
     if (!alive) {
         a0 = df_h2(0u);
         a1 = df_h2(0u);
@@ -384,9 +403,9 @@ __device__ __forceinline__ void df_blend_eye(DfEyeState& st, bool alive, h2 mean
 
 // max transmittance of a lane's 4 pixels >= fp16(1/255); T >= 0, so fp16 order is bit order
 __device__ __forceinline__ bool df_alive(const DfEyeState& st, uint32_t thrBits) {
-    const uint32_t a = df_u32(st.T[0]), b = df_u32(st.T[1]);
-    const uint32_t m = max(max(a & 0xFFFFu, a >> 16), max(b & 0xFFFFu, b >> 16));
-    return m >= thrBits;
+    const df_u16x2 m = __builtin_elementwise_max(__builtin_bit_cast(df_u16x2, st.T[0]),
+                                                 __builtin_bit_cast(df_u16x2, st.T[1]));
+    return max((uint32_t)m.x, (uint32_t)m.y) >= thrBits;
 }
 
 template <int NW>
@@ -451,12 +470,19 @@ __global__ __launch_bounds__(NW * 64) void k_df_blend(const uint2* __restrict__ 
                 }
                 const uint4 s0 = stg[2 * j], s1 = stg[2 * j + 1];
                 const h2 opr = df_h2(s1.z), gb = df_h2(s1.w);
-                // gMean.x >= -60000.0h: the eye's mean is real (uniform over the wave)
+                // gMean.x >= -60000.0h: the eye's mean is real (uniform over the wave).  An eye whose
+                // alphas are 0 on every live lane is an identity update for the wave: skipped.
                 const h2 mL = df_h2(s0.x), mR = df_h2(s0.w);
-                if ((float)mL.x >= -60000.0f)
-                    df_blend_eye(E[0], aL, mL, df_h2(s0.y), df_h2(s0.z), opr, gb, PX, PY, tbl);
-                if ((float)mR.x >= -60000.0f)
-                    df_blend_eye(E[1], aR, mR, df_h2(s1.x), df_h2(s1.y), opr, gb, PX, PY, tbl);
+                if ((float)mL.x >= -60000.0f) {
+                    h2 p0, p1;
+                    df_quadform(mL, df_h2(s0.y), df_h2(s0.z), PX, PY, p0, p1);
+                    if (__any(aL && !df_all_cut(p0, p1))) df_blend_eye(E[0], aL, p0, p1, opr, gb, tbl);
+                }
+                if ((float)mR.x >= -60000.0f) {
+                    h2 p0, p1;
+                    df_quadform(mR, df_h2(s1.x), df_h2(s1.y), PX, PY, p0, p1);
+                    if (__any(aR && !df_all_cut(p0, p1))) df_blend_eye(E[1], aR, p0, p1, opr, gb, tbl);
+                }
             }
             df_wave_sync();  // the stage is rewritten by the next batch
         }
@@ -479,6 +505,106 @@ __global__ __launch_bounds__(NW * 64) void k_df_blend(const uint2* __restrict__ 
                     store_color_px(fmt, (char*)(trow + (size_t)(bx + 1u) * bpp), (ur >> 16) | (ug & 0xFFFF0000u),
                                    (ub >> 16) | (ua & 0xFFFF0000u));
             }
+    }
+}
+
+// k_df_blend_eye: one wave per (tile, eye) unit.  An eye's updates only depend on its own
+// transmittance (the per-eye test maxTrans >= 1/255 of :1872 and :1915 is monotone, and the joint
+// break of :1866 fires only once both eyes' tests fail), so the two eyes of a tile are independent
+// walks: each stops when its own lanes are all done, and 2 x tiles units balance better than tiles.
+// Lane l stages record l of the 64-entry batch: the eye's mean and conic and the fp16 opacity and
+// colour (uint4 + uint), read back per entry as uniform-address broadcasts.
+constexpr uint32_t kDfEyeBatch = 64;
+template <int NW>
+__global__ __launch_bounds__(NW * 64) void k_df_blend_eye(const uint2* __restrict__ headers,
+                                                          const uint32_t* __restrict__ gids,
+                                                          const StereoTiledRenderData* __restrict__ rd,
+                                                          const uint16_t* __restrict__ expTable,
+                                                          uint32_t* __restrict__ queue, uint32_t tilesX,
+                                                          uint32_t tileCount, uint32_t W, uint32_t H,
+                                                          uint8_t* __restrict__ color, size_t pitch, int fmt) {
+    __shared__ __attribute__((aligned(16))) uint16_t tbl[65536];
+    __shared__ __attribute__((aligned(16))) uint4 stageA[NW][kDfEyeBatch];
+    __shared__ uint32_t stageB[NW][kDfEyeBatch];
+    __shared__ uint16_t div255[256];
+    {
+        const uint4* src = (const uint4*)expTable;
+        uint4* dst = (uint4*)tbl;
+        for (int i = threadIdx.x; i < 65536 * 2 / 16; i += NW * 64) dst[i] = src[i];
+        if (threadIdx.x < 256) div255[threadIdx.x] = f_to_hbits((float)threadIdx.x / 255.0f);  // getColor
+    }
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    const uint32_t thrBits = (uint32_t)f_to_hbits(1.0f / 255.0f);  // half(1.0h / 255.0h)
+    const uint32_t bpp = fmt == GSM_COLOR_FORMAT_RGBA16F ? 8u : (fmt == GSM_COLOR_FORMAT_RGBA32F ? 16u : 4u);
+    const h2 ONE = {(h1)1.0f, (h1)1.0f};
+    uint4* sA = stageA[wave];
+    uint32_t* sB = stageB[wave];
+    const uint32_t units = 2u * tileCount;
+    for (;;) {
+        uint32_t u = 0;
+        if (lane == 0) u = atomicAdd(queue, 1u);
+        u = (uint32_t)__shfl((int)u, 0, 64);
+        if (u >= units) break;
+        const uint32_t t = u >> 1, eye = u & 1u;
+        const uint2 hd = headers[t];
+        const uint32_t tileX = t % tilesX, tileY = t / tilesX;
+        const uint32_t bx = tileX * kDfTile + (lane & 7u) * 2u, by = tileY * kDfTile + (lane >> 3) * 2u;
+        const h2 PX = {(h1)(float)bx, (h1)(float)(bx + 1u)};
+        const h2 PY = {(h1)(float)by, (h1)(float)(by + 1u)};
+        DfEyeState E;
+        E.T[0] = E.T[1] = ONE;
+        E.Cr[0] = E.Cr[1] = E.Cg[0] = E.Cg[1] = E.Cb[0] = E.Cb[1] = df_h2(0u);
+        bool done = false;
+        for (uint32_t b0 = 0; b0 < hd.y && !done; b0 += kDfEyeBatch) {
+            const uint32_t n = min(kDfEyeBatch, hd.y - b0);
+            if (lane < n) {
+                const uint32_t g = gids[hd.x + b0 + lane];
+                const uint32_t* w = (const uint32_t*)(rd + g);
+                const uint32_t mean = w[3 * eye], cc = w[3 * eye + 1], cxy = w[3 * eye + 2] & 0xFFFFu;
+                const uint32_t c = w[6];  // colorR, G, B, opacity (bytes 24..27)
+                sA[lane] = make_uint4(mean, cc, cxy | ((uint32_t)div255[c >> 24] << 16),
+                                      (uint32_t)div255[c & 0xFFu] | ((uint32_t)div255[(c >> 8) & 0xFFu] << 16));
+                sB[lane] = (uint32_t)div255[(c >> 16) & 0xFFu];
+            }
+            df_wave_sync();
+            for (uint32_t j = 0; j < n; ++j) {
+                const bool alive = df_alive(E, thrBits);
+                if (!__any(alive)) {  // every lane of this eye is done
+                    done = true;
+                    break;
+                }
+                const uint4 ra = sA[j];
+                const h2 mean = df_h2(ra.x);
+                if ((float)mean.x >= -60000.0f) {  // gMean.x >= -60000.0h (uniform)
+                    h2 p0, p1;
+                    df_quadform(mean, df_h2(ra.y), df_h2(ra.z), PX, PY, p0, p1);
+                    if (__any(alive && !df_all_cut(p0, p1))) {
+                        const h2 opr = {df_h2(ra.z).y, df_h2(ra.w).x};
+                        const h2 gb = {df_h2(ra.w).y, df_h2(sB[j]).x};
+                        df_blend_eye(E, alive, p0, p1, opr, gb, tbl);
+                    }
+                }
+            }
+            df_wave_sync();  // the stage is rewritten by the next batch
+        }
+        // (C, 1 - T) of the eye's pixel (x, y) lands in target row H - 1 - y, column eye * W + x; a
+        // tile with an empty list is not an active tile and keeps the clear value (0, 0, 0, 1)
+        const uint32_t clearA = hd.y == 0 ? 0x3C003C00u : 0u;
+#pragma unroll
+        for (int row = 0; row < 2; ++row) {
+            const uint32_t y = by + (uint32_t)row;
+            if (y >= H) continue;
+            uint8_t* trow = color + (size_t)(H - 1u - y) * pitch + (size_t)eye * W * bpp;
+            const uint32_t ur = df_u32(E.Cr[row]), ug = df_u32(E.Cg[row]);
+            const uint32_t ub = df_u32(E.Cb[row]), ua = df_u32(ONE - E.T[row]) | clearA;
+            if (bx < W)
+                store_color_px(fmt, (char*)(trow + (size_t)bx * bpp), (ur & 0xFFFFu) | (ug << 16),
+                               (ub & 0xFFFFu) | (ua << 16));
+            if (bx + 1u < W)
+                store_color_px(fmt, (char*)(trow + (size_t)(bx + 1u) * bpp), (ur >> 16) | (ug & 0xFFFF0000u),
+                               (ub >> 16) | (ua & 0xFFFF0000u));
+        }
     }
 }
 
@@ -538,12 +664,19 @@ constexpr int kDfBlendWaves = 16;
 void df_launch_blend(const uint32_t* sortedGids, const DfArgs& a, const DfArena& A, void* color, size_t pitch,
                      int colorFormat, int numCUs, hipStream_t s) {
     uint32_t grid = (uint32_t)(numCUs > 0 ? numCUs : 256);
-    const uint32_t need = (a.tileCount + kDfBlendWaves - 1) / kDfBlendWaves;
+    const uint32_t need = (2u * a.tileCount + kDfBlendWaves - 1) / kDfBlendWaves;
     if (grid > need) grid = need;
     if (grid == 0) return;
-    hipLaunchKernelGGL(k_df_blend<kDfBlendWaves>, dim3(grid), dim3(kDfBlendWaves * 64), 0, s, A.headers, sortedGids,
-                       A.renderData, A.expTable, A.queue, a.tilesX, a.tileCount, (uint32_t)a.width,
-                       (uint32_t)a.height, (uint8_t*)color, pitch, colorFormat);
+    // GSM_DF_BLEND=pair: one wave per tile for both eyes (A/B); default: one wave per (tile, eye)
+    const char* v = getenv("GSM_DF_BLEND");
+    if (v && v[0] == 'p')
+        hipLaunchKernelGGL(k_df_blend<kDfBlendWaves>, dim3(grid), dim3(kDfBlendWaves * 64), 0, s, A.headers,
+                           sortedGids, A.renderData, A.expTable, A.queue, a.tilesX, a.tileCount, (uint32_t)a.width,
+                           (uint32_t)a.height, (uint8_t*)color, pitch, colorFormat);
+    else
+        hipLaunchKernelGGL(k_df_blend_eye<kDfBlendWaves>, dim3(grid), dim3(kDfBlendWaves * 64), 0, s, A.headers,
+                           sortedGids, A.renderData, A.expTable, A.queue, a.tilesX, a.tileCount, (uint32_t)a.width,
+                           (uint32_t)a.height, (uint8_t*)color, pitch, colorFormat);
 }
 
 }  // namespace gsm

@@ -401,6 +401,45 @@ __device__ __forceinline__ void df_blend_eye(DfEyeState& st, bool alive, h2 p0, 
     st.T[1] = st.T[1] * (ONE - a1);
 }
 
+// the same step from the staged words of k_df_blend_eye: opacity = hi(zw), r = lo(rg), g = hi(rg),
+// b = lo(bw), each used in place through op_sel
+__device__ __forceinline__ void df_blend_eye_w(DfEyeState& st, bool alive, h2 p0, h2 p1, uint32_t zw, uint32_t rg,
+                                               uint32_t bw, const uint16_t* tbl) {
+    const h2 ONE = {(h1)1.0f, (h1)1.0f};
+    const h1 c099 = (h1)0.99;
+    const h2 C099 = {c099, c099};
+    const uint32_t b0 = df_u32(p0), b1 = df_u32(p1);
+    df_u16x2 e0, e1;
+    e0.x = tbl[b0 & 0xFFFFu];
+    e0.y = tbl[b0 >> 16];
+    e1.x = tbl[b1 & 0xFFFFu];
+    e1.y = tbl[b1 >> 16];
+    const h2 op = df_hi(df_h2(zw));
+    h2 a0 = __builtin_elementwise_min(op * __builtin_bit_cast(h2, e0), C099);
+    h2 a1 = __builtin_elementwise_min(op * __builtin_bit_cast(h2, e1), C099);
+    if (!alive) {
+        a0 = df_h2(0u);
+        a1 = df_h2(0u);
+    }
+    const h2 w0 = a0 * st.T[0], w1 = a1 * st.T[1];
+    const h2 r = df_lo(df_h2(rg)), g = df_hi(df_h2(rg)), b = df_lo(df_h2(bw));
+    st.Cr[0] = st.Cr[0] + r * w0;
+    st.Cr[1] = st.Cr[1] + r * w1;
+    st.Cg[0] = st.Cg[0] + g * w0;
+    st.Cg[1] = st.Cg[1] + g * w1;
+    st.Cb[0] = st.Cb[0] + b * w0;
+    st.Cb[1] = st.Cb[1] + b * w1;
+    st.T[0] = st.T[0] * (ONE - a0);
+    st.T[1] = st.T[1] * (ONE - a1);
+}
+
+// gMean.x >= -60000.0h on the fp16 bits of a uniform word (integer compares, so the test stays on
+// the scalar unit): +0..+inf, or -0..-60000 (0xFB53); NaN and -inf fail
+__device__ __forceinline__ bool df_mean_valid(uint32_t meanWord) {
+    const uint32_t x = meanWord & 0xFFFFu;
+    return x <= 0x7C00u || (x >= 0x8000u && x <= 0xFB53u);
+}
+
 // max transmittance of a lane's 4 pixels >= fp16(1/255); T >= 0, so fp16 order is bit order
 __device__ __forceinline__ bool df_alive(const DfEyeState& st, uint32_t thrBits) {
     const df_u16x2 m = __builtin_elementwise_max(__builtin_bit_cast(df_u16x2, st.T[0]),
@@ -525,7 +564,7 @@ __global__ __launch_bounds__(NW * 64) void k_df_blend_eye(const uint2* __restric
                                                           uint8_t* __restrict__ color, size_t pitch, int fmt) {
     __shared__ __attribute__((aligned(16))) uint16_t tbl[65536];
     __shared__ __attribute__((aligned(16))) uint4 stageA[NW][kDfEyeBatch];
-    __shared__ uint32_t stageB[NW][kDfEyeBatch];
+    __shared__ __attribute__((aligned(16))) uint32_t stageB[NW][kDfEyeBatch];
     __shared__ uint16_t div255[256];
     {
         const uint4* src = (const uint4*)expTable;
@@ -566,25 +605,29 @@ __global__ __launch_bounds__(NW * 64) void k_df_blend_eye(const uint2* __restric
                 sA[lane] = make_uint4(mean, cc, cxy | ((uint32_t)div255[c >> 24] << 16),
                                       (uint32_t)div255[c & 0xFFu] | ((uint32_t)div255[(c >> 8) & 0xFFu] << 16));
                 sB[lane] = (uint32_t)div255[(c >> 16) & 0xFFu];
+            } else {  // padding entries: mean -inf, skipped by the mean test
+                sA[lane] = make_uint4(0xFC00FC00u, 0u, 0u, 0u);
             }
             df_wave_sync();
-            for (uint32_t j = 0; j < n; ++j) {
-                const bool alive = df_alive(E, thrBits);
-                if (!__any(alive)) {  // every lane of this eye is done
-                    done = true;
-                    break;
-                }
-                const uint4 ra = sA[j];
-                const h2 mean = df_h2(ra.x);
-                if ((float)mean.x >= -60000.0f) {  // gMean.x >= -60000.0h (uniform)
-                    h2 p0, p1;
-                    df_quadform(mean, df_h2(ra.y), df_h2(ra.z), PX, PY, p0, p1);
-                    if (__any(alive && !df_all_cut(p0, p1))) {
-                        const h2 opr = {df_h2(ra.z).y, df_h2(ra.w).x};
-                        const h2 gb = {df_h2(ra.w).y, df_h2(sB[j]).x};
-                        df_blend_eye(E, alive, p0, p1, opr, gb, tbl);
+            for (uint32_t j0 = 0; j0 < n; j0 += 4) {
+#pragma unroll
+                for (uint32_t jj = 0; jj < 4; ++jj) {
+                    const uint32_t j = j0 + jj;
+                    const bool alive = df_alive(E, thrBits);
+                    if (__builtin_amdgcn_ballot_w64(alive) == 0) {  // every lane of this eye is done
+                        done = true;
+                        break;
+                    }
+                    const uint4 ra = sA[j];
+                    const uint32_t mw = __builtin_amdgcn_readfirstlane(ra.x);
+                    if (df_mean_valid(mw)) {  // uniform
+                        h2 p0, p1;
+                        df_quadform(df_h2(mw), df_h2(ra.y), df_h2(ra.z), PX, PY, p0, p1);
+                        if (__builtin_amdgcn_ballot_w64(alive && !df_all_cut(p0, p1)) != 0)
+                            df_blend_eye_w(E, alive, p0, p1, ra.z, ra.w, sB[j], tbl);
                     }
                 }
+                if (done) break;
             }
             df_wave_sync();  // the stage is rewritten by the next batch
         }

@@ -898,6 +898,10 @@ void launch_unit_order(uint32_t numUnits, const DeviceArena& A, hipStream_t s) {
     hipLaunchKernelGGL(k_unit_order, dim3(1), dim3(1024), 0, s, A.unitCost, A.unitOrder, numUnits);
 }
 
+void launch_unit_order_costs(const uint16_t* cost, uint32_t* order, uint32_t numUnits, hipStream_t s) {
+    hipLaunchKernelGGL(k_unit_order, dim3(1), dim3(1024), 0, s, cost, order, numUnits);
+}
+
 void launch_blend(const uint32_t* sortedVals, const FrameGeometry& g, const DeviceArena& A, void* color,
                   size_t colorPitch, void* depth, size_t depthPitch, int numCUs, bool costOrder, int colorFormat,
                   hipStream_t s) {

@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <vector>
@@ -46,6 +47,9 @@ class DepthFirstRenderer {
     std::vector<void*> allocations_;
     // last frame
     uint32_t lastCount_ = 0, lastTilesX_ = 0, lastTilesY_ = 0;
+    uint64_t schedKey_ = ~0ull;  // geometry the unit costs belong to
+    hipStream_t side_ = nullptr;  // blend-schedule stream
+    hipEvent_t evFrame_ = nullptr, evOrder_ = nullptr;
     const uint32_t* depthOrder_ = nullptr;
     const uint32_t* instTiles_ = nullptr;
     const uint32_t* instGids_ = nullptr;
@@ -66,6 +70,11 @@ void DepthFirstRenderer::release() {
     for (auto& e : events_)
         if (e) hipEventDestroy(e);
     events_.clear();
+    if (evFrame_) hipEventDestroy(evFrame_);
+    if (evOrder_) hipEventDestroy(evOrder_);
+    if (side_) hipStreamDestroy(side_);
+    evFrame_ = evOrder_ = nullptr;
+    side_ = nullptr;
 }
 
 gsm_status DepthFirstRenderer::alloc(void** p, size_t bytes) {
@@ -141,6 +150,8 @@ gsm_status DepthFirstRenderer::create(const gsm_renderer_config& cfg, int hipDev
     GSM_DF_ALLOC(A.headers, (size_t)r->maxTiles_ * sizeof(uint2));
     GSM_DF_ALLOC(A.queue, 4);
     GSM_DF_ALLOC(A.expTable, 65536 * 2);
+    GSM_DF_ALLOC(A.unitCost, (size_t)r->maxTiles_ * 2 * sizeof(uint16_t));
+    GSM_DF_ALLOC(A.unitOrder, (size_t)r->maxTiles_ * 2 * sizeof(uint32_t));
 #undef GSM_DF_ALLOC
     if (st != GSM_OK) {
         delete r;
@@ -222,6 +233,29 @@ gsm_status DepthFirstRenderer::renderStereoSbs(hipStream_t s, const gsm_gaussian
     const bool half = config_.precision == GSM_PRECISION_FLOAT16;
     const uint32_t nb = (a.count + kDfBlock - 1) / kDfBlock;
 
+    // The blend schedule's ordering kernel only needs the previous frame's walk lengths, so it
+    // runs on a side stream beside this frame's projection and sorts (joined before the blend).
+    const char* sv = getenv("GSM_DF_SCHED");
+    const bool costOrder = !(sv && sv[0] == '0');
+    if (costOrder && !side_) {
+        if (hipStreamCreateWithFlags(&side_, hipStreamNonBlocking) != hipSuccess ||
+            hipEventCreateWithFlags(&evFrame_, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&evOrder_, hipEventDisableTiming) != hipSuccess)
+            return GSM_ERR_ENCODER_CREATION_FAILED;
+    }
+    {
+        const uint64_t key = ((uint64_t)a.tilesX << 32) | a.tilesY;
+        if (key != schedKey_) {  // costs of another geometry: start from index order
+            hipMemsetAsync(A_.unitCost, 0, (size_t)a.tileCount * 2 * sizeof(uint16_t), s);
+            schedKey_ = key;
+        }
+    }
+    if (costOrder) {
+        hipEventRecord(evFrame_, s);  // after the previous frame's blend wrote the costs
+        hipStreamWaitEvent(side_, evFrame_, 0);
+        launch_unit_order_costs(A_.unitCost, A_.unitOrder, 2 * a.tileCount, side_);
+        hipEventRecord(evOrder_, side_);
+    }
     const bool prof = (profiling_ & 1) != 0;                   // every stage bracketed
     const bool blendOnly = !prof && (profiling_ & 8) != 0;      // only the blend's pair of events
     hipEvent_t* ev = (prof || blendOnly) ? frameEvents(profFrames_) : nullptr;
@@ -244,8 +278,12 @@ gsm_status DepthFirstRenderer::renderStereoSbs(hipStream_t s, const gsm_gaussian
     const int ic = radix_sort_bits(A_.ikeys, A_.ivals, &A_.instHdr->totalAssignments, maxInstances_, 0, tileBits,
                                    A_.radixHist, A_.radixBinTotals, s);
     df_launch_ranges(A_.ikeys[ic], a, A_, s);
+    // Blend schedule: (tile, eye) units handed out longest first by the walk lengths the previous
+    // frame of the same geometry measured (the image does not depend on the order, only the load
+    // balance does).  GSM_DF_SCHED=0: index order.
+    if (costOrder) hipStreamWaitEvent(s, evOrder_, 0);
     if (prof || blendOnly) hipEventRecord(ev[4], s);
-    df_launch_blend(A_.ivals[ic], a, A_, color, pitch, fmt, numCUs_, s);
+    df_launch_blend(A_.ivals[ic], a, A_, color, pitch, fmt, numCUs_, costOrder, s);
     if (prof || blendOnly) {
         hipEventRecord(ev[5], s);
         profFrames_++;

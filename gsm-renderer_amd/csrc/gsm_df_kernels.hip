@@ -561,7 +561,9 @@ __global__ __launch_bounds__(NW * 64) void k_df_blend_eye(const uint2* __restric
                                                           const uint16_t* __restrict__ expTable,
                                                           uint32_t* __restrict__ queue, uint32_t tilesX,
                                                           uint32_t tileCount, uint32_t W, uint32_t H,
-                                                          uint8_t* __restrict__ color, size_t pitch, int fmt) {
+                                                          uint8_t* __restrict__ color, size_t pitch, int fmt,
+                                                          const uint32_t* __restrict__ order,
+                                                          uint16_t* __restrict__ unitCost) {
     __shared__ __attribute__((aligned(16))) uint16_t tbl[65536];
     __shared__ __attribute__((aligned(16))) uint4 stageA[NW][kDfEyeBatch];
     __shared__ __attribute__((aligned(16))) uint32_t stageB[NW][kDfEyeBatch];
@@ -581,10 +583,11 @@ __global__ __launch_bounds__(NW * 64) void k_df_blend_eye(const uint2* __restric
     uint32_t* sB = stageB[wave];
     const uint32_t units = 2u * tileCount;
     for (;;) {
-        uint32_t u = 0;
-        if (lane == 0) u = atomicAdd(queue, 1u);
-        u = (uint32_t)__shfl((int)u, 0, 64);
-        if (u >= units) break;
+        uint32_t qi = 0;
+        if (lane == 0) qi = atomicAdd(queue, 1u);
+        qi = __builtin_amdgcn_readfirstlane(qi);
+        if (qi >= units) break;
+        const uint32_t u = order ? __builtin_amdgcn_readfirstlane(order[qi]) : qi;
         const uint32_t t = u >> 1, eye = u & 1u;
         const uint2 hd = headers[t];
         const uint32_t tileX = t % tilesX, tileY = t / tilesX;
@@ -595,6 +598,7 @@ __global__ __launch_bounds__(NW * 64) void k_df_blend_eye(const uint2* __restric
         E.T[0] = E.T[1] = ONE;
         E.Cr[0] = E.Cr[1] = E.Cg[0] = E.Cg[1] = E.Cb[0] = E.Cb[1] = df_h2(0u);
         bool done = false;
+        uint32_t walked = hd.y;  // entries this unit walked (its cost for the next frame's order)
         for (uint32_t b0 = 0; b0 < hd.y && !done; b0 += kDfEyeBatch) {
             const uint32_t n = min(kDfEyeBatch, hd.y - b0);
             if (lane < n) {
@@ -627,10 +631,14 @@ __global__ __launch_bounds__(NW * 64) void k_df_blend_eye(const uint2* __restric
                             df_blend_eye_w(E, alive, p0, p1, ra.z, ra.w, sB[j], tbl);
                     }
                 }
-                if (done) break;
+                if (done) {
+                    walked = b0 + j0;  // to the group of 4 (a cost estimate for the schedule)
+                    break;
+                }
             }
             df_wave_sync();  // the stage is rewritten by the next batch
         }
+        if (unitCost && lane == 0) unitCost[u] = (uint16_t)min(walked, 65535u);
         // (C, 1 - T) of the eye's pixel (x, y) lands in target row H - 1 - y, column eye * W + x; a
         // tile with an empty list is not an active tile and keeps the clear value (0, 0, 0, 1)
         const uint32_t clearA = hd.y == 0 ? 0x3C003C00u : 0u;
@@ -705,7 +713,7 @@ void df_launch_ranges(const uint32_t* sortedTiles, const DfArgs& a, const DfAren
 
 constexpr int kDfBlendWaves = 16;
 void df_launch_blend(const uint32_t* sortedGids, const DfArgs& a, const DfArena& A, void* color, size_t pitch,
-                     int colorFormat, int numCUs, hipStream_t s) {
+                     int colorFormat, int numCUs, bool costOrder, hipStream_t s) {
     uint32_t grid = (uint32_t)(numCUs > 0 ? numCUs : 256);
     const uint32_t need = (2u * a.tileCount + kDfBlendWaves - 1) / kDfBlendWaves;
     if (grid > need) grid = need;
@@ -719,7 +727,8 @@ void df_launch_blend(const uint32_t* sortedGids, const DfArgs& a, const DfArena&
     else
         hipLaunchKernelGGL(k_df_blend_eye<kDfBlendWaves>, dim3(grid), dim3(kDfBlendWaves * 64), 0, s, A.headers,
                            sortedGids, A.renderData, A.expTable, A.queue, a.tilesX, a.tileCount, (uint32_t)a.width,
-                           (uint32_t)a.height, (uint8_t*)color, pitch, colorFormat);
+                           (uint32_t)a.height, (uint8_t*)color, pitch, colorFormat,
+                           costOrder ? (const uint32_t*)A.unitOrder : nullptr, A.unitCost);
 }
 
 }  // namespace gsm

@@ -104,6 +104,8 @@ void launch_blend(const uint32_t* sortedVals, const FrameGeometry& geo, const De
 // orders the blend units by the walk lengths the previous frame measured (longest first), so
 // the dynamic queue hands out long units before short ones
 void launch_unit_order(uint32_t numUnits, const DeviceArena& A, hipStream_t stream);
+// the same ordering for any cost array (the DepthFirst blend's (tile, eye) units)
+void launch_unit_order_costs(const uint16_t* cost, uint32_t* order, uint32_t numUnits, hipStream_t stream);
 // blend kernel shape: pixel pairs per lane (0 = quadrant kernel) and blend units per tile
 int blend_pairs_per_lane(uint32_t numTiles, int numCUs);
 uint32_t blend_units_per_tile(uint32_t numTiles, int numCUs);

@@ -563,7 +563,7 @@ __global__ __launch_bounds__(NW * 64) void k_df_blend_eye(const uint2* __restric
                                                           uint32_t tileCount, uint32_t W, uint32_t H,
                                                           uint8_t* __restrict__ color, size_t pitch, int fmt,
                                                           const uint32_t* __restrict__ order,
-                                                          uint16_t* __restrict__ unitCost) {
+                                                          uint16_t* __restrict__ unitCost, int flags) {
     __shared__ __attribute__((aligned(16))) uint16_t tbl[65536];
     __shared__ __attribute__((aligned(16))) uint4 stageA[NW][kDfEyeBatch];
     __shared__ __attribute__((aligned(16))) uint32_t stageB[NW][kDfEyeBatch];
@@ -582,12 +582,20 @@ __global__ __launch_bounds__(NW * 64) void k_df_blend_eye(const uint2* __restric
     uint4* sA = stageA[wave];
     uint32_t* sB = stageB[wave];
     const uint32_t units = 2u * tileCount;
-    for (;;) {
-        uint32_t qi = 0;
-        if (lane == 0) qi = atomicAdd(queue, 1u);
-        qi = __builtin_amdgcn_readfirstlane(qi);
+    // First unit static, then the queue.  With the schedule on (flags bit 1) one wave per SIMD
+    // takes one of the gridDim.x * 4 longest units first and runs it at the top priority, so each
+    // SIMD pairs its longest walk with shorter ones (the makespan is the longest walk's); with
+    // flags bit 0 a walk's priority rises with its age.
+    constexpr uint32_t NTOP = 4;
+    const bool split = (flags & 2) != 0 && order != nullptr, agePrio = (flags & 1) != 0;
+    uint32_t qi = !split ? blockIdx.x * NW + wave
+                         : (wave < NTOP ? blockIdx.x * NTOP + wave
+                                        : gridDim.x * NTOP + blockIdx.x * (NW - NTOP) + (wave - NTOP));
+    bool topPrio = split && wave < NTOP;
+    for (;; topPrio = false) {
         if (qi >= units) break;
-        const uint32_t u = order ? __builtin_amdgcn_readfirstlane(order[qi]) : qi;
+        uint32_t u = order ? __builtin_amdgcn_readfirstlane(order[qi]) : qi;
+        if (u >= units) u = qi;  // a schedule is a permutation of [0, units); never trust it further
         const uint32_t t = u >> 1, eye = u & 1u;
         const uint2 hd = headers[t];
         const uint32_t tileX = t % tilesX, tileY = t / tilesX;
@@ -601,6 +609,13 @@ __global__ __launch_bounds__(NW * 64) void k_df_blend_eye(const uint2* __restric
         uint32_t walked = hd.y;  // entries this unit walked (its cost for the next frame's order)
         for (uint32_t b0 = 0; b0 < hd.y && !done; b0 += kDfEyeBatch) {
             const uint32_t n = min(kDfEyeBatch, hd.y - b0);
+            if (topPrio) {
+                if (b0 == 0) __builtin_amdgcn_s_setprio(3);
+            } else if (agePrio) {
+                if (b0 == 0) __builtin_amdgcn_s_setprio(1);
+                else if (b0 == 128u) __builtin_amdgcn_s_setprio(2);
+                else if (b0 == 320u && !split) __builtin_amdgcn_s_setprio(3);
+            }
             if (lane < n) {
                 const uint32_t g = gids[hd.x + b0 + lane];
                 const uint32_t* w = (const uint32_t*)(rd + g);
@@ -638,6 +653,10 @@ __global__ __launch_bounds__(NW * 64) void k_df_blend_eye(const uint2* __restric
             }
             df_wave_sync();  // the stage is rewritten by the next batch
         }
+        if (agePrio || topPrio) __builtin_amdgcn_s_setprio(0);
+        uint32_t nq = 0;
+        if (lane == 0) nq = atomicAdd(queue, 1u);
+        qi = __builtin_amdgcn_readfirstlane(nq) + gridDim.x * NW;
         if (unitCost && lane == 0) unitCost[u] = (uint16_t)min(walked, 65535u);
         // (C, 1 - T) of the eye's pixel (x, y) lands in target row H - 1 - y, column eye * W + x; a
         // tile with an empty list is not an active tile and keeps the clear value (0, 0, 0, 1)
@@ -718,7 +737,11 @@ void df_launch_blend(const uint32_t* sortedGids, const DfArgs& a, const DfArena&
     const uint32_t need = (2u * a.tileCount + kDfBlendWaves - 1) / kDfBlendWaves;
     if (grid > need) grid = need;
     if (grid == 0) return;
-    // GSM_DF_BLEND=pair: one wave per tile for both eyes (A/B); default: one wave per (tile, eye)
+    // GSM_DF_BLEND=pair: one wave per tile for both eyes (A/B); default: one wave per (tile, eye).
+    // GSM_DF_PRIO=0 / GSM_DF_SPLIT=0 switch off the age priority / top-priority long first units.
+    const char* pv = getenv("GSM_DF_PRIO");
+    const char* sp = getenv("GSM_DF_SPLIT");
+    const int flags = ((pv && pv[0] == '0') ? 0 : 1) | ((sp && sp[0] == '0') ? 0 : 2);
     const char* v = getenv("GSM_DF_BLEND");
     if (v && v[0] == 'p')
         hipLaunchKernelGGL(k_df_blend<kDfBlendWaves>, dim3(grid), dim3(kDfBlendWaves * 64), 0, s, A.headers,
@@ -728,7 +751,7 @@ void df_launch_blend(const uint32_t* sortedGids, const DfArgs& a, const DfArena&
         hipLaunchKernelGGL(k_df_blend_eye<kDfBlendWaves>, dim3(grid), dim3(kDfBlendWaves * 64), 0, s, A.headers,
                            sortedGids, A.renderData, A.expTable, A.queue, a.tilesX, a.tileCount, (uint32_t)a.width,
                            (uint32_t)a.height, (uint8_t*)color, pitch, colorFormat,
-                           costOrder ? (const uint32_t*)A.unitOrder : nullptr, A.unitCost);
+                           costOrder ? (const uint32_t*)A.unitOrder : nullptr, A.unitCost, flags);
 }
 
 }  // namespace gsm

@@ -308,6 +308,10 @@ def run_depthfirst(args, c, world_np, harm_np, world, harm, dev):
     torch.cuda.synchronize()
     stage_ms = renderer.stage_times_ms()
     stage_ms["blend_timed_region"] = blend_ms_timed
+    renderer.set_profiling(stage_events=False, blend_stats=True)  # one more frame: walk statistics
+    step()
+    torch.cuda.synchronize()
+    walk = [int(x) for x in renderer.copy_buffer(gsm_amd.DepthFirstBuffer.BLEND_STATS)]
     cnt = renderer.counters()
     ms_per_step = elapsed / args.steps * 1e3
     A, T, P = cnt["total_instances"], cnt["tile_count"], 2 * W * H
@@ -351,6 +355,7 @@ def run_depthfirst(args, c, world_np, harm_np, world, harm, dev):
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
                      "algorithmic_bytes": b_blend, "avg_launch_ms": blend_ms_timed,
                      "note": "blend is VALU/LDS-bound (fp16 math per pixel, both eyes per entry)"},
+        "blend_walk": {"walked": walk[0], "with_mean": walk[1], "blended": walk[2], "list_entries": walk[3]},
         "cpu_baseline": cpu, "stages_ms": stage_ms, "blend_gb_per_s": achieved, "parity_vs_oracle": parity,
     }
     print(json.dumps(out))

@@ -49,6 +49,7 @@ class DepthFirstRenderer {
     uint32_t lastCount_ = 0, lastTilesX_ = 0, lastTilesY_ = 0;
     uint64_t schedKey_ = ~0ull;  // geometry the unit costs belong to
     hipStream_t side_ = nullptr;  // blend-schedule stream
+    unsigned long long* statsBuf_ = nullptr;  // blend walk statistics (profiling bit 1)
     hipEvent_t evFrame_ = nullptr, evOrder_ = nullptr;
     const uint32_t* depthOrder_ = nullptr;
     const uint32_t* instTiles_ = nullptr;
@@ -282,6 +283,8 @@ gsm_status DepthFirstRenderer::renderStereoSbs(hipStream_t s, const gsm_gaussian
     // frame of the same geometry measured (the image does not depend on the order, only the load
     // balance does).  GSM_DF_SCHED=0: index order.
     if (costOrder) hipStreamWaitEvent(s, evOrder_, 0);
+    A_.blendStats = (profiling_ & 2) ? statsBuf_ : nullptr;
+    if (A_.blendStats) hipMemsetAsync(statsBuf_, 0, 4 * sizeof(unsigned long long), s);
     if (prof || blendOnly) hipEventRecord(ev[4], s);
     df_launch_blend(A_.ivals[ic], a, A_, color, pitch, fmt, numCUs_, costOrder, s);
     if (prof || blendOnly) {
@@ -331,6 +334,7 @@ gsm_status DepthFirstRenderer::debugCopy(int which, void* dst, size_t bytes, siz
         case GSM_DF_BUF_INSTANCE_TILES: src = instTiles_; full = (size_t)c.total_instances * 4; break;
         case GSM_DF_BUF_INSTANCE_GAUSSIANS: src = instGids_; full = (size_t)c.total_instances * 4; break;
         case GSM_DF_BUF_HEADERS: src = A_.headers; full = (size_t)c.tile_count * 8; break;
+        case GSM_DF_BUF_BLEND_STATS: src = (profiling_ & 2) ? statsBuf_ : nullptr; full = 32; break;
         default: return GSM_ERR_INVALID_ARGUMENT;
     }
     if (needed) *needed = full;
@@ -352,11 +356,19 @@ gsm_status DepthFirstRenderer::debugCopy(int which, void* dst, size_t bytes, siz
     }
     if (!src) return GSM_ERR_RENDER_FAILED;
     if (hipMemcpy(dst, src, cpy, hipMemcpyDeviceToHost) != hipSuccess) return GSM_ERR_RENDER_FAILED;
+    if (which == GSM_DF_BUF_INSTANCE_GAUSSIANS) {  // drop the blend's skip flags (kDfSkipShift)
+        uint32_t* v = (uint32_t*)dst;
+        for (size_t i = 0; i < cpy / 4; ++i) v[i] &= kDfGidMask;
+    }
     return GSM_OK;
 }
 
 gsm_status DepthFirstRenderer::setProfiling(int flags) {
     hipSetDevice(device_);
+    if ((flags & 2) && !statsBuf_) {
+        gsm_status st = alloc((void**)&statsBuf_, 4 * sizeof(unsigned long long));
+        if (st != GSM_OK) return st;
+    }
     if ((flags & 9) && events_.empty()) {  // bit 0: every stage, bit 3: the blend only
         events_.assign((size_t)kRing * (GSM_DF_STAGE_COUNT + 1), nullptr);
         for (auto& e : events_)

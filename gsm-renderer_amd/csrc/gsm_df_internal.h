@@ -54,9 +54,15 @@ struct DfArena {
     uint16_t* expTable = nullptr;                 // [65536] stereo alpha table (r^2 cutoff folded)
     uint16_t* unitCost = nullptr;                 // [2 * maxTiles] entries each (tile, eye) unit walked
     uint32_t* unitOrder = nullptr;                // [2 * maxTiles] units, longest last-frame walk first
+    unsigned long long* blendStats = nullptr;     // [4] profiling bit 1: entries walked / with a real
+                                                  // mean / blended, list entries (null: not counted)
 };
 
 constexpr int kDfBlock = 256;
+// instance values: gaussian id in bits 0-29 (max_gaussians <= 30M < 2^30); bit 30 + e set when eye e
+// provably adds nothing to the instance's tile (k_df_instances, df_eye_misses_tile)
+constexpr uint32_t kDfSkipShift = 30;
+constexpr uint32_t kDfGidMask = (1u << kDfSkipShift) - 1u;
 
 // depthFirstStereoProjectCullKernel (DepthFirstShaders.metal:341-499) + per-block visible counts
 void df_launch_project(bool halfInput, uint32_t shDegree, const void* world, const void* harmonics,

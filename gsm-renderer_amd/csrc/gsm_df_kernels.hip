@@ -260,11 +260,57 @@ __global__ __launch_bounds__(kDfBlock) void k_df_icount(const TileAssignmentHead
     if (threadIdx.x == 0) sums[blockIdx.x] = s;
 }
 
+// Instance flags (bits 30, 31 of the instance's gaussian id, gsm_df_internal.h kDfSkipShift): eye e
+// provably contributes nothing to tile (x0, y0).  The blend evaluates, per pixel, the fp16 form
+// p = fl(fl(fl(fl(dx*dx)*cxx) + fl(fl(dy*dy)*cyy)) + fl(fl(dx*dy)*cxy2)) with dx = fl(px - mx), and an
+// eye's alpha is 0 exactly when p is in (9, +inf] (stereo_exp_table_entry).  With Q the same form in
+// real arithmetic on the same fp16 inputs, a = cxx dx^2, b = cyy dy^2 and rho = |cxy2| / (2 sqrt(cxx cyy)):
+// every product and sum above rounds once with relative error <= u = 2^-11 while nothing overflows, so
+// p >= (1 - u) (Q - 9.02 u (a + b)), and |c| <= rho (a + b), Q >= (1 - rho)(a + b) give
+// p >= (1 - u) Q (1 - 9.02 u / (1 - rho)).  The flag is set only when that bound exceeds 9 for the
+// minimum of Q over the tile's pixel rectangle (continuous, so it bounds every pixel), with
+// rho <= 15/16, |dx|, |dy| <= 200 and a + b <= 16000 over the tile (no fp16 overflow, no NaN), pixel
+// coordinates below 2048 (exact in fp16) and finite positive cxx, cyy.  Such an entry is an identity
+// step of the blend for that eye, which then skips it without reading its record.
+__device__ __forceinline__ bool df_eye_misses_tile(uint32_t meanW, uint32_t ccW, uint32_t cxyW, int x0, int y0) {
+    const float mxf = hbits_to_f((uint16_t)(meanW & 0xFFFFu)), myf = hbits_to_f((uint16_t)(meanW >> 16));
+    if (!(mxf >= -60000.0f)) return true;  // the blend's mean test skips this eye anyway
+    if (x0 + 15 >= 2048 || y0 + 15 >= 2048) return false;
+    const double cxx = (double)hbits_to_f((uint16_t)(ccW & 0xFFFFu)), cyy = (double)hbits_to_f((uint16_t)(ccW >> 16));
+    const double cxy = (double)hbits_to_f((uint16_t)(cxyW & 0xFFFFu));
+    if (!(cxx > 0.0 && cyy > 0.0 && cxx < 65504.0 && cyy < 65504.0 && __builtin_fabs(cxy) < 65504.0)) return false;
+    if (!(__builtin_fabs((double)myf) < 65504.0)) return false;
+    const double dx0 = (double)x0 - (double)mxf, dx1 = dx0 + 15.0;
+    const double dy0 = (double)y0 - (double)myf, dy1 = dy0 + 15.0;
+    if (!(__builtin_fabs(dx0) <= 200.0 && __builtin_fabs(dx1) <= 200.0 && __builtin_fabs(dy0) <= 200.0 &&
+          __builtin_fabs(dy1) <= 200.0))
+        return false;
+    if (dx0 <= 0.0 && dx1 >= 0.0 && dy0 <= 0.0 && dy1 >= 0.0) return false;  // the mean is inside: Q min = 0
+    const double rho = __builtin_fabs(cxy) / (2.0 * __builtin_sqrt(cxx * cyy));
+    if (!(rho <= 15.0 / 16.0)) return false;
+    const double ax = __builtin_fmax(dx0 * dx0, dx1 * dx1), ay = __builtin_fmax(dy0 * dy0, dy1 * dy1);
+    if (!(cxx * ax + cyy * ay <= 16000.0)) return false;
+    // min of Q over the rectangle: on its boundary (Q is convex with its minimum at the mean, outside)
+    auto q = [&](double dx, double dy) { return cxx * dx * dx + cyy * dy * dy + cxy * dx * dy; };
+    auto along_y = [&](double X) {  // edge dx = X: minimise over dy in [dy0, dy1]
+        const double t = __builtin_fmin(__builtin_fmax(-cxy * X / (2.0 * cyy), dy0), dy1);
+        return q(X, t);
+    };
+    auto along_x = [&](double Y) {
+        const double t = __builtin_fmin(__builtin_fmax(-cxy * Y / (2.0 * cxx), dx0), dx1);
+        return q(t, Y);
+    };
+    const double qmin = __builtin_fmin(__builtin_fmin(along_y(dx0), along_y(dx1)), __builtin_fmin(along_x(dy0), along_x(dy1)));
+    const double u = 1.0 / 2048.0;
+    return qmin * (1.0 - u) * (1.0 - 10.0 * u / (1.0 - rho)) > 9.0 + 1e-3;
+}
+
 __global__ __launch_bounds__(kDfBlock) void k_df_instances(const TileAssignmentHeader* __restrict__ visHdr,
                                                            const uint32_t* __restrict__ order,
                                                            const uint32_t* __restrict__ touched,
                                                            const short4* __restrict__ bounds,
                                                            const uint32_t* __restrict__ blockOffsets,
+                                                           const StereoTiledRenderData* __restrict__ rd,
                                                            uint32_t maxInstances, uint32_t tilesX,
                                                            uint32_t* __restrict__ tiles, uint32_t* __restrict__ gids) {
     __shared__ uint32_t lds[kDfBlock / 64];
@@ -277,11 +323,15 @@ __global__ __launch_bounds__(kDfBlock) void k_df_instances(const TileAssignmentH
     if (c == 0) return;
     uint64_t wp = (uint64_t)blockOffsets[blockIdx.x] + off;
     const short4 r = bounds[g];
+    const uint4 w0 = ((const uint4*)(rd + g))[0], w1 = ((const uint4*)(rd + g))[1];
     for (int ty = r.z; ty <= r.w; ++ty)
         for (int tx = r.x; tx <= r.y; ++tx) {
             if (wp >= maxInstances) return;
             tiles[wp] = (uint32_t)(ty * (int)tilesX + tx) & 0xFFFFu;  // ushort tile id
-            gids[wp] = g;
+            const int x0 = tx * (int)kDfTile, y0 = ty * (int)kDfTile;
+            const uint32_t fl = (df_eye_misses_tile(w0.x, w0.y, w0.z, x0, y0) ? 1u : 0u) |
+                                (df_eye_misses_tile(w0.w, w1.x, w1.y, x0, y0) ? 2u : 0u);
+            gids[wp] = g | (fl << kDfSkipShift);
             wp++;
         }
 }
@@ -491,7 +541,7 @@ __global__ __launch_bounds__(NW * 64) void k_df_blend(const uint2* __restrict__ 
             const uint32_t n = min(kDfBatch, hd.y - b0);
             const uint32_t rec = lane >> 1;
             if (rec < n) {
-                const uint32_t g = gids[hd.x + b0 + rec];
+                const uint32_t g = gids[hd.x + b0 + rec] & kDfGidMask;
                 uint4 v = ((const uint4*)(rd + g))[lane & 1u];
                 if (lane & 1u) {  // colorR, G, B, opacity (bytes 24..27) -> fp16 {op, r}, {g, b}
                     const uint32_t c = v.z;
@@ -554,7 +604,7 @@ __global__ __launch_bounds__(NW * 64) void k_df_blend(const uint2* __restrict__ 
 // Lane l stages record l of the 64-entry batch: the eye's mean and conic and the fp16 opacity and
 // colour (uint4 + uint), read back per entry as uniform-address broadcasts.
 constexpr uint32_t kDfEyeBatch = 64;
-template <int NW>
+template <int NW, bool STATS>
 __global__ __launch_bounds__(NW * 64) void k_df_blend_eye(const uint2* __restrict__ headers,
                                                           const uint32_t* __restrict__ gids,
                                                           const StereoTiledRenderData* __restrict__ rd,
@@ -563,7 +613,8 @@ __global__ __launch_bounds__(NW * 64) void k_df_blend_eye(const uint2* __restric
                                                           uint32_t tileCount, uint32_t W, uint32_t H,
                                                           uint8_t* __restrict__ color, size_t pitch, int fmt,
                                                           const uint32_t* __restrict__ order,
-                                                          uint16_t* __restrict__ unitCost, int flags) {
+                                                          uint16_t* __restrict__ unitCost, int flags,
+                                                          unsigned long long* __restrict__ stats) {
     __shared__ __attribute__((aligned(16))) uint16_t tbl[65536];
     __shared__ __attribute__((aligned(16))) uint4 stageA[NW][kDfEyeBatch];
     __shared__ __attribute__((aligned(16))) uint32_t stageB[NW][kDfEyeBatch];
@@ -607,6 +658,7 @@ __global__ __launch_bounds__(NW * 64) void k_df_blend_eye(const uint2* __restric
         E.Cr[0] = E.Cr[1] = E.Cg[0] = E.Cg[1] = E.Cb[0] = E.Cb[1] = df_h2(0u);
         bool done = false;
         uint32_t walked = hd.y;  // entries this unit walked (its cost for the next frame's order)
+        uint32_t nValid = 0, nBlend = 0;  // STATS: entries with a real mean / with a blend step
         for (uint32_t b0 = 0; b0 < hd.y && !done; b0 += kDfEyeBatch) {
             const uint32_t n = min(kDfEyeBatch, hd.y - b0);
             if (topPrio) {
@@ -616,15 +668,16 @@ __global__ __launch_bounds__(NW * 64) void k_df_blend_eye(const uint2* __restric
                 else if (b0 == 128u) __builtin_amdgcn_s_setprio(2);
                 else if (b0 == 320u && !split) __builtin_amdgcn_s_setprio(3);
             }
-            if (lane < n) {
-                const uint32_t g = gids[hd.x + b0 + lane];
+            const uint32_t gw = lane < n ? gids[hd.x + b0 + lane] : 0u;
+            if (lane < n && !((gw >> (kDfSkipShift + eye)) & 1u)) {
+                const uint32_t g = gw & kDfGidMask;
                 const uint32_t* w = (const uint32_t*)(rd + g);
                 const uint32_t mean = w[3 * eye], cc = w[3 * eye + 1], cxy = w[3 * eye + 2] & 0xFFFFu;
                 const uint32_t c = w[6];  // colorR, G, B, opacity (bytes 24..27)
                 sA[lane] = make_uint4(mean, cc, cxy | ((uint32_t)div255[c >> 24] << 16),
                                       (uint32_t)div255[c & 0xFFu] | ((uint32_t)div255[(c >> 8) & 0xFFu] << 16));
                 sB[lane] = (uint32_t)div255[(c >> 16) & 0xFFu];
-            } else {  // padding entries: mean -inf, skipped by the mean test
+            } else {  // padding and flagged entries: mean -inf, skipped by the mean test
                 sA[lane] = make_uint4(0xFC00FC00u, 0u, 0u, 0u);
             }
             df_wave_sync();
@@ -642,8 +695,11 @@ __global__ __launch_bounds__(NW * 64) void k_df_blend_eye(const uint2* __restric
                     if (df_mean_valid(mw)) {  // uniform
                         h2 p0, p1;
                         df_quadform(df_h2(mw), df_h2(ra.y), df_h2(ra.z), PX, PY, p0, p1);
-                        if (__builtin_amdgcn_ballot_w64(alive && !df_all_cut(p0, p1)) != 0)
+                        if (STATS) nValid++;
+                        if (__builtin_amdgcn_ballot_w64(alive && !df_all_cut(p0, p1)) != 0) {
                             df_blend_eye_w(E, alive, p0, p1, ra.z, ra.w, sB[j], tbl);
+                            if (STATS) nBlend++;
+                        }
                     }
                 }
                 if (done) {
@@ -658,6 +714,12 @@ __global__ __launch_bounds__(NW * 64) void k_df_blend_eye(const uint2* __restric
         if (lane == 0) nq = atomicAdd(queue, 1u);
         qi = __builtin_amdgcn_readfirstlane(nq) + gridDim.x * NW;
         if (unitCost && lane == 0) unitCost[u] = (uint16_t)min(walked, 65535u);
+        if (STATS && lane == 0) {
+            atomicAdd(&stats[0], (unsigned long long)walked);
+            atomicAdd(&stats[1], (unsigned long long)nValid);
+            atomicAdd(&stats[2], (unsigned long long)nBlend);
+            atomicAdd(&stats[3], (unsigned long long)hd.y);
+        }
         // (C, 1 - T) of the eye's pixel (x, y) lands in target row H - 1 - y, column eye * W + x; a
         // tile with an empty list is not an active tile and keeps the clear value (0, 0, 0, 1)
         const uint32_t clearA = hd.y == 0 ? 0x3C003C00u : 0u;
@@ -721,7 +783,7 @@ void df_launch_instances(const uint32_t* order, const DfArgs& a, const DfArena& 
     const uint32_t blocks = (a.count + kDfBlock - 1) / kDfBlock;
     if (blocks == 0) return;
     hipLaunchKernelGGL(k_df_instances, dim3(blocks), dim3(kDfBlock), 0, s, A.visHdr, order, A.touched, A.bounds,
-                       A.instSums, a.maxInstances, a.tilesX, A.ikeys[0], A.ivals[0]);
+                       A.instSums, A.renderData, a.maxInstances, a.tilesX, A.ikeys[0], A.ivals[0]);
 }
 
 void df_launch_ranges(const uint32_t* sortedTiles, const DfArgs& a, const DfArena& A, hipStream_t s) {
@@ -747,11 +809,16 @@ void df_launch_blend(const uint32_t* sortedGids, const DfArgs& a, const DfArena&
         hipLaunchKernelGGL(k_df_blend<kDfBlendWaves>, dim3(grid), dim3(kDfBlendWaves * 64), 0, s, A.headers,
                            sortedGids, A.renderData, A.expTable, A.queue, a.tilesX, a.tileCount, (uint32_t)a.width,
                            (uint32_t)a.height, (uint8_t*)color, pitch, colorFormat);
+    else if (A.blendStats)
+        hipLaunchKernelGGL((k_df_blend_eye<kDfBlendWaves, true>), dim3(grid), dim3(kDfBlendWaves * 64), 0, s,
+                           A.headers, sortedGids, A.renderData, A.expTable, A.queue, a.tilesX, a.tileCount,
+                           (uint32_t)a.width, (uint32_t)a.height, (uint8_t*)color, pitch, colorFormat,
+                           costOrder ? (const uint32_t*)A.unitOrder : nullptr, A.unitCost, flags, A.blendStats);
     else
-        hipLaunchKernelGGL(k_df_blend_eye<kDfBlendWaves>, dim3(grid), dim3(kDfBlendWaves * 64), 0, s, A.headers,
-                           sortedGids, A.renderData, A.expTable, A.queue, a.tilesX, a.tileCount, (uint32_t)a.width,
-                           (uint32_t)a.height, (uint8_t*)color, pitch, colorFormat,
-                           costOrder ? (const uint32_t*)A.unitOrder : nullptr, A.unitCost, flags);
+        hipLaunchKernelGGL((k_df_blend_eye<kDfBlendWaves, false>), dim3(grid), dim3(kDfBlendWaves * 64), 0, s,
+                           A.headers, sortedGids, A.renderData, A.expTable, A.queue, a.tilesX, a.tileCount,
+                           (uint32_t)a.width, (uint32_t)a.height, (uint8_t*)color, pitch, colorFormat,
+                           costOrder ? (const uint32_t*)A.unitOrder : nullptr, A.unitCost, flags, nullptr);
 }
 
 }  // namespace gsm

@@ -442,6 +442,7 @@ class DepthFirstBuffer(enum.IntEnum):  # include/gsm_depthfirst.h gsm_depthfirst
     INSTANCE_TILES = 5
     INSTANCE_GAUSSIANS = 6
     HEADERS = 7
+    BLEND_STATS = 8
 
 
 DF_STAGES = ("project", "depth_sort", "instances", "tile_sort", "blend")  # gsm_depthfirst_stage
@@ -506,8 +507,8 @@ class DepthFirstRenderer:
         st = _lib().gsm_depthfirst_last_gpu_time(self._h, C.byref(s))
         return float(s.value) if st == 0 else None
 
-    def set_profiling(self, stage_events: bool = True, blend_events: bool = False):
-        flags = (1 if stage_events else 0) | (8 if blend_events else 0)
+    def set_profiling(self, stage_events: bool = True, blend_events: bool = False, blend_stats: bool = False):
+        flags = (1 if stage_events else 0) | (2 if blend_stats else 0) | (8 if blend_events else 0)
         _check(_lib().gsm_depthfirst_set_profiling(self._h, flags), "set_profiling")
 
     def stage_times_ms(self) -> dict:
@@ -537,6 +538,8 @@ class DepthFirstRenderer:
             return raw.view(np.uint32).reshape(-1, 2)
         if which in (DepthFirstBuffer.DEPTH_ORDER, DepthFirstBuffer.INSTANCE_GAUSSIANS):
             return raw.view(np.int32)
+        if which == DepthFirstBuffer.BLEND_STATS:
+            return raw.view(np.uint64)
         return raw.view(np.uint32)
 
 

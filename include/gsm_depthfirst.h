@@ -71,15 +71,18 @@ typedef enum {
     GSM_DF_BUF_DEPTH_ORDER = 4,      /* int32[visible] ids after the depth sort [primitiveIndices] */
     GSM_DF_BUF_INSTANCE_TILES = 5,   /* uint32[total_instances] sorted tile ids [instanceTileIds] */
     GSM_DF_BUF_INSTANCE_GAUSSIANS = 6, /* int32[total_instances] [instanceGaussianIndices] */
-    GSM_DF_BUF_HEADERS = 7           /* GaussianHeader[tile_count] {offset, count} [tileHeaders] */
+    GSM_DF_BUF_HEADERS = 7,          /* GaussianHeader[tile_count] {offset, count} [tileHeaders] */
+    GSM_DF_BUF_BLEND_STATS = 8       /* uint64[4] (profiling bit 1): list entries the blend walked, of
+                                        which had the eye's mean, of which blended; list entries */
 } gsm_depthfirst_buffer;
 
 gsm_status gsm_depthfirst_debug_counters(gsm_depthfirst *renderer, gsm_depthfirst_counters *out);
 /* Copies min(bytes, size) bytes; *needed (nullable) receives the full size. */
 gsm_status gsm_depthfirst_debug_copy(gsm_depthfirst *renderer, int which, void *host_dst, size_t bytes,
                                      size_t *needed);
-/* bit 0: bracket every stage with HIP events (GSM_DF_STAGE_*); bit 3: only the blend (two
- * events per frame, for timing the blend inside a timed loop). */
+/* bit 0: bracket every stage with HIP events (GSM_DF_STAGE_*); bit 1: count the blend's walk
+ * (GSM_DF_BUF_BLEND_STATS); bit 3: only the blend (two events per frame, for timing the blend
+ * inside a timed loop). */
 gsm_status gsm_depthfirst_set_profiling(gsm_depthfirst *renderer, int enable);
 typedef enum {
     GSM_DF_STAGE_PROJECT = 0, /* project both eyes + visibility compaction */

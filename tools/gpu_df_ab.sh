@@ -8,5 +8,5 @@ tail -1 gpurun_out/pytest_df.log
 for v in ${DF_VARIANTS:-default:}; do
   name=${v%%:*}; envs=${v#*:}
   env ${envs//,/ } timeout -k 10 240 python bench.py --config cfg5_1m_sh2_stereo_2x1440x1600_f16 --steps 30 --warmup 5 --cpu-baseline 0 > gpurun_out/df_bench_$name.log 2>&1 || exit 1
-  python3 -c "import json;d=json.loads(open('gpurun_out/df_bench_$name.log').read().strip().splitlines()[-1]);print('$name',round(d['value'],1),{k:round(x,4) for k,x in d['stages_ms'].items()},d['parity_vs_oracle'])"
+  python3 -c "import json;d=json.loads(open('gpurun_out/df_bench_$name.log').read().strip().splitlines()[-1]);print('$name',round(d['value'],1),{k:round(x,4) for k,x in d['stages_ms'].items()},d['parity_vs_oracle'],d.get('blend_walk'))"
 done

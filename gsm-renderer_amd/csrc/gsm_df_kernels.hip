@@ -668,20 +668,26 @@ __global__ __launch_bounds__(NW * 64) void k_df_blend_eye(const uint2* __restric
                 else if (b0 == 128u) __builtin_amdgcn_s_setprio(2);
                 else if (b0 == 320u && !split) __builtin_amdgcn_s_setprio(3);
             }
+            // the batch's entries that are not flagged for this eye, compacted in list order (the
+            // flagged ones are identity steps); padded with mean -inf to a multiple of 4
             const uint32_t gw = lane < n ? gids[hd.x + b0 + lane] : 0u;
-            if (lane < n && !((gw >> (kDfSkipShift + eye)) & 1u)) {
+            const bool keep = lane < n && !((gw >> (kDfSkipShift + eye)) & 1u);
+            const uint64_t km = __builtin_amdgcn_ballot_w64(keep);
+            const uint32_t nk = (uint32_t)__popcll(km);
+            if (keep) {
+                const uint32_t pos = __builtin_amdgcn_mbcnt_hi((uint32_t)(km >> 32),
+                                                               __builtin_amdgcn_mbcnt_lo((uint32_t)km, 0u));
                 const uint32_t g = gw & kDfGidMask;
                 const uint32_t* w = (const uint32_t*)(rd + g);
                 const uint32_t mean = w[3 * eye], cc = w[3 * eye + 1], cxy = w[3 * eye + 2] & 0xFFFFu;
                 const uint32_t c = w[6];  // colorR, G, B, opacity (bytes 24..27)
-                sA[lane] = make_uint4(mean, cc, cxy | ((uint32_t)div255[c >> 24] << 16),
-                                      (uint32_t)div255[c & 0xFFu] | ((uint32_t)div255[(c >> 8) & 0xFFu] << 16));
-                sB[lane] = (uint32_t)div255[(c >> 16) & 0xFFu];
-            } else {  // padding and flagged entries: mean -inf, skipped by the mean test
-                sA[lane] = make_uint4(0xFC00FC00u, 0u, 0u, 0u);
+                sA[pos] = make_uint4(mean, cc, cxy | ((uint32_t)div255[c >> 24] << 16),
+                                     (uint32_t)div255[c & 0xFFu] | ((uint32_t)div255[(c >> 8) & 0xFFu] << 16));
+                sB[pos] = (uint32_t)div255[(c >> 16) & 0xFFu];
             }
+            if (lane < 4u && nk + lane < ((nk + 3u) & ~3u)) sA[nk + lane] = make_uint4(0xFC00FC00u, 0u, 0u, 0u);
             df_wave_sync();
-            for (uint32_t j0 = 0; j0 < n; j0 += 4) {
+            for (uint32_t j0 = 0; j0 < nk; j0 += 4) {
 #pragma unroll
                 for (uint32_t jj = 0; jj < 4; ++jj) {
                     const uint32_t j = j0 + jj;
@@ -703,7 +709,7 @@ __global__ __launch_bounds__(NW * 64) void k_df_blend_eye(const uint2* __restric
                     }
                 }
                 if (done) {
-                    walked = b0 + j0;  // to the group of 4 (a cost estimate for the schedule)
+                    walked = b0 + n;  // list entries traversed (a cost estimate for the schedule)
                     break;
                 }
             }

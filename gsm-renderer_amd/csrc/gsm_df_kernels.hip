@@ -260,49 +260,76 @@ __global__ __launch_bounds__(kDfBlock) void k_df_icount(const TileAssignmentHead
     if (threadIdx.x == 0) sums[blockIdx.x] = s;
 }
 
-// Instance flags (bits 30, 31 of the instance's gaussian id, gsm_df_internal.h kDfSkipShift): eye e
-// provably contributes nothing to tile (x0, y0).  The blend evaluates, per pixel, the fp16 form
+// Tile-level skip test of the blend's staging: eye e of an entry provably contributes nothing to
+// the unit's tile (x0, y0).  The blend evaluates, per pixel, the fp16 form
 // p = fl(fl(fl(fl(dx*dx)*cxx) + fl(fl(dy*dy)*cyy)) + fl(fl(dx*dy)*cxy2)) with dx = fl(px - mx), and an
 // eye's alpha is 0 exactly when p is in (9, +inf] (stereo_exp_table_entry).  With Q the same form in
 // real arithmetic on the same fp16 inputs, a = cxx dx^2, b = cyy dy^2 and rho = |cxy2| / (2 sqrt(cxx cyy)):
 // every product and sum above rounds once with relative error <= u = 2^-11 while nothing overflows, so
 // p >= (1 - u) (Q - 9.02 u (a + b)), and |c| <= rho (a + b), Q >= (1 - rho)(a + b) give
-// p >= (1 - u) Q (1 - 9.02 u / (1 - rho)).  The flag is set only when that bound exceeds 9 for the
+// p >= (1 - u) Q (1 - 9.02 u / (1 - rho)).  The entry is skipped only when that bound exceeds 9 for the
 // minimum of Q over the tile's pixel rectangle (continuous, so it bounds every pixel), with
 // rho <= 15/16, |dx|, |dy| <= 200 and a + b <= 16000 over the tile (no fp16 overflow, no NaN), pixel
 // coordinates below 2048 (exact in fp16) and finite positive cxx, cyy.  Such an entry is an identity
-// step of the blend for that eye, which then skips it without reading its record.
-__device__ __forceinline__ bool df_eye_misses_tile(uint32_t meanW, uint32_t ccW, uint32_t cxyW, int x0, int y0) {
-    const float mxf = hbits_to_f((uint16_t)(meanW & 0xFFFFu)), myf = hbits_to_f((uint16_t)(meanW >> 16));
-    if (!(mxf >= -60000.0f)) return true;  // the blend's mean test skips this eye anyway
+// step of the blend for that eye (C + c * (0 * T) = C, T * (1 - 0) = T).
+// The per-gaussian part of the test, once per eye; the per-tile part in fp32 (every quantity is
+// bounded, so fp32 evaluation errors stay below 1e-6 relative, covered by the extra 1e-5 factor).
+// Divisions and square roots here use the hardware approximations (v_rcp_f32, v_rsq_f32, ~1 ulp):
+// they only move the edge minimiser t by ~1e-7 relative (Q rises by at most cyy * (2e-5)^2 there) and
+// rho by ~1e-6 (the factor by ~1.3e-6), both inside the 1e-3 absolute and 1e-5 relative slack.
+struct DfEyeSkip {
+    float mx, my, cxx, cyy, cxy, factor, hx, hy;  // hx = 1 / (2 cxx), hy = 1 / (2 cyy)
+    int mode;  // 0: test per tile, 1: always skip (the eye's mean test fails), 2: never skip
+};
+__device__ __forceinline__ DfEyeSkip df_eye_skip_setup(uint32_t meanW, uint32_t ccW, uint32_t cxyW) {
+    DfEyeSkip e;
+    e.mx = hbits_to_f((uint16_t)(meanW & 0xFFFFu));
+    e.my = hbits_to_f((uint16_t)(meanW >> 16));
+    e.cxx = hbits_to_f((uint16_t)(ccW & 0xFFFFu));
+    e.cyy = hbits_to_f((uint16_t)(ccW >> 16));
+    e.cxy = hbits_to_f((uint16_t)(cxyW & 0xFFFFu));
+    e.factor = 0.0f;
+    e.mode = 2;
+    if (!(e.mx >= -60000.0f)) {  // the blend's mean test skips this eye anyway
+        e.mode = 1;
+        return e;
+    }
+    if (!(e.cxx > 0.0f && e.cyy > 0.0f && e.cxx < 65504.0f && e.cyy < 65504.0f && __builtin_fabsf(e.cxy) < 65504.0f &&
+          __builtin_fabsf(e.my) < 65504.0f))
+        return e;
+    const float rho = 0.5f * __builtin_fabsf(e.cxy) * __builtin_amdgcn_rsqf(e.cxx * e.cyy);
+    if (!(rho <= 15.0f / 16.0f)) return e;
+    const float u = 1.0f / 2048.0f;
+    e.factor = (1.0f - u) * (1.0f - 10.0f * u * __builtin_amdgcn_rcpf(1.0f - rho)) * (1.0f - 1e-5f);
+    e.hx = __builtin_amdgcn_rcpf(2.0f * e.cxx);
+    e.hy = __builtin_amdgcn_rcpf(2.0f * e.cyy);
+    e.mode = 0;
+    return e;
+}
+__device__ __forceinline__ bool df_eye_misses_tile(const DfEyeSkip& e, int x0, int y0) {
+    if (e.mode != 0) return e.mode == 1;
     if (x0 + 15 >= 2048 || y0 + 15 >= 2048) return false;
-    const double cxx = (double)hbits_to_f((uint16_t)(ccW & 0xFFFFu)), cyy = (double)hbits_to_f((uint16_t)(ccW >> 16));
-    const double cxy = (double)hbits_to_f((uint16_t)(cxyW & 0xFFFFu));
-    if (!(cxx > 0.0 && cyy > 0.0 && cxx < 65504.0 && cyy < 65504.0 && __builtin_fabs(cxy) < 65504.0)) return false;
-    if (!(__builtin_fabs((double)myf) < 65504.0)) return false;
-    const double dx0 = (double)x0 - (double)mxf, dx1 = dx0 + 15.0;
-    const double dy0 = (double)y0 - (double)myf, dy1 = dy0 + 15.0;
-    if (!(__builtin_fabs(dx0) <= 200.0 && __builtin_fabs(dx1) <= 200.0 && __builtin_fabs(dy0) <= 200.0 &&
-          __builtin_fabs(dy1) <= 200.0))
+    const float dx0 = (float)x0 - e.mx, dx1 = dx0 + 15.0f;
+    const float dy0 = (float)y0 - e.my, dy1 = dy0 + 15.0f;
+    if (!(__builtin_fabsf(dx0) <= 200.0f && __builtin_fabsf(dx1) <= 200.0f && __builtin_fabsf(dy0) <= 200.0f &&
+          __builtin_fabsf(dy1) <= 200.0f))
         return false;
-    if (dx0 <= 0.0 && dx1 >= 0.0 && dy0 <= 0.0 && dy1 >= 0.0) return false;  // the mean is inside: Q min = 0
-    const double rho = __builtin_fabs(cxy) / (2.0 * __builtin_sqrt(cxx * cyy));
-    if (!(rho <= 15.0 / 16.0)) return false;
-    const double ax = __builtin_fmax(dx0 * dx0, dx1 * dx1), ay = __builtin_fmax(dy0 * dy0, dy1 * dy1);
-    if (!(cxx * ax + cyy * ay <= 16000.0)) return false;
+    if (dx0 <= 0.0f && dx1 >= 0.0f && dy0 <= 0.0f && dy1 >= 0.0f) return false;  // the mean is inside: Q min = 0
+    const float ax = __builtin_fmaxf(dx0 * dx0, dx1 * dx1), ay = __builtin_fmaxf(dy0 * dy0, dy1 * dy1);
+    if (!(e.cxx * ax + e.cyy * ay <= 16000.0f)) return false;
     // min of Q over the rectangle: on its boundary (Q is convex with its minimum at the mean, outside)
-    auto q = [&](double dx, double dy) { return cxx * dx * dx + cyy * dy * dy + cxy * dx * dy; };
-    auto along_y = [&](double X) {  // edge dx = X: minimise over dy in [dy0, dy1]
-        const double t = __builtin_fmin(__builtin_fmax(-cxy * X / (2.0 * cyy), dy0), dy1);
+    auto q = [&](float dx, float dy) { return e.cxx * dx * dx + e.cyy * dy * dy + e.cxy * dx * dy; };
+    auto along_y = [&](float X) {  // edge dx = X: minimise over dy in [dy0, dy1]
+        const float t = __builtin_fminf(__builtin_fmaxf(-e.cxy * X * e.hy, dy0), dy1);
         return q(X, t);
     };
-    auto along_x = [&](double Y) {
-        const double t = __builtin_fmin(__builtin_fmax(-cxy * Y / (2.0 * cxx), dx0), dx1);
+    auto along_x = [&](float Y) {
+        const float t = __builtin_fminf(__builtin_fmaxf(-e.cxy * Y * e.hx, dx0), dx1);
         return q(t, Y);
     };
-    const double qmin = __builtin_fmin(__builtin_fmin(along_y(dx0), along_y(dx1)), __builtin_fmin(along_x(dy0), along_x(dy1)));
-    const double u = 1.0 / 2048.0;
-    return qmin * (1.0 - u) * (1.0 - 10.0 * u / (1.0 - rho)) > 9.0 + 1e-3;
+    const float qmin = __builtin_fminf(__builtin_fminf(along_y(dx0), along_y(dx1)),
+                                       __builtin_fminf(along_x(dy0), along_x(dy1)));
+    return qmin * e.factor > 9.0f + 1e-3f;
 }
 
 __global__ __launch_bounds__(kDfBlock) void k_df_instances(const TileAssignmentHeader* __restrict__ visHdr,
@@ -310,7 +337,6 @@ __global__ __launch_bounds__(kDfBlock) void k_df_instances(const TileAssignmentH
                                                            const uint32_t* __restrict__ touched,
                                                            const short4* __restrict__ bounds,
                                                            const uint32_t* __restrict__ blockOffsets,
-                                                           const StereoTiledRenderData* __restrict__ rd,
                                                            uint32_t maxInstances, uint32_t tilesX,
                                                            uint32_t* __restrict__ tiles, uint32_t* __restrict__ gids) {
     __shared__ uint32_t lds[kDfBlock / 64];
@@ -323,17 +349,30 @@ __global__ __launch_bounds__(kDfBlock) void k_df_instances(const TileAssignmentH
     if (c == 0) return;
     uint64_t wp = (uint64_t)blockOffsets[blockIdx.x] + off;
     const short4 r = bounds[g];
-    const uint4 w0 = ((const uint4*)(rd + g))[0], w1 = ((const uint4*)(rd + g))[1];
     for (int ty = r.z; ty <= r.w; ++ty)
         for (int tx = r.x; tx <= r.y; ++tx) {
             if (wp >= maxInstances) return;
             tiles[wp] = (uint32_t)(ty * (int)tilesX + tx) & 0xFFFFu;  // ushort tile id
-            const int x0 = tx * (int)kDfTile, y0 = ty * (int)kDfTile;
-            const uint32_t fl = (df_eye_misses_tile(w0.x, w0.y, w0.z, x0, y0) ? 1u : 0u) |
-                                (df_eye_misses_tile(w0.w, w1.x, w1.y, x0, y0) ? 2u : 0u);
-            gids[wp] = g | (fl << kDfSkipShift);
+            gids[wp] = g;
             wp++;
         }
+}
+
+// k_df_flags: one thread per instance (depth order, before the tile sort): bit kDfSkipShift + e of
+// the instance's gaussian id is set when eye e provably adds nothing to the instance's tile
+__global__ __launch_bounds__(256) void k_df_flags(const TileAssignmentHeader* __restrict__ instHdr,
+                                                  const uint32_t* __restrict__ tiles, uint32_t* __restrict__ gids,
+                                                  const StereoTiledRenderData* __restrict__ rd, uint32_t tilesX) {
+    const uint32_t total = instHdr->totalAssignments;
+    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < total; i += gridDim.x * 256u) {
+        const uint32_t g = gids[i], t = tiles[i];
+        const uint4 w0 = ((const uint4*)(rd + g))[0];
+        const uint2 w1 = ((const uint2*)(rd + g))[2];
+        const int x0 = (int)((t % tilesX) * kDfTile), y0 = (int)((t / tilesX) * kDfTile);
+        const uint32_t fl = (df_eye_misses_tile(df_eye_skip_setup(w0.x, w0.y, w0.z), x0, y0) ? 1u : 0u) |
+                            (df_eye_misses_tile(df_eye_skip_setup(w0.w, w1.x, w1.y), x0, y0) ? 2u : 0u);
+        if (fl) gids[i] = g | (fl << kDfSkipShift);
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -668,7 +707,7 @@ __global__ __launch_bounds__(NW * 64) void k_df_blend_eye(const uint2* __restric
                 else if (b0 == 128u) __builtin_amdgcn_s_setprio(2);
                 else if (b0 == 320u && !split) __builtin_amdgcn_s_setprio(3);
             }
-            // the batch's entries that are not flagged for this eye, compacted in list order (the
+            // the batch's entries not flagged for this eye (k_df_flags), compacted in list order (the
             // flagged ones are identity steps); padded with mean -inf to a multiple of 4
             const uint32_t gw = lane < n ? gids[hd.x + b0 + lane] : 0u;
             const bool keep = lane < n && !((gw >> (kDfSkipShift + eye)) & 1u);
@@ -677,8 +716,7 @@ __global__ __launch_bounds__(NW * 64) void k_df_blend_eye(const uint2* __restric
             if (keep) {
                 const uint32_t pos = __builtin_amdgcn_mbcnt_hi((uint32_t)(km >> 32),
                                                                __builtin_amdgcn_mbcnt_lo((uint32_t)km, 0u));
-                const uint32_t g = gw & kDfGidMask;
-                const uint32_t* w = (const uint32_t*)(rd + g);
+                const uint32_t* w = (const uint32_t*)(rd + (gw & kDfGidMask));
                 const uint32_t mean = w[3 * eye], cc = w[3 * eye + 1], cxy = w[3 * eye + 2] & 0xFFFFu;
                 const uint32_t c = w[6];  // colorR, G, B, opacity (bytes 24..27)
                 sA[pos] = make_uint4(mean, cc, cxy | ((uint32_t)div255[c >> 24] << 16),
@@ -789,7 +827,15 @@ void df_launch_instances(const uint32_t* order, const DfArgs& a, const DfArena& 
     const uint32_t blocks = (a.count + kDfBlock - 1) / kDfBlock;
     if (blocks == 0) return;
     hipLaunchKernelGGL(k_df_instances, dim3(blocks), dim3(kDfBlock), 0, s, A.visHdr, order, A.touched, A.bounds,
-                       A.instSums, A.renderData, a.maxInstances, a.tilesX, A.ikeys[0], A.ivals[0]);
+                       A.instSums, a.maxInstances, a.tilesX, A.ikeys[0], A.ivals[0]);
+}
+
+void df_launch_flags(const DfArgs& a, const DfArena& A, hipStream_t s) {
+    uint32_t blocks = (a.maxInstances + 255u) / 256u;  // grid-stride over the device-side total
+    if (blocks > 8192u) blocks = 8192u;
+    if (blocks == 0) return;
+    hipLaunchKernelGGL(k_df_flags, dim3(blocks), dim3(256), 0, s, A.instHdr, A.ikeys[0], A.ivals[0], A.renderData,
+                       a.tilesX);
 }
 
 void df_launch_ranges(const uint32_t* sortedTiles, const DfArgs& a, const DfArena& A, hipStream_t s) {

@@ -31,6 +31,9 @@ cat $OUT/traffic.json
 step bench_cfg2 600 python bench.py --traffic-json $OUT/traffic.json
 step bench_cfg3 600 python bench.py --traffic-json $OUT/traffic.json --config cfg3_5m_sh3_4k_f16 --steps 30 --warmup 3
 step bench_cfg5 600 python bench.py --traffic-json $OUT/traffic.json --config cfg5_1m_sh2_stereo_2x1440x1600_f16 --steps 30 --warmup 3
+step bench_cfg5_global 600 python bench.py --traffic-json $OUT/traffic.json --config cfg5_1m_sh2_stereo_2x1440x1600_f16 --steps 30 --warmup 3 --stereo-path global --cpu-baseline 0
+step kernel_trace_cfg5 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/kt5 -o run -- \
+     python bench.py --config cfg5_1m_sh2_stereo_2x1440x1600_f16 --steps 30 --warmup 5 --cpu-baseline 0 --parity 0
 step kernel_trace 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/kt -o run -- \
      python bench.py --traffic-json $OUT/traffic.json --steps 50 --warmup 5 --cpu-baseline 0 --parity 0
 echo "=== done"

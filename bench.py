@@ -48,6 +48,8 @@ def parse():
                    help="blend HBM bytes and VALU instructions per launch (tools/traffic.py)")
     p.add_argument("--stereo-path", choices=("depthfirst", "global"), default="depthfirst",
                    help="stereo configs: DepthFirst semantics (SURVEY 8f rank 1) or two Global views")
+    p.add_argument("--traffic-json-df", default=os.path.join(ROOT, "profiles", "traffic_cfg5_r01.json"),
+                   help="blend PMC traffic / VALU count of the DepthFirst config (tools/gpu_df_pmc.sh)")
     p.add_argument("--df-max-gaussians", type=int, default=6_000_000,
                    help="DepthFirst RendererConfig.maxGaussians (reference default 6M -> 24M instances)")
     p.add_argument("--multi", choices=("alltoall", "replicas"), default="alltoall",
@@ -320,6 +322,17 @@ def run_depthfirst(args, c, world_np, harm_np, world, harm, dev):
     b_blend = A * 36 + P * 8 + T * 8
     t_blend = blend_ms_timed * 1e-3
     achieved = b_blend / t_blend / 1e9 if t_blend > 0 else 0.0
+    traffic, valu_insts = None, None
+    tj_path = args.traffic_json_df
+    if os.path.exists(tj_path):
+        try:
+            with open(tj_path) as f:
+                tj = json.load(f)
+            if tj.get("config") == args.config:  # measured on this workload only
+                traffic = tj.get("blend_hbm_bytes_per_launch")
+                valu_insts = tj.get("blend_valu_insts_per_launch")
+        except Exception:
+            traffic = None
     parity, cpu = None, None
     if args.parity or args.cpu_baseline:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -351,10 +364,14 @@ def run_depthfirst(args, c, world_np, harm_np, world, harm, dev):
                    "gaussians": n, "width": W, "height": H, "sh_components": sh, "instances": A,
                    "visible": cnt["visible"], "tiles": T, "max_gaussians": cfg.max_gaussians,
                    "parallelism": "single GPU"},
-        "roofline": {"bound": "hbm", "kernel": "k_df_blend", "achieved": achieved, "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+        "roofline": {"bound": "hbm", "kernel": "k_df_blend_eye", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "algorithmic_bytes": b_blend, "avg_launch_ms": blend_ms_timed,
-                     "note": "blend is VALU/LDS-bound (fp16 math per pixel, both eyes per entry)"},
+                     "note": "blend is VALU/LDS-bound (fp16 math per pixel per (tile, eye) unit)"},
+        "roofline_valu": ({"bound": "valu", "kernel": "k_df_blend_eye", "unit": "G wave-instr/s",
+                           "achieved": valu_insts / t_blend / 1e9, "peak": VALU_PEAK_GIPS,
+                           "frac": valu_insts / t_blend / 1e9 / VALU_PEAK_GIPS, "insts_per_launch": valu_insts}
+                          if (valu_insts and t_blend > 0) else None),
         "blend_walk": {"walked": walk[0], "with_mean": walk[1], "blended": walk[2], "list_entries": walk[3]},
         "cpu_baseline": cpu, "stages_ms": stage_ms, "blend_gb_per_s": achieved, "parity_vs_oracle": parity,
     }

@@ -271,8 +271,7 @@ gsm_status DepthFirstRenderer::renderStereoSbs(hipStream_t s, const gsm_gaussian
     if (prof) hipEventRecord(ev[2], s);
     df_launch_instance_counts(A_.dvals[dc], a, A_, s);
     launch_scan_sums(A_.instSums, nb, maxInstances_, A_.instHdr, A_.queue, s);
-    df_launch_instances(A_.dvals[dc], a, A_, s);
-    df_launch_flags(a, A_, s);
+    df_launch_instances(A_.dvals[dc], a, A_, s);  // with the blend's skip flags
     if (prof) hipEventRecord(ev[3], s);
     // TileSortEncoder (DepthFirstRenderer.swift:683-768): stable sort by the 16-bit tile id
     uint32_t tileBits = 0;

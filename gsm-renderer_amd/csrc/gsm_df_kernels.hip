@@ -375,6 +375,65 @@ __global__ __launch_bounds__(256) void k_df_flags(const TileAssignmentHeader* __
     }
 }
 
+// k_df_expand: the same instances as k_df_instances, expanded cooperatively: the block's 256
+// gaussians (in depth order) get their offsets from one block scan, then thread t writes the
+// block's instances t, t + 256, ... (consecutive threads, consecutive slots: coalesced stores, no
+// thread walks a long rect alone) and sets the blend's skip flags of each (k_df_flags' test, with
+// each gaussian's per-eye setup computed once into LDS).
+__global__ __launch_bounds__(kDfBlock) void k_df_expand(const TileAssignmentHeader* __restrict__ visHdr,
+                                                        const uint32_t* __restrict__ order,
+                                                        const uint32_t* __restrict__ touched,
+                                                        const short4* __restrict__ bounds,
+                                                        const uint32_t* __restrict__ blockOffsets,
+                                                        const StereoTiledRenderData* __restrict__ rd,
+                                                        uint32_t maxInstances, uint32_t tilesX,
+                                                        uint32_t* __restrict__ tiles, uint32_t* __restrict__ gids) {
+    __shared__ uint32_t lds[kDfBlock / 64];
+    __shared__ uint32_t sOff[kDfBlock];
+    __shared__ uint32_t sG[kDfBlock];
+    __shared__ short4 sR[kDfBlock];
+    __shared__ DfEyeSkip sE[2][kDfBlock];
+    const uint32_t tid = threadIdx.x;
+    const uint32_t i = blockIdx.x * kDfBlock + tid;
+    const uint32_t V = visHdr->totalAssignments;
+    const uint32_t g = i < V ? order[i] : 0u;
+    const uint32_t c = i < V ? touched[g] : 0u;
+    uint32_t total;
+    const uint32_t off = block_exclusive_scan<kDfBlock>(c, lds, &total);
+    sOff[tid] = off;
+    sG[tid] = g;
+    if (c > 0) {
+        sR[tid] = bounds[g];
+        const uint4 w0 = ((const uint4*)(rd + g))[0];
+        const uint2 w1 = ((const uint2*)(rd + g))[2];
+        sE[0][tid] = df_eye_skip_setup(w0.x, w0.y, w0.z);
+        sE[1][tid] = df_eye_skip_setup(w0.w, w1.x, w1.y);
+    }
+    __syncthreads();
+    if (total == 0) return;
+    const uint64_t base = (uint64_t)blockOffsets[blockIdx.x];
+    for (uint32_t k = tid; k < total; k += kDfBlock) {
+        const uint64_t wp = base + k;
+        if (wp >= maxInstances) break;
+        // owner: the last gaussian whose offset is <= k (gaussians without instances share an
+        // offset with the next one, so the last of equal offsets is the one with instances)
+        uint32_t lo = 0, hi = kDfBlock;
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (sOff[mid] <= k) lo = mid; else hi = mid;
+        }
+        const short4 r = sR[lo];
+        const uint32_t w = (uint32_t)(r.y - r.x + 1), local = k - sOff[lo];
+        const uint32_t dy = local / w, dx = local - dy * w;
+        const int tx = r.x + (int)dx, ty = r.z + (int)dy;
+        tiles[wp] = (uint32_t)(ty * (int)tilesX + tx) & 0xFFFFu;  // ushort tile id
+        const int x0 = tx * (int)kDfTile, y0 = ty * (int)kDfTile;
+        const uint32_t fl = (df_eye_misses_tile(sE[0][lo], x0, y0) ? 1u : 0u) |
+                            (df_eye_misses_tile(sE[1][lo], x0, y0) ? 2u : 0u);
+        gids[wp] = sG[lo] | (fl << kDfSkipShift);
+    }
+}
+
 // ---------------------------------------------------------------------------
 // 4. tile ranges (extractTileRangesKernel, DepthFirstShaders.metal:1258-1313): two binary searches
 //    per tile; an empty tile's offset is its lower bound, an empty frame gives {0, 0}
@@ -826,8 +885,15 @@ void df_launch_instance_counts(const uint32_t* order, const DfArgs& a, const DfA
 void df_launch_instances(const uint32_t* order, const DfArgs& a, const DfArena& A, hipStream_t s) {
     const uint32_t blocks = (a.count + kDfBlock - 1) / kDfBlock;
     if (blocks == 0) return;
+    const char* v = getenv("GSM_DF_EXPAND");  // 0: one thread per gaussian + k_df_flags (A/B)
+    if (!(v && v[0] == '0')) {
+        hipLaunchKernelGGL(k_df_expand, dim3(blocks), dim3(kDfBlock), 0, s, A.visHdr, order, A.touched, A.bounds,
+                           A.instSums, A.renderData, a.maxInstances, a.tilesX, A.ikeys[0], A.ivals[0]);
+        return;
+    }
     hipLaunchKernelGGL(k_df_instances, dim3(blocks), dim3(kDfBlock), 0, s, A.visHdr, order, A.touched, A.bounds,
                        A.instSums, a.maxInstances, a.tilesX, A.ikeys[0], A.ivals[0]);
+    df_launch_flags(a, A, s);
 }
 
 void df_launch_flags(const DfArgs& a, const DfArena& A, hipStream_t s) {

@@ -11,6 +11,8 @@ import sys
 from collections import defaultdict
 
 root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/round/pmc"
+kernel = sys.argv[2] if len(sys.argv) > 2 else "k_blend_px"          # kernel name substring
+config = sys.argv[3] if len(sys.argv) > 3 else "cfg2_1m_sh3_1080p_f16"
 acc = defaultdict(lambda: defaultdict(list))
 for path in sorted(glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True)):
     with open(path) as f:
@@ -18,13 +20,13 @@ for path in sorted(glob.glob(os.path.join(root, "**", "*counter_collection.csv")
             acc[row.get("Kernel_Name", "?")][row["Counter_Name"]].append(float(row["Counter_Value"]))
 out = {}
 for k, cs in acc.items():
-    if "k_blend_px" not in k or "FETCH_SIZE" not in cs or "WRITE_SIZE" not in cs:
+    if kernel not in k or "FETCH_SIZE" not in cs or "WRITE_SIZE" not in cs:
         continue
     f = sum(cs["FETCH_SIZE"]) / len(cs["FETCH_SIZE"])
     w = sum(cs["WRITE_SIZE"]) / len(cs["WRITE_SIZE"])
     out = {
         "kernel": k.split("(")[0],
-        "config": "cfg2_1m_sh3_1080p_f16",
+        "config": config,
         "source": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes (tools/gpu_round.sh)",
         "fetch_size_kb": round(f, 1),
         "write_size_kb": round(w, 1),
@@ -33,6 +35,6 @@ for k, cs in acc.items():
         "blend_valu_insts_per_launch": (int(round(sum(cs["SQ_INSTS_VALU"]) / len(cs["SQ_INSTS_VALU"])))
                                         if "SQ_INSTS_VALU" in cs else None),
         "note": "includes each workgroup's 128 KiB exp-table load and the re-reads of a tile's list by "
-                "both half-tile units; Infinity-Cache hits are counted by these fabric counters",
+                "every unit of the tile; Infinity-Cache hits are counted by these fabric counters",
     }
 print(json.dumps(out, indent=1))

@@ -148,7 +148,7 @@ gsm_status DepthFirstRenderer::create(const gsm_renderer_config& cfg, int hipDev
     }
     GSM_DF_ALLOC(A.radixHist, (size_t)256 * rgrid * 4);
     GSM_DF_ALLOC(A.radixBinTotals, 256 * 4);
-    GSM_DF_ALLOC(A.headers, (size_t)r->maxTiles_ * sizeof(uint2));
+    GSM_DF_ALLOC(A.starts, ((size_t)r->maxTiles_ + 1) * sizeof(uint32_t));
     GSM_DF_ALLOC(A.queue, 4);
     GSM_DF_ALLOC(A.expTable, 65536 * 2);
     GSM_DF_ALLOC(A.unitCost, (size_t)r->maxTiles_ * 2 * sizeof(uint16_t));
@@ -163,7 +163,7 @@ gsm_status DepthFirstRenderer::create(const gsm_renderer_config& cfg, int hipDev
     if (hipMemcpy(A.expTable, expt.data(), 65536 * 2, hipMemcpyHostToDevice) != hipSuccess ||
         hipMemset(A.visHdr, 0, sizeof(TileAssignmentHeader)) != hipSuccess ||
         hipMemset(A.instHdr, 0, sizeof(TileAssignmentHeader)) != hipSuccess ||
-        hipMemset(A.headers, 0, (size_t)r->maxTiles_ * sizeof(uint2)) != hipSuccess) {
+        hipMemset(A.starts, 0, ((size_t)r->maxTiles_ + 1) * sizeof(uint32_t)) != hipSuccess) {
         delete r;
         return GSM_ERR_FAILED_TO_ALLOCATE_BUFFER;
     }
@@ -333,7 +333,7 @@ gsm_status DepthFirstRenderer::debugCopy(int which, void* dst, size_t bytes, siz
         case GSM_DF_BUF_DEPTH_ORDER: src = depthOrder_; full = (size_t)c.visible * 4; break;
         case GSM_DF_BUF_INSTANCE_TILES: src = instTiles_; full = (size_t)c.total_instances * 4; break;
         case GSM_DF_BUF_INSTANCE_GAUSSIANS: src = instGids_; full = (size_t)c.total_instances * 4; break;
-        case GSM_DF_BUF_HEADERS: src = A_.headers; full = (size_t)c.tile_count * 8; break;
+        case GSM_DF_BUF_HEADERS: full = (size_t)c.tile_count * 8; break;
         case GSM_DF_BUF_BLEND_STATS: src = (profiling_ & 2) ? statsBuf_ : nullptr; full = 32; break;
         default: return GSM_ERR_INVALID_ARGUMENT;
     }
@@ -352,6 +352,18 @@ gsm_status DepthFirstRenderer::debugCopy(int which, void* dst, size_t bytes, siz
             w[4 * i + 3] = b[i].w;
         }
         std::memcpy(dst, w.data(), cpy);
+        return GSM_OK;
+    }
+    if (which == GSM_DF_BUF_HEADERS) {  // GaussianHeader {offset, count} from the run starts
+        std::vector<uint32_t> st((size_t)c.tile_count + 1);
+        if (hipMemcpy(st.data(), A_.starts, st.size() * 4, hipMemcpyDeviceToHost) != hipSuccess)
+            return GSM_ERR_RENDER_FAILED;
+        std::vector<uint32_t> h((size_t)c.tile_count * 2);
+        for (size_t t = 0; t < c.tile_count; ++t) {
+            h[2 * t] = st[t];
+            h[2 * t + 1] = st[t + 1] - st[t];
+        }
+        std::memcpy(dst, h.data(), cpy);
         return GSM_OK;
     }
     if (!src) return GSM_ERR_RENDER_FAILED;

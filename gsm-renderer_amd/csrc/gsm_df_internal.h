@@ -49,7 +49,7 @@ struct DfArena {
     uint32_t* ivals[2] = {nullptr, nullptr};      // [maxInstances] gaussian ids
     uint32_t* radixHist = nullptr;
     uint32_t* radixBinTotals = nullptr;
-    uint2* headers = nullptr;                     // [tileCount] {offset, count}
+    uint32_t* starts = nullptr;                   // [tileCount + 1] first instance of each tile
     uint32_t* queue = nullptr;                    // blend work counter
     uint16_t* expTable = nullptr;                 // [65536] stereo alpha table (r^2 cutoff folded)
     uint16_t* unitCost = nullptr;                 // [2 * maxTiles] entries each (tile, eye) unit walked

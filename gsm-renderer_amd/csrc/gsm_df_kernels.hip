@@ -435,31 +435,33 @@ __global__ __launch_bounds__(kDfBlock) void k_df_expand(const TileAssignmentHead
 }
 
 // ---------------------------------------------------------------------------
-// 4. tile ranges (extractTileRangesKernel, DepthFirstShaders.metal:1258-1313): two binary searches
-//    per tile; an empty tile's offset is its lower bound, an empty frame gives {0, 0}
+// 4. tile ranges (extractTileRangesKernel, DepthFirstShaders.metal:1258-1313): the reference's two
+//    binary searches per tile become the run starts of the sorted tile ids; header t is
+//    {starts[t], starts[t + 1] - starts[t]} -- the lower bound for an empty tile, {0, 0} for an
+//    empty frame (the debug copy rebuilds the reference's GaussianHeader array from them)
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_df_ranges(const uint32_t* __restrict__ tiles,
+__global__ __launch_bounds__(256) void k_df_starts(const uint32_t* __restrict__ tiles,
                                                    const TileAssignmentHeader* __restrict__ instHdr,
-                                                   uint32_t tileCount, uint2* __restrict__ headers) {
-    const uint32_t t = blockIdx.x * 256u + threadIdx.x;
-    if (t >= tileCount) return;
+                                                   uint32_t tileCount, uint32_t* __restrict__ starts) {
+    // one pass over the tile-sorted instances: starts[t] = first position whose tile is >= t
+    // (the reference's lower bound, so an empty tile gets the position of the next run), for
+    // t = 0 .. tileCount; 4 positions per thread and step
     const uint32_t total = instHdr->totalAssignments;
-    if (total == 0) {
-        headers[t] = make_uint2(0u, 0u);
-        return;
+    const uint32_t stride = gridDim.x * 256u * 4u;
+    for (uint32_t i0 = (blockIdx.x * 256u + threadIdx.x) * 4u; i0 <= total; i0 += stride) {
+        uint32_t k[5];
+        k[0] = i0 == 0 ? 0u : tiles[i0 - 1];
+#pragma unroll
+        for (uint32_t j = 0; j < 4; ++j) k[j + 1] = i0 + j < total ? tiles[i0 + j] : 0u;
+#pragma unroll
+        for (uint32_t j = 0; j < 4; ++j) {
+            const uint32_t i = i0 + j;
+            if (i > total) break;
+            const uint32_t first = i == 0 ? 0u : k[j] + 1u;
+            const uint32_t cur = i == total ? tileCount : min(k[j + 1], tileCount);
+            for (uint32_t t = first; t <= cur; ++t) starts[t] = i;
+        }
     }
-    uint32_t l = 0, r = total;
-    while (l < r) {
-        const uint32_t m = (l + r) >> 1;
-        if (tiles[m] < t) l = m + 1; else r = m;
-    }
-    const uint32_t s = l;
-    r = total;
-    while (l < r) {
-        const uint32_t m = (l + r) >> 1;
-        if (tiles[m] <= t) l = m + 1; else r = m;
-    }
-    headers[t] = make_uint2(s, l - s);
 }
 
 // ---------------------------------------------------------------------------
@@ -596,7 +598,7 @@ __device__ __forceinline__ bool df_alive(const DfEyeState& st, uint32_t thrBits)
 }
 
 template <int NW>
-__global__ __launch_bounds__(NW * 64) void k_df_blend(const uint2* __restrict__ headers,
+__global__ __launch_bounds__(NW * 64) void k_df_blend(const uint32_t* __restrict__ starts,
                                                       const uint32_t* __restrict__ gids,
                                                       const StereoTiledRenderData* __restrict__ rd,
                                                       const uint16_t* __restrict__ expTable,
@@ -623,7 +625,8 @@ __global__ __launch_bounds__(NW * 64) void k_df_blend(const uint2* __restrict__ 
         if (lane == 0) t = atomicAdd(queue, 1u);
         t = (uint32_t)__shfl((int)t, 0, 64);
         if (t >= tileCount) break;
-        const uint2 hd = headers[t];
+        const uint32_t st0 = starts[t];
+        const uint2 hd = make_uint2(st0, starts[t + 1] - st0);
         const uint32_t tileX = t % tilesX, tileY = t / tilesX;
         const uint32_t bx = tileX * kDfTile + (lane & 7u) * 2u, by = tileY * kDfTile + (lane >> 3) * 2u;
         const h2 PX = {(h1)(float)bx, (h1)(float)(bx + 1u)};
@@ -703,7 +706,7 @@ __global__ __launch_bounds__(NW * 64) void k_df_blend(const uint2* __restrict__ 
 // colour (uint4 + uint), read back per entry as uniform-address broadcasts.
 constexpr uint32_t kDfEyeBatch = 64;
 template <int NW, bool STATS>
-__global__ __launch_bounds__(NW * 64) void k_df_blend_eye(const uint2* __restrict__ headers,
+__global__ __launch_bounds__(NW * 64) void k_df_blend_eye(const uint32_t* __restrict__ starts,
                                                           const uint32_t* __restrict__ gids,
                                                           const StereoTiledRenderData* __restrict__ rd,
                                                           const uint16_t* __restrict__ expTable,
@@ -746,7 +749,8 @@ __global__ __launch_bounds__(NW * 64) void k_df_blend_eye(const uint2* __restric
         uint32_t u = order ? __builtin_amdgcn_readfirstlane(order[qi]) : qi;
         if (u >= units) u = qi;  // a schedule is a permutation of [0, units); never trust it further
         const uint32_t t = u >> 1, eye = u & 1u;
-        const uint2 hd = headers[t];
+        const uint32_t st0 = starts[t];
+        const uint2 hd = make_uint2(st0, starts[t + 1] - st0);
         const uint32_t tileX = t % tilesX, tileY = t / tilesX;
         const uint32_t bx = tileX * kDfTile + (lane & 7u) * 2u, by = tileY * kDfTile + (lane >> 3) * 2u;
         const h2 PX = {(h1)(float)bx, (h1)(float)(bx + 1u)};
@@ -905,9 +909,9 @@ void df_launch_flags(const DfArgs& a, const DfArena& A, hipStream_t s) {
 }
 
 void df_launch_ranges(const uint32_t* sortedTiles, const DfArgs& a, const DfArena& A, hipStream_t s) {
-    const uint32_t blocks = (a.tileCount + 255u) / 256u;
-    if (blocks == 0) return;
-    hipLaunchKernelGGL(k_df_ranges, dim3(blocks), dim3(256), 0, s, sortedTiles, A.instHdr, a.tileCount, A.headers);
+    uint32_t blocks = (a.maxInstances + 1u + 1023u) / 1024u;  // grid-stride over the device-side total
+    if (blocks > 4096u) blocks = 4096u;
+    hipLaunchKernelGGL(k_df_starts, dim3(blocks), dim3(256), 0, s, sortedTiles, A.instHdr, a.tileCount, A.starts);
 }
 
 constexpr int kDfBlendWaves = 16;
@@ -924,17 +928,17 @@ void df_launch_blend(const uint32_t* sortedGids, const DfArgs& a, const DfArena&
     const int flags = ((pv && pv[0] == '0') ? 0 : 1) | ((sp && sp[0] == '0') ? 0 : 2);
     const char* v = getenv("GSM_DF_BLEND");
     if (v && v[0] == 'p')
-        hipLaunchKernelGGL(k_df_blend<kDfBlendWaves>, dim3(grid), dim3(kDfBlendWaves * 64), 0, s, A.headers,
+        hipLaunchKernelGGL(k_df_blend<kDfBlendWaves>, dim3(grid), dim3(kDfBlendWaves * 64), 0, s, A.starts,
                            sortedGids, A.renderData, A.expTable, A.queue, a.tilesX, a.tileCount, (uint32_t)a.width,
                            (uint32_t)a.height, (uint8_t*)color, pitch, colorFormat);
     else if (A.blendStats)
         hipLaunchKernelGGL((k_df_blend_eye<kDfBlendWaves, true>), dim3(grid), dim3(kDfBlendWaves * 64), 0, s,
-                           A.headers, sortedGids, A.renderData, A.expTable, A.queue, a.tilesX, a.tileCount,
+                           A.starts, sortedGids, A.renderData, A.expTable, A.queue, a.tilesX, a.tileCount,
                            (uint32_t)a.width, (uint32_t)a.height, (uint8_t*)color, pitch, colorFormat,
                            costOrder ? (const uint32_t*)A.unitOrder : nullptr, A.unitCost, flags, A.blendStats);
     else
         hipLaunchKernelGGL((k_df_blend_eye<kDfBlendWaves, false>), dim3(grid), dim3(kDfBlendWaves * 64), 0, s,
-                           A.headers, sortedGids, A.renderData, A.expTable, A.queue, a.tilesX, a.tileCount,
+                           A.starts, sortedGids, A.renderData, A.expTable, A.queue, a.tilesX, a.tileCount,
                            (uint32_t)a.width, (uint32_t)a.height, (uint8_t*)color, pitch, colorFormat,
                            costOrder ? (const uint32_t*)A.unitOrder : nullptr, A.unitCost, flags, nullptr);
 }

@@ -761,6 +761,20 @@ __global__ __launch_bounds__(NW * 64) void k_df_blend_eye(const uint32_t* __rest
         bool done = false;
         uint32_t walked = hd.y;  // entries this unit walked (its cost for the next frame's order)
         uint32_t nValid = 0, nBlend = 0;  // STATS: entries with a real mean / with a blend step
+        // Loads run one batch ahead: while batch k blends, the records of batch k + 1 and the ids of
+        // batch k + 2 are in flight.  They are unpredicated (index clamped to the list, so every lane
+        // holds a valid id) -- a predicated load would merge with the old register and force its
+        // wait into the loop.
+        const uint32_t* lst = gids + hd.x;
+        const uint32_t last = hd.y > 0 ? hd.y - 1u : 0u;
+        uint32_t gwA = 0, gwB = 0;
+        uint4 rcA = make_uint4(0u, 0u, 0u, 0u);
+        if (hd.y > 0) {
+            gwA = lst[min(lane, last)];
+            const uint32_t* w = (const uint32_t*)(rd + (gwA & kDfGidMask));
+            rcA = make_uint4(w[3 * eye], w[3 * eye + 1], w[3 * eye + 2], w[6]);
+            gwB = lst[min(kDfEyeBatch + lane, last)];
+        }
         for (uint32_t b0 = 0; b0 < hd.y && !done; b0 += kDfEyeBatch) {
             const uint32_t n = min(kDfEyeBatch, hd.y - b0);
             if (topPrio) {
@@ -770,19 +784,25 @@ __global__ __launch_bounds__(NW * 64) void k_df_blend_eye(const uint32_t* __rest
                 else if (b0 == 128u) __builtin_amdgcn_s_setprio(2);
                 else if (b0 == 320u && !split) __builtin_amdgcn_s_setprio(3);
             }
-            // the batch's entries not flagged for this eye (k_df_flags), compacted in list order (the
+            // the batch's entries not flagged for this eye (k_df_expand), compacted in list order (the
             // flagged ones are identity steps); padded with mean -inf to a multiple of 4
-            const uint32_t gw = lane < n ? gids[hd.x + b0 + lane] : 0u;
+            const uint32_t gw = gwA;
+            const uint4 rc = rcA;
             const bool keep = lane < n && !((gw >> (kDfSkipShift + eye)) & 1u);
             const uint64_t km = __builtin_amdgcn_ballot_w64(keep);
             const uint32_t nk = (uint32_t)__popcll(km);
+            // next batch's records, and the ids of the one after
+            {
+                const uint32_t* w = (const uint32_t*)(rd + (gwB & kDfGidMask));
+                rcA = make_uint4(w[3 * eye], w[3 * eye + 1], w[3 * eye + 2], w[6]);
+                gwA = gwB;
+                gwB = lst[min(b0 + 2u * kDfEyeBatch + lane, last)];
+            }
             if (keep) {
                 const uint32_t pos = __builtin_amdgcn_mbcnt_hi((uint32_t)(km >> 32),
                                                                __builtin_amdgcn_mbcnt_lo((uint32_t)km, 0u));
-                const uint32_t* w = (const uint32_t*)(rd + (gw & kDfGidMask));
-                const uint32_t mean = w[3 * eye], cc = w[3 * eye + 1], cxy = w[3 * eye + 2] & 0xFFFFu;
-                const uint32_t c = w[6];  // colorR, G, B, opacity (bytes 24..27)
-                sA[pos] = make_uint4(mean, cc, cxy | ((uint32_t)div255[c >> 24] << 16),
+                const uint32_t c = rc.w;  // colorR, G, B, opacity (bytes 24..27)
+                sA[pos] = make_uint4(rc.x, rc.y, (rc.z & 0xFFFFu) | ((uint32_t)div255[c >> 24] << 16),
                                      (uint32_t)div255[c & 0xFFu] | ((uint32_t)div255[(c >> 8) & 0xFFu] << 16));
                 sB[pos] = (uint32_t)div255[(c >> 16) & 0xFFu];
             }

@@ -316,3 +316,21 @@ def test_df_config5_full_size(gsm, cuda, oracle):
     assert r["overflow"] == 0
     assert_df_equal(g, r)
     g["renderer"].close()
+
+
+@pytest.mark.gpu
+def test_df_wide_frame_and_schedule_independence(gsm, cuda, oracle):
+    """Per-eye width 2100 (> 2048: fp16 pixel coordinates round, the blend's skip test must stand
+    aside there) and three frames on one handle: the unit order of frames 2 and 3 comes from the
+    previous frame's walk costs, the image must not change."""
+    from gsm_amd import scenes
+    n, w, h = 20000, 2100, 96
+    world, harm = _scene(n, w, h, 4, 1, 17, spread=0.9)
+    L, R = scenes.make_camera(w, h, -0.032), scenes.make_camera(w, h, 0.032)
+    r = oracle.df_render_stereo(world, harm, 4, L, R, w, h)
+    g = gpu_df(gsm, cuda, world, harm, 4, L, R, w, h)
+    assert_df_equal(g, r)
+    for _ in range(2):
+        g2 = gpu_df(gsm, cuda, world, harm, 4, L, R, w, h, renderer=g["renderer"])
+        assert np.array_equal(g2["color"], r["color"]), first_diff(g2["color"], r["color"])
+    g["renderer"].close()

@@ -573,7 +573,9 @@ __global__ __launch_bounds__(NT) void k_blend_px(
             t[0] = tStart;
             t[1] = __builtin_amdgcn_s_memrealtime();
             t[2] = ((unsigned long long)count << 32) | nproc;
-            t[3] = ((unsigned long long)ncomp << 32) | (unsigned long long)__builtin_amdgcn_s_getreg(4 | (31 << 11));
+            const unsigned long long xcc = (unsigned long long)__builtin_amdgcn_s_getreg(20 | (3 << 11));  // XCC_ID
+            t[3] = (xcc << 48) | ((unsigned long long)(ncomp & 0xFFFFu) << 32) |
+                   (unsigned long long)__builtin_amdgcn_s_getreg(4 | (31 << 11));
         }
         if (agePrio || topPrio) __builtin_amdgcn_s_setprio(0);
         topPrio = false;

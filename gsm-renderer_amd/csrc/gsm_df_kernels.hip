@@ -260,76 +260,16 @@ __global__ __launch_bounds__(kDfBlock) void k_df_icount(const TileAssignmentHead
     if (threadIdx.x == 0) sums[blockIdx.x] = s;
 }
 
-// Tile-level skip test of the blend's staging: eye e of an entry provably contributes nothing to
-// the unit's tile (x0, y0).  The blend evaluates, per pixel, the fp16 form
-// p = fl(fl(fl(fl(dx*dx)*cxx) + fl(fl(dy*dy)*cyy)) + fl(fl(dx*dy)*cxy2)) with dx = fl(px - mx), and an
-// eye's alpha is 0 exactly when p is in (9, +inf] (stereo_exp_table_entry).  With Q the same form in
-// real arithmetic on the same fp16 inputs, a = cxx dx^2, b = cyy dy^2 and rho = |cxy2| / (2 sqrt(cxx cyy)):
-// every product and sum above rounds once with relative error <= u = 2^-11 while nothing overflows, so
-// p >= (1 - u) (Q - 9.02 u (a + b)), and |c| <= rho (a + b), Q >= (1 - rho)(a + b) give
-// p >= (1 - u) Q (1 - 9.02 u / (1 - rho)).  The entry is skipped only when that bound exceeds 9 for the
-// minimum of Q over the tile's pixel rectangle (continuous, so it bounds every pixel), with
-// rho <= 15/16, |dx|, |dy| <= 200 and a + b <= 16000 over the tile (no fp16 overflow, no NaN), pixel
-// coordinates below 2048 (exact in fp16) and finite positive cxx, cyy.  Such an entry is an identity
-// step of the blend for that eye (C + c * (0 * T) = C, T * (1 - 0) = T).
-// The per-gaussian part of the test, once per eye; the per-tile part in fp32 (every quantity is
-// bounded, so fp32 evaluation errors stay below 1e-6 relative, covered by the extra 1e-5 factor).
-// Divisions and square roots here use the hardware approximations (v_rcp_f32, v_rsq_f32, ~1 ulp):
-// they only move the edge minimiser t by ~1e-7 relative (Q rises by at most cyy * (2e-5)^2 there) and
-// rho by ~1e-6 (the factor by ~1.3e-6), both inside the 1e-3 absolute and 1e-5 relative slack.
-struct DfEyeSkip {
-    float mx, my, cxx, cyy, cxy, factor, hx, hy;  // hx = 1 / (2 cxx), hy = 1 / (2 cyy)
-    int mode;  // 0: test per tile, 1: always skip (the eye's mean test fails), 2: never skip
-};
+// DepthFirst skip flags: eye e of an entry provably contributes nothing to the 16x16 tile (x0, y0)
+// -- every pixel has p in (9, +inf], where the stereo alpha is 0 (stereo_exp_table_entry), so the
+// entry is an identity step of the blend for that eye (C + c * (0 * T) = C, T * (1 - 0) = T).  The
+// rounding-error bound is quad_exceeds' (gsm_device.h).
+typedef QuadBound DfEyeSkip;
 __device__ __forceinline__ DfEyeSkip df_eye_skip_setup(uint32_t meanW, uint32_t ccW, uint32_t cxyW) {
-    DfEyeSkip e;
-    e.mx = hbits_to_f((uint16_t)(meanW & 0xFFFFu));
-    e.my = hbits_to_f((uint16_t)(meanW >> 16));
-    e.cxx = hbits_to_f((uint16_t)(ccW & 0xFFFFu));
-    e.cyy = hbits_to_f((uint16_t)(ccW >> 16));
-    e.cxy = hbits_to_f((uint16_t)(cxyW & 0xFFFFu));
-    e.factor = 0.0f;
-    e.mode = 2;
-    if (!(e.mx >= -60000.0f)) {  // the blend's mean test skips this eye anyway
-        e.mode = 1;
-        return e;
-    }
-    if (!(e.cxx > 0.0f && e.cyy > 0.0f && e.cxx < 65504.0f && e.cyy < 65504.0f && __builtin_fabsf(e.cxy) < 65504.0f &&
-          __builtin_fabsf(e.my) < 65504.0f))
-        return e;
-    const float rho = 0.5f * __builtin_fabsf(e.cxy) * __builtin_amdgcn_rsqf(e.cxx * e.cyy);
-    if (!(rho <= 15.0f / 16.0f)) return e;
-    const float u = 1.0f / 2048.0f;
-    e.factor = (1.0f - u) * (1.0f - 10.0f * u * __builtin_amdgcn_rcpf(1.0f - rho)) * (1.0f - 1e-5f);
-    e.hx = __builtin_amdgcn_rcpf(2.0f * e.cxx);
-    e.hy = __builtin_amdgcn_rcpf(2.0f * e.cyy);
-    e.mode = 0;
-    return e;
+    return quad_bound_setup(meanW, ccW, cxyW, true);
 }
 __device__ __forceinline__ bool df_eye_misses_tile(const DfEyeSkip& e, int x0, int y0) {
-    if (e.mode != 0) return e.mode == 1;
-    if (x0 + 15 >= 2048 || y0 + 15 >= 2048) return false;
-    const float dx0 = (float)x0 - e.mx, dx1 = dx0 + 15.0f;
-    const float dy0 = (float)y0 - e.my, dy1 = dy0 + 15.0f;
-    if (!(__builtin_fabsf(dx0) <= 200.0f && __builtin_fabsf(dx1) <= 200.0f && __builtin_fabsf(dy0) <= 200.0f &&
-          __builtin_fabsf(dy1) <= 200.0f))
-        return false;
-    if (dx0 <= 0.0f && dx1 >= 0.0f && dy0 <= 0.0f && dy1 >= 0.0f) return false;  // the mean is inside: Q min = 0
-    const float ax = __builtin_fmaxf(dx0 * dx0, dx1 * dx1), ay = __builtin_fmaxf(dy0 * dy0, dy1 * dy1);
-    if (!(e.cxx * ax + e.cyy * ay <= 16000.0f)) return false;
-    // min of Q over the rectangle: on its boundary (Q is convex with its minimum at the mean, outside)
-    auto q = [&](float dx, float dy) { return e.cxx * dx * dx + e.cyy * dy * dy + e.cxy * dx * dy; };
-    auto along_y = [&](float X) {  // edge dx = X: minimise over dy in [dy0, dy1]
-        const float t = __builtin_fminf(__builtin_fmaxf(-e.cxy * X * e.hy, dy0), dy1);
-        return q(X, t);
-    };
-    auto along_x = [&](float Y) {
-        const float t = __builtin_fminf(__builtin_fmaxf(-e.cxy * Y * e.hx, dx0), dx1);
-        return q(t, Y);
-    };
-    const float qmin = __builtin_fminf(__builtin_fminf(along_y(dx0), along_y(dx1)),
-                                       __builtin_fminf(along_x(dy0), along_x(dy1)));
-    return qmin * e.factor > 9.0f + 1e-3f;
+    return quad_exceeds(e, x0, y0, (int)kDfTile - 1, (int)kDfTile - 1, 9.0f);
 }
 
 __global__ __launch_bounds__(kDfBlock) void k_df_instances(const TileAssignmentHeader* __restrict__ visHdr,

@@ -178,16 +178,16 @@ gsm_status gsm_sort_pairs_u32(void* keys, void* values, uint32_t n, uint32_t key
     if (n == 0) return GSM_OK;
     if (key_bits == 0 || key_bits > 32) key_bits = 32;
     hipStream_t s = (hipStream_t)stream;
-    const uint32_t grid = gsm::radix_grid_for_capacity(n);
     uint32_t *k2 = nullptr, *v2 = nullptr, *hist = nullptr, *bins = nullptr, *np = nullptr;
     gsm_status st = GSM_OK;
     if (hipMalloc(&k2, (size_t)n * 4) != hipSuccess || hipMalloc(&v2, (size_t)n * 4) != hipSuccess ||
-        hipMalloc(&hist, (size_t)256 * grid * 4) != hipSuccess || hipMalloc(&bins, 256 * 4) != hipSuccess ||
+        hipMalloc(&hist, gsm::radix_workspace_bytes(n)) != hipSuccess || hipMalloc(&bins, 256 * 4) != hipSuccess ||
         hipMalloc(&np, 4) != hipSuccess) {
         st = GSM_ERR_FAILED_TO_ALLOCATE_BUFFER;
     }
     if (st == GSM_OK) {
         hipMemcpyAsync(np, &n, 4, hipMemcpyHostToDevice, s);
+        hipMemsetAsync(hist, 0, gsm::radix_workspace_bytes(n), s);
         uint32_t* kb[2] = {(uint32_t*)keys, k2};
         uint32_t* vb[2] = {(uint32_t*)values, v2};
         const int digits = (int)((key_bits + 7) / 8);

@@ -125,7 +125,6 @@ gsm_status DepthFirstRenderer::create(const gsm_renderer_config& cfg, int hipDev
     r->numCUs_ = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
     const size_t G = r->maxGaussians_, cap = r->maxInstances_;
     const size_t nb = (G + kDfBlock - 1) / kDfBlock;
-    const uint32_t rgrid = radix_grid_for_capacity(r->maxInstances_);
     DfArena& A = r->A_;
     gsm_status st = GSM_OK;
 #define GSM_DF_ALLOC(ptr, bytes) \
@@ -146,7 +145,10 @@ gsm_status DepthFirstRenderer::create(const gsm_renderer_config& cfg, int hipDev
         GSM_DF_ALLOC(A.ikeys[i], cap * 4);
         GSM_DF_ALLOC(A.ivals[i], cap * 4);
     }
-    GSM_DF_ALLOC(A.radixHist, (size_t)256 * rgrid * 4);
+    GSM_DF_ALLOC(A.radixHist, radix_workspace_bytes(r->maxInstances_ > r->maxGaussians_ ? r->maxInstances_ : r->maxGaussians_));
+    if (st == GSM_OK &&
+        hipMemset(A.radixHist, 0, radix_workspace_bytes(r->maxInstances_ > r->maxGaussians_ ? r->maxInstances_ : r->maxGaussians_)) != hipSuccess)
+        st = GSM_ERR_FAILED_TO_ALLOCATE_BUFFER;
     GSM_DF_ALLOC(A.radixBinTotals, 256 * 4);
     GSM_DF_ALLOC(A.starts, ((size_t)r->maxTiles_ + 1) * sizeof(uint32_t));
     GSM_DF_ALLOC(A.queue, 4);

@@ -122,6 +122,8 @@ int radix_sort_pairs(uint32_t* keys[2], uint32_t* vals[2], const uint32_t* nPtr,
 int radix_sort_bits(uint32_t* keys[2], uint32_t* vals[2], const uint32_t* nPtr, uint32_t capacity,
                     uint32_t shift, uint32_t bits, uint32_t* hist, uint32_t* binTotals, hipStream_t stream);
 uint32_t radix_grid_for_capacity(uint32_t capacity);
+// bytes of the sort workspace (`hist` argument above) for a capacity; zero it once at allocation
+size_t radix_workspace_bytes(uint32_t capacity);
 // stable per-tile sort by the 16-bit depth key of runs already grouped by tile (one wave per tile)
 void tile_depth_sort(uint32_t* keysIn, uint32_t* valsIn, uint32_t* keysOut, uint32_t* valsOut,
                      const uint32_t* tileStart, uint32_t tileBegin, uint32_t numTiles, hipStream_t stream);

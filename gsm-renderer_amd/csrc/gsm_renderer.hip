@@ -98,7 +98,6 @@ gsm_status GlobalRenderer::create(const gsm_renderer_config& cfg, int hipDevice,
     const size_t G = r->maxGaussians_;
     const size_t cap = r->maxAssignments_;
     const size_t nb = (G + kProjectBlock - 1) / kProjectBlock;
-    const uint32_t rgrid = radix_grid_for_capacity(r->maxAssignments_);
     DeviceArena& A = r->arena_;
     gsm_status st = GSM_OK;
 #define GSM_ALLOC(ptr, bytes)                                              \
@@ -117,7 +116,9 @@ gsm_status GlobalRenderer::create(const gsm_renderer_config& cfg, int hipDevice,
     GSM_ALLOC(A.keys[1], cap * sizeof(uint32_t));
     GSM_ALLOC(A.vals[0], cap * sizeof(uint32_t));
     GSM_ALLOC(A.vals[1], cap * sizeof(uint32_t));
-    GSM_ALLOC(A.radixHist, (size_t)256 * rgrid * sizeof(uint32_t));
+    GSM_ALLOC(A.radixHist, radix_workspace_bytes(r->maxAssignments_));
+    if (st == GSM_OK && hipMemset(A.radixHist, 0, radix_workspace_bytes(r->maxAssignments_)) != hipSuccess)
+        st = GSM_ERR_FAILED_TO_ALLOCATE_BUFFER;
     GSM_ALLOC(A.radixBinTotals, 256 * sizeof(uint32_t));
     GSM_ALLOC(A.tileStart, ((size_t)r->tileCount_ + 1) * sizeof(uint32_t));
     GSM_ALLOC(A.tileQueue, sizeof(uint32_t));

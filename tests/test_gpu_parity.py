@@ -155,6 +155,23 @@ def test_radix_sort_random_large(gsm, cuda):
         np.testing.assert_array_equal(v.cpu().numpy(), np.argsort(keys, kind="stable"))
 
 
+@pytest.mark.parametrize("variant", ["onesweep", "classic"])
+def test_radix_sort_variants(gsm, cuda, variant, monkeypatch):
+    """Both radix schedules (GSM_RADIX, read per sort) give the stable order: the opt-in onesweep
+    passes with decoupled look-back and the default upsweep / scan / downsweep."""
+    monkeypatch.setenv("GSM_RADIX", variant)
+    rng = np.random.default_rng(11)
+    for n, bits in [(5, 32), (4096, 12), (4097, 32), (1_000_003, 32), (2_500_000, 14)]:
+        keys = rng.integers(0, 2 ** bits, n, dtype=np.uint64).astype(np.uint32)
+        keys[: n // 4] = keys[-1]
+        for _ in range(2):  # a second sort reuses nothing stale from the first
+            k = cuda.from_numpy(keys.view(np.int32).copy()).cuda()
+            v = cuda.arange(n, dtype=cuda.int32, device="cuda")
+            gsm.sort_pairs_u32(k, v, key_bits=bits)
+            np.testing.assert_array_equal(k.cpu().numpy().view(np.uint32), np.sort(keys, kind="stable"))
+            np.testing.assert_array_equal(v.cpu().numpy(), np.argsort(keys, kind="stable"))
+
+
 def _synth(n, w, h, sh, prec, seed, **kw):
     from gsm_amd import scenes
     world, harm, cam = scenes.gen_scene(n, w, h, sh, prec, seed=seed, **kw)

@@ -32,6 +32,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "gsm-renderer_amd"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec); measured copy ceiling ~6290
+BLEND_EVENT_PERIOD = 5  # timed frames per bracketed blend (HIP events), see the timed loop
 VALU_PEAK_GIPS = 1024 * 2.4 / 4  # wave64 packed-fp16 VALU instructions per ns, whole chip
 
 
@@ -147,8 +148,9 @@ def main():
     for _ in range(args.warmup):
         step()
     # timed region: only the blend (the roofline kernel) is bracketed by HIP events on the render
-    # stream -- two events per frame; the per-stage breakdown comes from a separate pass below
-    renderer.set_profiling(stage_events=False, blend_events=True)
+    # stream -- two events on every BLEND_EVENT_PERIOD-th frame (each bracketed frame costs ~10 us
+    # of event overhead, tools/exp_events.py); the per-stage breakdown comes from a separate pass below
+    renderer.set_profiling(stage_events=False, blend_events=True, blend_event_period=BLEND_EVENT_PERIOD)
     torch.cuda.synchronize()
     if world_size > 1:
         dist.barrier()
@@ -250,7 +252,7 @@ def main():
                                   if world_size > 1 else "single GPU"},
         "roofline": {"bound": "hbm", "kernel": "k_blend", "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "algorithmic_bytes": b_blend, "avg_launch_ms": blend_ms_timed,
+                     "algorithmic_bytes": b_blend, "launch_timing": f"HIP events around the blend on every {BLEND_EVENT_PERIOD}th frame of the timed region", "avg_launch_ms": blend_ms_timed,
                      "note": "blend is VALU/LDS-bound (fp16 math per pixel per entry); HBM fraction "
                              "reported per the metric"},
         # the blend's real bound: packed-fp16 VALU issue.  Peak = 1024 SIMDs x one wave64
@@ -296,7 +298,7 @@ def run_depthfirst(args, c, world_np, harm_np, world, harm, dev):
 
     for _ in range(args.warmup):
         step()
-    renderer.set_profiling(stage_events=False, blend_events=True)
+    renderer.set_profiling(stage_events=False, blend_events=True, blend_event_period=BLEND_EVENT_PERIOD)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -366,7 +368,7 @@ def run_depthfirst(args, c, world_np, harm_np, world, harm, dev):
                    "parallelism": "single GPU"},
         "roofline": {"bound": "hbm", "kernel": "k_df_blend_eye", "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "algorithmic_bytes": b_blend, "avg_launch_ms": blend_ms_timed,
+                     "algorithmic_bytes": b_blend, "launch_timing": f"HIP events around the blend on every {BLEND_EVENT_PERIOD}th frame of the timed region", "avg_launch_ms": blend_ms_timed,
                      "note": "blend is VALU/LDS-bound (fp16 math per pixel per (tile, eye) unit)"},
         "roofline_valu": ({"bound": "valu", "kernel": "k_df_blend_eye", "unit": "G wave-instr/s",
                            "achieved": valu_insts / t_blend / 1e9, "peak": VALU_PEAK_GIPS,

@@ -58,6 +58,7 @@ class DepthFirstRenderer {
     static constexpr int kRing = 64;
     std::vector<hipEvent_t> events_;  // [kRing][GSM_DF_STAGE_COUNT + 1]
     uint32_t profFrames_ = 0;
+    uint32_t sampleFrame_ = 0;  // frames since setProfiling (blend-event sampling)
     int profiling_ = 0;
     hipEvent_t* frameEvents(uint32_t f) { return &events_[(f % kRing) * (GSM_DF_STAGE_COUNT + 1)]; }
 };
@@ -260,7 +261,9 @@ gsm_status DepthFirstRenderer::renderStereoSbs(hipStream_t s, const gsm_gaussian
         hipEventRecord(evOrder_, side_);
     }
     const bool prof = (profiling_ & 1) != 0;                   // every stage bracketed
-    const bool blendOnly = !prof && (profiling_ & 8) != 0;      // only the blend's pair of events
+    // only the blend's pair of events, on every frame or every period-th (bits 8-15)
+    const uint32_t period = ((uint32_t)profiling_ >> 8) & 0xFFu;
+    const bool blendOnly = !prof && (profiling_ & 8) != 0 && (period <= 1 || (sampleFrame_++ % period) == 0);
     hipEvent_t* ev = (prof || blendOnly) ? frameEvents(profFrames_) : nullptr;
     if (prof) hipEventRecord(ev[0], s);
     df_launch_project(half, deg, in.gaussians, in.harmonics, a, A_, s);
@@ -390,6 +393,7 @@ gsm_status DepthFirstRenderer::setProfiling(int flags) {
     }
     profiling_ = flags;
     profFrames_ = 0;
+    sampleFrame_ = 0;
     return GSM_OK;
 }
 

@@ -310,7 +310,9 @@ gsm_status GlobalRenderer::runFrame(hipStream_t s, const ProjectArgs& a, uint32_
                                     void* color, size_t colorPitch, void* depth, size_t depthPitch,
                                     Front&& front) {
     const bool prof = (profiling_ & 1) != 0;         // every stage bracketed by events
-    const bool blendOnly = !prof && (profiling_ & 8) != 0;  // only the blend (2 events per frame)
+    // only the blend (2 events per frame), on every frame or every period-th (bits 8-15)
+    const uint32_t period = ((uint32_t)profiling_ >> 8) & 0xFFu;
+    const bool blendOnly = !prof && (profiling_ & 8) != 0 && (period <= 1 || (sampleFrame_++ % period) == 0);
     const bool keep = (profiling_ & 2) != 0;
     const uint32_t nb = (a.count + kProjectBlock - 1) / kProjectBlock;
     lastCount_ = a.count;
@@ -546,6 +548,7 @@ gsm_status GlobalRenderer::setProfiling(int flags) {
     }
     profiling_ = flags;
     profFrames_ = 0;  // restart the averaging window
+    sampleFrame_ = 0;
     haveTimes_ = false;
     return GSM_OK;
 }

@@ -389,9 +389,10 @@ class GlobalRenderer:
 
     # -- introspection (include/gsm_debug.h) --
     def set_profiling(self, stage_events: bool = True, keep_unsorted: bool = False,
-                      blend_trace: bool = False, blend_events: bool = False):
+                      blend_trace: bool = False, blend_events: bool = False, blend_event_period: int = 1):
+        """blend_event_period > 1: with blend_events, bracket the blend on every period-th frame only."""
         flags = (1 if stage_events else 0) | (2 if keep_unsorted else 0) | (4 if blend_trace else 0) | \
-            (8 if blend_events else 0)
+            (8 if blend_events else 0) | ((max(1, min(255, int(blend_event_period))) & 0xFF) << 8)
         _check(_lib().gsm_global_set_profiling(self._h, flags), "gsm_global_set_profiling")
 
     def stage_times_ms(self) -> dict:
@@ -507,8 +508,10 @@ class DepthFirstRenderer:
         st = _lib().gsm_depthfirst_last_gpu_time(self._h, C.byref(s))
         return float(s.value) if st == 0 else None
 
-    def set_profiling(self, stage_events: bool = True, blend_events: bool = False, blend_stats: bool = False):
-        flags = (1 if stage_events else 0) | (2 if blend_stats else 0) | (8 if blend_events else 0)
+    def set_profiling(self, stage_events: bool = True, blend_events: bool = False, blend_stats: bool = False,
+                      blend_event_period: int = 1):
+        flags = (1 if stage_events else 0) | (2 if blend_stats else 0) | (8 if blend_events else 0) | \
+            ((max(1, min(255, int(blend_event_period))) & 0xFF) << 8)
         _check(_lib().gsm_depthfirst_set_profiling(self._h, flags), "set_profiling")
 
     def stage_times_ms(self) -> dict:

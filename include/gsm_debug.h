@@ -49,7 +49,9 @@ gsm_status gsm_global_debug_copy(gsm_renderer *renderer, int which, void *host_d
 /* `enable` is a bit set: bit 0 brackets every stage by HIP events on the frame's stream,
  * bit 1 keeps the unsorted keys (GSM_BUF_KEYS/VALUES) for readback, bit 2 records a
  * per-unit blend trace (GSM_BUF_BLEND_TRACE), bit 3 (without bit 0) brackets only the blend
- * (two events per frame; the other stages then report 0).  Every event costs frame time. */
+ * (two events per frame; the other stages then report 0); bits 8-15, with bit 3: a period P > 1
+ * brackets the blend on every P-th frame only (the average is over the bracketed frames).
+ * Every event costs frame time (~10 us per bracketed frame at config 2). */
 gsm_status gsm_global_set_profiling(gsm_renderer *renderer, int enable);
 
 enum {

@@ -82,7 +82,7 @@ gsm_status gsm_depthfirst_debug_copy(gsm_depthfirst *renderer, int which, void *
                                      size_t *needed);
 /* bit 0: bracket every stage with HIP events (GSM_DF_STAGE_*); bit 1: count the blend's walk
  * (GSM_DF_BUF_BLEND_STATS); bit 3: only the blend (two events per frame, for timing the blend
- * inside a timed loop). */
+ * inside a timed loop); bits 8-15 with bit 3: a period P > 1 brackets every P-th frame only. */
 gsm_status gsm_depthfirst_set_profiling(gsm_depthfirst *renderer, int enable);
 typedef enum {
     GSM_DF_STAGE_PROJECT = 0, /* project both eyes + visibility compaction */

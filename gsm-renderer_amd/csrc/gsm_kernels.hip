@@ -461,40 +461,72 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_blocks(uint32_t* __restri
 // 3. duplicate with keys (tileScatterIndirectKernel GlobalShaders.metal:623-678 +
 //    computeSortKeysKernel :266-295): key = tile<<16 | (fp16 depth ^ 0x8000), value = gid
 // ---------------------------------------------------------------------------
+// Small rects (<= kMaskTiles tiles, the projection's answer mask) are written cooperatively: the
+// block's slots [0, total) are handed out to consecutive threads, each finding its gaussian by a
+// binary search over the block's exclusive offsets in LDS and its tile as the k-th set bit of the
+// mask -- consecutive threads write consecutive keys (coalesced) and a gaussian with many tiles
+// no longer serialises its wave.  Large rects keep one thread looping over their rect.  Slot
+// order is the reference's (ascending gid, then ty-major, tx-minor).
 __global__ __launch_bounds__(kProjectBlock) void k_scatter(
     ProjectArgs P, const GaussianRenderData* __restrict__ rd, const short4* __restrict__ bounds,
     const uint32_t* __restrict__ counts, const uint32_t* __restrict__ masks,
     const uint32_t* __restrict__ blockOffsets, uint32_t* __restrict__ keys, uint32_t* __restrict__ vals,
     const float2* __restrict__ sincos) {
     __shared__ uint32_t lds[kProjectBlock / 64];
+    __shared__ uint32_t sOff[kProjectBlock];
+    __shared__ uint32_t sMask[kProjectBlock];  // 0: no cooperative slots (large rect or no tiles)
+    __shared__ uint32_t sRect[kProjectBlock];  // x0 | rw << 16 (rw <= 32)
+    __shared__ int sTy0[kProjectBlock];
+    __shared__ uint32_t sD[kProjectBlock];     // depth bits of the key
     const uint32_t gid = blockIdx.x * kProjectBlock + threadIdx.x;
     uint32_t c = (gid < P.count) ? counts[gid] : 0u;
     uint32_t total;
-    uint32_t off = block_exclusive_scan<kProjectBlock>(c, lds, &total);
-    if (c == 0) return;
-    uint64_t wp = (uint64_t)blockOffsets[blockIdx.x] + off;
-    if (wp >= P.maxAssignments) return;
-    const short4 r = bounds[gid];
-    const uint32_t rdz = ((const uint4*)(rd + gid))->z;
-    const uint32_t dbits = ((rdz >> 16) ^ 0x8000u) & 0xFFFFu;
-    const int ty0 = max((int)r.z, (int)P.rowBegin), ty1 = min((int)r.w, (int)P.rowEnd - 1);
-    const int rw = (int)r.y - (int)r.x + 1;
-    if ((ty1 - ty0 + 1) * rw <= kMaskTiles) {
-        // the projection's answers, in its scan order (ty-major, tx-minor)
-        uint32_t mask = masks[gid];
-        uint32_t bit = 0;
-        for (int ty = ty0; ty <= ty1 && mask; ++ty)
-            for (int tx = (int)r.x; tx <= (int)r.y; ++tx, ++bit)
-                if ((mask >> bit) & 1u) {
-                    mask &= ~(1u << bit);
-                    if (wp < P.maxAssignments) {
-                        keys[wp] = ((uint32_t)(ty * (int)P.bin.tilesX + tx) << 16) | dbits;
-                        vals[wp] = gid;
-                        wp++;
-                    }
-                }
-        return;
+    const uint32_t off = block_exclusive_scan<kProjectBlock>(c, lds, &total);
+    const uint32_t base = blockOffsets[blockIdx.x];
+    bool large = false;
+    short4 r = make_short4(0, -1, 0, -1);
+    uint32_t dbits = 0;
+    int ty0 = 0, ty1 = -1;
+    uint32_t mask = 0;
+    if (c != 0) {
+        r = bounds[gid];
+        const uint32_t rdz = ((const uint4*)(rd + gid))->z;
+        dbits = ((rdz >> 16) ^ 0x8000u) & 0xFFFFu;
+        ty0 = max((int)r.z, (int)P.rowBegin);
+        ty1 = min((int)r.w, (int)P.rowEnd - 1);
+        const int rw = (int)r.y - (int)r.x + 1;
+        large = (ty1 - ty0 + 1) * rw > kMaskTiles;
+        if (!large) mask = masks[gid];
+        sRect[threadIdx.x] = ((uint32_t)(int)r.x & 0xFFFFu) | ((uint32_t)rw << 16);
     }
+    sOff[threadIdx.x] = off;
+    sMask[threadIdx.x] = mask;
+    sD[threadIdx.x] = dbits;
+    sTy0[threadIdx.x] = ty0;
+    __syncthreads();
+    for (uint32_t sl = threadIdx.x; sl < total; sl += kProjectBlock) {
+        // owner: the largest g with sOff[g] <= sl (zero-count gaussians share the next offset)
+        uint32_t lo = 0, hi = kProjectBlock - 1;
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi + 1) >> 1;
+            if (sOff[mid] <= sl) lo = mid;
+            else hi = mid - 1;
+        }
+        uint32_t m = sMask[lo];
+        if (m == 0) continue;  // a large rect: its own thread writes it
+        const uint64_t wp = (uint64_t)base + sl;
+        if (wp >= P.maxAssignments) continue;
+        for (uint32_t k = sl - sOff[lo]; k > 0; --k) m &= m - 1u;
+        const uint32_t bit = (uint32_t)__builtin_ctz(m);
+        const uint32_t rect = sRect[lo];
+        const uint32_t rwo = rect >> 16;
+        const int ty = sTy0[lo] + (int)(bit / rwo), tx = (int)(rect & 0xFFFFu) + (int)(bit % rwo);
+        keys[wp] = ((uint32_t)(ty * (int)P.bin.tilesX + tx) << 16) | sD[lo];
+        vals[wp] = blockIdx.x * kProjectBlock + lo;
+    }
+    if (!large) return;
+    uint64_t wp = (uint64_t)base + off;
+    if (wp >= P.maxAssignments) return;
     // large rects: repeat the tests (tileScatterIndirectKernel, GlobalShaders.metal:623-678)
     uint4 rdw = *(const uint4*)(rd + gid);
     uint16_t hmx = (uint16_t)(rdw.x & 0xFFFFu), hmy = (uint16_t)(rdw.x >> 16);

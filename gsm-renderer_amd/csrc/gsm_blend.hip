@@ -93,6 +93,20 @@ __global__ __launch_bounds__(NT) void k_blend_px(
     __shared__ uint32_t cscr[NW][16];  // compaction: the alive groups of each wave, in order
     __shared__ __attribute__((aligned(16))) uint4 lrecA[kLdsRecords ? NW : 1][64];  // current batch records
     __shared__ uint32_t lrecB[kLdsRecords ? NW : 1][64];
+    // flags bits 8-30: this frame's unit-order epoch when the launch did not join the ordering
+    // stream; one acquire per workgroup (before the table load) -- if the order is incomplete the
+    // workgroup walks index order and leaves the costs alone (k_unit_order may still read them)
+    __shared__ uint32_t sOrderOk;
+    if (((uint32_t)flags >> 8) != 0u) {
+        if (threadIdx.x == 0)
+            sOrderOk = order && __hip_atomic_load(&order[numTiles * UPT], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) ==
+                                    ((uint32_t)flags >> 8);
+        __syncthreads();
+        if (!sOrderOk) {
+            order = nullptr;
+            unitCost = nullptr;
+        }
+    }
     {
         const uint4* src = (const uint4*)expTable;
         uint4* dst = (uint4*)tbl;
@@ -567,7 +581,7 @@ __global__ __launch_bounds__(NT) void k_blend_px(
         for (int q = 0; q < P; ++q)
             write_pair(ux + offX[q], uy + offY[q], (count > 0) ? (ONE - T[q]) : ONE, R[q], G[q], B[q], D[q]);
     unit_end:
-        if (lane == 0) unitCost[u] = (uint16_t)min(nproc, 65535u);
+        if (unitCost && lane == 0) unitCost[u] = (uint16_t)min(nproc, 65535u);
         if (trace && lane == 0) {
             unsigned long long* t = trace + (size_t)u * 4;
             t[0] = tStart;
@@ -803,8 +817,10 @@ __device__ __forceinline__ uint64_t uo_match8(uint32_t d, bool valid) {
     return peers;
 }
 
+// order[n] <- epoch once the permutation is complete (release, device scope): a blend launched
+// without a stream join checks it and falls back to index order (k_blend_px).
 __global__ __launch_bounds__(1024) void k_unit_order(const uint16_t* __restrict__ cost,
-                                                     uint32_t* __restrict__ order, uint32_t n) {
+                                                     uint32_t* __restrict__ order, uint32_t n, uint32_t epoch) {
     __shared__ uint32_t wmax[kUoWaves];
     __shared__ uint32_t base[kUoBuckets];
     __shared__ uint32_t wcnt[kUoWaves][kUoBuckets];
@@ -851,7 +867,8 @@ __global__ __launch_bounds__(1024) void k_unit_order(const uint16_t* __restrict_
         if (valid) {
             uint32_t before = base[bk];
             for (uint32_t k = 0; k < w; ++k) before += wcnt[k][bk];
-            order[before + (uint32_t)__popcll(peers & lt)] = i;
+            const uint32_t pos = before + (uint32_t)__popcll(peers & lt);
+            if (pos < n) order[pos] = i;
         }
         __syncthreads();
         if (t < kUoBuckets) {
@@ -861,6 +878,9 @@ __global__ __launch_bounds__(1024) void k_unit_order(const uint16_t* __restrict_
         }
         __syncthreads();
     }
+    __threadfence();
+    __syncthreads();
+    if (t == 0) __hip_atomic_store(&order[n], epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 
@@ -896,17 +916,17 @@ bool blend_schedule_enabled(uint32_t numTiles, int numCUs) {
     return !(v && v[0] == '0');
 }
 
-void launch_unit_order(uint32_t numUnits, const DeviceArena& A, hipStream_t s) {
-    hipLaunchKernelGGL(k_unit_order, dim3(1), dim3(1024), 0, s, A.unitCost, A.unitOrder, numUnits);
+void launch_unit_order(uint32_t numUnits, const DeviceArena& A, hipStream_t s, uint32_t epoch) {
+    hipLaunchKernelGGL(k_unit_order, dim3(1), dim3(1024), 0, s, A.unitCost, A.unitOrder, numUnits, epoch);
 }
 
 void launch_unit_order_costs(const uint16_t* cost, uint32_t* order, uint32_t numUnits, hipStream_t s) {
-    hipLaunchKernelGGL(k_unit_order, dim3(1), dim3(1024), 0, s, cost, order, numUnits);
+    hipLaunchKernelGGL(k_unit_order, dim3(1), dim3(1024), 0, s, cost, order, numUnits, 0u);
 }
 
 void launch_blend(const uint32_t* sortedVals, const FrameGeometry& g, const DeviceArena& A, void* color,
                   size_t colorPitch, void* depth, size_t depthPitch, int numCUs, bool costOrder, int colorFormat,
-                  hipStream_t s) {
+                  hipStream_t s, uint32_t orderEpoch) {
     const uint32_t t0 = g.rowBegin * g.tilesX, t1 = g.rowEnd * g.tilesX;
     if (t1 <= t0) return;
     const uint32_t numTiles = t1 - t0;
@@ -917,7 +937,7 @@ void launch_blend(const uint32_t* sortedVals, const FrameGeometry& g, const Devi
     const char* pv = getenv("GSM_BLEND_PRIO");  // age-raised wave priority (default on)
     const char* sp = getenv("GSM_BLEND_SPLIT");  // long units on half the waves at top priority
     const int flags = vec | ((pv && pv[0] == '0') ? 0 : 2) | ((costOrder && !(sp && sp[0] == '0')) ? 4 : 0) |
-                      ((colorFormat & 15) << 4);
+                      ((colorFormat & 15) << 4) | (costOrder ? (int)((orderEpoch & 0x7FFFFFu) << 8) : 0);
     // A.tileQueue was zeroed by k_scan_blocks earlier in the frame
     const int P = blend_pairs_per_lane(numTiles, numCUs);
     const int waves = blend_waves_per_wg(numTiles, numCUs);

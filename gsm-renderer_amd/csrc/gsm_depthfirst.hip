@@ -155,7 +155,7 @@ gsm_status DepthFirstRenderer::create(const gsm_renderer_config& cfg, int hipDev
     GSM_DF_ALLOC(A.queue, 4);
     GSM_DF_ALLOC(A.expTable, 65536 * 2);
     GSM_DF_ALLOC(A.unitCost, (size_t)r->maxTiles_ * 2 * sizeof(uint16_t));
-    GSM_DF_ALLOC(A.unitOrder, (size_t)r->maxTiles_ * 2 * sizeof(uint32_t));
+    GSM_DF_ALLOC(A.unitOrder, ((size_t)r->maxTiles_ * 2 + 1) * sizeof(uint32_t));  // + the ready word
 #undef GSM_DF_ALLOC
     if (st != GSM_OK) {
         delete r;

@@ -100,10 +100,12 @@ void launch_headers(const uint32_t* sortedKeys, const FrameGeometry& geo, const 
 // front-to-back fp16 blend + clear (GlobalShaders.metal:140-154, 1030-1187)
 void launch_blend(const uint32_t* sortedVals, const FrameGeometry& geo, const DeviceArena& A,
                   void* color, size_t colorPitch, void* depth, size_t depthPitch, int numCUs,
-                  bool costOrder, int colorFormat, hipStream_t stream);
+                  bool costOrder, int colorFormat, hipStream_t stream, uint32_t orderEpoch = 0);
 // orders the blend units by the walk lengths the previous frame measured (longest first), so
 // the dynamic queue hands out long units before short ones
-void launch_unit_order(uint32_t numUnits, const DeviceArena& A, hipStream_t stream);
+// order[numUnits] <- epoch when done (A.unitOrder holds numUnits + 1 words); launch_blend with
+// the same nonzero epoch needs no stream join (workgroups fall back to index order)
+void launch_unit_order(uint32_t numUnits, const DeviceArena& A, hipStream_t stream, uint32_t epoch);
 // the same ordering for any cost array (the DepthFirst blend's (tile, eye) units)
 void launch_unit_order_costs(const uint16_t* cost, uint32_t* order, uint32_t numUnits, hipStream_t stream);
 // blend kernel shape: pixel pairs per lane (0 = quadrant kernel) and blend units per tile

@@ -123,7 +123,7 @@ gsm_status GlobalRenderer::create(const gsm_renderer_config& cfg, int hipDevice,
     GSM_ALLOC(A.tileStart, ((size_t)r->tileCount_ + 1) * sizeof(uint32_t));
     GSM_ALLOC(A.tileQueue, sizeof(uint32_t));
     GSM_ALLOC(A.unitCost, (size_t)r->tileCount_ * 4 * sizeof(uint16_t));
-    GSM_ALLOC(A.unitOrder, (size_t)r->tileCount_ * 4 * sizeof(uint32_t));
+    GSM_ALLOC(A.unitOrder, ((size_t)r->tileCount_ * 4 + 1) * sizeof(uint32_t));  // + the ready word
     GSM_ALLOC(A.expTable, 65536 * sizeof(uint16_t));
     GSM_ALLOC(A.sincosTable, 65536 * sizeof(float2));
 #undef GSM_ALLOC
@@ -337,11 +337,18 @@ gsm_status GlobalRenderer::runFrame(hipStream_t s, const ProjectArgs& a, uint32_
             hipEventCreateWithFlags(&evOrder_, hipEventDisableTiming) != hipSuccess)
             return GSM_ERR_ENCODER_CREATION_FAILED;
     }
+    // GSM_BLEND_JOIN=0: no join back -- the blend checks the order's ready word (epoch) and walks
+    // index order if the side stream has not finished (A/B; default: the stream join)
+    const char* jv = getenv("GSM_BLEND_JOIN");
+    const bool join = !(jv && jv[0] == '0');
+    uint32_t orderEpoch = 0;
     if (costOrder) {
+        orderEpoch_ = orderEpoch_ % 0x7FFFFFu + 1u;
+        orderEpoch = join ? 0u : orderEpoch_;
         hipEventRecord(evFrame_, s);  // after the previous frame's blend wrote the costs
         hipStreamWaitEvent(side_, evFrame_, 0);
-        launch_unit_order(units, arena_, side_);
-        hipEventRecord(evOrder_, side_);
+        launch_unit_order(units, arena_, side_, orderEpoch_);
+        if (join) hipEventRecord(evOrder_, side_);
     }
 
     hipEvent_t* ev = (prof || blendOnly) ? frameEvents(profFrames_) : nullptr;
@@ -394,10 +401,10 @@ gsm_status GlobalRenderer::runFrame(hipStream_t s, const ProjectArgs& a, uint32_
     if (prof) hipEventRecord(ev[4], s);
     if (fullRadix) launch_headers(sortedKeys_, g, arena_, s);  // else done inside the sort
     arena_.blendTrace = (profiling_ & 4) ? traceBuf_ : nullptr;
-    if (costOrder) hipStreamWaitEvent(s, evOrder_, 0);
+    if (costOrder && join) hipStreamWaitEvent(s, evOrder_, 0);
     if (prof || blendOnly) hipEventRecord(ev[5], s);
     launch_blend(sortedVals_, g, arena_, color, colorPitch, depth, depthPitch, numCUs_, costOrder,
-                 (int)config_.color_format, s);
+                 (int)config_.color_format, s, orderEpoch);
     if (prof || blendOnly) hipEventRecord(ev[6], s);
     if (prof || blendOnly) profFrames_++;
     haveTimes_ = profFrames_ > 0;

@@ -366,6 +366,21 @@ def test_stereo_is_unsupported_like_the_reference(gsm, cuda):
     rend.close()
 
 
+def test_join_free_schedule_frames_match(gsm, cuda, oracle, monkeypatch):
+    """GSM_BLEND_JOIN=0: the blend reads the unit order only once k_unit_order's ready word holds
+    this frame's epoch (index order otherwise); every frame stays bit-exact, whichever it took."""
+    monkeypatch.setenv("GSM_BLEND_JOIN", "0")
+    case = _synth(200_000, 1280, 720, 16, 1, 33)
+    r = oracle_render(oracle, case)
+    g = gpu_render(gsm, cuda, case, keep=False)
+    assert_frame_equal(g, r)
+    for _ in range(4):  # later frames take last frame's cost order
+        g2 = gpu_render(gsm, cuda, case, renderer=g["renderer"], keep=False)
+        assert np.array_equal(g["color"], g2["color"])
+        assert np.array_equal(g["depth"], g2["depth"])
+    g["renderer"].close()
+
+
 @pytest.mark.parametrize("cfg_name", ["cfg2_1m_sh3_1080p_f16"])
 def test_full_size_config_bit_exact(gsm, cuda, oracle, cfg_name):
     """BASELINE configs[1] (1M, SH3, 1920x1080, fp16) end to end against the oracle."""

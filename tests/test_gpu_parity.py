@@ -381,15 +381,26 @@ def test_join_free_schedule_frames_match(gsm, cuda, oracle, monkeypatch):
     g["renderer"].close()
 
 
-@pytest.mark.parametrize("cfg_name", ["cfg2_1m_sh3_1080p_f16"])
-def test_full_size_config_bit_exact(gsm, cuda, oracle, cfg_name):
-    """BASELINE configs[1] (1M, SH3, 1920x1080, fp16) end to end against the oracle."""
+@pytest.mark.parametrize("cfg_name,precision", [
+    ("cfg2_1m_sh3_1080p_f16", None),
+    # the same 1M / SH3 / 1080p frame from PackedWorldGaussian (48 B) + fp32 SH
+    # (globalProjectCullKernel, GlobalShaders.metal:127-131)
+    ("cfg2_1m_sh3_1080p_f16", 0),
+    # BASELINE configs[2]: 5M, SH3, 3840x2160 -- ~13M assignments, 2 x 7-bit tile passes, near the
+    # reference's 16.78M radix cap (GlobalShaders.metal:866-911), which this sort does not have
+    ("cfg3_5m_sh3_4k_f16", None),
+])
+def test_full_size_config_bit_exact(gsm, cuda, oracle, cfg_name, precision):
+    """BASELINE configs[1] and [2] end to end against the oracle, every intermediate bit for bit."""
     from gsm_amd import scenes
     c = scenes.CONFIGS[cfg_name]
-    case = _synth(c["count"], c["width"], c["height"], c["sh"], c["precision"], 42)
+    prec = c["precision"] if precision is None else precision
+    case = _synth(c["count"], c["width"], c["height"], c["sh"], prec, 42)
     r = oracle_render(oracle, case)
     g = gpu_render(gsm, cuda, case, keep=False)
     assert r["overflow"] == 0
+    if cfg_name.startswith("cfg3"):
+        assert 10_000_000 < r["total_assignments"] < 16_777_216
     assert_frame_equal(g, r)
     g["renderer"].close()
 

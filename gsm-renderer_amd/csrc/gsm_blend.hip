@@ -71,7 +71,7 @@ constexpr bool kBlendU4 = false;  // 4-entry groups at P = 2 (measured: no gain)
 // Records of the walk's current 64-entry batch staged in LDS and read back with uniform
 // addresses (one ds_read_b128 + one ds_read_b32 broadcast per entry) instead of 5 v_readlane.
 constexpr bool kLdsRecords = true;
-template <int NT, int P, bool EXECM, int EXPT = 0, bool COMPACT = false>
+template <int NT, int P, bool COMPACT = false>
 __global__ __launch_bounds__(NT) void k_blend_px(
     const uint32_t* __restrict__ tileStart, const uint32_t* __restrict__ sortedVals,
     const BlendRecordA* __restrict__ recA, const uint32_t* __restrict__ recB,
@@ -81,7 +81,7 @@ __global__ __launch_bounds__(NT) void k_blend_px(
     const uint32_t* __restrict__ order, uint16_t* __restrict__ unitCost,
     unsigned long long* __restrict__ trace) {
     static_assert(P == 1 || P == 2 || P == 4, "pairs per lane");
-    static_assert(!COMPACT || (P == 2 && EXECM), "compaction: half tiles, EXEC-masked updates");
+    static_assert(!COMPACT || P == 2, "compaction: half tiles");
     constexpr uint32_t U = (P == 2 && kBlendU4) ? 4 : 4 / P;  // entries per pipeline group
     constexpr uint32_t NG = 64 / U;      // groups per 64-entry batch
     constexpr uint32_t EXITG = 16 / U;   // exit test every 16 entries
@@ -93,20 +93,6 @@ __global__ __launch_bounds__(NT) void k_blend_px(
     __shared__ uint32_t cscr[NW][16];  // compaction: the alive groups of each wave, in order
     __shared__ __attribute__((aligned(16))) uint4 lrecA[kLdsRecords ? NW : 1][64];  // current batch records
     __shared__ uint32_t lrecB[kLdsRecords ? NW : 1][64];
-    // flags bits 8-30: this frame's unit-order epoch when the launch did not join the ordering
-    // stream; one acquire per workgroup (before the table load) -- if the order is incomplete the
-    // workgroup walks index order and leaves the costs alone (k_unit_order may still read them)
-    __shared__ uint32_t sOrderOk;
-    if (((uint32_t)flags >> 8) != 0u) {
-        if (threadIdx.x == 0)
-            sOrderOk = order && __hip_atomic_load(&order[numTiles * UPT], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) ==
-                                    ((uint32_t)flags >> 8);
-        __syncthreads();
-        if (!sOrderOk) {
-            order = nullptr;
-            unitCost = nullptr;
-        }
-    }
     {
         const uint4* src = (const uint4*)expTable;
         uint4* dst = (uint4*)tbl;
@@ -350,12 +336,8 @@ __global__ __launch_bounds__(NT) void k_blend_px(
                                 // raw table words: first used in stage 3, after the current
                                 // group's blend, so the LDS latency hides behind it
                                 const uint32_t pb = as_u32(pq[q]);
-                                if (EXPT == 1) {  // timing experiment: no table reads (wrong image)
-                                    en[k][q] = __builtin_bit_cast(u16x2, pb ^ 0x55555555u);
-                                } else {
-                                    en[k][q].x = tbl[pb & 0xFFFFu];
-                                    en[k][q].y = tbl[pb >> 16];
-                                }
+                                en[k][q].x = tbl[pb & 0xFFFFu];
+                                en[k][q].y = tbl[pb >> 16];
                             }
                         }
                     }
@@ -375,24 +357,11 @@ __global__ __launch_bounds__(NT) void k_blend_px(
                             const uint32_t o = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)gm, 0xB1, 0xF, 0xF, false);
                             gm = max(gm, o);
                         }
-                        alive = alive && (EXPT == 2 || !(gm < thrBits));  // T >= 0: fp16 order == bit order
+                        alive = alive && !(gm < thrBits);  // T >= 0: fp16 order == bit order
                         const h2 rgv = as_h2(rgc[k]), bdv = as_h2(bdc[k]);
                         // a dead lane keeps T and C (alpha 0 would give the same bits: C + c*0 == C,
-                        // T*1 == T): EXECM runs the updates under an EXEC mask of the live lanes,
-                        // otherwise w and T are selected per lane
-                        if (!EXECM) {
-#pragma unroll
-                            for (int q = 0; q < P; ++q) {
-                                const h2 Tn = T[q] * om[k][q];
-                                const h2 aT = ac[k][q] * T[q];  // (GlobalShaders.metal:1137-1149)
-                                const h2 w = alive ? aT : ZERO;
-                                T[q] = alive ? Tn : T[q];
-                                R[q] = R[q] + splat_lo(rgv) * w;
-                                G[q] = G[q] + splat_hi(rgv) * w;
-                                B[q] = B[q] + splat_lo(bdv) * w;
-                                D[q] = D[q] + splat_hi(bdv) * w;
-                            }
-                        } else if (alive) {
+                        // T*1 == T): the updates run under an EXEC mask of the live lanes
+                        if (alive) {
 #pragma unroll
                             for (int q = 0; q < P; ++q) {
                                 const h2 w = ac[k][q] * T[q];  // (GlobalShaders.metal:1137-1149)
@@ -598,205 +567,6 @@ __global__ __launch_bounds__(NT) void k_blend_px(
 }
 
 // ---------------------------------------------------------------------------
-// k_blend_lanes: group-granular blend.  The unit of work is one reference thread's 4x2 pixel
-// group (item = tile * 64 + group); a wave holds 32 of them, two lanes per group (one pixel
-// row each, two pixel pairs per lane).  Every group walks its tile's list only until its own
-// saturation break (GlobalShaders.metal:1086-1088), and the moment a group finishes its two
-// lanes take the next item, so no lane waits for a slower group of the same unit.  Records
-// are gathered per lane (no broadcast): entry cur's record and entry cur+1's index are
-// loaded one iteration ahead (ping-pong registers, unrolled by two so no load result is
-// copied in a loop phi).  Items are handed out a tile at a time per wave (one atomic per
-// tile; the first tile of every wave is static).
-// ---------------------------------------------------------------------------
-template <int NT>
-__global__ __launch_bounds__(NT) void k_blend_lanes(
-    const uint32_t* __restrict__ tileStart, const uint32_t* __restrict__ sortedVals,
-    const BlendRecordA* __restrict__ recA, const uint32_t* __restrict__ recB,
-    const uint16_t* __restrict__ expTable, uint32_t* __restrict__ queue, uint32_t tileBegin,
-    uint32_t numTiles, uint32_t tilesX, uint32_t W, uint32_t H, uint8_t* __restrict__ color,
-    size_t colorPitch, uint8_t* __restrict__ depth, size_t depthPitch, int flags) {
-    constexpr uint32_t NW = NT / 64;
-    const bool vecStores = (flags & 1) != 0;
-    __shared__ __attribute__((aligned(16))) uint16_t tbl[65536];
-    {
-        const uint4* src = (const uint4*)expTable;
-        uint4* dst = (uint4*)tbl;
-        for (int i = threadIdx.x; i < 65536 * 2 / 16; i += NT) dst[i] = src[i];
-    }
-    __syncthreads();
-
-    const uint32_t lane = threadIdx.x & 63;
-    const uint32_t rowInGroup = lane & 1u;
-    const uint64_t slotBit = 1ull << (lane & ~1u);  // the even lane of this lane's slot
-    const h2 ONE = {(h1)1.0f, (h1)1.0f};
-    const h2 ZERO = {(h1)0.0f, (h1)0.0f};
-    const uint32_t thrBits = (uint32_t)__builtin_bit_cast(uint16_t, (h1)(1.0f / 255.0f));
-    const h1 c099 = (h1)0.99;
-    const h2 C099 = {c099, c099};
-    const uint32_t gridWaves = gridDim.x * NW;
-
-    // Wave-uniform tile stream: the tile being handed out and `left` of its 64 groups still to
-    // give.  The first tile of every wave is static; later ones come from the queue (a wave
-    // fetches a tile ~2 (1080p) to ~8 (4K) times, so the fetch latency is not hidden).
-    auto tile_bounds = [&](uint32_t t, uint32_t& s0, uint32_t& s1) {
-        if (t < numTiles) {
-            s0 = __builtin_amdgcn_readfirstlane(tileStart[tileBegin + t]);
-            s1 = __builtin_amdgcn_readfirstlane(tileStart[tileBegin + t + 1]);
-        } else {
-            s0 = s1 = 0;
-        }
-    };
-    uint32_t curTile = blockIdx.x * NW + (threadIdx.x >> 6);
-    uint32_t cs0, cs1;
-    tile_bounds(curTile, cs0, cs1);
-    uint32_t nextItem = 0, left = curTile < numTiles ? 64u : 0u;
-    bool exhausted = curTile >= numTiles;
-
-    // per-lane slot state
-    bool act = false;
-    uint32_t cur = 0, end = 0, wait = 0, outX = 0, outY = 0;
-    bool hasList = false;
-    h2 T[2], R[2], G[2], B[2], D[2], X[2], Y = ZERO;
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-        T[q] = ONE;
-        R[q] = G[q] = B[q] = D[q] = X[q] = ZERO;
-    }
-    // pipeline registers in two sets: the record of entry cur and the index of entry cur+1
-    uint4 ra0 = make_uint4(0, 0, 0, 0), ra1 = make_uint4(0, 0, 0, 0);
-    uint32_t rb0 = 0, rb1 = 0, ix0 = 0, ix1 = 0;
-
-    auto refill = [&]() {
-        uint64_t freeM = __ballot(!act) & 0x5555555555555555ull;  // one bit per free slot
-        while (freeM && !exhausted) {
-            if (left == 0) {  // next tile from the queue
-                uint32_t t = 0;
-                if (lane == 0) t = atomicAdd(queue, 1u);
-                curTile = __builtin_amdgcn_readfirstlane(t) + gridWaves;
-                if (curTile >= numTiles) {
-                    exhausted = true;
-                    break;
-                }
-                tile_bounds(curTile, cs0, cs1);
-                nextItem = 0;
-                left = 64;
-            }
-            const uint32_t nFree = (uint32_t)__popcll(freeM);
-            const uint32_t take = nFree < left ? nFree : left;
-            const uint32_t rank = (uint32_t)__popcll(freeM & (slotBit - 1ull));
-            if ((freeM & slotBit) && rank < take) {
-                const uint32_t g = nextItem + rank;  // group of the tile: reference thread (g&7, g>>3)
-                const uint32_t tile = tileBegin + curTile;
-                const uint32_t tx = tile % tilesX, ty = tile / tilesX;
-                cur = cs0;
-                end = cs1;
-                hasList = cs1 > cs0;
-                wait = 2;  // two iterations fill the pipeline
-                act = true;
-                outX = tx * kTileWidth + (g & 7u) * 4u;
-                outY = ty * kTileHeight + (g >> 3) * 2u + rowInGroup;
-                X[0] = h2{(h1)(float)outX, (h1)(float)(outX + 1u)};
-                X[1] = h2{(h1)(float)(outX + 2u), (h1)(float)(outX + 3u)};
-                Y = h2{(h1)(float)outY, (h1)(float)outY};
-#pragma unroll
-                for (int q = 0; q < 2; ++q) {
-                    T[q] = ONE;
-                    R[q] = G[q] = B[q] = D[q] = ZERO;
-                }
-            }
-            for (uint32_t k = 0; k < take; ++k) freeM &= freeM - 1ull;  // drop the served slots
-            nextItem += take;
-            left -= take;
-        }
-    };
-
-    auto finish = [&]() {  // the group's 8 pixels (GlobalShaders.metal:1152-1186)
-        if (outY < H) {
-            uint8_t* crow = color + (size_t)outY * colorPitch;
-#pragma unroll
-            for (int q = 0; q < 2; ++q) {
-                const uint32_t px = outX + 2u * (uint32_t)q;
-                // empty tiles keep the clear colour (0,0,0,1) (GlobalShaders.metal:140-154)
-                const h2 Av = hasList ? (ONE - T[q]) : ONE;
-                const uint32_t ur = as_u32(R[q]), ug = as_u32(G[q]), ub = as_u32(B[q]), ua = as_u32(Av);
-                const uint32_t p0a = (ur & 0xFFFFu) | (ug << 16);
-                const uint32_t p0b = (ub & 0xFFFFu) | (ua << 16);
-                const uint32_t p1a = (ur >> 16) | (ug & 0xFFFF0000u);
-                const uint32_t p1b = (ub >> 16) | (ua & 0xFFFF0000u);
-                const uint32_t ud = as_u32(D[q]);
-                if (vecStores && px + 1 < W) {
-                    *(uint4*)(crow + (size_t)px * 8) = make_uint4(p0a, p0b, p1a, p1b);
-                    if (depth) *(uint32_t*)(depth + (size_t)outY * depthPitch + (size_t)px * 2) = ud;
-                } else {
-                    if (px < W) {
-                        uint32_t* c0 = (uint32_t*)(crow + (size_t)px * 8);
-                        c0[0] = p0a;
-                        c0[1] = p0b;
-                        if (depth) *(uint16_t*)(depth + (size_t)outY * depthPitch + (size_t)px * 2) = (uint16_t)(ud & 0xFFFFu);
-                    }
-                    if (px + 1 < W) {
-                        uint32_t* c1 = (uint32_t*)(crow + (size_t)(px + 1) * 8);
-                        c1[0] = p1a;
-                        c1[1] = p1b;
-                        if (depth) *(uint16_t*)(depth + (size_t)outY * depthPitch + (size_t)(px + 1) * 2) = (uint16_t)(ud >> 16);
-                    }
-                }
-            }
-        }
-        act = false;
-    };
-
-    // One list entry per slot: first the loads of the next entry (record of cur+1 through the
-    // index in `ix`, index of cur+2; unpredicated and clamped to the tile's list -- or to entry 0,
-    // which the renderer keeps a valid gaussian id), then the blend of entry cur from (ra, rb).
-    auto step = [&](const uint4 ra, const uint32_t rb, const uint32_t ix, uint4& na, uint32_t& nb, uint32_t& nx) {
-        na = *(const uint4*)(recA + ix);
-        nb = recB[ix];
-        const uint32_t ahead = wait == 2 ? 0u : (wait == 1 ? 1u : 2u);
-        nx = sortedVals[end > cur + ahead ? cur + ahead : (end > 0 ? end - 1u : 0u)];
-        if (act && wait == 0) {
-            // group break (GlobalShaders.metal:1086-1088): max T over the group's 8 pixels
-            const u16x2 tm = __builtin_elementwise_max(__builtin_bit_cast(u16x2, T[0]), __builtin_bit_cast(u16x2, T[1]));
-            const uint32_t tb = __builtin_bit_cast(uint32_t, tm);
-            uint32_t gm = max(tb & 0xFFFFu, tb >> 16);
-            const uint32_t o = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)gm, 0xB1, 0xF, 0xF, false);
-            gm = max(gm, o);  // the other row of the group (partner lane, same slot)
-            if (gm < thrBits || cur >= end) {
-                finish();
-            } else {
-                const h2 mean = as_h2(ra.x), cc = as_h2(ra.y), oc = as_h2(ra.z), rgv = as_h2(ra.w), bdv = as_h2(rb);
-                const h2 dyv = Y - splat_hi(mean);
-                const h2 dyy = (dyv * dyv) * splat_hi(cc);
-#pragma unroll
-                for (int q = 0; q < 2; ++q) {
-                    const h2 dx = X[q] - splat_lo(mean);
-                    // p = ((dx*dx)*cxx + (dy*dy)*cyy) + (dx*dy)*cxy2 (GlobalShaders.metal:1115-1122)
-                    const h2 pq = ((dx * dx) * splat_lo(cc) + dyy) + (dx * dyv) * splat_lo(oc);
-                    // a = min(opacity * exp(-0.5h * p), 0.99h) (GlobalShaders.metal:1124-1131)
-                    const h2 a = __builtin_elementwise_min(splat_hi(oc) * lookup2(tbl, pq), C099);
-                    const h2 w = a * T[q];  // (GlobalShaders.metal:1137-1149)
-                    T[q] = T[q] * (ONE - a);
-                    R[q] = R[q] + splat_lo(rgv) * w;
-                    G[q] = G[q] + splat_hi(rgv) * w;
-                    B[q] = B[q] + splat_lo(bdv) * w;
-                    D[q] = D[q] + splat_hi(bdv) * w;
-                }
-                cur++;
-            }
-        } else if (act) {
-            wait--;
-        }
-    };
-
-    refill();
-    while (__ballot(act) != 0) {
-        step(ra0, rb0, ix0, ra1, rb1, ix1);
-        step(ra1, rb1, ix1, ra0, rb0, ix0);
-        refill();
-    }
-}
-
-// ---------------------------------------------------------------------------
 // Blend schedule: the units in descending order of the walk each made in the previous frame
 // (longest-processing-time-first list scheduling on the persistent waves), as a stable
 // counting sort into 256 buckets of walk length (bucket width = max walk / 256, so the order
@@ -817,10 +587,8 @@ __device__ __forceinline__ uint64_t uo_match8(uint32_t d, bool valid) {
     return peers;
 }
 
-// order[n] <- epoch once the permutation is complete (release, device scope): a blend launched
-// without a stream join checks it and falls back to index order (k_blend_px).
 __global__ __launch_bounds__(1024) void k_unit_order(const uint16_t* __restrict__ cost,
-                                                     uint32_t* __restrict__ order, uint32_t n, uint32_t epoch) {
+                                                     uint32_t* __restrict__ order, uint32_t n) {
     __shared__ uint32_t wmax[kUoWaves];
     __shared__ uint32_t base[kUoBuckets];
     __shared__ uint32_t wcnt[kUoWaves][kUoBuckets];
@@ -878,15 +646,10 @@ __global__ __launch_bounds__(1024) void k_unit_order(const uint16_t* __restrict_
         }
         __syncthreads();
     }
-    __threadfence();
-    __syncthreads();
-    if (t == 0) __hip_atomic_store(&order[n], epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 
 int blend_pairs_per_lane(uint32_t numTiles, int numCUs) {
-    const char* v = getenv("GSM_BLEND_PAIRS");
-    if (v && (atoi(v) == 1 || atoi(v) == 2 || atoi(v) == 4)) return atoi(v);
     // Half tiles (2 pairs per lane) while the tiles outnumber the 8-wave slots; a smaller frame
     // or a slab of a multi-GPU frame has fewer units than slots, its blend time is its longest
     // unit's walk, and quadrant units (1 pair per lane, ~38 instead of ~61 VALU per entry)
@@ -899,34 +662,26 @@ uint32_t blend_units_per_tile(uint32_t numTiles, int numCUs) {
 }
 
 static int blend_waves_per_wg(uint32_t numTiles, int numCUs) {
-    const char* v = getenv("GSM_BLEND_WAVES");
-    if (v && (atoi(v) == 8 || atoi(v) == 12 || atoi(v) == 16)) return atoi(v);
     // 16 waves per CU hide more latency once every wave slot gets >= 6 units (4K: 16200 tiles);
     // with fewer units per slot the tail dominates and 8 waves finish first (1080p)
     const uint64_t units = (uint64_t)numTiles * blend_units_per_tile(numTiles, numCUs);
     return units >= 6ull * (uint64_t)numCUs * 16u ? 16 : 8;
 }
 
-bool blend_schedule_enabled(uint32_t numTiles, int numCUs) {
-    (void)numTiles;
-    (void)numCUs;
-    const char* v = getenv("GSM_BLEND_SCHED");  // 0 = index order; default: last frame's cost order
-    // Measured (events, µs): 1080p 8 waves 293 -> 248 with the order; 4K 16 waves 703 -> 660.
-    // (At 4K with 8 waves the order cost 4 % of L2 locality, but 4K runs 16 waves.)
-    return !(v && v[0] == '0');
-}
-
-void launch_unit_order(uint32_t numUnits, const DeviceArena& A, hipStream_t s, uint32_t epoch) {
-    hipLaunchKernelGGL(k_unit_order, dim3(1), dim3(1024), 0, s, A.unitCost, A.unitOrder, numUnits, epoch);
+void launch_unit_order(uint32_t numUnits, const DeviceArena& A, hipStream_t s) {
+    hipLaunchKernelGGL(k_unit_order, dim3(1), dim3(1024), 0, s, A.unitCost, A.unitOrder, numUnits);
 }
 
 void launch_unit_order_costs(const uint16_t* cost, uint32_t* order, uint32_t numUnits, hipStream_t s) {
-    hipLaunchKernelGGL(k_unit_order, dim3(1), dim3(1024), 0, s, cost, order, numUnits, 0u);
+    hipLaunchKernelGGL(k_unit_order, dim3(1), dim3(1024), 0, s, cost, order, numUnits);
 }
 
+// Measured schedule choices: units longest-first by last frame's walk (costOrder;
+// 1080p 8 waves 293 -> 248 us, 4K 16 waves 703 -> 660), the longest on one top-priority wave per
+// SIMD (flags bit 2), later units' priority rising with the age of their walk (flags bit 1).
 void launch_blend(const uint32_t* sortedVals, const FrameGeometry& g, const DeviceArena& A, void* color,
                   size_t colorPitch, void* depth, size_t depthPitch, int numCUs, bool costOrder, int colorFormat,
-                  hipStream_t s, uint32_t orderEpoch) {
+                  hipStream_t s) {
     const uint32_t t0 = g.rowBegin * g.tilesX, t1 = g.rowEnd * g.tilesX;
     if (t1 <= t0) return;
     const uint32_t numTiles = t1 - t0;
@@ -934,76 +689,28 @@ void launch_blend(const uint32_t* sortedVals, const FrameGeometry& g, const Devi
                      (depth == nullptr || ((((uintptr_t)depth) & 7u) == 0 && (depthPitch & 7u) == 0)))
                         ? 1
                         : 0;
-    const char* pv = getenv("GSM_BLEND_PRIO");  // age-raised wave priority (default on)
-    const char* sp = getenv("GSM_BLEND_SPLIT");  // long units on half the waves at top priority
-    const int flags = vec | ((pv && pv[0] == '0') ? 0 : 2) | ((costOrder && !(sp && sp[0] == '0')) ? 4 : 0) |
-                      ((colorFormat & 15) << 4) | (costOrder ? (int)((orderEpoch & 0x7FFFFFu) << 8) : 0);
+    const int flags = vec | 2 | (costOrder ? 4 : 0) | ((colorFormat & 15) << 4);
     // A.tileQueue was zeroed by k_scan_blocks earlier in the frame
     const int P = blend_pairs_per_lane(numTiles, numCUs);
     const int waves = blend_waves_per_wg(numTiles, numCUs);
-    const char* ev = getenv("GSM_BLEND_EXECM");  // dead lanes: EXEC mask (default) or selects
-    const bool execm = !(ev && ev[0] == '0');
-    const char* lv = getenv("GSM_BLEND_LANES");  // group-granular k_blend_lanes
-    if (lv && lv[0] == '1') {
-        uint32_t lgrid = (numTiles + (uint32_t)waves - 1) / (uint32_t)waves;
-        if (lgrid > (uint32_t)numCUs) lgrid = (uint32_t)numCUs;
-        if (waves == 16)
-            hipLaunchKernelGGL((k_blend_lanes<1024>), dim3(lgrid), dim3(1024), 0, s, A.tileStart, sortedVals, A.recA,
-                               A.recB, A.expTable, A.tileQueue, t0, numTiles, g.tilesX, g.width, g.height,
-                               (uint8_t*)color, colorPitch, (uint8_t*)depth, depthPitch, flags);
-        else
-            hipLaunchKernelGGL((k_blend_lanes<512>), dim3(lgrid), dim3(512), 0, s, A.tileStart, sortedVals, A.recA,
-                               A.recB, A.expTable, A.tileQueue, t0, numTiles, g.tilesX, g.width, g.height,
-                               (uint8_t*)color, colorPitch, (uint8_t*)depth, depthPitch, flags);
-        return;
-    }
     const uint32_t units = numTiles * (4u / (uint32_t)P);
     uint32_t grid = (units + (uint32_t)waves - 1) / (uint32_t)waves;
     if (grid > (uint32_t)numCUs) grid = (uint32_t)numCUs;
-#define GSM_LAUNCH_PX(NTH, PP)                                                                      \
-    if (execm) GSM_LAUNCH_PXE(NTH, PP, true, 0);                                                      \
-    else GSM_LAUNCH_PXE(NTH, PP, false, 0)
-#define GSM_LAUNCH_PXE(NTH, PP, EM, X)                                                              \
-    hipLaunchKernelGGL((k_blend_px<NTH, PP, EM, X>), dim3(grid), dim3(NTH), 0, s, A.tileStart, sortedVals, \
-                       A.recA, A.recB, A.expTable, A.tileQueue, t0, numTiles, g.tilesX, g.width,    \
-                       g.height, (uint8_t*)color, colorPitch, (uint8_t*)depth, depthPitch, flags,    \
-                       costOrder ? A.unitOrder : nullptr, A.unitCost, A.blendTrace)
-#define GSM_LAUNCH_P(NTH)                    \
-    if (P == 1) GSM_LAUNCH_PX(NTH, 1);       \
-    else if (P == 4) GSM_LAUNCH_PX(NTH, 4);  \
-    else GSM_LAUNCH_PX(NTH, 2)
-    const char* xv = getenv("GSM_BLEND_EXPT");  // timing experiments (wrong images): 1 no table, 2 no break
-    if (xv && (xv[0] == '1' || xv[0] == '2') && P == 2 && waves == 8 && execm) {
-        if (xv[0] == '1') GSM_LAUNCH_PXE(512, 2, true, 1);
-        else GSM_LAUNCH_PXE(512, 2, true, 2);
-        return;
-    }
-    const char* cv = getenv("GSM_BLEND_COMPACT");  // groups move to 1 pair per lane when <= 16 alive
-    if (P == 2 && execm && !(cv && cv[0] == '0')) {
-        if (waves == 12) hipLaunchKernelGGL((k_blend_px<768, 2, true, 0, true>), dim3(grid), dim3(768), 0, s,
-                                            A.tileStart, sortedVals, A.recA, A.recB, A.expTable, A.tileQueue, t0,
-                                            numTiles, g.tilesX, g.width, g.height, (uint8_t*)color, colorPitch,
-                                            (uint8_t*)depth, depthPitch, flags, costOrder ? A.unitOrder : nullptr,
-                                            A.unitCost, A.blendTrace);
-        else if (waves == 16) hipLaunchKernelGGL((k_blend_px<1024, 2, true, 0, true>), dim3(grid), dim3(1024), 0, s,
-                                            A.tileStart, sortedVals, A.recA, A.recB, A.expTable, A.tileQueue, t0,
-                                            numTiles, g.tilesX, g.width, g.height, (uint8_t*)color, colorPitch,
-                                            (uint8_t*)depth, depthPitch, flags, costOrder ? A.unitOrder : nullptr,
-                                            A.unitCost, A.blendTrace);
-        else hipLaunchKernelGGL((k_blend_px<512, 2, true, 0, true>), dim3(grid), dim3(512), 0, s, A.tileStart,
-                                sortedVals, A.recA, A.recB, A.expTable, A.tileQueue, t0, numTiles, g.tilesX,
-                                g.width, g.height, (uint8_t*)color, colorPitch, (uint8_t*)depth, depthPitch, flags,
-                                costOrder ? A.unitOrder : nullptr, A.unitCost, A.blendTrace);
-        return;
-    }
-    if (waves == 16) {
-        GSM_LAUNCH_P(1024);
+    const uint32_t* order = costOrder ? A.unitOrder : nullptr;
+#define GSM_LAUNCH_BLEND(NTH, PP, CMP)                                                                       \
+    hipLaunchKernelGGL((k_blend_px<NTH, PP, CMP>), dim3(grid), dim3(NTH), 0, s, A.tileStart, sortedVals, A.recA, \
+                       A.recB, A.expTable, A.tileQueue, t0, numTiles, g.tilesX, g.width, g.height,          \
+                       (uint8_t*)color, colorPitch, (uint8_t*)depth, depthPitch, flags, order, A.unitCost,  \
+                       A.blendTrace)
+    // half tiles compact to one pair per lane once <= 16 of their 32 groups are alive
+    if (P == 1) {
+        if (waves == 16) GSM_LAUNCH_BLEND(1024, 1, false);
+        else GSM_LAUNCH_BLEND(512, 1, false);
     } else {
-        GSM_LAUNCH_P(512);
+        if (waves == 16) GSM_LAUNCH_BLEND(1024, 2, true);
+        else GSM_LAUNCH_BLEND(512, 2, true);
     }
-#undef GSM_LAUNCH_P
-#undef GSM_LAUNCH_PX
-#undef GSM_LAUNCH_PXE
+#undef GSM_LAUNCH_BLEND
 }
 
 }  // namespace gsm

@@ -191,7 +191,10 @@ gsm_status gsm_sort_pairs_u32(void* keys, void* values, uint32_t n, uint32_t key
         uint32_t* kb[2] = {(uint32_t*)keys, k2};
         uint32_t* vb[2] = {(uint32_t*)values, v2};
         const int digits = (int)((key_bits + 7) / 8);
-        int res = gsm::radix_sort_pairs(kb, vb, np, n, 0, digits, hist, bins, s);
+        int dev = 0;
+        hipGetDevice(&dev);
+        const bool ballot = gsm::tuning_from_env(dev).ballotRank;  // read per call: no renderer here
+        int res = gsm::radix_sort_pairs(kb, vb, np, n, 0, digits, hist, bins, s, ballot);
         if (res == 1) {
             hipMemcpyAsync(keys, k2, (size_t)n * 4, hipMemcpyDeviceToDevice, s);
             hipMemcpyAsync(values, v2, (size_t)n * 4, hipMemcpyDeviceToDevice, s);
@@ -204,6 +207,17 @@ gsm_status gsm_sort_pairs_u32(void* keys, void* values, uint32_t n, uint32_t key
     hipFree(bins);
     hipFree(np);
     return st;
+}
+
+gsm_status gsm_debug_sort_rank_probe(int hip_device, int* lane_ordered) {
+    if (!lane_ordered) return GSM_ERR_INVALID_ARGUMENT;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || hip_device < 0 || hip_device >= ndev) {
+        (void)hipGetLastError();
+        return GSM_ERR_DEVICE_NOT_AVAILABLE;
+    }
+    *lane_ordered = gsm::sort_lane_ordered_atomics(hip_device) ? 1 : 0;
+    return GSM_OK;
 }
 
 }  // extern "C"

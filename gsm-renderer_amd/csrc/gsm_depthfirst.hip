@@ -41,6 +41,7 @@ class DepthFirstRenderer {
     int device_ = -1;
     int numCUs_ = 256;
     gsm_renderer_config config_{};
+    Tuning tuning_{};  // A/B switches, read once at create
     uint32_t maxGaussians_ = 1, maxWidth_ = 1, maxHeight_ = 1, maxInstances_ = 4;
     uint32_t maxTiles_ = 1;
     DfArena A_;
@@ -124,6 +125,7 @@ gsm_status DepthFirstRenderer::create(const gsm_renderer_config& cfg, int hipDev
         return GSM_ERR_DEVICE_NOT_AVAILABLE;
     }
     r->numCUs_ = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+    r->tuning_ = tuning_from_env(dev);
     const size_t G = r->maxGaussians_, cap = r->maxInstances_;
     const size_t nb = (G + kDfBlock - 1) / kDfBlock;
     DfArena& A = r->A_;
@@ -155,7 +157,7 @@ gsm_status DepthFirstRenderer::create(const gsm_renderer_config& cfg, int hipDev
     GSM_DF_ALLOC(A.queue, 4);
     GSM_DF_ALLOC(A.expTable, 65536 * 2);
     GSM_DF_ALLOC(A.unitCost, (size_t)r->maxTiles_ * 2 * sizeof(uint16_t));
-    GSM_DF_ALLOC(A.unitOrder, ((size_t)r->maxTiles_ * 2 + 1) * sizeof(uint32_t));  // + the ready word
+    GSM_DF_ALLOC(A.unitOrder, (size_t)r->maxTiles_ * 2 * sizeof(uint32_t));
 #undef GSM_DF_ALLOC
     if (st != GSM_OK) {
         delete r;
@@ -239,8 +241,7 @@ gsm_status DepthFirstRenderer::renderStereoSbs(hipStream_t s, const gsm_gaussian
 
     // The blend schedule's ordering kernel only needs the previous frame's walk lengths, so it
     // runs on a side stream beside this frame's projection and sorts (joined before the blend).
-    const char* sv = getenv("GSM_DF_SCHED");
-    const bool costOrder = !(sv && sv[0] == '0');
+    const bool costOrder = tuning_.costOrder;
     if (costOrder && !side_) {
         if (hipStreamCreateWithFlags(&side_, hipStreamNonBlocking) != hipSuccess ||
             hipEventCreateWithFlags(&evFrame_, hipEventDisableTiming) != hipSuccess ||
@@ -272,7 +273,7 @@ gsm_status DepthFirstRenderer::renderStereoSbs(hipStream_t s, const gsm_gaussian
     if (prof) hipEventRecord(ev[1], s);
     // DepthRadixSortEncoder, 32-bit keys (DepthFirstRenderer.swift:664-681): stable LSD, 4 x 8 bits
     const int dc = radix_sort_bits(A_.dkeys, A_.dvals, &A_.visHdr->totalAssignments, maxGaussians_, 0, 32,
-                                   A_.radixHist, A_.radixBinTotals, s);
+                                   A_.radixHist, A_.radixBinTotals, s, tuning_.ballotRank);
     if (prof) hipEventRecord(ev[2], s);
     df_launch_instance_counts(A_.dvals[dc], a, A_, s);
     launch_scan_sums(A_.instSums, nb, maxInstances_, A_.instHdr, A_.queue, s);
@@ -282,11 +283,11 @@ gsm_status DepthFirstRenderer::renderStereoSbs(hipStream_t s, const gsm_gaussian
     uint32_t tileBits = 0;
     while (tileBits < 16 && ((a.tileCount - 1u) >> tileBits)) tileBits++;
     const int ic = radix_sort_bits(A_.ikeys, A_.ivals, &A_.instHdr->totalAssignments, maxInstances_, 0, tileBits,
-                                   A_.radixHist, A_.radixBinTotals, s);
+                                   A_.radixHist, A_.radixBinTotals, s, tuning_.ballotRank);
     df_launch_ranges(A_.ikeys[ic], a, A_, s);
     // Blend schedule: (tile, eye) units handed out longest first by the walk lengths the previous
     // frame of the same geometry measured (the image does not depend on the order, only the load
-    // balance does).  GSM_DF_SCHED=0: index order.
+    // balance does).  Tuning::costOrder false (GSM_BLEND_SCHED=0 at create): index order.
     if (costOrder) hipStreamWaitEvent(s, evOrder_, 0);
     A_.blendStats = (profiling_ & 2) ? statsBuf_ : nullptr;
     if (A_.blendStats) hipMemsetAsync(statsBuf_, 0, 4 * sizeof(unsigned long long), s);

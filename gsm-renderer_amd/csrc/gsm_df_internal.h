@@ -60,7 +60,7 @@ struct DfArena {
 
 constexpr int kDfBlock = 256;
 // instance values: gaussian id in bits 0-29 (max_gaussians <= 30M < 2^30); bit 30 + e set when eye e
-// provably adds nothing to the instance's tile (k_df_flags, df_eye_misses_tile)
+// provably adds nothing to the instance's tile (k_df_expand, df_eye_misses_tile)
 constexpr uint32_t kDfSkipShift = 30;
 constexpr uint32_t kDfGidMask = (1u << kDfSkipShift) - 1u;
 
@@ -73,8 +73,6 @@ void df_launch_compact(const DfArgs& a, const DfArena& A, hipStream_t stream);
 // applyDepthOrderingKernel + instance prefix sum + createInstancesStereoKernel (:623-640, :790-826)
 void df_launch_instance_counts(const uint32_t* order, const DfArgs& a, const DfArena& A, hipStream_t stream);
 void df_launch_instances(const uint32_t* order, const DfArgs& a, const DfArena& A, hipStream_t stream);
-// the blend's per-instance skip flags (k_df_flags), on the unsorted instances
-void df_launch_flags(const DfArgs& a, const DfArena& A, hipStream_t stream);
 // extractTileRangesKernel (:1258-1313)
 void df_launch_ranges(const uint32_t* sortedTiles, const DfArgs& a, const DfArena& A, hipStream_t stream);
 // clearStereoRenderTextureKernel + depthFirstStereoRender + DepthFirstStereoCopyEncoder

@@ -5,9 +5,9 @@
 // Frame: project both eyes once per gaussian (k_df_project) -> compact the visible ones with
 // their 32-bit depth keys (k_df_compact) -> stable LSD depth sort (gsm_sort.hip) -> per-gaussian
 // tile counts in depth order, scan, instance expansion of the union rect (k_df_icount,
-// k_df_instances) -> stable LSD sort by tile id -> tile ranges (k_df_ranges) -> one persistent
-// blend kernel that clears, composites both eyes per 16x16 tile and writes the two eyes side by
-// side with the copy pass's row flip (k_df_blend).
+// k_df_expand) -> stable LSD sort by tile id -> tile ranges (k_df_starts) -> one persistent
+// blend kernel that clears, composites each (tile, eye) of 16x16 pixels and writes the two eyes
+// side by side with the copy pass's row flip (k_df_blend_eye).
 // Numeric contract: DESIGN.md (built with -ffp-contract=off, IEEE div/sqrt); bit-exact with
 // oracle/gsm_oracle.c og_df_render_stereo.
 #include <hip/hip_runtime.h>
@@ -272,54 +272,13 @@ __device__ __forceinline__ bool df_eye_misses_tile(const DfEyeSkip& e, int x0, i
     return quad_exceeds(e, x0, y0, (int)kDfTile - 1, (int)kDfTile - 1, 9.0f);
 }
 
-__global__ __launch_bounds__(kDfBlock) void k_df_instances(const TileAssignmentHeader* __restrict__ visHdr,
-                                                           const uint32_t* __restrict__ order,
-                                                           const uint32_t* __restrict__ touched,
-                                                           const short4* __restrict__ bounds,
-                                                           const uint32_t* __restrict__ blockOffsets,
-                                                           uint32_t maxInstances, uint32_t tilesX,
-                                                           uint32_t* __restrict__ tiles, uint32_t* __restrict__ gids) {
-    __shared__ uint32_t lds[kDfBlock / 64];
-    const uint32_t i = blockIdx.x * kDfBlock + threadIdx.x;
-    const uint32_t V = visHdr->totalAssignments;
-    const uint32_t g = i < V ? order[i] : 0u;
-    const uint32_t c = i < V ? touched[g] : 0u;
-    uint32_t total;
-    const uint32_t off = block_exclusive_scan<kDfBlock>(c, lds, &total);
-    if (c == 0) return;
-    uint64_t wp = (uint64_t)blockOffsets[blockIdx.x] + off;
-    const short4 r = bounds[g];
-    for (int ty = r.z; ty <= r.w; ++ty)
-        for (int tx = r.x; tx <= r.y; ++tx) {
-            if (wp >= maxInstances) return;
-            tiles[wp] = (uint32_t)(ty * (int)tilesX + tx) & 0xFFFFu;  // ushort tile id
-            gids[wp] = g;
-            wp++;
-        }
-}
-
-// k_df_flags: one thread per instance (depth order, before the tile sort): bit kDfSkipShift + e of
-// the instance's gaussian id is set when eye e provably adds nothing to the instance's tile
-__global__ __launch_bounds__(256) void k_df_flags(const TileAssignmentHeader* __restrict__ instHdr,
-                                                  const uint32_t* __restrict__ tiles, uint32_t* __restrict__ gids,
-                                                  const StereoTiledRenderData* __restrict__ rd, uint32_t tilesX) {
-    const uint32_t total = instHdr->totalAssignments;
-    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < total; i += gridDim.x * 256u) {
-        const uint32_t g = gids[i], t = tiles[i];
-        const uint4 w0 = ((const uint4*)(rd + g))[0];
-        const uint2 w1 = ((const uint2*)(rd + g))[2];
-        const int x0 = (int)((t % tilesX) * kDfTile), y0 = (int)((t / tilesX) * kDfTile);
-        const uint32_t fl = (df_eye_misses_tile(df_eye_skip_setup(w0.x, w0.y, w0.z), x0, y0) ? 1u : 0u) |
-                            (df_eye_misses_tile(df_eye_skip_setup(w0.w, w1.x, w1.y), x0, y0) ? 2u : 0u);
-        if (fl) gids[i] = g | (fl << kDfSkipShift);
-    }
-}
-
-// k_df_expand: the same instances as k_df_instances, expanded cooperatively: the block's 256
-// gaussians (in depth order) get their offsets from one block scan, then thread t writes the
-// block's instances t, t + 256, ... (consecutive threads, consecutive slots: coalesced stores, no
-// thread walks a long rect alone) and sets the blend's skip flags of each (k_df_flags' test, with
-// each gaussian's per-eye setup computed once into LDS).
+// k_df_expand: the instances of the union rects (ty-major, tx-minor, DepthFirstShaders.metal:790-826),
+// expanded cooperatively: the block's 256 gaussians (in depth order) get their offsets from one
+// block scan, then thread t writes the block's instances t, t + 256, ... (consecutive threads,
+// consecutive slots: coalesced stores, no thread walks a long rect alone), clamped to
+// maxInstances.  Each instance also gets the blend's skip flags: bit kDfSkipShift + e of the
+// gaussian id is set when eye e provably adds nothing to the instance's tile
+// (df_eye_misses_tile, with each gaussian's per-eye setup computed once into LDS).
 __global__ __launch_bounds__(kDfBlock) void k_df_expand(const TileAssignmentHeader* __restrict__ visHdr,
                                                         const uint32_t* __restrict__ order,
                                                         const uint32_t* __restrict__ touched,
@@ -409,19 +368,17 @@ __global__ __launch_bounds__(256) void k_df_starts(const uint32_t* __restrict__ 
 //    side-by-side copy (DepthFirstStereoCopyEncoder.swift:29-99, DepthFirstShaders.metal:1990-2018)
 //
 // Persistent workgroups, one per CU: the 128 KiB stereo alpha table sits in LDS and the waves
-// pull 16x16 tiles from a device counter.  A lane is one reference thread: a 2x2 pixel group of
-// both eyes, held as packed fp16 pairs (row 0 = {x, x+1}, row 1).  The tile's list is walked in
-// batches of kDfBatch records: lane pairs gather one 32-byte record (the u8 colour and opacity
-// turned into fp16 c/255 on the way) into the wave's LDS stage, then every entry is read back
-// as a uniform-address broadcast.  Per lane and entry the reference's control flow -- the
+// pull (tile, eye) units from a device counter.  A lane is one reference thread: a 2x2 pixel
+// group of one eye, held as packed fp16 pairs (row 0 = {x, x+1}, row 1).  The tile's list is
+// walked in batches of records staged in the wave's LDS (the u8 colour and opacity turned into
+// fp16 c/255 on the way), every entry read back as a uniform-address broadcast.  Per lane and
+// entry the reference's control flow -- the
 // joint break when both eyes' max transmittance < 1/255, the per-eye test, the all-zero skip and
 // the r^2 > 9 cutoff -- is applied as data: an eye that is done, or a pixel past the cutoff
 // (folded into the table, stereo_exp_table_entry), gets alpha 0, which leaves its colour and
 // transmittance bit-identical (C + c * (0 * T) = C, T * (1 - 0) = T), and a dead lane stays
 // dead (T never grows).  The wave leaves the list once every lane is done.
 // ---------------------------------------------------------------------------
-constexpr uint32_t kDfBatch = 32;
-
 __device__ __forceinline__ void df_wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -535,107 +492,6 @@ __device__ __forceinline__ bool df_alive(const DfEyeState& st, uint32_t thrBits)
     const df_u16x2 m = __builtin_elementwise_max(__builtin_bit_cast(df_u16x2, st.T[0]),
                                                  __builtin_bit_cast(df_u16x2, st.T[1]));
     return max((uint32_t)m.x, (uint32_t)m.y) >= thrBits;
-}
-
-template <int NW>
-__global__ __launch_bounds__(NW * 64) void k_df_blend(const uint32_t* __restrict__ starts,
-                                                      const uint32_t* __restrict__ gids,
-                                                      const StereoTiledRenderData* __restrict__ rd,
-                                                      const uint16_t* __restrict__ expTable,
-                                                      uint32_t* __restrict__ queue, uint32_t tilesX,
-                                                      uint32_t tileCount, uint32_t W, uint32_t H,
-                                                      uint8_t* __restrict__ color, size_t pitch, int fmt) {
-    __shared__ __attribute__((aligned(16))) uint16_t tbl[65536];
-    __shared__ __attribute__((aligned(16))) uint4 stage[NW][kDfBatch * 2];
-    __shared__ uint16_t div255[256];
-    {
-        const uint4* src = (const uint4*)expTable;
-        uint4* dst = (uint4*)tbl;
-        for (int i = threadIdx.x; i < 65536 * 2 / 16; i += NW * 64) dst[i] = src[i];
-        if (threadIdx.x < 256) div255[threadIdx.x] = f_to_hbits((float)threadIdx.x / 255.0f);  // getColor
-    }
-    __syncthreads();
-    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
-    const uint32_t thrBits = (uint32_t)f_to_hbits(1.0f / 255.0f);  // half(1.0h / 255.0h)
-    const uint32_t bpp = fmt == GSM_COLOR_FORMAT_RGBA16F ? 8u : (fmt == GSM_COLOR_FORMAT_RGBA32F ? 16u : 4u);
-    const h2 ONE = {(h1)1.0f, (h1)1.0f};
-    uint4* stg = stage[wave];
-    for (;;) {
-        uint32_t t = 0;
-        if (lane == 0) t = atomicAdd(queue, 1u);
-        t = (uint32_t)__shfl((int)t, 0, 64);
-        if (t >= tileCount) break;
-        const uint32_t st0 = starts[t];
-        const uint2 hd = make_uint2(st0, starts[t + 1] - st0);
-        const uint32_t tileX = t % tilesX, tileY = t / tilesX;
-        const uint32_t bx = tileX * kDfTile + (lane & 7u) * 2u, by = tileY * kDfTile + (lane >> 3) * 2u;
-        const h2 PX = {(h1)(float)bx, (h1)(float)(bx + 1u)};
-        const h2 PY = {(h1)(float)by, (h1)(float)(by + 1u)};
-        DfEyeState E[2];
-#pragma unroll
-        for (int e = 0; e < 2; ++e) {
-            E[e].T[0] = E[e].T[1] = ONE;
-            E[e].Cr[0] = E[e].Cr[1] = E[e].Cg[0] = E[e].Cg[1] = E[e].Cb[0] = E[e].Cb[1] = df_h2(0u);
-        }
-        bool done = false;
-        for (uint32_t b0 = 0; b0 < hd.y && !done; b0 += kDfBatch) {
-            const uint32_t n = min(kDfBatch, hd.y - b0);
-            const uint32_t rec = lane >> 1;
-            if (rec < n) {
-                const uint32_t g = gids[hd.x + b0 + rec] & kDfGidMask;
-                uint4 v = ((const uint4*)(rd + g))[lane & 1u];
-                if (lane & 1u) {  // colorR, G, B, opacity (bytes 24..27) -> fp16 {op, r}, {g, b}
-                    const uint32_t c = v.z;
-                    v.z = (uint32_t)div255[c >> 24] | ((uint32_t)div255[c & 0xFFu] << 16);
-                    v.w = (uint32_t)div255[(c >> 8) & 0xFFu] | ((uint32_t)div255[(c >> 16) & 0xFFu] << 16);
-                }
-                stg[lane] = v;
-            }
-            df_wave_sync();
-            for (uint32_t j = 0; j < n; ++j) {
-                const bool aL = df_alive(E[0], thrBits), aR = df_alive(E[1], thrBits);
-                if (!__any(aL || aR)) {  // every lane has taken the reference's break
-                    done = true;
-                    break;
-                }
-                const uint4 s0 = stg[2 * j], s1 = stg[2 * j + 1];
-                const h2 opr = df_h2(s1.z), gb = df_h2(s1.w);
-                // gMean.x >= -60000.0h: the eye's mean is real (uniform over the wave).  An eye whose
-                // alphas are 0 on every live lane is an identity update for the wave: skipped.
-                const h2 mL = df_h2(s0.x), mR = df_h2(s0.w);
-                if ((float)mL.x >= -60000.0f) {
-                    h2 p0, p1;
-                    df_quadform(mL, df_h2(s0.y), df_h2(s0.z), PX, PY, p0, p1);
-                    if (__any(aL && !df_all_cut(p0, p1))) df_blend_eye(E[0], aL, p0, p1, opr, gb, tbl);
-                }
-                if ((float)mR.x >= -60000.0f) {
-                    h2 p0, p1;
-                    df_quadform(mR, df_h2(s1.x), df_h2(s1.y), PX, PY, p0, p1);
-                    if (__any(aR && !df_all_cut(p0, p1))) df_blend_eye(E[1], aR, p0, p1, opr, gb, tbl);
-                }
-            }
-            df_wave_sync();  // the stage is rewritten by the next batch
-        }
-        // (C, 1 - T) of eye e's pixel (x, y) lands in target row H - 1 - y, column e * W + x; a tile
-        // with an empty list is not an active tile and keeps the clear value (0, 0, 0, 1)
-        const uint32_t clearA = hd.y == 0 ? 0x3C003C00u : 0u;
-#pragma unroll
-        for (int e = 0; e < 2; ++e)
-#pragma unroll
-            for (int row = 0; row < 2; ++row) {
-                const uint32_t y = by + (uint32_t)row;
-                if (y >= H) continue;
-                uint8_t* trow = color + (size_t)(H - 1u - y) * pitch + (size_t)e * W * bpp;
-                const uint32_t ur = df_u32(E[e].Cr[row]), ug = df_u32(E[e].Cg[row]);
-                const uint32_t ub = df_u32(E[e].Cb[row]), ua = df_u32(ONE - E[e].T[row]) | clearA;
-                if (bx < W)
-                    store_color_px(fmt, (char*)(trow + (size_t)bx * bpp), (ur & 0xFFFFu) | (ug << 16),
-                                   (ub & 0xFFFFu) | (ua << 16));
-                if (bx + 1u < W)
-                    store_color_px(fmt, (char*)(trow + (size_t)(bx + 1u) * bpp), (ur >> 16) | (ug & 0xFFFF0000u),
-                                   (ub >> 16) | (ua & 0xFFFF0000u));
-            }
-    }
 }
 
 // k_df_blend_eye: one wave per (tile, eye) unit.  An eye's updates only depend on its own
@@ -849,23 +705,8 @@ void df_launch_instance_counts(const uint32_t* order, const DfArgs& a, const DfA
 void df_launch_instances(const uint32_t* order, const DfArgs& a, const DfArena& A, hipStream_t s) {
     const uint32_t blocks = (a.count + kDfBlock - 1) / kDfBlock;
     if (blocks == 0) return;
-    const char* v = getenv("GSM_DF_EXPAND");  // 0: one thread per gaussian + k_df_flags (A/B)
-    if (!(v && v[0] == '0')) {
-        hipLaunchKernelGGL(k_df_expand, dim3(blocks), dim3(kDfBlock), 0, s, A.visHdr, order, A.touched, A.bounds,
-                           A.instSums, A.renderData, a.maxInstances, a.tilesX, A.ikeys[0], A.ivals[0]);
-        return;
-    }
-    hipLaunchKernelGGL(k_df_instances, dim3(blocks), dim3(kDfBlock), 0, s, A.visHdr, order, A.touched, A.bounds,
-                       A.instSums, a.maxInstances, a.tilesX, A.ikeys[0], A.ivals[0]);
-    df_launch_flags(a, A, s);
-}
-
-void df_launch_flags(const DfArgs& a, const DfArena& A, hipStream_t s) {
-    uint32_t blocks = (a.maxInstances + 255u) / 256u;  // grid-stride over the device-side total
-    if (blocks > 8192u) blocks = 8192u;
-    if (blocks == 0) return;
-    hipLaunchKernelGGL(k_df_flags, dim3(blocks), dim3(256), 0, s, A.instHdr, A.ikeys[0], A.ivals[0], A.renderData,
-                       a.tilesX);
+    hipLaunchKernelGGL(k_df_expand, dim3(blocks), dim3(kDfBlock), 0, s, A.visHdr, order, A.touched, A.bounds,
+                       A.instSums, A.renderData, a.maxInstances, a.tilesX, A.ikeys[0], A.ivals[0]);
 }
 
 void df_launch_ranges(const uint32_t* sortedTiles, const DfArgs& a, const DfArena& A, hipStream_t s) {
@@ -881,17 +722,10 @@ void df_launch_blend(const uint32_t* sortedGids, const DfArgs& a, const DfArena&
     const uint32_t need = (2u * a.tileCount + kDfBlendWaves - 1) / kDfBlendWaves;
     if (grid > need) grid = need;
     if (grid == 0) return;
-    // GSM_DF_BLEND=pair: one wave per tile for both eyes (A/B); default: one wave per (tile, eye).
-    // GSM_DF_PRIO=0 / GSM_DF_SPLIT=0 switch off the age priority / top-priority long first units.
-    const char* pv = getenv("GSM_DF_PRIO");
-    const char* sp = getenv("GSM_DF_SPLIT");
-    const int flags = ((pv && pv[0] == '0') ? 0 : 1) | ((sp && sp[0] == '0') ? 0 : 2);
-    const char* v = getenv("GSM_DF_BLEND");
-    if (v && v[0] == 'p')
-        hipLaunchKernelGGL(k_df_blend<kDfBlendWaves>, dim3(grid), dim3(kDfBlendWaves * 64), 0, s, A.starts,
-                           sortedGids, A.renderData, A.expTable, A.queue, a.tilesX, a.tileCount, (uint32_t)a.width,
-                           (uint32_t)a.height, (uint8_t*)color, pitch, colorFormat);
-    else if (A.blendStats)
+    // one wave per (tile, eye); age-raised priority (bit 0) and the longest first units on one
+    // top-priority wave per SIMD (bit 1), as the Global blend
+    const int flags = 1 | 2;
+    if (A.blendStats)
         hipLaunchKernelGGL((k_df_blend_eye<kDfBlendWaves, true>), dim3(grid), dim3(kDfBlendWaves * 64), 0, s,
                            A.starts, sortedGids, A.renderData, A.expTable, A.queue, a.tilesX, a.tileCount,
                            (uint32_t)a.width, (uint32_t)a.height, (uint8_t*)color, pitch, colorFormat,

@@ -68,6 +68,23 @@ struct DeviceArena {
     float2* sincosTable = nullptr;             // [65536]
 };
 
+// A/B switches of the frame pipeline.  Read ONCE, when a renderer is created (tuning_from_env),
+// never per frame; every setting renders the same image, only the schedule differs.
+struct Tuning {
+    bool fullRadix = false;   // GSM_SORT=radix4: 4 x 8-bit passes over (tile << 16 | depth) keys instead
+                              // of the tile passes + per-tile depth sort
+    bool ballotRank = false;  // stable ranks from ballot matches instead of lane-ordered LDS atomics:
+                              // set when the create-time device probe (sort_lane_ordered_atomics) fails,
+                              // or forced by GSM_SORT_RANK=ballot
+    bool costOrder = true;    // GSM_BLEND_SCHED=0: blend units in index order instead of last frame's walks
+};
+// the environment's settings plus the device probe; `device` is a HIP device id
+Tuning tuning_from_env(int device);
+// Create-time probe of the one undocumented hardware property the default sort ranks rely on:
+// the lanes of one ds_add_rtn_u32 that hit the same LDS address receive their old values in lane
+// order.  Runs a small kernel once per device and process (cached); false -> ballot ranks.
+bool sort_lane_ordered_atomics(int device);
+
 constexpr int kProjectBlock = 256;
 constexpr int kRadixBlock = 256;
 constexpr int kRadixItems = 16;  // keys per thread per chunk (4096-key chunks)
@@ -100,34 +117,33 @@ void launch_headers(const uint32_t* sortedKeys, const FrameGeometry& geo, const 
 // front-to-back fp16 blend + clear (GlobalShaders.metal:140-154, 1030-1187)
 void launch_blend(const uint32_t* sortedVals, const FrameGeometry& geo, const DeviceArena& A,
                   void* color, size_t colorPitch, void* depth, size_t depthPitch, int numCUs,
-                  bool costOrder, int colorFormat, hipStream_t stream, uint32_t orderEpoch = 0);
+                  bool costOrder, int colorFormat, hipStream_t stream);
 // orders the blend units by the walk lengths the previous frame measured (longest first), so
-// the dynamic queue hands out long units before short ones
-// order[numUnits] <- epoch when done (A.unitOrder holds numUnits + 1 words); launch_blend with
-// the same nonzero epoch needs no stream join (workgroups fall back to index order)
-void launch_unit_order(uint32_t numUnits, const DeviceArena& A, hipStream_t stream, uint32_t epoch);
+// the dynamic queue hands out long units before short ones (A.unitOrder[numUnits])
+void launch_unit_order(uint32_t numUnits, const DeviceArena& A, hipStream_t stream);
 // the same ordering for any cost array (the DepthFirst blend's (tile, eye) units)
 void launch_unit_order_costs(const uint16_t* cost, uint32_t* order, uint32_t numUnits, hipStream_t stream);
 // blend kernel shape: pixel pairs per lane (0 = quadrant kernel) and blend units per tile
 int blend_pairs_per_lane(uint32_t numTiles, int numCUs);
 uint32_t blend_units_per_tile(uint32_t numTiles, int numCUs);
-// whether the blend follows last frame's cost order (few units per wave slot) or index order
-bool blend_schedule_enabled(uint32_t numTiles, int numCUs);
 
 // Stable LSD radix sort of (key, value) pairs; n read from device memory *nPtr.
 // Returns the index (0/1) of the ping-pong buffer holding the result.
+// ballot: ranks from ballot matches (Tuning::ballotRank) instead of lane-ordered LDS atomics.
 int radix_sort_pairs(uint32_t* keys[2], uint32_t* vals[2], const uint32_t* nPtr, uint32_t capacity,
                      int firstDigit, int numDigits, uint32_t* hist, uint32_t* binTotals,
-                     hipStream_t stream);
+                     hipStream_t stream, bool ballot);
 // Stable LSD radix sort by bits [shift, shift + bits) only, in ceil(bits / 8) passes of
 // near-equal digit widths (4..8 bits).  Returns the ping-pong index of the result.
 int radix_sort_bits(uint32_t* keys[2], uint32_t* vals[2], const uint32_t* nPtr, uint32_t capacity,
-                    uint32_t shift, uint32_t bits, uint32_t* hist, uint32_t* binTotals, hipStream_t stream);
+                    uint32_t shift, uint32_t bits, uint32_t* hist, uint32_t* binTotals, hipStream_t stream,
+                    bool ballot);
 uint32_t radix_grid_for_capacity(uint32_t capacity);
 // bytes of the sort workspace (`hist` argument above) for a capacity; zero it once at allocation
 size_t radix_workspace_bytes(uint32_t capacity);
 // stable per-tile sort by the 16-bit depth key of runs already grouped by tile (one wave per tile)
 void tile_depth_sort(uint32_t* keysIn, uint32_t* valsIn, uint32_t* keysOut, uint32_t* valsOut,
-                     const uint32_t* tileStart, uint32_t tileBegin, uint32_t numTiles, hipStream_t stream);
+                     const uint32_t* tileStart, uint32_t tileBegin, uint32_t numTiles, hipStream_t stream,
+                     bool ballot);
 
 }  // namespace gsm

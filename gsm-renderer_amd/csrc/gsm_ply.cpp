@@ -300,6 +300,16 @@ gsm_ply_status load_compressed(const uint8_t* data, size_t size, const Header& h
     for (int k = 0; k < 18; ++k) co[k] = find(chunkOff, kChunk[k]);
     const long oPos = find(vertexOff, "packed_position"), oRot = find(vertexOff, "packed_rotation");
     const long oScale = find(vertexOff, "packed_scale"), oColor = find(vertexOff, "packed_color");
+    // The reader takes 4 bytes at every one of these offsets whatever the declared type (as the
+    // reference's loadUnaligned, PLYLoader.swift:318-334).  A narrower property placed last in its
+    // element would make that read run past the element -- and, for the last chunk or vertex,
+    // past the buffer: such files are rejected instead.
+    for (int k = 0; k < 18; ++k)
+        if (co[k] >= 0 && (size_t)co[k] + 4 > chunkStride)
+            return fail(GSM_PLY_ERR_INSUFFICIENT_DATA, "Compressed PLY chunk property narrower than 4 bytes at the end of the element");
+    for (long o : {oPos, oRot, oScale, oColor})
+        if (o >= 0 && (size_t)o + 4 > vertexStride)
+            return fail(GSM_PLY_ERR_INSUFFICIENT_DATA, "Compressed PLY packed property narrower than 4 bytes at the end of the element");
 
     alloc_records(s, vertexCount);
     s->harmonics.assign(3 * vertexCount, 0.0f);

@@ -94,6 +94,7 @@ gsm_status GlobalRenderer::create(const gsm_renderer_config& cfg, int hipDevice,
         return GSM_ERR_DEVICE_NOT_AVAILABLE;
     }
     r->numCUs_ = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+    r->tuning_ = tuning_from_env(dev);
 
     const size_t G = r->maxGaussians_;
     const size_t cap = r->maxAssignments_;
@@ -123,7 +124,7 @@ gsm_status GlobalRenderer::create(const gsm_renderer_config& cfg, int hipDevice,
     GSM_ALLOC(A.tileStart, ((size_t)r->tileCount_ + 1) * sizeof(uint32_t));
     GSM_ALLOC(A.tileQueue, sizeof(uint32_t));
     GSM_ALLOC(A.unitCost, (size_t)r->tileCount_ * 4 * sizeof(uint16_t));
-    GSM_ALLOC(A.unitOrder, ((size_t)r->tileCount_ * 4 + 1) * sizeof(uint32_t));  // + the ready word
+    GSM_ALLOC(A.unitOrder, (size_t)r->tileCount_ * 4 * sizeof(uint32_t));
     GSM_ALLOC(A.expTable, 65536 * sizeof(uint16_t));
     GSM_ALLOC(A.sincosTable, 65536 * sizeof(float2));
 #undef GSM_ALLOC
@@ -330,25 +331,18 @@ gsm_status GlobalRenderer::runFrame(hipStream_t s, const ProjectArgs& a, uint32_
         hipMemsetAsync(arena_.unitCost, 0, (size_t)units * sizeof(uint16_t), s);
         schedKey_ = key;
     }
-    bool costOrder = units > 0 && blend_schedule_enabled((rowEnd_ - rowBegin_) * tilesX_, numCUs_);
+    const bool costOrder = units > 0 && tuning_.costOrder;
     if (costOrder && !side_) {
         if (hipStreamCreateWithFlags(&side_, hipStreamNonBlocking) != hipSuccess ||
             hipEventCreateWithFlags(&evFrame_, hipEventDisableTiming) != hipSuccess ||
             hipEventCreateWithFlags(&evOrder_, hipEventDisableTiming) != hipSuccess)
             return GSM_ERR_ENCODER_CREATION_FAILED;
     }
-    // GSM_BLEND_JOIN=0: no join back -- the blend checks the order's ready word (epoch) and walks
-    // index order if the side stream has not finished (A/B; default: the stream join)
-    const char* jv = getenv("GSM_BLEND_JOIN");
-    const bool join = !(jv && jv[0] == '0');
-    uint32_t orderEpoch = 0;
     if (costOrder) {
-        orderEpoch_ = orderEpoch_ % 0x7FFFFFu + 1u;
-        orderEpoch = join ? 0u : orderEpoch_;
         hipEventRecord(evFrame_, s);  // after the previous frame's blend wrote the costs
         hipStreamWaitEvent(side_, evFrame_, 0);
-        launch_unit_order(units, arena_, side_, orderEpoch_);
-        if (join) hipEventRecord(evOrder_, side_);
+        launch_unit_order(units, arena_, side_);
+        hipEventRecord(evOrder_, side_);
     }
 
     hipEvent_t* ev = (prof || blendOnly) ? frameEvents(profFrames_) : nullptr;
@@ -377,22 +371,22 @@ gsm_status GlobalRenderer::runFrame(hipStream_t s, const ProjectArgs& a, uint32_
     // Frame sort.  Default: a stable LSD sort by the tile field only
     // (ceil(tileBits / 8) passes), tile starts from the runs, then each tile's run sorted
     // stably by depth by one wave in LDS -- the same order as the reference's 4-pass sort of
-    // (tile << 16 | depth) keys.  GSM_SORT=radix4 keeps the 4 full 8-bit passes (A/B).
-    const char* sv = getenv("GSM_SORT");
-    const bool fullRadix = sv && std::strcmp(sv, "radix4") == 0;
+    // (tile << 16 | depth) keys.  Tuning::fullRadix keeps the 4 full 8-bit passes (A/B).
+    const bool fullRadix = tuning_.fullRadix;
+    const bool ballot = tuning_.ballotRank;
     if (!fullRadix) {
         uint32_t tileBits = 1;
         while (tileBits < 16 && (tileCount_ - 1u) >> tileBits) tileBits++;
         const int res = radix_sort_bits(kb, vb, &arena_.header->totalAssignments, maxAssignments_, 16, tileBits,
-                                        arena_.radixHist, arena_.radixBinTotals, s);
+                                        arena_.radixHist, arena_.radixBinTotals, s, ballot);
         launch_headers(kb[res], g, arena_, s);
         tile_depth_sort(kb[res], vb[res], kb[res ^ 1], vb[res ^ 1], arena_.tileStart, rowBegin_ * tilesX_,
-                        (rowEnd_ - rowBegin_) * tilesX_, s);
+                        (rowEnd_ - rowBegin_) * tilesX_, s, ballot);
         sortedKeys_ = kb[res ^ 1];
         sortedVals_ = vb[res ^ 1];
     } else {
         const int res = radix_sort_pairs(kb, vb, &arena_.header->totalAssignments, maxAssignments_, 0,
-                                         sortPassCount(), arena_.radixHist, arena_.radixBinTotals, s);
+                                         sortPassCount(), arena_.radixHist, arena_.radixBinTotals, s, ballot);
         sortedKeys_ = kb[res];
         sortedVals_ = vb[res];
     }
@@ -401,10 +395,10 @@ gsm_status GlobalRenderer::runFrame(hipStream_t s, const ProjectArgs& a, uint32_
     if (prof) hipEventRecord(ev[4], s);
     if (fullRadix) launch_headers(sortedKeys_, g, arena_, s);  // else done inside the sort
     arena_.blendTrace = (profiling_ & 4) ? traceBuf_ : nullptr;
-    if (costOrder && join) hipStreamWaitEvent(s, evOrder_, 0);
+    if (costOrder) hipStreamWaitEvent(s, evOrder_, 0);
     if (prof || blendOnly) hipEventRecord(ev[5], s);
     launch_blend(sortedVals_, g, arena_, color, colorPitch, depth, depthPitch, numCUs_, costOrder,
-                 (int)config_.color_format, s, orderEpoch);
+                 (int)config_.color_format, s);
     if (prof || blendOnly) hipEventRecord(ev[6], s);
     if (prof || blendOnly) profFrames_++;
     haveTimes_ = profFrames_ > 0;

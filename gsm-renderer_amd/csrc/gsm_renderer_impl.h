@@ -57,6 +57,7 @@ class GlobalRenderer {
     int device_ = -1;
     int numCUs_ = 256;
     gsm_renderer_config config_{};
+    Tuning tuning_{};  // A/B switches, read once at create
     uint32_t maxGaussians_ = 1, maxWidth_ = 1, maxHeight_ = 1;
     uint32_t tilesX_ = 1, tilesY_ = 1, tileCount_ = 1;
     uint32_t rowBegin_ = 0, rowEnd_ = 1;
@@ -66,8 +67,7 @@ class GlobalRenderer {
     static constexpr int kEventRing = 128;  // frames of stage events kept for averaging
     std::vector<hipEvent_t> events_;       // [kEventRing][GSM_STAGE_COUNT + 1]
     uint32_t profFrames_ = 0;
-    uint32_t sampleFrame_ = 0;
-    uint32_t orderEpoch_ = 0;  // frames with a blend schedule (the unit order's ready word)  // frames since setProfiling (blend-event sampling)
+    uint32_t sampleFrame_ = 0;  // frames since setProfiling (blend-event sampling)
     hipEvent_t* frameEvents(uint32_t frame) { return &events_[(frame % kEventRing) * (GSM_STAGE_COUNT + 1)]; }
     int profiling_ = 0;
     bool haveTimes_ = false;

@@ -228,6 +228,7 @@ _SIGNATURES = {
     "gsm_depthfirst_set_profiling": ([C.c_void_p, C.c_int], C.c_int),
     "gsm_depthfirst_stage_times": ([C.c_void_p, C.POINTER(C.c_float), C.c_int], C.c_int),
     "gsm_depthfirst_last_gpu_time": ([C.c_void_p, C.POINTER(C.c_double)], C.c_int),
+    "gsm_debug_sort_rank_probe": ([C.c_int, C.POINTER(C.c_int)], C.c_int),
 }
 
 SPLAT_RECORD_BYTES = 48  # include/gsm_multigpu.h GSM_SPLAT_RECORD_BYTES
@@ -551,6 +552,14 @@ def sort_pairs_u32(keys, values, key_bits: int = 32, stream=None):
     n = int(keys.numel())
     _check(_lib().gsm_sort_pairs_u32(_ptr(keys), _ptr(values), n, int(key_bits), _stream_handle(stream)),
            "gsm_sort_pairs_u32")
+
+
+def sort_rank_probe(device: int = 0) -> bool:
+    """True when the device serves same-address LDS atomics of one wave in lane order (the sorts'
+    default stable ranks); False -> the renderers rank by ballot matches."""
+    out = C.c_int(0)
+    _check(_lib().gsm_debug_sort_rank_probe(int(device), C.byref(out)), "gsm_debug_sort_rank_probe")
+    return bool(out.value)
 
 
 def abi_version() -> int:

@@ -60,8 +60,12 @@ def exchange(send, send_counts, recv, group=None, staged: bool = False) -> int:
     rc = [int(x) for x in recv_counts.tolist()]
     out_bytes = sum(rc) * RECORD_BYTES
     in_bytes = sum(sc) * RECORD_BYTES
-    if recv.numel() < out_bytes:
-        raise ValueError(f"receive buffer holds {recv.numel()} B, {out_bytes} B arriving")
+    # a too-small receive buffer on any rank must stop every rank before the records collective
+    # (one rank raising alone would leave the others blocked in it)
+    short = torch.tensor([1 if recv.numel() < out_bytes else 0], dtype=torch.int32, device=send_counts.device)
+    dist.all_reduce(short, op=dist.ReduceOp.MAX, group=group)
+    if int(short.item()):
+        raise ValueError(f"a receive buffer is too small (this rank: {recv.numel()} B for {out_bytes} B arriving)")
     dist.all_to_all_single(recv[:out_bytes], send[:in_bytes],
                            output_split_sizes=[c * RECORD_BYTES for c in rc],
                            input_split_sizes=[c * RECORD_BYTES for c in sc], group=group)

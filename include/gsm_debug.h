@@ -77,6 +77,13 @@ gsm_status gsm_global_set_tile_rows(gsm_renderer *renderer, uint32_t row_begin, 
  * `stream` before returning. */
 gsm_status gsm_sort_pairs_u32(void *keys, void *values, uint32_t n, uint32_t key_bits, void *stream);
 
+/* The create-time device probe behind the sorts' stable ranks: *lane_ordered = 1 when the lanes
+ * of one ds_add_rtn_u32 that hit the same LDS address on `hip_device` receive their old values in
+ * lane order (the sorts then rank with one LDS atomic per key), 0 when they do not (ranks from
+ * ballot matches).  GSM_SORT_RANK=ballot in the environment at create forces the ballot ranks.
+ * Cached per device and process; no reference counterpart (a gfx950 design choice). */
+gsm_status gsm_debug_sort_rank_probe(int hip_device, int *lane_ordered);
+
 #ifdef __cplusplus
 }
 #endif

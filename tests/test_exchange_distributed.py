@@ -35,13 +35,22 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, n_per, q):
+def _worker(rank, world, port, n_per, q, short_rank=-1):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     send = _records(rank, world, n_per)
     counts = torch.tensor(n_per[rank], dtype=torch.int32)
-    recv = torch.zeros(sum(n_per[r][rank] for r in range(world)) * R + 64, dtype=torch.uint8)
+    need = sum(n_per[r][rank] for r in range(world)) * R
+    recv = torch.zeros(need - R if rank == short_rank else need + 64, dtype=torch.uint8)
+    if short_rank >= 0:  # every rank must raise, none may block in the records collective
+        try:
+            exchange.exchange(send, counts, recv)
+            q.put((rank, -1, False))
+        except ValueError:
+            q.put((rank, 0, True))
+        dist.destroy_process_group()
+        return
     got = exchange.exchange(send, counts, recv)
     sends = [_records(r, world, n_per) for r in range(world)]
     want = exchange.emulate(sends, n_per)[rank]
@@ -68,6 +77,20 @@ def test_gloo_all_to_all_delivers_slab_records_in_rank_order(n_per):
     for rank, got, ok in res:
         assert got == sum(n_per[r][rank] for r in range(world))
         assert ok
+
+
+def test_too_small_receive_buffer_raises_on_every_rank():
+    n_per = [[2, 0, 4], [1, 1, 1], [0, 3, 2]]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 3, port, n_per, q, 1)) for r in range(3)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+    assert all(p.exitcode == 0 for p in procs)
+    assert all(ok for _, _, ok in (q.get(timeout=5) for _ in range(3)))
 
 
 def test_id_ranges_and_slab_rows_cover_everything():

@@ -155,11 +155,19 @@ def test_radix_sort_random_large(gsm, cuda):
         np.testing.assert_array_equal(v.cpu().numpy(), np.argsort(keys, kind="stable"))
 
 
-@pytest.mark.parametrize("variant", ["onesweep", "classic"])
+def test_sort_rank_probe_reports_lane_order(gsm, cuda):
+    """The create-time probe behind the default sort ranks (include/gsm_debug.h): on MI355X the
+    lanes of one same-address ds_add_rtn_u32 are served in lane order (tools/exp/lds_atomic_order.hip);
+    if a driver or firmware changed that, the renderers would switch to ballot ranks by themselves
+    and this test names the change."""
+    assert gsm.sort_rank_probe(0) is True
+
+
+@pytest.mark.parametrize("variant", ["atomic", "ballot"])
 def test_radix_sort_variants(gsm, cuda, variant, monkeypatch):
-    """Both radix schedules (GSM_RADIX, read per sort) give the stable order: the opt-in onesweep
-    passes with decoupled look-back and the default upsweep / scan / downsweep."""
-    monkeypatch.setenv("GSM_RADIX", variant)
+    """Both stable-rank forms (GSM_SORT_RANK, read at create / per stand-alone sort) give the stable
+    order: lane-ordered LDS atomics (default when the probe passes) and ballot matches."""
+    monkeypatch.setenv("GSM_SORT_RANK", variant)
     rng = np.random.default_rng(11)
     for n, bits in [(5, 32), (4096, 12), (4097, 32), (1_000_003, 32), (2_500_000, 14)]:
         keys = rng.integers(0, 2 ** bits, n, dtype=np.uint64).astype(np.uint32)
@@ -366,15 +374,21 @@ def test_stereo_is_unsupported_like_the_reference(gsm, cuda):
     rend.close()
 
 
-def test_join_free_schedule_frames_match(gsm, cuda, oracle, monkeypatch):
-    """GSM_BLEND_JOIN=0: the blend reads the unit order only once k_unit_order's ready word holds
-    this frame's epoch (index order otherwise); every frame stays bit-exact, whichever it took."""
-    monkeypatch.setenv("GSM_BLEND_JOIN", "0")
+@pytest.mark.parametrize("env", [{"GSM_SORT_RANK": "ballot"}, {"GSM_BLEND_SCHED": "0"},
+                                 {"GSM_SORT": "radix4"}])
+def test_create_time_switches_frames_match(gsm, cuda, oracle, monkeypatch, env):
+    """The A/B switches read once at create (Tuning, gsm_internal.h) -- ballot sort ranks, index-order
+    blend schedule, the 4 x 8-bit full-key sort -- render the same frames bit for bit, first and
+    later frames (later ones take last frame's cost order when the schedule is on)."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
     case = _synth(200_000, 1280, 720, 16, 1, 33)
     r = oracle_render(oracle, case)
     g = gpu_render(gsm, cuda, case, keep=False)
+    for k in env:  # read at create: the live renderer keeps its setting
+        monkeypatch.delenv(k)
     assert_frame_equal(g, r)
-    for _ in range(4):  # later frames take last frame's cost order
+    for _ in range(3):
         g2 = gpu_render(gsm, cuda, case, renderer=g["renderer"], keep=False)
         assert np.array_equal(g["color"], g2["color"])
         assert np.array_equal(g["depth"], g2["depth"])

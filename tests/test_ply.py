@@ -145,6 +145,14 @@ BAD = [
     (b"ply\nformat binary_little_endian 1.0\nelement chunk 1\nproperty float min_x\nelement vertex 300\n"
      b"property uint packed_position\nproperty uint packed_rotation\nproperty uint packed_scale\nproperty uint packed_color\n"
      b"end_header\n" + b"\0" * (4 + 300 * 16), "INSUFFICIENT_DATA"),
+    # a property read as 4 bytes but declared narrower, last in its element: the read would run past
+    # the end of the file (the reference reads it unchecked, PLYLoader.swift:318-334)
+    (b"ply\nformat binary_little_endian 1.0\nelement chunk 1\nproperty float min_y\nproperty ushort min_x\n"
+     b"element vertex 1\nproperty uint packed_position\nproperty uint packed_rotation\nproperty uint packed_scale\n"
+     b"property uint packed_color\nend_header\n" + b"\0" * (6 + 16), "INSUFFICIENT_DATA"),
+    (b"ply\nformat binary_little_endian 1.0\nelement chunk 1\nproperty float min_x\n"
+     b"element vertex 1\nproperty uint packed_position\nproperty uint packed_rotation\nproperty uint packed_scale\n"
+     b"property uchar packed_color\nend_header\n" + b"\0" * (4 + 13), "INSUFFICIENT_DATA"),
 ]
 
 

@@ -1,0 +1,104 @@
+// Probe (not part of the product): the VALU issue peak that prices the blend's roofline_valu.
+//
+// Every wave runs ITERS x 16 copies of ONE vector instruction on 8 independent accumulators
+// (inline asm, so the count and the opcode are exact), with 1, 2, 4 and 8 waves per SIMD on every
+// CU.  Reported per (instruction, waves/SIMD): chip-wide wave-instructions per ns (HIP events over
+// the launch) and the implied cycles per instruction per SIMD at the clock measured in-kernel from
+// s_memtime (shader clock) against s_memrealtime (100 MHz constant).
+//   hipcc --offload-arch=gfx950 -O3 -o valu_peak valu_peak.hip && ./valu_peak
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+
+constexpr int ITERS = 2048;
+
+#define REP8(X) X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
+
+template <int OP>
+__global__ void k_peak(unsigned* out, unsigned long long* clk) {
+    unsigned a0 = threadIdx.x, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4, a5 = a0 + 5, a6 = a0 + 6,
+             a7 = a0 + 7;
+    const unsigned m = 0x3C003C01u, c = 0x00010001u;
+    const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+    const unsigned long long r0 = __builtin_amdgcn_s_memrealtime();
+    for (int it = 0; it < ITERS; ++it) {
+#pragma unroll
+        for (int rep = 0; rep < 2; ++rep) {
+#define ACC(i)                                                                                                 \
+    if (OP == 0) asm volatile("v_pk_mul_f16 %0, %0, %1" : "+v"(a##i) : "v"(m));                              \
+    if (OP == 1) asm volatile("v_pk_add_f16 %0, %0, %1" : "+v"(a##i) : "v"(m));                              \
+    if (OP == 2) asm volatile("v_pk_fma_f16 %0, %0, %1, %2" : "+v"(a##i) : "v"(m), "v"(c));                  \
+    if (OP == 3) asm volatile("v_mul_f32 %0, %0, %1" : "+v"(a##i) : "v"(m));                                 \
+    if (OP == 4) asm volatile("v_fma_f32 %0, %0, %1, %2" : "+v"(a##i) : "v"(m), "v"(c));                     \
+    if (OP == 5) asm volatile("v_add_u32 %0, %0, %1" : "+v"(a##i) : "v"(m));                                 \
+    if (OP == 6) asm volatile("v_pk_max_u16 %0, %0, %1" : "+v"(a##i) : "v"(m));
+            REP8(ACC)
+#undef ACC
+        }
+    }
+    const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+    const unsigned long long r1 = __builtin_amdgcn_s_memrealtime();
+    out[blockIdx.x * blockDim.x + threadIdx.x] = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7;
+    if (threadIdx.x == 0) {
+        clk[2 * blockIdx.x] = t1 - t0;
+        clk[2 * blockIdx.x + 1] = r1 - r0;
+    }
+}
+
+template <int OP>
+static void run(const char* name, int cus, unsigned* out, unsigned long long* clk) {
+    for (int wps = 1; wps <= 8; wps *= 2) {
+        // waves per CU = 4 * wps, in workgroups of at most 1024 threads
+        const int threads = 64 * 4 * wps;
+        const int block = threads > 1024 ? 1024 : threads;
+        const int perCU = threads / block;
+        const dim3 grid(cus * perCU);
+        float best = 1e30f;
+        double ghz = 0;
+        for (int rep = 0; rep < 3; ++rep) {
+            hipEvent_t a, b;
+            hipEventCreate(&a);
+            hipEventCreate(&b);
+            hipEventRecord(a);
+            hipLaunchKernelGGL(k_peak<OP>, grid, dim3(block), 0, 0, out, clk);
+            hipEventRecord(b);
+            hipEventSynchronize(b);
+            float ms = 0;
+            hipEventElapsedTime(&ms, a, b);
+            if (ms < best) {
+                best = ms;
+                unsigned long long h[2];
+                hipMemcpy(h, clk, 16, hipMemcpyDeviceToHost);
+                ghz = (double)h[0] / ((double)h[1] * 10.0);  // s_memtime ticks per ns (memrealtime 100 MHz)
+            }
+            hipEventDestroy(a);
+            hipEventDestroy(b);
+        }
+        const double waveInstr = (double)grid.x * (block / 64) * ITERS * 16.0;
+        const double perNs = waveInstr / (best * 1e6);
+        const double simds = cus * 4.0;
+        // cycles per wave-instruction per SIMD at the in-kernel clock
+        const double cyc = simds * ghz / perNs;
+        printf("%-14s waves/SIMD=%d  %8.1f G wave-instr/s  clock %.2f GHz  %5.2f cycles/instr/SIMD\n", name, wps,
+               perNs, ghz, cyc);
+    }
+}
+
+int main() {
+    hipDeviceProp_t p;
+    hipGetDeviceProperties(&p, 0);
+    const int cus = p.multiProcessorCount;
+    unsigned* out;
+    unsigned long long* clk;
+    hipMalloc(&out, (size_t)cus * 2048 * 4);
+    hipMalloc(&clk, (size_t)cus * 2 * 16);
+    printf("%s, %d CUs\n", p.name, cus);
+    run<0>("v_pk_mul_f16", cus, out, clk);
+    run<1>("v_pk_add_f16", cus, out, clk);
+    run<2>("v_pk_fma_f16", cus, out, clk);
+    run<3>("v_mul_f32", cus, out, clk);
+    run<4>("v_fma_f32", cus, out, clk);
+    run<5>("v_add_u32", cus, out, clk);
+    run<6>("v_pk_max_u16", cus, out, clk);
+    return 0;
+}

@@ -33,7 +33,17 @@ sys.path.insert(0, os.path.join(ROOT, "gsm-renderer_amd"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec); measured copy ceiling ~6290
 BLEND_EVENT_PERIOD = 5  # timed frames per bracketed blend (HIP events), see the timed loop
-VALU_PEAK_GIPS = 1024 * 2.4 / 4  # wave64 packed-fp16 VALU instructions per ns, whole chip
+# Packed-fp16 VALU issue peak (the blend's bound), measured by tools/exp/valu_peak.hip
+# (profiles/r02_valu_peak.txt): independent v_pk_fma_f16 on every SIMD reach 566 G wave-instr/s
+# at 8 waves per SIMD (4.19 cycles per instruction at the 2.3 GHz held under load; 32-bit VALU
+# ops issue at ~2.3 cycles, so packed 16-bit ops issue at half their rate).  At the 2 waves per
+# SIMD the Global blend runs with (one 512-thread workgroup per CU) the same probe reaches 509
+# (v_pk_fma) / 400 (v_pk_mul).  Spec-derived ceiling: 1024 SIMDs x 2.4 GHz / 4 cycles = 614.4.
+VALU_PEAK_GIPS = 566.0
+VALU_PEAK_SPEC_GIPS = 1024 * 2.4 / 4
+VALU_PEAK_2WPS_GIPS = 508.5
+# FETCH_SIZE corrections calibrated on MI355X (tools/exp/fetch_calib.hip, profiles/r02_fetch_calibration.json)
+FETCH_TABLE_RAW_BYTES = 514.5 * 1024  # the blend's 128 KiB LDS table load: 8 XCD L2 misses, tallied at 1/2
 
 
 def parse():
@@ -44,18 +54,24 @@ def parse():
     p.add_argument("--config", default="cfg2_1m_sh3_1080p_f16")
     p.add_argument("--cpu-baseline", type=int, default=1, help="time the C oracle (rank 0, N=1)")
     p.add_argument("--cpu-threads", type=int, default=16)
+    p.add_argument("--cpu-one-thread", type=int, default=1, help="also time one oracle frame on 1 thread (<= 1M)")
+    p.add_argument("--orbit-steps", type=int, default=50,
+                   help="moving-camera frames timed after the static ones (single GPU, mono); 0 = off")
     p.add_argument("--parity", type=int, default=1, help="compare the frame with the oracle")
-    p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"),
-                   help="blend HBM bytes and VALU instructions per launch (tools/traffic.py)")
+    p.add_argument("--traffic-json", default=None,
+                   help="blend PMC numbers per launch (tools/traffic.py), used when measured on --config; "
+                        "default profiles/PMC_TAG_pmc_blend_<cfgN>.json")
+    p.add_argument("--pmc-tag", default="r02", help="round tag of the default PMC files in profiles/")
     p.add_argument("--stereo-path", choices=("depthfirst", "global"), default="depthfirst",
                    help="stereo configs: DepthFirst semantics (SURVEY 8f rank 1) or two Global views")
-    p.add_argument("--traffic-json-df", default=os.path.join(ROOT, "profiles", "traffic_cfg5_r01.json"),
-                   help="blend PMC traffic / VALU count of the DepthFirst config (tools/gpu_df_pmc.sh)")
     p.add_argument("--df-max-gaussians", type=int, default=6_000_000,
                    help="DepthFirst RendererConfig.maxGaussians (reference default 6M -> 24M instances)")
     p.add_argument("--multi", choices=("alltoall", "replicas"), default="alltoall",
                    help="N>1 partition: all-to-all of projected records (8e) or projection replicas")
-    return p.parse_args()
+    a = p.parse_args()
+    if a.traffic_json is None:
+        a.traffic_json = os.path.join(ROOT, "profiles", f"{a.pmc_tag}_pmc_blend_{a.config.split('_')[0]}.json")
+    return a
 
 
 def main():
@@ -150,22 +166,7 @@ def main():
     # timed region: only the blend (the roofline kernel) is bracketed by HIP events on the render
     # stream -- two events on every BLEND_EVENT_PERIOD-th frame (each bracketed frame costs ~10 us
     # of event overhead, tools/exp_events.py); the per-stage breakdown comes from a separate pass below
-    renderer.set_profiling(stage_events=False, blend_events=True, blend_event_period=BLEND_EVENT_PERIOD)
-    torch.cuda.synchronize()
-    if world_size > 1:
-        dist.barrier()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    if world_size > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if world_size > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    blend_ms_timed = renderer.stage_times_ms()["blend"]
+    elapsed, blend_ms_timed = timed_loop(args.steps, step, renderer, world_size, dev)
     # per-stage breakdown: 10 more frames with every stage bracketed (not part of `value`)
     renderer.set_profiling(stage_events=True)
     for _ in range(10):
@@ -176,6 +177,27 @@ def main():
     counters = renderer.counters()
     ms_per_step = elapsed / args.steps * 1e3
     fps = 1e3 / ms_per_step
+    # the same frame under camera motion (single GPU, mono): every step a new view, 0.25 degrees
+    # further along an orbit about the scene centre, so the blend schedule (last frame's walk
+    # lengths, k_unit_order) is always one frame stale -- what the static `value` cannot show
+    orbit = None
+    orbit_last_cam = None
+    if world_size == 1 and not stereo and args.orbit_steps > 0:
+        cams = [gsm_amd.CameraParams.from_dict(scenes.orbit_camera(W, H, 0.25 * (i + 1)))
+                for i in range(args.warmup + args.orbit_steps)]
+        it = iter(cams)
+
+        def step_orbit():
+            renderer.render(cptr, dptr, inp, next(it), W, H, stream=stream, color_pitch=pitch_c,
+                            depth_pitch=pitch_d)
+        for _ in range(args.warmup):
+            step_orbit()
+        o_elapsed, o_blend = timed_loop(args.orbit_steps, step_orbit, renderer, 1, dev)
+        orbit_last_cam = scenes.orbit_camera(W, H, 0.25 * (args.warmup + args.orbit_steps))
+        orbit = {"value": args.orbit_steps / o_elapsed, "unit": "frames/s", "steps": args.orbit_steps,
+                 "ms_per_step": o_elapsed / args.orbit_steps * 1e3, "blend_ms": o_blend,
+                 "camera": "orbit about (0, 0, 5.5), +0.25 deg about y per frame (scenes.orbit_camera)",
+                 "parity_last_frame": None}
 
     if rank != 0:
         renderer.close()
@@ -190,17 +212,27 @@ def main():
     b_blend = A * 20 + P * 10 + T * 8
     t_blend = blend_ms_timed * 1e-3
     achieved = b_blend / t_blend / 1e9 if t_blend > 0 else 0.0
-    traffic = None
-    valu_insts = None
-    if os.path.exists(args.traffic_json):
-        try:
-            with open(args.traffic_json) as f:
-                tj = json.load(f)
-            if tj.get("config") == args.config and world_size == 1:  # measured on this workload only
-                traffic = tj.get("blend_hbm_bytes_per_launch")
-                valu_insts = tj.get("blend_valu_insts_per_launch")
-        except Exception:
-            traffic = None
+    # blend units per tile (gsm_blend.hip blend_pairs_per_lane): half tiles while the frame's tiles
+    # outnumber 8 waves x CUs, quadrants otherwise; every unit reads the tile's whole list
+    n_cus = torch.cuda.get_device_properties(dev).multi_processor_count
+    units_per_tile = 2 if T > 8 * n_cus else 4
+    traffic = valu_insts = traffic_note = None
+    tj = load_pmc(args.traffic_json, args.config, world_size, "k_blend_px")
+    if tj:
+        raw_fetch = tj["fetch_size_kib"] * 1024
+        write = tj["write_size_kib"] * 1024
+        # the wide parts of the blend's reads are doubled (FETCH counts half of a wide stream):
+        # the table prologue (calibrated raw bytes) and the tile lists (4 B/lane coalesced, read
+        # once per unit); the record gathers (random 16 B + 4 B) count one 64-B unit per
+        # fetched segment and stay as counted (tools/exp/fetch_calib.hip)
+        list_bytes = units_per_tile * A * 4
+        traffic = int(raw_fetch + FETCH_TABLE_RAW_BYTES + list_bytes / 2 + write)
+        traffic_note = (f"FETCH_SIZE {tj['fetch_size_kib']:.0f} KiB + WRITE_SIZE {tj['write_size_kib']:.0f} KiB "
+                        f"per launch ({tj['source']}); wide parts doubled: table {FETCH_TABLE_RAW_BYTES:.0f} B, "
+                        f"lists {list_bytes // 2} B; gathers as counted (profiles/r02_fetch_calibration.json); "
+                        f"upper bound if every gather segment were 128 B: {int(2 * raw_fetch + write)} B")
+        valu_insts = tj.get("valu_insts_per_launch")
+    stage_sum = sum(v for k, v in stage_ms.items() if k != "blend_timed_region")
     sort_gkeys = A / (stage_ms["sort"] * 1e-3) / 1e9 if stage_ms["sort"] > 0 else 0.0
 
     parity = None
@@ -218,17 +250,34 @@ def main():
             refs = [O.render(world_np, harm_np, sh, cv, W, H, max_gaussians=n, nthreads=threads) for cv in views]
             times.append(time.perf_counter() - t)
         if args.parity:
+            if orbit is not None:  # the buffer holds the last orbit frame: check it, then redo the static one
+                ro = O.render(world_np, harm_np, sh, orbit_last_cam, W, H, max_gaussians=n, nthreads=threads)
+                got = color[:H].view(torch.int16).cpu().numpy().view(np.uint16)
+                orbit["parity_last_frame"] = bool(np.array_equal(got, ro["color"]))
+                renderer.render(cptr, dptr, inp, cam, W, H, stream=stream, color_pitch=pitch_c, depth_pitch=pitch_d)
+                torch.cuda.synchronize()
             got = color[:H].view(torch.int16).cpu().numpy().view(np.uint16)
             parity = all(bool(np.array_equal(got[:, v * W:(v + 1) * W], r["color"])) for v, r in enumerate(refs)) \
                 and int(refs[-1]["total_assignments"]) == A
         if args.cpu_baseline:
             med = float(np.median(times))
-            cpu = {"value": 1.0 / med, "unit": "frames/s", "cores": threads, "kind": "port",
-                   "sample": f"{reps} full frames of {args.config} ({n} gaussians, {len(views)} view(s) of "
-                             f"{W}x{H}) with the C oracle (oracle/gsm_oracle.c, pthreads), median "
-                             f"{med:.2f} s/frame",
-                   "stages_s": {k: round(v, 4) for k, v in refs[-1]["times"].items()}}
+            cpu = cpu_baseline_entry(med, threads, f"{reps} full frames of {args.config} ({n} gaussians, "
+                                     f"{len(views)} view(s) of {W}x{H}) with the C oracle (oracle/gsm_oracle.c, "
+                                     f"pthreads), median {med:.2f} s/frame", refs[-1]["times"])
+            if args.cpu_one_thread and not stereo and n <= 1_000_000:
+                t = time.perf_counter()
+                O.render(world_np, harm_np, sh, cam_d, W, H, max_gaussians=n, nthreads=1)
+                t1 = time.perf_counter() - t
+                cpu["one_thread"] = {"value": 1.0 / t1, "unit": "frames/s", "cores": 1,
+                                     "sample": f"1 full frame of {args.config}, 1 thread, {t1:.2f} s"}
 
+    # SURVEY.md 8(d) B_frame: the minimal dataflow of one frame (inputs of all N, SH of the visible
+    # V, render data, assignment write, K = 4 sort passes of key + value read and write, blend reads,
+    # targets, headers), against the whole frame's time
+    V = visible_count(renderer, gsm_amd)
+    s_w = 32 if prec else 48
+    s_sh = 3 * sh * (2 if prec else 4)
+    b_frame = n * s_w + V * s_sh + V * 16 + A * 8 + 4 * A * 16 + A * 20 + P * 10 + T * 8
     out = {
         "metric": "frames/sec @ N Gaussians × W×H (1/2/4/8 GPU); sort Gkeys/s; blend HBM GB/s",
         "value": fps,
@@ -246,34 +295,99 @@ def main():
                                f"{'2x' if stereo else ''}{W}x{H}{' side-by-side stereo' if stereo else ''} "
                                f"{'fp16 PackedWorldGaussianHalf' if prec else 'fp32 PackedWorldGaussian'}",
                    "gaussians": n, "width": W, "height": H, "sh_components": sh,
-                   "assignments": A, "tiles": T,
+                   "visible": V, "assignments": A, "tiles": T,
                    "parallelism": (f"dp{world_size} tile-row slabs, "
                                    + ("all-to-all of projected records" if alltoall else "projection replicas"))
                                   if world_size > 1 else "single GPU"},
-        "roofline": {"bound": "hbm", "kernel": "k_blend", "achieved": achieved, "peak": HBM_PEAK_GBS,
+        "roofline": {"bound": "hbm", "kernel": "k_blend_px", "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "traffic_over_algorithmic": (traffic / b_blend) if traffic else None,
+                     "traffic_note": traffic_note,
                      "algorithmic_bytes": b_blend, "launch_timing": f"HIP events around the blend on every {BLEND_EVENT_PERIOD}th frame of the timed region", "avg_launch_ms": blend_ms_timed,
-                     "note": "blend is VALU/LDS-bound (fp16 math per pixel per entry); HBM fraction "
+                     "note": "blend is bound by packed-fp16 VALU issue (roofline_valu); HBM fraction "
                              "reported per the metric"},
-        # the blend's real bound: packed-fp16 VALU issue.  Peak = 1024 SIMDs x one wave64
-        # v_pk_* instruction per 4 cycles x 2.4 GHz (measured issue cost of v_pk_mul_f16 with
-        # >= 2 waves per SIMD: tools/exp/valu_lat.hip); instructions per launch from the
-        # SQ_INSTS_VALU PMC pass of tools/gpu_round.sh (config 2 only).
-        "roofline_valu": ({"bound": "valu", "kernel": "k_blend", "unit": "G wave-instr/s",
+        "roofline_valu": ({"bound": "valu", "kernel": "k_blend_px", "unit": "G wave-instr/s",
                            "achieved": valu_insts / t_blend / 1e9, "peak": VALU_PEAK_GIPS,
                            "frac": valu_insts / t_blend / 1e9 / VALU_PEAK_GIPS,
-                           "insts_per_launch": valu_insts}
+                           "frac_of_peak_at_2_waves_per_simd": valu_insts / t_blend / 1e9 / VALU_PEAK_2WPS_GIPS,
+                           "frac_of_spec_peak": valu_insts / t_blend / 1e9 / VALU_PEAK_SPEC_GIPS,
+                           "insts_per_launch": valu_insts,
+                           "peak_source": "tools/exp/valu_peak.hip, profiles/r02_valu_peak.txt"}
                           if (valu_insts and t_blend > 0) else None),
+        "roofline_frame": {"bound": "hbm", "achieved": b_frame / (ms_per_step * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
+                           "unit": "GB/s", "frac": b_frame / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                           "algorithmic_bytes": b_frame,
+                           "formula": "N*S_w + V*S_sh + V*16 + A*8 + 4*A*16 + A*20 + P*10 + T*8 (SURVEY.md 8d)"},
         "cpu_baseline": cpu,
         "stages_ms": stage_ms,
+        "stages_sum_ms": stage_sum,
         "sort_gkeys_per_s": sort_gkeys,
         "blend_gb_per_s": achieved,
+        "orbit": orbit,
         "parity_vs_oracle": parity,
     }
     print(json.dumps(out))
     renderer.close()
     if world_size > 1:
         dist.destroy_process_group()
+
+
+def timed_loop(steps, step, renderer, world_size, dev):
+    """K steps between barriers and device syncs; returns (max-over-ranks seconds, blend ms)."""
+    import torch
+    import torch.distributed as dist
+    renderer.set_profiling(stage_events=False, blend_events=True, blend_event_period=BLEND_EVENT_PERIOD)
+    torch.cuda.synchronize()
+    if world_size > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    if world_size > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world_size > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    return elapsed, renderer.stage_times_ms()["blend"]
+
+
+def load_pmc(path, config, world_size, kernel):
+    """PMC numbers of tools/traffic.py, only when measured on this very workload and kernel."""
+    if not path or not os.path.exists(path) or world_size != 1:
+        return None
+    try:
+        with open(path) as f:
+            tj = json.load(f)
+    except Exception:
+        return None
+    ok = tj.get("config") == config and "fetch_size_kib" in tj and kernel in tj.get("kernel", "")
+    return tj if ok else None
+
+
+def visible_count(renderer, gsm_amd):
+    """V of SURVEY 8(d): gaussians that passed every cull (non-empty tile rect) in the last frame."""
+    b = renderer.copy_buffer(gsm_amd.BufferId.BOUNDS).reshape(-1, 4)
+    return int(np.count_nonzero((b[:, 0] <= b[:, 1]) & (b[:, 2] <= b[:, 3])))
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
+def cpu_baseline_entry(median_s, threads, sample, stage_times):
+    return {"value": 1.0 / median_s, "unit": "frames/s", "cores": threads, "kind": "port",
+            "host_cpus": os.cpu_count(), "cpu_model": cpu_model(), "sample": sample,
+            "stages_s": {k: round(v, 4) for k, v in stage_times.items()}}
 
 
 def run_depthfirst(args, c, world_np, harm_np, world, harm, dev):
@@ -324,17 +438,16 @@ def run_depthfirst(args, c, world_np, harm_np, world, harm, dev):
     b_blend = A * 36 + P * 8 + T * 8
     t_blend = blend_ms_timed * 1e-3
     achieved = b_blend / t_blend / 1e9 if t_blend > 0 else 0.0
-    traffic, valu_insts = None, None
-    tj_path = args.traffic_json_df
-    if os.path.exists(tj_path):
-        try:
-            with open(tj_path) as f:
-                tj = json.load(f)
-            if tj.get("config") == args.config:  # measured on this workload only
-                traffic = tj.get("blend_hbm_bytes_per_launch")
-                valu_insts = tj.get("blend_valu_insts_per_launch")
-        except Exception:
-            traffic = None
+    traffic = valu_insts = traffic_note = None
+    tj = load_pmc(args.traffic_json, args.config, 1, "k_df_blend_eye")
+    if tj:
+        raw_fetch, write = tj["fetch_size_kib"] * 1024, tj["write_size_kib"] * 1024
+        list_bytes = 2 * A * 4  # one unit per (tile, eye): each tile list is read twice
+        traffic = int(raw_fetch + FETCH_TABLE_RAW_BYTES + list_bytes / 2 + write)
+        traffic_note = (f"FETCH_SIZE {tj['fetch_size_kib']:.0f} KiB + WRITE_SIZE {tj['write_size_kib']:.0f} KiB per "
+                        f"launch; wide parts doubled (table, lists), gathers as counted "
+                        f"(profiles/r02_fetch_calibration.json); upper bound {int(2 * raw_fetch + write)} B")
+        valu_insts = tj.get("valu_insts_per_launch")
     parity, cpu = None, None
     if args.parity or args.cpu_baseline:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -351,10 +464,9 @@ def run_depthfirst(args, c, world_np, harm_np, world, harm, dev):
             parity = bool(np.array_equal(got, ref["color"])) and int(ref["total_instances"]) == A
         if args.cpu_baseline:
             med = float(np.median(times))
-            cpu = {"value": 1.0 / med, "unit": "frames/s", "cores": threads, "kind": "port",
-                   "sample": f"{len(times)} full DepthFirst stereo frames of {args.config} with the C oracle "
-                             f"(og_df_render_stereo, pthreads), median {med:.2f} s/frame",
-                   "stages_s": {k: round(v, 4) for k, v in ref["times"].items()}}
+            cpu = cpu_baseline_entry(med, threads, f"{len(times)} full DepthFirst stereo frames of {args.config} "
+                                     f"with the C oracle (og_df_render_stereo, pthreads), median {med:.2f} s/frame",
+                                     ref["times"])
     out = {
         "metric": "frames/sec @ N Gaussians × W×H (1/2/4/8 GPU); sort Gkeys/s; blend HBM GB/s",
         "value": 1e3 / ms_per_step, "unit": "frames/s", "n_gpus": 1, "steps": args.steps,
@@ -368,8 +480,9 @@ def run_depthfirst(args, c, world_np, harm_np, world, harm, dev):
                    "parallelism": "single GPU"},
         "roofline": {"bound": "hbm", "kernel": "k_df_blend_eye", "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "traffic_over_algorithmic": (traffic / b_blend) if traffic else None, "traffic_note": traffic_note,
                      "algorithmic_bytes": b_blend, "launch_timing": f"HIP events around the blend on every {BLEND_EVENT_PERIOD}th frame of the timed region", "avg_launch_ms": blend_ms_timed,
-                     "note": "blend is VALU/LDS-bound (fp16 math per pixel per (tile, eye) unit)"},
+                     "note": "blend is bound by packed-fp16 VALU issue (fp16 math per pixel per (tile, eye) unit)"},
         "roofline_valu": ({"bound": "valu", "kernel": "k_df_blend_eye", "unit": "G wave-instr/s",
                            "achieved": valu_insts / t_blend / 1e9, "peak": VALU_PEAK_GIPS,
                            "frac": valu_insts / t_blend / 1e9 / VALU_PEAK_GIPS, "insts_per_launch": valu_insts}

@@ -79,8 +79,9 @@ __global__ __launch_bounds__(NT) void k_blend_px(
     uint32_t numTiles, uint32_t tilesX, uint32_t W, uint32_t H, uint8_t* __restrict__ color,
     size_t colorPitch, uint8_t* __restrict__ depth, size_t depthPitch, int flags,
     const uint32_t* __restrict__ order, uint16_t* __restrict__ unitCost,
-    unsigned long long* __restrict__ trace) {
-    static_assert(P == 1 || P == 2 || P == 4, "pairs per lane");
+    unsigned long long* __restrict__ trace, const uint32_t* __restrict__ half0,
+    const uint32_t* __restrict__ half1, const uint32_t* __restrict__ halfCount, uint32_t tileCount) {
+    static_assert(P == 1 || P == 2, "pairs per lane: quadrant or half-tile units (half-tile lists)");
     static_assert(!COMPACT || P == 2, "compaction: half tiles");
     constexpr uint32_t U = (P == 2 && kBlendU4) ? 4 : 4 / P;  // entries per pipeline group
     constexpr uint32_t NG = 64 / U;      // groups per 64-entry batch
@@ -212,8 +213,12 @@ __global__ __launch_bounds__(NT) void k_blend_px(
         const uint32_t tileX = tile % tilesX, tileY = tile / tilesX;
         const uint32_t ux = tileX * kTileWidth + (P == 4 ? 0u : (part & 1u) * 16u);
         const uint32_t uy = tileY * kTileHeight + (P == 1 ? (part >> 1) * 8u : 0u);
+        // the unit walks its half's list: the tile's sorted entries without those whose skip flag for
+        // this half is set (k_scatter, k_half_lists) -- they would leave every pixel of it unchanged
         const uint32_t start = __builtin_amdgcn_readfirstlane(tileStart[tile]);
-        const uint32_t count = __builtin_amdgcn_readfirstlane(tileStart[tile + 1]) - start;
+        const uint32_t full = __builtin_amdgcn_readfirstlane(tileStart[tile + 1]) - start;
+        const uint32_t hsel = part & 1u;
+        const uint32_t count = __builtin_amdgcn_readfirstlane(halfCount[hsel * tileCount + tile]);
         unsigned long long tStart = 0;
         if (trace) tStart = __builtin_amdgcn_s_memrealtime();
         uint32_t nproc = 0;
@@ -231,7 +236,7 @@ __global__ __launch_bounds__(NT) void k_blend_px(
 #pragma unroll
             for (int k = 0; k < P; ++k) X[k] = h2{(h1)(float)(ux + offX[k]), (h1)(float)(ux + offX[k] + 1u)};
             Yv = h2{(h1)(float)(uy + offY[0]), (h1)(float)(uy + offY[P - 1])};
-            const uint32_t* lst = sortedVals + start;
+            const uint32_t* lst = (hsel ? half1 : half0) + start;
             // Batch registers: lane l of bA/bB holds list entry b0 + l, nA/nB entry b0 + 64 + l,
             // mA/mB entry b0 + 128 + l, nI the index of entry b0 + 192 + l.  Loads are
             // unpredicated (clamped index) and issued one batch ahead of their first use, so
@@ -548,7 +553,7 @@ __global__ __launch_bounds__(NT) void k_blend_px(
         // write (GlobalShaders.metal:1152-1186); empty tiles keep the clear colour (0,0,0,1)
 #pragma unroll
         for (int q = 0; q < P; ++q)
-            write_pair(ux + offX[q], uy + offY[q], (count > 0) ? (ONE - T[q]) : ONE, R[q], G[q], B[q], D[q]);
+            write_pair(ux + offX[q], uy + offY[q], (full > 0) ? (ONE - T[q]) : ONE, R[q], G[q], B[q], D[q]);
     unit_end:
         if (unitCost && lane == 0) unitCost[u] = (uint16_t)min(nproc, 65535u);
         if (trace && lane == 0) {
@@ -681,7 +686,7 @@ void launch_unit_order_costs(const uint16_t* cost, uint32_t* order, uint32_t num
 // SIMD (flags bit 2), later units' priority rising with the age of their walk (flags bit 1).
 void launch_blend(const uint32_t* sortedVals, const FrameGeometry& g, const DeviceArena& A, void* color,
                   size_t colorPitch, void* depth, size_t depthPitch, int numCUs, bool costOrder, int colorFormat,
-                  hipStream_t s) {
+                  hipStream_t s, int wavesOverride) {
     const uint32_t t0 = g.rowBegin * g.tilesX, t1 = g.rowEnd * g.tilesX;
     if (t1 <= t0) return;
     const uint32_t numTiles = t1 - t0;
@@ -692,7 +697,7 @@ void launch_blend(const uint32_t* sortedVals, const FrameGeometry& g, const Devi
     const int flags = vec | 2 | (costOrder ? 4 : 0) | ((colorFormat & 15) << 4);
     // A.tileQueue was zeroed by k_scan_blocks earlier in the frame
     const int P = blend_pairs_per_lane(numTiles, numCUs);
-    const int waves = blend_waves_per_wg(numTiles, numCUs);
+    const int waves = wavesOverride ? wavesOverride : blend_waves_per_wg(numTiles, numCUs);
     const uint32_t units = numTiles * (4u / (uint32_t)P);
     uint32_t grid = (units + (uint32_t)waves - 1) / (uint32_t)waves;
     if (grid > (uint32_t)numCUs) grid = (uint32_t)numCUs;
@@ -701,13 +706,15 @@ void launch_blend(const uint32_t* sortedVals, const FrameGeometry& g, const Devi
     hipLaunchKernelGGL((k_blend_px<NTH, PP, CMP>), dim3(grid), dim3(NTH), 0, s, A.tileStart, sortedVals, A.recA, \
                        A.recB, A.expTable, A.tileQueue, t0, numTiles, g.tilesX, g.width, g.height,          \
                        (uint8_t*)color, colorPitch, (uint8_t*)depth, depthPitch, flags, order, A.unitCost,  \
-                       A.blendTrace)
+                       A.blendTrace, A.halfVals[0], A.halfVals[1], A.halfCount, g.tileCount)
     // half tiles compact to one pair per lane once <= 16 of their 32 groups are alive
     if (P == 1) {
         if (waves == 16) GSM_LAUNCH_BLEND(1024, 1, false);
+        else if (waves == 12) GSM_LAUNCH_BLEND(768, 1, false);
         else GSM_LAUNCH_BLEND(512, 1, false);
     } else {
         if (waves == 16) GSM_LAUNCH_BLEND(1024, 2, true);
+        else if (waves == 12) GSM_LAUNCH_BLEND(768, 2, true);
         else GSM_LAUNCH_BLEND(512, 2, true);
     }
 #undef GSM_LAUNCH_BLEND

@@ -411,7 +411,8 @@ __device__ __forceinline__ void obb_extents(const Cov2& cov, float* ex, float* e
 // p >= (1 - u) Q (1 - 9.02 u / (1 - rho)).  quad_exceeds() is true only when that bound exceeds the
 // threshold for the minimum of Q over the pixel rectangle (continuous, so it bounds every pixel), with
 // rho <= 15/16, |dx|, |dy| <= 200 and a + b <= 16000 over the rectangle (no fp16 overflow, no NaN),
-// pixel coordinates below 2048 (exact in fp16) and finite positive cxx, cyy.  Divisions and square roots
+// the rectangle widened by the fp16 rounding of its pixel coordinates (fp16_coord_margin: exact below
+// 2048) and finite positive cxx, cyy.  Divisions and square roots
 // use the hardware approximations (v_rcp_f32, v_rsq_f32, ~1 ulp): they move the edge minimiser t by
 // ~1e-7 relative (Q rises by at most cyy * (2e-5)^2 there) and rho by ~1e-6 (the factor by ~1.3e-6),
 // inside the 1e-3 absolute and 1e-5 relative slack; fp32 evaluation of the bounded quantities adds
@@ -448,10 +449,20 @@ __device__ __forceinline__ QuadBound quad_bound_setup(uint32_t meanW, uint32_t c
     e.mode = 0;
     return e;
 }
+// fp16 pixel coordinates: integers below 2048 are exact; in [2048, 4096) the blends' fp16(x) moves
+// a coordinate by at most 1, in [4096, 8192) by at most 2 -- the rectangle grows by that margin
+__device__ __forceinline__ int fp16_coord_margin(int maxCoord) {
+    return maxCoord < 2048 ? 0 : (maxCoord < 4096 ? 1 : (maxCoord < 8192 ? 2 : -1));
+}
 // every pixel (x, y) with x0 <= x <= x0 + wm1, y0 <= y <= y0 + hm1 has p > thresh
 __device__ __forceinline__ bool quad_exceeds(const QuadBound& e, int x0, int y0, int wm1, int hm1, float thresh) {
     if (e.mode != 0) return e.mode == 1;
-    if (x0 + wm1 >= 2048 || y0 + hm1 >= 2048) return false;
+    const int mxm = fp16_coord_margin(x0 + wm1), mym = fp16_coord_margin(y0 + hm1);
+    if (mxm < 0 || mym < 0) return false;
+    x0 -= mxm;
+    wm1 += 2 * mxm;
+    y0 -= mym;
+    hm1 += 2 * mym;
     const float dx0 = (float)x0 - e.mx, dx1 = dx0 + (float)wm1;
     const float dy0 = (float)y0 - e.my, dy1 = dy0 + (float)hm1;
     if (!(__builtin_fabsf(dx0) <= 200.0f && __builtin_fabsf(dx1) <= 200.0f && __builtin_fabsf(dy0) <= 200.0f &&
@@ -475,6 +486,45 @@ __device__ __forceinline__ bool quad_exceeds(const QuadBound& e, int x0, int y0,
     return qmin * e.factor > thresh + 1e-3f;
 }
 
+// Column-band zero test for the Global blend's half-tile lists (k_scatter skip flags).  With the
+// notation above, Q(dx, dy) >= dx^2 det / cyy for every dy (det = cxx cyy - (cxy2 / 2)^2, the minimum
+// over dy), so every pixel whose real dx satisfies |dx| > ex, ex = sqrt(L' cyy / det), has Q > L' and,
+// by the same rounding bound as quad_exceeds, p >= factor Q > factor L' = thresh + 1e-3.  A band of
+// pixel columns [x0, x1] has fp16 coordinates in [x0 - m, x1 + m] (fp16_coord_margin), so when that
+// interval lies beyond ex on one side of the mean every pixel of the band, in any row, has p > thresh.
+// The rounding bound's preconditions are checked over the band and the tile's rows (|dx|, |dy| <= 200,
+// cxx dx^2 + cyy dy^2 <= 16000, rho <= 15/16, finite positive cxx, cyy); ex carries a 1e-5 relative and
+// 1e-4 absolute margin for the fp32 evaluation (hardware rsq/rcp, ~1 ulp).  k_scatter checks the
+// preconditions once over a gaussian's whole tile rect (band_rect_ok) and then needs two compares per
+// band (half_skip_flags): cheap enough for every (gaussian, tile) of the frame.
+struct BandSkip {
+    float mx, my, cxx, cyy, ex;
+    bool valid;
+};
+__device__ __forceinline__ BandSkip band_skip_setup(uint32_t meanW, uint32_t ccW, uint32_t cxyW, float thresh) {
+    BandSkip b;
+    b.mx = hbits_to_f((uint16_t)(meanW & 0xFFFFu));
+    b.my = hbits_to_f((uint16_t)(meanW >> 16));
+    b.cxx = hbits_to_f((uint16_t)(ccW & 0xFFFFu));
+    b.cyy = hbits_to_f((uint16_t)(ccW >> 16));
+    const float cxy = hbits_to_f((uint16_t)(cxyW & 0xFFFFu));
+    b.ex = 0.0f;
+    b.valid = false;
+    if (!(b.cxx > 0.0f && b.cyy > 0.0f && b.cxx < 65504.0f && b.cyy < 65504.0f && __builtin_fabsf(cxy) < 65504.0f &&
+          __builtin_fabsf(b.mx) < 65504.0f && __builtin_fabsf(b.my) < 65504.0f))
+        return b;
+    const float rho = 0.5f * __builtin_fabsf(cxy) * __builtin_amdgcn_rsqf(b.cxx * b.cyy);
+    if (!(rho <= 15.0f / 16.0f)) return b;
+    const float u = 1.0f / 2048.0f;
+    const float factor = (1.0f - u) * (1.0f - 10.0f * u * __builtin_amdgcn_rcpf(1.0f - rho)) * (1.0f - 1e-5f);
+    const float L = (thresh + 1e-3f) * __builtin_amdgcn_rcpf(factor) * (1.0f + 1e-5f);
+    const float det = b.cxx * b.cyy - 0.25f * cxy * cxy;
+    if (!(det > 0.0f)) return b;
+    // det >= (1 - rho^2) cxx cyy > 0.12 cxx cyy: no cancellation worth more than the relative margin
+    b.ex = __builtin_sqrtf(L * b.cyy * __builtin_amdgcn_rcpf(det)) * (1.0f + 1e-5f) + 1e-4f;
+    b.valid = __builtin_isfinite(b.ex);
+    return b;
+}
 // Colour target store of one rgba16f pixel in config.color_format (include/gsm_renderer.h
 // conversion rules; oracle og_convert_color): rgba32f widens, the 8-bit formats clamp to
 // [0, 1], sRGB-encode rgb and round to nearest.

@@ -64,6 +64,9 @@ struct DeviceArena {
     uint32_t* tileQueue = nullptr;             // [1] blend work counter
     uint16_t* unitCost = nullptr;              // [4 * tileCount] list entries each blend unit walked
     uint32_t* unitOrder = nullptr;             // [4 * tileCount] blend units, longest last-frame walk first
+    uint32_t* halfVals[2] = {nullptr, nullptr};  // [cap] per half tile: the tile's sorted gaussian ids whose
+                                                 // skip flag for that half is clear, from the tile's start
+    uint32_t* halfCount = nullptr;             // [2 * tileCount] entries of each half list (half-major)
     uint16_t* expTable = nullptr;              // [65536]
     float2* sincosTable = nullptr;             // [65536]
 };
@@ -77,6 +80,7 @@ struct Tuning {
                               // set when the create-time device probe (sort_lane_ordered_atomics) fails,
                               // or forced by GSM_SORT_RANK=ballot
     bool costOrder = true;    // GSM_BLEND_SCHED=0: blend units in index order instead of last frame's walks
+    int blendWaves = 0;       // GSM_BLEND_WAVES=8|12|16: waves per blend workgroup (0: by frame size)
 };
 // the environment's settings plus the device probe; `device` is a HIP device id
 Tuning tuning_from_env(int device);
@@ -84,6 +88,16 @@ Tuning tuning_from_env(int device);
 // the lanes of one ds_add_rtn_u32 that hit the same LDS address receive their old values in lane
 // order.  Runs a small kernel once per device and process (cached); false -> ballot ranks.
 bool sort_lane_ordered_atomics(int device);
+
+// Half-tile skip flags of an assignment (the value word's two top bits, set by k_scatter): bit
+// kHalfSkipShift + h when every pixel of half h (16 px columns [16h, 16h + 16) of the 32x16 tile)
+// provably gets alpha 0 from the gaussian -- its fp16 quadratic form p exceeds kBlendZeroP there
+// (quad_exceeds, gsm_device.h), and the blend's exp table is 0 for every fp16 p above it
+// (tests/golden/exp_h_table.npy: 34.65625 is the largest p with a nonzero entry), so alpha =
+// min(op * 0, 0.99) = 0 and the pixel's colour and transmittance stay bit-identical.
+constexpr uint32_t kHalfSkipShift = 30;
+constexpr uint32_t kGidMask = (1u << kHalfSkipShift) - 1u;
+constexpr float kBlendZeroP = 34.65625f;
 
 constexpr int kProjectBlock = 256;
 constexpr int kRadixBlock = 256;
@@ -102,7 +116,7 @@ void launch_partition(bool halfInput, uint32_t shDegree, const void* world, cons
                       hipStream_t stream);
 // received records -> per-gaussian arrays + tile counts of the renderer's rows (replaces project)
 void launch_records_in(const void* records, const ProjectArgs& args, const DeviceArena& A,
-                       hipStream_t stream);
+                       hipStream_t stream, const uint32_t* devCount = nullptr);
 void launch_scan_blocks(uint32_t numBlocks, const ProjectArgs& args, const DeviceArena& A,
                         hipStream_t stream);
 // the same scan for any array of nb per-block sums: exclusive scan in place, the total clamped
@@ -111,13 +125,16 @@ void launch_scan_sums(uint32_t* sums, uint32_t nb, uint32_t cap, TileAssignmentH
                       hipStream_t stream);
 // duplicate-with-keys (GlobalShaders.metal:623-678 fused with :266-295)
 void launch_scatter(const ProjectArgs& args, const DeviceArena& A, hipStream_t stream);
+// the blend's half-tile lists from the sorted values (skip flags, k_scatter), tiles [tileBegin, +numTiles)
+void launch_half_lists(const uint32_t* sortedVals, uint32_t tileBegin, uint32_t numTiles, const DeviceArena& A,
+                       uint32_t tileCount, hipStream_t stream);
 // per-tile binary search headers (GlobalShaders.metal:304-363), tiles of rows [rowBegin,rowEnd)
 void launch_headers(const uint32_t* sortedKeys, const FrameGeometry& geo, const DeviceArena& A,
                     hipStream_t stream);
 // front-to-back fp16 blend + clear (GlobalShaders.metal:140-154, 1030-1187)
 void launch_blend(const uint32_t* sortedVals, const FrameGeometry& geo, const DeviceArena& A,
                   void* color, size_t colorPitch, void* depth, size_t depthPitch, int numCUs,
-                  bool costOrder, int colorFormat, hipStream_t stream);
+                  bool costOrder, int colorFormat, hipStream_t stream, int waves = 0);
 // orders the blend units by the walk lengths the previous frame measured (longest first), so
 // the dynamic queue hands out long units before short ones (A.unitOrder[numUnits])
 void launch_unit_order(uint32_t numUnits, const DeviceArena& A, hipStream_t stream);
@@ -141,9 +158,10 @@ int radix_sort_bits(uint32_t* keys[2], uint32_t* vals[2], const uint32_t* nPtr, 
 uint32_t radix_grid_for_capacity(uint32_t capacity);
 // bytes of the sort workspace (`hist` argument above) for a capacity; zero it once at allocation
 size_t radix_workspace_bytes(uint32_t capacity);
-// stable per-tile sort by the 16-bit depth key of runs already grouped by tile (one wave per tile)
+// stable per-tile sort by the 16-bit depth key of runs already grouped by tile (one workgroup per
+// tile), which also writes the blend's half-tile lists (as launch_half_lists)
 void tile_depth_sort(uint32_t* keysIn, uint32_t* valsIn, uint32_t* keysOut, uint32_t* valsOut,
                      const uint32_t* tileStart, uint32_t tileBegin, uint32_t numTiles, hipStream_t stream,
-                     bool ballot);
+                     bool ballot, uint32_t* half0, uint32_t* half1, uint32_t* halfCount, uint32_t tileCount);
 
 }  // namespace gsm

@@ -357,16 +357,20 @@ __global__ __launch_bounds__(kProjectBlock) void k_part_pack(
     }
 }
 
-// slab owner: received records -> the renderer's per-gaussian arrays + tile counts for its rows
+// slab owner: received records -> the renderer's per-gaussian arrays + tile counts for its rows.
+// devCount (may be null): the record count on the device (multi-GPU exchange); P.count is then the
+// capacity the grid covers and the ids past the count get no tiles.
 __global__ __launch_bounds__(kProjectBlock) void k_records_in(
     const SplatRecord* __restrict__ in, ProjectArgs P, GaussianRenderData* __restrict__ outRD,
     short4* __restrict__ outBounds, BlendRecordA* __restrict__ outA, uint32_t* __restrict__ outB,
     uint32_t* __restrict__ counts, uint32_t* __restrict__ masks, uint32_t* __restrict__ blockSums,
-    const float2* __restrict__ sincos) {
+    const float2* __restrict__ sincos, const uint32_t* __restrict__ devCount) {
     __shared__ uint32_t lds[kProjectBlock / 64];
     const uint32_t gid = blockIdx.x * kProjectBlock + threadIdx.x;
+    const uint32_t n = devCount ? min(*devCount, P.count) : P.count;
     uint32_t ntiles = 0;
-    if (gid < P.count) {
+    if (gid >= n && gid < P.count) counts[gid] = 0;
+    if (gid < n) {
         const SplatRecord r = in[gid];
         *(uint4*)(outRD + gid) = r.rd;
         outBounds[gid] = r.bounds;
@@ -467,17 +471,41 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_blocks(uint32_t* __restri
 // mask -- consecutive threads write consecutive keys (coalesced) and a gaussian with many tiles
 // no longer serialises its wave.  Large rects keep one thread looping over their rect.  Slot
 // order is the reference's (ascending gid, then ty-major, tx-minor).
+// Every value also carries the blend's half-tile skip flags (kHalfSkipShift, gsm_internal.h): the
+// gaussian's column band bound (BandSkip of its fp16 blend record) is set up once per gaussian and
+// checked once against its whole tile rect (band_rect_ok), so a (gaussian, tile) slot only compares
+// the two 16-column halves of its tile with the band [mx - ex, mx + ex] (half_skip_flags).
+__device__ __forceinline__ bool band_rect_ok(const BandSkip& b, int x0, int x1, int y0, int y1) {
+    if (!b.valid) return false;
+    const int mxm = fp16_coord_margin(x1), mym = fp16_coord_margin(y1);
+    if (mxm < 0 || mym < 0) return false;
+    const float ax = __builtin_fmaxf(__builtin_fabsf((float)(x0 - mxm) - b.mx), __builtin_fabsf((float)(x1 + mxm) - b.mx));
+    const float ay = __builtin_fmaxf(__builtin_fabsf((float)(y0 - mym) - b.my), __builtin_fabsf((float)(y1 + mym) - b.my));
+    return ax <= 200.0f && ay <= 200.0f && b.cxx * (ax * ax) + b.cyy * (ay * ay) <= 16000.0f;
+}
+// ex < 0: no skipping for this gaussian; otherwise the band test (BandSkip) on the two halves of tile tx
+__device__ __forceinline__ uint32_t half_skip_flags(float mx, float ex, int tx) {
+    if (ex < 0.0f) return 0u;
+    const int x0 = tx * (int)kTileWidth;
+    constexpr int hw = (int)kTileWidth / 2;
+    const int m0 = fp16_coord_margin(x0 + hw - 1), m1 = fp16_coord_margin(x0 + 2 * hw - 1);
+    const bool l = (float)(x0 - m0) - mx > ex || (float)(x0 + hw - 1 + m0) - mx < -ex;
+    const bool r = (float)(x0 + hw - m1) - mx > ex || (float)(x0 + 2 * hw - 1 + m1) - mx < -ex;
+    return (l ? 1u : 0u) | (r ? 2u : 0u);
+}
+
 __global__ __launch_bounds__(kProjectBlock) void k_scatter(
     ProjectArgs P, const GaussianRenderData* __restrict__ rd, const short4* __restrict__ bounds,
     const uint32_t* __restrict__ counts, const uint32_t* __restrict__ masks,
     const uint32_t* __restrict__ blockOffsets, uint32_t* __restrict__ keys, uint32_t* __restrict__ vals,
-    const float2* __restrict__ sincos) {
+    const float2* __restrict__ sincos, const BlendRecordA* __restrict__ recA) {
     __shared__ uint32_t lds[kProjectBlock / 64];
     __shared__ uint32_t sOff[kProjectBlock];
     __shared__ uint32_t sMask[kProjectBlock];  // 0: no cooperative slots (large rect or no tiles)
     __shared__ uint32_t sRect[kProjectBlock];  // x0 | rw << 16 (rw <= 32)
     __shared__ int sTy0[kProjectBlock];
     __shared__ uint32_t sD[kProjectBlock];     // depth bits of the key
+    __shared__ float2 sBand[kProjectBlock];    // skip-flag band of each gaussian: mean x, half width (< 0: none)
     const uint32_t gid = blockIdx.x * kProjectBlock + threadIdx.x;
     uint32_t c = (gid < P.count) ? counts[gid] : 0u;
     uint32_t total;
@@ -488,8 +516,15 @@ __global__ __launch_bounds__(kProjectBlock) void k_scatter(
     uint32_t dbits = 0;
     int ty0 = 0, ty1 = -1;
     uint32_t mask = 0;
+    float2 band = make_float2(0.0f, -1.0f);
     if (c != 0) {
         r = bounds[gid];
+        const uint4 ra = *(const uint4*)(recA + gid);
+        const BandSkip b = band_skip_setup(ra.x, ra.y, ra.z, kBlendZeroP);
+        const int by0 = max((int)r.z, (int)P.rowBegin), by1 = min((int)r.w, (int)P.rowEnd - 1);
+        if (band_rect_ok(b, (int)r.x * (int)kTileWidth, (int)r.y * (int)kTileWidth + (int)kTileWidth - 1,
+                         by0 * (int)kTileHeight, by1 * (int)kTileHeight + (int)kTileHeight - 1))
+            band = make_float2(b.mx, b.ex);
         const uint32_t rdz = ((const uint4*)(rd + gid))->z;
         dbits = ((rdz >> 16) ^ 0x8000u) & 0xFFFFu;
         ty0 = max((int)r.z, (int)P.rowBegin);
@@ -503,6 +538,7 @@ __global__ __launch_bounds__(kProjectBlock) void k_scatter(
     sMask[threadIdx.x] = mask;
     sD[threadIdx.x] = dbits;
     sTy0[threadIdx.x] = ty0;
+    sBand[threadIdx.x] = band;
     __syncthreads();
     for (uint32_t sl = threadIdx.x; sl < total; sl += kProjectBlock) {
         // owner: the largest g with sOff[g] <= sl (zero-count gaussians share the next offset)
@@ -522,7 +558,8 @@ __global__ __launch_bounds__(kProjectBlock) void k_scatter(
         const uint32_t rwo = rect >> 16;
         const int ty = sTy0[lo] + (int)(bit / rwo), tx = (int)(rect & 0xFFFFu) + (int)(bit % rwo);
         keys[wp] = ((uint32_t)(ty * (int)P.bin.tilesX + tx) << 16) | sD[lo];
-        vals[wp] = blockIdx.x * kProjectBlock + lo;
+        const float2 bd = sBand[lo];
+        vals[wp] = (blockIdx.x * kProjectBlock + lo) | (half_skip_flags(bd.x, bd.y, tx) << kHalfSkipShift);
     }
     if (!large) return;
     uint64_t wp = (uint64_t)base + off;
@@ -542,7 +579,7 @@ __global__ __launch_bounds__(kProjectBlock) void k_scatter(
                 if (wp < P.maxAssignments) {
                     uint32_t tile = (uint32_t)(ty * (int)P.bin.tilesX + tx);
                     keys[wp] = (tile << 16) | dbits;
-                    vals[wp] = gid;
+                    vals[wp] = gid | (half_skip_flags(band.x, band.y, tx) << kHalfSkipShift);
                     wp++;
                 }
             }
@@ -578,6 +615,79 @@ __global__ __launch_bounds__(256) void k_tile_starts(const uint32_t* __restrict_
             for (uint32_t t = prev + 1u; t <= cur; ++t) tileStart[t] = i;
         }
     }
+}
+
+// ---------------------------------------------------------------------------
+// 5. the blend's half-tile lists: per tile, the sorted ids whose skip flag for half h is clear, in
+//    list order, compacted to the tile's start in halfVals[h], and their counts.  One workgroup per
+//    tile, 1024 entries per step (4 per thread, block scan of the keep counts).
+// ---------------------------------------------------------------------------
+constexpr uint32_t kHlThreads = 256;
+__global__ __launch_bounds__(kHlThreads) void k_half_lists(const uint32_t* __restrict__ tileStart,
+                                                           const uint32_t* __restrict__ sortedVals,
+                                                           uint32_t tileBegin, uint32_t tileCount,
+                                                           uint32_t* __restrict__ half0, uint32_t* __restrict__ half1,
+                                                           uint32_t* __restrict__ halfCount) {
+    __shared__ uint32_t part[2][kHlThreads / 64];
+    const uint32_t t = tileBegin + blockIdx.x;
+    const uint32_t start = tileStart[t], n = tileStart[t + 1] - start;
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    uint32_t base0 = 0, base1 = 0;
+    for (uint32_t b = 0; b < n; b += 4 * kHlThreads) {
+        const uint32_t i0 = b + threadIdx.x * 4u;
+        uint32_t v[4];
+        uint32_t k0 = 0, k1 = 0;
+#pragma unroll
+        for (uint32_t j = 0; j < 4; ++j) {
+            v[j] = i0 + j < n ? sortedVals[start + i0 + j] : (3u << kHalfSkipShift);
+            k0 += ((v[j] >> kHalfSkipShift) & 1u) ^ 1u;
+            k1 += ((v[j] >> (kHalfSkipShift + 1)) & 1u) ^ 1u;
+        }
+        // exclusive scans of the two keep counts over the block (thread order = list order)
+        const uint32_t packed = k0 | (k1 << 16);
+        uint32_t inc = packed;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t x = __shfl_up(inc, o, 64);
+            if (lane >= (uint32_t)o) inc += x;
+        }
+        if (lane == 63) {
+            part[0][wave] = inc & 0xFFFFu;
+            part[1][wave] = inc >> 16;
+        }
+        __syncthreads();
+        uint32_t off0 = 0, off1 = 0, tot0 = 0, tot1 = 0;
+#pragma unroll
+        for (uint32_t w = 0; w < kHlThreads / 64; ++w) {
+            if (w < wave) {
+                off0 += part[0][w];
+                off1 += part[1][w];
+            }
+            tot0 += part[0][w];
+            tot1 += part[1][w];
+        }
+        uint32_t p0 = base0 + off0 + (inc & 0xFFFFu) - k0, p1 = base1 + off1 + (inc >> 16) - k1;
+#pragma unroll
+        for (uint32_t j = 0; j < 4; ++j) {
+            const uint32_t g = v[j] & kGidMask;
+            if (!((v[j] >> kHalfSkipShift) & 1u)) half0[start + p0++] = g;
+            if (!((v[j] >> (kHalfSkipShift + 1)) & 1u)) half1[start + p1++] = g;
+        }
+        base0 += tot0;
+        base1 += tot1;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        halfCount[t] = base0;
+        halfCount[tileCount + t] = base1;
+    }
+}
+
+void launch_half_lists(const uint32_t* sortedVals, uint32_t tileBegin, uint32_t numTiles, const DeviceArena& A,
+                       uint32_t tileCount, hipStream_t s) {
+    if (numTiles == 0) return;
+    hipLaunchKernelGGL(k_half_lists, dim3(numTiles), dim3(kHlThreads), 0, s, A.tileStart, sortedVals, tileBegin,
+                       tileCount, A.halfVals[0], A.halfVals[1], A.halfCount);
 }
 
 // ---------------------------------------------------------------------------
@@ -641,12 +751,13 @@ void launch_partition(bool halfInput, uint32_t deg, const void* world, const voi
                        slabs.n, B.blockSlabCounts, B.slabBase, (SplatRecord*)send, capacity);
 }
 
-void launch_records_in(const void* records, const ProjectArgs& a, const DeviceArena& A, hipStream_t s) {
+void launch_records_in(const void* records, const ProjectArgs& a, const DeviceArena& A, hipStream_t s,
+                       const uint32_t* devCount) {
     const uint32_t blocks = (a.count + kProjectBlock - 1) / kProjectBlock;
     if (blocks == 0) return;
     hipLaunchKernelGGL(k_records_in, dim3(blocks), dim3(kProjectBlock), 0, s, (const SplatRecord*)records, a,
                        A.renderData, A.bounds, A.recA, A.recB, A.tileCounts, A.tileMasks, A.blockSums,
-                       A.sincosTable);
+                       A.sincosTable, devCount);
 }
 
 void launch_scan_sums(uint32_t* sums, uint32_t nb, uint32_t cap, TileAssignmentHeader* hdr, uint32_t* queue,
@@ -663,7 +774,7 @@ void launch_scatter(const ProjectArgs& a, const DeviceArena& A, hipStream_t s) {
     const uint32_t blocks = (a.count + kProjectBlock - 1) / kProjectBlock;
     if (blocks == 0) return;
     hipLaunchKernelGGL(k_scatter, dim3(blocks), dim3(kProjectBlock), 0, s, a, A.renderData, A.bounds,
-                       A.tileCounts, A.tileMasks, A.blockSums, A.keys[0], A.vals[0], A.sincosTable);
+                       A.tileCounts, A.tileMasks, A.blockSums, A.keys[0], A.vals[0], A.sincosTable, A.recA);
 }
 
 void launch_headers(const uint32_t* sortedKeys, const FrameGeometry& g, const DeviceArena& A,

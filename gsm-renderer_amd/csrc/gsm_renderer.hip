@@ -125,6 +125,9 @@ gsm_status GlobalRenderer::create(const gsm_renderer_config& cfg, int hipDevice,
     GSM_ALLOC(A.tileQueue, sizeof(uint32_t));
     GSM_ALLOC(A.unitCost, (size_t)r->tileCount_ * 4 * sizeof(uint16_t));
     GSM_ALLOC(A.unitOrder, (size_t)r->tileCount_ * 4 * sizeof(uint32_t));
+    GSM_ALLOC(A.halfVals[0], cap * sizeof(uint32_t));
+    GSM_ALLOC(A.halfVals[1], cap * sizeof(uint32_t));
+    GSM_ALLOC(A.halfCount, (size_t)r->tileCount_ * 2 * sizeof(uint32_t));
     GSM_ALLOC(A.expTable, 65536 * sizeof(uint16_t));
     GSM_ALLOC(A.sincosTable, 65536 * sizeof(float2));
 #undef GSM_ALLOC
@@ -145,7 +148,9 @@ gsm_status GlobalRenderer::create(const gsm_renderer_config& cfg, int hipDevice,
         // every entry of the value buffers is a valid gaussian id at all times (the blend's
         // clamped, unpredicated gathers may read entry 0 of an empty frame)
         hipMemset(A.vals[0], 0, cap * sizeof(uint32_t)) != hipSuccess ||
-        hipMemset(A.vals[1], 0, cap * sizeof(uint32_t)) != hipSuccess) {
+        hipMemset(A.vals[1], 0, cap * sizeof(uint32_t)) != hipSuccess ||
+        hipMemset(A.halfVals[0], 0, cap * sizeof(uint32_t)) != hipSuccess ||
+        hipMemset(A.halfVals[1], 0, cap * sizeof(uint32_t)) != hipSuccess) {
         delete r;
         return GSM_ERR_FAILED_TO_ALLOCATE_BUFFER;
     }
@@ -250,14 +255,16 @@ gsm_status GlobalRenderer::render(hipStream_t s, const gsm_gaussian_input& in,
 
 gsm_status GlobalRenderer::renderRecords(hipStream_t s, const void* records, uint32_t count, uint32_t width,
                                          uint32_t height, void* color, size_t colorPitch, void* depth,
-                                         size_t depthPitch) {
+                                         size_t depthPitch, const uint32_t* devCount) {
+    // devCount: the count lives on the device (multi-GPU exchange, gsm_multigpu_render); `count` is
+    // then the capacity the grids cover
     gsm_status st = validateFrame(count, !records, width, height, color, colorPitch, depth, depthPitch);
     if (st != GSM_OK) return st;
     gsm_camera_params cam;
     std::memset(&cam, 0, sizeof(cam));
     const ProjectArgs a = frameArgs(cam, width, height, count, 1);
     return runFrame(s, a, width, height, color, colorPitch, depth, depthPitch,
-                    [&](const ProjectArgs& pa) { launch_records_in(records, pa, arena_, s); });
+                    [&](const ProjectArgs& pa) { launch_records_in(records, pa, arena_, s, devCount); });
 }
 
 gsm_status GlobalRenderer::projectPartition(hipStream_t s, const gsm_gaussian_input& in,
@@ -381,7 +388,8 @@ gsm_status GlobalRenderer::runFrame(hipStream_t s, const ProjectArgs& a, uint32_
                                         arena_.radixHist, arena_.radixBinTotals, s, ballot);
         launch_headers(kb[res], g, arena_, s);
         tile_depth_sort(kb[res], vb[res], kb[res ^ 1], vb[res ^ 1], arena_.tileStart, rowBegin_ * tilesX_,
-                        (rowEnd_ - rowBegin_) * tilesX_, s, ballot);
+                        (rowEnd_ - rowBegin_) * tilesX_, s, ballot, arena_.halfVals[0], arena_.halfVals[1],
+                        arena_.halfCount, tileCount_);
         sortedKeys_ = kb[res ^ 1];
         sortedVals_ = vb[res ^ 1];
     } else {
@@ -394,11 +402,15 @@ gsm_status GlobalRenderer::runFrame(hipStream_t s, const ProjectArgs& a, uint32_
     unsortedVals_ = keep ? arena_.valsKeep : nullptr;
     if (prof) hipEventRecord(ev[4], s);
     if (fullRadix) launch_headers(sortedKeys_, g, arena_, s);  // else done inside the sort
+    // the blend walks per-half lists without the entries its half provably skips (k_scatter flags);
+    // the tile sort writes them, the 4-pass sort needs the separate pass
+    if (fullRadix)
+        launch_half_lists(sortedVals_, rowBegin_ * tilesX_, (rowEnd_ - rowBegin_) * tilesX_, arena_, tileCount_, s);
     arena_.blendTrace = (profiling_ & 4) ? traceBuf_ : nullptr;
     if (costOrder) hipStreamWaitEvent(s, evOrder_, 0);
     if (prof || blendOnly) hipEventRecord(ev[5], s);
     launch_blend(sortedVals_, g, arena_, color, colorPitch, depth, depthPitch, numCUs_, costOrder,
-                 (int)config_.color_format, s);
+                 (int)config_.color_format, s, tuning_.blendWaves);
     if (prof || blendOnly) hipEventRecord(ev[6], s);
     if (prof || blendOnly) profFrames_++;
     haveTimes_ = profFrames_ > 0;
@@ -513,6 +525,10 @@ gsm_status GlobalRenderer::debugCopy(int which, void* dst, size_t bytes, size_t*
     }
     if (!src) return full == 0 ? GSM_OK : GSM_ERR_MISSING_REQUIRED_BUFFER;
     if (cpy && hipMemcpy(dst, src, cpy, hipMemcpyDeviceToHost) != hipSuccess) return GSM_ERR_RENDER_FAILED;
+    if (which == GSM_BUF_VALUES || which == GSM_BUF_SORTED_VALUES) {  // the reference's ids: no skip flags
+        uint32_t* v = (uint32_t*)dst;
+        for (size_t i = 0; i < cpy / 4; ++i) v[i] &= kGidMask;
+    }
     return GSM_OK;
 }
 

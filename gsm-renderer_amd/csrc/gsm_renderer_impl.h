@@ -29,7 +29,11 @@ class GlobalRenderer {
                                 uint32_t first, uint32_t count, const uint32_t* slabRows, uint32_t numSlabs,
                                 void* send, uint64_t capacity, uint32_t* sendCounts);
     gsm_status renderRecords(hipStream_t stream, const void* records, uint32_t count, uint32_t width,
-                             uint32_t height, void* color, size_t colorPitch, void* depth, size_t depthPitch);
+                             uint32_t height, void* color, size_t colorPitch, void* depth, size_t depthPitch,
+                             const uint32_t* devCount = nullptr);
+    uint32_t maxGaussians() const { return maxGaussians_; }
+    uint32_t tilesY() const { return tilesY_; }
+    bool halfPrecision() const { return config_.precision == GSM_PRECISION_FLOAT16; }
 
     gsm_status counters(gsm_debug_counters* out);
     gsm_status debugCopy(int which, void* dst, size_t bytes, size_t* needed);

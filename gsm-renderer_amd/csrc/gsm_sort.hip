@@ -446,24 +446,73 @@ __device__ void ts_pass_global(const uint32_t* __restrict__ kin, const uint32_t*
     }
 }
 
+// The blend's half-tile lists (skip flags in the value word, k_scatter): one row of 256 sorted
+// entries (position row * 256 + tid) per call, in position order; wave ballots give the ranks, `tot`
+// (LDS) the per-wave counts, base0/base1 the entries of earlier rows.
+__device__ __forceinline__ void ts_half_row(uint32_t v, bool valid, uint32_t (*tot)[kTsThreads / 64], uint32_t& base0,
+                                            uint32_t& base1, uint32_t* __restrict__ h0, uint32_t* __restrict__ h1) {
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    const bool k0 = valid && !((v >> kHalfSkipShift) & 1u);
+    const bool k1 = valid && !((v >> (kHalfSkipShift + 1)) & 1u);
+    const uint64_t m0 = __ballot(k0), m1 = __ballot(k1);
+    if (lane == 0) {
+        tot[0][wave] = (uint32_t)__popcll(m0);
+        tot[1][wave] = (uint32_t)__popcll(m1);
+    }
+    __syncthreads();
+    uint32_t o0 = base0, o1 = base1, a0 = 0, a1 = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < kTsThreads / 64; ++w) {
+        if (w < wave) {
+            o0 += tot[0][w];
+            o1 += tot[1][w];
+        }
+        a0 += tot[0][w];
+        a1 += tot[1][w];
+    }
+    const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    if (k0) h0[o0 + (uint32_t)__popcll(m0 & lt)] = v & kGidMask;
+    if (k1) h1[o1 + (uint32_t)__popcll(m1 & lt)] = v & kGidMask;
+    base0 += a0;
+    base1 += a1;
+    __syncthreads();  // tot is rewritten by the next row
+}
+
 template <bool BALLOT>
 __global__ __launch_bounds__(kTsThreads) void k_tile_sort(
     uint32_t* __restrict__ keysIn, uint32_t* __restrict__ valsIn, uint32_t* __restrict__ keysOut,
-    uint32_t* __restrict__ valsOut, const uint32_t* __restrict__ tileStart, uint32_t tileBegin) {
+    uint32_t* __restrict__ valsOut, const uint32_t* __restrict__ tileStart, uint32_t tileBegin,
+    uint32_t* __restrict__ half0, uint32_t* __restrict__ half1, uint32_t* __restrict__ halfCount,
+    uint32_t tileCount) {
     __shared__ __attribute__((aligned(16))) uint32_t buf[kTsCap];
     __shared__ __attribute__((aligned(16))) uint32_t wcnt[4][256];
     __shared__ uint32_t part[4];
+    __shared__ uint32_t tot[2][kTsThreads / 64];
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
     const uint32_t t = tileBegin + blockIdx.x;
     const uint32_t start = tileStart[t];
     const uint32_t n = tileStart[t + 1] - start;
-    if (n == 0) return;  // uniform: the whole workgroup leaves
+    uint32_t base0 = 0, base1 = 0;
+    if (n == 0) {  // uniform: the whole workgroup leaves
+        if (tid == 0) halfCount[t] = halfCount[tileCount + t] = 0;
+        return;
+    }
     if (n > kTsCap) {  // rare: the same two passes streamed through global memory
         ts_pass_global<BALLOT>(keysIn + start, valsIn + start, keysOut + start, valsOut + start, n, 0, wcnt, part, buf);
         ts_pass_global<BALLOT>(keysOut + start, valsOut + start, keysIn + start, valsIn + start, n, 8, wcnt, part, buf);
-        for (uint32_t i = tid; i < n; i += kTsThreads) {
-            keysOut[start + i] = keysIn[start + i];
-            valsOut[start + i] = valsIn[start + i];
+        for (uint32_t b = 0; b < n; b += kTsThreads) {
+            const uint32_t i = b + tid;
+            uint32_t v = 0;
+            if (i < n) {
+                keysOut[start + i] = keysIn[start + i];
+                v = valsIn[start + i];
+                valsOut[start + i] = v;
+            }
+            ts_half_row(v, i < n, tot, base0, base1, half0 + start, half1 + start);
+        }
+        if (tid == 0) {
+            halfCount[t] = base0;
+            halfCount[tileCount + t] = base1;
         }
         return;
     }
@@ -493,28 +542,42 @@ __global__ __launch_bounds__(kTsThreads) void k_tile_sort(
     for (uint32_t w = 0; w < 4; ++w) wcnt[w][tid] = 0;
     __syncthreads();
     ts_rank_pass<BALLOT>(x, pos, E, seg, n, 24, wcnt, part);  // high depth byte
+    // the sorted run staged in LDS by position, then written in position order: coalesced key and
+    // value stores, and the half-tile lists compacted row by row
+#pragma unroll
+    for (uint32_t j = 0; j < kTsItems; ++j)
+        if (j < E && seg + j * 64u + lane < n) buf[pos[j]] = x[j];
+    __syncthreads();
     uint32_t* kout = keysOut + start;
     uint32_t* vout = valsOut + start;
     const uint32_t tileBits = t << 16;
-#pragma unroll
-    for (uint32_t j = 0; j < kTsItems; ++j) {
-        if (j < E && seg + j * 64u + lane < n) {
-            kout[pos[j]] = tileBits | (x[j] >> 16);
-            vout[pos[j]] = vin[x[j] & 0xFFFFu];
+    for (uint32_t j = 0; j < E; ++j) {
+        const uint32_t p = j * kTsThreads + tid;
+        uint32_t v = 0;
+        if (p < n) {
+            const uint32_t w = buf[p];
+            v = vin[w & 0xFFFFu];
+            kout[p] = tileBits | (w >> 16);
+            vout[p] = v;
         }
+        ts_half_row(v, p < n, tot, base0, base1, half0 + start, half1 + start);
+    }
+    if (tid == 0) {
+        halfCount[t] = base0;
+        halfCount[tileCount + t] = base1;
     }
 }
 
 void tile_depth_sort(uint32_t* keysIn, uint32_t* valsIn, uint32_t* keysOut, uint32_t* valsOut,
                      const uint32_t* tileStart, uint32_t tileBegin, uint32_t numTiles, hipStream_t s,
-                     bool ballot) {
+                     bool ballot, uint32_t* half0, uint32_t* half1, uint32_t* halfCount, uint32_t tileCount) {
     if (numTiles == 0) return;
     if (ballot)
         hipLaunchKernelGGL(k_tile_sort<true>, dim3(numTiles), dim3(kTsThreads), 0, s, keysIn, valsIn, keysOut,
-                           valsOut, tileStart, tileBegin);
+                           valsOut, tileStart, tileBegin, half0, half1, halfCount, tileCount);
     else
         hipLaunchKernelGGL(k_tile_sort<false>, dim3(numTiles), dim3(kTsThreads), 0, s, keysIn, valsIn, keysOut,
-                           valsOut, tileStart, tileBegin);
+                           valsOut, tileStart, tileBegin, half0, half1, halfCount, tileCount);
 }
 
 // ---------------------------------------------------------------------------
@@ -580,6 +643,9 @@ Tuning tuning_from_env(int device) {
     t.ballotRank = (rv && std::strcmp(rv, "ballot") == 0) || !sort_lane_ordered_atomics(device);
     const char* bv = getenv("GSM_BLEND_SCHED");
     t.costOrder = !(bv && bv[0] == '0');
+    const char* wv = getenv("GSM_BLEND_WAVES");
+    const int w = wv ? atoi(wv) : 0;
+    t.blendWaves = (w == 8 || w == 12 || w == 16) ? w : 0;
     return t;
 }
 

@@ -229,6 +229,11 @@ _SIGNATURES = {
     "gsm_depthfirst_stage_times": ([C.c_void_p, C.POINTER(C.c_float), C.c_int], C.c_int),
     "gsm_depthfirst_last_gpu_time": ([C.c_void_p, C.POINTER(C.c_double)], C.c_int),
     "gsm_debug_sort_rank_probe": ([C.c_int, C.POINTER(C.c_int)], C.c_int),
+    "gsm_multigpu_create": ([C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_void_p)], C.c_int),
+    "gsm_multigpu_destroy": ([C.c_void_p], None),
+    "gsm_multigpu_render": ([C.c_void_p, C.c_void_p, C.POINTER(_Input), C.POINTER(_Camera), C.c_uint32,
+                             C.c_uint32, C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t, C.c_void_p], C.c_int),
+    "gsm_multigpu_debug_counts": ([C.c_void_p, C.POINTER(C.c_uint32)], C.c_int),
 }
 
 SPLAT_RECORD_BYTES = 48  # include/gsm_multigpu.h GSM_SPLAT_RECORD_BYTES
@@ -552,6 +557,56 @@ def sort_pairs_u32(keys, values, key_bits: int = 32, stream=None):
     n = int(keys.numel())
     _check(_lib().gsm_sort_pairs_u32(_ptr(keys), _ptr(values), n, int(key_bits), _stream_handle(stream)),
            "gsm_sort_pairs_u32")
+
+
+class MultiGpuRenderer:
+    """gsm_multigpu_* (include/gsm_multigpu.h): one frame of a GlobalRenderer split by tile-row slab
+    across the ranks of an RCCL communicator, records exchanged by peer writes over xGMI and the
+    bands gathered on rank 0 -- all inside libgsm_amd.so, no host round trip in a frame.
+    comm: the ncclComm_t as an int (torch: the NCCL backend's _comm_ptr())."""
+
+    def __init__(self, renderer: "GlobalRenderer", comm: int, rank: int, world_size: int):
+        h = C.c_void_p()
+        _check(_lib().gsm_multigpu_create(renderer._h, C.c_void_p(int(comm)), int(rank), int(world_size), C.byref(h)),
+               "gsm_multigpu_create")
+        self._h = h
+        self.renderer = renderer
+        self.world_size = int(world_size)
+
+    @staticmethod
+    def torch_comm(device) -> int:
+        """The ncclComm_t of torch.distributed's default NCCL process group on `device`."""
+        import torch.distributed as dist
+        return int(dist.group.WORLD._get_backend(torch.device("cuda", int(device)))._comm_ptr())
+
+    def render(self, color_texture, depth_texture, input: GaussianInput, camera: CameraParams, width: int,
+               height: int, gather: bool = True, stream=None, color_pitch: Optional[int] = None,
+               depth_pitch: Optional[int] = None):
+        inp = _Input(_ptr(input.gaussians), _ptr(input.harmonics), int(input.gaussian_count),
+                     int(input.sh_components))
+        cam = _camera_struct(camera)
+        cp = color_pitch if color_pitch is not None else int(width) * 8
+        dp = depth_pitch if depth_pitch is not None else int(width) * 2
+        col = _ptr(color_texture)
+        st = _lib().gsm_multigpu_render(self._h, _stream_handle(stream), C.byref(inp), C.byref(cam), int(width),
+                                        int(height), col, cp, _ptr(depth_texture), dp, col if gather else None)
+        _check(st, "gsm_multigpu_render")
+
+    def counts(self) -> np.ndarray:
+        out = (C.c_uint32 * (self.world_size * self.world_size))()
+        _check(_lib().gsm_multigpu_debug_counts(self._h, out), "gsm_multigpu_debug_counts")
+        return np.array(out, np.uint32).reshape(self.world_size, self.world_size)
+
+    def close(self):
+        if getattr(self, "_h", None) and self._h.value:
+            _lib().gsm_multigpu_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def sort_rank_probe(device: int = 0) -> bool:

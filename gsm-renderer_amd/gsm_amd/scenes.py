@@ -45,6 +45,25 @@ def make_camera(width: int, height: int, eye_offset_x: float = 0.0) -> dict:
             "focal_x": width * f / (2 * aspect), "focal_y": height * f / 2, "near": 0.1, "far": 10.0}
 
 
+def orbit_camera(width: int, height: int, angle_deg: float, pivot_z: float = 5.5) -> dict:
+    """make_camera's camera moved on a circle about the y axis through (0, 0, pivot_z), still looking
+    at that point: angle 0 is make_camera itself.  Used for the moving-camera benchmark (bench.py
+    --camera-path orbit), where every frame sees a slightly different view."""
+    a = math.radians(angle_deg)
+    c, s = np.float32(math.cos(a)), np.float32(math.sin(a))
+    R = np.array([[c, 0, s], [0, 1, 0], [-s, 0, c]], np.float32)        # camera-to-world rotation
+    pos = np.array([0, 0, pivot_z], np.float32) + R @ np.array([0, 0, -pivot_z], np.float32)
+    Rt = R.T
+    t = -(Rt @ pos)
+    V = np.eye(4, dtype=np.float32)
+    V[:3, :3] = Rt
+    V[:3, 3] = t
+    cam = make_camera(width, height)
+    cam["view"] = V.T.reshape(-1).astype(np.float32)  # column-major flat
+    cam["position"] = pos.astype(np.float32)
+    return cam
+
+
 def _f16_bits(x: np.ndarray) -> np.ndarray:
     return np.asarray(x, np.float32).astype(np.float16).view(np.uint16)
 

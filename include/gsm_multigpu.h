@@ -14,6 +14,11 @@
  * The slab's pixels are bit-identical to a single-GPU gsm_global_render of the frame:
  * projection is per gaussian, and the ascending-id concatenation preserves the
  * stable-sort tie order (determinism contract).
+ *
+ * gsm_multigpu_* run the whole protocol inside the library over the caller's RCCL
+ * communicator (steps 1-3 plus the band gather), enqueue-only with no host round trip;
+ * gsm_global_project_partition / gsm_global_render_records remain for callers that move
+ * the records themselves.
  */
 #ifndef GSM_MULTIGPU_H
 #define GSM_MULTIGPU_H
@@ -48,6 +53,38 @@ gsm_status gsm_global_render_records(gsm_renderer *renderer, void *stream, const
                                      uint32_t count, uint32_t width, uint32_t height,
                                      void *color_rgba16f, size_t color_pitch_bytes,
                                      void *depth_r16f, size_t depth_pitch_bytes);
+
+/* --- the frame across a communicator ------------------------------------------------------
+ * One renderer per rank (gsm_global_create on that rank's GPU, config.max_gaussians >= the
+ * frame's gaussian count) and the rank's RCCL communicator (ncclComm_t as void*; libgsm_amd
+ * loads RCCL at run time and uses the copy the process has already loaded, so a communicator
+ * from torch.distributed works).  Collective: every rank of the communicator calls create,
+ * each frame and destroy.  create allocates the send / receive buffers (48 B x max_gaussians
+ * each) and opens every peer's receive buffer once from its IPC handle; GSM_ERR_UNSUPPORTED
+ * when no RCCL can be loaded, GSM_ERR_INVALID_ARGUMENT when rank / world_size do not match the
+ * communicator or world_size > GSM_MAX_SLABS. */
+typedef struct gsm_multigpu gsm_multigpu;
+gsm_status gsm_multigpu_create(gsm_renderer *renderer, void *nccl_comm, int rank, int world_size,
+                               gsm_multigpu **out);
+void gsm_multigpu_destroy(gsm_multigpu *multigpu);
+
+/* One frame of gsm_global_render (GlobalRenderer.swift:201-238) across the communicator.  Every
+ * rank passes the same input (device pointers on its own GPU; it reads only its id range
+ * [r * ceil(N / W), +ceil(N / W))), camera and size.  Rank r owns tile rows
+ * [r * ceil(tiles_y / W), +ceil(tiles_y / W)) and writes them into its full-frame-addressed
+ * color / depth targets; per frame, on `stream`: projection of its ids, all-gather of the
+ * per-slab record counts, peer writes of every record into its owner's receive buffer over
+ * xGMI, one ordering all-reduce, the slab render with the record count read on the device, and,
+ * when gather_color is set on rank 0 (it must then equal color, with color_pitch = 8 * width)
+ * and on every other rank (any non-NULL value), the bands sent to rank 0's frame.  No host
+ * synchronisation anywhere in the frame. */
+gsm_status gsm_multigpu_render(gsm_multigpu *multigpu, void *stream, const gsm_gaussian_input *input,
+                               const gsm_camera_params *camera, uint32_t width, uint32_t height,
+                               void *color_rgba16f, size_t color_pitch_bytes, void *depth_r16f,
+                               size_t depth_pitch_bytes, void *gather_color);
+
+/* The last frame's world x world record counts (row = source rank, column = slab), synchronous. */
+gsm_status gsm_multigpu_debug_counts(gsm_multigpu *multigpu, uint32_t *host_counts);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,66 @@
+"""The multi-GPU frame behind the C ABI (include/gsm_multigpu.h, csrc/gsm_multigpu.hip) on one MI355X:
+a world-size-1 RCCL communicator from torch.distributed drives the whole protocol -- partition
+projection, counts all-gather, peer-write exchange (to itself), ordering all-reduce, slab render
+from the device-side count -- and the frame equals the single-GPU frame and the oracle bit for bit.
+The N > 1 runs are the driver's (8-GPU node); the exchange order across ranks is covered on CPU by
+tests/test_exchange_distributed.py and the composition of slabs by
+tests/test_gpu_parity.py::test_partitioned_frame_matches_single_gpu."""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.fixture(scope="module")
+def nccl_world1(cuda):
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(_free_port())
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=cuda.device("cuda", 0))
+    yield dist
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("n,w,h,sh,prec", [(60_000, 640, 360, 16, 1), (30_000, 1280, 720, 4, 0)])
+def test_world1_rccl_frame_matches_single_gpu_and_oracle(gsm, cuda, oracle, nccl_world1, n, w, h, sh, prec):
+    from gsm_amd import scenes
+    world, harm, cam = scenes.gen_scene(n, w, h, sh, prec, seed=5)
+    wt = cuda.from_numpy(world.view(np.uint8).reshape(-1).copy()).cuda()
+    ht = cuda.from_numpy(harm.view(np.uint8).reshape(-1).copy()).cuda()
+    inp = gsm.GaussianInput(wt, ht, n, sh)
+    cp = gsm.CameraParams.from_dict(cam)
+    cfg = gsm.RendererConfig(max_gaussians=n, max_width=w, max_height=h, precision=prec, gaussian_color_space=0)
+    rend = gsm.GlobalRenderer(device=0, config=cfg)
+    mg = gsm.MultiGpuRenderer(rend, gsm.MultiGpuRenderer.torch_comm(0), 0, 1)
+    color = cuda.full((h, w, 4), float("nan"), dtype=cuda.float16, device="cuda")
+    depth = cuda.full((h, w), float("nan"), dtype=cuda.float16, device="cuda")
+    for _ in range(2):  # a second frame reuses the exchange buffers and the IPC mapping
+        mg.render(color, depth, inp, cp, w, h)
+    cuda.cuda.synchronize()
+    ref = oracle.render(world, harm, sh, cam, w, h, max_gaussians=n)
+    got = color.view(cuda.int16).cpu().numpy().view(np.uint16)
+    assert np.array_equal(got, ref["color"])
+    assert np.array_equal(depth.view(cuda.int16).cpu().numpy().view(np.uint16), ref["depth"])
+    counts = mg.counts()
+    with_tiles = int(np.count_nonzero(ref["tile_counts"]))
+    assert counts.shape == (1, 1) and with_tiles <= counts[0, 0] <= n
+    assert rend.debug_read_total_assignments() == ref["total_assignments"]
+    mg.close()
+    rend.close()
+
+
+def test_create_rejects_a_mismatched_world(gsm, cuda, nccl_world1):
+    rend = gsm.GlobalRenderer(device=0, config=gsm.RendererConfig(max_gaussians=16, max_width=64, max_height=32))
+    with pytest.raises(gsm.RendererError) as e:
+        gsm.MultiGpuRenderer(rend, gsm.MultiGpuRenderer.torch_comm(0), 0, 2)
+    assert e.value.status == gsm.Status.INVALID_ARGUMENT
+    rend.close()

@@ -19,6 +19,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="cfg2_1m_sh3_1080p_f16")
     ap.add_argument("--frames", type=int, default=5)
+    ap.add_argument("--angle", type=float, default=0.0, help="orbit camera angle (scenes.orbit_camera)")
     args = ap.parse_args()
     import torch
     import gsm_amd
@@ -34,7 +35,7 @@ def main():
     color = torch.empty((H, W, 4), dtype=torch.float16, device=dev)
     depth = torch.empty((H, W), dtype=torch.float16, device=dev)
     inp = gsm_amd.GaussianInput(world, harm, n, sh)
-    cp = gsm_amd.CameraParams.from_dict(cam)
+    cp = gsm_amd.CameraParams.from_dict(scenes.orbit_camera(W, H, args.angle) if args.angle else cam)
     for _ in range(3):
         r.render(color, depth, inp, cp, W, H)
     r.set_profiling(True, blend_trace=True)
@@ -58,7 +59,7 @@ def main():
     busy = dur.sum() / (span * max(occ))
     wk = walked > 0
     out = {
-        "config": args.config, "units": int(units), "blend_ms_events": st.get("blend"),
+        "config": args.config, "angle": args.angle, "units": int(units), "blend_ms_events": st.get("blend"),
         "trace_span_us": span / 1e3, "max_concurrent": int(max(occ)),
         "slot_busy_frac": float(busy),
         "mean_unit_us": float(dur.mean() / 1e3), "max_unit_us": float(dur.max() / 1e3),
@@ -69,7 +70,7 @@ def main():
     }
     print(json.dumps(out))
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
-    np.savez_compressed(os.path.join(ROOT, "gpurun_out", f"blend_trace_{args.config}.npz"), trace=tr)
+    np.savez_compressed(os.path.join(ROOT, "gpurun_out", f"blend_trace_{args.config}_{args.angle:g}.npz"), trace=tr)
 
 
 if __name__ == "__main__":

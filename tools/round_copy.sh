@@ -1,13 +1,18 @@
 #!/bin/bash
 # Copy the judged artefacts of tools/gpu_round.sh from gpurun_out/round/ into profiles/ (round tag $1).
 set -eu
-R=${1:-r01}
+R=${1:-r02}
 cd "$(dirname "$0")/.."
 IN=gpurun_out/round
-for c in cfg2 cfg3 cfg5 cfg5_global; do tail -n 1 $IN/bench_$c.log | python -m json.tool > profiles/${R}_bench_$c.json; done
-cp $IN/pytest_gpu.log profiles/${R}_pytest_gpu.log
-cp "$(find $IN/kt -name '*kernel_stats.csv' | head -1)" profiles/${R}_kernel_stats_cfg2.csv
-cp "$(find $IN/kt5 -name '*kernel_stats.csv' | head -1)" profiles/${R}_kernel_stats_cfg5_depthfirst.csv
-cp $IN/pmc_summary.txt profiles/${R}_pmc_cfg2.txt
-cp $IN/traffic.json profiles/traffic_${R}.json
+for f in $IN/bench_*.log; do
+  b=$(basename $f .log); tail -n 1 $f | python -m json.tool > profiles/${R}_$b.json
+done
+[ -f $IN/pytest_gpu.log ] && cp $IN/pytest_gpu.log profiles/${R}_pytest_gpu.log
+[ -f $IN/smoke.log ] && cp $IN/smoke.log profiles/${R}_smoke.log
+for d in $IN/kt_*; do
+  c=${d##*/kt_}
+  f=$(find $d -name '*kernel_stats.csv' | head -1); [ -n "$f" ] && cp "$f" profiles/${R}_kernel_stats_$c.csv
+done
+for f in $IN/pmc_summary_*.txt; do [ -f $f ] && cp $f profiles/${R}_$(basename $f); done
+for f in $IN/pmc_blend_*.json; do [ -f $f ] && cp $f profiles/${R}_$(basename $f); done
 ls -la profiles

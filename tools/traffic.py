@@ -1,8 +1,13 @@
-"""Per-launch HBM traffic of the blend kernel from rocprofv3 PMC passes (tools/gpu_round.sh).
+"""Per-launch PMC numbers of one kernel from rocprofv3 --pmc passes (tools/gpu_round.sh), raw.
 
-MI355X_MICROARCH.md (HBM section): FETCH_SIZE / WRITE_SIZE come from the L2's fabric request
-counters; on gfx950 FETCH_SIZE reports half the bytes of wide coalesced reads, so it is doubled;
-WRITE_SIZE is exact.  Both are in KiB per dispatch.  Prints the JSON bench.py reads."""
+Prints the JSON bench.py reads (--traffic-json): FETCH_SIZE and WRITE_SIZE (KiB per dispatch, the
+L2's fabric request counters) and SQ_INSTS_VALU (wave-instructions per dispatch), averaged over
+the dispatches.  The counter corrections are bench.py's (roofline "traffic"), calibrated on
+MI355X by tools/exp/fetch_calib.hip (profiles/r02_fetch_calibration.json):
+  * wide coalesced streams: FETCH_SIZE counts half their bytes (MI355X_MICROARCH.md) -> x2;
+  * random gathers of 4 or 16 B: one 64-B FETCH unit per distinct 64-B segment fetched -> x1;
+  * WRITE_SIZE exact.
+usage: traffic.py PMC_DIR KERNEL_SUBSTRING CONFIG_NAME"""
 import csv
 import glob
 import json
@@ -11,30 +16,32 @@ import sys
 from collections import defaultdict
 
 root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/round/pmc"
-kernel = sys.argv[2] if len(sys.argv) > 2 else "k_blend_px"          # kernel name substring
+kernel = sys.argv[2] if len(sys.argv) > 2 else "k_blend_px"
 config = sys.argv[3] if len(sys.argv) > 3 else "cfg2_1m_sh3_1080p_f16"
 acc = defaultdict(lambda: defaultdict(list))
 for path in sorted(glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True)):
     with open(path) as f:
         for row in csv.DictReader(f):
             acc[row.get("Kernel_Name", "?")][row["Counter_Name"]].append(float(row["Counter_Value"]))
+
+
+def mean(cs, name):
+    v = cs.get(name)
+    return sum(v) / len(v) if v else None
+
+
 out = {}
 for k, cs in acc.items():
     if kernel not in k or "FETCH_SIZE" not in cs or "WRITE_SIZE" not in cs:
         continue
-    f = sum(cs["FETCH_SIZE"]) / len(cs["FETCH_SIZE"])
-    w = sum(cs["WRITE_SIZE"]) / len(cs["WRITE_SIZE"])
     out = {
         "kernel": k.split("(")[0],
         "config": config,
-        "source": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes (tools/gpu_round.sh)",
-        "fetch_size_kb": round(f, 1),
-        "write_size_kb": round(w, 1),
-        "correction": "FETCH_SIZE x2 (gfx950 counts half of wide reads), WRITE_SIZE exact",
-        "blend_hbm_bytes_per_launch": int(round((2 * f + w) * 1024)),
-        "blend_valu_insts_per_launch": (int(round(sum(cs["SQ_INSTS_VALU"]) / len(cs["SQ_INSTS_VALU"])))
-                                        if "SQ_INSTS_VALU" in cs else None),
-        "note": "includes each workgroup's 128 KiB exp-table load and the re-reads of a tile's list by "
-                "every unit of the tile; Infinity-Cache hits are counted by these fabric counters",
+        "source": "rocprofv3 --pmc passes of bench.py (tools/gpu_round.sh): FETCH_SIZE, WRITE_SIZE and "
+                  "SQ_INSTS_VALU each in its own pass",
+        "fetch_size_kib": round(mean(cs, "FETCH_SIZE"), 1),
+        "write_size_kib": round(mean(cs, "WRITE_SIZE"), 1),
+        "valu_insts_per_launch": int(round(mean(cs, "SQ_INSTS_VALU"))) if "SQ_INSTS_VALU" in cs else None,
+        "grbm_gui_active": mean(cs, "GRBM_GUI_ACTIVE"),
     }
 print(json.dumps(out, indent=1))

@@ -89,7 +89,10 @@ def main():
     # collectives; timings meaningless).  The driver's multi-GPU runs use RCCL ("nccl").
     backend = os.environ.get("BENCH_DIST_BACKEND", "nccl")
     gpu = local_rank % max(1, torch.cuda.device_count()) if backend == "gloo" else local_rank
-    if world_size > 1:
+    # BENCH_FORCE_MULTI=1 runs the N>1 code path (C-ABI multi-GPU frame over an RCCL communicator)
+    # at world size 1 -- a one-GPU rehearsal of what the driver's 8-GPU runs execute
+    force_multi = os.environ.get("BENCH_FORCE_MULTI") == "1"
+    if world_size > 1 or force_multi:
         torch.cuda.set_device(gpu)
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
@@ -129,8 +132,18 @@ def main():
     cam = gsm_amd.CameraParams.from_dict(cam_d)
     stream = torch.cuda.current_stream(dev)
 
-    alltoall = world_size > 1 and args.multi == "alltoall"
-    if alltoall:
+    alltoall = (world_size > 1 or force_multi) and args.multi == "alltoall"
+    # N > 1 over RCCL: the whole partitioned frame runs inside libgsm_amd.so (gsm_multigpu_render,
+    # include/gsm_multigpu.h): counts all-gathered on the device, records pushed to their slab
+    # owners over xGMI, bands sent to rank 0 -- no host round trip in a frame.  The gloo rehearsal
+    # (BENCH_DIST_BACKEND=gloo, several ranks on one GPU) has no RCCL communicator and moves the
+    # records through gsm_amd.exchange instead.
+    native_multi = alltoall and backend == "nccl"
+    if native_multi:
+        full_c = torch.zeros((H, TW, 4), dtype=torch.float16, device=dev)  # rank 0: the gathered frame
+        full_d = torch.zeros((H, TW), dtype=torch.float16, device=dev)
+        mg = gsm_amd.MultiGpuRenderer(renderer, gsm_amd.MultiGpuRenderer.torch_comm(gpu), rank, world_size)
+    elif alltoall:
         first, cnt = exchange.id_range(n, world_size, rank)
         rows = exchange.slab_rows(tiles_y, H, world_size)
         send_cap = max(cnt, 1) * world_size
@@ -146,6 +159,9 @@ def main():
         if stereo:
             renderer.render_stereo_sbs(cptr, dptr, inp, cam_l, cam_r, W, H, stream=stream,
                                        color_pitch=pitch_c, depth_pitch=pitch_d)
+        elif native_multi:
+            mg.render(full_c, full_d, inp, cam, W, H, gather=True, stream=stream)
+            return
         elif alltoall:
             renderer.project_partition(inp, cam, W, H, first, cnt, rows, send, send_cap, send_counts,
                                        stream=stream)
@@ -182,7 +198,7 @@ def main():
     # lengths, k_unit_order) is always one frame stale -- what the static `value` cannot show
     orbit = None
     orbit_last_cam = None
-    if world_size == 1 and not stereo and args.orbit_steps > 0:
+    if world_size == 1 and not stereo and not native_multi and args.orbit_steps > 0:
         cams = [gsm_amd.CameraParams.from_dict(scenes.orbit_camera(W, H, 0.25 * (i + 1)))
                 for i in range(args.warmup + args.orbit_steps)]
         it = iter(cams)
@@ -199,10 +215,25 @@ def main():
                  "camera": "orbit about (0, 0, 5.5), +0.25 deg about y per frame (scenes.orbit_camera)",
                  "parity_last_frame": None}
 
+    multi_parity = None
+    if native_multi and args.parity:  # the gathered N-GPU frame against the oracle (rank 0)
+        step()
+        torch.cuda.synchronize()
+        dist.barrier()
+        if rank == 0:
+            sys.path.insert(0, os.path.join(ROOT, "oracle"))
+            import oracle as O  # parity checker only
+            ref = O.render(world_np, harm_np, sh, cam_d, W, H, max_gaussians=n,
+                           nthreads=max(1, min(args.cpu_threads, os.cpu_count() or 1)))
+            multi_parity = bool(np.array_equal(full_c.view(torch.int16).cpu().numpy().view(np.uint16), ref["color"]))
+    if native_multi:
+        mg.close()
     if rank != 0:
         renderer.close()
         dist.destroy_process_group()
         return
+    if force_multi:
+        dist.destroy_process_group()
 
     A = counters["total_assignments"]
     T = counters["tile_count"]
@@ -237,7 +268,7 @@ def main():
 
     parity = None
     cpu = None
-    if world_size == 1 and (args.parity or args.cpu_baseline):
+    if world_size == 1 and not native_multi and (args.parity or args.cpu_baseline):
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import oracle as O  # CPU baseline + parity checker only
         threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
@@ -297,7 +328,9 @@ def main():
                    "gaussians": n, "width": W, "height": H, "sh_components": sh,
                    "visible": V, "assignments": A, "tiles": T,
                    "parallelism": (f"dp{world_size} tile-row slabs, "
-                                   + ("all-to-all of projected records" if alltoall else "projection replicas"))
+                                   + ("records pushed to slab owners over xGMI inside libgsm_amd (gsm_multigpu_render)"
+                                      if native_multi else
+                                      ("all-to-all of projected records" if alltoall else "projection replicas")))
                                   if world_size > 1 else "single GPU"},
         "roofline": {"bound": "hbm", "kernel": "k_blend_px", "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
@@ -324,7 +357,7 @@ def main():
         "sort_gkeys_per_s": sort_gkeys,
         "blend_gb_per_s": achieved,
         "orbit": orbit,
-        "parity_vs_oracle": parity,
+        "parity_vs_oracle": multi_parity if native_multi else parity,
     }
     print(json.dumps(out))
     renderer.close()

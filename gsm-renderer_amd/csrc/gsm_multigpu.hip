@@ -105,7 +105,9 @@ __global__ __launch_bounds__(256) void k_push(const SplatRecord* __restrict__ se
         dst[1] = b;
         dst[2] = c;
     }
-    __threadfence_system();  // the peers read these after the ordering collective
+    // no fence: the receive buffers are uncached device memory (MultiGpu::create), so these stores
+    // reach the owner's HBM directly and are complete when the kernel is; the ordering collective
+    // that follows on every rank's stream orders them before any owner's read
 }
 }  // namespace
 
@@ -168,7 +170,10 @@ gsm_status MultiGpu::create(GlobalRenderer* r, void* comm, int rank, int world, 
     bool ok = hipMalloc(&m->send_, m->sendCap_ * sizeof(SplatRecord)) == hipSuccess &&
               hipMalloc(&m->sendCounts_, kMaxSlabs * 4) == hipSuccess &&
               hipMalloc(&m->countsAll_, kMaxSlabs * kMaxSlabs * 4) == hipSuccess &&
-              hipMalloc(&m->recv_, G * sizeof(SplatRecord)) == hipSuccess &&  // a slab receives each id once
+              // a slab receives each id at most once; uncached, so peers' xGMI stores and the owner's
+              // reads meet in HBM without any L2 holding a stale line of the previous frame
+              hipExtMallocWithFlags((void**)&m->recv_, G * sizeof(SplatRecord), hipDeviceMallocUncached) ==
+                  hipSuccess &&
               hipMalloc(&m->recvCount_, 4) == hipSuccess && hipMalloc(&m->order_, 4) == hipSuccess &&
               hipMemset(m->order_, 0, 4) == hipSuccess && hipMemset(m->recvCount_, 0, 4) == hipSuccess;
     // receive buffers of every rank, opened once from their IPC handles (gathered over RCCL)

@@ -36,6 +36,10 @@ struct SplatRecord {
     uint32_t pad;
 };
 static_assert(sizeof(SplatRecord) == 48, "SplatRecord must be 48 B");
+// the receive buffer of every slab owner (peer device pointers; the multi-GPU exchange)
+struct SlabPeers {
+    SplatRecord* recv[kMaxSlabs];
+};
 struct PartitionBuffers {
     SplatRecord* records = nullptr;     // [maxG] projected records of the rank's range
     uint32_t* masks = nullptr;          // [maxG] slabs each gaussian meets
@@ -114,6 +118,13 @@ void launch_partition(bool halfInput, uint32_t shDegree, const void* world, cons
                       const ProjectArgs& args, const SlabTable& slabs, const PartitionBuffers& B,
                       const float2* sincos, void* send, uint64_t capacity, uint32_t* sendCounts,
                       hipStream_t stream);
+// the first half of launch_partition (projection + per-slab counts, no packing), then the records
+// written straight to every slab owner from the all-gathered count matrix (gsm_multigpu.hip)
+void launch_partition_counts(bool halfInput, uint32_t shDegree, const void* world, const void* harmonics,
+                             const ProjectArgs& args, const SlabTable& slabs, const PartitionBuffers& B,
+                             const float2* sincos, uint32_t* sendCounts, hipStream_t stream);
+void launch_partition_push(const ProjectArgs& args, uint32_t world, uint32_t rank, const PartitionBuffers& B,
+                           const uint32_t* counts, const SlabPeers& peers, uint32_t* recvCount, hipStream_t stream);
 // received records -> per-gaussian arrays + tile counts of the renderer's rows (replaces project)
 void launch_records_in(const void* records, const ProjectArgs& args, const DeviceArena& A,
                        hipStream_t stream, const uint32_t* devCount = nullptr);

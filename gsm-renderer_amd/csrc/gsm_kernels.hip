@@ -617,6 +617,54 @@ __global__ __launch_bounds__(256) void k_tile_starts(const uint32_t* __restrict_
     }
 }
 
+// The multi-GPU frame's direct exchange (gsm_multigpu.hip): k_part_pack with every slab's records
+// written straight into the slab owner's receive buffer (peer pointers over xGMI) at the offset the
+// all-gathered count matrix gives -- counts[r * world + s] = records rank r holds for slab s, so
+// rank r's records of slab s start after those of ranks 0..r-1 (ascending id order at the owner).
+// Block 0 also leaves the rank's own receive count in *recvCount.
+__global__ __launch_bounds__(kProjectBlock) void k_part_push(
+    const SplatRecord* __restrict__ records, const uint32_t* __restrict__ masks, uint32_t count,
+    uint32_t world, uint32_t rank, const uint32_t* __restrict__ blockSlabOffsets,
+    const uint32_t* __restrict__ counts, SlabPeers peers, uint32_t* __restrict__ recvCount) {
+    __shared__ uint32_t wcnt[kProjectBlock / 64][kMaxSlabs];
+    __shared__ uint32_t dstOff[kMaxSlabs];
+    const uint32_t gid = blockIdx.x * kProjectBlock + threadIdx.x;
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (threadIdx.x < world) {
+        uint32_t before = 0;
+        for (uint32_t r = 0; r < rank; ++r) before += counts[r * world + threadIdx.x];
+        dstOff[threadIdx.x] = before;
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        uint32_t mine = 0;
+        for (uint32_t r = 0; r < world; ++r) mine += counts[r * world + rank];
+        *recvCount = mine;
+    }
+    const uint32_t mask = gid < count ? masks[gid] : 0u;
+    const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    uint32_t rnk[kMaxSlabs];
+    for (uint32_t sl = 0; sl < world; ++sl) {
+        const uint64_t b = __ballot((mask >> sl) & 1u);
+        rnk[sl] = (uint32_t)__popcll(b & lt);
+        if (lane == 0) wcnt[wave][sl] = (uint32_t)__popcll(b);
+    }
+    __syncthreads();
+    if (!mask) return;
+    const uint4* src = (const uint4*)(records + gid);
+    const uint4 a = src[0], b = src[1], c = src[2];
+    for (uint32_t sl = 0; sl < world; ++sl) {
+        if (!((mask >> sl) & 1u)) continue;
+        uint32_t before = 0;
+        for (uint32_t w = 0; w < wave; ++w) before += wcnt[w][sl];
+        const uint64_t pos =
+            (uint64_t)dstOff[sl] + blockSlabOffsets[(size_t)sl * gridDim.x + blockIdx.x] + before + rnk[sl];
+        uint4* dst = (uint4*)(peers.recv[sl] + pos);
+        dst[0] = a;
+        dst[1] = b;
+        dst[2] = c;
+    }
+}
+
 // ---------------------------------------------------------------------------
 // 5. the blend's half-tile lists: per tile, the sorted ids whose skip flag for half h is clear, in
 //    list order, compacted to the tile's start in halfVals[h], and their counts.  One workgroup per
@@ -749,6 +797,32 @@ void launch_partition(bool halfInput, uint32_t deg, const void* world, const voi
                        sendCounts, B.slabBase);
     hipLaunchKernelGGL(k_part_pack, dim3(blocks), dim3(kProjectBlock), 0, s, B.records, B.masks, a.count,
                        slabs.n, B.blockSlabCounts, B.slabBase, (SplatRecord*)send, capacity);
+}
+
+void launch_partition_counts(bool halfInput, uint32_t deg, const void* world, const void* harm, const ProjectArgs& a,
+                             const SlabTable& slabs, const PartitionBuffers& B, const float2* sincos,
+                             uint32_t* sendCounts, hipStream_t s) {
+    const uint32_t blocks = (a.count + kProjectBlock - 1) / kProjectBlock;
+    if (blocks == 0) {
+        hipMemsetAsync(sendCounts, 0, slabs.n * sizeof(uint32_t), s);
+        return;
+    }
+    if (halfInput) launch_project_part_t<true>(deg, world, harm, a, slabs, B, sincos, s);
+    else launch_project_part_t<false>(deg, world, harm, a, slabs, B, sincos, s);
+    hipLaunchKernelGGL(k_part_scan, dim3(1), dim3(1024), 0, s, B.blockSlabCounts, blocks, slabs.n, sendCounts,
+                       B.slabBase);
+}
+
+void launch_partition_push(const ProjectArgs& a, uint32_t world, uint32_t rank, const PartitionBuffers& B,
+                           const uint32_t* counts, const SlabPeers& peers, uint32_t* recvCount, hipStream_t s) {
+    const uint32_t blocks = (a.count + kProjectBlock - 1) / kProjectBlock;
+    if (blocks == 0) {  // no ids here: the receive count still comes from the matrix
+        hipLaunchKernelGGL(k_part_push, dim3(1), dim3(kProjectBlock), 0, s, B.records, B.masks, 0u, world, rank,
+                           B.blockSlabCounts, counts, peers, recvCount);
+        return;
+    }
+    hipLaunchKernelGGL(k_part_push, dim3(blocks), dim3(kProjectBlock), 0, s, B.records, B.masks, a.count, world,
+                       rank, B.blockSlabCounts, counts, peers, recvCount);
 }
 
 void launch_records_in(const void* records, const ProjectArgs& a, const DeviceArena& A, hipStream_t s,

@@ -3,13 +3,14 @@
 //
 // One process and one GlobalRenderer per GPU; the caller hands over its RCCL communicator.  Per
 // frame, enqueue-only on the caller's stream, no host synchronisation:
-//   1. project the rank's id range once, records packed per destination slab
-//      (GlobalRenderer::projectPartition: k_project_part, k_part_scan, k_part_pack);
+//   1. project the rank's id range once and count its records per destination slab
+//      (GlobalRenderer::partitionCounts: k_project_part, k_part_scan);
 //   2. ncclAllGather of the per-slab counts: every rank holds the world x world count matrix on
 //      the device;
-//   3. k_push: every record goes straight into its slab owner's receive buffer over xGMI (peer
-//      pointers opened once from IPC handles), at the offset the count matrix gives -- rank order,
-//      so the receiver's records are in ascending id order (the stable sort's tie order);
+//   3. k_part_push: every record goes straight from the projection into its slab owner's receive
+//      buffer over xGMI (peer pointers opened once from IPC handles), at the offset the count matrix
+//      gives -- rank order, so the receiver's records are in ascending id order (the stable sort's
+//      tie order); no send buffer, no copy pass;
 //   4. ncclAllReduce of one word orders every rank's pushes before every rank's render;
 //   5. the owner renders its tile rows from the received records, their count read on the device;
 //   6. the bands are gathered into rank 0's frame with grouped ncclSend / ncclRecv (fixed sizes:
@@ -66,49 +67,6 @@ const Rccl& rccl() {
     return R;
 }
 
-struct PeerTable {
-    SplatRecord* recv[kMaxSlabs];
-};
-
-// k_push: record i of the rank's send buffer (slab-major) -> its slab owner's receive buffer.
-// counts[r * world + d] = records rank r sends to slab d.  Thread 0 also leaves the rank's own
-// receive count in *recvCount.
-__global__ __launch_bounds__(256) void k_push(const SplatRecord* __restrict__ send,
-                                              const uint32_t* __restrict__ counts, uint32_t rank, uint32_t world,
-                                              PeerTable peers, uint32_t* __restrict__ recvCount) {
-    __shared__ uint32_t sendOff[kMaxSlabs + 1], dstOff[kMaxSlabs];
-    if (threadIdx.x == 0) {
-        uint32_t o = 0;
-        for (uint32_t d = 0; d < world; ++d) {
-            sendOff[d] = o;
-            o += counts[rank * world + d];
-            uint32_t before = 0;
-            for (uint32_t r = 0; r < rank; ++r) before += counts[r * world + d];
-            dstOff[d] = before;
-        }
-        sendOff[world] = o;
-        if (blockIdx.x == 0) {
-            uint32_t mine = 0;
-            for (uint32_t r = 0; r < world; ++r) mine += counts[r * world + rank];
-            *recvCount = mine;
-        }
-    }
-    __syncthreads();
-    const uint32_t total = sendOff[world];
-    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < total; i += gridDim.x * 256u) {
-        uint32_t d = 0;
-        while (d + 1 < world && i >= sendOff[d + 1]) ++d;
-        const uint4* src = (const uint4*)(send + i);
-        uint4* dst = (uint4*)(peers.recv[d] + dstOff[d] + (i - sendOff[d]));
-        const uint4 a = src[0], b = src[1], c = src[2];
-        dst[0] = a;
-        dst[1] = b;
-        dst[2] = c;
-    }
-    // no fence: the receive buffers are uncached device memory (MultiGpu::create), so these stores
-    // reach the owner's HBM directly and are complete when the kernel is; the ordering collective
-    // that follows on every rank's stream orders them before any owner's read
-}
 }  // namespace
 
 class MultiGpu {
@@ -125,14 +83,12 @@ class MultiGpu {
     GlobalRenderer* r_ = nullptr;
     ncclComm_t comm_ = nullptr;
     int rank_ = 0, world_ = 1, device_ = 0;
-    SplatRecord* send_ = nullptr;
-    uint64_t sendCap_ = 0;
     uint32_t* sendCounts_ = nullptr;
     uint32_t* countsAll_ = nullptr;
     SplatRecord* recv_ = nullptr;
     uint32_t* recvCount_ = nullptr;
     int* order_ = nullptr;  // the ordering collective's word
-    PeerTable peers_{};
+    SlabPeers peers_{};
     std::vector<void*> opened_;
 };
 
@@ -140,9 +96,9 @@ void MultiGpu::release() {
     hipSetDevice(device_);
     for (void* p : opened_) hipIpcCloseMemHandle(p);
     opened_.clear();
-    for (void* p : {(void*)send_, (void*)sendCounts_, (void*)countsAll_, (void*)recv_, (void*)recvCount_, (void*)order_})
+    for (void* p : {(void*)sendCounts_, (void*)countsAll_, (void*)recv_, (void*)recvCount_, (void*)order_})
         if (p) hipFree(p);
-    send_ = recv_ = nullptr;
+    recv_ = nullptr;
     sendCounts_ = countsAll_ = recvCount_ = nullptr;
     order_ = nullptr;
 }
@@ -165,13 +121,12 @@ gsm_status MultiGpu::create(GlobalRenderer* r, void* comm, int rank, int world, 
     m->world_ = world;
     m->device_ = r->device();
     const uint64_t G = r->maxGaussians();
-    const uint64_t per = (G + (uint64_t)world - 1) / (uint64_t)world;  // the rank's id range bound
-    m->sendCap_ = per * (uint64_t)world;  // a gaussian meets at most every slab once
-    bool ok = hipMalloc(&m->send_, m->sendCap_ * sizeof(SplatRecord)) == hipSuccess &&
-              hipMalloc(&m->sendCounts_, kMaxSlabs * 4) == hipSuccess &&
+    bool ok = hipMalloc(&m->sendCounts_, kMaxSlabs * 4) == hipSuccess &&
               hipMalloc(&m->countsAll_, kMaxSlabs * kMaxSlabs * 4) == hipSuccess &&
-              // a slab receives each id at most once; uncached, so peers' xGMI stores and the owner's
-              // reads meet in HBM without any L2 holding a stale line of the previous frame
+              // a slab receives each id at most once; uncached, so peers' xGMI stores (k_part_push, no
+              // fence: they are complete when the kernel is, and the ordering collective on every
+              // stream follows it) and the owner's reads meet in HBM without any L2 holding a stale
+              // line of the previous frame
               hipExtMallocWithFlags((void**)&m->recv_, G * sizeof(SplatRecord), hipDeviceMallocUncached) ==
                   hipSuccess &&
               hipMalloc(&m->recvCount_, 4) == hipSuccess && hipMalloc(&m->order_, 4) == hipSuccess &&
@@ -231,14 +186,10 @@ gsm_status MultiGpu::render(hipStream_t s, const gsm_gaussian_input& in, const g
     const uint32_t first = rank * perIds < N ? rank * perIds : N;
     const uint32_t cnt = perIds < N - first ? perIds : N - first;
 
-    gsm_status st = r_->projectPartition(s, in, cam, width, height, first, cnt, rows, world, send_, sendCap_,
-                                         sendCounts_);
+    gsm_status st = r_->partitionCounts(s, in, cam, width, height, first, cnt, rows, world, sendCounts_);
     if (st != GSM_OK) return st;
     if (R.allGather(sendCounts_, countsAll_, world, ncclUint32, comm_, s) != ncclSuccess) return GSM_ERR_RENDER_FAILED;
-    uint32_t grid = (uint32_t)((sendCap_ + 255) / 256);
-    if (grid > 2048u) grid = 2048u;
-    if (grid == 0) grid = 1;
-    hipLaunchKernelGGL(k_push, dim3(grid), dim3(256), 0, s, send_, countsAll_, rank, world, peers_, recvCount_);
+    if ((st = r_->partitionPush(s, world, rank, countsAll_, peers_, recvCount_)) != GSM_OK) return st;
     if (R.allReduce(order_, order_, 1, ncclInt32, ncclSum, comm_, s) != ncclSuccess) return GSM_ERR_RENDER_FAILED;
     const uint32_t y0 = rows[rank] * kTileHeight < height ? rows[rank] * kTileHeight : height;
     const uint32_t y1 = rows[rank + 1] * kTileHeight < height ? rows[rank + 1] * kTileHeight : height;

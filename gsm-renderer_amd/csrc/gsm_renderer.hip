@@ -267,24 +267,22 @@ gsm_status GlobalRenderer::renderRecords(hipStream_t s, const void* records, uin
                     [&](const ProjectArgs& pa) { launch_records_in(records, pa, arena_, s, devCount); });
 }
 
-gsm_status GlobalRenderer::projectPartition(hipStream_t s, const gsm_gaussian_input& in,
-                                            const gsm_camera_params& camp, uint32_t width, uint32_t height,
-                                            uint32_t first, uint32_t count, const uint32_t* slabRows,
-                                            uint32_t numSlabs, void* send, uint64_t capacity,
-                                            uint32_t* sendCounts) {
+gsm_status GlobalRenderer::preparePartition(const gsm_gaussian_input& in, const gsm_camera_params& camp,
+                                            uint32_t width, uint32_t height, uint32_t first, uint32_t count,
+                                            const uint32_t* slabRows, uint32_t numSlabs, bool needSend,
+                                            const void* send, const uint32_t* sendCounts, PartitionFrame* f) {
     if ((uint64_t)first + count > in.gaussian_count || count > maxGaussians_)
         return GSM_ERR_INVALID_GAUSSIAN_COUNT;
     if (width == 0 || height == 0 || width > maxWidth_ || height > maxHeight_)
         return GSM_ERR_INVALID_DIMENSIONS;
     if (!slabRows || numSlabs == 0 || numSlabs > kMaxSlabs) return GSM_ERR_INVALID_ARGUMENT;
-    if (!sendCounts || (count > 0 && (!send || !in.gaussians || !in.harmonics)))
+    if (!sendCounts || (count > 0 && ((needSend && !send) || !in.gaussians || !in.harmonics)))
         return GSM_ERR_MISSING_REQUIRED_BUFFER;
-    SlabTable slabs;
-    std::memset(&slabs, 0, sizeof(slabs));
-    slabs.n = numSlabs;
+    std::memset(&f->slabs, 0, sizeof(f->slabs));
+    f->slabs.n = numSlabs;
     for (uint32_t i = 0; i <= numSlabs; ++i) {
         if (slabRows[i] > tilesY_ || (i > 0 && slabRows[i] < slabRows[i - 1])) return GSM_ERR_INVALID_ARGUMENT;
-        slabs.rows[i] = slabRows[i];
+        f->slabs.rows[i] = slabRows[i];
     }
     if (hipSetDevice(device_) != hipSuccess) return GSM_ERR_DEVICE_NOT_AVAILABLE;
     if (!part_.records) {  // lazily: only ranks of a partitioned frame need these
@@ -298,17 +296,53 @@ gsm_status GlobalRenderer::projectPartition(hipStream_t s, const gsm_gaussian_in
             return st;
         }
     }
-    const bool half = config_.precision == GSM_PRECISION_FLOAT16;
-    ProjectArgs a = frameArgs(camp, width, height, count, in.sh_components);
-    a.rowBegin = 0;
-    a.rowEnd = tilesY_;
-    const size_t ws = half ? sizeof(PackedWorldGaussianHalf) : sizeof(PackedWorldGaussian);
-    const size_t hs = (size_t)in.sh_components * 3 * (half ? 2 : 4);
-    const char* world = (const char*)in.gaussians + (size_t)first * ws;
-    const char* harm = (const char*)in.harmonics + (size_t)first * hs;
+    f->half = config_.precision == GSM_PRECISION_FLOAT16;
+    f->a = frameArgs(camp, width, height, count, in.sh_components);
+    f->a.rowBegin = 0;
+    f->a.rowEnd = tilesY_;
+    const size_t ws = f->half ? sizeof(PackedWorldGaussianHalf) : sizeof(PackedWorldGaussian);
+    const size_t hs = (size_t)in.sh_components * 3 * (f->half ? 2 : 4);
+    f->world = (const char*)in.gaussians + (size_t)first * ws;
+    f->harm = (const char*)in.harmonics + (size_t)first * hs;
     const uint32_t k = in.sh_components;
-    const uint32_t deg = k <= 1 ? 0u : (k <= 4 ? 1u : (k <= 9 ? 2u : 3u));
-    launch_partition(half, deg, world, harm, a, slabs, part_, arena_.sincosTable, send, capacity, sendCounts, s);
+    f->deg = k <= 1 ? 0u : (k <= 4 ? 1u : (k <= 9 ? 2u : 3u));
+    return GSM_OK;
+}
+
+gsm_status GlobalRenderer::projectPartition(hipStream_t s, const gsm_gaussian_input& in,
+                                            const gsm_camera_params& camp, uint32_t width, uint32_t height,
+                                            uint32_t first, uint32_t count, const uint32_t* slabRows,
+                                            uint32_t numSlabs, void* send, uint64_t capacity,
+                                            uint32_t* sendCounts) {
+    PartitionFrame f;
+    gsm_status st = preparePartition(in, camp, width, height, first, count, slabRows, numSlabs, true, send,
+                                     sendCounts, &f);
+    if (st != GSM_OK) return st;
+    launch_partition(f.half, f.deg, f.world, f.harm, f.a, f.slabs, part_, arena_.sincosTable, send, capacity,
+                     sendCounts, s);
+    if (hipGetLastError() != hipSuccess) return GSM_ERR_RENDER_FAILED;
+    return GSM_OK;
+}
+
+gsm_status GlobalRenderer::partitionCounts(hipStream_t s, const gsm_gaussian_input& in, const gsm_camera_params& camp,
+                                           uint32_t width, uint32_t height, uint32_t first, uint32_t count,
+                                           const uint32_t* slabRows, uint32_t numSlabs, uint32_t* sendCounts) {
+    PartitionFrame f;
+    gsm_status st = preparePartition(in, camp, width, height, first, count, slabRows, numSlabs, false, nullptr,
+                                     sendCounts, &f);
+    if (st != GSM_OK) return st;
+    launch_partition_counts(f.half, f.deg, f.world, f.harm, f.a, f.slabs, part_, arena_.sincosTable, sendCounts, s);
+    partCount_ = count;
+    if (hipGetLastError() != hipSuccess) return GSM_ERR_RENDER_FAILED;
+    return GSM_OK;
+}
+
+gsm_status GlobalRenderer::partitionPush(hipStream_t s, uint32_t world, uint32_t rank, const uint32_t* counts,
+                                         const SlabPeers& peers, uint32_t* recvCount) {
+    ProjectArgs a;
+    std::memset(&a, 0, sizeof(a));
+    a.count = partCount_;
+    launch_partition_push(a, world, rank, part_, counts, peers, recvCount, s);
     if (hipGetLastError() != hipSuccess) return GSM_ERR_RENDER_FAILED;
     return GSM_OK;
 }

@@ -28,6 +28,13 @@ class GlobalRenderer {
                                 const gsm_camera_params& camera, uint32_t width, uint32_t height,
                                 uint32_t first, uint32_t count, const uint32_t* slabRows, uint32_t numSlabs,
                                 void* send, uint64_t capacity, uint32_t* sendCounts);
+    // the same projection for the direct exchange: per-slab counts first, then the records written
+    // into every slab owner's receive buffer once the count matrix is on the device (gsm_multigpu.hip)
+    gsm_status partitionCounts(hipStream_t stream, const gsm_gaussian_input& input, const gsm_camera_params& camera,
+                               uint32_t width, uint32_t height, uint32_t first, uint32_t count,
+                               const uint32_t* slabRows, uint32_t numSlabs, uint32_t* sendCounts);
+    gsm_status partitionPush(hipStream_t stream, uint32_t world, uint32_t rank, const uint32_t* counts,
+                             const SlabPeers& peers, uint32_t* recvCount);
     gsm_status renderRecords(hipStream_t stream, const void* records, uint32_t count, uint32_t width,
                              uint32_t height, void* color, size_t colorPitch, void* depth, size_t depthPitch,
                              const uint32_t* devCount = nullptr);
@@ -55,6 +62,19 @@ class GlobalRenderer {
     gsm_status runFrame(hipStream_t s, const ProjectArgs& a, uint32_t width, uint32_t height, void* color,
                         size_t colorPitch, void* depth, size_t depthPitch, Front&& front);
     PartitionBuffers part_;
+    uint32_t partCount_ = 0;  // ids of the last partitionCounts
+    struct PartitionFrame {
+        ProjectArgs a;
+        SlabTable slabs;
+        const void* world;
+        const void* harm;
+        uint32_t deg;
+        bool half;
+    };
+    gsm_status preparePartition(const gsm_gaussian_input& in, const gsm_camera_params& camera, uint32_t width,
+                                uint32_t height, uint32_t first, uint32_t count, const uint32_t* slabRows,
+                                uint32_t numSlabs, bool needSend, const void* send, const uint32_t* sendCounts,
+                                PartitionFrame* f);
     void release();
     int sortPassCount() const;
 

@@ -19,6 +19,10 @@ __global__ void k_peak(unsigned* out, unsigned long long* clk) {
     unsigned a0 = threadIdx.x, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4, a5 = a0 + 5, a6 = a0 + 6,
              a7 = a0 + 7;
     const unsigned m = 0x3C003C01u, c = 0x00010001u;
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    f2 p0 = {(float)threadIdx.x, 1.f}, p1 = p0 + 1.f, p2 = p0 + 2.f, p3 = p0 + 3.f, p4 = p0 + 4.f, p5 = p0 + 5.f,
+       p6 = p0 + 6.f, p7 = p0 + 7.f;
+    const f2 pm = {0.999f, 1.001f}, pc = {0.5f, 0.25f};
     const unsigned long long t0 = __builtin_amdgcn_s_memtime();
     const unsigned long long r0 = __builtin_amdgcn_s_memrealtime();
     for (int it = 0; it < ITERS; ++it) {
@@ -31,14 +35,17 @@ __global__ void k_peak(unsigned* out, unsigned long long* clk) {
     if (OP == 3) asm volatile("v_mul_f32 %0, %0, %1" : "+v"(a##i) : "v"(m));                                 \
     if (OP == 4) asm volatile("v_fma_f32 %0, %0, %1, %2" : "+v"(a##i) : "v"(m), "v"(c));                     \
     if (OP == 5) asm volatile("v_add_u32 %0, %0, %1" : "+v"(a##i) : "v"(m));                                 \
-    if (OP == 6) asm volatile("v_pk_max_u16 %0, %0, %1" : "+v"(a##i) : "v"(m));
+    if (OP == 6) asm volatile("v_pk_max_u16 %0, %0, %1" : "+v"(a##i) : "v"(m));                              \
+    if (OP == 7) asm volatile("v_pk_mul_f32 %0, %0, %1" : "+v"(p##i) : "v"(pm));                             \
+    if (OP == 8) asm volatile("v_pk_fma_f32 %0, %0, %1, %2" : "+v"(p##i) : "v"(pm), "v"(pc));
             REP8(ACC)
 #undef ACC
         }
     }
     const unsigned long long t1 = __builtin_amdgcn_s_memtime();
     const unsigned long long r1 = __builtin_amdgcn_s_memrealtime();
-    out[blockIdx.x * blockDim.x + threadIdx.x] = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7;
+    const f2 ps = p0 + p1 + p2 + p3 + p4 + p5 + p6 + p7;
+    out[blockIdx.x * blockDim.x + threadIdx.x] = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7 ^ (unsigned)(ps.x + ps.y);
     if (threadIdx.x == 0) {
         clk[2 * blockIdx.x] = t1 - t0;
         clk[2 * blockIdx.x + 1] = r1 - r0;
@@ -100,5 +107,7 @@ int main() {
     run<4>("v_fma_f32", cus, out, clk);
     run<5>("v_add_u32", cus, out, clk);
     run<6>("v_pk_max_u16", cus, out, clk);
+    run<7>("v_pk_mul_f32", cus, out, clk);
+    run<8>("v_pk_fma_f32", cus, out, clk);
     return 0;
 }

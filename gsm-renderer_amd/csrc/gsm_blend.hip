@@ -74,7 +74,7 @@ constexpr bool kLdsRecords = true;
 template <int NT, int P, bool COMPACT = false>
 __global__ __launch_bounds__(NT) void k_blend_px(
     const uint32_t* __restrict__ tileStart, const uint32_t* __restrict__ sortedVals,
-    const BlendRecordA* __restrict__ recA, const uint32_t* __restrict__ recB,
+    const BlendRecord* __restrict__ rec,
     const uint16_t* __restrict__ expTable, uint32_t* __restrict__ queue, uint32_t tileBegin,
     uint32_t numTiles, uint32_t tilesX, uint32_t W, uint32_t H, uint8_t* __restrict__ color,
     size_t colorPitch, uint8_t* __restrict__ depth, size_t depthPitch, int flags,
@@ -177,10 +177,13 @@ __global__ __launch_bounds__(NT) void k_blend_px(
         offX[0] = (grp & 3u) * 4u + (lane & 1u) * 2u;
         offY[0] = (grp >> 2) * 2u + ((lane >> 1) & 1u);
     } else if (P == 2) {
+        // a 4x2 group on lanes 2g (columns 0-1) and 2g + 1 (columns 2-3), each lane 2x2 pixels:
+        // pair 0 = row 0, pair 1 = row 1 of the same two columns, so the dx terms of the quadratic
+        // form are shared by the lane's pairs and the dy terms come as one pair of rows
         const uint32_t grp = lane >> 1;
-        offX[0] = (grp & 3u) * 4u;
-        offX[P - 1] = offX[0] + 2u;
-        offY[0] = offY[P - 1] = (grp >> 2) * 2u + (lane & 1u);
+        offX[0] = offX[P - 1] = (grp & 3u) * 4u + (lane & 1u) * 2u;
+        offY[0] = (grp >> 2) * 2u;
+        offY[P - 1] = offY[0] + 1u;
     } else {
         offX[0] = offX[2 % P] = (lane & 7u) * 4u;
         offX[1 % P] = offX[3 % P] = (lane & 7u) * 4u + 2u;
@@ -249,12 +252,12 @@ __global__ __launch_bounds__(NT) void k_blend_px(
             const uint32_t gi0 = lst[min(lane, last)];
             const uint32_t gi1 = lst[min(64u + lane, last)];
             const uint32_t gi2 = lst[min(128u + lane, last)];
-            uint4 bA = *(const uint4*)(recA + gi0);
-            uint32_t bB = recB[gi0];
-            uint4 nA = *(const uint4*)(recA + gi1);
-            uint32_t nB = recB[gi1];
-            uint4 mA = *(const uint4*)(recA + gi2);
-            uint32_t mB = recB[gi2];
+            uint4 bA = *(const uint4*)(rec + gi0);
+            uint32_t bB = rec[gi0].b;
+            uint4 nA = *(const uint4*)(rec + gi1);
+            uint32_t nB = rec[gi1].b;
+            uint4 mA = *(const uint4*)(rec + gi2);
+            uint32_t mB = rec[gi2].b;
             uint32_t nI = lst[min(192u + lane, last)];
             if (lane == 0) nextQ = atomicAdd(queue, 1u);
             if (lane >= count) {
@@ -272,11 +275,19 @@ __global__ __launch_bounds__(NT) void k_blend_px(
             bool alive = true;
             uint32_t eC = 0, b0C = 0;  // compaction: next entry, its batch base
             // p = ((dx*dx)*cxx + (dy*dy)*cyy) + (dx*dy)*cxy2 (GlobalShaders.metal:1115-1122);
-            // the dy terms are shared by the pairs of a row
+            // the dy terms are computed once for the lane's rows, at P = 2 the dx terms once for its
+            // two columns (the same operations per pixel, fewer of them per lane)
             auto quadform = [&](uint32_t r0, uint32_t r1, uint32_t r2, h2 (&pq)[P]) {
                 const h2 mean = as_h2(r0), cc = as_h2(r1), oc = as_h2(r2);
                 const h2 dyv = Yv - splat_hi(mean);
                 const h2 dyy = (dyv * dyv) * splat_hi(cc);
+                if constexpr (P == 2) {
+                    const h2 dx = X[0] - splat_lo(mean);
+                    const h2 dxx = (dx * dx) * splat_lo(cc);
+                    pq[0] = (dxx + splat_lo(dyy)) + (dx * splat_lo(dyv)) * splat_lo(oc);
+                    pq[P - 1] = (dxx + splat_hi(dyy)) + (dx * splat_hi(dyv)) * splat_lo(oc);
+                    return;
+                }
 #pragma unroll
                 for (int k = 0; k < P; ++k) {
                     const h2 dx = X[k] - splat_lo(mean);
@@ -418,8 +429,8 @@ __global__ __launch_bounds__(NT) void k_blend_px(
                 const bool mv = b0 + 128u + lane < count;
                 nA = mv ? mA : pad;
                 nB = mv ? mB : 0u;
-                mA = *(const uint4*)(recA + nI);
-                mB = recB[nI];
+                mA = *(const uint4*)(rec + nI);
+                mB = rec[nI].b;
                 nI = lst[min(b0 + 256u + lane, last)];
             }
         compact_phase:
@@ -440,11 +451,12 @@ __global__ __launch_bounds__(NT) void k_blend_px(
                 const uint32_t gp = lane >> 2, kk = lane & 1u, rr = (lane >> 1) & 1u;
                 const bool valid1 = gp < ng;
                 const uint32_t sg = cscr[wv][valid1 ? gp : 0u];
-                const int srcAddr = (int)((2u * sg + rr) * 4u);
+                // half-tile layout: columns 2kk..2kk+1 of group sg sit on lane 2sg + kk, row rr in pair rr
+                const int srcAddr = (int)((2u * sg + kk) * 4u);
                 auto pick = [&](h2 v0, h2 v1) {
                     const uint32_t a0 = (uint32_t)__builtin_amdgcn_ds_bpermute(srcAddr, (int)as_u32(v0));
                     const uint32_t a1 = (uint32_t)__builtin_amdgcn_ds_bpermute(srcAddr, (int)as_u32(v1));
-                    return as_h2(kk ? a1 : a0);
+                    return as_h2(rr ? a1 : a0);
                 };
                 h2 T1 = pick(T[0], T[1]), R1 = pick(R[0], R[1]), G1 = pick(G[0], G[1]);
                 h2 B1 = pick(B[0], B[1]), D1 = pick(D[0], D[1]);
@@ -466,8 +478,8 @@ __global__ __launch_bounds__(NT) void k_blend_px(
                     const bool mv = base + 128u + lane < count;
                     nA = mv ? mA : pad;
                     nB = mv ? mB : 0u;
-                    mA = *(const uint4*)(recA + nI);
-                    mB = recB[nI];
+                    mA = *(const uint4*)(rec + nI);
+                    mB = rec[nI].b;
                     nI = lst[min(base + 256u + lane, last)];
                 };
                 uint32_t e = eC, bb = b0C;
@@ -703,8 +715,8 @@ void launch_blend(const uint32_t* sortedVals, const FrameGeometry& g, const Devi
     if (grid > (uint32_t)numCUs) grid = (uint32_t)numCUs;
     const uint32_t* order = costOrder ? A.unitOrder : nullptr;
 #define GSM_LAUNCH_BLEND(NTH, PP, CMP)                                                                       \
-    hipLaunchKernelGGL((k_blend_px<NTH, PP, CMP>), dim3(grid), dim3(NTH), 0, s, A.tileStart, sortedVals, A.recA, \
-                       A.recB, A.expTable, A.tileQueue, t0, numTiles, g.tilesX, g.width, g.height,          \
+    hipLaunchKernelGGL((k_blend_px<NTH, PP, CMP>), dim3(grid), dim3(NTH), 0, s, A.tileStart, sortedVals, A.rec, \
+                       A.expTable, A.tileQueue, t0, numTiles, g.tilesX, g.width, g.height,          \
                        (uint8_t*)color, colorPitch, (uint8_t*)depth, depthPitch, flags, order, A.unitCost,  \
                        A.blendTrace, A.halfVals[0], A.halfVals[1], A.halfCount, g.tileCount)
     // half tiles compact to one pair per lane once <= 16 of their 32 groups are alive

@@ -51,8 +51,7 @@ struct PartitionBuffers {
 struct DeviceArena {
     GaussianRenderData* renderData = nullptr;  // [maxG]
     short4* bounds = nullptr;                  // [maxG]
-    BlendRecordA* recA = nullptr;              // [maxG]
-    uint32_t* recB = nullptr;                  // [maxG]
+    BlendRecord* rec = nullptr;                // [maxG] blend records, 32 B each
     uint32_t* tileCounts = nullptr;            // [maxG]
     uint32_t* tileMasks = nullptr;             // [maxG] tile tests of rects <= 32 tiles, scan order
     uint32_t* blockSums = nullptr;             // [ceil(maxG/256) + 1]

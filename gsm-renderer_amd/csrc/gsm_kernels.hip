@@ -213,11 +213,31 @@ __device__ __forceinline__ uint32_t count_tiles(const ProjOut& o, int rowBegin, 
     return n;
 }
 
+// The blend's half-tile skip band of a projected gaussian (BandSkip of its fp16 blend record),
+// checked once against its tile rect within rows [rowBegin, rowEnd): (mean x, half width), or a
+// negative width when the band may not be used.  Stored in the blend record's padding for k_scatter.
+__device__ __forceinline__ bool band_rect_ok(const BandSkip& b, int x0, int x1, int y0, int y1) {
+    if (!b.valid) return false;
+    const int mxm = fp16_coord_margin(x1), mym = fp16_coord_margin(y1);
+    if (mxm < 0 || mym < 0) return false;
+    const float ax = __builtin_fmaxf(__builtin_fabsf((float)(x0 - mxm) - b.mx), __builtin_fabsf((float)(x1 + mxm) - b.mx));
+    const float ay = __builtin_fmaxf(__builtin_fabsf((float)(y0 - mym) - b.my), __builtin_fabsf((float)(y1 + mym) - b.my));
+    return ax <= 200.0f && ay <= 200.0f && b.cxx * (ax * ax) + b.cyy * (ay * ay) <= 16000.0f;
+}
+__device__ __forceinline__ float2 band_of(const BlendRecordA& ra, short4 r, int rowBegin, int rowEnd) {
+    const BandSkip b = band_skip_setup(ra.x, ra.y, ra.z, kBlendZeroP);
+    const int by0 = max((int)r.z, rowBegin), by1 = min((int)r.w, rowEnd - 1);
+    if (band_rect_ok(b, (int)r.x * (int)kTileWidth, (int)r.y * (int)kTileWidth + (int)kTileWidth - 1,
+                     by0 * (int)kTileHeight, by1 * (int)kTileHeight + (int)kTileHeight - 1))
+        return make_float2(b.mx, b.ex);
+    return make_float2(0.0f, -1.0f);
+}
+
 template <bool HALF, int DEG>
 __global__ __launch_bounds__(kProjectBlock) void k_project(
     const void* __restrict__ world, const void* __restrict__ harm, ProjectArgs P,
     GaussianRenderData* __restrict__ outRD, short4* __restrict__ outBounds,
-    BlendRecordA* __restrict__ outA, uint32_t* __restrict__ outB, uint32_t* __restrict__ counts,
+    BlendRecord* __restrict__ outRec, uint32_t* __restrict__ counts,
     uint32_t* __restrict__ masks, uint32_t* __restrict__ blockSums, const float2* __restrict__ sincos) {
     __shared__ uint32_t lds[kProjectBlock / 64];
     __shared__ uint16_t div255[256];
@@ -229,11 +249,13 @@ __global__ __launch_bounds__(kProjectBlock) void k_project(
         outBounds[gid] = o.bounds;
         if (o.vis) {
             *(uint4*)(outRD + gid) = o.rd;
-            outA[gid] = o.ra;
-            outB[gid] = o.rb;
             uint32_t mask;
             ntiles = count_tiles(o, (int)P.rowBegin, (int)P.rowEnd, &mask);  // rows limited to the slab
             masks[gid] = mask;
+            const float2 band = ntiles ? band_of(o.ra, o.bounds, (int)P.rowBegin, (int)P.rowEnd) : make_float2(0.f, -1.f);
+            uint4* rp = (uint4*)(outRec + gid);
+            rp[0] = make_uint4(o.ra.x, o.ra.y, o.ra.z, o.ra.w);
+            rp[1] = make_uint4(o.rb, __float_as_uint(band.x), __float_as_uint(band.y), 0u);
         }
         counts[gid] = ntiles;
     }
@@ -362,7 +384,7 @@ __global__ __launch_bounds__(kProjectBlock) void k_part_pack(
 // capacity the grid covers and the ids past the count get no tiles.
 __global__ __launch_bounds__(kProjectBlock) void k_records_in(
     const SplatRecord* __restrict__ in, ProjectArgs P, GaussianRenderData* __restrict__ outRD,
-    short4* __restrict__ outBounds, BlendRecordA* __restrict__ outA, uint32_t* __restrict__ outB,
+    short4* __restrict__ outBounds, BlendRecord* __restrict__ outRec,
     uint32_t* __restrict__ counts, uint32_t* __restrict__ masks, uint32_t* __restrict__ blockSums,
     const float2* __restrict__ sincos, const uint32_t* __restrict__ devCount) {
     __shared__ uint32_t lds[kProjectBlock / 64];
@@ -374,8 +396,8 @@ __global__ __launch_bounds__(kProjectBlock) void k_records_in(
         const SplatRecord r = in[gid];
         *(uint4*)(outRD + gid) = r.rd;
         outBounds[gid] = r.bounds;
-        outA[gid] = r.ra;
-        outB[gid] = r.rb;
+        uint4* rp = (uint4*)(outRec + gid);
+        rp[0] = make_uint4(r.ra.x, r.ra.y, r.ra.z, r.ra.w);
         // the values k_project had in registers, rebuilt from the record exactly as k_scatter does
         ProjOut o;
         o.bounds = r.bounds;
@@ -390,6 +412,8 @@ __global__ __launch_bounds__(kProjectBlock) void k_records_in(
         ntiles = count_tiles(o, (int)P.rowBegin, (int)P.rowEnd, &mask);
         counts[gid] = ntiles;
         masks[gid] = mask;
+        const float2 band = ntiles ? band_of(r.ra, r.bounds, (int)P.rowBegin, (int)P.rowEnd) : make_float2(0.f, -1.f);
+        rp[1] = make_uint4(r.rb, __float_as_uint(band.x), __float_as_uint(band.y), 0u);
     }
     uint32_t s = block_reduce_add<kProjectBlock>(ntiles, lds);
     if (threadIdx.x == 0) blockSums[blockIdx.x] = s;
@@ -472,17 +496,8 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_blocks(uint32_t* __restri
 // no longer serialises its wave.  Large rects keep one thread looping over their rect.  Slot
 // order is the reference's (ascending gid, then ty-major, tx-minor).
 // Every value also carries the blend's half-tile skip flags (kHalfSkipShift, gsm_internal.h): the
-// gaussian's column band bound (BandSkip of its fp16 blend record) is set up once per gaussian and
-// checked once against its whole tile rect (band_rect_ok), so a (gaussian, tile) slot only compares
-// the two 16-column halves of its tile with the band [mx - ex, mx + ex] (half_skip_flags).
-__device__ __forceinline__ bool band_rect_ok(const BandSkip& b, int x0, int x1, int y0, int y1) {
-    if (!b.valid) return false;
-    const int mxm = fp16_coord_margin(x1), mym = fp16_coord_margin(y1);
-    if (mxm < 0 || mym < 0) return false;
-    const float ax = __builtin_fmaxf(__builtin_fabsf((float)(x0 - mxm) - b.mx), __builtin_fabsf((float)(x1 + mxm) - b.mx));
-    const float ay = __builtin_fmaxf(__builtin_fabsf((float)(y0 - mym) - b.my), __builtin_fabsf((float)(y1 + mym) - b.my));
-    return ax <= 200.0f && ay <= 200.0f && b.cxx * (ax * ax) + b.cyy * (ay * ay) <= 16000.0f;
-}
+// projection left each gaussian's column band in its blend record (band_of), so a (gaussian, tile)
+// slot only compares the two 16-column halves of its tile with [mx - ex, mx + ex] (half_skip_flags).
 // ex < 0: no skipping for this gaussian; otherwise the band test (BandSkip) on the two halves of tile tx
 __device__ __forceinline__ uint32_t half_skip_flags(float mx, float ex, int tx) {
     if (ex < 0.0f) return 0u;
@@ -498,7 +513,7 @@ __global__ __launch_bounds__(kProjectBlock) void k_scatter(
     ProjectArgs P, const GaussianRenderData* __restrict__ rd, const short4* __restrict__ bounds,
     const uint32_t* __restrict__ counts, const uint32_t* __restrict__ masks,
     const uint32_t* __restrict__ blockOffsets, uint32_t* __restrict__ keys, uint32_t* __restrict__ vals,
-    const float2* __restrict__ sincos, const BlendRecordA* __restrict__ recA) {
+    const float2* __restrict__ sincos, const BlendRecord* __restrict__ rec) {
     __shared__ uint32_t lds[kProjectBlock / 64];
     __shared__ uint32_t sOff[kProjectBlock];
     __shared__ uint32_t sMask[kProjectBlock];  // 0: no cooperative slots (large rect or no tiles)
@@ -519,14 +534,11 @@ __global__ __launch_bounds__(kProjectBlock) void k_scatter(
     float2 band = make_float2(0.0f, -1.0f);
     if (c != 0) {
         r = bounds[gid];
-        const uint4 ra = *(const uint4*)(recA + gid);
-        const BandSkip b = band_skip_setup(ra.x, ra.y, ra.z, kBlendZeroP);
-        const int by0 = max((int)r.z, (int)P.rowBegin), by1 = min((int)r.w, (int)P.rowEnd - 1);
-        if (band_rect_ok(b, (int)r.x * (int)kTileWidth, (int)r.y * (int)kTileWidth + (int)kTileWidth - 1,
-                         by0 * (int)kTileHeight, by1 * (int)kTileHeight + (int)kTileHeight - 1))
-            band = make_float2(b.mx, b.ex);
-        const uint32_t rdz = ((const uint4*)(rd + gid))->z;
-        dbits = ((rdz >> 16) ^ 0x8000u) & 0xFFFFu;
+        const uint4 r1 = ((const uint4*)(rec + gid))[1];  // the band k_project left in the padding
+        band = make_float2(__uint_as_float(r1.y), __uint_as_float(r1.z));
+        // the key's depth: the fp16 depth bits of the blend record (b = colB | depth << 16, the same
+        // bits as GaussianRenderData.depth), so the scatter reads one 16-B slot per gaussian
+        dbits = ((r1.x >> 16) ^ 0x8000u) & 0xFFFFu;
         ty0 = max((int)r.z, (int)P.rowBegin);
         ty1 = min((int)r.w, (int)P.rowEnd - 1);
         const int rw = (int)r.y - (int)r.x + 1;
@@ -748,7 +760,7 @@ static void launch_project_t(uint32_t deg, const void* world, const void* harm, 
     if (blocks == 0) return;
 #define GSM_LAUNCH_PROJ(D)                                                                     \
     hipLaunchKernelGGL((k_project<HALF, D>), dim3(blocks), dim3(kProjectBlock), 0, s, world,   \
-                       harm, a, A.renderData, A.bounds, A.recA, A.recB, A.tileCounts, A.tileMasks, \
+                       harm, a, A.renderData, A.bounds, A.rec, A.tileCounts, A.tileMasks, \
                        A.blockSums, A.sincosTable)
     switch (deg) {
         case 0: GSM_LAUNCH_PROJ(0); break;
@@ -830,7 +842,7 @@ void launch_records_in(const void* records, const ProjectArgs& a, const DeviceAr
     const uint32_t blocks = (a.count + kProjectBlock - 1) / kProjectBlock;
     if (blocks == 0) return;
     hipLaunchKernelGGL(k_records_in, dim3(blocks), dim3(kProjectBlock), 0, s, (const SplatRecord*)records, a,
-                       A.renderData, A.bounds, A.recA, A.recB, A.tileCounts, A.tileMasks, A.blockSums,
+                       A.renderData, A.bounds, A.rec, A.tileCounts, A.tileMasks, A.blockSums,
                        A.sincosTable, devCount);
 }
 
@@ -848,7 +860,7 @@ void launch_scatter(const ProjectArgs& a, const DeviceArena& A, hipStream_t s) {
     const uint32_t blocks = (a.count + kProjectBlock - 1) / kProjectBlock;
     if (blocks == 0) return;
     hipLaunchKernelGGL(k_scatter, dim3(blocks), dim3(kProjectBlock), 0, s, a, A.renderData, A.bounds,
-                       A.tileCounts, A.tileMasks, A.blockSums, A.keys[0], A.vals[0], A.sincosTable, A.recA);
+                       A.tileCounts, A.tileMasks, A.blockSums, A.keys[0], A.vals[0], A.sincosTable, A.rec);
 }
 
 void launch_headers(const uint32_t* sortedKeys, const FrameGeometry& g, const DeviceArena& A,

@@ -107,8 +107,7 @@ gsm_status GlobalRenderer::create(const gsm_renderer_config& cfg, int hipDevice,
     } while (0)
     GSM_ALLOC(A.renderData, G * sizeof(GaussianRenderData));
     GSM_ALLOC(A.bounds, G * sizeof(short4));
-    GSM_ALLOC(A.recA, G * sizeof(BlendRecordA));
-    GSM_ALLOC(A.recB, G * sizeof(uint32_t));
+    GSM_ALLOC(A.rec, G * sizeof(BlendRecord));
     GSM_ALLOC(A.tileCounts, G * sizeof(uint32_t));
     GSM_ALLOC(A.tileMasks, G * sizeof(uint32_t));
     GSM_ALLOC(A.blockSums, (nb + 1) * sizeof(uint32_t));

@@ -105,6 +105,16 @@ static_assert(sizeof(RenderParams) == 32, "RenderParams must be 32 B");
 struct BlendRecordA {
     uint32_t x, y, z, w;
 };
+// The blend reads a record as one 16-B and one 4-B load of the same 32-B slot: one 64-B memory
+// segment per gathered entry instead of one per array (tools/exp/fetch_calib.hip: a gather costs a
+// 64-B segment whatever its width).
+struct BlendRecord {
+    BlendRecordA a;
+    uint32_t b;
+    float bandX, bandHalfWidth;  // the half-tile skip band (k_project / k_records_in -> k_scatter)
+    uint32_t pad;
+};
+static_assert(sizeof(BlendRecord) == 32, "BlendRecord is one 32-B slot");
 
 // BridgingTypes.h:250-276 -- 32 B projected splat of the DepthFirst stereo path: per eye fp16
 // mean, conic (cxx, cyy, 2*cxy) and depth; shared u8 colour/opacity and fp16 centre depth.

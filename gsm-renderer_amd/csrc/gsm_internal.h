@@ -15,6 +15,8 @@ struct ProjectArgs {
     uint32_t rowBegin, rowEnd;  // slab of tile rows; full frame = [0, tilesY)
     uint32_t count;
     uint32_t maxAssignments;
+    uint32_t keepRenderData;  // write GaussianRenderData of every visible gaussian (debug readback);
+                              // otherwise only where the scatter needs it (rects over kMaskTiles tiles)
     // per-frame constants of projectCovariance2D / stabilizeCovariance2D / computeDepthFactor,
     // evaluated once on the host with the same IEEE fp32 operations the kernels would repeat
     // per gaussian (GaussianShared.h:326-375, 655-714, 275-278)

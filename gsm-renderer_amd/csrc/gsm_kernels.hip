@@ -248,7 +248,10 @@ __global__ __launch_bounds__(kProjectBlock) void k_project(
         const ProjOut o = project_gaussian<HALF, DEG>(world, harm, gid, P, sincos, div255);
         outBounds[gid] = o.bounds;
         if (o.vis) {
-            *(uint4*)(outRD + gid) = o.rd;
+            // GaussianRenderData: the frame itself only reads it for rects the scatter re-tests
+            const int ry0 = max((int)o.bounds.z, (int)P.rowBegin), ry1 = min((int)o.bounds.w, (int)P.rowEnd - 1);
+            if (P.keepRenderData || (ry1 - ry0 + 1) * ((int)o.bounds.y - (int)o.bounds.x + 1) > kMaskTiles)
+                *(uint4*)(outRD + gid) = o.rd;
             uint32_t mask;
             ntiles = count_tiles(o, (int)P.rowBegin, (int)P.rowEnd, &mask);  // rows limited to the slab
             masks[gid] = mask;
@@ -394,7 +397,9 @@ __global__ __launch_bounds__(kProjectBlock) void k_records_in(
     if (gid >= n && gid < P.count) counts[gid] = 0;
     if (gid < n) {
         const SplatRecord r = in[gid];
-        *(uint4*)(outRD + gid) = r.rd;
+        const int ry0 = max((int)r.bounds.z, (int)P.rowBegin), ry1 = min((int)r.bounds.w, (int)P.rowEnd - 1);
+        if (P.keepRenderData || (ry1 - ry0 + 1) * ((int)r.bounds.y - (int)r.bounds.x + 1) > kMaskTiles)
+            *(uint4*)(outRD + gid) = r.rd;
         outBounds[gid] = r.bounds;
         uint4* rp = (uint4*)(outRec + gid);
         rp[0] = make_uint4(r.ra.x, r.ra.y, r.ra.z, r.ra.w);

@@ -356,6 +356,10 @@ gsm_status GlobalRenderer::runFrame(hipStream_t s, const ProjectArgs& a, uint32_
     const bool blendOnly = !prof && (profiling_ & 8) != 0 && (period <= 1 || (sampleFrame_++ % period) == 0);
     const bool keep = (profiling_ & 2) != 0;
     const uint32_t nb = (a.count + kProjectBlock - 1) / kProjectBlock;
+    // GaussianRenderData for readback only when profiling (bits 0, 1), gsm_debug.h
+    ProjectArgs fa = a;
+    fa.keepRenderData = (profiling_ & 3) ? 1u : 0u;
+    keptRenderData_ = fa.keepRenderData != 0;
     lastCount_ = a.count;
     lastWidth_ = width;
     lastHeight_ = height;
@@ -387,7 +391,7 @@ gsm_status GlobalRenderer::runFrame(hipStream_t s, const ProjectArgs& a, uint32_
 
     hipEvent_t* ev = (prof || blendOnly) ? frameEvents(profFrames_) : nullptr;
     if (prof) hipEventRecord(ev[0], s);
-    front(a);
+    front(fa);
     if (prof) hipEventRecord(ev[1], s);
     launch_scan_blocks(nb, a, arena_, s);
     if (prof) hipEventRecord(ev[2], s);
@@ -515,7 +519,11 @@ gsm_status GlobalRenderer::debugCopy(int which, void* dst, size_t bytes, size_t*
     size_t full = 0;
     std::vector<short4> tmpBounds;
     switch (which) {
-        case GSM_BUF_RENDER_DATA: src = arena_.renderData; full = n * 16; break;
+        case GSM_BUF_RENDER_DATA:
+            if (!keptRenderData_) return GSM_ERR_MISSING_REQUIRED_BUFFER;  // frame not profiled (gsm_debug.h)
+            src = arena_.renderData;
+            full = n * 16;
+            break;
         case GSM_BUF_BOUNDS: full = n * 16; break;
         case GSM_BUF_TILE_COUNTS: src = arena_.tileCounts; full = n * 4; break;
         case GSM_BUF_KEYS: src = unsortedKeys_; full = tot * 4; break;

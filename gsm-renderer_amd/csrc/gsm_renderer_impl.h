@@ -94,6 +94,7 @@ class GlobalRenderer {
     uint32_t sampleFrame_ = 0;  // frames since setProfiling (blend-event sampling)
     hipEvent_t* frameEvents(uint32_t frame) { return &events_[(frame % kEventRing) * (GSM_STAGE_COUNT + 1)]; }
     int profiling_ = 0;
+    bool keptRenderData_ = false;  // the last frame wrote GaussianRenderData for readback
     bool haveTimes_ = false;
     uint32_t lastCount_ = 0, lastWidth_ = 0, lastHeight_ = 0;
     const uint32_t* sortedKeys_ = nullptr;

@@ -29,7 +29,9 @@ typedef struct {
 
 /* Buffers that can be copied back (reference resource named in brackets). */
 typedef enum {
-    GSM_BUF_RENDER_DATA = 0,   /* GaussianRenderData[count], 16 B each [interleavedGaussians] */
+    GSM_BUF_RENDER_DATA = 0,   /* GaussianRenderData[count], 16 B each [interleavedGaussians]; kept only
+                                  by frames rendered with profiling bit 0 or 1 set (else
+                                  GSM_ERR_MISSING_REQUIRED_BUFFER): the blend reads its own records */
     GSM_BUF_BOUNDS = 1,        /* int32[count][4] minTX,maxTX,minTY,maxTY [boundsCache] */
     GSM_BUF_TILE_COUNTS = 2,   /* uint32[count] tiles per gaussian [coverageBuffer] */
     GSM_BUF_KEYS = 3,          /* uint32[total] unsorted sort keys [sortKeys before sort] */

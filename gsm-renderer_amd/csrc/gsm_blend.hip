@@ -73,8 +73,7 @@ constexpr bool kBlendU4 = false;  // 4-entry groups at P = 2 (measured: no gain)
 constexpr bool kLdsRecords = true;
 template <int NT, int P, bool COMPACT = false>
 __global__ __launch_bounds__(NT) void k_blend_px(
-    const uint32_t* __restrict__ tileStart, const uint32_t* __restrict__ sortedVals,
-    const BlendRecord* __restrict__ rec,
+    const uint32_t* __restrict__ tileStart, const BlendRecord* __restrict__ rec,
     const uint16_t* __restrict__ expTable, uint32_t* __restrict__ queue, uint32_t tileBegin,
     uint32_t numTiles, uint32_t tilesX, uint32_t W, uint32_t H, uint8_t* __restrict__ color,
     size_t colorPitch, uint8_t* __restrict__ depth, size_t depthPitch, int flags,
@@ -696,7 +695,7 @@ void launch_unit_order_costs(const uint16_t* cost, uint32_t* order, uint32_t num
 // Measured schedule choices: units longest-first by last frame's walk (costOrder;
 // 1080p 8 waves 293 -> 248 us, 4K 16 waves 703 -> 660), the longest on one top-priority wave per
 // SIMD (flags bit 2), later units' priority rising with the age of their walk (flags bit 1).
-void launch_blend(const uint32_t* sortedVals, const FrameGeometry& g, const DeviceArena& A, void* color,
+void launch_blend(const FrameGeometry& g, const DeviceArena& A, void* color,
                   size_t colorPitch, void* depth, size_t depthPitch, int numCUs, bool costOrder, int colorFormat,
                   hipStream_t s, int wavesOverride) {
     const uint32_t t0 = g.rowBegin * g.tilesX, t1 = g.rowEnd * g.tilesX;
@@ -715,7 +714,7 @@ void launch_blend(const uint32_t* sortedVals, const FrameGeometry& g, const Devi
     if (grid > (uint32_t)numCUs) grid = (uint32_t)numCUs;
     const uint32_t* order = costOrder ? A.unitOrder : nullptr;
 #define GSM_LAUNCH_BLEND(NTH, PP, CMP)                                                                       \
-    hipLaunchKernelGGL((k_blend_px<NTH, PP, CMP>), dim3(grid), dim3(NTH), 0, s, A.tileStart, sortedVals, A.rec, \
+    hipLaunchKernelGGL((k_blend_px<NTH, PP, CMP>), dim3(grid), dim3(NTH), 0, s, A.tileStart, A.rec, \
                        A.expTable, A.tileQueue, t0, numTiles, g.tilesX, g.width, g.height,          \
                        (uint8_t*)color, colorPitch, (uint8_t*)depth, depthPitch, flags, order, A.unitCost,  \
                        A.blendTrace, A.halfVals[0], A.halfVals[1], A.halfCount, g.tileCount)

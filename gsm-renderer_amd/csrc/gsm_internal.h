@@ -106,7 +106,10 @@ constexpr float kBlendZeroP = 34.65625f;
 
 constexpr int kProjectBlock = 256;
 constexpr int kRadixBlock = 256;
-constexpr int kRadixItems = 16;  // keys per thread per chunk (4096-key chunks)
+#ifndef GSM_RADIX_ITEMS
+#define GSM_RADIX_ITEMS 16
+#endif
+constexpr int kRadixItems = GSM_RADIX_ITEMS;  // keys per thread per chunk (4096-key chunks)
 constexpr int kRadixChunk = kRadixBlock * kRadixItems;
 
 // project + cull + SH + tile count + per-block count sums (GlobalShaders.metal:19-123, 563-616)
@@ -144,7 +147,7 @@ void launch_half_lists(const uint32_t* sortedVals, uint32_t tileBegin, uint32_t 
 void launch_headers(const uint32_t* sortedKeys, const FrameGeometry& geo, const DeviceArena& A,
                     hipStream_t stream);
 // front-to-back fp16 blend + clear (GlobalShaders.metal:140-154, 1030-1187)
-void launch_blend(const uint32_t* sortedVals, const FrameGeometry& geo, const DeviceArena& A,
+void launch_blend(const FrameGeometry& geo, const DeviceArena& A,
                   void* color, size_t colorPitch, void* depth, size_t depthPitch, int numCUs,
                   bool costOrder, int colorFormat, hipStream_t stream, int waves = 0);
 // orders the blend units by the walk lengths the previous frame measured (longest first), so
@@ -171,9 +174,11 @@ uint32_t radix_grid_for_capacity(uint32_t capacity);
 // bytes of the sort workspace (`hist` argument above) for a capacity; zero it once at allocation
 size_t radix_workspace_bytes(uint32_t capacity);
 // stable per-tile sort by the 16-bit depth key of runs already grouped by tile (one workgroup per
-// tile), which also writes the blend's half-tile lists (as launch_half_lists)
+// tile), which writes the blend's half-tile lists (as launch_half_lists) and, when `full`, the sorted
+// keys and values (keysOut / valsOut; the reference's sorted arrays, read back by captured frames)
 void tile_depth_sort(uint32_t* keysIn, uint32_t* valsIn, uint32_t* keysOut, uint32_t* valsOut,
                      const uint32_t* tileStart, uint32_t tileBegin, uint32_t numTiles, hipStream_t stream,
-                     bool ballot, uint32_t* half0, uint32_t* half1, uint32_t* halfCount, uint32_t tileCount);
+                     bool ballot, uint32_t* half0, uint32_t* half1, uint32_t* halfCount, uint32_t tileCount,
+                     bool full, int numCUs);
 
 }  // namespace gsm

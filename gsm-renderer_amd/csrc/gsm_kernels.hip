@@ -233,6 +233,12 @@ __device__ __forceinline__ float2 band_of(const BlendRecordA& ra, short4 r, int 
     return make_float2(0.0f, -1.0f);
 }
 
+// The tile tests (count_tiles' loop) are shared out over the block: every (gaussian, tile of its
+// rect) candidate of the block's 256 gaussians goes to one thread, consecutive candidates to
+// consecutive threads (owner by binary search over the block's exclusive candidate offsets), and
+// the answers meet in LDS (mask bits for rects of <= 32 tiles, a counter beyond).  A thread no
+// longer walks its own rect while the rest of its wave waits, so one large rect costs its wave
+// nothing extra.  Candidate k of a gaussian is bit k of count_tiles' mask (ty-major, tx-minor).
 template <bool HALF, int DEG>
 __global__ __launch_bounds__(kProjectBlock) void k_project(
     const void* __restrict__ world, const void* __restrict__ harm, ProjectArgs P,
@@ -241,27 +247,82 @@ __global__ __launch_bounds__(kProjectBlock) void k_project(
     uint32_t* __restrict__ masks, uint32_t* __restrict__ blockSums, const float2* __restrict__ sincos) {
     __shared__ uint32_t lds[kProjectBlock / 64];
     __shared__ uint16_t div255[256];
+    __shared__ float4 sEll[kProjectBlock];   // cmx, cmy, conic A, conic B
+    __shared__ float2 sEll2[kProjectBlock];  // conic C, level w
+    __shared__ uint32_t sOff[kProjectBlock];  // exclusive candidate offsets
+    __shared__ uint32_t sRect[kProjectBlock]; // x0 | rw << 16
+    __shared__ int sTy0[kProjectBlock];
+    __shared__ uint32_t sMask[kProjectBlock];
+    __shared__ uint32_t sMore[kProjectBlock];  // hits among candidates >= 32 (large rects)
     fill_div255(div255);
-    const uint32_t gid = blockIdx.x * kProjectBlock + threadIdx.x;
-    uint32_t ntiles = 0;
+    const uint32_t tid = threadIdx.x;
+    const uint32_t gid = blockIdx.x * kProjectBlock + tid;
+    ProjOut o;
+    o.vis = false;
+    o.countable = false;
+    o.bounds = make_short4(0, -1, 0, -1);
+    uint32_t area = 0;
+    int ty0 = 0;
     if (gid < P.count) {
-        const ProjOut o = project_gaussian<HALF, DEG>(world, harm, gid, P, sincos, div255);
+        o = project_gaussian<HALF, DEG>(world, harm, gid, P, sincos, div255);
         outBounds[gid] = o.bounds;
         if (o.vis) {
             // GaussianRenderData: the frame itself only reads it for rects the scatter re-tests
             const int ry0 = max((int)o.bounds.z, (int)P.rowBegin), ry1 = min((int)o.bounds.w, (int)P.rowEnd - 1);
             if (P.keepRenderData || (ry1 - ry0 + 1) * ((int)o.bounds.y - (int)o.bounds.x + 1) > kMaskTiles)
                 *(uint4*)(outRD + gid) = o.rd;
-            uint32_t mask;
-            ntiles = count_tiles(o, (int)P.rowBegin, (int)P.rowEnd, &mask);  // rows limited to the slab
-            masks[gid] = mask;
-            const float2 band = ntiles ? band_of(o.ra, o.bounds, (int)P.rowBegin, (int)P.rowEnd) : make_float2(0.f, -1.f);
-            uint4* rp = (uint4*)(outRec + gid);
-            rp[0] = make_uint4(o.ra.x, o.ra.y, o.ra.z, o.ra.w);
-            rp[1] = make_uint4(o.rb, __float_as_uint(band.x), __float_as_uint(band.y), 0u);
+            if (o.countable && ry1 >= ry0) {  // rows limited to the slab
+                area = (uint32_t)((ry1 - ry0 + 1) * ((int)o.bounds.y - (int)o.bounds.x + 1));
+                ty0 = ry0;
+            }
         }
-        counts[gid] = ntiles;
     }
+    sEll[tid] = make_float4(o.cmx, o.cmy, o.k.A, o.k.B);
+    sEll2[tid] = make_float2(o.k.C, o.w);
+    sRect[tid] = ((uint32_t)(int)o.bounds.x & 0xFFFFu) | ((uint32_t)((int)o.bounds.y - (int)o.bounds.x + 1) << 16);
+    sTy0[tid] = ty0;
+    sMask[tid] = 0;
+    sMore[tid] = 0;
+    uint32_t total;
+    sOff[tid] = block_exclusive_scan<kProjectBlock>(area, lds, &total);  // (its barriers publish the LDS above)
+    __syncthreads();
+    for (uint32_t c = tid; c < total; c += kProjectBlock) {
+        uint32_t lo = 0, hi = kProjectBlock - 1;  // owner: the largest g with sOff[g] <= c
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi + 1) >> 1;
+            if (sOff[mid] <= c) lo = mid;
+            else hi = mid - 1;
+        }
+        const uint32_t k = c - sOff[lo];
+        const uint32_t rect = sRect[lo], rw = rect >> 16;
+        // k / rw from the hardware reciprocal (within one of the quotient), then corrected exactly
+        uint32_t row = (uint32_t)((float)k * __builtin_amdgcn_rcpf((float)rw));
+        if (row * rw > k) row--;
+        else if ((row + 1u) * rw <= k) row++;
+        const int ty = sTy0[lo] + (int)row, tx = (int)(rect & 0xFFFFu) + (int)(k - row * rw);
+        const float4 e = sEll[lo];
+        const float2 e2 = sEll2[lo];
+        Conic kk;
+        kk.A = e.z;
+        kk.B = e.w;
+        kk.C = e2.x;
+        if (intersects_tile(tx, ty, e.x, e.y, kk, e2.y)) {
+            if (k < (uint32_t)kMaskTiles) atomicOr(&sMask[lo], 1u << k);
+            else atomicAdd(&sMore[lo], 1u);
+        }
+    }
+    __syncthreads();
+    uint32_t ntiles = 0;
+    if (gid < P.count && o.vis) {
+        const uint32_t mask = sMask[tid];
+        ntiles = (uint32_t)__builtin_popcount(mask) + sMore[tid];
+        masks[gid] = mask;
+        const float2 band = ntiles ? band_of(o.ra, o.bounds, (int)P.rowBegin, (int)P.rowEnd) : make_float2(0.f, -1.f);
+        uint4* rp = (uint4*)(outRec + gid);
+        rp[0] = make_uint4(o.ra.x, o.ra.y, o.ra.z, o.ra.w);
+        rp[1] = make_uint4(o.rb, __float_as_uint(band.x), __float_as_uint(band.y), 0u);
+    }
+    if (gid < P.count) counts[gid] = ntiles;
     uint32_t s = block_reduce_add<kProjectBlock>(ntiles, lds);
     if (threadIdx.x == 0) blockSums[blockIdx.x] = s;
 }

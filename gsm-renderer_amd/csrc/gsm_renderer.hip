@@ -355,10 +355,13 @@ gsm_status GlobalRenderer::runFrame(hipStream_t s, const ProjectArgs& a, uint32_
     const uint32_t period = ((uint32_t)profiling_ >> 8) & 0xFFu;
     const bool blendOnly = !prof && (profiling_ & 8) != 0 && (period <= 1 || (sampleFrame_++ % period) == 0);
     const bool keep = (profiling_ & 2) != 0;
+    // captured frame: the reference's intermediates (render data, sorted keys / values) are kept
+    // for readback; the product path writes neither (the blend reads its records and half lists)
+    const bool capture = (profiling_ & (2 | 16)) != 0;
     const uint32_t nb = (a.count + kProjectBlock - 1) / kProjectBlock;
     // GaussianRenderData for readback only when profiling (bits 0, 1), gsm_debug.h
     ProjectArgs fa = a;
-    fa.keepRenderData = (profiling_ & 3) ? 1u : 0u;
+    fa.keepRenderData = capture ? 1u : 0u;
     keptRenderData_ = fa.keepRenderData != 0;
     lastCount_ = a.count;
     lastWidth_ = width;
@@ -426,9 +429,9 @@ gsm_status GlobalRenderer::runFrame(hipStream_t s, const ProjectArgs& a, uint32_
         launch_headers(kb[res], g, arena_, s);
         tile_depth_sort(kb[res], vb[res], kb[res ^ 1], vb[res ^ 1], arena_.tileStart, rowBegin_ * tilesX_,
                         (rowEnd_ - rowBegin_) * tilesX_, s, ballot, arena_.halfVals[0], arena_.halfVals[1],
-                        arena_.halfCount, tileCount_);
-        sortedKeys_ = kb[res ^ 1];
-        sortedVals_ = vb[res ^ 1];
+                        arena_.halfCount, tileCount_, capture, numCUs_);
+        sortedKeys_ = capture ? kb[res ^ 1] : nullptr;
+        sortedVals_ = capture ? vb[res ^ 1] : nullptr;
     } else {
         const int res = radix_sort_pairs(kb, vb, &arena_.header->totalAssignments, maxAssignments_, 0,
                                          sortPassCount(), arena_.radixHist, arena_.radixBinTotals, s, ballot);
@@ -446,7 +449,7 @@ gsm_status GlobalRenderer::runFrame(hipStream_t s, const ProjectArgs& a, uint32_
     arena_.blendTrace = (profiling_ & 4) ? traceBuf_ : nullptr;
     if (costOrder) hipStreamWaitEvent(s, evOrder_, 0);
     if (prof || blendOnly) hipEventRecord(ev[5], s);
-    launch_blend(sortedVals_, g, arena_, color, colorPitch, depth, depthPitch, numCUs_, costOrder,
+    launch_blend(g, arena_, color, colorPitch, depth, depthPitch, numCUs_, costOrder,
                  (int)config_.color_format, s, tuning_.blendWaves);
     if (prof || blendOnly) hipEventRecord(ev[6], s);
     if (prof || blendOnly) profFrames_++;
@@ -528,8 +531,16 @@ gsm_status GlobalRenderer::debugCopy(int which, void* dst, size_t bytes, size_t*
         case GSM_BUF_TILE_COUNTS: src = arena_.tileCounts; full = n * 4; break;
         case GSM_BUF_KEYS: src = unsortedKeys_; full = tot * 4; break;
         case GSM_BUF_VALUES: src = unsortedVals_; full = tot * 4; break;
-        case GSM_BUF_SORTED_KEYS: src = sortedKeys_; full = tot * 4; break;
-        case GSM_BUF_SORTED_VALUES: src = sortedVals_; full = tot * 4; break;
+        case GSM_BUF_SORTED_KEYS:  // kept by captured frames only (gsm_debug.h)
+            if (!sortedKeys_) return GSM_ERR_MISSING_REQUIRED_BUFFER;
+            src = sortedKeys_;
+            full = tot * 4;
+            break;
+        case GSM_BUF_SORTED_VALUES:
+            if (!sortedVals_) return GSM_ERR_MISSING_REQUIRED_BUFFER;
+            src = sortedVals_;
+            full = tot * 4;
+            break;
         case GSM_BUF_HEADERS: full = (size_t)tileCount_ * 8; break;
         case GSM_BUF_EXP_TABLE: src = arena_.expTable; full = 65536 * 2; break;
         case GSM_BUF_BLEND_TRACE: src = (profiling_ & 4) ? traceBuf_ : nullptr; full = (size_t)tileCount_ * 4 * 4 * 8; break;

@@ -12,6 +12,7 @@
 // every block owns a contiguous range, so the sort is stable like the reference's.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
@@ -478,35 +479,43 @@ __device__ __forceinline__ void ts_half_row(uint32_t v, bool valid, uint32_t (*t
     __syncthreads();  // tot is rewritten by the next row
 }
 
-template <bool BALLOT>
+// One workgroup per tile (a persistent variant that prefetched the next tile's run was slower:
+// the sort is bound by LDS round trips and barriers, so resident workgroups matter more than
+// memory latency).  FULL: also write the sorted run (keys and values) -- the reference's sorted
+// arrays, read back by captured frames only; the blend walks the half-tile lists alone.
+template <bool BALLOT, bool FULL>
 __global__ __launch_bounds__(kTsThreads) void k_tile_sort(
     uint32_t* __restrict__ keysIn, uint32_t* __restrict__ valsIn, uint32_t* __restrict__ keysOut,
     uint32_t* __restrict__ valsOut, const uint32_t* __restrict__ tileStart, uint32_t tileBegin,
     uint32_t* __restrict__ half0, uint32_t* __restrict__ half1, uint32_t* __restrict__ halfCount,
     uint32_t tileCount) {
     __shared__ __attribute__((aligned(16))) uint32_t buf[kTsCap];
+    __shared__ __attribute__((aligned(16))) uint32_t vbuf[kTsCap];  // the run's values in input order
     __shared__ __attribute__((aligned(16))) uint32_t wcnt[4][256];
     __shared__ uint32_t part[4];
     __shared__ uint32_t tot[2][kTsThreads / 64];
+    __shared__ uint32_t rowTot[2][kTsItems][kTsThreads / 64];
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
     const uint32_t t = tileBegin + blockIdx.x;
     const uint32_t start = tileStart[t];
     const uint32_t n = tileStart[t + 1] - start;
-    uint32_t base0 = 0, base1 = 0;
     if (n == 0) {  // uniform: the whole workgroup leaves
         if (tid == 0) halfCount[t] = halfCount[tileCount + t] = 0;
         return;
     }
     if (n > kTsCap) {  // rare: the same two passes streamed through global memory
+        uint32_t base0 = 0, base1 = 0;
         ts_pass_global<BALLOT>(keysIn + start, valsIn + start, keysOut + start, valsOut + start, n, 0, wcnt, part, buf);
         ts_pass_global<BALLOT>(keysOut + start, valsOut + start, keysIn + start, valsIn + start, n, 8, wcnt, part, buf);
         for (uint32_t b = 0; b < n; b += kTsThreads) {
             const uint32_t i = b + tid;
             uint32_t v = 0;
             if (i < n) {
-                keysOut[start + i] = keysIn[start + i];
                 v = valsIn[start + i];
-                valsOut[start + i] = v;
+                if constexpr (FULL) {
+                    keysOut[start + i] = keysIn[start + i];
+                    valsOut[start + i] = v;
+                }
             }
             ts_half_row(v, i < n, tot, base0, base1, half0 + start, half1 + start);
         }
@@ -521,11 +530,19 @@ __global__ __launch_bounds__(kTsThreads) void k_tile_sort(
     const uint32_t E = (n + kTsThreads - 1) / kTsThreads;  // items per thread
     const uint32_t seg = wave * 64u * E;                    // this wave's segment of the run
     uint32_t x[kTsItems], pos[kTsItems];
-    // all of the run's keys in flight at once; word = depth << 16 | position in the run
+    // all of the run's keys and values in flight at once (one memory latency per tile); word =
+    // depth << 16 | position in the run; the values wait in LDS for the sorted positions
 #pragma unroll
     for (uint32_t j = 0; j < kTsItems; ++j) {
         const uint32_t i = seg + j * 64u + lane;
-        x[j] = (j < E && i < n) ? ((kin[i] & 0xFFFFu) << 16) | i : 0u;
+        const bool ok = j < E && i < n;
+        x[j] = ok ? ((kin[i] & 0xFFFFu) << 16) | i : 0u;
+        pos[j] = ok ? vin[i] : 0u;
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < kTsItems; ++j) {
+        const uint32_t i = seg + j * 64u + lane;
+        if (j < E && i < n) vbuf[i] = pos[j];
     }
 #pragma unroll
     for (uint32_t w = 0; w < 4; ++w) wcnt[w][tid] = 0;
@@ -542,8 +559,9 @@ __global__ __launch_bounds__(kTsThreads) void k_tile_sort(
     for (uint32_t w = 0; w < 4; ++w) wcnt[w][tid] = 0;
     __syncthreads();
     ts_rank_pass<BALLOT>(x, pos, E, seg, n, 24, wcnt, part);  // high depth byte
-    // the sorted run staged in LDS by position, then written in position order: coalesced key and
-    // value stores, and the half-tile lists compacted row by row
+    // the sorted run staged in LDS by position, then read in position order (row j = positions
+    // j * 256 + tid): coalesced key and value stores when FULL, and the half-tile lists compacted
+    // with one ballot per row and half and a single barrier for all rows
 #pragma unroll
     for (uint32_t j = 0; j < kTsItems; ++j)
         if (j < E && seg + j * 64u + lane < n) buf[pos[j]] = x[j];
@@ -551,16 +569,49 @@ __global__ __launch_bounds__(kTsThreads) void k_tile_sort(
     uint32_t* kout = keysOut + start;
     uint32_t* vout = valsOut + start;
     const uint32_t tileBits = t << 16;
-    for (uint32_t j = 0; j < E; ++j) {
+    const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    uint32_t v[kTsItems], r0[kTsItems], r1[kTsItems];  // value, rank among the row's kept entries
+#pragma unroll
+    for (uint32_t j = 0; j < kTsItems; ++j) {
+        if (j >= E) break;
         const uint32_t p = j * kTsThreads + tid;
-        uint32_t v = 0;
+        v[j] = 0;
         if (p < n) {
             const uint32_t w = buf[p];
-            v = vin[w & 0xFFFFu];
-            kout[p] = tileBits | (w >> 16);
-            vout[p] = v;
+            v[j] = vbuf[w & 0xFFFFu];
+            if constexpr (FULL) {
+                kout[p] = tileBits | (w >> 16);
+                vout[p] = v[j];
+            }
         }
-        ts_half_row(v, p < n, tot, base0, base1, half0 + start, half1 + start);
+        const bool k0 = p < n && !((v[j] >> kHalfSkipShift) & 1u);
+        const bool k1 = p < n && !((v[j] >> (kHalfSkipShift + 1)) & 1u);
+        const uint64_t m0 = __ballot(k0), m1 = __ballot(k1);
+        r0[j] = k0 ? (uint32_t)__popcll(m0 & lt) : 0xFFFFFFFFu;
+        r1[j] = k1 ? (uint32_t)__popcll(m1 & lt) : 0xFFFFFFFFu;
+        if (lane == 0) {
+            rowTot[0][j][wave] = (uint32_t)__popcll(m0);
+            rowTot[1][j][wave] = (uint32_t)__popcll(m1);
+        }
+    }
+    __syncthreads();
+    uint32_t base0 = 0, base1 = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < kTsItems; ++j) {
+        if (j >= E) break;
+        uint32_t o0 = base0, o1 = base1;
+#pragma unroll
+        for (uint32_t w = 0; w < kTsThreads / 64; ++w) {
+            const uint32_t c0 = rowTot[0][j][w], c1 = rowTot[1][j][w];
+            if (w < wave) {
+                o0 += c0;
+                o1 += c1;
+            }
+            base0 += c0;
+            base1 += c1;
+        }
+        if (r0[j] != 0xFFFFFFFFu) half0[start + o0 + r0[j]] = v[j] & kGidMask;
+        if (r1[j] != 0xFFFFFFFFu) half1[start + o1 + r1[j]] = v[j] & kGidMask;
     }
     if (tid == 0) {
         halfCount[t] = base0;
@@ -570,14 +621,21 @@ __global__ __launch_bounds__(kTsThreads) void k_tile_sort(
 
 void tile_depth_sort(uint32_t* keysIn, uint32_t* valsIn, uint32_t* keysOut, uint32_t* valsOut,
                      const uint32_t* tileStart, uint32_t tileBegin, uint32_t numTiles, hipStream_t s,
-                     bool ballot, uint32_t* half0, uint32_t* half1, uint32_t* halfCount, uint32_t tileCount) {
+                     bool ballot, uint32_t* half0, uint32_t* half1, uint32_t* halfCount, uint32_t tileCount,
+                     bool full, int numCUs) {
     if (numTiles == 0) return;
-    if (ballot)
-        hipLaunchKernelGGL(k_tile_sort<true>, dim3(numTiles), dim3(kTsThreads), 0, s, keysIn, valsIn, keysOut,
-                           valsOut, tileStart, tileBegin, half0, half1, halfCount, tileCount);
-    else
-        hipLaunchKernelGGL(k_tile_sort<false>, dim3(numTiles), dim3(kTsThreads), 0, s, keysIn, valsIn, keysOut,
-                           valsOut, tileStart, tileBegin, half0, half1, halfCount, tileCount);
+    (void)numCUs;
+#define GSM_TILE_SORT(B, F)                                                                                  \
+    hipLaunchKernelGGL((k_tile_sort<B, F>), dim3(numTiles), dim3(kTsThreads), 0, s, keysIn, valsIn, keysOut, \
+                       valsOut, tileStart, tileBegin, half0, half1, halfCount, tileCount)
+    if (ballot) {
+        if (full) GSM_TILE_SORT(true, true);
+        else GSM_TILE_SORT(true, false);
+    } else {
+        if (full) GSM_TILE_SORT(false, true);
+        else GSM_TILE_SORT(false, false);
+    }
+#undef GSM_TILE_SORT
 }
 
 // ---------------------------------------------------------------------------

@@ -395,10 +395,14 @@ class GlobalRenderer:
 
     # -- introspection (include/gsm_debug.h) --
     def set_profiling(self, stage_events: bool = True, keep_unsorted: bool = False,
-                      blend_trace: bool = False, blend_events: bool = False, blend_event_period: int = 1):
-        """blend_event_period > 1: with blend_events, bracket the blend on every period-th frame only."""
+                      blend_trace: bool = False, blend_events: bool = False, blend_event_period: int = 1,
+                      capture: bool = False):
+        """blend_event_period > 1: with blend_events, bracket the blend on every period-th frame only.
+        capture (implied by keep_unsorted): keep the render data and the sorted keys / values for
+        copy_buffer (include/gsm_debug.h); the product path writes neither."""
         flags = (1 if stage_events else 0) | (2 if keep_unsorted else 0) | (4 if blend_trace else 0) | \
-            (8 if blend_events else 0) | ((max(1, min(255, int(blend_event_period))) & 0xFF) << 8)
+            (8 if blend_events else 0) | (16 if capture else 0) | \
+            ((max(1, min(255, int(blend_event_period))) & 0xFF) << 8)
         _check(_lib().gsm_global_set_profiling(self._h, flags), "gsm_global_set_profiling")
 
     def stage_times_ms(self) -> dict:

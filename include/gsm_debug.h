@@ -30,14 +30,15 @@ typedef struct {
 /* Buffers that can be copied back (reference resource named in brackets). */
 typedef enum {
     GSM_BUF_RENDER_DATA = 0,   /* GaussianRenderData[count], 16 B each [interleavedGaussians]; kept only
-                                  by frames rendered with profiling bit 0 or 1 set (else
+                                  by captured frames (profiling bit 1 or 4; else
                                   GSM_ERR_MISSING_REQUIRED_BUFFER): the blend reads its own records */
     GSM_BUF_BOUNDS = 1,        /* int32[count][4] minTX,maxTX,minTY,maxTY [boundsCache] */
     GSM_BUF_TILE_COUNTS = 2,   /* uint32[count] tiles per gaussian [coverageBuffer] */
     GSM_BUF_KEYS = 3,          /* uint32[total] unsorted sort keys [sortKeys before sort] */
     GSM_BUF_VALUES = 4,        /* int32[total] unsorted gaussian ids [tileIndices] */
-    GSM_BUF_SORTED_KEYS = 5,   /* uint32[total] [sortKeys after sort] */
-    GSM_BUF_SORTED_VALUES = 6, /* int32[total] [sortedIndices] */
+    GSM_BUF_SORTED_KEYS = 5,   /* uint32[total] [sortKeys after sort]; captured frames only (as
+                                  RENDER_DATA): the blend walks per-half-tile lists instead */
+    GSM_BUF_SORTED_VALUES = 6, /* int32[total] [sortedIndices]; captured frames only */
     GSM_BUF_HEADERS = 7,       /* GaussianHeader[tile_count] {offset,count} [orderedHeaders] */
     GSM_BUF_EXP_TABLE = 8,     /* uint16[65536] blend exp table indexed by fp16 quad-form bits */
     GSM_BUF_BLEND_TRACE = 9    /* uint64[blend units][4] {start, end (100 MHz ticks), count<<32 | entries
@@ -49,7 +50,9 @@ gsm_status gsm_global_debug_counters(gsm_renderer *renderer, gsm_debug_counters 
 gsm_status gsm_global_debug_copy(gsm_renderer *renderer, int which, void *host_dst, size_t bytes,
                                  size_t *needed);
 /* `enable` is a bit set: bit 0 brackets every stage by HIP events on the frame's stream,
- * bit 1 keeps the unsorted keys (GSM_BUF_KEYS/VALUES) for readback, bit 2 records a
+ * bit 1 keeps the unsorted keys (GSM_BUF_KEYS/VALUES) for readback and captures (bit 4),
+ * bit 4 captures the reference's intermediates the product path does not write
+ * (GSM_BUF_RENDER_DATA, GSM_BUF_SORTED_KEYS/VALUES; the frame costs their writes), bit 2 records a
  * per-unit blend trace (GSM_BUF_BLEND_TRACE), bit 3 (without bit 0) brackets only the blend
  * (two events per frame; the other stages then report 0); bits 8-15, with bit 3: a period P > 1
  * brackets the blend on every P-th frame only (the average is over the bracketed frames).

@@ -34,7 +34,7 @@ def gpu_render(gsm, torch, case, renderer=None, color_fill=None, keep=True, dept
         cfg = gsm.RendererConfig(max_gaussians=case["max_gaussians"], max_width=maxw, max_height=maxh,
                                  precision=prec, gaussian_color_space=case.get("color_space", 0))
         renderer = gsm.GlobalRenderer(config=cfg)
-    renderer.set_profiling(stage_events=True, keep_unsorted=keep)
+    renderer.set_profiling(stage_events=True, keep_unsorted=keep, capture=True)
     world = to_dev(torch, case["world"])
     harm = to_dev(torch, case["harm"])
     n = len(case["world"]) if case.get("count") is None else case["count"]

@@ -1,0 +1,19 @@
+#!/bin/bash
+# PMC counters of every kernel of a bench config (CFG, default config 3), one rocprofv3 pass per
+# counter set; per-kernel means into gpurun_out/pmcall/summary.txt.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+cfg=${CFG:-cfg3_5m_sh3_4k_f16}
+OUT=gpurun_out/pmcall
+rm -rf $OUT; mkdir -p $OUT
+CMD="python bench.py --config $cfg --steps 5 --warmup 2 --cpu-baseline 0 --parity 0 --orbit-steps 0"
+i=0
+for set in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE" \
+           "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM" \
+           FETCH_SIZE WRITE_SIZE; do
+  i=$((i+1))
+  timeout -s KILL 120 rocprofv3 --pmc $set --output-format csv -d $OUT/p$i -o p$i -- $CMD > $OUT/p$i.log 2>&1 || { echo "pass $i failed"; tail -5 $OUT/p$i.log; exit 1; }
+done
+python tools/pmc_summary.py $OUT > $OUT/summary.txt
+cat $OUT/summary.txt

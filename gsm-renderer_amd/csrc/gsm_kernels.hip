@@ -254,6 +254,11 @@ __global__ __launch_bounds__(kProjectBlock) void k_project(
     __shared__ int sTy0[kProjectBlock];
     __shared__ uint32_t sMask[kProjectBlock];
     __shared__ uint32_t sMore[kProjectBlock];  // hits among candidates >= 32 (large rects)
+    // the block's first kCandCap candidates: owner << 8 | k for rects of <= kCandRect tiles,
+    // kSearch for the candidates of larger rects (their owner comes from a binary search)
+    constexpr uint32_t kCandCap = 4096, kCandRect = 64;
+    constexpr uint16_t kSearch = 0xFFFFu;
+    __shared__ uint16_t sCand[kCandCap];
     fill_div255(div255);
     const uint32_t tid = threadIdx.x;
     const uint32_t gid = blockIdx.x * kProjectBlock + tid;
@@ -284,16 +289,30 @@ __global__ __launch_bounds__(kProjectBlock) void k_project(
     sMask[tid] = 0;
     sMore[tid] = 0;
     uint32_t total;
-    sOff[tid] = block_exclusive_scan<kProjectBlock>(area, lds, &total);  // (its barriers publish the LDS above)
+    const uint32_t coff = block_exclusive_scan<kProjectBlock>(area, lds, &total);
+    sOff[tid] = coff;
+    const uint32_t nCand = min(total, kCandCap);
+    for (uint32_t i = tid; i < nCand; i += kProjectBlock) sCand[i] = kSearch;
+    __syncthreads();
+    if (area <= kCandRect)
+        for (uint32_t k = 0; k < area && coff + k < kCandCap; ++k) sCand[coff + k] = (uint16_t)((tid << 8) | k);
     __syncthreads();
     for (uint32_t c = tid; c < total; c += kProjectBlock) {
-        uint32_t lo = 0, hi = kProjectBlock - 1;  // owner: the largest g with sOff[g] <= c
-        while (lo < hi) {
-            const uint32_t mid = (lo + hi + 1) >> 1;
-            if (sOff[mid] <= c) lo = mid;
-            else hi = mid - 1;
+        uint32_t lo, k;
+        const uint32_t v = c < kCandCap ? (uint32_t)sCand[c] : (uint32_t)kSearch;
+        if (v != kSearch) {
+            lo = v >> 8;
+            k = v & 0xFFu;
+        } else {
+            lo = 0;
+            uint32_t hi = kProjectBlock - 1;  // owner: the largest g with sOff[g] <= c
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi + 1) >> 1;
+                if (sOff[mid] <= c) lo = mid;
+                else hi = mid - 1;
+            }
+            k = c - sOff[lo];
         }
-        const uint32_t k = c - sOff[lo];
         const uint32_t rect = sRect[lo], rw = rect >> 16;
         // k / rw from the hardware reciprocal (within one of the quotient), then corrected exactly
         uint32_t row = (uint32_t)((float)k * __builtin_amdgcn_rcpf((float)rw));
@@ -587,6 +606,11 @@ __global__ __launch_bounds__(kProjectBlock) void k_scatter(
     __shared__ int sTy0[kProjectBlock];
     __shared__ uint32_t sD[kProjectBlock];     // depth bits of the key
     __shared__ float2 sBand[kProjectBlock];    // skip-flag band of each gaussian: mean x, half width (< 0: none)
+    // the block's first kOwnCap slots: owner << 5 | tile bit of each small-rect slot, kNoOwner for the
+    // slots of large rects (their own thread writes them); later slots take the binary search
+    constexpr uint32_t kOwnCap = 4096;
+    constexpr uint16_t kNoOwner = 0xFFFFu;
+    __shared__ uint16_t sOwn[kOwnCap];
     const uint32_t gid = blockIdx.x * kProjectBlock + threadIdx.x;
     uint32_t c = (gid < P.count) ? counts[gid] : 0u;
     uint32_t total;
@@ -617,21 +641,40 @@ __global__ __launch_bounds__(kProjectBlock) void k_scatter(
     sD[threadIdx.x] = dbits;
     sTy0[threadIdx.x] = ty0;
     sBand[threadIdx.x] = band;
+    const uint32_t nOwn = min(total, kOwnCap);
+    for (uint32_t i = threadIdx.x; i < nOwn; i += kProjectBlock) sOwn[i] = kNoOwner;
+    __syncthreads();
+    {  // each small rect lists its slots (<= 32, one per set bit of its mask, in bit order)
+        uint32_t m = mask;
+        for (uint32_t i = off; m != 0 && i < kOwnCap; ++i) {
+            sOwn[i] = (uint16_t)((threadIdx.x << 5) | (uint32_t)__builtin_ctz(m));
+            m &= m - 1u;
+        }
+    }
     __syncthreads();
     for (uint32_t sl = threadIdx.x; sl < total; sl += kProjectBlock) {
-        // owner: the largest g with sOff[g] <= sl (zero-count gaussians share the next offset)
-        uint32_t lo = 0, hi = kProjectBlock - 1;
-        while (lo < hi) {
-            const uint32_t mid = (lo + hi + 1) >> 1;
-            if (sOff[mid] <= sl) lo = mid;
-            else hi = mid - 1;
+        uint32_t lo, bit;
+        if (sl < kOwnCap) {
+            const uint32_t v = sOwn[sl];
+            if (v == kNoOwner) continue;  // a large rect: its own thread writes it
+            lo = v >> 5;
+            bit = v & 31u;
+        } else {
+            // owner: the largest g with sOff[g] <= sl (zero-count gaussians share the next offset)
+            lo = 0;
+            uint32_t hi = kProjectBlock - 1;
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi + 1) >> 1;
+                if (sOff[mid] <= sl) lo = mid;
+                else hi = mid - 1;
+            }
+            uint32_t m = sMask[lo];
+            if (m == 0) continue;  // a large rect: its own thread writes it
+            for (uint32_t k = sl - sOff[lo]; k > 0; --k) m &= m - 1u;
+            bit = (uint32_t)__builtin_ctz(m);
         }
-        uint32_t m = sMask[lo];
-        if (m == 0) continue;  // a large rect: its own thread writes it
         const uint64_t wp = (uint64_t)base + sl;
         if (wp >= P.maxAssignments) continue;
-        for (uint32_t k = sl - sOff[lo]; k > 0; --k) m &= m - 1u;
-        const uint32_t bit = (uint32_t)__builtin_ctz(m);
         const uint32_t rect = sRect[lo];
         const uint32_t rwo = rect >> 16;
         const int ty = sTy0[lo] + (int)(bit / rwo), tx = (int)(rect & 0xFFFFu) + (int)(bit % rwo);

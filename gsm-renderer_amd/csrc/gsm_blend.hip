@@ -19,6 +19,9 @@ namespace gsm {
 
 typedef _Float16 h1;
 typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+// `color += gColor * w` (GlobalShaders.metal:1137-1145, DepthFirstShaders.metal:1783-1786): one
+// fused multiply-add, a single rounding per channel (the numeric contract; the oracle's hfma)
+__device__ __forceinline__ h2 blend_acc(h2 acc, h2 c, h2 w) { return __builtin_elementwise_fma(c, w, acc); }
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ h2 as_h2(uint32_t u) { return __builtin_bit_cast(h2, u); }
@@ -381,10 +384,10 @@ __global__ __launch_bounds__(NT) void k_blend_px(
                             for (int q = 0; q < P; ++q) {
                                 const h2 w = ac[k][q] * T[q];  // (GlobalShaders.metal:1137-1149)
                                 T[q] = T[q] * om[k][q];
-                                R[q] = R[q] + splat_lo(rgv) * w;
-                                G[q] = G[q] + splat_hi(rgv) * w;
-                                B[q] = B[q] + splat_lo(bdv) * w;
-                                D[q] = D[q] + splat_hi(bdv) * w;
+                                R[q] = blend_acc(R[q], splat_lo(rgv), w);
+                                G[q] = blend_acc(G[q], splat_hi(rgv), w);
+                                B[q] = blend_acc(B[q], splat_lo(bdv), w);
+                                D[q] = blend_acc(D[q], splat_hi(bdv), w);
                             }
                         }
                     }
@@ -531,10 +534,10 @@ __global__ __launch_bounds__(NT) void k_blend_px(
                             const h2 rgv = as_h2(rgc1[k]), bdv = as_h2(bdc1[k]);
                             const h2 w = ac1[k] * T1;  // (GlobalShaders.metal:1137-1149)
                             T1 = T1 * om1[k];
-                            R1 = R1 + splat_lo(rgv) * w;
-                            G1 = G1 + splat_hi(rgv) * w;
-                            B1 = B1 + splat_lo(bdv) * w;
-                            D1 = D1 + splat_hi(bdv) * w;
+                            R1 = blend_acc(R1, splat_lo(rgv), w);
+                            G1 = blend_acc(G1, splat_hi(rgv), w);
+                            B1 = blend_acc(B1, splat_lo(bdv), w);
+                            D1 = blend_acc(D1, splat_hi(bdv), w);
                         }
                     }
                     e += U1;

@@ -389,6 +389,9 @@ __device__ __forceinline__ uint32_t df_u32(h2 v) { return __builtin_bit_cast(uin
 __device__ __forceinline__ h2 df_lo(h2 v) { return h2{v.x, v.x}; }
 __device__ __forceinline__ h2 df_hi(h2 v) { return h2{v.y, v.y}; }
 typedef unsigned short df_u16x2 __attribute__((ext_vector_type(2)));
+// `color += gColor * (a * trans)` (DepthFirstShaders.metal:1783-1786, 1909-1953): one fused
+// multiply-add, a single rounding per channel (the numeric contract; the oracle's hfma)
+__device__ __forceinline__ h2 df_acc(h2 acc, h2 c, h2 w) { return __builtin_elementwise_fma(c, w, acc); }
 
 struct DfEyeState {
     h2 T[2], Cr[2], Cg[2], Cb[2];  // [row]: {x, x + 1}
@@ -438,12 +441,12 @@ __device__ __forceinline__ void df_blend_eye(DfEyeState& st, bool alive, h2 p0, 
     }
     const h2 w0 = a0 * st.T[0], w1 = a1 * st.T[1];
     const h2 r = df_hi(opr), g = df_lo(gb), b = df_hi(gb);
-    st.Cr[0] = st.Cr[0] + r * w0;
-    st.Cr[1] = st.Cr[1] + r * w1;
-    st.Cg[0] = st.Cg[0] + g * w0;
-    st.Cg[1] = st.Cg[1] + g * w1;
-    st.Cb[0] = st.Cb[0] + b * w0;
-    st.Cb[1] = st.Cb[1] + b * w1;
+    st.Cr[0] = df_acc(st.Cr[0], r, w0);
+    st.Cr[1] = df_acc(st.Cr[1], r, w1);
+    st.Cg[0] = df_acc(st.Cg[0], g, w0);
+    st.Cg[1] = df_acc(st.Cg[1], g, w1);
+    st.Cb[0] = df_acc(st.Cb[0], b, w0);
+    st.Cb[1] = df_acc(st.Cb[1], b, w1);
     st.T[0] = st.T[0] * (ONE - a0);
     st.T[1] = st.T[1] * (ONE - a1);
 }
@@ -470,12 +473,12 @@ __device__ __forceinline__ void df_blend_eye_w(DfEyeState& st, bool alive, h2 p0
     }
     const h2 w0 = a0 * st.T[0], w1 = a1 * st.T[1];
     const h2 r = df_lo(df_h2(rg)), g = df_hi(df_h2(rg)), b = df_lo(df_h2(bw));
-    st.Cr[0] = st.Cr[0] + r * w0;
-    st.Cr[1] = st.Cr[1] + r * w1;
-    st.Cg[0] = st.Cg[0] + g * w0;
-    st.Cg[1] = st.Cg[1] + g * w1;
-    st.Cb[0] = st.Cb[0] + b * w0;
-    st.Cb[1] = st.Cb[1] + b * w1;
+    st.Cr[0] = df_acc(st.Cr[0], r, w0);
+    st.Cr[1] = df_acc(st.Cr[1], r, w1);
+    st.Cg[0] = df_acc(st.Cg[0], g, w0);
+    st.Cg[1] = df_acc(st.Cg[1], g, w1);
+    st.Cb[0] = df_acc(st.Cb[0], b, w0);
+    st.Cb[1] = df_acc(st.Cb[1], b, w1);
     st.T[0] = st.T[0] * (ONE - a0);
     st.T[1] = st.T[1] * (ONE - a1);
 }

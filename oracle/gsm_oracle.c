@@ -118,6 +118,38 @@ static inline float H(uint16_t h) { return g_h2f[h]; }
 static inline uint16_t hadd(uint16_t a, uint16_t b) { return og_f2h(H(a) + H(b)); }
 static inline uint16_t hsub(uint16_t a, uint16_t b) { return og_f2h(H(a) - H(b)); }
 static inline uint16_t hmul(uint16_t a, uint16_t b) { return og_f2h(H(a) * H(b)); }
+
+/* next fp16 bit pattern above / below a finite h (signed zeros step to the smallest subnormals) */
+static uint16_t h_next_up(uint16_t h) {
+    if (h == 0x8000u) return 0x0001u;
+    return (h & 0x8000u) ? (uint16_t)(h - 1u) : (uint16_t)(h + 1u);
+}
+static uint16_t h_next_down(uint16_t h) {
+    if (h == 0x0000u) return 0x8001u;
+    return (h & 0x8000u) ? (uint16_t)(h + 1u) : (uint16_t)(h - 1u);
+}
+
+/* fp16 fused multiply-add a*b + c with ONE rounding to nearest even (the GPU's v_pk_fma_f16;
+ * the blend's `C += c * w` accumulations, GlobalShaders.metal:1137-1145).  The
+ * product is exact in double (22 significant bits); s = p + c rounds at most once and TwoSum
+ * gives its exact error e.  Rounding s to fp16 is the correct rounding of p + c unless s lies
+ * exactly on an fp16 midpoint, where the sign of e decides. */
+static uint16_t hfma(uint16_t a, uint16_t b, uint16_t c) {
+    const double p = (double)H(a) * (double)H(b), cc = (double)H(c);
+    const double s = p + cc;
+    const uint16_t h = og_d2h(s);
+    if (!isfinite(s) || (h & 0x7C00u) == 0x7C00u) return h;
+    const double bb = s - p;
+    const double e = (p - (s - bb)) + (cc - bb);
+    const double v = (double)H(h);
+    if (e == 0.0 || v == s) return h;
+    const uint16_t n = s > v ? h_next_up(h) : h_next_down(h);
+    if ((n & 0x7C00u) == 0x7C00u) return h;
+    const double nv = (double)H(n);
+    if (s != 0.5 * (v + nv)) return h;  /* not a midpoint: s and p + c round alike */
+    return (e > 0.0) == (nv > v) ? n : h;
+}
+uint16_t og_hfma(uint16_t a, uint16_t b, uint16_t c) { ensure_init(); return hfma(a, b, c); }
 /* IEEE minNum / maxNum (a NaN operand yields the other operand). */
 static inline uint16_t hmin(uint16_t a, uint16_t b) {
     float fa = H(a), fb = H(b);
@@ -873,10 +905,10 @@ static void blend_tiles(void *vctx, uint32_t lo, uint32_t hi) {
                     if (!any) continue;
                     for (int q = 0; q < 8; ++q) {
                         uint16_t w = hmul(a[q], T[q]);
-                        C[q][0] = hadd(C[q][0], hmul(g->cr, w));
-                        C[q][1] = hadd(C[q][1], hmul(g->cg, w));
-                        C[q][2] = hadd(C[q][2], hmul(g->cb, w));
-                        D[q] = hadd(D[q], hmul(g->dep, w));
+                        C[q][0] = hfma(g->cr, w, C[q][0]);  /* color += gColor * w: fused */
+                        C[q][1] = hfma(g->cg, w, C[q][1]);
+                        C[q][2] = hfma(g->cb, w, C[q][2]);
+                        D[q] = hfma(g->dep, w, D[q]);
                         T[q] = hmul(T[q], hsub(H_ONE, a[q]));
                     }
                 }
@@ -1424,7 +1456,7 @@ static void df_blend_tiles(void *vctx, uint32_t lo, uint32_t hi) {
                         if (!any) continue;
                         for (int q = 0; q < 4; ++q) {
                             uint16_t w = hmul(a[q], T[e][q]);
-                            for (int ch = 0; ch < 3; ++ch) C[e][q][ch] = hadd(C[e][q][ch], hmul(gc[ch], w));
+                            for (int ch = 0; ch < 3; ++ch) C[e][q][ch] = hfma(gc[ch], w, C[e][q][ch]);
                             T[e][q] = hmul(T[e][q], hsub(ONE, a[q]));
                         }
                     }

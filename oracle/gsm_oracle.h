@@ -130,6 +130,8 @@ float og_h2f(uint16_t h);
 uint16_t og_d2h(double d);
 /* Correctly rounded fp16 e^x for every fp16 x (DESIGN.md numeric contract). */
 uint16_t og_exp_h(uint16_t x_bits);
+/* fp16 a*b + c with one rounding to nearest even (the blend's fused `C += c * w`) */
+uint16_t og_hfma(uint16_t a, uint16_t b, uint16_t c);
 /* Deterministic fp32 math (fixed polynomials, see tools/fit_polys.py). */
 float og_atan2f(float y, float x);
 float og_log2f(float x);

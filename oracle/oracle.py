@@ -106,6 +106,8 @@ def lib():
         L.og_d2h.restype = C.c_uint16
         L.og_exp_h.argtypes = [C.c_uint16]
         L.og_exp_h.restype = C.c_uint16
+        L.og_hfma.argtypes = [C.c_uint16, C.c_uint16, C.c_uint16]
+        L.og_hfma.restype = C.c_uint16
         for name in ("og_atan2f",):
             getattr(L, name).argtypes = [C.c_float, C.c_float]
             getattr(L, name).restype = C.c_float

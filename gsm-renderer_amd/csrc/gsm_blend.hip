@@ -682,9 +682,12 @@ uint32_t blend_units_per_tile(uint32_t numTiles, int numCUs) {
 
 static int blend_waves_per_wg(uint32_t numTiles, int numCUs) {
     // 16 waves per CU hide more latency once every wave slot gets >= 6 units (4K: 16200 tiles);
-    // with fewer units per slot the tail dominates and 8 waves finish first (1080p)
+    // with fewer units per slot the tail weighs more: 12 waves from 2 units per slot (1080p: 8160
+    // units, 3213 -> 3268 frames/s; two 1440x1600 views 1046 -> 1086, r02 fused-accumulate blend),
+    // 8 below
     const uint64_t units = (uint64_t)numTiles * blend_units_per_tile(numTiles, numCUs);
-    return units >= 6ull * (uint64_t)numCUs * 16u ? 16 : 8;
+    if (units >= 6ull * (uint64_t)numCUs * 16u) return 16;
+    return units >= 2ull * (uint64_t)numCUs * 12u ? 12 : 8;
 }
 
 void launch_unit_order(uint32_t numUnits, const DeviceArena& A, hipStream_t s) {

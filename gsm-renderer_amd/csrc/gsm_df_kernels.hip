@@ -292,6 +292,11 @@ __global__ __launch_bounds__(kDfBlock) void k_df_expand(const TileAssignmentHead
     __shared__ uint32_t sG[kDfBlock];
     __shared__ short4 sR[kDfBlock];
     __shared__ DfEyeSkip sE[2][kDfBlock];
+    // the block's first kCandCap instances: owner << 8 | local index for rects of <= kCandRect
+    // tiles, kSearch for the instances of larger rects (their owner comes from a binary search)
+    constexpr uint32_t kCandCap = 4096, kCandRect = 64;
+    constexpr uint16_t kSearch = 0xFFFFu;
+    __shared__ uint16_t sCand[kCandCap];
     const uint32_t tid = threadIdx.x;
     const uint32_t i = blockIdx.x * kDfBlock + tid;
     const uint32_t V = visHdr->totalAssignments;
@@ -308,22 +313,40 @@ __global__ __launch_bounds__(kDfBlock) void k_df_expand(const TileAssignmentHead
         sE[0][tid] = df_eye_skip_setup(w0.x, w0.y, w0.z);
         sE[1][tid] = df_eye_skip_setup(w0.w, w1.x, w1.y);
     }
+    const uint32_t nCand = min(total, kCandCap);
+    for (uint32_t j = tid; j < nCand; j += kDfBlock) sCand[j] = kSearch;
     __syncthreads();
     if (total == 0) return;
+    if (c <= kCandRect)
+        for (uint32_t j = 0; j < c && off + j < kCandCap; ++j) sCand[off + j] = (uint16_t)((tid << 8) | j);
+    __syncthreads();
     const uint64_t base = (uint64_t)blockOffsets[blockIdx.x];
     for (uint32_t k = tid; k < total; k += kDfBlock) {
         const uint64_t wp = base + k;
         if (wp >= maxInstances) break;
-        // owner: the last gaussian whose offset is <= k (gaussians without instances share an
-        // offset with the next one, so the last of equal offsets is the one with instances)
-        uint32_t lo = 0, hi = kDfBlock;
-        while (hi - lo > 1) {
-            const uint32_t mid = (lo + hi) >> 1;
-            if (sOff[mid] <= k) lo = mid; else hi = mid;
+        uint32_t lo, local;
+        const uint32_t cv = k < kCandCap ? (uint32_t)sCand[k] : (uint32_t)kSearch;
+        if (cv != kSearch) {
+            lo = cv >> 8;
+            local = cv & 0xFFu;
+        } else {
+            // owner: the last gaussian whose offset is <= k (gaussians without instances share an
+            // offset with the next one, so the last of equal offsets is the one with instances)
+            lo = 0;
+            uint32_t hi = kDfBlock;
+            while (hi - lo > 1) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (sOff[mid] <= k) lo = mid; else hi = mid;
+            }
+            local = k - sOff[lo];
         }
         const short4 r = sR[lo];
-        const uint32_t w = (uint32_t)(r.y - r.x + 1), local = k - sOff[lo];
-        const uint32_t dy = local / w, dx = local - dy * w;
+        const uint32_t w = (uint32_t)(r.y - r.x + 1);
+        // local / w from the hardware reciprocal (within one of the quotient), corrected exactly
+        uint32_t dy = (uint32_t)((float)local * __builtin_amdgcn_rcpf((float)w));
+        if (dy * w > local) dy--;
+        else if ((dy + 1u) * w <= local) dy++;
+        const uint32_t dx = local - dy * w;
         const int tx = r.x + (int)dx, ty = r.z + (int)dy;
         tiles[wp] = (uint32_t)(ty * (int)tilesX + tx) & 0xFFFFu;  // ushort tile id
         const int x0 = tx * (int)kDfTile, y0 = ty * (int)kDfTile;

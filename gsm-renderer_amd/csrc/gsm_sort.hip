@@ -558,7 +558,11 @@ __global__ __launch_bounds__(kTsThreads) void k_tile_sort(
 #pragma unroll
     for (uint32_t w = 0; w < 4; ++w) wcnt[w][tid] = 0;
     __syncthreads();
+#ifdef GSM_TS_HIGH_BALLOT
+    ts_rank_pass<true>(x, pos, E, seg, n, 24, wcnt, part);  // high depth byte
+#else
     ts_rank_pass<BALLOT>(x, pos, E, seg, n, 24, wcnt, part);  // high depth byte
+#endif
     // the sorted run staged in LDS by position, then read in position order (row j = positions
     // j * 256 + tid): coalesced key and value stores when FULL, and the half-tile lists compacted
     // with one ballot per row and half and a single barrier for all rows

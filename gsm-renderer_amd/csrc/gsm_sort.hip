@@ -558,11 +558,9 @@ __global__ __launch_bounds__(kTsThreads) void k_tile_sort(
 #pragma unroll
     for (uint32_t w = 0; w < 4; ++w) wcnt[w][tid] = 0;
     __syncthreads();
-#ifdef GSM_TS_HIGH_BALLOT
-    ts_rank_pass<true>(x, pos, E, seg, n, 24, wcnt, part);  // high depth byte
-#else
-    ts_rank_pass<BALLOT>(x, pos, E, seg, n, 24, wcnt, part);  // high depth byte
-#endif
+    // high depth byte: the atomic ranks stay faster than ballot matches even though a tile's depths
+    // share few high bytes (r02, config 3: 66.1 against 80.7 us with ballot ranks for this pass)
+    ts_rank_pass<BALLOT>(x, pos, E, seg, n, 24, wcnt, part);
     // the sorted run staged in LDS by position, then read in position order (row j = positions
     // j * 256 + tid): coalesced key and value stores when FULL, and the half-tile lists compacted
     // with one ballot per row and half and a single barrier for all rows

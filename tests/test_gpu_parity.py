@@ -246,6 +246,34 @@ def test_null_depth_and_determinism(gsm, cuda, oracle):
     g1["renderer"].close()
 
 
+def test_uncaptured_frame_keeps_only_what_the_blend_reads(gsm, cuda, oracle):
+    """A frame rendered without capture (profiling bit 4 / keep_unsorted) writes neither the render
+    data nor the sorted arrays (include/gsm_debug.h); their readback fails loudly, the image and the
+    header counters still equal the oracle's, and a captured frame on the same renderer brings them back."""
+    case = _synth(30_000, 640, 360, 16, 1, 23)
+    r = oracle_render(oracle, case)
+    g = gpu_render(gsm, cuda, case, keep=False)  # captured: every intermediate
+    assert_frame_equal(g, r)
+    rend = g["renderer"]
+    rend.set_profiling(stage_events=False)
+    w, h = case["width"], case["height"]
+    color = cuda.empty((h, w, 4), dtype=cuda.float16, device="cuda")
+    dep = cuda.empty((h, w), dtype=cuda.float16, device="cuda")
+    inp = gsm.GaussianInput(to_dev(cuda, case["world"]), to_dev(cuda, case["harm"]), len(case["world"]), case["sh"])
+    rend.render(color, dep, inp, gsm.CameraParams.from_dict(case["cam"]), w, h)
+    cuda.cuda.synchronize()
+    assert np.array_equal(color.view(cuda.int16).cpu().numpy().view(np.uint16), r["color"])
+    assert np.array_equal(dep.view(cuda.int16).cpu().numpy().view(np.uint16), r["depth"])
+    assert rend.counters()["total_assignments"] == r["total_assignments"]
+    for buf in (gsm.BufferId.RENDER_DATA, gsm.BufferId.SORTED_KEYS, gsm.BufferId.SORTED_VALUES):
+        with pytest.raises(gsm.RendererError) as e:
+            rend.copy_buffer(buf)
+        assert e.value.status == gsm.Status.MISSING_REQUIRED_BUFFER
+    g2 = gpu_render(gsm, cuda, case, renderer=rend, keep=False)
+    assert_frame_equal(g2, r)
+    rend.close()
+
+
 def test_tile_row_slabs_compose_to_full_frame(gsm, cuda, oracle):
     """Multi-GPU slab partition: rows [b, e) rendered alone equal the full frame there."""
     case = _synth(30_000, 640, 360, 16, 1, 31)

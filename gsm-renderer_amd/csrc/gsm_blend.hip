@@ -586,85 +586,15 @@ __global__ __launch_bounds__(NT) void k_blend_px(
 }
 
 // ---------------------------------------------------------------------------
-// Blend schedule: the units in descending order of the walk each made in the previous frame
-// (longest-processing-time-first list scheduling on the persistent waves), as a stable
-// counting sort into 256 buckets of walk length (bucket width = max walk / 256, so the order
-// is exact to ~1 % of the longest walk; index order, i.e. tile locality, inside a bucket).
-// One workgroup of 1024 threads: histogram, scan, then a stable ranked scatter in chunks of
-// 1024 units (wave ballot match + per-wave bucket counters).
+// Blend schedule (unit_order_block, gsm_device.h) as a kernel of its own: the records path of a
+// multi-GPU slab and the DepthFirst renderer run it before the blend; the single-GPU frame runs
+// the same block inside its projection launch (k_project, one extra workgroup).
 // ---------------------------------------------------------------------------
-constexpr uint32_t kUoBuckets = 256, kUoWaves = 16;
-
-__device__ __forceinline__ uint64_t uo_match8(uint32_t d, bool valid) {
-    uint64_t peers = __ballot(valid);
-#pragma unroll
-    for (int bit = 0; bit < 8; ++bit) {
-        const bool set = (d >> bit) & 1u;
-        const uint64_t m = __ballot(set);
-        peers &= set ? m : ~m;
-    }
-    return peers;
-}
-
 __global__ __launch_bounds__(1024) void k_unit_order(const uint16_t* __restrict__ cost,
                                                      uint32_t* __restrict__ order, uint32_t n) {
-    __shared__ uint32_t wmax[kUoWaves];
     __shared__ uint32_t base[kUoBuckets];
-    __shared__ uint32_t wcnt[kUoWaves][kUoBuckets];
-    const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
-    // pass 1: the longest walk
-    uint32_t m = 0;
-    for (uint32_t i = t; i < n; i += 1024) m = max(m, (uint32_t)cost[i]);
-    for (int off = 32; off > 0; off >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, off));
-    if (lane == 0) wmax[w] = m;
-    if (t < kUoBuckets) base[t] = 0;
-    __syncthreads();
-    uint32_t mx = 0;
-    for (uint32_t k = 0; k < kUoWaves; ++k) mx = max(mx, wmax[k]);
-    const uint32_t den = mx + 1u;
-    auto bucket = [&](uint32_t i) {  // 0 = longest walks
-        return (kUoBuckets - 1u) - min(kUoBuckets - 1u, (uint32_t)cost[i] * kUoBuckets / den);
-    };
-    // pass 2: bucket sizes, then their exclusive scan (bucket-major = descending walk)
-    for (uint32_t i = t; i < n; i += 1024) atomicAdd(&base[bucket(i)], 1u);
-    __syncthreads();
-    if (w == 0) {
-        const uint4 c = *(const uint4*)(base + lane * 4u);
-        const uint32_t local = c.x + c.y + c.z + c.w;
-        uint32_t inc = local;
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t v = __shfl_up(inc, o, 64);
-            if (lane >= (uint32_t)o) inc += v;
-        }
-        const uint32_t e = inc - local;
-        *(uint4*)(base + lane * 4u) = make_uint4(e, e + c.x, e + c.x + c.y, e + c.x + c.y + c.z);
-    }
-    __syncthreads();
-    // pass 3: stable scatter, chunks of 1024 units in index order
-    const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-    for (uint32_t c0 = 0; c0 < n; c0 += 1024) {
-        const uint32_t i = c0 + t;
-        const bool valid = i < n;
-        const uint32_t bk = valid ? bucket(i) : 0u;
-        const uint64_t peers = uo_match8(bk, valid);
-        for (uint32_t k = t; k < kUoWaves * kUoBuckets; k += 1024) (&wcnt[0][0])[k] = 0;
-        __syncthreads();
-        if (valid && (peers & lt) == 0) wcnt[w][bk] = (uint32_t)__popcll(peers);
-        __syncthreads();
-        if (valid) {
-            uint32_t before = base[bk];
-            for (uint32_t k = 0; k < w; ++k) before += wcnt[k][bk];
-            const uint32_t pos = before + (uint32_t)__popcll(peers & lt);
-            if (pos < n) order[pos] = i;
-        }
-        __syncthreads();
-        if (t < kUoBuckets) {
-            uint32_t add = 0;
-            for (uint32_t k = 0; k < kUoWaves; ++k) add += wcnt[k][t];
-            base[t] += add;
-        }
-        __syncthreads();
-    }
+    __shared__ uint32_t wmax[1024 / 64];
+    unit_order_block<1024>(cost, order, n, base, wmax);
 }
 
 

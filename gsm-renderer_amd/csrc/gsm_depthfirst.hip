@@ -49,9 +49,7 @@ class DepthFirstRenderer {
     // last frame
     uint32_t lastCount_ = 0, lastTilesX_ = 0, lastTilesY_ = 0;
     uint64_t schedKey_ = ~0ull;  // geometry the unit costs belong to
-    hipStream_t side_ = nullptr;  // blend-schedule stream
     unsigned long long* statsBuf_ = nullptr;  // blend walk statistics (profiling bit 1)
-    hipEvent_t evFrame_ = nullptr, evOrder_ = nullptr;
     const uint32_t* depthOrder_ = nullptr;
     const uint32_t* instTiles_ = nullptr;
     const uint32_t* instGids_ = nullptr;
@@ -73,11 +71,6 @@ void DepthFirstRenderer::release() {
     for (auto& e : events_)
         if (e) hipEventDestroy(e);
     events_.clear();
-    if (evFrame_) hipEventDestroy(evFrame_);
-    if (evOrder_) hipEventDestroy(evOrder_);
-    if (side_) hipStreamDestroy(side_);
-    evFrame_ = evOrder_ = nullptr;
-    side_ = nullptr;
 }
 
 gsm_status DepthFirstRenderer::alloc(void** p, size_t bytes) {
@@ -239,27 +232,16 @@ gsm_status DepthFirstRenderer::renderStereoSbs(hipStream_t s, const gsm_gaussian
     const bool half = config_.precision == GSM_PRECISION_FLOAT16;
     const uint32_t nb = (a.count + kDfBlock - 1) / kDfBlock;
 
-    // The blend schedule's ordering kernel only needs the previous frame's walk lengths, so it
-    // runs on a side stream beside this frame's projection and sorts (joined before the blend).
+    // The blend schedule only needs the previous frame's walk lengths: one extra workgroup of the
+    // projection launch orders the units while the others project (no side stream, no join).
     const bool costOrder = tuning_.costOrder;
-    if (costOrder && !side_) {
-        if (hipStreamCreateWithFlags(&side_, hipStreamNonBlocking) != hipSuccess ||
-            hipEventCreateWithFlags(&evFrame_, hipEventDisableTiming) != hipSuccess ||
-            hipEventCreateWithFlags(&evOrder_, hipEventDisableTiming) != hipSuccess)
-            return GSM_ERR_ENCODER_CREATION_FAILED;
-    }
+    a.schedUnits = costOrder ? 2u * a.tileCount : 0u;
     {
         const uint64_t key = ((uint64_t)a.tilesX << 32) | a.tilesY;
         if (key != schedKey_) {  // costs of another geometry: start from index order
             hipMemsetAsync(A_.unitCost, 0, (size_t)a.tileCount * 2 * sizeof(uint16_t), s);
             schedKey_ = key;
         }
-    }
-    if (costOrder) {
-        hipEventRecord(evFrame_, s);  // after the previous frame's blend wrote the costs
-        hipStreamWaitEvent(side_, evFrame_, 0);
-        launch_unit_order_costs(A_.unitCost, A_.unitOrder, 2 * a.tileCount, side_);
-        hipEventRecord(evOrder_, side_);
     }
     const bool prof = (profiling_ & 1) != 0;                   // every stage bracketed
     // only the blend's pair of events, on every frame or every period-th (bits 8-15)
@@ -288,7 +270,7 @@ gsm_status DepthFirstRenderer::renderStereoSbs(hipStream_t s, const gsm_gaussian
     // Blend schedule: (tile, eye) units handed out longest first by the walk lengths the previous
     // frame of the same geometry measured (the image does not depend on the order, only the load
     // balance does).  Tuning::costOrder false (GSM_BLEND_SCHED=0 at create): index order.
-    if (costOrder) hipStreamWaitEvent(s, evOrder_, 0);
+
     A_.blendStats = (profiling_ & 2) ? statsBuf_ : nullptr;
     if (A_.blendStats) hipMemsetAsync(statsBuf_, 0, 4 * sizeof(unsigned long long), s);
     if (prof || blendOnly) hipEventRecord(ev[4], s);

@@ -31,6 +31,7 @@ struct DfArgs {
     float mid[3];       // midpoint of the two camera centres (SH direction)
     float inputIsSRGB;
     uint32_t shComponents, count, tilesX, tilesY, tileCount, maxInstances;
+    uint32_t schedUnits;  // > 0: the projection launch also orders this many blend units (block 0)
 };
 
 // The DepthFirstResources analogue (DepthFirstResources.swift:380-470), sized at create time.

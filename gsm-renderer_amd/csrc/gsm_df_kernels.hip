@@ -118,9 +118,21 @@ __global__ __launch_bounds__(kDfBlock) void k_df_project(const void* __restrict_
                                                          short4* __restrict__ outBounds,
                                                          uint32_t* __restrict__ touchedOut,
                                                          uint32_t* __restrict__ depthKeys,
-                                                         uint32_t* __restrict__ blockSums) {
+                                                         uint32_t* __restrict__ blockSums,
+                                                         const uint16_t* __restrict__ unitCost,
+                                                         uint32_t* __restrict__ unitOrder) {
     __shared__ uint32_t lds[kDfBlock / 64];
-    const uint32_t gid = blockIdx.x * kDfBlock + threadIdx.x;
+    // block 0 of a scheduled launch orders the blend's (tile, eye) units from the previous frame's
+    // walks while the other blocks project (unit_order_block; no side stream, no join)
+    if (P.schedUnits) {
+        if (blockIdx.x == 0) {
+            __shared__ uint32_t uoBase[kUoBuckets], uoMax[kDfBlock / 64];
+            unit_order_block<kDfBlock>(unitCost, unitOrder, P.schedUnits, uoBase, uoMax);
+            return;
+        }
+    }
+    const uint32_t blk = blockIdx.x - (P.schedUnits ? 1u : 0u);
+    const uint32_t gid = blk * kDfBlock + threadIdx.x;
     uint32_t vis = 0;
     if (gid < P.count) {
         float pos[3], scale[3], rot[4], opacity;
@@ -221,7 +233,7 @@ __global__ __launch_bounds__(kDfBlock) void k_df_project(const void* __restrict_
         }
     }
     const uint32_t s = block_reduce_add<kDfBlock>(vis, lds);
-    if (threadIdx.x == 0) blockSums[blockIdx.x] = s;
+    if (threadIdx.x == 0) blockSums[blk] = s;
 }
 
 // ---------------------------------------------------------------------------
@@ -696,10 +708,11 @@ template <bool HALF>
 static void df_launch_project_t(uint32_t deg, const void* world, const void* harm, const DfArgs& a,
                                 const DfArena& A, hipStream_t s) {
     const uint32_t blocks = (a.count + kDfBlock - 1) / kDfBlock;
-    if (blocks == 0) return;
+    if (blocks == 0 && a.schedUnits == 0) return;  // (an empty frame still orders its blend units)
 #define GSM_DF_PROJ(D)                                                                                   \
-    hipLaunchKernelGGL((k_df_project<HALF, D>), dim3(blocks), dim3(kDfBlock), 0, s, world, harm, a,       \
-                       A.renderData, A.bounds, A.touched, A.depthKeys, A.blockSums)
+    hipLaunchKernelGGL((k_df_project<HALF, D>), dim3(blocks + (a.schedUnits ? 1u : 0u)), dim3(kDfBlock), 0, s,  \
+                       world, harm, a, A.renderData, A.bounds, A.touched, A.depthKeys, A.blockSums, A.unitCost, \
+                       A.unitOrder)
     switch (deg) {
         case 0: GSM_DF_PROJ(0); break;
         case 1: GSM_DF_PROJ(1); break;

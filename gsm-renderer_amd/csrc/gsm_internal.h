@@ -17,6 +17,8 @@ struct ProjectArgs {
     uint32_t maxAssignments;
     uint32_t keepRenderData;  // write GaussianRenderData of every visible gaussian (debug readback);
                               // otherwise only where the scatter needs it (rects over kMaskTiles tiles)
+    uint32_t schedUnits;      // > 0: the projection launch also orders this many blend units
+                              // (unit_order_block in one extra workgroup, block 0)
     // per-frame constants of projectCovariance2D / stabilizeCovariance2D / computeDepthFactor,
     // evaluated once on the host with the same IEEE fp32 operations the kernels would repeat
     // per gaussian (GaussianShared.h:326-375, 655-714, 275-278)
@@ -180,5 +182,75 @@ void tile_depth_sort(uint32_t* keysIn, uint32_t* valsIn, uint32_t* keysOut, uint
                      const uint32_t* tileStart, uint32_t tileBegin, uint32_t numTiles, hipStream_t stream,
                      bool ballot, uint32_t* half0, uint32_t* half1, uint32_t* halfCount, uint32_t tileCount,
                      bool full, int numCUs);
+
+// Blend schedule (the blend's unit order): the units in descending order of the walk each made
+// in the previous frame (longest-processing-time-first list scheduling on the blend's persistent
+// waves), as a counting sort into kUoBuckets buckets of walk length (bucket width = max walk /
+// 256, so the order is exact to ~1 % of the longest walk; any order inside a bucket -- the image
+// does not depend on the schedule).  One workgroup of NT threads: the longest walk, bucket sizes
+// (LDS atomics), their scan, a scatter with one LDS atomic per unit; every pass keeps 8 loads per
+// thread in flight.  `base` = LDS[kUoBuckets], `wmax` = LDS[NT / 64].
+constexpr uint32_t kUoBuckets = 256;
+template <int NT>
+__device__ __forceinline__ void unit_order_block(const uint16_t* __restrict__ cost, uint32_t* __restrict__ order,
+                                                 uint32_t n, uint32_t* base, uint32_t* wmax) {
+    static_assert(NT >= (int)kUoBuckets && NT % 64 == 0, "one thread per bucket");
+    constexpr uint32_t UN = 8;
+    const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
+    auto load = [&](uint32_t b0, uint32_t (&c)[UN]) {
+#pragma unroll
+        for (uint32_t k = 0; k < UN; ++k) {
+            const uint32_t i = b0 + k * (uint32_t)NT + t;
+            c[k] = i < n ? (uint32_t)cost[i] : 0u;
+        }
+    };
+    uint32_t m = 0;
+    for (uint32_t b0 = 0; b0 < n; b0 += (uint32_t)NT * UN) {
+        uint32_t c[UN];
+        load(b0, c);
+#pragma unroll
+        for (uint32_t k = 0; k < UN; ++k) m = max(m, c[k]);
+    }
+    for (int off = 32; off > 0; off >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, off));
+    if (lane == 0) wmax[w] = m;
+    if (t < kUoBuckets) base[t] = 0;
+    __syncthreads();
+    uint32_t mx = 0;
+    for (uint32_t k = 0; k < (uint32_t)NT / 64u; ++k) mx = max(mx, wmax[k]);
+    const float scale = (float)kUoBuckets / (float)(mx + 1u);  // bucket 0 = the longest walks
+    auto bucket = [&](uint32_t c) { return (kUoBuckets - 1u) - min(kUoBuckets - 1u, (uint32_t)((float)c * scale)); };
+    for (uint32_t b0 = 0; b0 < n; b0 += (uint32_t)NT * UN) {
+        uint32_t c[UN];
+        load(b0, c);
+#pragma unroll
+        for (uint32_t k = 0; k < UN; ++k)
+            if (b0 + k * (uint32_t)NT + t < n) atomicAdd(&base[bucket(c[k])], 1u);
+    }
+    __syncthreads();
+    if (w == 0) {
+        const uint4 c = *(const uint4*)(base + lane * 4u);
+        const uint32_t local = c.x + c.y + c.z + c.w;
+        uint32_t inc = local;
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t v = __shfl_up(inc, o, 64);
+            if (lane >= (uint32_t)o) inc += v;
+        }
+        const uint32_t e = inc - local;
+        *(uint4*)(base + lane * 4u) = make_uint4(e, e + c.x, e + c.x + c.y, e + c.x + c.y + c.z);
+    }
+    __syncthreads();
+    for (uint32_t b0 = 0; b0 < n; b0 += (uint32_t)NT * UN) {
+        uint32_t c[UN];
+        load(b0, c);
+#pragma unroll
+        for (uint32_t k = 0; k < UN; ++k) {
+            const uint32_t i = b0 + k * (uint32_t)NT + t;
+            if (i < n) {
+                const uint32_t pos = atomicAdd(&base[bucket(c[k])], 1u);
+                if (pos < n) order[pos] = i;
+            }
+        }
+    }
+}
 
 }  // namespace gsm

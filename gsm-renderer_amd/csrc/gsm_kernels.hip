@@ -244,9 +244,20 @@ __global__ __launch_bounds__(kProjectBlock) void k_project(
     const void* __restrict__ world, const void* __restrict__ harm, ProjectArgs P,
     GaussianRenderData* __restrict__ outRD, short4* __restrict__ outBounds,
     BlendRecord* __restrict__ outRec, uint32_t* __restrict__ counts,
-    uint32_t* __restrict__ masks, uint32_t* __restrict__ blockSums, const float2* __restrict__ sincos) {
+    uint32_t* __restrict__ masks, uint32_t* __restrict__ blockSums, const float2* __restrict__ sincos,
+    const uint16_t* __restrict__ unitCost, uint32_t* __restrict__ unitOrder) {
     __shared__ uint32_t lds[kProjectBlock / 64];
     __shared__ uint16_t div255[256];
+    // block 0 of a scheduled launch orders the blend's units from the previous frame's walks while
+    // the other blocks project (no launch, no second stream, no join before the blend)
+    if (P.schedUnits) {
+        if (blockIdx.x == 0) {
+            __shared__ uint32_t uoBase[kUoBuckets], uoMax[kProjectBlock / 64];
+            unit_order_block<kProjectBlock>(unitCost, unitOrder, P.schedUnits, uoBase, uoMax);
+            return;
+        }
+    }
+    const uint32_t blk = blockIdx.x - (P.schedUnits ? 1u : 0u);
     __shared__ float4 sEll[kProjectBlock];   // cmx, cmy, conic A, conic B
     __shared__ float2 sEll2[kProjectBlock];  // conic C, level w
     __shared__ uint32_t sOff[kProjectBlock];  // exclusive candidate offsets
@@ -261,7 +272,7 @@ __global__ __launch_bounds__(kProjectBlock) void k_project(
     __shared__ uint16_t sCand[kCandCap];
     fill_div255(div255);
     const uint32_t tid = threadIdx.x;
-    const uint32_t gid = blockIdx.x * kProjectBlock + tid;
+    const uint32_t gid = blk * kProjectBlock + tid;
     ProjOut o;
     o.vis = false;
     o.countable = false;
@@ -343,7 +354,7 @@ __global__ __launch_bounds__(kProjectBlock) void k_project(
     }
     if (gid < P.count) counts[gid] = ntiles;
     uint32_t s = block_reduce_add<kProjectBlock>(ntiles, lds);
-    if (threadIdx.x == 0) blockSums[blockIdx.x] = s;
+    if (threadIdx.x == 0) blockSums[blk] = s;
 }
 
 // ---------------------------------------------------------------------------
@@ -866,11 +877,11 @@ template <bool HALF>
 static void launch_project_t(uint32_t deg, const void* world, const void* harm, const ProjectArgs& a,
                              const DeviceArena& A, hipStream_t s) {
     const uint32_t blocks = (a.count + kProjectBlock - 1) / kProjectBlock;
-    if (blocks == 0) return;
+    if (blocks == 0 && a.schedUnits == 0) return;  // (an empty frame still orders its blend units)
 #define GSM_LAUNCH_PROJ(D)                                                                     \
-    hipLaunchKernelGGL((k_project<HALF, D>), dim3(blocks), dim3(kProjectBlock), 0, s, world,   \
-                       harm, a, A.renderData, A.bounds, A.rec, A.tileCounts, A.tileMasks, \
-                       A.blockSums, A.sincosTable)
+    hipLaunchKernelGGL((k_project<HALF, D>), dim3(blocks + (a.schedUnits ? 1u : 0u)), dim3(kProjectBlock), 0, s, \
+                       world, harm, a, A.renderData, A.bounds, A.rec, A.tileCounts, A.tileMasks,           \
+                       A.blockSums, A.sincosTable, A.unitCost, A.unitOrder)
     switch (deg) {
         case 0: GSM_LAUNCH_PROJ(0); break;
         case 1: GSM_LAUNCH_PROJ(1); break;

@@ -32,11 +32,6 @@ void GlobalRenderer::release() {
     for (auto& e : events_)
         if (e) hipEventDestroy(e);
     events_.clear();
-    if (evFrame_) hipEventDestroy(evFrame_);
-    if (evOrder_) hipEventDestroy(evOrder_);
-    if (side_) hipStreamDestroy(side_);
-    evFrame_ = evOrder_ = nullptr;
-    side_ = nullptr;
 }
 
 gsm_status GlobalRenderer::alloc(void** p, size_t bytes) {
@@ -249,7 +244,10 @@ gsm_status GlobalRenderer::render(hipStream_t s, const gsm_gaussian_input& in,
     const uint32_t deg = k <= 1 ? 0u : (k <= 4 ? 1u : (k <= 9 ? 2u : 3u));
     const bool half = config_.precision == GSM_PRECISION_FLOAT16;
     return runFrame(s, a, width, height, color, colorPitch, depth, depthPitch,
-                    [&](const ProjectArgs& pa) { launch_project(half, deg, in.gaussians, in.harmonics, pa, arena_, s); });
+                    [&](const ProjectArgs& pa) {
+                        launch_project(half, deg, in.gaussians, in.harmonics, pa, arena_, s);
+                        return true;  // the projection launch ordered the blend units (pa.schedUnits)
+                    });
 }
 
 gsm_status GlobalRenderer::renderRecords(hipStream_t s, const void* records, uint32_t count, uint32_t width,
@@ -263,7 +261,10 @@ gsm_status GlobalRenderer::renderRecords(hipStream_t s, const void* records, uin
     std::memset(&cam, 0, sizeof(cam));
     const ProjectArgs a = frameArgs(cam, width, height, count, 1);
     return runFrame(s, a, width, height, color, colorPitch, depth, depthPitch,
-                    [&](const ProjectArgs& pa) { launch_records_in(records, pa, arena_, s, devCount); });
+                    [&](const ProjectArgs& pa) {
+                        launch_records_in(records, pa, arena_, s, devCount);
+                        return false;  // k_unit_order runs before the blend
+                    });
 }
 
 gsm_status GlobalRenderer::preparePartition(const gsm_gaussian_input& in, const gsm_camera_params& camp,
@@ -368,8 +369,8 @@ gsm_status GlobalRenderer::runFrame(hipStream_t s, const ProjectArgs& a, uint32_
     lastHeight_ = height;
     // Blend schedule: the units ordered by the walk lengths the previous frame of the same
     // geometry measured (the image does not depend on the order, only the load balance does).
-    // The ordering kernel only needs those costs, so it runs on a side stream beside this
-    // frame's projection and sort.
+    // The ordering only needs those costs: one extra workgroup of the projection launch does it
+    // (unit_order_block) while the others project; the records path launches k_unit_order.
     const uint32_t upt = blend_units_per_tile((rowEnd_ - rowBegin_) * tilesX_, numCUs_);
     const uint32_t units = (rowEnd_ - rowBegin_) * tilesX_ * upt;
     const uint64_t key = ((uint64_t)upt << 60) ^ ((uint64_t)width << 40) ^ ((uint64_t)height << 20) ^
@@ -379,22 +380,11 @@ gsm_status GlobalRenderer::runFrame(hipStream_t s, const ProjectArgs& a, uint32_
         schedKey_ = key;
     }
     const bool costOrder = units > 0 && tuning_.costOrder;
-    if (costOrder && !side_) {
-        if (hipStreamCreateWithFlags(&side_, hipStreamNonBlocking) != hipSuccess ||
-            hipEventCreateWithFlags(&evFrame_, hipEventDisableTiming) != hipSuccess ||
-            hipEventCreateWithFlags(&evOrder_, hipEventDisableTiming) != hipSuccess)
-            return GSM_ERR_ENCODER_CREATION_FAILED;
-    }
-    if (costOrder) {
-        hipEventRecord(evFrame_, s);  // after the previous frame's blend wrote the costs
-        hipStreamWaitEvent(side_, evFrame_, 0);
-        launch_unit_order(units, arena_, side_);
-        hipEventRecord(evOrder_, side_);
-    }
+    fa.schedUnits = costOrder ? units : 0u;
 
     hipEvent_t* ev = (prof || blendOnly) ? frameEvents(profFrames_) : nullptr;
     if (prof) hipEventRecord(ev[0], s);
-    front(fa);
+    const bool scheduled = front(fa);
     if (prof) hipEventRecord(ev[1], s);
     launch_scan_blocks(nb, a, arena_, s);
     if (prof) hipEventRecord(ev[2], s);
@@ -447,7 +437,8 @@ gsm_status GlobalRenderer::runFrame(hipStream_t s, const ProjectArgs& a, uint32_
     if (fullRadix)
         launch_half_lists(sortedVals_, rowBegin_ * tilesX_, (rowEnd_ - rowBegin_) * tilesX_, arena_, tileCount_, s);
     arena_.blendTrace = (profiling_ & 4) ? traceBuf_ : nullptr;
-    if (costOrder) hipStreamWaitEvent(s, evOrder_, 0);
+    // the schedule from the walks the previous frame's blend recorded (same stream: no join)
+    if (costOrder && !scheduled) launch_unit_order(units, arena_, s);
     if (prof || blendOnly) hipEventRecord(ev[5], s);
     launch_blend(g, arena_, color, colorPitch, depth, depthPitch, numCUs_, costOrder,
                  (int)config_.color_format, s, tuning_.blendWaves);

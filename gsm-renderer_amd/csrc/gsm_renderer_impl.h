@@ -103,8 +103,6 @@ class GlobalRenderer {
     const uint32_t* unsortedVals_ = nullptr;
     unsigned long long* traceBuf_ = nullptr;  // blend unit trace (profiling bit 2)
     uint64_t schedKey_ = ~0ull;               // geometry the unit costs belong to
-    hipStream_t side_ = nullptr;              // blend-schedule stream (beside project/sort)
-    hipEvent_t evFrame_ = nullptr, evOrder_ = nullptr;
 };
 
 }  // namespace gsm

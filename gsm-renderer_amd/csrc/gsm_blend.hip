@@ -82,7 +82,8 @@ __global__ __launch_bounds__(NT) void k_blend_px(
     size_t colorPitch, uint8_t* __restrict__ depth, size_t depthPitch, int flags,
     const uint32_t* __restrict__ order, uint16_t* __restrict__ unitCost,
     unsigned long long* __restrict__ trace, const uint32_t* __restrict__ half0,
-    const uint32_t* __restrict__ half1, const uint32_t* __restrict__ halfCount, uint32_t tileCount) {
+    const uint32_t* __restrict__ half1, const uint32_t* __restrict__ halfCount, uint32_t tileCount,
+    uint32_t* __restrict__ costMax) {
     static_assert(P == 1 || P == 2, "pairs per lane: quadrant or half-tile units (half-tile lists)");
     static_assert(!COMPACT || P == 2, "compaction: half tiles");
     constexpr uint32_t U = (P == 2 && kBlendU4) ? 4 : 4 / P;  // entries per pipeline group
@@ -211,6 +212,7 @@ __global__ __launch_bounds__(NT) void k_blend_px(
                          : (wv < NTOP ? blockIdx.x * NTOP + wv
                                       : gridDim.x * NTOP + blockIdx.x * (NW - NTOP) + (wv - NTOP));
     bool topPrio = split && wv < NTOP;
+    uint32_t waveMax = 0;  // this wave's longest walk, for the next frame's schedule (costMax)
     while (qi < numUnits) {
         uint32_t u = order ? __builtin_amdgcn_readfirstlane(order[qi]) : qi;
         if (u >= numUnits) u = qi;  // a schedule is a permutation of [0, numUnits); never trust it further
@@ -570,6 +572,7 @@ __global__ __launch_bounds__(NT) void k_blend_px(
             write_pair(ux + offX[q], uy + offY[q], (full > 0) ? (ONE - T[q]) : ONE, R[q], G[q], B[q], D[q]);
     unit_end:
         if (unitCost && lane == 0) unitCost[u] = (uint16_t)min(nproc, 65535u);
+        waveMax = max(waveMax, min(nproc, 65535u));
         if (trace && lane == 0) {
             unsigned long long* t = trace + (size_t)u * 4;
             t[0] = tStart;
@@ -583,6 +586,7 @@ __global__ __launch_bounds__(NT) void k_blend_px(
         topPrio = false;
         qi = __builtin_amdgcn_readfirstlane(nextQ) + gridWaves;
     }
+    if (unitCost && lane == 0 && waveMax) atomicMax(&costMax[(blockIdx.x * NW + wv) % kCostMaxSlots], waveMax);
 }
 
 // ---------------------------------------------------------------------------
@@ -591,10 +595,11 @@ __global__ __launch_bounds__(NT) void k_blend_px(
 // the same block inside its projection launch (k_project, one extra workgroup).
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(1024) void k_unit_order(const uint16_t* __restrict__ cost,
-                                                     uint32_t* __restrict__ order, uint32_t n) {
+                                                     uint32_t* __restrict__ order, uint32_t n,
+                                                     uint32_t* __restrict__ costMax) {
     __shared__ uint32_t base[kUoBuckets];
     __shared__ uint32_t wmax[1024 / 64];
-    unit_order_block<1024>(cost, order, n, base, wmax);
+    unit_order_block<1024>(cost, order, n, base, wmax, costMax);
 }
 
 
@@ -621,12 +626,9 @@ static int blend_waves_per_wg(uint32_t numTiles, int numCUs) {
 }
 
 void launch_unit_order(uint32_t numUnits, const DeviceArena& A, hipStream_t s) {
-    hipLaunchKernelGGL(k_unit_order, dim3(1), dim3(1024), 0, s, A.unitCost, A.unitOrder, numUnits);
+    hipLaunchKernelGGL(k_unit_order, dim3(1), dim3(1024), 0, s, A.unitCost, A.unitOrder, numUnits, A.costMax);
 }
 
-void launch_unit_order_costs(const uint16_t* cost, uint32_t* order, uint32_t numUnits, hipStream_t s) {
-    hipLaunchKernelGGL(k_unit_order, dim3(1), dim3(1024), 0, s, cost, order, numUnits);
-}
 
 // Measured schedule choices: units longest-first by last frame's walk (costOrder;
 // 1080p 8 waves 293 -> 248 us, 4K 16 waves 703 -> 660), the longest on one top-priority wave per
@@ -653,7 +655,7 @@ void launch_blend(const FrameGeometry& g, const DeviceArena& A, void* color,
     hipLaunchKernelGGL((k_blend_px<NTH, PP, CMP>), dim3(grid), dim3(NTH), 0, s, A.tileStart, A.rec, \
                        A.expTable, A.tileQueue, t0, numTiles, g.tilesX, g.width, g.height,          \
                        (uint8_t*)color, colorPitch, (uint8_t*)depth, depthPitch, flags, order, A.unitCost,  \
-                       A.blendTrace, A.halfVals[0], A.halfVals[1], A.halfCount, g.tileCount)
+                       A.blendTrace, A.halfVals[0], A.halfVals[1], A.halfCount, g.tileCount, A.costMax)
     // half tiles compact to one pair per lane once <= 16 of their 32 groups are alive
     if (P == 1) {
         if (waves == 16) GSM_LAUNCH_BLEND(1024, 1, false);

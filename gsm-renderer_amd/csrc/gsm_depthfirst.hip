@@ -151,6 +151,7 @@ gsm_status DepthFirstRenderer::create(const gsm_renderer_config& cfg, int hipDev
     GSM_DF_ALLOC(A.expTable, 65536 * 2);
     GSM_DF_ALLOC(A.unitCost, (size_t)r->maxTiles_ * 2 * sizeof(uint16_t));
     GSM_DF_ALLOC(A.unitOrder, (size_t)r->maxTiles_ * 2 * sizeof(uint32_t));
+    GSM_DF_ALLOC(A.costMax, kCostMaxSlots * sizeof(uint32_t));
 #undef GSM_DF_ALLOC
     if (st != GSM_OK) {
         delete r;
@@ -161,6 +162,7 @@ gsm_status DepthFirstRenderer::create(const gsm_renderer_config& cfg, int hipDev
     if (hipMemcpy(A.expTable, expt.data(), 65536 * 2, hipMemcpyHostToDevice) != hipSuccess ||
         hipMemset(A.visHdr, 0, sizeof(TileAssignmentHeader)) != hipSuccess ||
         hipMemset(A.instHdr, 0, sizeof(TileAssignmentHeader)) != hipSuccess ||
+        hipMemset(A.costMax, 0, kCostMaxSlots * sizeof(uint32_t)) != hipSuccess ||
         hipMemset(A.starts, 0, ((size_t)r->maxTiles_ + 1) * sizeof(uint32_t)) != hipSuccess) {
         delete r;
         return GSM_ERR_FAILED_TO_ALLOCATE_BUFFER;
@@ -240,6 +242,7 @@ gsm_status DepthFirstRenderer::renderStereoSbs(hipStream_t s, const gsm_gaussian
         const uint64_t key = ((uint64_t)a.tilesX << 32) | a.tilesY;
         if (key != schedKey_) {  // costs of another geometry: start from index order
             hipMemsetAsync(A_.unitCost, 0, (size_t)a.tileCount * 2 * sizeof(uint16_t), s);
+            hipMemsetAsync(A_.costMax, 0, kCostMaxSlots * sizeof(uint32_t), s);
             schedKey_ = key;
         }
     }

@@ -55,6 +55,7 @@ struct DfArena {
     uint16_t* expTable = nullptr;                 // [65536] stereo alpha table (r^2 cutoff folded)
     uint16_t* unitCost = nullptr;                 // [2 * maxTiles] entries each (tile, eye) unit walked
     uint32_t* unitOrder = nullptr;                // [2 * maxTiles] units, longest last-frame walk first
+    uint32_t* costMax = nullptr;                  // [kCostMaxSlots] longest walk of the last blend
     unsigned long long* blendStats = nullptr;     // [4] profiling bit 1: entries walked / with a real
                                                   // mean / blended, list entries (null: not counted)
 };
@@ -78,8 +79,9 @@ void df_launch_instances(const uint32_t* order, const DfArgs& a, const DfArena& 
 void df_launch_ranges(const uint32_t* sortedTiles, const DfArgs& a, const DfArena& A, hipStream_t stream);
 // clearStereoRenderTextureKernel + depthFirstStereoRender + DepthFirstStereoCopyEncoder
 // (:1813-1982; DepthFirstStereoCopyEncoder.swift:29-99) in one persistent kernel
-// costOrder: hand the units out longest-last-frame-walk first (A.unitOrder, filled by
-// launch_unit_order_costs from A.unitCost); the blend records this frame's walks into A.unitCost
+// costOrder: hand the units out longest-last-frame-walk first (A.unitOrder, filled by block 0 of
+// the projection launch from A.unitCost); the blend records this frame's walks into A.unitCost
+// and each wave's longest into A.costMax
 void df_launch_blend(const uint32_t* sortedGids, const DfArgs& a, const DfArena& A, void* color, size_t pitch,
                      int colorFormat, int numCUs, bool costOrder, hipStream_t stream);
 

@@ -120,14 +120,15 @@ __global__ __launch_bounds__(kDfBlock) void k_df_project(const void* __restrict_
                                                          uint32_t* __restrict__ depthKeys,
                                                          uint32_t* __restrict__ blockSums,
                                                          const uint16_t* __restrict__ unitCost,
-                                                         uint32_t* __restrict__ unitOrder) {
+                                                         uint32_t* __restrict__ unitOrder,
+                                                         uint32_t* __restrict__ costMax) {
     __shared__ uint32_t lds[kDfBlock / 64];
     // block 0 of a scheduled launch orders the blend's (tile, eye) units from the previous frame's
     // walks while the other blocks project (unit_order_block; no side stream, no join)
     if (P.schedUnits) {
         if (blockIdx.x == 0) {
             __shared__ uint32_t uoBase[kUoBuckets], uoMax[kDfBlock / 64];
-            unit_order_block<kDfBlock>(unitCost, unitOrder, P.schedUnits, uoBase, uoMax);
+            unit_order_block<kDfBlock>(unitCost, unitOrder, P.schedUnits, uoBase, uoMax, costMax);
             return;
         }
     }
@@ -549,7 +550,8 @@ __global__ __launch_bounds__(NW * 64) void k_df_blend_eye(const uint32_t* __rest
                                                           uint8_t* __restrict__ color, size_t pitch, int fmt,
                                                           const uint32_t* __restrict__ order,
                                                           uint16_t* __restrict__ unitCost, int flags,
-                                                          unsigned long long* __restrict__ stats) {
+                                                          unsigned long long* __restrict__ stats,
+                                                          uint32_t* __restrict__ costMax) {
     __shared__ __attribute__((aligned(16))) uint16_t tbl[65536];
     __shared__ __attribute__((aligned(16))) uint4 stageA[NW][kDfEyeBatch];
     __shared__ __attribute__((aligned(16))) uint32_t stageB[NW][kDfEyeBatch];
@@ -578,6 +580,7 @@ __global__ __launch_bounds__(NW * 64) void k_df_blend_eye(const uint32_t* __rest
                          : (wave < NTOP ? blockIdx.x * NTOP + wave
                                         : gridDim.x * NTOP + blockIdx.x * (NW - NTOP) + (wave - NTOP));
     bool topPrio = split && wave < NTOP;
+    uint32_t waveMax = 0;  // this wave's longest walk, for the next frame's schedule (costMax)
     for (;; topPrio = false) {
         if (qi >= units) break;
         uint32_t u = order ? __builtin_amdgcn_readfirstlane(order[qi]) : qi;
@@ -675,6 +678,7 @@ __global__ __launch_bounds__(NW * 64) void k_df_blend_eye(const uint32_t* __rest
         if (lane == 0) nq = atomicAdd(queue, 1u);
         qi = __builtin_amdgcn_readfirstlane(nq) + gridDim.x * NW;
         if (unitCost && lane == 0) unitCost[u] = (uint16_t)min(walked, 65535u);
+        waveMax = max(waveMax, min(walked, 65535u));
         if (STATS && lane == 0) {
             atomicAdd(&stats[0], (unsigned long long)walked);
             atomicAdd(&stats[1], (unsigned long long)nValid);
@@ -699,6 +703,7 @@ __global__ __launch_bounds__(NW * 64) void k_df_blend_eye(const uint32_t* __rest
                                (ub >> 16) | (ua & 0xFFFF0000u));
         }
     }
+    if (unitCost && lane == 0 && waveMax) atomicMax(&costMax[(blockIdx.x * NW + wave) % kCostMaxSlots], waveMax);
 }
 
 // ---------------------------------------------------------------------------
@@ -712,7 +717,7 @@ static void df_launch_project_t(uint32_t deg, const void* world, const void* har
 #define GSM_DF_PROJ(D)                                                                                   \
     hipLaunchKernelGGL((k_df_project<HALF, D>), dim3(blocks + (a.schedUnits ? 1u : 0u)), dim3(kDfBlock), 0, s,  \
                        world, harm, a, A.renderData, A.bounds, A.touched, A.depthKeys, A.blockSums, A.unitCost, \
-                       A.unitOrder)
+                       A.unitOrder, A.costMax)
     switch (deg) {
         case 0: GSM_DF_PROJ(0); break;
         case 1: GSM_DF_PROJ(1); break;
@@ -768,12 +773,14 @@ void df_launch_blend(const uint32_t* sortedGids, const DfArgs& a, const DfArena&
         hipLaunchKernelGGL((k_df_blend_eye<kDfBlendWaves, true>), dim3(grid), dim3(kDfBlendWaves * 64), 0, s,
                            A.starts, sortedGids, A.renderData, A.expTable, A.queue, a.tilesX, a.tileCount,
                            (uint32_t)a.width, (uint32_t)a.height, (uint8_t*)color, pitch, colorFormat,
-                           costOrder ? (const uint32_t*)A.unitOrder : nullptr, A.unitCost, flags, A.blendStats);
+                           costOrder ? (const uint32_t*)A.unitOrder : nullptr, A.unitCost, flags, A.blendStats,
+                           A.costMax);
     else
         hipLaunchKernelGGL((k_df_blend_eye<kDfBlendWaves, false>), dim3(grid), dim3(kDfBlendWaves * 64), 0, s,
                            A.starts, sortedGids, A.renderData, A.expTable, A.queue, a.tilesX, a.tileCount,
                            (uint32_t)a.width, (uint32_t)a.height, (uint8_t*)color, pitch, colorFormat,
-                           costOrder ? (const uint32_t*)A.unitOrder : nullptr, A.unitCost, flags, nullptr);
+                           costOrder ? (const uint32_t*)A.unitOrder : nullptr, A.unitCost, flags, nullptr,
+                           A.costMax);
 }
 
 }  // namespace gsm

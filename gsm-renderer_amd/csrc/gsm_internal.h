@@ -65,6 +65,7 @@ struct DeviceArena {
     uint32_t* keysKeep = nullptr;              // [cap] unsorted copy (profiling/debug only)
     uint32_t* valsKeep = nullptr;
     unsigned long long* blendTrace = nullptr;  // [4 * tiles * 4] (profiling bit 2 only)
+    uint32_t* costMax = nullptr;               // [kCostMaxSlots] longest walk of the last blend
     uint32_t* radixHist = nullptr;             // [256 * radixGrid]
     uint32_t* radixBinTotals = nullptr;        // [256]
     uint32_t* tileStart = nullptr;             // [tileCount + 1] first sorted entry of each tile
@@ -155,8 +156,6 @@ void launch_blend(const FrameGeometry& geo, const DeviceArena& A,
 // orders the blend units by the walk lengths the previous frame measured (longest first), so
 // the dynamic queue hands out long units before short ones (A.unitOrder[numUnits])
 void launch_unit_order(uint32_t numUnits, const DeviceArena& A, hipStream_t stream);
-// the same ordering for any cost array (the DepthFirst blend's (tile, eye) units)
-void launch_unit_order_costs(const uint16_t* cost, uint32_t* order, uint32_t numUnits, hipStream_t stream);
 // blend kernel shape: pixel pairs per lane (0 = quadrant kernel) and blend units per tile
 int blend_pairs_per_lane(uint32_t numTiles, int numCUs);
 uint32_t blend_units_per_tile(uint32_t numTiles, int numCUs);
@@ -189,11 +188,14 @@ void tile_depth_sort(uint32_t* keysIn, uint32_t* valsIn, uint32_t* keysOut, uint
 // 256, so the order is exact to ~1 % of the longest walk; any order inside a bucket -- the image
 // does not depend on the schedule).  One workgroup of NT threads: the longest walk, bucket sizes
 // (LDS atomics), their scan, a scatter with one LDS atomic per unit; every pass keeps 8 loads per
-// thread in flight.  `base` = LDS[kUoBuckets], `wmax` = LDS[NT / 64].
+// thread in flight.  `base` = LDS[kUoBuckets], `wmax` = LDS[NT / 64]; the longest walk comes from
+// `costMax` (kCostMaxSlots words the blend's waves atomicMax into).
 constexpr uint32_t kUoBuckets = 256;
+constexpr uint32_t kCostMaxSlots = 64;  // words of the longest-walk maximum (spread atomics)
 template <int NT>
 __device__ __forceinline__ void unit_order_block(const uint16_t* __restrict__ cost, uint32_t* __restrict__ order,
-                                                 uint32_t n, uint32_t* base, uint32_t* wmax) {
+                                                 uint32_t n, uint32_t* base, uint32_t* wmax,
+                                                 uint32_t* __restrict__ costMax) {
     static_assert(NT >= (int)kUoBuckets && NT % 64 == 0, "one thread per bucket");
     constexpr uint32_t UN = 8;
     const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
@@ -204,17 +206,14 @@ __device__ __forceinline__ void unit_order_block(const uint16_t* __restrict__ co
             c[k] = i < n ? (uint32_t)cost[i] : 0u;
         }
     };
-    uint32_t m = 0;
-    for (uint32_t b0 = 0; b0 < n; b0 += (uint32_t)NT * UN) {
-        uint32_t c[UN];
-        load(b0, c);
-#pragma unroll
-        for (uint32_t k = 0; k < UN; ++k) m = max(m, c[k]);
-    }
+    // the longest walk: the previous frame's blend left each wave's longest in one of kCostMaxSlots
+    // words (atomicMax at its exit); read them and clear them for this frame's blend
+    uint32_t m = t < kCostMaxSlots ? costMax[t] : 0u;
     for (int off = 32; off > 0; off >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, off));
     if (lane == 0) wmax[w] = m;
     if (t < kUoBuckets) base[t] = 0;
     __syncthreads();
+    if (t < kCostMaxSlots) costMax[t] = 0;
     uint32_t mx = 0;
     for (uint32_t k = 0; k < (uint32_t)NT / 64u; ++k) mx = max(mx, wmax[k]);
     const float scale = (float)kUoBuckets / (float)(mx + 1u);  // bucket 0 = the longest walks

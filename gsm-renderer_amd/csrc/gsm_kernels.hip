@@ -245,7 +245,7 @@ __global__ __launch_bounds__(kProjectBlock) void k_project(
     GaussianRenderData* __restrict__ outRD, short4* __restrict__ outBounds,
     BlendRecord* __restrict__ outRec, uint32_t* __restrict__ counts,
     uint32_t* __restrict__ masks, uint32_t* __restrict__ blockSums, const float2* __restrict__ sincos,
-    const uint16_t* __restrict__ unitCost, uint32_t* __restrict__ unitOrder) {
+    const uint16_t* __restrict__ unitCost, uint32_t* __restrict__ unitOrder, uint32_t* __restrict__ costMax) {
     __shared__ uint32_t lds[kProjectBlock / 64];
     __shared__ uint16_t div255[256];
     // block 0 of a scheduled launch orders the blend's units from the previous frame's walks while
@@ -253,7 +253,7 @@ __global__ __launch_bounds__(kProjectBlock) void k_project(
     if (P.schedUnits) {
         if (blockIdx.x == 0) {
             __shared__ uint32_t uoBase[kUoBuckets], uoMax[kProjectBlock / 64];
-            unit_order_block<kProjectBlock>(unitCost, unitOrder, P.schedUnits, uoBase, uoMax);
+            unit_order_block<kProjectBlock>(unitCost, unitOrder, P.schedUnits, uoBase, uoMax, costMax);
             return;
         }
     }
@@ -881,7 +881,7 @@ static void launch_project_t(uint32_t deg, const void* world, const void* harm, 
 #define GSM_LAUNCH_PROJ(D)                                                                     \
     hipLaunchKernelGGL((k_project<HALF, D>), dim3(blocks + (a.schedUnits ? 1u : 0u)), dim3(kProjectBlock), 0, s, \
                        world, harm, a, A.renderData, A.bounds, A.rec, A.tileCounts, A.tileMasks,           \
-                       A.blockSums, A.sincosTable, A.unitCost, A.unitOrder)
+                       A.blockSums, A.sincosTable, A.unitCost, A.unitOrder, A.costMax)
     switch (deg) {
         case 0: GSM_LAUNCH_PROJ(0); break;
         case 1: GSM_LAUNCH_PROJ(1); break;

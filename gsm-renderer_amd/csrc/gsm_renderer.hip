@@ -119,6 +119,7 @@ gsm_status GlobalRenderer::create(const gsm_renderer_config& cfg, int hipDevice,
     GSM_ALLOC(A.tileQueue, sizeof(uint32_t));
     GSM_ALLOC(A.unitCost, (size_t)r->tileCount_ * 4 * sizeof(uint16_t));
     GSM_ALLOC(A.unitOrder, (size_t)r->tileCount_ * 4 * sizeof(uint32_t));
+    GSM_ALLOC(A.costMax, kCostMaxSlots * sizeof(uint32_t));
     GSM_ALLOC(A.halfVals[0], cap * sizeof(uint32_t));
     GSM_ALLOC(A.halfVals[1], cap * sizeof(uint32_t));
     GSM_ALLOC(A.halfCount, (size_t)r->tileCount_ * 2 * sizeof(uint32_t));
@@ -139,6 +140,7 @@ gsm_status GlobalRenderer::create(const gsm_renderer_config& cfg, int hipDevice,
         hipMemset(A.header, 0, sizeof(TileAssignmentHeader)) != hipSuccess ||
         hipMemset(A.tileStart, 0, ((size_t)r->tileCount_ + 1) * sizeof(uint32_t)) != hipSuccess ||
         hipMemset(A.unitCost, 0, (size_t)r->tileCount_ * 4 * sizeof(uint16_t)) != hipSuccess ||
+        hipMemset(A.costMax, 0, kCostMaxSlots * sizeof(uint32_t)) != hipSuccess ||
         // every entry of the value buffers is a valid gaussian id at all times (the blend's
         // clamped, unpredicated gathers may read entry 0 of an empty frame)
         hipMemset(A.vals[0], 0, cap * sizeof(uint32_t)) != hipSuccess ||
@@ -377,6 +379,7 @@ gsm_status GlobalRenderer::runFrame(hipStream_t s, const ProjectArgs& a, uint32_
                          ((uint64_t)rowBegin_ << 10) ^ rowEnd_;
     if (key != schedKey_) {
         hipMemsetAsync(arena_.unitCost, 0, (size_t)units * sizeof(uint16_t), s);
+        hipMemsetAsync(arena_.costMax, 0, kCostMaxSlots * sizeof(uint32_t), s);
         schedKey_ = key;
     }
     const bool costOrder = units > 0 && tuning_.costOrder;

@@ -213,6 +213,10 @@ __global__ __launch_bounds__(NT) void k_blend_px(
                                       : gridDim.x * NTOP + blockIdx.x * (NW - NTOP) + (wv - NTOP));
     bool topPrio = split && wv < NTOP;
     uint32_t waveMax = 0;  // this wave's longest walk, for the next frame's schedule (costMax)
+    // dynamic units: positions gridWaves + stripe + stripes * k from this workgroup's counter
+    const uint32_t stripes = (gridDim.x % kQueueStripes) == 0 ? kQueueStripes : 1u;
+    const uint32_t stripe = blockIdx.x % stripes;
+    uint32_t* const myQueue = queue + stripe * kQueueStride;
     while (qi < numUnits) {
         uint32_t u = order ? __builtin_amdgcn_readfirstlane(order[qi]) : qi;
         if (u >= numUnits) u = qi;  // a schedule is a permutation of [0, numUnits); never trust it further
@@ -263,7 +267,7 @@ __global__ __launch_bounds__(NT) void k_blend_px(
             uint4 mA = *(const uint4*)(rec + gi2);
             uint32_t mB = rec[gi2].b;
             uint32_t nI = lst[min(192u + lane, last)];
-            if (lane == 0) nextQ = atomicAdd(queue, 1u);
+            if (lane == 0) nextQ = atomicAdd(myQueue, 1u);
             if (lane >= count) {
                 bA = pad;
                 bB = 0u;
@@ -564,7 +568,7 @@ __global__ __launch_bounds__(NT) void k_blend_px(
             }
         unit_done:;
         } else {
-            if (lane == 0) nextQ = atomicAdd(queue, 1u);
+            if (lane == 0) nextQ = atomicAdd(myQueue, 1u);
         }
         // write (GlobalShaders.metal:1152-1186); empty tiles keep the clear colour (0,0,0,1)
 #pragma unroll
@@ -584,7 +588,7 @@ __global__ __launch_bounds__(NT) void k_blend_px(
         }
         if (agePrio || topPrio) __builtin_amdgcn_s_setprio(0);
         topPrio = false;
-        qi = __builtin_amdgcn_readfirstlane(nextQ) + gridWaves;
+        qi = gridWaves + stripe + stripes * __builtin_amdgcn_readfirstlane(nextQ);
     }
     if (unitCost && lane == 0 && waveMax) atomicMax(&costMax[(blockIdx.x * NW + wv) % kCostMaxSlots], waveMax);
 }

@@ -147,7 +147,7 @@ gsm_status DepthFirstRenderer::create(const gsm_renderer_config& cfg, int hipDev
         st = GSM_ERR_FAILED_TO_ALLOCATE_BUFFER;
     GSM_DF_ALLOC(A.radixBinTotals, 256 * 4);
     GSM_DF_ALLOC(A.starts, ((size_t)r->maxTiles_ + 1) * sizeof(uint32_t));
-    GSM_DF_ALLOC(A.queue, 4);
+    GSM_DF_ALLOC(A.queue, kQueueStripes * kQueueStride * sizeof(uint32_t));
     GSM_DF_ALLOC(A.expTable, 65536 * 2);
     GSM_DF_ALLOC(A.unitCost, (size_t)r->maxTiles_ * 2 * sizeof(uint16_t));
     GSM_DF_ALLOC(A.unitOrder, (size_t)r->maxTiles_ * 2 * sizeof(uint32_t));

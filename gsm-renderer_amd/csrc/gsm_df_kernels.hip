@@ -581,6 +581,9 @@ __global__ __launch_bounds__(NW * 64) void k_df_blend_eye(const uint32_t* __rest
                                         : gridDim.x * NTOP + blockIdx.x * (NW - NTOP) + (wave - NTOP));
     bool topPrio = split && wave < NTOP;
     uint32_t waveMax = 0;  // this wave's longest walk, for the next frame's schedule (costMax)
+    // dynamic units from the workgroup's stripe of the queue (kQueueStripes, gsm_internal.h)
+    const uint32_t stripes = (gridDim.x % kQueueStripes) == 0 ? kQueueStripes : 1u;
+    const uint32_t stripe = blockIdx.x % stripes;
     for (;; topPrio = false) {
         if (qi >= units) break;
         uint32_t u = order ? __builtin_amdgcn_readfirstlane(order[qi]) : qi;
@@ -675,8 +678,8 @@ __global__ __launch_bounds__(NW * 64) void k_df_blend_eye(const uint32_t* __rest
         }
         if (agePrio || topPrio) __builtin_amdgcn_s_setprio(0);
         uint32_t nq = 0;
-        if (lane == 0) nq = atomicAdd(queue, 1u);
-        qi = __builtin_amdgcn_readfirstlane(nq) + gridDim.x * NW;
+        if (lane == 0) nq = atomicAdd(queue + stripe * kQueueStride, 1u);
+        qi = gridDim.x * NW + stripe + stripes * __builtin_amdgcn_readfirstlane(nq);
         if (unitCost && lane == 0) unitCost[u] = (uint16_t)min(walked, 65535u);
         waveMax = max(waveMax, min(walked, 65535u));
         if (STATS && lane == 0) {

@@ -69,7 +69,7 @@ struct DeviceArena {
     uint32_t* radixHist = nullptr;             // [256 * radixGrid]
     uint32_t* radixBinTotals = nullptr;        // [256]
     uint32_t* tileStart = nullptr;             // [tileCount + 1] first sorted entry of each tile
-    uint32_t* tileQueue = nullptr;             // [1] blend work counter
+    uint32_t* tileQueue = nullptr;             // [kQueueStripes * kQueueStride] blend work counters
     uint16_t* unitCost = nullptr;              // [4 * tileCount] list entries each blend unit walked
     uint32_t* unitOrder = nullptr;             // [4 * tileCount] blend units, longest last-frame walk first
     uint32_t* halfVals[2] = {nullptr, nullptr};  // [cap] per half tile: the tile's sorted gaussian ids whose
@@ -191,6 +191,11 @@ void tile_depth_sort(uint32_t* keysIn, uint32_t* valsIn, uint32_t* keysOut, uint
 // thread in flight.  `base` = LDS[kUoBuckets], `wmax` = LDS[NT / 64]; the longest walk comes from
 // `costMax` (kCostMaxSlots words the blend's waves atomicMax into).
 constexpr uint32_t kUoBuckets = 256;
+// The blend's dynamic queue is striped: workgroup b draws positions of the schedule congruent to
+// b % kQueueStripes from counter b % kQueueStripes (words kQueueStride apart, one 64-B line each),
+// so the same-address atomics of the many waves spread over 8 lines (r02: with one counter the
+// average gap between a wave's units at 4K was 7.7 us of queueing).
+constexpr uint32_t kQueueStripes = 8, kQueueStride = 16;
 constexpr uint32_t kCostMaxSlots = 64;  // words of the longest-walk maximum (spread atomics)
 template <int NT>
 __device__ __forceinline__ void unit_order_block(const uint16_t* __restrict__ cost, uint32_t* __restrict__ order,

@@ -577,7 +577,8 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_blocks(uint32_t* __restri
         hdr->maxCapacity = maxAssignments;
         hdr->paddedCount = ((tot + 1023u) / 1024u) * 1024u;
         hdr->overflow = ovf;
-        *blendQueue = 0;  // the blend's work counter for this frame (saves a memset launch)
+        // the blend's work counters for this frame (saves a memset launch)
+        for (uint32_t q = 0; q < kQueueStripes; ++q) blendQueue[q * kQueueStride] = 0;
     }
 }
 

@@ -116,7 +116,7 @@ gsm_status GlobalRenderer::create(const gsm_renderer_config& cfg, int hipDevice,
         st = GSM_ERR_FAILED_TO_ALLOCATE_BUFFER;
     GSM_ALLOC(A.radixBinTotals, 256 * sizeof(uint32_t));
     GSM_ALLOC(A.tileStart, ((size_t)r->tileCount_ + 1) * sizeof(uint32_t));
-    GSM_ALLOC(A.tileQueue, sizeof(uint32_t));
+    GSM_ALLOC(A.tileQueue, kQueueStripes * kQueueStride * sizeof(uint32_t));
     GSM_ALLOC(A.unitCost, (size_t)r->tileCount_ * 4 * sizeof(uint16_t));
     GSM_ALLOC(A.unitOrder, (size_t)r->tileCount_ * 4 * sizeof(uint32_t));
     GSM_ALLOC(A.costMax, kCostMaxSlots * sizeof(uint32_t));

@@ -68,6 +68,21 @@ def main():
         "occupancy_deciles": [occ[i] for i in range(0, 200, 20)],
         "occupancy_tail": [occ[i] for i in range(180, 200, 2)],
     }
+    # per wave slot (XCC_ID << 48 | HW_ID of t[3]): the gaps between a slot's consecutive units
+    # (unit end -> next unit's first list load: the order / tile-start / half-count loads)
+    t3 = tr[:, 3].astype(np.uint64)
+    slot = ((t3 >> np.uint64(48)) << np.uint64(32)) | (t3 & np.uint64(0xFFFFFFFF))
+    gaps = []
+    for sid in np.unique(slot):
+        sel = np.nonzero(slot == sid)[0]
+        o = sel[np.argsort(start[sel])]
+        if o.size > 1:
+            gaps.extend((start[o[1:]] - end[o[:-1]]).tolist())
+    gaps = np.array(gaps) if gaps else np.zeros(1)
+    out["slots"] = int(np.unique(slot).size)
+    out["inter_unit_gap_us_mean"] = float(gaps.mean() / 1e3)
+    out["inter_unit_gap_us_p90"] = float(np.percentile(gaps, 90) / 1e3)
+    out["gap_frac_of_slot_time"] = float(gaps.sum() / max(1.0, dur.sum() + gaps.sum()))
     print(json.dumps(out))
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
     np.savez_compressed(os.path.join(ROOT, "gpurun_out", f"blend_trace_{args.config}_{args.angle:g}.npz"), trace=tr)

@@ -55,7 +55,6 @@ __device__ __forceinline__ uint32_t quad_max_u32(uint32_t v) {
 // k_blend_px: one wave per blend unit, P pixel pairs per lane.
 //   P = 1: 16x8 quadrant of a tile (4 units per tile), a 4x2 group spans 4 lanes
 //   P = 2: 16x16 half tile (2 units per tile), a group spans 2 lanes (rows)
-//   P = 4: the 32x16 tile, a lane is one reference thread (4x2 pixels)
 // More pairs per lane give every list entry's uniform work (5 readlanes, the dy terms of
 // the quadratic form) to more pixels and P independent T chains per lane; fewer give
 // shorter walks (a unit walks until its slowest group breaks).  The list is walked in
@@ -70,10 +69,9 @@ __device__ __forceinline__ void blend_wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-constexpr bool kBlendU4 = false;  // 4-entry groups at P = 2 (measured: no gain)
-// Records of the walk's current 64-entry batch staged in LDS and read back with uniform
-// addresses (one ds_read_b128 + one ds_read_b32 broadcast per entry) instead of 5 v_readlane.
-constexpr bool kLdsRecords = true;
+// The records of the walk's current 64-entry batch are staged in LDS and read back with uniform
+// addresses (one ds_read_b128 + one ds_read_b32 broadcast per entry) instead of 5 v_readlane;
+// 2-entry pipeline groups at P = 2 (4-entry groups measured no gain).
 template <int NT, int P, bool COMPACT = false>
 __global__ __launch_bounds__(NT) void k_blend_px(
     const uint32_t* __restrict__ tileStart, const BlendRecord* __restrict__ rec,
@@ -86,17 +84,17 @@ __global__ __launch_bounds__(NT) void k_blend_px(
     uint32_t* __restrict__ costMax) {
     static_assert(P == 1 || P == 2, "pairs per lane: quadrant or half-tile units (half-tile lists)");
     static_assert(!COMPACT || P == 2, "compaction: half tiles");
-    constexpr uint32_t U = (P == 2 && kBlendU4) ? 4 : 4 / P;  // entries per pipeline group
+    constexpr uint32_t U = 4 / P;  // entries per pipeline group
     constexpr uint32_t NG = 64 / U;      // groups per 64-entry batch
     constexpr uint32_t EXITG = 16 / U;   // exit test every 16 entries
     constexpr uint32_t UPT = 4 / P;      // units per tile
     constexpr uint32_t NW = NT / 64;
-    constexpr uint32_t UNROLL = P == 4 ? 1 : NG;  // P = 4: 64 one-entry groups stay a loop
+    constexpr uint32_t UNROLL = NG;
     const bool agePrio = (flags & 2) != 0;
     __shared__ __attribute__((aligned(16))) uint16_t tbl[65536];
     __shared__ uint32_t cscr[NW][16];  // compaction: the alive groups of each wave, in order
-    __shared__ __attribute__((aligned(16))) uint4 lrecA[kLdsRecords ? NW : 1][64];  // current batch records
-    __shared__ uint32_t lrecB[kLdsRecords ? NW : 1][64];
+    __shared__ __attribute__((aligned(16))) uint4 lrecA[NW][64];  // current batch records
+    __shared__ uint32_t lrecB[NW][64];
     {
         const uint4* src = (const uint4*)expTable;
         uint4* dst = (uint4*)tbl;
@@ -179,7 +177,7 @@ __global__ __launch_bounds__(NT) void k_blend_px(
         const uint32_t grp = lane >> 2;
         offX[0] = (grp & 3u) * 4u + (lane & 1u) * 2u;
         offY[0] = (grp >> 2) * 2u + ((lane >> 1) & 1u);
-    } else if (P == 2) {
+    } else {
         // a 4x2 group on lanes 2g (columns 0-1) and 2g + 1 (columns 2-3), each lane 2x2 pixels:
         // pair 0 = row 0, pair 1 = row 1 of the same two columns, so the dx terms of the quadratic
         // form are shared by the lane's pairs and the dy terms come as one pair of rows
@@ -187,11 +185,6 @@ __global__ __launch_bounds__(NT) void k_blend_px(
         offX[0] = offX[P - 1] = (grp & 3u) * 4u + (lane & 1u) * 2u;
         offY[0] = (grp >> 2) * 2u;
         offY[P - 1] = offY[0] + 1u;
-    } else {
-        offX[0] = offX[2 % P] = (lane & 7u) * 4u;
-        offX[1 % P] = offX[3 % P] = (lane & 7u) * 4u + 2u;
-        offY[0] = offY[1 % P] = (lane >> 3) * 2u;
-        offY[2 % P] = offY[3 % P] = (lane >> 3) * 2u + 1u;
     }
     const h2 ONE = {(h1)1.0f, (h1)1.0f};
     const h2 ZERO = {(h1)0.0f, (h1)0.0f};
@@ -222,7 +215,7 @@ __global__ __launch_bounds__(NT) void k_blend_px(
         if (u >= numUnits) u = qi;  // a schedule is a permutation of [0, numUnits); never trust it further
         const uint32_t tile = tileBegin + u / UPT, part = u % UPT;
         const uint32_t tileX = tile % tilesX, tileY = tile / tilesX;
-        const uint32_t ux = tileX * kTileWidth + (P == 4 ? 0u : (part & 1u) * 16u);
+        const uint32_t ux = tileX * kTileWidth + (part & 1u) * 16u;
         const uint32_t uy = tileY * kTileHeight + (P == 1 ? (part >> 1) * 8u : 0u);
         // the unit walks its half's list: the tile's sorted entries without those whose skip flag for
         // this half is set (k_scatter, k_half_lists) -- they would leave every pixel of it unchanged
@@ -296,20 +289,13 @@ __global__ __launch_bounds__(NT) void k_blend_px(
                     pq[P - 1] = (dxx + splat_hi(dyy)) + (dx * splat_hi(dyv)) * splat_lo(oc);
                     return;
                 }
-#pragma unroll
-                for (int k = 0; k < P; ++k) {
-                    const h2 dx = X[k] - splat_lo(mean);
-                    const bool r2nd = (P == 4) && (k >= 2);
-                    const h2 dy = r2nd ? splat_hi(dyv) : splat_lo(dyv);
-                    const h2 yy = r2nd ? splat_hi(dyy) : splat_lo(dyy);
-                    pq[k] = ((dx * dx) * splat_lo(cc) + yy) + (dx * dy) * splat_lo(oc);
-                }
+                // P = 1: one pair per lane
+                const h2 dx = X[0] - splat_lo(mean);
+                pq[0] = ((dx * dx) * splat_lo(cc) + splat_lo(dyy)) + (dx * splat_lo(dyv)) * splat_lo(oc);
             };
-            if (kLdsRecords) {
-                lrecA[wv][lane] = bA;
-                lrecB[wv][lane] = bB;
-                blend_wave_sync();
-            }
+            lrecA[wv][lane] = bA;
+            lrecB[wv][lane] = bB;
+            blend_wave_sync();
             // prime group 0
 #pragma unroll
             for (uint32_t k = 0; k < U; ++k) {
@@ -331,30 +317,20 @@ __global__ __launch_bounds__(NT) void k_blend_px(
                     // stage 1: the next group's table words go in flight (independent of T)
                     {
                         const bool nb = gi + 1 == NG;
-                        if (kLdsRecords && nb) {  // every entry of this batch was read: stage the next one
+                        if (nb) {  // every entry of this batch was read: stage the next one
                             lrecA[wv][lane] = nA;
                             lrecB[wv][lane] = nB;
                             blend_wave_sync();
                         }
-                        const uint32_t sx = nb ? nA.x : bA.x, sy = nb ? nA.y : bA.y;
-                        const uint32_t sz = nb ? nA.z : bA.z, sw = nb ? nA.w : bA.w;
-                        const uint32_t sb = nb ? nB : bB;
 #pragma unroll
                         for (uint32_t k = 0; k < U; ++k) {
                             const uint32_t j = ((gi + 1) * U + k) & 63u;
                             h2 pq[P];
-                            if (kLdsRecords) {
-                                const uint4 ra = lrecA[wv][j];
-                                opn[k] = ra.z;
-                                quadform(ra.x, ra.y, ra.z, pq);
-                                rgn[k] = ra.w;
-                                bdn[k] = lrecB[wv][j];
-                            } else {
-                                opn[k] = __builtin_amdgcn_readlane(sz, j);
-                                quadform(__builtin_amdgcn_readlane(sx, j), __builtin_amdgcn_readlane(sy, j), opn[k], pq);
-                                rgn[k] = __builtin_amdgcn_readlane(sw, j);
-                                bdn[k] = __builtin_amdgcn_readlane(sb, j);
-                            }
+                            const uint4 ra = lrecA[wv][j];
+                            opn[k] = ra.z;
+                            quadform(ra.x, ra.y, ra.z, pq);
+                            rgn[k] = ra.w;
+                            bdn[k] = lrecB[wv][j];
 #pragma unroll
                             for (int q = 0; q < P; ++q) {
                                 // raw table words: first used in stage 3, after the current

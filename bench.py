@@ -68,6 +68,9 @@ def parse():
                    help="DepthFirst RendererConfig.maxGaussians (reference default 6M -> 24M instances)")
     p.add_argument("--multi", choices=("alltoall", "replicas"), default="alltoall",
                    help="N>1 partition: all-to-all of projected records (8e) or projection replicas")
+    p.add_argument("--multi-extra-config", default="cfg3_5m_sh3_4k_f16",
+                   help="N>1: also time this config's frame on the N GPUs (BASELINE config 4: the 4K scene), "
+                        "reported under 'config4'; 'none' = off")
     a = p.parse_args()
     if a.traffic_json is None:
         a.traffic_json = os.path.join(ROOT, "profiles", f"{a.pmc_tag}_pmc_blend_{a.config.split('_')[0]}.json")
@@ -88,11 +91,17 @@ def main():
     # BENCH_DIST_BACKEND=gloo rehearses the N>1 protocol with several ranks on one GPU (CPU-staged
     # collectives; timings meaningless).  The driver's multi-GPU runs use RCCL ("nccl").
     backend = os.environ.get("BENCH_DIST_BACKEND", "nccl")
-    gpu = local_rank % max(1, torch.cuda.device_count()) if backend == "gloo" else local_rank
+    # BENCH_SAME_GPU=1 maps every rank onto the visible GPUs round robin with RCCL too: an N-rank
+    # rehearsal of the multi-GPU protocol (IPC receive buffers, RCCL collectives) on a one-GPU box
+    same_gpu = backend == "gloo" or os.environ.get("BENCH_SAME_GPU") == "1"
+    gpu = local_rank % max(1, torch.cuda.device_count()) if same_gpu else local_rank
     # BENCH_FORCE_MULTI=1 runs the N>1 code path (C-ABI multi-GPU frame over an RCCL communicator)
     # at world size 1 -- a one-GPU rehearsal of what the driver's 8-GPU runs execute
     force_multi = os.environ.get("BENCH_FORCE_MULTI") == "1"
     if world_size > 1 or force_multi:
+        if world_size == 1:  # plain `python bench.py`: a world of one without a launcher
+            for k, v in (("RANK", "0"), ("WORLD_SIZE", "1"), ("MASTER_ADDR", "127.0.0.1"), ("MASTER_PORT", "29533")):
+                os.environ.setdefault(k, v)
         torch.cuda.set_device(gpu)
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
@@ -139,11 +148,26 @@ def main():
     # (BENCH_DIST_BACKEND=gloo, several ranks on one GPU) has no RCCL communicator and moves the
     # records through gsm_amd.exchange instead.
     native_multi = alltoall and backend == "nccl"
+    multi_fallback = None
     if native_multi:
         full_c = torch.zeros((H, TW, 4), dtype=torch.float16, device=dev)  # rank 0: the gathered frame
         full_d = torch.zeros((H, TW), dtype=torch.float16, device=dev)
-        mg = gsm_amd.MultiGpuRenderer(renderer, gsm_amd.MultiGpuRenderer.torch_comm(gpu), rank, world_size)
-    elif alltoall:
+        mg = None
+        try:
+            mg = gsm_amd.MultiGpuRenderer(renderer, gsm_amd.MultiGpuRenderer.torch_comm(gpu), rank, world_size)
+        except gsm_amd.RendererError as e:  # e.g. IPC receive buffers that cannot be opened on this node
+            multi_fallback = f"rank {rank}: {e}"
+        # create is collective: every rank takes the native frame or none does
+        ok = torch.tensor([0 if mg is None else 1], dtype=torch.int32, device=dev)
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        if int(ok.item()) == 0:
+            if mg is not None:
+                mg.close()
+            native_multi = False
+            multi_fallback = multi_fallback or "another rank's gsm_multigpu_create failed"
+            print(f"bench: native multi-GPU frame unavailable ({multi_fallback}); "
+                  "records move through gsm_amd.exchange (RCCL all-to-all, host-read counts)", file=sys.stderr)
+    if alltoall and not native_multi:
         first, cnt = exchange.id_range(n, world_size, rank)
         rows = exchange.slab_rows(tiles_y, H, world_size)
         send_cap = max(cnt, 1) * world_size
@@ -226,6 +250,10 @@ def main():
             ref = O.render(world_np, harm_np, sh, cam_d, W, H, max_gaussians=n,
                            nthreads=max(1, min(args.cpu_threads, os.cpu_count() or 1)))
             multi_parity = bool(np.array_equal(full_c.view(torch.int16).cpu().numpy().view(np.uint16), ref["color"]))
+    # BASELINE config 4 (the 4K scene of config 3 on N GPUs): timed the same way after `value`
+    multi_4k = None
+    if native_multi and args.multi_extra_config not in ("", "none", args.config):
+        multi_4k = multi_extra_frame(args, gsm_amd, scenes, dev, gpu, rank, world_size)
     if native_multi:
         mg.close()
     if rank != 0:
@@ -359,10 +387,48 @@ def main():
         "orbit": orbit,
         "parity_vs_oracle": multi_parity if native_multi else parity,
     }
+    if multi_fallback:
+        out["multi_fallback"] = multi_fallback
+    if multi_4k:
+        out["config4"] = multi_4k
     print(json.dumps(out))
     renderer.close()
     if world_size > 1:
         dist.destroy_process_group()
+
+
+def multi_extra_frame(args, gsm_amd, scenes, dev, gpu, rank, world_size):
+    """BASELINE.json configs[3]: config 3's 4K scene partitioned over the N GPUs by tile-row slab
+    (gsm_multigpu_render), timed like `value` (barriers, max over ranks); rank 0 gathers the frame.
+    Parity of the partitioned frame is checked on the main config; this is a throughput line."""
+    import torch
+    c = scenes.CONFIGS[args.multi_extra_config]
+    n, W, H, sh, prec = c["count"], c["width"], c["height"], c["sh"], c["precision"]
+    world_np, harm_np, cam_d = scenes.gen_scene(n, W, H, sh, prec, seed=42)
+    world = torch.from_numpy(world_np.view(np.uint8).reshape(-1).copy()).to(dev)
+    harm = torch.from_numpy(harm_np.view(np.uint8).reshape(-1).copy()).to(dev)
+    del world_np, harm_np
+    cfg = gsm_amd.RendererConfig(max_gaussians=n, max_width=W, max_height=H, precision=prec,
+                                 gaussian_color_space=gsm_amd.GaussianColorSpace.LINEAR)
+    r = gsm_amd.GlobalRenderer(device=dev.index, config=cfg)
+    mg = gsm_amd.MultiGpuRenderer(r, gsm_amd.MultiGpuRenderer.torch_comm(gpu), rank, world_size)
+    full_c = torch.zeros((H, W, 4), dtype=torch.float16, device=dev)
+    full_d = torch.zeros((H, W), dtype=torch.float16, device=dev)
+    inp = gsm_amd.GaussianInput(world, harm, n, sh)
+    cam = gsm_amd.CameraParams.from_dict(cam_d)
+    stream = torch.cuda.current_stream(dev)
+
+    def step():
+        mg.render(full_c, full_d, inp, cam, W, H, gather=True, stream=stream)
+    for _ in range(3):
+        step()
+    steps = max(1, min(args.steps, 20))
+    elapsed, _ = timed_loop(steps, step, r, world_size, dev)
+    mg.close()
+    r.close()
+    return {"value": steps / elapsed, "unit": "frames/s", "n_gpus": world_size, "steps": steps, "warmup": 3,
+            "ms_per_step": elapsed / steps * 1e3, "workload": f"{args.multi_extra_config}: {n} gaussians "
+            f"{W}x{H} partitioned by tile-row slab over {world_size} GPUs (BASELINE config 4)"}
 
 
 def timed_loop(steps, step, renderer, world_size, dev):

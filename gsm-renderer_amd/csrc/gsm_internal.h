@@ -67,7 +67,7 @@ struct DeviceArena {
     unsigned long long* blendTrace = nullptr;  // [4 * tiles * 4] (profiling bit 2 only)
     uint32_t* costMax = nullptr;               // [kCostMaxSlots] longest walk of the last blend
     uint32_t* radixHist = nullptr;             // [256 * radixGrid]
-    uint32_t* radixBinTotals = nullptr;        // [256]
+    uint32_t* radixBinTotals = nullptr;        // [kSortTotalsWords] (radix_sort_tiles)
     uint32_t* tileStart = nullptr;             // [tileCount + 1] first sorted entry of each tile
     uint32_t* tileQueue = nullptr;             // [kQueueStripes * kQueueStride] blend work counters
     uint16_t* unitCost = nullptr;              // [4 * tileCount] list entries each blend unit walked
@@ -114,6 +114,10 @@ constexpr int kRadixBlock = 256;
 #endif
 constexpr int kRadixItems = GSM_RADIX_ITEMS;  // keys per thread per chunk (4096-key chunks)
 constexpr int kRadixChunk = kRadixBlock * kRadixItems;
+// radix_sort_tiles' digit totals (two passes, 256 words each) + the last pass's block table (one
+// uint4 per block, <= 1024 + 256 blocks)
+constexpr uint32_t kTileTableEntries = 1024 + 256;
+constexpr size_t kSortTotalsWords = 512 + 4 * (size_t)kTileTableEntries;
 
 // project + cull + SH + tile count + per-block count sums (GlobalShaders.metal:19-123, 563-616)
 void launch_project(bool halfInput, uint32_t shDegree, const void* world, const void* harmonics,
@@ -171,6 +175,11 @@ int radix_sort_pairs(uint32_t* keys[2], uint32_t* vals[2], const uint32_t* nPtr,
 int radix_sort_bits(uint32_t* keys[2], uint32_t* vals[2], const uint32_t* nPtr, uint32_t capacity,
                     uint32_t shift, uint32_t bits, uint32_t* hist, uint32_t* binTotals, hipStream_t stream,
                     bool ballot);
+// the frame sort's tile field (bits <= 16) with the tile starts written by its last pass
+// (tileStart[0..numTiles], lower bounds for empty tiles); binTotals: kSortTotalsWords words
+int radix_sort_tiles(uint32_t* keys[2], uint32_t* vals[2], const uint32_t* nPtr, uint32_t capacity, uint32_t shift,
+                     uint32_t bits, uint32_t* hist, uint32_t* binTotals, uint32_t* tileStart, uint32_t numTiles,
+                     hipStream_t stream, bool ballot);
 uint32_t radix_grid_for_capacity(uint32_t capacity);
 // bytes of the sort workspace (`hist` argument above) for a capacity; zero it once at allocation
 size_t radix_workspace_bytes(uint32_t capacity);

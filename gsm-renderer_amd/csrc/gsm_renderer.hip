@@ -114,7 +114,7 @@ gsm_status GlobalRenderer::create(const gsm_renderer_config& cfg, int hipDevice,
     GSM_ALLOC(A.radixHist, radix_workspace_bytes(r->maxAssignments_));
     if (st == GSM_OK && hipMemset(A.radixHist, 0, radix_workspace_bytes(r->maxAssignments_)) != hipSuccess)
         st = GSM_ERR_FAILED_TO_ALLOCATE_BUFFER;
-    GSM_ALLOC(A.radixBinTotals, 256 * sizeof(uint32_t));
+    GSM_ALLOC(A.radixBinTotals, kSortTotalsWords * sizeof(uint32_t));  // radix_sort_tiles: totals + block table
     GSM_ALLOC(A.tileStart, ((size_t)r->tileCount_ + 1) * sizeof(uint32_t));
     GSM_ALLOC(A.tileQueue, kQueueStripes * kQueueStride * sizeof(uint32_t));
     GSM_ALLOC(A.unitCost, (size_t)r->tileCount_ * 4 * sizeof(uint16_t));
@@ -409,7 +409,7 @@ gsm_status GlobalRenderer::runFrame(hipStream_t s, const ProjectArgs& a, uint32_
     g.height = height;
     g.maxAssignments = maxAssignments_;
     // Frame sort.  Default: a stable LSD sort by the tile field only
-    // (ceil(tileBits / 8) passes), tile starts from the runs, then each tile's run sorted
+    // (ceil(tileBits / 8) passes, the last one writing the tile starts), then each tile's run sorted
     // stably by depth by one wave in LDS -- the same order as the reference's 4-pass sort of
     // (tile << 16 | depth) keys.  Tuning::fullRadix keeps the 4 full 8-bit passes (A/B).
     const bool fullRadix = tuning_.fullRadix;
@@ -417,9 +417,10 @@ gsm_status GlobalRenderer::runFrame(hipStream_t s, const ProjectArgs& a, uint32_
     if (!fullRadix) {
         uint32_t tileBits = 1;
         while (tileBits < 16 && (tileCount_ - 1u) >> tileBits) tileBits++;
-        const int res = radix_sort_bits(kb, vb, &arena_.header->totalAssignments, maxAssignments_, 16, tileBits,
-                                        arena_.radixHist, arena_.radixBinTotals, s, ballot);
-        launch_headers(kb[res], g, arena_, s);
+        // the last tile pass also writes the tile starts (radix_sort_tiles: no pass over the keys)
+        const int res = radix_sort_tiles(kb, vb, &arena_.header->totalAssignments, maxAssignments_, 16, tileBits,
+                                         arena_.radixHist, arena_.radixBinTotals, arena_.tileStart, tileCount_, s,
+                                         ballot);
         tile_depth_sort(kb[res], vb[res], kb[res ^ 1], vb[res ^ 1], arena_.tileStart, rowBegin_ * tilesX_,
                         (rowEnd_ - rowBegin_) * tilesX_, s, ballot, arena_.halfVals[0], arena_.halfVals[1],
                         arena_.halfCount, tileCount_, capture, numCUs_);

@@ -145,7 +145,7 @@ gsm_status DepthFirstRenderer::create(const gsm_renderer_config& cfg, int hipDev
     if (st == GSM_OK &&
         hipMemset(A.radixHist, 0, radix_workspace_bytes(r->maxInstances_ > r->maxGaussians_ ? r->maxInstances_ : r->maxGaussians_)) != hipSuccess)
         st = GSM_ERR_FAILED_TO_ALLOCATE_BUFFER;
-    GSM_DF_ALLOC(A.radixBinTotals, 256 * 4);
+    GSM_DF_ALLOC(A.radixBinTotals, kSortTotalsWords * 4);  // radix_sort_tiles: totals + block table
     GSM_DF_ALLOC(A.starts, ((size_t)r->maxTiles_ + 1) * sizeof(uint32_t));
     GSM_DF_ALLOC(A.queue, kQueueStripes * kQueueStride * sizeof(uint32_t));
     GSM_DF_ALLOC(A.expTable, 65536 * 2);
@@ -267,9 +267,9 @@ gsm_status DepthFirstRenderer::renderStereoSbs(hipStream_t s, const gsm_gaussian
     // TileSortEncoder (DepthFirstRenderer.swift:683-768): stable sort by the 16-bit tile id
     uint32_t tileBits = 0;
     while (tileBits < 16 && ((a.tileCount - 1u) >> tileBits)) tileBits++;
-    const int ic = radix_sort_bits(A_.ikeys, A_.ivals, &A_.instHdr->totalAssignments, maxInstances_, 0, tileBits,
-                                   A_.radixHist, A_.radixBinTotals, s, tuning_.ballotRank);
-    df_launch_ranges(A_.ikeys[ic], a, A_, s);
+    // the last pass also writes the tile ranges' starts (radix_sort_tiles: no pass over the instances)
+    const int ic = radix_sort_tiles(A_.ikeys, A_.ivals, &A_.instHdr->totalAssignments, maxInstances_, 0, tileBits,
+                                    A_.radixHist, A_.radixBinTotals, A_.starts, a.tileCount, s, tuning_.ballotRank);
     // Blend schedule: (tile, eye) units handed out longest first by the walk lengths the previous
     // frame of the same geometry measured (the image does not depend on the order, only the load
     // balance does).  Tuning::costOrder false (GSM_BLEND_SCHED=0 at create): index order.

@@ -76,7 +76,6 @@ void df_launch_compact(const DfArgs& a, const DfArena& A, hipStream_t stream);
 void df_launch_instance_counts(const uint32_t* order, const DfArgs& a, const DfArena& A, hipStream_t stream);
 void df_launch_instances(const uint32_t* order, const DfArgs& a, const DfArena& A, hipStream_t stream);
 // extractTileRangesKernel (:1258-1313)
-void df_launch_ranges(const uint32_t* sortedTiles, const DfArgs& a, const DfArena& A, hipStream_t stream);
 // clearStereoRenderTextureKernel + depthFirstStereoRender + DepthFirstStereoCopyEncoder
 // (:1813-1982; DepthFirstStereoCopyEncoder.swift:29-99) in one persistent kernel
 // costOrder: hand the units out longest-last-frame-walk first (A.unitOrder, filled by block 0 of

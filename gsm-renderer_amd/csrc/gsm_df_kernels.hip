@@ -5,7 +5,8 @@
 // Frame: project both eyes once per gaussian (k_df_project) -> compact the visible ones with
 // their 32-bit depth keys (k_df_compact) -> stable LSD depth sort (gsm_sort.hip) -> per-gaussian
 // tile counts in depth order, scan, instance expansion of the union rect (k_df_icount,
-// k_df_expand) -> stable LSD sort by tile id -> tile ranges (k_df_starts) -> one persistent
+// k_df_expand) -> stable LSD sort by tile id, its last pass writing the tile ranges
+// (radix_sort_tiles) -> one persistent
 // blend kernel that clears, composites each (tile, eye) of 16x16 pixels and writes the two eyes
 // side by side with the copy pass's row flip (k_df_blend_eye).
 // Numeric contract: DESIGN.md (built with -ffp-contract=off, IEEE div/sqrt); bit-exact with
@@ -371,33 +372,11 @@ __global__ __launch_bounds__(kDfBlock) void k_df_expand(const TileAssignmentHead
 
 // ---------------------------------------------------------------------------
 // 4. tile ranges (extractTileRangesKernel, DepthFirstShaders.metal:1258-1313): the reference's two
-//    binary searches per tile become the run starts of the sorted tile ids; header t is
-//    {starts[t], starts[t + 1] - starts[t]} -- the lower bound for an empty tile, {0, 0} for an
-//    empty frame (the debug copy rebuilds the reference's GaussianHeader array from them)
+//    binary searches per tile become the tile starts the sort's last pass writes (radix_sort_tiles,
+//    gsm_sort.hip); header t is {starts[t], starts[t + 1] - starts[t]} -- the lower bound for an
+//    empty tile, {0, 0} for an empty frame (the debug copy rebuilds the reference's GaussianHeader
+//    array from them)
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_df_starts(const uint32_t* __restrict__ tiles,
-                                                   const TileAssignmentHeader* __restrict__ instHdr,
-                                                   uint32_t tileCount, uint32_t* __restrict__ starts) {
-    // one pass over the tile-sorted instances: starts[t] = first position whose tile is >= t
-    // (the reference's lower bound, so an empty tile gets the position of the next run), for
-    // t = 0 .. tileCount; 4 positions per thread and step
-    const uint32_t total = instHdr->totalAssignments;
-    const uint32_t stride = gridDim.x * 256u * 4u;
-    for (uint32_t i0 = (blockIdx.x * 256u + threadIdx.x) * 4u; i0 <= total; i0 += stride) {
-        uint32_t k[5];
-        k[0] = i0 == 0 ? 0u : tiles[i0 - 1];
-#pragma unroll
-        for (uint32_t j = 0; j < 4; ++j) k[j + 1] = i0 + j < total ? tiles[i0 + j] : 0u;
-#pragma unroll
-        for (uint32_t j = 0; j < 4; ++j) {
-            const uint32_t i = i0 + j;
-            if (i > total) break;
-            const uint32_t first = i == 0 ? 0u : k[j] + 1u;
-            const uint32_t cur = i == total ? tileCount : min(k[j + 1], tileCount);
-            for (uint32_t t = first; t <= cur; ++t) starts[t] = i;
-        }
-    }
-}
 
 // ---------------------------------------------------------------------------
 // 5. blend (clearStereoRenderTextureKernel :1813-1823, depthFirstStereoRender :1825-1982) and the
@@ -754,12 +733,6 @@ void df_launch_instances(const uint32_t* order, const DfArgs& a, const DfArena& 
     if (blocks == 0) return;
     hipLaunchKernelGGL(k_df_expand, dim3(blocks), dim3(kDfBlock), 0, s, A.visHdr, order, A.touched, A.bounds,
                        A.instSums, A.renderData, a.maxInstances, a.tilesX, A.ikeys[0], A.ivals[0]);
-}
-
-void df_launch_ranges(const uint32_t* sortedTiles, const DfArgs& a, const DfArena& A, hipStream_t s) {
-    uint32_t blocks = (a.maxInstances + 1u + 1023u) / 1024u;  // grid-stride over the device-side total
-    if (blocks > 4096u) blocks = 4096u;
-    hipLaunchKernelGGL(k_df_starts, dim3(blocks), dim3(256), 0, s, sortedTiles, A.instHdr, a.tileCount, A.starts);
 }
 
 constexpr int kDfBlendWaves = 16;

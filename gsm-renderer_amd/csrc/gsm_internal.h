@@ -114,10 +114,8 @@ constexpr int kRadixBlock = 256;
 #endif
 constexpr int kRadixItems = GSM_RADIX_ITEMS;  // keys per thread per chunk (4096-key chunks)
 constexpr int kRadixChunk = kRadixBlock * kRadixItems;
-// radix_sort_tiles' digit totals (two passes, 256 words each) + the last pass's block table (one
-// uint4 per block, <= 1024 + 256 blocks)
-constexpr uint32_t kTileTableEntries = 1024 + 256;
-constexpr size_t kSortTotalsWords = 512 + 4 * (size_t)kTileTableEntries;
+// radix_sort_tiles' workspace beside the histogram: two passes' digit totals + the bucket starts
+constexpr size_t kSortTotalsWords = 768;
 
 // project + cull + SH + tile count + per-block count sums (GlobalShaders.metal:19-123, 563-616)
 void launch_project(bool halfInput, uint32_t shDegree, const void* world, const void* harmonics,

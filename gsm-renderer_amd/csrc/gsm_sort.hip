@@ -70,179 +70,17 @@ __device__ __forceinline__ uint32_t wave_rank(uint32_t* cnt, uint32_t d, bool va
     }
 }
 
-// ---------------------------------------------------------------------------
-// Tile starts from the sort itself (radix_sort_tiles).  The frame sort's keys are tile << 16 |
-// depth; its passes sort the tile field, low digit first.  In the last pass the blocks do not
-// split the keys evenly: they cover the buckets the previous pass left (bucket l = the run of keys
-// whose low digit is l, in order), per keys each, so no block straddles two buckets.  The first
-// block of bucket l then starts digit h's output at exactly the keys < (h, l) -- all keys of high
-// digits < h plus those of digit h in buckets < l, the blocks before it -- which is the first
-// position of tile (h << lowBits | l), or its lower bound when the tile is empty.  That block
-// writes the start of every tile of its bucket (and of the empty buckets before it), the last
-// block those of the empty buckets after the last one: the k_tile_starts pass over all keys goes.
-// With one pass there is one bucket (every key), lowBits = 0.
-struct TileStarts {
-    const uint32_t* bucketCnt;  // [1 << lowBits] keys per bucket: the previous pass's digit totals
-    uint32_t lowBits;           // bits of the previous passes (the low tile digit)
-    uint32_t baseGrid;          // blocks an even split would use (radix_grid_for_capacity)
-    uint32_t numTiles;
-    uint32_t* tileStart;        // [numTiles + 1]
-    // the last pass's block table {begin, end, bucket | first << 16 | last << 17, prev}: written by
-    // block 0 of the previous pass's downsweep (it scans the digit totals anyway), so a block of the
-    // last pass reads one entry instead of scanning the buckets itself; null with one pass
-    uint4* table;
-};
-
-struct BucketBlock {
-    uint32_t begin, end;  // this block's keys
-    uint32_t bucket;      // their low digit
-    uint32_t prev;        // first bucket whose tile starts this block writes (first blocks)
-    bool first, last;     // first block of its bucket / last block holding keys
-};
-
-// Exclusive scan over the 256 threads of a block (part: kWaves words of LDS); *total = the sum.
-__device__ __forceinline__ uint32_t radix_block_scan(uint32_t v, uint32_t* part, uint32_t* total) {
-    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
-    uint32_t inc = v;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t x = __shfl_up(inc, o, 64);
-        if (lane >= (uint32_t)o) inc += x;
-    }
-    if (lane == 63) part[wave] = inc;
-    __syncthreads();
-    uint32_t off = 0, tot = 0;
-#pragma unroll
-    for (int w = 0; w < kWaves; ++w) {
-        if ((uint32_t)w < wave) off += part[w];
-        tot += part[w];
-    }
-    __syncthreads();
-    *total = tot;
-    return off + inc - v;
-}
-
-// Every thread gets block b's range.  Thread t < 2^lowBits handles bucket t (lowBits <= 8).  The
-// blocks are the pieces of the even split [k * per, (k + 1) * per) cut at the bucket boundaries,
-// so every block but a bucket's first starts on a chunk boundary (aligned loads) and the pieces
-// number at most baseGrid + buckets.
-__device__ BucketBlock bucket_block(const TileStarts& ts, const uint32_t* nPtr, uint32_t b, uint32_t* sCnt,
-                                    uint32_t* sPart, uint32_t* sRes) {
-    const uint32_t L = 1u << ts.lowBits, tid = threadIdx.x;
-    const uint32_t n = *nPtr;
-    if (ts.table) {  // the previous pass's block 0 laid the blocks out (write_block_table)
-        BucketBlock r{};
-        if (n == 0u) return r;
-        const uint4 e = ts.table[b];
-        r.begin = e.x;
-        r.end = e.y;
-        r.bucket = e.z & 0xFFFFu;
-        r.first = (e.z >> 16) & 1u;
-        r.last = (e.z >> 17) & 1u;
-        r.prev = e.w;
-        return r;
-    }
-    uint32_t per = (n + ts.baseGrid - 1u) / ts.baseGrid;
-    per = per ? (per + kRadixChunk - 1u) / kRadixChunk * kRadixChunk : kRadixChunk;
-    const uint32_t c = tid < L ? (L == 1u ? n : ts.bucketCnt[tid]) : 0u;
-    sCnt[tid] = c;
-    if (tid == 0) sRes[0] = sRes[1] = sRes[2] = sRes[3] = 0u;
-    uint32_t total, nbTotal;
-    const uint32_t cEx = radix_block_scan(c, sPart, &total);
-    const uint32_t k0 = cEx / per;
-    const uint32_t nb = c ? (cEx + c + per - 1u) / per - k0 : 0u;
-    const uint32_t bEx = radix_block_scan(nb, sPart, &nbTotal);
-    if (nb && b >= bEx && b < bEx + nb) {
-        const uint32_t k = k0 + (b - bEx);
-        sRes[0] = max(cEx, k * per);
-        sRes[1] = min(cEx + c, (k + 1u) * per);
-        sRes[2] = tid;
-        sRes[3] = b == bEx ? 1u : 0u;
-    }
-    __syncthreads();
-    BucketBlock r;
-    r.begin = sRes[0];
-    r.end = sRes[1];
-    r.bucket = sRes[2];
-    r.first = sRes[3] != 0u;
-    r.last = nbTotal > 0u && b == nbTotal - 1u;
-    r.prev = r.bucket;
-    if (r.first)
-        while (r.prev > 0u && sCnt[r.prev - 1u] == 0u) r.prev--;
-    return r;
-}
-
-// Block 0 of the first tile pass's downsweep: the last pass's blocks (bucket_block's layout) from
-// this pass's digit totals.  tid = bucket (R buckets), c its keys, cEx the keys before it.
-__device__ void write_block_table(const TileStarts& ts, uint32_t R, uint32_t n, uint32_t c, uint32_t cEx,
-                                  uint32_t* part) {
-    const uint32_t tid = threadIdx.x, grid = ts.baseGrid + R;
-    uint32_t per = (n + ts.baseGrid - 1u) / ts.baseGrid;
-    per = per ? (per + kRadixChunk - 1u) / kRadixChunk * kRadixChunk : kRadixChunk;
-    const uint32_t k0 = cEx / per;
-    const uint32_t nb = (tid < R && c) ? (cEx + c + per - 1u) / per - k0 : 0u;
-    uint32_t nbTotal;
-    const uint32_t bEx = radix_block_scan(nb, part, &nbTotal);
-    // the nonempty bucket before this one: its tiles' starts come from this bucket's first block
-    part[2 * kWaves + (tid & 255u)] = c;  // reuse: bucket counts (R <= 256)
-    __syncthreads();
-    uint32_t prev = tid;
-    if (nb)
-        while (prev > 0u && part[2 * kWaves + prev - 1u] == 0u) prev--;
-    for (uint32_t j = 0; j < nb; ++j) {
-        const uint32_t k = k0 + j, b = bEx + j;
-        ts.table[b] = make_uint4(max(cEx, k * per), min(cEx + c, (k + 1u) * per),
-                                 tid | (j == 0u ? 1u << 16 : 0u) | (b == nbTotal - 1u ? 1u << 17 : 0u), prev);
-    }
-    for (uint32_t b = nbTotal + tid; b < grid; b += kRadixBlock) ts.table[b] = make_uint4(0u, 0u, 0u, 0u);
-}
-
-template <int BITS, bool BUCKETED>
+template <int BITS>
 __global__ __launch_bounds__(kRadixBlock) void k_radix_upsweep(const uint32_t* __restrict__ keys,
                                                                const uint32_t* __restrict__ nPtr,
                                                                uint32_t shift,
-                                                               uint32_t* __restrict__ hist,
-                                                               TileStarts ts) {
+                                                               uint32_t* __restrict__ hist) {
     constexpr uint32_t R = 1u << BITS;
     __shared__ uint32_t cnt[kWaves][R];
     const uint32_t wave = threadIdx.x >> 6;
     for (int i = threadIdx.x; i < kWaves * (int)R; i += kRadixBlock) (&cnt[0][0])[i] = 0;
     __syncthreads();
     uint32_t begin, end;
-    if constexpr (BUCKETED) {
-        __shared__ uint32_t sCnt[kRadixBlock], sPart[2 * kWaves], sRes[4];
-        const BucketBlock bb = bucket_block(ts, nPtr, blockIdx.x, sCnt, sPart, sRes);
-        begin = bb.begin;
-        end = bb.end;
-        // a bucket's first block starts anywhere: 16-byte loads from the aligned position before
-        // it, keys outside [begin, end) not counted
-        for (uint32_t cbase = begin & ~3u; cbase < end; cbase += kRadixChunk) {
-            uint4 q[kRadixItems / 4];
-#pragma unroll
-            for (int i = 0; i < kRadixItems / 4; ++i) {
-                const uint32_t idx = cbase + (uint32_t)(i * kRadixBlock + threadIdx.x) * 4u;
-                q[i] = idx + 3u < end ? *(const uint4*)(keys + idx)
-                                      : make_uint4(idx < end ? keys[idx] : 0u, idx + 1u < end ? keys[idx + 1u] : 0u,
-                                                   idx + 2u < end ? keys[idx + 2u] : 0u, 0u);
-            }
-#pragma unroll
-            for (int i = 0; i < kRadixItems / 4; ++i) {
-                const uint32_t idx = cbase + (uint32_t)(i * kRadixBlock + threadIdx.x) * 4u;
-                const uint32_t kk[4] = {q[i].x, q[i].y, q[i].z, q[i].w};
-#pragma unroll
-                for (uint32_t c = 0; c < 4; ++c)
-                    if (idx + c >= begin && idx + c < end) atomicAdd(&cnt[wave][(kk[c] >> shift) & (R - 1u)], 1u);
-            }
-        }
-        __syncthreads();
-        for (uint32_t d = threadIdx.x; d < R; d += kRadixBlock) {
-            uint32_t s = 0;
-#pragma unroll
-            for (int w = 0; w < kWaves; ++w) s += cnt[w][d];
-            hist[(size_t)d * gridDim.x + blockIdx.x] = s;
-        }
-        return;
-    }
     block_range(*nPtr, gridDim.x, blockIdx.x, &begin, &end);
     // a chunk's keys are all loaded before any is counted (16 loads in flight per thread);
     // order does not matter for a histogram, so they come as 16-byte vectors
@@ -274,21 +112,17 @@ __global__ __launch_bounds__(kRadixBlock) void k_radix_upsweep(const uint32_t* _
 }
 
 // One workgroup per digit: exclusive scan of hist[d][0..grid) in place, digit total out.
-// grid <= kScanCols, so every thread holds at most 8 entries in registers (one read, one write).
-constexpr uint32_t kScanPer = 8, kScanCols = 256 * kScanPer;
+// grid <= 1024, so every thread holds at most 4 entries in registers (one read, one write).
 __global__ __launch_bounds__(256) void k_radix_scan(uint32_t* __restrict__ hist, uint32_t grid,
                                                     uint32_t* __restrict__ binTotals) {
     __shared__ uint32_t part[4];
     const uint32_t d = blockIdx.x;
     uint32_t* row = hist + (size_t)d * grid;
-    const uint32_t b0 = threadIdx.x * kScanPer;
-    uint32_t v[kScanPer];
-    uint32_t local = 0;
+    const uint32_t b0 = threadIdx.x * 4u;
+    uint32_t v[4];
 #pragma unroll
-    for (uint32_t i = 0; i < kScanPer; ++i) {
-        v[i] = b0 + i < grid ? row[b0 + i] : 0u;
-        local += v[i];
-    }
+    for (int i = 0; i < 4; ++i) v[i] = b0 + i < grid ? row[b0 + i] : 0u;
+    const uint32_t local = v[0] + v[1] + v[2] + v[3];
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     uint32_t inc = local;
 #pragma unroll
@@ -306,7 +140,7 @@ __global__ __launch_bounds__(256) void k_radix_scan(uint32_t* __restrict__ hist,
     }
     uint32_t run = off + inc - local;
 #pragma unroll
-    for (uint32_t i = 0; i < kScanPer; ++i)
+    for (int i = 0; i < 4; ++i)
         if (b0 + i < grid) {
             row[b0 + i] = run;
             run += v[i];
@@ -314,8 +148,30 @@ __global__ __launch_bounds__(256) void k_radix_scan(uint32_t* __restrict__ hist,
     if (threadIdx.x == 0) binTotals[d] = tot;
 }
 
+// ---------------------------------------------------------------------------
+// Tile starts from the sort itself (radix_sort_tiles).  The frame sort's keys are tile << 16 |
+// depth (the DepthFirst instance keys: the tile alone); its passes sort the tile field, low digit
+// first.  The first pass leaves buckets: bucket l = the run of keys whose low digit is l, starting
+// at bucketStart[l] (block 0 of that pass writes these, the exclusive scan of its digit totals).
+// In the last pass, the keys of bucket l that precede digit h's output are exactly those of tile
+// (h << lowBits | l)'s predecessors: all keys of high digits < h and the keys of digit h in
+// buckets < l.  So where a block's chunk holds the start p of bucket l, the start of tile
+// (h, l) is digit h's output base at that chunk plus the chunk's keys of digit h before p (counted
+// again from the chunk's keys, still in L2, in the few chunks that hold a bucket start) -- a lower
+// bound also when the tile is empty.  The block holding p = bucketStart[l] writes the
+// starts of every tile of bucket l; the last block those of the empty buckets at the end
+// (bucketStart = n); no separate pass over the sorted keys.  One pass: one bucket, lowBits = 0.
+struct TileStarts {
+    const uint32_t* bucketStart;  // [1 << lowBits] (null with one pass: the single bucket starts at 0)
+    uint32_t* bucketStartOut;     // first pass: written by its block 0
+    uint32_t lowBits;             // bits of the first pass (the low tile digit)
+    uint32_t numTiles;
+    uint32_t* tileStart;          // [numTiles + 1]
+};
+
 // Digits >= 2^BITS do not exist: their counters stay 0 (thread tid owns digit tid of 256).
-template <int BITS, bool BALLOT, bool BUCKETED>
+// STARTS: the last pass of radix_sort_tiles (tile starts written, see TileStarts).
+template <int BITS, bool BALLOT, bool STARTS>
 __global__ __launch_bounds__(kRadixBlock) void k_radix_downsweep(
     const uint32_t* __restrict__ keysIn, const uint32_t* __restrict__ valsIn,
     uint32_t* __restrict__ keysOut, uint32_t* __restrict__ valsOut, const uint32_t* __restrict__ nPtr,
@@ -329,21 +185,21 @@ __global__ __launch_bounds__(kRadixBlock) void k_radix_downsweep(
     __shared__ uint32_t sVals[kRadixChunk];
     __shared__ uint32_t part[kWaves];
 
+    // STARTS: the chunk's keys per digit before a bucket start (1 << BITS words: with the arrays
+    // above, 4 blocks per CU still fit for BITS <= 7)
+    __shared__ uint32_t sCntB[1u << BITS];
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint32_t n = *nPtr;
     uint32_t begin, end;
-    BucketBlock bb{};
-    if constexpr (BUCKETED) {
-        __shared__ uint32_t sCnt[kRadixBlock], sPart[2 * kWaves], sRes[4];
-        bb = bucket_block(ts, nPtr, blockIdx.x, sCnt, sPart, sRes);
-        begin = bb.begin;
-        end = bb.end;
-        if (n == 0u && blockIdx.x == 0)  // no keys: every tile starts (and ends) at 0
-            for (uint32_t t = tid; t <= ts.numTiles; t += kRadixBlock) ts.tileStart[t] = 0u;
-    } else {
-        block_range(n, gridDim.x, blockIdx.x, &begin, &end);
-    }
+    block_range(n, gridDim.x, blockIdx.x, &begin, &end);
+    if (STARTS && n == 0u && blockIdx.x == 0)  // no keys: every tile starts (and ends) at 0
+        for (uint32_t t = tid; t <= ts.numTiles; t += kRadixBlock) ts.tileStart[t] = 0u;
     if (begin >= end) return;
+    const uint32_t L = 1u << ts.lowBits;
+    // STARTS: bucket l's start (uniform l: a scalar load); the first bucket not yet handled
+    auto bucketAt = [&](uint32_t l) -> uint32_t { return ts.bucketStart ? ts.bucketStart[l] : 0u; };
+    uint32_t nextL = 0;  // (starts are non-decreasing: the earlier blocks' buckets come first)
+    if (STARTS) nextL = (uint32_t)__syncthreads_count(tid < L && bucketAt(tid) < begin);
 
     // global base of every digit for this block: exclusive scan over digits + block column offset
     {
@@ -361,38 +217,52 @@ __global__ __launch_bounds__(kRadixBlock) void k_radix_downsweep(
         for (int w = 0; w < kWaves; ++w)
             if ((uint32_t)w < wave) off += part[w];
         binBase[tid] = off + inc - t + (tid < R ? hist[(size_t)tid * gridDim.x + blockIdx.x] : 0u);
+        // first pass of radix_sort_tiles: its digits are the last pass's buckets
+        if (!STARTS && ts.bucketStartOut && blockIdx.x == 0 && tid < R) ts.bucketStartOut[tid] = off + inc - t;
 #pragma unroll
         for (int w = 0; w < kWaves; ++w) waveCnt[w][tid] = 0;
-        if (!BUCKETED && ts.table && blockIdx.x == 0) {  // first tile pass: lay out the last pass's blocks
-            __shared__ uint32_t tpart[2 * kWaves + 256];
-            write_block_table(ts, R, n, t, off + inc - t, tpart);
-        }
-        if (BUCKETED && bb.first && tid < R)  // tiles (tid, l) of this bucket and the empty ones before it
-            for (uint32_t l = bb.prev; l <= bb.bucket; ++l) {
-                const uint32_t t = (tid << ts.lowBits) | l;
-                if (t <= ts.numTiles) ts.tileStart[t] = binBase[tid];
-            }
         __syncthreads();
     }
 
     const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-    // chunks start on 64-key boundaries (a bucket's first block: keys before begin are not its own)
-    const uint32_t abegin = BUCKETED ? (begin & ~63u) : begin;
-    for (uint32_t cbase = abegin; cbase < end; cbase += kRadixChunk) {
+    for (uint32_t cbase = begin; cbase < end; cbase += kRadixChunk) {
         uint32_t k[kRadixItems], v[kRadixItems], rank[kRadixItems];
+        // STARTS: the first bucket start p0 in this chunk, at item jp, lane lp of wave wp
+        uint32_t p0 = ~0u, wp = ~0u, jp = 0, lp = 0;
+        if constexpr (STARTS) {
+            if (nextL < L && bucketAt(nextL) < cbase + min((uint32_t)kRadixChunk, end - cbase)) {
+                p0 = bucketAt(nextL);
+                const uint32_t r = p0 - cbase;
+                wp = r / (64u * kRadixItems);
+                jp = (r / 64u) % kRadixItems;
+                lp = r % 64u;
+            }
+        }
         // wave w owns elements [cbase + w*64*items, +64*items): item j at + j*64 + lane (index order)
 #pragma unroll
         for (int j = 0; j < kRadixItems; ++j) {
             const uint32_t idx = cbase + wave * (64 * kRadixItems) + j * 64 + lane;
-            const bool valid = idx < end && (!BUCKETED || idx >= begin);
+            const bool valid = idx < end;
             k[j] = valid ? keysIn[idx] : 0xFFFFFFFFu;
             v[j] = valid ? valsIn[idx] : 0u;
         }
 #pragma unroll
         for (int j = 0; j < kRadixItems; ++j) {
             const uint32_t idx = cbase + wave * (64 * kRadixItems) + j * 64 + lane;
-            const bool valid = idx < end && (!BUCKETED || idx >= begin);
+            const bool valid = idx < end;
             const uint32_t d = (k[j] >> shift) & (R - 1u);
+            if (STARTS && wave == wp && (uint32_t)j == jp) {
+                // the wave's digit counts before p0: its counters before item jp (LDS operations of
+                // a wave complete in order) plus item jp's lanes before lp
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                for (uint32_t q = lane; q < R; q += 64u) sCntB[q] = waveCnt[wave][q];
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                if (valid && lane < lp) atomicAdd(&sCntB[d], 1u);
+            }
             rank[j] = wave_rank<BITS, BALLOT>(waveCnt[wave], d, valid, lt);
         }
         __syncthreads();
@@ -424,7 +294,7 @@ __global__ __launch_bounds__(kRadixBlock) void k_radix_downsweep(
 #pragma unroll
         for (int j = 0; j < kRadixItems; ++j) {
             const uint32_t idx = cbase + wave * (64 * kRadixItems) + j * 64 + lane;
-            if (idx < end && (!BUCKETED || idx >= begin)) {
+            if (idx < end) {
                 const uint32_t d = (k[j] >> shift) & (R - 1u);
                 const uint32_t pos = localStart[d] + waveCnt[wave][d] + rank[j];
                 sKeys[pos] = k[j];
@@ -432,7 +302,34 @@ __global__ __launch_bounds__(kRadixBlock) void k_radix_downsweep(
             }
         }
         __syncthreads();
-        const uint32_t cn = min((uint32_t)kRadixChunk, end - cbase) - (BUCKETED && cbase < begin ? begin - cbase : 0u);
+        const uint32_t cn = min((uint32_t)kRadixChunk, end - cbase);
+        if constexpr (STARTS) {  // buckets starting in this chunk (uniform; most chunks have none)
+            if (p0 != ~0u) {  // at p0: the earlier waves' keys of digit h plus wave wp's before p0
+                do {          // (empty buckets share their successor's start)
+                    const uint32_t tt = (tid << ts.lowBits) | nextL;
+                    if (tid < R && tt <= ts.numTiles)
+                        ts.tileStart[tt] = binBase[tid] + waveCnt[wp][tid] + sCntB[tid];
+                    ++nextL;
+                } while (nextL < L && bucketAt(nextL) == p0);
+                __syncthreads();
+            }
+            // further starts in the same chunk (small buckets): count the keys before them again
+            while (nextL < L && bucketAt(nextL) < cbase + cn) {
+                const uint32_t p = bucketAt(nextL);
+                if (tid < R) sCntB[tid] = 0u;
+                __syncthreads();
+                // the chunk's keys before p per digit (the keys are still in L2)
+                for (uint32_t i = cbase + tid; i < p; i += kRadixBlock)
+                    atomicAdd(&sCntB[(keysIn[i] >> shift) & (R - 1u)], 1u);
+                __syncthreads();
+                do {  // every bucket starting at p (empty buckets share their successor's start)
+                    const uint32_t tt = (tid << ts.lowBits) | nextL;
+                    if (tid < R && tt <= ts.numTiles) ts.tileStart[tt] = binBase[tid] + sCntB[tid];
+                    ++nextL;
+                } while (nextL < L && bucketAt(nextL) == p);
+                __syncthreads();
+            }
+        }
         for (uint32_t p = tid; p < cn; p += kRadixBlock) {
             const uint32_t key = sKeys[p];
             const uint32_t d = (key >> shift) & (R - 1u);
@@ -446,54 +343,53 @@ __global__ __launch_bounds__(kRadixBlock) void k_radix_downsweep(
         for (int w = 0; w < kWaves; ++w) waveCnt[w][tid] = 0;
         __syncthreads();
     }
-    if (BUCKETED && bb.last) {  // binBase[h] now = the keys of high digits <= h: tiles past the last bucket
-        if (tid < R)
-            for (uint32_t l = bb.bucket + 1u; l < (1u << ts.lowBits); ++l) {
-                const uint32_t t = (tid << ts.lowBits) | l;
-                if (t <= ts.numTiles) ts.tileStart[t] = binBase[tid];
+    if (STARTS && end == n) {  // the last block: binBase[h] = the keys of high digits <= h; the
+        if (tid < R)           // buckets left start at n (empty)
+            for (uint32_t l = nextL; l < L; ++l) {
+                const uint32_t tt = (tid << ts.lowBits) | l;
+                if (tt <= ts.numTiles) ts.tileStart[tt] = binBase[tid];
             }
         if (tid == 0) ts.tileStart[ts.numTiles] = n;
     }
 }
 
 size_t radix_workspace_bytes(uint32_t capacity) {
-    (void)capacity;  // per-block digit counts: <= kScanCols blocks x 256 digits
-    return (size_t)256 * kScanCols * sizeof(uint32_t);
+    (void)capacity;  // per-block digit counts: <= 1024 blocks x 256 digits
+    return (size_t)256 * 1024 * sizeof(uint32_t);
 }
 
 uint32_t radix_grid_for_capacity(uint32_t capacity) {
-    // <= 1024 blocks, so a bucketed pass (radix_sort_tiles: + up to 256 buckets) stays within the
-    // kScanCols columns k_radix_scan holds in registers
+    // <= 1024 blocks: k_radix_scan holds a digit's column in 4 registers per thread
     uint32_t g = (capacity + kRadixChunk - 1) / kRadixChunk;
     if (g > 1024) g = 1024;
     if (g < 1) g = 1;
     return g;
 }
 
-// one LSD pass; with ts (radix_sort_tiles' last pass) the blocks cover the previous pass's buckets
-// and the downsweep writes the tile starts (grid = ts->baseGrid + buckets)
+// one LSD pass; ts: a pass of radix_sort_tiles (its first writes the bucket starts, its last --
+// starts = true -- the tile starts)
 static void radix_pass(uint32_t* kin, uint32_t* vin, uint32_t* kout, uint32_t* vout, const uint32_t* nPtr,
                        uint32_t grid, uint32_t shift, int bits, uint32_t* hist, uint32_t* binTotals,
-                       hipStream_t s, bool ballot, const TileStarts* ts = nullptr, bool bucketed = true) {
+                       hipStream_t s, bool ballot, const TileStarts* ts = nullptr, bool starts = false) {
     const TileStarts t = ts ? *ts : TileStarts{};
-#define GSM_RADIX_PASS(B, K)                                                                                  \
-    hipLaunchKernelGGL((k_radix_upsweep<B, K>), dim3(grid), dim3(kRadixBlock), 0, s, kin, nPtr, shift, hist, t); \
-    hipLaunchKernelGGL(k_radix_scan, dim3(1u << B), dim3(256), 0, s, hist, grid, binTotals);                 \
-    if (ballot)                                                                                               \
-        hipLaunchKernelGGL((k_radix_downsweep<B, true, K>), dim3(grid), dim3(kRadixBlock), 0, s, kin, vin, kout, \
-                           vout, nPtr, shift, hist, binTotals, t);                                            \
-    else                                                                                                      \
-        hipLaunchKernelGGL((k_radix_downsweep<B, false, K>), dim3(grid), dim3(kRadixBlock), 0, s, kin, vin, kout, \
+#define GSM_RADIX_PASS(B, S)                                                                                \
+    hipLaunchKernelGGL(k_radix_upsweep<B>, dim3(grid), dim3(kRadixBlock), 0, s, kin, nPtr, shift, hist);    \
+    hipLaunchKernelGGL(k_radix_scan, dim3(1u << B), dim3(256), 0, s, hist, grid, binTotals);               \
+    if (ballot)                                                                                             \
+        hipLaunchKernelGGL((k_radix_downsweep<B, true, S>), dim3(grid), dim3(kRadixBlock), 0, s, kin, vin, kout, \
+                           vout, nPtr, shift, hist, binTotals, t);                                          \
+    else                                                                                                    \
+        hipLaunchKernelGGL((k_radix_downsweep<B, false, S>), dim3(grid), dim3(kRadixBlock), 0, s, kin, vin, kout, \
                            vout, nPtr, shift, hist, binTotals, t)
-#define GSM_RADIX_BITS(K)                    \
+#define GSM_RADIX_BITS(S)                    \
     switch (bits) {                          \
-        case 4: GSM_RADIX_PASS(4, K); break; \
-        case 5: GSM_RADIX_PASS(5, K); break; \
-        case 6: GSM_RADIX_PASS(6, K); break; \
-        case 7: GSM_RADIX_PASS(7, K); break; \
-        default: GSM_RADIX_PASS(8, K); break; \
+        case 4: GSM_RADIX_PASS(4, S); break; \
+        case 5: GSM_RADIX_PASS(5, S); break; \
+        case 6: GSM_RADIX_PASS(6, S); break; \
+        case 7: GSM_RADIX_PASS(7, S); break; \
+        default: GSM_RADIX_PASS(8, S); break; \
     }
-    if (ts && bucketed) {
+    if (starts) {
         GSM_RADIX_BITS(true)
     } else {
         GSM_RADIX_BITS(false)
@@ -535,33 +431,31 @@ int radix_sort_bits(uint32_t* keys[2], uint32_t* vals[2], const uint32_t* nPtr, 
 }
 
 // The frame sort's tile passes (radix_sort_bits over the tile field, bits <= 16: one or two
-// passes) with the tile starts written by the last pass (TileStarts above).  binTotals holds 512
-// words + the last pass's block table (kTileTableEntries x 16 B): the first pass's digit totals stay
-// in [0, 256) as the last pass's buckets.
+// passes) with the tile starts written by the last pass (TileStarts above).  binTotals holds
+// kSortTotalsWords words: the last pass's digit totals, the first pass's at +256, its bucket
+// starts at +512.
 int radix_sort_tiles(uint32_t* keys[2], uint32_t* vals[2], const uint32_t* nPtr, uint32_t capacity, uint32_t shift,
                      uint32_t bits, uint32_t* hist, uint32_t* binTotals, uint32_t* tileStart, uint32_t numTiles,
                      hipStream_t s, bool ballot) {
     const uint32_t grid = radix_grid_for_capacity(capacity);
     if (bits > 16) bits = 16;
     TileStarts ts{};
-    ts.baseGrid = grid;
     ts.numTiles = numTiles;
     ts.tileStart = tileStart;
     if (bits <= 8) {  // one pass, one bucket
-        const uint32_t b = bits < 4 ? 4 : bits;
-        ts.bucketCnt = nPtr;
-        ts.lowBits = 0;
-        radix_pass(keys[0], vals[0], keys[1], vals[1], nPtr, grid + 1u, shift, (int)b, hist, binTotals, s, ballot, &ts);
+        radix_pass(keys[0], vals[0], keys[1], vals[1], nPtr, grid, shift, (int)(bits < 4 ? 4 : bits), hist,
+                   binTotals, s, ballot, &ts, true);
         return 1;
     }
     const uint32_t lo = (bits + 1u) / 2u, hi = bits - lo;  // radix_sort_bits' digit widths
-    ts.table = (uint4*)(binTotals + 512);  // kSortTotalsWords
-    radix_pass(keys[0], vals[0], keys[1], vals[1], nPtr, grid, shift, (int)lo, hist, binTotals, s, ballot, &ts,
-               false);
-    ts.bucketCnt = binTotals;
+    TileStarts first{};
+    first.bucketStartOut = binTotals + 512;
+    radix_pass(keys[0], vals[0], keys[1], vals[1], nPtr, grid, shift, (int)lo, hist, binTotals + 256, s, ballot,
+               &first, false);
+    ts.bucketStart = binTotals + 512;
     ts.lowBits = lo;
-    radix_pass(keys[1], vals[1], keys[0], vals[0], nPtr, grid + (1u << lo), shift + lo, (int)hi, hist, binTotals + 256,
-               s, ballot, &ts);
+    radix_pass(keys[1], vals[1], keys[0], vals[0], nPtr, grid, shift + lo, (int)hi, hist, binTotals, s, ballot, &ts,
+               true);
     return 0;
 }
 

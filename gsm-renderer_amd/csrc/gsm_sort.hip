@@ -156,9 +156,11 @@ __global__ __launch_bounds__(256) void k_radix_scan(uint32_t* __restrict__ hist,
 // In the last pass, the keys of bucket l that precede digit h's output are exactly those of tile
 // (h << lowBits | l)'s predecessors: all keys of high digits < h and the keys of digit h in
 // buckets < l.  So where a block's chunk holds the start p of bucket l, the start of tile
-// (h, l) is digit h's output base at that chunk plus the chunk's keys of digit h before p (counted
-// again from the chunk's keys, still in L2, in the few chunks that hold a bucket start) -- a lower
-// bound also when the tile is empty.  The block holding p = bucketStart[l] writes the
+// (h, l) is digit h's output base at that chunk plus the chunk's keys of digit h before p -- a lower
+// bound also when the tile is empty.  Those counts: the earlier waves' (the per-digit wave scan)
+// plus the holding wave's counters copied when its rank loop reaches p's item (a further start
+// in the same chunk, rare, recounts the chunk's keys before it from L2).  The block holding
+// p = bucketStart[l] writes the
 // starts of every tile of bucket l; the last block those of the empty buckets at the end
 // (bucketStart = n); no separate pass over the sorted keys.  One pass: one bucket, lowBits = 0.
 struct TileStarts {

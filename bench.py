@@ -7,12 +7,16 @@ resident in HBM.  Default workload = BASELINE.json configs[1]: 1M gaussians, SH3
 1920x1080, PackedWorldGaussianHalf (fp16).
 
 N>1 (torch.distributed.run, one rank per GPU, RCCL over xGMI), --multi:
-  alltoall (default): rank r projects ids [r*N/n, (r+1)*N/n) once and packs a
-      48-byte record per (gaussian, slab it meets); all_to_all of the counts and of the
-      records (gsm_amd.exchange); every rank renders its band of tile rows from the records;
+  alltoall (default): the whole partitioned frame inside libgsm_amd.so
+      (gsm_multigpu_render over torch's RCCL communicator): rank r projects ids
+      [r*N/n, (r+1)*N/n) once, per-slab counts are all-gathered, each 48-byte record is
+      written straight into its slab owner's receive buffer over xGMI, every rank renders its
+      band of tile rows; if any rank cannot create that frame, every rank falls back to the
+      RCCL all-to-all of gsm_amd.exchange ("multi_fallback" in the line);
   replicas: every rank projects all gaussians and keeps its band's assignments.
 Either way the bands are gathered on rank 0 inside the timed step.  The frame is fixed as N
-grows -> "scaling": "strong".
+grows -> "scaling": "strong".  The line also carries "config4": BASELINE configs[3], the 4K
+scene of config 3 partitioned over the same N GPUs, timed the same way.
 
 Prints ONE JSON line on rank 0 (contract in the task statement), including
 "roofline" for the dominant kernel (the blend) and "cpu_baseline" (the C oracle
@@ -402,6 +406,7 @@ def multi_extra_frame(args, gsm_amd, scenes, dev, gpu, rank, world_size):
     (gsm_multigpu_render), timed like `value` (barriers, max over ranks); rank 0 gathers the frame.
     Parity of the partitioned frame is checked on the main config; this is a throughput line."""
     import torch
+    import torch.distributed  # noqa: F401 (the create check below is collective)
     c = scenes.CONFIGS[args.multi_extra_config]
     n, W, H, sh, prec = c["count"], c["width"], c["height"], c["sh"], c["precision"]
     world_np, harm_np, cam_d = scenes.gen_scene(n, W, H, sh, prec, seed=42)
@@ -411,7 +416,18 @@ def multi_extra_frame(args, gsm_amd, scenes, dev, gpu, rank, world_size):
     cfg = gsm_amd.RendererConfig(max_gaussians=n, max_width=W, max_height=H, precision=prec,
                                  gaussian_color_space=gsm_amd.GaussianColorSpace.LINEAR)
     r = gsm_amd.GlobalRenderer(device=dev.index, config=cfg)
-    mg = gsm_amd.MultiGpuRenderer(r, gsm_amd.MultiGpuRenderer.torch_comm(gpu), rank, world_size)
+    mg, err = None, None
+    try:
+        mg = gsm_amd.MultiGpuRenderer(r, gsm_amd.MultiGpuRenderer.torch_comm(gpu), rank, world_size)
+    except gsm_amd.RendererError as e:
+        err = f"rank {rank}: {e}"
+    ok = torch.tensor([0 if mg is None else 1], dtype=torch.int32, device=dev)
+    torch.distributed.all_reduce(ok, op=torch.distributed.ReduceOp.MIN)  # collective: all or none
+    if int(ok.item()) == 0:
+        if mg is not None:
+            mg.close()
+        r.close()
+        return {"error": err or "another rank's gsm_multigpu_create failed"}
     full_c = torch.zeros((H, W, 4), dtype=torch.float16, device=dev)
     full_d = torch.zeros((H, W), dtype=torch.float16, device=dev)
     inp = gsm_amd.GaussianInput(world, harm, n, sh)

@@ -220,4 +220,35 @@ gsm_status gsm_debug_sort_rank_probe(int hip_device, int* lane_ordered) {
     return GSM_OK;
 }
 
+gsm_status gsm_debug_partition_counts(gsm_renderer* r, void* stream, const gsm_gaussian_input* input,
+                                      const gsm_camera_params* camera, uint32_t width, uint32_t height,
+                                      uint32_t first, uint32_t count, const uint32_t* slab_rows,
+                                      uint32_t num_slabs, uint32_t* d_send_counts) {
+    if (!r || !r->impl || !input || !camera || !slab_rows || !d_send_counts) return GSM_ERR_INVALID_ARGUMENT;
+    return r->impl->partitionCounts((hipStream_t)stream, *input, *camera, width, height, first, count, slab_rows,
+                                    num_slabs, d_send_counts);
+}
+
+gsm_status gsm_debug_partition_push(gsm_renderer* r, void* stream, uint32_t world, uint32_t rank,
+                                    const uint32_t* d_counts, void* const* recv_buffers, uint32_t* d_recv_count) {
+    if (!r || !r->impl || !d_counts || !recv_buffers || !d_recv_count || world < 1 || world > gsm::kMaxSlabs ||
+        rank >= world)
+        return GSM_ERR_INVALID_ARGUMENT;
+    gsm::SlabPeers peers{};
+    for (uint32_t p = 0; p < world; ++p) {
+        if (!recv_buffers[p]) return GSM_ERR_INVALID_ARGUMENT;
+        peers.recv[p] = (gsm::SplatRecord*)recv_buffers[p];
+    }
+    return r->impl->partitionPush((hipStream_t)stream, world, rank, d_counts, peers, d_recv_count);
+}
+
+gsm_status gsm_debug_render_records_device_count(gsm_renderer* r, void* stream, const void* records,
+                                                 uint32_t capacity, const uint32_t* d_count, uint32_t width,
+                                                 uint32_t height, void* color, size_t color_pitch, void* depth,
+                                                 size_t depth_pitch) {
+    if (!r || !r->impl || !d_count) return GSM_ERR_INVALID_ARGUMENT;
+    return r->impl->renderRecords((hipStream_t)stream, records, capacity, width, height, color, color_pitch, depth,
+                                  depth_pitch, d_count);
+}
+
 }  // extern "C"

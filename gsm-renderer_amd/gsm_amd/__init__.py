@@ -229,6 +229,14 @@ _SIGNATURES = {
     "gsm_depthfirst_stage_times": ([C.c_void_p, C.POINTER(C.c_float), C.c_int], C.c_int),
     "gsm_depthfirst_last_gpu_time": ([C.c_void_p, C.POINTER(C.c_double)], C.c_int),
     "gsm_debug_sort_rank_probe": ([C.c_int, C.POINTER(C.c_int)], C.c_int),
+    "gsm_debug_partition_counts": ([C.c_void_p, C.c_void_p, C.POINTER(_Input), C.POINTER(_Camera), C.c_uint32,
+                                    C.c_uint32, C.c_uint32, C.c_uint32, C.POINTER(C.c_uint32), C.c_uint32,
+                                    C.c_void_p], C.c_int),
+    "gsm_debug_partition_push": ([C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p,
+                                  C.POINTER(C.c_void_p), C.c_void_p], C.c_int),
+    "gsm_debug_render_records_device_count": ([C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p,
+                                               C.c_uint32, C.c_uint32, C.c_void_p, C.c_size_t, C.c_void_p,
+                                               C.c_size_t], C.c_int),
     "gsm_multigpu_create": ([C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_void_p)], C.c_int),
     "gsm_multigpu_destroy": ([C.c_void_p], None),
     "gsm_multigpu_render": ([C.c_void_p, C.c_void_p, C.POINTER(_Input), C.POINTER(_Camera), C.c_uint32,
@@ -359,6 +367,36 @@ class GlobalRenderer:
                                               int(width), int(height), _ptr(color_texture), cp,
                                               _ptr(depth_texture), dp)
         _check(st, "gsm_global_render_records")
+
+    def debug_partition_counts(self, input: GaussianInput, camera: CameraParams, width: int, height: int,
+                               first: int, count: int, slab_rows, send_counts, stream=None):
+        """gsm_debug_partition_counts: the native multi-GPU frame's projection of ids
+        [first, first+count) with per-slab record counts into `send_counts` (device uint32)."""
+        inp = _Input(_ptr(input.gaussians), _ptr(input.harmonics), int(input.gaussian_count),
+                     int(input.sh_components))
+        cam = _camera_struct(camera)
+        rows = (C.c_uint32 * len(slab_rows))(*[int(x) for x in slab_rows])
+        _check(_lib().gsm_debug_partition_counts(self._h, _stream_handle(stream), C.byref(inp), C.byref(cam),
+                                                 int(width), int(height), int(first), int(count), rows,
+                                                 len(slab_rows) - 1, _ptr(send_counts)),
+               "gsm_debug_partition_counts")
+
+    def debug_partition_push(self, world: int, rank: int, counts, recv_buffers, recv_count, stream=None):
+        """gsm_debug_partition_push: the last partition's records written into their slab owners'
+        receive buffers (device tensors, one per rank) at the offsets of the device count matrix."""
+        bufs = (C.c_void_p * len(recv_buffers))(*[_ptr(b) for b in recv_buffers])
+        _check(_lib().gsm_debug_partition_push(self._h, _stream_handle(stream), int(world), int(rank),
+                                               _ptr(counts), bufs, _ptr(recv_count)),
+               "gsm_debug_partition_push")
+
+    def debug_render_records_device_count(self, color_texture, depth_texture, records, capacity: int, count,
+                                          width: int, height: int, stream=None):
+        """gsm_debug_render_records_device_count: render_records with the count read on the device."""
+        _check(_lib().gsm_debug_render_records_device_count(self._h, _stream_handle(stream), _ptr(records),
+                                                            int(capacity), _ptr(count), int(width), int(height),
+                                                            _ptr(color_texture), int(width) * self._bpp,
+                                                            _ptr(depth_texture), int(width) * 2),
+               "gsm_debug_render_records_device_count")
 
     def render_stereo(self, color_texture, depth_texture, input: GaussianInput, left: CameraParams,
                       right: CameraParams, width: int, height: int, stream=None):

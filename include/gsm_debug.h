@@ -89,6 +89,29 @@ gsm_status gsm_sort_pairs_u32(void *keys, void *values, uint32_t n, uint32_t key
  * Cached per device and process; no reference counterpart (a gfx950 design choice). */
 gsm_status gsm_debug_sort_rank_probe(int hip_device, int *lane_ordered);
 
+/* The device steps of gsm_multigpu_render (gsm_multigpu.h) without RCCL, so W virtual ranks can run
+ * the native exchange in one process on one GPU (tests): the caller plays the collectives --
+ * gathers every rank's per-slab counts into the W x W matrix (row r = rank r) on the device and
+ * orders the pushes before the renders by stream order.
+ *   partition_counts: project ids [first, first + count) and count the records per slab
+ *     (slab_rows: num_slabs + 1 tile-row boundaries) into d_send_counts (device, num_slabs words);
+ *   partition_push: write every record of the last partition_counts straight into its slab
+ *     owner's receive buffer (recv_buffers: host array of `world` device pointers, each holding
+ *     GSM_SPLAT_RECORD_BYTES x max_gaussians) at the offset the count matrix d_counts gives;
+ *     d_recv_count (device) receives this rank's incoming record count;
+ *   render_records_device_count: gsm_global_render_records with the record count read on the
+ *     device (d_count) and `capacity` records the grids cover. */
+gsm_status gsm_debug_partition_counts(gsm_renderer *renderer, void *stream, const gsm_gaussian_input *input,
+                                      const gsm_camera_params *camera, uint32_t width, uint32_t height,
+                                      uint32_t first, uint32_t count, const uint32_t *slab_rows,
+                                      uint32_t num_slabs, uint32_t *d_send_counts);
+gsm_status gsm_debug_partition_push(gsm_renderer *renderer, void *stream, uint32_t world, uint32_t rank,
+                                    const uint32_t *d_counts, void *const *recv_buffers, uint32_t *d_recv_count);
+gsm_status gsm_debug_render_records_device_count(gsm_renderer *renderer, void *stream, const void *records,
+                                                 uint32_t capacity, const uint32_t *d_count, uint32_t width,
+                                                 uint32_t height, void *color, size_t color_pitch, void *depth,
+                                                 size_t depth_pitch);
+
 #ifdef __cplusplus
 }
 #endif

@@ -64,3 +64,57 @@ def test_create_rejects_a_mismatched_world(gsm, cuda, nccl_world1):
         gsm.MultiGpuRenderer(rend, gsm.MultiGpuRenderer.torch_comm(0), 0, 2)
     assert e.value.status == gsm.Status.INVALID_ARGUMENT
     rend.close()
+
+
+@pytest.mark.parametrize("world,n,w,h,prec", [(2, 40_000, 640, 360, 1), (3, 60_000, 1280, 720, 1),
+                                              (8, 50_000, 640, 360, 0)])
+def test_native_exchange_virtual_ranks(gsm, cuda, oracle, world, n, w, h, prec):
+    """The device steps of gsm_multigpu_render for world > 1 without RCCL (include/gsm_debug.h): W
+    renderers on one GPU play the ranks -- each projects its id range and counts its records per slab
+    (k_project_part), the count matrix is stacked on the device (the all-gather), every rank's
+    k_part_push writes its records straight into every slab owner's receive buffer at the matrix's
+    offsets, and each owner renders its rows from the count read on the device.  Ids and slab rows
+    are split as gsm_multigpu.hip splits them.  The composed frame equals the oracle bit for bit:
+    the push offsets, the receive counts and the rank-ordered ties of world > 1 (the world-1 RCCL
+    test above cannot reach them)."""
+    import math
+    from gsm_amd import scenes
+    sh = 16 if prec else 4
+    world_np, harm_np, cam_d = scenes.gen_scene(n, w, h, sh, prec, seed=78)
+    ref = oracle.render(world_np, harm_np, sh, cam_d, w, h, max_gaussians=n)
+    wt = cuda.from_numpy(world_np.view(np.uint8).reshape(-1).copy()).cuda()
+    ht = cuda.from_numpy(harm_np.view(np.uint8).reshape(-1).copy()).cuda()
+    inp = gsm.GaussianInput(wt, ht, n, sh)
+    cam = gsm.CameraParams.from_dict(cam_d)
+    tiles_y = (h + 15) // 16
+    per_rows = math.ceil(tiles_y / world)
+    rows = [min(i * per_rows, tiles_y) for i in range(world + 1)]
+    per_ids = math.ceil(n / world)
+    cfg = gsm.RendererConfig(max_gaussians=n, max_width=w, max_height=h, precision=prec, gaussian_color_space=0)
+    ranks = [gsm.GlobalRenderer(device=0, config=cfg) for _ in range(world)]
+    send = [cuda.zeros(world, dtype=cuda.int32, device="cuda") for _ in range(world)]
+    for rk in range(world):
+        first = min(rk * per_ids, n)
+        ranks[rk].debug_partition_counts(inp, cam, w, h, first, min(per_ids, n - first), rows, send[rk])
+    counts = cuda.stack(send).contiguous()  # row r = rank r's records per slab (the all-gather)
+    recv = [cuda.zeros(n * gsm.SPLAT_RECORD_BYTES, dtype=cuda.uint8, device="cuda") for _ in range(world)]
+    recv_count = [cuda.full((1,), -1, dtype=cuda.int32, device="cuda") for _ in range(world)]
+    for rk in range(world):
+        ranks[rk].debug_partition_push(world, rk, counts, recv, recv_count[rk])
+    color = cuda.full((h, w, 4), float("nan"), dtype=cuda.float16, device="cuda")
+    depth = cuda.full((h, w), float("nan"), dtype=cuda.float16, device="cuda")
+    for d in range(world):
+        if rows[d] == rows[d + 1]:
+            continue
+        ranks[d].set_tile_rows(rows[d], rows[d + 1])
+        ranks[d].debug_render_records_device_count(color, depth, recv[d], n, recv_count[d], w, h)
+    cuda.cuda.synchronize()
+    cm = counts.cpu().numpy().astype(np.int64)
+    assert [int(c.item()) for c in recv_count] == [int(x) for x in cm.sum(axis=0)]
+    with_tiles = int(np.count_nonzero(ref["tile_counts"]))
+    assert with_tiles <= cm.sum() <= with_tiles * world
+    got = color.view(cuda.int16).cpu().numpy().view(np.uint16)
+    assert np.array_equal(got, ref["color"])
+    assert np.array_equal(depth.view(cuda.int16).cpu().numpy().view(np.uint16), ref["depth"])
+    for rend in ranks:
+        rend.close()

@@ -569,18 +569,6 @@ __global__ __launch_bounds__(NT) void k_blend_px(
     if (unitCost && lane == 0 && waveMax) atomicMax(&costMax[(blockIdx.x * NW + wv) % kCostMaxSlots], waveMax);
 }
 
-// ---------------------------------------------------------------------------
-// Blend schedule (unit_order_block, gsm_device.h) as a kernel of its own: the records path of a
-// multi-GPU slab and the DepthFirst renderer run it before the blend; the single-GPU frame runs
-// the same block inside its projection launch (k_project, one extra workgroup).
-// ---------------------------------------------------------------------------
-__global__ __launch_bounds__(1024) void k_unit_order(const uint16_t* __restrict__ cost,
-                                                     uint32_t* __restrict__ order, uint32_t n,
-                                                     uint32_t* __restrict__ costMax) {
-    __shared__ uint32_t base[kUoBuckets];
-    __shared__ uint32_t wmax[1024 / 64];
-    unit_order_block<1024>(cost, order, n, base, wmax, costMax);
-}
 
 
 int blend_pairs_per_lane(uint32_t numTiles, int numCUs) {
@@ -605,9 +593,6 @@ static int blend_waves_per_wg(uint32_t numTiles, int numCUs) {
     return units >= 2ull * (uint64_t)numCUs * 12u ? 12 : 8;
 }
 
-void launch_unit_order(uint32_t numUnits, const DeviceArena& A, hipStream_t s) {
-    hipLaunchKernelGGL(k_unit_order, dim3(1), dim3(1024), 0, s, A.unitCost, A.unitOrder, numUnits, A.costMax);
-}
 
 
 // Measured schedule choices: units longest-first by last frame's walk (costOrder;

@@ -155,9 +155,6 @@ void launch_headers(const uint32_t* sortedKeys, const FrameGeometry& geo, const 
 void launch_blend(const FrameGeometry& geo, const DeviceArena& A,
                   void* color, size_t colorPitch, void* depth, size_t depthPitch, int numCUs,
                   bool costOrder, int colorFormat, hipStream_t stream, int waves = 0);
-// orders the blend units by the walk lengths the previous frame measured (longest first), so
-// the dynamic queue hands out long units before short ones (A.unitOrder[numUnits])
-void launch_unit_order(uint32_t numUnits, const DeviceArena& A, hipStream_t stream);
 // blend kernel shape: pixel pairs per lane (0 = quadrant kernel) and blend units per tile
 int blend_pairs_per_lane(uint32_t numTiles, int numCUs);
 uint32_t blend_units_per_tile(uint32_t numTiles, int numCUs);

@@ -480,9 +480,19 @@ __global__ __launch_bounds__(kProjectBlock) void k_records_in(
     const SplatRecord* __restrict__ in, ProjectArgs P, GaussianRenderData* __restrict__ outRD,
     short4* __restrict__ outBounds, BlendRecord* __restrict__ outRec,
     uint32_t* __restrict__ counts, uint32_t* __restrict__ masks, uint32_t* __restrict__ blockSums,
-    const float2* __restrict__ sincos, const uint32_t* __restrict__ devCount) {
+    const float2* __restrict__ sincos, const uint32_t* __restrict__ devCount, const uint16_t* __restrict__ unitCost,
+    uint32_t* __restrict__ unitOrder, uint32_t* __restrict__ costMax) {
     __shared__ uint32_t lds[kProjectBlock / 64];
-    const uint32_t gid = blockIdx.x * kProjectBlock + threadIdx.x;
+    // block 0 of a scheduled launch orders the blend's units (as k_project's: no k_unit_order launch)
+    if (P.schedUnits) {
+        if (blockIdx.x == 0) {
+            __shared__ uint32_t uoBase[kUoBuckets], uoMax[kProjectBlock / 64];
+            unit_order_block<kProjectBlock>(unitCost, unitOrder, P.schedUnits, uoBase, uoMax, costMax);
+            return;
+        }
+    }
+    const uint32_t blk = blockIdx.x - (P.schedUnits ? 1u : 0u);
+    const uint32_t gid = blk * kProjectBlock + threadIdx.x;
     const uint32_t n = devCount ? min(*devCount, P.count) : P.count;
     uint32_t ntiles = 0;
     if (gid >= n && gid < P.count) counts[gid] = 0;
@@ -512,7 +522,7 @@ __global__ __launch_bounds__(kProjectBlock) void k_records_in(
         rp[1] = make_uint4(r.rb, __float_as_uint(band.x), __float_as_uint(band.y), 0u);
     }
     uint32_t s = block_reduce_add<kProjectBlock>(ntiles, lds);
-    if (threadIdx.x == 0) blockSums[blockIdx.x] = s;
+    if (threadIdx.x == 0) blockSums[blk] = s;
 }
 
 // ---------------------------------------------------------------------------
@@ -961,10 +971,10 @@ void launch_partition_push(const ProjectArgs& a, uint32_t world, uint32_t rank, 
 void launch_records_in(const void* records, const ProjectArgs& a, const DeviceArena& A, hipStream_t s,
                        const uint32_t* devCount) {
     const uint32_t blocks = (a.count + kProjectBlock - 1) / kProjectBlock;
-    if (blocks == 0) return;
-    hipLaunchKernelGGL(k_records_in, dim3(blocks), dim3(kProjectBlock), 0, s, (const SplatRecord*)records, a,
-                       A.renderData, A.bounds, A.rec, A.tileCounts, A.tileMasks, A.blockSums,
-                       A.sincosTable, devCount);
+    if (blocks == 0 && a.schedUnits == 0) return;  // (an empty frame still orders its blend units)
+    hipLaunchKernelGGL(k_records_in, dim3(blocks + (a.schedUnits ? 1u : 0u)), dim3(kProjectBlock), 0, s,
+                       (const SplatRecord*)records, a, A.renderData, A.bounds, A.rec, A.tileCounts, A.tileMasks,
+                       A.blockSums, A.sincosTable, devCount, A.unitCost, A.unitOrder, A.costMax);
 }
 
 void launch_scan_sums(uint32_t* sums, uint32_t nb, uint32_t cap, TileAssignmentHeader* hdr, uint32_t* queue,

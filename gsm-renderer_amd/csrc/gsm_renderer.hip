@@ -248,7 +248,6 @@ gsm_status GlobalRenderer::render(hipStream_t s, const gsm_gaussian_input& in,
     return runFrame(s, a, width, height, color, colorPitch, depth, depthPitch,
                     [&](const ProjectArgs& pa) {
                         launch_project(half, deg, in.gaussians, in.harmonics, pa, arena_, s);
-                        return true;  // the projection launch ordered the blend units (pa.schedUnits)
                     });
 }
 
@@ -265,7 +264,6 @@ gsm_status GlobalRenderer::renderRecords(hipStream_t s, const void* records, uin
     return runFrame(s, a, width, height, color, colorPitch, depth, depthPitch,
                     [&](const ProjectArgs& pa) {
                         launch_records_in(records, pa, arena_, s, devCount);
-                        return false;  // k_unit_order runs before the blend
                     });
 }
 
@@ -372,7 +370,7 @@ gsm_status GlobalRenderer::runFrame(hipStream_t s, const ProjectArgs& a, uint32_
     // Blend schedule: the units ordered by the walk lengths the previous frame of the same
     // geometry measured (the image does not depend on the order, only the load balance does).
     // The ordering only needs those costs: one extra workgroup of the projection launch does it
-    // (unit_order_block) while the others project; the records path launches k_unit_order.
+    // (unit_order_block) while the others project (k_project, or k_records_in on the records path).
     const uint32_t upt = blend_units_per_tile((rowEnd_ - rowBegin_) * tilesX_, numCUs_);
     const uint32_t units = (rowEnd_ - rowBegin_) * tilesX_ * upt;
     const uint64_t key = ((uint64_t)upt << 60) ^ ((uint64_t)width << 40) ^ ((uint64_t)height << 20) ^
@@ -387,7 +385,7 @@ gsm_status GlobalRenderer::runFrame(hipStream_t s, const ProjectArgs& a, uint32_
 
     hipEvent_t* ev = (prof || blendOnly) ? frameEvents(profFrames_) : nullptr;
     if (prof) hipEventRecord(ev[0], s);
-    const bool scheduled = front(fa);
+    front(fa);  // the projection (or records) launch; its block 0 orders the blend units (fa.schedUnits)
     if (prof) hipEventRecord(ev[1], s);
     launch_scan_blocks(nb, a, arena_, s);
     if (prof) hipEventRecord(ev[2], s);
@@ -442,7 +440,6 @@ gsm_status GlobalRenderer::runFrame(hipStream_t s, const ProjectArgs& a, uint32_
         launch_half_lists(sortedVals_, rowBegin_ * tilesX_, (rowEnd_ - rowBegin_) * tilesX_, arena_, tileCount_, s);
     arena_.blendTrace = (profiling_ & 4) ? traceBuf_ : nullptr;
     // the schedule from the walks the previous frame's blend recorded (same stream: no join)
-    if (costOrder && !scheduled) launch_unit_order(units, arena_, s);
     if (prof || blendOnly) hipEventRecord(ev[5], s);
     launch_blend(g, arena_, color, colorPitch, depth, depthPitch, numCUs_, costOrder,
                  (int)config_.color_format, s, tuning_.blendWaves);

@@ -81,8 +81,34 @@ def parse():
     return a
 
 
+def launch_ranks(args) -> int:
+    """`python bench.py --gpus N` without a launcher: start N rank processes (torch.distributed.run,
+    one per GPU, 127.0.0.1) from this process, which has made no GPU call, and return their exit
+    code.  Fails loudly when the node has fewer than N GPUs (BENCH_SAME_GPU=1: a rehearsal with the
+    ranks sharing the visible GPUs)."""
+    import socket
+    import subprocess
+
+    import torch
+    have = torch.cuda.device_count()  # counts devices without initialising the GPU on this image
+    if have < args.gpus and os.environ.get("BENCH_SAME_GPU") != "1":
+        print(f"bench: --gpus {args.gpus} needs {args.gpus} GPUs, this node has {have}", file=sys.stderr)
+        return 3
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args))
+    if int(os.environ.get("WORLD_SIZE", "1")) != args.gpus:
+        print(f"bench: WORLD_SIZE={os.environ.get('WORLD_SIZE')} but --gpus {args.gpus}", file=sys.stderr)
+        sys.exit(2)
     import torch
     import torch.distributed as dist
 
@@ -92,12 +118,12 @@ def main():
     world_size = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    # BENCH_DIST_BACKEND=gloo rehearses the N>1 protocol with several ranks on one GPU (CPU-staged
-    # collectives; timings meaningless).  The driver's multi-GPU runs use RCCL ("nccl").
-    backend = os.environ.get("BENCH_DIST_BACKEND", "nccl")
-    # BENCH_SAME_GPU=1 maps every rank onto the visible GPUs round robin with RCCL too: an N-rank
-    # rehearsal of the multi-GPU protocol (IPC receive buffers, RCCL collectives) on a one-GPU box
-    same_gpu = backend == "gloo" or os.environ.get("BENCH_SAME_GPU") == "1"
+    # BENCH_SAME_GPU=1 maps every rank onto the visible GPUs round robin: an N-rank rehearsal of the
+    # multi-GPU frame (IPC-mapped exchange memory, cross-process flag barriers) on a one-GPU box.
+    # Ranks sharing a GPU cannot form an RCCL communicator ("Duplicate GPU detected"), so the host
+    # side (handle exchange, timing barriers) then runs over gloo; the frame itself uses neither.
+    same_gpu = os.environ.get("BENCH_SAME_GPU") == "1" or os.environ.get("BENCH_DIST_BACKEND") == "gloo"
+    backend = os.environ.get("BENCH_DIST_BACKEND", "gloo" if same_gpu else "nccl")
     gpu = local_rank % max(1, torch.cuda.device_count()) if same_gpu else local_rank
     # BENCH_FORCE_MULTI=1 runs the N>1 code path (C-ABI multi-GPU frame over an RCCL communicator)
     # at world size 1 -- a one-GPU rehearsal of what the driver's 8-GPU runs execute
@@ -151,18 +177,17 @@ def main():
     # owners over xGMI, bands sent to rank 0 -- no host round trip in a frame.  The gloo rehearsal
     # (BENCH_DIST_BACKEND=gloo, several ranks on one GPU) has no RCCL communicator and moves the
     # records through gsm_amd.exchange instead.
-    native_multi = alltoall and backend == "nccl"
+    native_multi = alltoall
     multi_fallback = None
     if native_multi:
-        full_c = torch.zeros((H, TW, 4), dtype=torch.float16, device=dev)  # rank 0: the gathered frame
-        full_d = torch.zeros((H, TW), dtype=torch.float16, device=dev)
         mg = None
-        try:
-            mg = gsm_amd.MultiGpuRenderer(renderer, gsm_amd.MultiGpuRenderer.torch_comm(gpu), rank, world_size)
-        except gsm_amd.RendererError as e:  # e.g. IPC receive buffers that cannot be opened on this node
+        try:  # exchange handles over torch.distributed (any backend); the frame needs no collective
+            mg = gsm_amd.MultiGpuRenderer.connect(renderer, rank, world_size, gsm_amd.MultiGpuRenderer.torch_allgather)
+            frame_ptr = mg.frame()[0]  # rank 0: the gathered frame (library memory, zero copy)
+        except gsm_amd.RendererError as e:  # e.g. exchange memory that cannot be opened on this node
             multi_fallback = f"rank {rank}: {e}"
         # create is collective: every rank takes the native frame or none does
-        ok = torch.tensor([0 if mg is None else 1], dtype=torch.int32, device=dev)
+        ok = torch.tensor([0 if mg is None else 1], dtype=torch.int32, device=dev if backend == "nccl" else "cpu")
         dist.all_reduce(ok, op=dist.ReduceOp.MIN)
         if int(ok.item()) == 0:
             if mg is not None:
@@ -188,7 +213,8 @@ def main():
             renderer.render_stereo_sbs(cptr, dptr, inp, cam_l, cam_r, W, H, stream=stream,
                                        color_pitch=pitch_c, depth_pitch=pitch_d)
         elif native_multi:
-            mg.render(full_c, full_d, inp, cam, W, H, gather=True, stream=stream)
+            mg.render(None, None, inp, cam, W, H, gather=True, stream=stream,
+                      gather_target=frame_ptr if rank == 0 else None)
             return
         elif alltoall:
             renderer.project_partition(inp, cam, W, H, first, cnt, rows, send, send_cap, send_counts,
@@ -210,7 +236,7 @@ def main():
     # timed region: only the blend (the roofline kernel) is bracketed by HIP events on the render
     # stream -- two events on every BLEND_EVENT_PERIOD-th frame (each bracketed frame costs ~10 us
     # of event overhead, tools/exp_events.py); the per-stage breakdown comes from a separate pass below
-    elapsed, blend_ms_timed = timed_loop(args.steps, step, renderer, world_size, dev)
+    elapsed, blend_ms_timed = timed_loop(args.steps, step, renderer, world_size, dev, backend)
     # per-stage breakdown: 10 more frames with every stage bracketed (not part of `value`)
     renderer.set_profiling(stage_events=True)
     for _ in range(10):
@@ -253,12 +279,18 @@ def main():
             import oracle as O  # parity checker only
             ref = O.render(world_np, harm_np, sh, cam_d, W, H, max_gaussians=n,
                            nthreads=max(1, min(args.cpu_threads, os.cpu_count() or 1)))
-            multi_parity = bool(np.array_equal(full_c.view(torch.int16).cpu().numpy().view(np.uint16), ref["color"]))
+            multi_parity = bool(np.array_equal(mg.copy_frame(W, H), ref["color"]))
     # BASELINE config 4 (the 4K scene of config 3 on N GPUs): timed the same way after `value`
     multi_4k = None
     if native_multi and args.multi_extra_config not in ("", "none", args.config):
-        multi_4k = multi_extra_frame(args, gsm_amd, scenes, dev, gpu, rank, world_size)
+        multi_4k = multi_extra_frame(args, gsm_amd, scenes, dev, gpu, rank, world_size, backend)
+    barrier_timeouts = None
     if native_multi:
+        t = torch.tensor([mg.status()], dtype=torch.int64, device=dev if backend == "nccl" else "cpu")
+        dist.all_reduce(t)  # every rank's barrier timeouts (0 on a healthy run)
+        barrier_timeouts = int(t.item())
+        torch.cuda.synchronize()
+        dist.barrier()  # no rank unmaps its exchange memory while a peer may still write into it
         mg.close()
     if rank != 0:
         renderer.close()
@@ -393,6 +425,8 @@ def main():
     }
     if multi_fallback:
         out["multi_fallback"] = multi_fallback
+    if barrier_timeouts is not None:
+        out["barrier_timeouts"] = barrier_timeouts
     if multi_4k:
         out["config4"] = multi_4k
     print(json.dumps(out))
@@ -401,7 +435,7 @@ def main():
         dist.destroy_process_group()
 
 
-def multi_extra_frame(args, gsm_amd, scenes, dev, gpu, rank, world_size):
+def multi_extra_frame(args, gsm_amd, scenes, dev, gpu, rank, world_size, backend):
     """BASELINE.json configs[3]: config 3's 4K scene partitioned over the N GPUs by tile-row slab
     (gsm_multigpu_render), timed like `value` (barriers, max over ranks); rank 0 gathers the frame.
     Parity of the partitioned frame is checked on the main config; this is a throughput line."""
@@ -418,36 +452,39 @@ def multi_extra_frame(args, gsm_amd, scenes, dev, gpu, rank, world_size):
     r = gsm_amd.GlobalRenderer(device=dev.index, config=cfg)
     mg, err = None, None
     try:
-        mg = gsm_amd.MultiGpuRenderer(r, gsm_amd.MultiGpuRenderer.torch_comm(gpu), rank, world_size)
+        mg = gsm_amd.MultiGpuRenderer.connect(r, rank, world_size, gsm_amd.MultiGpuRenderer.torch_allgather)
     except gsm_amd.RendererError as e:
         err = f"rank {rank}: {e}"
-    ok = torch.tensor([0 if mg is None else 1], dtype=torch.int32, device=dev)
+    ok = torch.tensor([0 if mg is None else 1], dtype=torch.int32, device=dev if backend == "nccl" else "cpu")
     torch.distributed.all_reduce(ok, op=torch.distributed.ReduceOp.MIN)  # collective: all or none
     if int(ok.item()) == 0:
         if mg is not None:
             mg.close()
         r.close()
         return {"error": err or "another rank's gsm_multigpu_create failed"}
-    full_c = torch.zeros((H, W, 4), dtype=torch.float16, device=dev)
-    full_d = torch.zeros((H, W), dtype=torch.float16, device=dev)
+    frame_ptr = mg.frame()[0]
     inp = gsm_amd.GaussianInput(world, harm, n, sh)
     cam = gsm_amd.CameraParams.from_dict(cam_d)
     stream = torch.cuda.current_stream(dev)
 
     def step():
-        mg.render(full_c, full_d, inp, cam, W, H, gather=True, stream=stream)
+        mg.render(None, None, inp, cam, W, H, gather=True, stream=stream, gather_target=frame_ptr if rank == 0 else None)
     for _ in range(3):
         step()
     steps = max(1, min(args.steps, 20))
-    elapsed, _ = timed_loop(steps, step, r, world_size, dev)
+    elapsed, _ = timed_loop(steps, step, r, world_size, dev, backend)
+    timeouts = mg.status()
+    torch.cuda.synchronize()
+    torch.distributed.barrier()
     mg.close()
     r.close()
     return {"value": steps / elapsed, "unit": "frames/s", "n_gpus": world_size, "steps": steps, "warmup": 3,
+            "barrier_timeouts": timeouts,
             "ms_per_step": elapsed / steps * 1e3, "workload": f"{args.multi_extra_config}: {n} gaussians "
             f"{W}x{H} partitioned by tile-row slab over {world_size} GPUs (BASELINE config 4)"}
 
 
-def timed_loop(steps, step, renderer, world_size, dev):
+def timed_loop(steps, step, renderer, world_size, dev, backend="nccl"):
     """K steps between barriers and device syncs; returns (max-over-ranks seconds, blend ms)."""
     import torch
     import torch.distributed as dist
@@ -463,7 +500,7 @@ def timed_loop(steps, step, renderer, world_size, dev):
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if world_size > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     return elapsed, renderer.stage_times_ms()["blend"]

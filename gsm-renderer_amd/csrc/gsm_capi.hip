@@ -238,6 +238,7 @@ gsm_status gsm_debug_partition_push(gsm_renderer* r, void* stream, uint32_t worl
     for (uint32_t p = 0; p < world; ++p) {
         if (!recv_buffers[p]) return GSM_ERR_INVALID_ARGUMENT;
         peers.recv[p] = (gsm::SplatRecord*)recv_buffers[p];
+        peers.cap[p] = r->impl->maxGaussians();  // (gsm_debug.h: each holds max_gaussians records)
     }
     return r->impl->partitionPush((hipStream_t)stream, world, rank, d_counts, peers, d_recv_count);
 }

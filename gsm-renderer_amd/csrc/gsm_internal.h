@@ -43,6 +43,7 @@ static_assert(sizeof(SplatRecord) == 48, "SplatRecord must be 48 B");
 // the receive buffer of every slab owner (peer device pointers; the multi-GPU exchange)
 struct SlabPeers {
     SplatRecord* recv[kMaxSlabs];
+    uint32_t cap[kMaxSlabs];  // records each receive buffer holds (k_part_push writes no further)
 };
 struct PartitionBuffers {
     SplatRecord* records = nullptr;     // [maxG] projected records of the rank's range

@@ -781,7 +781,7 @@ __global__ __launch_bounds__(kProjectBlock) void k_part_push(
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         uint32_t mine = 0;
         for (uint32_t r = 0; r < world; ++r) mine += counts[r * world + rank];
-        *recvCount = mine;
+        *recvCount = min(mine, peers.cap[rank]);
     }
     const uint32_t mask = gid < count ? masks[gid] : 0u;
     const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
@@ -801,6 +801,7 @@ __global__ __launch_bounds__(kProjectBlock) void k_part_push(
         for (uint32_t w = 0; w < wave; ++w) before += wcnt[w][sl];
         const uint64_t pos =
             (uint64_t)dstOff[sl] + blockSlabOffsets[(size_t)sl * gridDim.x + blockIdx.x] + before + rnk[sl];
+        if (pos >= peers.cap[sl]) continue;  // never past an owner's receive buffer
         uint4* dst = (uint4*)(peers.recv[sl] + pos);
         dst[0] = a;
         dst[1] = b;

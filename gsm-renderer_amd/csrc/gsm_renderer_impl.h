@@ -40,6 +40,12 @@ class GlobalRenderer {
                              const uint32_t* devCount = nullptr);
     uint32_t maxGaussians() const { return maxGaussians_; }
     uint32_t tilesY() const { return tilesY_; }
+    uint32_t maxWidth() const { return maxWidth_; }
+    uint32_t maxHeight() const { return maxHeight_; }
+    uint32_t colorBytesPerPixel() const {
+        return config_.color_format == GSM_COLOR_FORMAT_RGBA16F ? 8u
+               : (config_.color_format == GSM_COLOR_FORMAT_RGBA32F ? 16u : 4u);
+    }
     bool halfPrecision() const { return config_.precision == GSM_PRECISION_FLOAT16; }
 
     gsm_status counters(gsm_debug_counters* out);

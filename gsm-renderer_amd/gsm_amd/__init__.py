@@ -242,10 +242,20 @@ _SIGNATURES = {
     "gsm_multigpu_render": ([C.c_void_p, C.c_void_p, C.POINTER(_Input), C.POINTER(_Camera), C.c_uint32,
                              C.c_uint32, C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t, C.c_void_p], C.c_int),
     "gsm_multigpu_debug_counts": ([C.c_void_p, C.POINTER(C.c_uint32)], C.c_int),
+    "gsm_multigpu_prepare": ([C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_void_p), C.c_void_p], C.c_int),
+    "gsm_multigpu_connect": ([C.c_void_p, C.c_void_p], C.c_int),
+    "gsm_multigpu_render_phase": ([C.c_void_p, C.c_int, C.c_void_p, C.POINTER(_Input), C.POINTER(_Camera),
+                                   C.c_uint32, C.c_uint32, C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t,
+                                   C.c_void_p], C.c_int),
+    "gsm_multigpu_frame": ([C.c_void_p, C.POINTER(C.c_void_p), C.POINTER(C.c_size_t)], C.c_int),
+    "gsm_multigpu_status": ([C.c_void_p, C.POINTER(C.c_uint32), C.c_int], C.c_int),
+    "gsm_multigpu_set_timeout_ms": ([C.c_void_p, C.c_uint32], C.c_int),
+    "gsm_multigpu_debug_copy_frame": ([C.c_void_p, C.c_void_p, C.c_size_t, C.c_uint32, C.c_uint32], C.c_int),
 }
 
 SPLAT_RECORD_BYTES = 48  # include/gsm_multigpu.h GSM_SPLAT_RECORD_BYTES
 MAX_SLABS = 16
+MULTIGPU_HANDLE_BYTES = 256  # GSM_MULTIGPU_HANDLE_BYTES
 
 
 def _lib():
@@ -603,17 +613,63 @@ def sort_pairs_u32(keys, values, key_bits: int = 32, stream=None):
 
 class MultiGpuRenderer:
     """gsm_multigpu_* (include/gsm_multigpu.h): one frame of a GlobalRenderer split by tile-row slab
-    across the ranks of an RCCL communicator, records exchanged by peer writes over xGMI and the
-    bands gathered on rank 0 -- all inside libgsm_amd.so, no host round trip in a frame.
-    comm: the ncclComm_t as an int (torch: the NCCL backend's _comm_ptr())."""
+    across the ranks of a node -- counts, records and slab pixels written straight into the owners'
+    exchange memory (peer mappings over xGMI), ordered by device-side flag barriers, the bands
+    gathered on rank 0 -- all inside libgsm_amd.so, no host round trip and no collective in a frame.
 
-    def __init__(self, renderer: "GlobalRenderer", comm: int, rank: int, world_size: int):
+    Two ways to set up (both collective):
+      MultiGpuRenderer(renderer, comm, rank, world)       handles exchanged over an RCCL
+                                                          communicator (torch: _comm_ptr());
+      MultiGpuRenderer.connect(renderer, rank, world, allgather)
+                                                          handles exchanged by the caller:
+                                                          allgather(bytes) -> list of every rank's
+                                                          bytes (e.g. torch.distributed over gloo)."""
+
+    def __init__(self, renderer: "GlobalRenderer", comm: Optional[int], rank: int, world_size: int, _handle=None):
+        self.renderer = renderer
+        self.rank = int(rank)
+        self.world_size = int(world_size)
+        if _handle is not None:
+            self._h = _handle
+            return
         h = C.c_void_p()
         _check(_lib().gsm_multigpu_create(renderer._h, C.c_void_p(int(comm)), int(rank), int(world_size), C.byref(h)),
                "gsm_multigpu_create")
         self._h = h
-        self.renderer = renderer
-        self.world_size = int(world_size)
+
+    @classmethod
+    def prepare(cls, renderer: "GlobalRenderer", rank: int, world_size: int):
+        """gsm_multigpu_prepare: (unconnected renderer, this rank's handle bytes)."""
+        h = C.c_void_p()
+        buf = C.create_string_buffer(MULTIGPU_HANDLE_BYTES)
+        _check(_lib().gsm_multigpu_prepare(renderer._h, int(rank), int(world_size), C.byref(h), buf),
+               "gsm_multigpu_prepare")
+        return cls(renderer, None, rank, world_size, _handle=h), bytes(buf.raw)
+
+    def connect_handles(self, handles):
+        """gsm_multigpu_connect with every rank's handle bytes, in rank order."""
+        blob = b"".join(bytes(x) for x in handles)
+        if len(blob) != MULTIGPU_HANDLE_BYTES * self.world_size:
+            raise ValueError("one handle per rank expected")
+        _check(_lib().gsm_multigpu_connect(self._h, C.c_char_p(blob)), "gsm_multigpu_connect")
+        return self
+
+    @classmethod
+    def connect(cls, renderer: "GlobalRenderer", rank: int, world_size: int, allgather):
+        mg, mine = cls.prepare(renderer, rank, world_size)
+        try:
+            return mg.connect_handles(allgather(mine))
+        except Exception:
+            mg.close()
+            raise
+
+    @staticmethod
+    def torch_allgather(data: bytes):
+        """Every rank's bytes over torch.distributed's default group (any backend)."""
+        import torch.distributed as dist
+        out = [None] * dist.get_world_size()
+        dist.all_gather_object(out, data)
+        return out
 
     @staticmethod
     def torch_comm(device) -> int:
@@ -621,18 +677,66 @@ class MultiGpuRenderer:
         import torch.distributed as dist
         return int(dist.group.WORLD._get_backend(torch.device("cuda", int(device)))._comm_ptr())
 
-    def render(self, color_texture, depth_texture, input: GaussianInput, camera: CameraParams, width: int,
-               height: int, gather: bool = True, stream=None, color_pitch: Optional[int] = None,
-               depth_pitch: Optional[int] = None):
+    def _args(self, input, camera, color_texture, depth_texture, width, color_pitch, depth_pitch):
         inp = _Input(_ptr(input.gaussians), _ptr(input.harmonics), int(input.gaussian_count),
                      int(input.sh_components))
         cam = _camera_struct(camera)
         cp = color_pitch if color_pitch is not None else int(width) * 8
         dp = depth_pitch if depth_pitch is not None else int(width) * 2
+        return inp, cam, cp, dp
+
+    def render(self, color_texture, depth_texture, input: GaussianInput, camera: CameraParams, width: int,
+               height: int, gather: bool = True, stream=None, color_pitch: Optional[int] = None,
+               depth_pitch: Optional[int] = None, gather_target=None):
+        """One frame.  gather: rank 0 receives the whole frame -- in color_texture (a copy of the
+        library frame), or, with gather_target = self.frame()[0], in the library frame itself; the
+        other ranks' color_texture is then unused (may be None)."""
+        self.render_phases(range(4), color_texture, depth_texture, input, camera, width, height, gather, stream,
+                           color_pitch, depth_pitch, gather_target)
+
+    def render_phases(self, phases, color_texture, depth_texture, input: GaussianInput, camera: CameraParams,
+                      width: int, height: int, gather: bool = True, stream=None, color_pitch: Optional[int] = None,
+                      depth_pitch: Optional[int] = None, gather_target=None):
+        """gsm_multigpu_render_phase for each phase in `phases` (virtual ranks: phase p of every rank
+        before phase p + 1 of any, include/gsm_multigpu.h)."""
+        inp, cam, cp, dp = self._args(input, camera, color_texture, depth_texture, width, color_pitch, depth_pitch)
         col = _ptr(color_texture)
-        st = _lib().gsm_multigpu_render(self._h, _stream_handle(stream), C.byref(inp), C.byref(cam), int(width),
-                                        int(height), col, cp, _ptr(depth_texture), dp, col if gather else None)
-        _check(st, "gsm_multigpu_render")
+        if gather:  # rank 0: the caller's target (a copy) or else the library frame; others: any non-NULL
+            if gather_target is not None:
+                g = _ptr(gather_target)
+            elif self.rank == 0:
+                g = col if col is not None else self.frame()[0]
+            else:
+                g = 1
+        else:
+            g = None
+        for p in phases:
+            st = _lib().gsm_multigpu_render_phase(self._h, int(p), _stream_handle(stream), C.byref(inp), C.byref(cam),
+                                                  int(width), int(height), col, cp, _ptr(depth_texture), dp, g)
+            _check(st, f"gsm_multigpu_render_phase({p})")
+
+    def frame(self):
+        """(device pointer, pitch bytes) of rank 0's gathered frame; (None, 0) elsewhere."""
+        p = C.c_void_p()
+        pitch = C.c_size_t()
+        _check(_lib().gsm_multigpu_frame(self._h, C.byref(p), C.byref(pitch)), "gsm_multigpu_frame")
+        return p.value, int(pitch.value)
+
+    def copy_frame(self, width: int, height: int) -> np.ndarray:
+        """Rank 0: the gathered rgba16f frame as uint16 bits [height, width, 4] (synchronous)."""
+        out = np.empty((int(height), int(width), 4), np.uint16)
+        _check(_lib().gsm_multigpu_debug_copy_frame(self._h, out.ctypes.data_as(C.c_void_p), int(width) * 8,
+                                                    int(width), int(height)), "gsm_multigpu_debug_copy_frame")
+        return out
+
+    def status(self, clear: bool = False) -> int:
+        """Barrier timeouts since create (0 on a healthy run)."""
+        out = C.c_uint32(0)
+        _check(_lib().gsm_multigpu_status(self._h, C.byref(out), 1 if clear else 0), "gsm_multigpu_status")
+        return int(out.value)
+
+    def set_timeout_ms(self, ms: int):
+        _check(_lib().gsm_multigpu_set_timeout_ms(self._h, int(ms)), "gsm_multigpu_set_timeout_ms")
 
     def counts(self) -> np.ndarray:
         out = (C.c_uint32 * (self.world_size * self.world_size))()

@@ -7,18 +7,22 @@
  *   1. every rank projects its contiguous range of gaussian ids once
  *      (gsm_global_project_partition) and gets, per slab, the records of the
  *      gaussians whose ellipse meets a tile of that slab, in ascending id order;
- *   2. an all-to-all(v) over the fabric (RCCL) delivers slab s's records to its owner,
- *      concatenated in source-rank order (so ascending id order overall);
+ *   2. the records reach slab s's owner concatenated in source-rank order (so
+ *      ascending id order overall);
  *   3. the owner, with gsm_global_set_tile_rows(slab), renders its rows from them
  *      (gsm_global_render_records).
  * The slab's pixels are bit-identical to a single-GPU gsm_global_render of the frame:
  * projection is per gaussian, and the ascending-id concatenation preserves the
  * stable-sort tie order (determinism contract).
  *
- * gsm_multigpu_* run the whole protocol inside the library over the caller's RCCL
- * communicator (steps 1-3 plus the band gather), enqueue-only with no host round trip;
- * gsm_global_project_partition / gsm_global_render_records remain for callers that move
- * the records themselves.
+ * gsm_multigpu_* run the whole protocol inside the library with no host round trip and no
+ * collective library in the frame: every rank owns one uncached "exchange" allocation (control
+ * words, the count matrix, its receive buffer of records and, on rank 0, the gathered frame),
+ * the ranks open each other's exchange allocations once (IPC handles), and per frame the
+ * counts, the records and the slab pixels are written straight into the owners' memory by the
+ * producing kernels (xGMI stores between GPUs), ordered by device-side flag barriers.
+ * gsm_global_project_partition / gsm_global_render_records remain for callers that move the
+ * records themselves.
  */
 #ifndef GSM_MULTIGPU_H
 #define GSM_MULTIGPU_H
@@ -31,6 +35,7 @@ extern "C" {
 
 #define GSM_SPLAT_RECORD_BYTES 48 /* projected gaussian: render data, blend record, tile rect */
 #define GSM_MAX_SLABS 16
+#define GSM_MULTIGPU_HANDLE_BYTES 256 /* one rank's exchange handle (gsm_multigpu_handle) */
 
 /* Project gaussians [first, first + count) of `input` (count <= config.max_gaussians) for a
  * width x height frame and pack, slab by slab, the records of those that meet slab s =
@@ -54,37 +59,86 @@ gsm_status gsm_global_render_records(gsm_renderer *renderer, void *stream, const
                                      void *color_rgba16f, size_t color_pitch_bytes,
                                      void *depth_r16f, size_t depth_pitch_bytes);
 
-/* --- the frame across a communicator ------------------------------------------------------
- * One renderer per rank (gsm_global_create on that rank's GPU, config.max_gaussians >= the
- * frame's gaussian count) and the rank's RCCL communicator (ncclComm_t as void*; libgsm_amd
- * loads RCCL at run time and uses the copy the process has already loaded, so a communicator
- * from torch.distributed works).  Collective: every rank of the communicator calls create,
- * each frame and destroy.  create allocates the send / receive buffers (48 B x max_gaussians
- * each) and opens every peer's receive buffer once from its IPC handle; GSM_ERR_UNSUPPORTED
- * when no RCCL can be loaded, GSM_ERR_INVALID_ARGUMENT when rank / world_size do not match the
- * communicator or world_size > GSM_MAX_SLABS. */
+/* --- the frame across the ranks of a node ---------------------------------------------------
+ * One renderer per rank (gsm_global_create on that rank's GPU; every rank with the same
+ * max_width / max_height).  Set-up is collective and happens once, in two steps around an
+ * exchange the caller performs with any transport (torch.distributed, MPI, sockets, ...):
+ *   gsm_multigpu_prepare   allocates this rank's exchange memory (uncached device memory:
+ *                          control words, 2 x W x W counts, max_gaussians x 48-B records,
+ *                          and on rank 0 the gathered frame, max_width x max_height pixels)
+ *                          and writes its GSM_MULTIGPU_HANDLE_BYTES handle into `handle`;
+ *   (caller)               all-gathers the handles: all[r * GSM_MULTIGPU_HANDLE_BYTES] = rank r's;
+ *   gsm_multigpu_connect   opens every peer's exchange memory (hipIpcOpenMemHandle; a handle
+ *                          from the same process is used directly) and checks that the ranks
+ *                          agree on the world and the frame limits.
+ * The frame capacity is the smallest max_gaussians of all ranks (a slab receives every id at
+ * most once): a frame with more gaussians returns GSM_ERR_INVALID_GAUSSIAN_COUNT on every rank
+ * alike, before anything is enqueued.
+ * gsm_multigpu_create does all three over an RCCL communicator (ncclComm_t as void*;
+ * libgsm_amd loads RCCL at run time and uses the copy the process has already loaded, so a
+ * communicator from torch.distributed works): GSM_ERR_UNSUPPORTED when no RCCL can be loaded,
+ * GSM_ERR_INVALID_ARGUMENT when rank / world_size do not match the communicator or
+ * world_size > GSM_MAX_SLABS. */
 typedef struct gsm_multigpu gsm_multigpu;
+gsm_status gsm_multigpu_prepare(gsm_renderer *renderer, int rank, int world_size, gsm_multigpu **out,
+                                void *handle);
+gsm_status gsm_multigpu_connect(gsm_multigpu *multigpu, const void *all_handles);
 gsm_status gsm_multigpu_create(gsm_renderer *renderer, void *nccl_comm, int rank, int world_size,
                                gsm_multigpu **out);
 void gsm_multigpu_destroy(gsm_multigpu *multigpu);
 
-/* One frame of gsm_global_render (GlobalRenderer.swift:201-238) across the communicator.  Every
- * rank passes the same input (device pointers on its own GPU; it reads only its id range
- * [r * ceil(N / W), +ceil(N / W))), camera and size.  Rank r owns tile rows
- * [r * ceil(tiles_y / W), +ceil(tiles_y / W)) and writes them into its full-frame-addressed
- * color / depth targets; per frame, on `stream`: projection of its ids, all-gather of the
- * per-slab record counts, peer writes of every record into its owner's receive buffer over
- * xGMI, one ordering all-reduce, the slab render with the record count read on the device, and,
- * when gather_color is set on rank 0 (it must then equal color, with color_pitch = 8 * width)
- * and on every other rank (any non-NULL value), the bands sent to rank 0's frame.  No host
- * synchronisation anywhere in the frame. */
+/* One frame of gsm_global_render (GlobalRenderer.swift:201-238) across the ranks.  Collective:
+ * every rank calls it once per frame with the same input (device pointers on its own GPU; it
+ * reads only its id range [r * ceil(N / W), +ceil(N / W))), camera, size and gather choice.
+ * Rank r owns tile rows [r * ceil(tiles_y / W), +ceil(tiles_y / W)).  Per frame, on `stream`:
+ *   1. projection of the rank's ids, per-slab record counts written into every rank's count
+ *      matrix, flag barrier;
+ *   2. every record written straight into its slab owner's receive buffer (offsets from the
+ *      count matrix: rank order), flag barrier;
+ *   3. the owner renders its rows from the received records (their count read on the device);
+ *      colour goes to rank 0's gathered frame when gathering, else to the rank's own color
+ *      target (full-frame addressed, rows outside the slab untouched); depth always to the
+ *      rank's own depth target (nullable);
+ *   4. gathering: every rank signals rank 0, whose stream waits for all slabs; a gather_color
+ *      other than gsm_multigpu_frame's buffer then receives a copy of the frame.
+ * Gathering: gather_color non-NULL on every rank (ranks other than 0 pass any non-NULL value;
+ * their color may then be NULL).  No host synchronisation anywhere in the frame.  A barrier
+ * that waits longer than the timeout (default 10 s; a peer that never calls) gives up, counts
+ * the event (gsm_multigpu_status) and lets the frame finish with undefined pixels: no wait on
+ * the device is unbounded. */
 gsm_status gsm_multigpu_render(gsm_multigpu *multigpu, void *stream, const gsm_gaussian_input *input,
                                const gsm_camera_params *camera, uint32_t width, uint32_t height,
                                void *color_rgba16f, size_t color_pitch_bytes, void *depth_r16f,
                                size_t depth_pitch_bytes, void *gather_color);
 
+/* Rank 0's gathered frame (library memory, valid until destroy): *color = its device pointer,
+ * *pitch_bytes = max_width x bytes per pixel of the configured colour format.  Passing it as
+ * gather_color skips the copy.  Other ranks: *color = NULL. */
+gsm_status gsm_multigpu_frame(gsm_multigpu *multigpu, void **color, size_t *pitch_bytes);
+
+/* Barrier timeouts since create (or the last clear), synchronous: 0 on a healthy run. */
+gsm_status gsm_multigpu_status(gsm_multigpu *multigpu, uint32_t *timeouts, int clear);
+/* Barrier timeout in milliseconds (default 10000, at least 1). */
+gsm_status gsm_multigpu_set_timeout_ms(gsm_multigpu *multigpu, uint32_t ms);
+
+/* Rank 0: copy rows [0, height) x width pixels of the gathered frame into host memory (dst_pitch
+ * bytes per row), synchronous (after the frame's stream work); GSM_ERR_INVALID_ARGUMENT elsewhere. */
+gsm_status gsm_multigpu_debug_copy_frame(gsm_multigpu *multigpu, void *host_dst, size_t dst_pitch_bytes,
+                                         uint32_t width, uint32_t height);
+
 /* The last frame's world x world record counts (row = source rank, column = slab), synchronous. */
 gsm_status gsm_multigpu_debug_counts(gsm_multigpu *multigpu, uint32_t *host_counts);
+
+/* gsm_multigpu_render in four phases (0: projection + counts + barrier; 1: records + barrier;
+ * 2: slab render + the gather signal; 3: rank 0's gather wait + copy); render = phases 0..3.
+ * For W ranks driven from ONE host thread (virtual ranks of a test or a timing tool, e.g. W
+ * renderers on one GPU sharing one stream): issue phase p of every rank before phase p + 1 of
+ * any, so that every barrier waits only for work enqueued before it. */
+gsm_status gsm_multigpu_render_phase(gsm_multigpu *multigpu, int phase, void *stream,
+                                     const gsm_gaussian_input *input, const gsm_camera_params *camera,
+                                     uint32_t width, uint32_t height, void *color_rgba16f,
+                                     size_t color_pitch_bytes, void *depth_r16f, size_t depth_pitch_bytes,
+                                     void *gather_color);
 
 #ifdef __cplusplus
 }

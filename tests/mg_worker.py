@@ -1,0 +1,104 @@
+"""One rank of the multi-GPU frame (include/gsm_multigpu.h) as its own process: the worker that
+tests/test_multigpu_ipc.py starts W times on one GPU.  Handles are exchanged over torch.distributed
+(gloo, 127.0.0.1); everything in the frame -- counts, records pushed into the peers' receive buffers
+through their IPC mappings, the flag barriers across the processes, the slab render, the band written
+straight into rank 0's gathered frame -- is the product path of libgsm_amd.so.
+
+Frames (same scene every rank, generated from the seed):
+  A  gathered into the library frame (gather_target = MultiGpuRenderer.frame()), read back on rank 0
+  B  the next camera, gathered into a caller tensor (the library's copy)
+  C  not gathered: every rank writes its band into its own colour/depth targets
+Rank 0 writes A and B, and every rank its band of C, as .npy files into --out, plus status.json."""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "gsm-renderer_amd"))
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--rank", type=int, required=True)
+    p.add_argument("--world", type=int, required=True)
+    p.add_argument("--port", type=int, required=True)
+    p.add_argument("--out", required=True)
+    p.add_argument("--n", type=int, default=40_000)
+    p.add_argument("--width", type=int, default=640)
+    p.add_argument("--height", type=int, default=360)
+    p.add_argument("--sh", type=int, default=16)
+    p.add_argument("--precision", type=int, default=1)
+    p.add_argument("--seed", type=int, default=11)
+    p.add_argument("--cap", type=int, default=0, help="max_gaussians of this rank (0: n)")
+    a = p.parse_args()
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(a.port)
+    import torch
+    import torch.distributed as dist
+
+    import gsm_amd
+    from gsm_amd import scenes
+
+    dist.init_process_group("gloo", rank=a.rank, world_size=a.world)
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    n, w, h = a.n, a.width, a.height
+    world_np, harm_np, cam_d = scenes.gen_scene(n, w, h, a.sh, a.precision, seed=a.seed)
+    wt = torch.from_numpy(world_np.view(np.uint8).reshape(-1).copy()).to(dev)
+    ht = torch.from_numpy(harm_np.view(np.uint8).reshape(-1).copy()).to(dev)
+    inp = gsm_amd.GaussianInput(wt, ht, n, a.sh)
+    cfg = gsm_amd.RendererConfig(max_gaussians=a.cap or n, max_width=w, max_height=h, precision=a.precision,
+                                 gaussian_color_space=0)
+    rend = gsm_amd.GlobalRenderer(device=0, config=cfg)
+    mg = gsm_amd.MultiGpuRenderer.connect(rend, a.rank, a.world, gsm_amd.MultiGpuRenderer.torch_allgather)
+    mg.set_timeout_ms(20000)
+    result = {"rank": a.rank}
+    stream = torch.cuda.current_stream(dev)
+    try:
+        if a.cap and a.cap < n:  # every rank must refuse the frame alike, before any barrier
+            try:
+                mg.render(None, None, inp, gsm_amd.CameraParams.from_dict(cam_d), w, h, gather=True, stream=stream)
+                result["refused"] = False
+            except gsm_amd.RendererError as e:
+                result["refused"] = e.status == gsm_amd.Status.INVALID_GAUSSIAN_COUNT
+            return
+        frame_ptr, _ = mg.frame()
+        # A: into the library frame (zero copy)
+        for _ in range(2):  # a second frame reuses every mapping and flag
+            mg.render(None, None, inp, gsm_amd.CameraParams.from_dict(cam_d), w, h, gather=True, stream=stream,
+                      gather_target=frame_ptr if a.rank == 0 else None)
+        torch.cuda.synchronize()
+        dist.barrier()
+        if a.rank == 0:
+            np.save(os.path.join(a.out, "frame_a.npy"), mg.copy_frame(w, h))
+        # B: the next camera, gathered into a caller tensor on rank 0
+        cam_b = scenes.orbit_camera(w, h, 3.0)
+        color = torch.full((h, w, 4), float("nan"), dtype=torch.float16, device=dev) if a.rank == 0 else None
+        mg.render(color, None, inp, gsm_amd.CameraParams.from_dict(cam_b), w, h, gather=True, stream=stream)
+        torch.cuda.synchronize()
+        if a.rank == 0:
+            np.save(os.path.join(a.out, "frame_b.npy"), color.view(torch.int16).cpu().numpy().view(np.uint16))
+        # C: no gather -- every rank's band in its own targets
+        color = torch.full((h, w, 4), float("nan"), dtype=torch.float16, device=dev)
+        depth = torch.full((h, w), float("nan"), dtype=torch.float16, device=dev)
+        mg.render(color, depth, inp, gsm_amd.CameraParams.from_dict(cam_d), w, h, gather=False, stream=stream)
+        torch.cuda.synchronize()
+        np.save(os.path.join(a.out, f"band_c_color_{a.rank}.npy"), color.view(torch.int16).cpu().numpy().view(np.uint16))
+        np.save(os.path.join(a.out, f"band_c_depth_{a.rank}.npy"), depth.view(torch.int16).cpu().numpy().view(np.uint16))
+        result["counts"] = mg.counts().tolist()
+        result["timeouts"] = mg.status()
+    finally:
+        torch.cuda.synchronize()
+        dist.barrier()  # no rank unmaps its exchange memory while a peer may still write into it
+        mg.close()
+        rend.close()
+        with open(os.path.join(a.out, f"status_{a.rank}.json"), "w") as f:
+            json.dump(result, f)
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

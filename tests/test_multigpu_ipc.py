@@ -1,0 +1,153 @@
+"""The N > 1 product path of include/gsm_multigpu.h with real processes, on one MI355X.
+
+Two (three) rank processes share GPU 0 (tests/mg_worker.py): each owns an uncached exchange
+allocation, the handles go over torch.distributed (gloo) and every rank opens its peers' allocations
+with hipIpcOpenMemHandle -- the set-up the 8-GPU node runs, where the mappings cross xGMI.  Per frame
+every record is stored by k_part_push straight into another process's receive buffer, the count
+matrix rows and the barrier flags cross the processes, the slab blends write their pixels into rank
+0's gathered frame, and rank 0's stream waits for every slab.  The frames must equal the oracle's bit
+for bit, with no barrier timeout.  (RCCL cannot run two ranks on one GPU -- "Duplicate GPU detected",
+DESIGN.md 7 -- which is one reason the frame uses no collective library.)
+
+The same kernels run for W virtual ranks in one process (phases issued rank by rank on one stream,
+include/gsm_multigpu.h gsm_multigpu_render_phase) up to config 4, 5M / SH3 / 4K over 8 ranks."""
+import json
+import math
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _run_ranks(tmp_path, world, extra=(), timeout=150):
+    port = _free_port()
+    env = dict(os.environ)
+    procs = [subprocess.Popen([sys.executable, "-u", os.path.join(ROOT, "tests", "mg_worker.py"), "--rank", str(r),
+                               "--world", str(world), "--port", str(port), "--out", str(tmp_path), *extra],
+                              stdout=subprocess.PIPE, stderr=subprocess.STDOUT, env=env) for r in range(world)]
+    outs = []
+    try:
+        for p in procs:
+            out, _ = p.communicate(timeout=timeout)
+            outs.append(out.decode(errors="replace"))
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    for r, (p, o) in enumerate(zip(procs, outs)):
+        assert p.returncode == 0, f"rank {r} exited {p.returncode}:\n{o[-3000:]}"
+    return [json.load(open(os.path.join(tmp_path, f"status_{r}.json"))) for r in range(world)]
+
+
+@pytest.mark.parametrize("world,n,w,h,sh,prec", [(2, 40_000, 640, 360, 16, 1), (3, 30_000, 1280, 720, 4, 0)])
+def test_processes_on_one_gpu_render_the_oracle_frame(oracle, tmp_path, world, n, w, h, sh, prec):
+    from gsm_amd import scenes
+    st = _run_ranks(tmp_path, world, ["--n", str(n), "--width", str(w), "--height", str(h), "--sh", str(sh),
+                                      "--precision", str(prec)])
+    assert all(s["timeouts"] == 0 for s in st)
+    world_np, harm_np, cam_d = scenes.gen_scene(n, w, h, sh, prec, seed=11)
+    ref = oracle.render(world_np, harm_np, sh, cam_d, w, h, max_gaussians=n)
+    # A: gathered into the library frame across the processes
+    assert np.array_equal(np.load(tmp_path / "frame_a.npy"), ref["color"])
+    # B: next camera, the library's copy into the caller's tensor
+    ref_b = oracle.render(world_np, harm_np, sh, scenes.orbit_camera(w, h, 3.0), w, h, max_gaussians=n)
+    assert np.array_equal(np.load(tmp_path / "frame_b.npy"), ref_b["color"])
+    # C: bands in each rank's own targets, composed here
+    tiles_y = (h + 15) // 16
+    per = math.ceil(tiles_y / world)
+    for r in range(world):
+        y0, y1 = min(r * per * 16, h), min((r + 1) * per * 16, h)
+        col = np.load(tmp_path / f"band_c_color_{r}.npy")
+        dep = np.load(tmp_path / f"band_c_depth_{r}.npy")
+        assert np.array_equal(col[y0:y1], ref["color"][y0:y1])
+        assert np.array_equal(dep[y0:y1], ref["depth"][y0:y1])
+        nan_rows = np.concatenate([col[:y0], col[y1:]]).reshape(-1)
+        assert np.all((nan_rows & 0x7C00) == 0x7C00)  # rows of other slabs untouched (NaN)
+    # every rank holds the same count matrix; its column sums are the slabs' receive counts
+    cm = np.array(st[0]["counts"], np.int64)
+    assert all(np.array_equal(np.array(s["counts"]), cm) for s in st)
+    with_tiles = int(np.count_nonzero(ref["tile_counts"]))
+    assert with_tiles <= cm.sum() <= with_tiles * world
+
+
+def test_processes_refuse_a_frame_over_the_smallest_capacity(tmp_path):
+    """A rank sized for less than the frame: every rank returns INVALID_GAUSSIAN_COUNT before any
+    barrier (no rank waits, no peer's receive buffer is overrun)."""
+    st = _run_ranks(tmp_path, 2, ["--n", "20000", "--cap", "15000"])
+    assert all(s["refused"] for s in st)
+
+
+def _virtual_frame(gsm, cuda, world, n, w, h, sh, prec, seed, cams):
+    from gsm_amd import scenes
+    world_np, harm_np, cam_d = scenes.gen_scene(n, w, h, sh, prec, seed=seed)
+    wt = cuda.from_numpy(world_np.view(np.uint8).reshape(-1).copy()).cuda()
+    ht = cuda.from_numpy(harm_np.view(np.uint8).reshape(-1).copy()).cuda()
+    del world_np, harm_np
+    inp = gsm.GaussianInput(wt, ht, n, sh)
+    cfg = gsm.RendererConfig(max_gaussians=n, max_width=w, max_height=h, precision=prec, gaussian_color_space=0)
+    rends = [gsm.GlobalRenderer(device=0, config=cfg) for _ in range(world)]
+    pre = [gsm.MultiGpuRenderer.prepare(r, k, world) for k, r in enumerate(rends)]
+    handles = [hd for _, hd in pre]
+    mgs = [m.connect_handles(handles) for m, _ in pre]
+    frame_ptr, _ = mgs[0].frame()
+    stream = cuda.cuda.current_stream()
+    frames = []
+    for cam in cams:
+        cp = gsm.CameraParams.from_dict(cam)
+        for ph in range(4):  # phase p of every rank before phase p + 1 of any (one stream)
+            for k, m in enumerate(mgs):
+                m.render_phases([ph], None, None, inp, cp, w, h, gather=True, stream=stream,
+                                gather_target=frame_ptr if k == 0 else None)
+        cuda.cuda.synchronize()
+        frames.append(mgs[0].copy_frame(w, h))
+    counts = mgs[0].counts()
+    timeouts = [m.status() for m in mgs]
+    for m in mgs:
+        m.close()
+    for r in rends:
+        r.close()
+    return frames, counts, timeouts
+
+
+@pytest.mark.parametrize("world,n,w,h,prec", [(2, 40_000, 640, 360, 1), (3, 60_000, 1280, 720, 1),
+                                              (8, 50_000, 640, 360, 0), (16, 30_000, 640, 360, 1)])
+def test_virtual_ranks_product_path(gsm, cuda, oracle, world, n, w, h, prec):
+    """W ranks of one process through the product kernels (barriers, pushes, gather into rank 0's
+    frame), two cameras: the second frame reuses the parity-double-buffered count matrix."""
+    from gsm_amd import scenes
+    sh = 16 if prec else 4
+    cams = [scenes.make_camera(w, h), scenes.orbit_camera(w, h, 5.0)]
+    frames, counts, timeouts = _virtual_frame(gsm, cuda, world, n, w, h, sh, prec, 78, cams)
+    assert timeouts == [0] * world
+    world_np, harm_np, _ = scenes.gen_scene(n, w, h, sh, prec, seed=78)
+    for got, cam in zip(frames, cams):
+        ref = oracle.render(world_np, harm_np, sh, cam, w, h, max_gaussians=n)
+        assert np.array_equal(got, ref["color"])
+    assert counts.shape == (world, world)
+
+
+def test_config4_virtual_ranks_full_size(gsm, cuda, oracle):
+    """BASELINE config 4: 5M gaussians, SH3, 3840x2160, fp16, partitioned over 8 ranks (virtual ranks
+    on one GPU, the product kernels and uncached exchange buffers) -- bit-exact with the oracle."""
+    from gsm_amd import scenes
+    c = scenes.CONFIGS["cfg3_5m_sh3_4k_f16"]
+    n, w, h, sh, prec = c["count"], c["width"], c["height"], c["sh"], c["precision"]
+    world_np, harm_np, cam_d = scenes.gen_scene(n, w, h, sh, prec, seed=42)
+    frames, counts, timeouts = _virtual_frame(gsm, cuda, 8, n, w, h, sh, prec, 42, [cam_d])
+    assert timeouts == [0] * 8
+    ref = oracle.render(world_np, harm_np, sh, cam_d, w, h, max_gaussians=n, nthreads=min(16, os.cpu_count() or 1))
+    assert np.array_equal(frames[0], ref["color"])
+    assert counts.sum() >= int(np.count_nonzero(ref["tile_counts"]))

@@ -49,7 +49,6 @@ struct PartitionBuffers {
     SplatRecord* records = nullptr;     // [maxG] projected records of the rank's range
     uint32_t* masks = nullptr;          // [maxG] slabs each gaussian meets
     uint32_t* blockSlabCounts = nullptr;  // [kMaxSlabs * blocks]
-    uint32_t* slabBase = nullptr;       // [kMaxSlabs]
 };
 
 // Device buffers of one renderer (the GlobalViewResources analogue, GlobalResources.swift:6-362).
@@ -134,18 +133,21 @@ void launch_partition_counts(bool halfInput, uint32_t shDegree, const void* worl
                              const ProjectArgs& args, const SlabTable& slabs, const PartitionBuffers& B,
                              const float2* sincos, uint32_t* sendCounts, hipStream_t stream);
 void launch_partition_push(const ProjectArgs& args, uint32_t world, uint32_t rank, const PartitionBuffers& B,
-                           const uint32_t* counts, const SlabPeers& peers, uint32_t* recvCount, hipStream_t stream);
+                           const uint32_t* counts, const SlabPeers& peers, uint32_t* recvCount, const SlabTable& slabs,
+                           hipStream_t stream);
 // received records -> per-gaussian arrays + tile counts of the renderer's rows (replaces project)
 void launch_records_in(const void* records, const ProjectArgs& args, const DeviceArena& A,
                        hipStream_t stream, const uint32_t* devCount = nullptr);
+// devCount (nullable): the gaussian count on the device (records path); only its blocks are scanned
 void launch_scan_blocks(uint32_t numBlocks, const ProjectArgs& args, const DeviceArena& A,
-                        hipStream_t stream);
+                        hipStream_t stream, const uint32_t* devCount = nullptr);
 // the same scan for any array of nb per-block sums: exclusive scan in place, the total clamped
 // to cap into hdr (overflow flag when it exceeds cap), *queue = 0
 void launch_scan_sums(uint32_t* sums, uint32_t nb, uint32_t cap, TileAssignmentHeader* hdr, uint32_t* queue,
                       hipStream_t stream);
 // duplicate-with-keys (GlobalShaders.metal:623-678 fused with :266-295)
-void launch_scatter(const ProjectArgs& args, const DeviceArena& A, hipStream_t stream);
+void launch_scatter(const ProjectArgs& args, const DeviceArena& A, hipStream_t stream,
+                    const uint32_t* devCount = nullptr);
 // the blend's half-tile lists from the sorted values (skip flags, k_scatter), tiles [tileBegin, +numTiles)
 void launch_half_lists(const uint32_t* sortedVals, uint32_t tileBegin, uint32_t numTiles, const DeviceArena& A,
                        uint32_t tileCount, hipStream_t stream);

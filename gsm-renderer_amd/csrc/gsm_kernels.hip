@@ -359,18 +359,87 @@ __global__ __launch_bounds__(kProjectBlock) void k_project(
 
 // ---------------------------------------------------------------------------
 // 1b. multi-GPU partition: a rank projects its range of gaussians once,
-//     keeps every projected gaussian whose ellipse meets a tile of slab s, and packs its
-//     48-byte splat record into slab s's segment of the send buffer in ascending id order.
-//     The slab owner rebuilds keys from the records (k_records_in + the usual scatter), so a
-//     record crosses the fabric once per (gaussian, slab), not once per tile.
+//     keeps every projected gaussian whose ellipse meets a tile of slab s, and sends its
+//     48-byte splat record to slab s's owner in ascending id order.  The record's last word
+//     carries the tile answers of the slab's part of the rect (rects of <= 32 tiles), so the
+//     owner rebuilds keys from it (k_records_in + the usual scatter) without repeating the
+//     tile tests; a record crosses the fabric once per (gaussian, slab), not once per tile.
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ bool meets_rows(const ProjOut& o, int rowBegin, int rowEnd) {
-    if (!o.countable) return false;
-    const int ty0 = max((int)o.bounds.z, rowBegin), ty1 = min((int)o.bounds.w, rowEnd - 1);
-    for (int ty = ty0; ty <= ty1; ++ty)
-        for (int tx = (int)o.bounds.x; tx <= (int)o.bounds.y; ++tx)
-            if (intersects_tile(tx, ty, o.cmx, o.cmy, o.k, o.w)) return true;
-    return false;
+// The tile tests of a block's gaussians shared out over its threads (as in k_project): every
+// (gaussian, tile of its rect) candidate on one thread, consecutive candidates on consecutive
+// threads, owner from an LDS table for rects of <= kCandRect tiles, by binary search beyond.
+// hit(lo, k, ty) is called for every candidate k (ty-major, tx-minor over the rect) of gaussian
+// lo whose ellipse meets tile row ty.  Ends with a barrier.
+struct TileTestLds {
+    static constexpr uint32_t kCandCap = 4096, kCandRect = 64;
+    static constexpr uint16_t kSearch = 0xFFFFu;
+    float4 ell[kProjectBlock];   // cmx, cmy, conic A, conic B
+    float2 ell2[kProjectBlock];  // conic C, level w
+    uint32_t off[kProjectBlock];  // exclusive candidate offsets
+    uint32_t rect[kProjectBlock]; // x0 | rw << 16
+    int ty0[kProjectBlock];
+    uint16_t cand[kCandCap];
+    uint32_t scan[kProjectBlock / 64];
+};
+template <class Hit>
+__device__ __forceinline__ void block_tile_tests(TileTestLds& L, const ProjOut& o, uint32_t area, int ty0, Hit&& hit) {
+    const uint32_t tid = threadIdx.x;
+    L.ell[tid] = make_float4(o.cmx, o.cmy, o.k.A, o.k.B);
+    L.ell2[tid] = make_float2(o.k.C, o.w);
+    L.rect[tid] = ((uint32_t)(int)o.bounds.x & 0xFFFFu) | ((uint32_t)((int)o.bounds.y - (int)o.bounds.x + 1) << 16);
+    L.ty0[tid] = ty0;
+    uint32_t total;
+    const uint32_t coff = block_exclusive_scan<kProjectBlock>(area, L.scan, &total);
+    L.off[tid] = coff;
+    const uint32_t nCand = min(total, TileTestLds::kCandCap);
+    for (uint32_t i = tid; i < nCand; i += kProjectBlock) L.cand[i] = TileTestLds::kSearch;
+    __syncthreads();
+    if (area <= TileTestLds::kCandRect)
+        for (uint32_t k = 0; k < area && coff + k < TileTestLds::kCandCap; ++k) L.cand[coff + k] = (uint16_t)((tid << 8) | k);
+    __syncthreads();
+    for (uint32_t c = tid; c < total; c += kProjectBlock) {
+        uint32_t lo, k;
+        const uint32_t v = c < TileTestLds::kCandCap ? (uint32_t)L.cand[c] : (uint32_t)TileTestLds::kSearch;
+        if (v != TileTestLds::kSearch) {
+            lo = v >> 8;
+            k = v & 0xFFu;
+        } else {
+            lo = 0;
+            uint32_t hi = kProjectBlock - 1;  // owner: the largest g with off[g] <= c
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi + 1) >> 1;
+                if (L.off[mid] <= c) lo = mid;
+                else hi = mid - 1;
+            }
+            k = c - L.off[lo];
+        }
+        const uint32_t rect = L.rect[lo], rw = rect >> 16;
+        // k / rw from the hardware reciprocal (within one of the quotient), then corrected exactly
+        uint32_t row = (uint32_t)((float)k * __builtin_amdgcn_rcpf((float)rw));
+        if (row * rw > k) row--;
+        else if ((row + 1u) * rw <= k) row++;
+        const int ty = L.ty0[lo] + (int)row, tx = (int)(rect & 0xFFFFu) + (int)(k - row * rw);
+        const float4 e = L.ell[lo];
+        const float2 e2 = L.ell2[lo];
+        Conic kk;
+        kk.A = e.z;
+        kk.B = e.w;
+        kk.C = e2.x;
+        if (intersects_tile(tx, ty, e.x, e.y, kk, e2.y)) hit(lo, k, ty);
+    }
+    __syncthreads();
+}
+
+// the slab's part of a record's tile answers: rows [rb, re) of the rect, scan order (ty - max(ty0,
+// rb)) * rw + tx - tx0 -- k_scatter's mask order for the slab -- when the whole rect has <= 32 tiles
+// (full = the rect's answers, bit (ty - ty0) * rw + tx - tx0); 0 otherwise (the owner re-tests)
+__device__ __forceinline__ uint32_t slab_tile_mask(short4 b, uint32_t full, int rb, int re) {
+    const int rw = (int)b.y - (int)b.x + 1;
+    if (((int)b.w - (int)b.z + 1) * rw > kMaskTiles) return 0u;
+    const int y0 = max((int)b.z, rb), y1 = min((int)b.w, re - 1);
+    if (y1 < y0) return 0u;
+    const uint32_t shift = (uint32_t)((y0 - (int)b.z) * rw), bits = (uint32_t)((y1 - y0 + 1) * rw);
+    return (full >> shift) & (bits >= 32u ? 0xFFFFFFFFu : ((1u << bits) - 1u));
 }
 
 template <bool HALF, int DEG>
@@ -380,102 +449,159 @@ __global__ __launch_bounds__(kProjectBlock) void k_project_part(
     uint32_t* __restrict__ blockSlabCounts, const float2* __restrict__ sincos) {
     __shared__ uint32_t wcnt[kProjectBlock / 64][kMaxSlabs];
     __shared__ uint16_t div255[256];
+    __shared__ TileTestLds L;
+    __shared__ uint32_t sTile[kProjectBlock];  // answers of candidates < 32
+    __shared__ uint32_t sSlab[kProjectBlock];  // slabs with a hit
+    __shared__ uint32_t sRows[kMaxSlabs + 1];
     fill_div255(div255);
-    const uint32_t gid = blockIdx.x * kProjectBlock + threadIdx.x;
-    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint32_t tid = threadIdx.x;
+    const uint32_t gid = blockIdx.x * kProjectBlock + tid;
+    const uint32_t lane = tid & 63, wave = tid >> 6;
+    if (tid <= slabs.n) sRows[tid] = slabs.rows[tid];
+    sTile[tid] = 0;
+    sSlab[tid] = 0;
+    ProjOut o;
+    o.vis = false;
+    o.countable = false;
+    o.bounds = make_short4(0, -1, 0, -1);
+    uint32_t area = 0;
+    if (gid < P.count) {
+        o = project_gaussian<HALF, DEG>(world, harm, gid, P, sincos, div255);
+        if (o.vis && o.countable)
+            area = (uint32_t)(((int)o.bounds.w - (int)o.bounds.z + 1) * ((int)o.bounds.y - (int)o.bounds.x + 1));
+    }
+    const uint32_t nSlabs = slabs.n;
+    block_tile_tests(L, o, area, (int)o.bounds.z, [&](uint32_t lo, uint32_t k, int ty) {
+        if (k < (uint32_t)kMaskTiles) atomicOr(&sTile[lo], 1u << k);
+        uint32_t sl = 0;  // the slab of row ty: slabs.rows is non-decreasing, at most 16 slabs
+        while (sl + 1u < nSlabs && (uint32_t)ty >= sRows[sl + 1u]) ++sl;
+        if ((uint32_t)ty >= sRows[sl] && (uint32_t)ty < sRows[sl + 1u]) atomicOr(&sSlab[lo], 1u << sl);
+    });
     uint32_t mask = 0;
     if (gid < P.count) {
-        const ProjOut o = project_gaussian<HALF, DEG>(world, harm, gid, P, sincos, div255);
+        mask = sSlab[tid];
         if (o.vis) {
             SplatRecord r;
             r.rd = o.rd;
             r.ra = o.ra;
             r.bounds = o.bounds;
             r.rb = o.rb;
-            r.pad = 0u;
+            r.pad = sTile[tid];  // the whole rect's answers (slab_tile_mask cuts the slab's part)
             records[gid] = r;
-            for (uint32_t sl = 0; sl < slabs.n; ++sl)
-                if (meets_rows(o, (int)slabs.rows[sl], (int)slabs.rows[sl + 1])) mask |= 1u << sl;
         }
         masks[gid] = mask;
     }
-    for (uint32_t sl = 0; sl < slabs.n; ++sl) {
+    for (uint32_t sl = 0; sl < nSlabs; ++sl) {
         const uint32_t c = (uint32_t)__popcll(__ballot((mask >> sl) & 1u));
         if (lane == 0) wcnt[wave][sl] = c;
     }
     __syncthreads();
-    if (threadIdx.x < slabs.n) {
+    if (tid < nSlabs) {
         uint32_t t = 0;
 #pragma unroll
-        for (int w = 0; w < kProjectBlock / 64; ++w) t += wcnt[w][threadIdx.x];
-        blockSlabCounts[(size_t)threadIdx.x * gridDim.x + blockIdx.x] = t;
+        for (int w = 0; w < kProjectBlock / 64; ++w) t += wcnt[w][tid];
+        blockSlabCounts[(size_t)tid * gridDim.x + blockIdx.x] = t;
     }
 }
 
-// one workgroup: per slab, exclusive scan of its block counts (in place), then the slab bases;
-// sendCounts[s] = records for slab s, slabBase[s] = its first record in the send buffer
-__global__ __launch_bounds__(1024) void k_part_scan(uint32_t* __restrict__ blockSlabCounts,
-                                                    uint32_t numBlocks, uint32_t numSlabs,
-                                                    uint32_t* __restrict__ sendCounts,
-                                                    uint32_t* __restrict__ slabBase) {
+// one workgroup per slab: exclusive scan of the slab's block counts (in place) and its total
+__global__ __launch_bounds__(1024) void k_part_scan(uint32_t* __restrict__ blockSlabCounts, uint32_t numBlocks,
+                                                    uint32_t* __restrict__ sendCounts) {
     __shared__ uint32_t lds[1024 / 64];
-    __shared__ uint32_t totals[kMaxSlabs];
-    for (uint32_t sl = 0; sl < numSlabs; ++sl) {
-        uint32_t* row = blockSlabCounts + (size_t)sl * numBlocks;
-        uint32_t carry = 0;
-        for (uint32_t base = 0; base < numBlocks; base += 1024) {
-            const uint32_t i = base + threadIdx.x;
-            const uint32_t v = i < numBlocks ? row[i] : 0u;
-            uint32_t tot;
-            const uint32_t ex = block_exclusive_scan<1024>(v, lds, &tot);
-            if (i < numBlocks) row[i] = carry + ex;
-            carry += tot;
-            __syncthreads();
-        }
-        if (threadIdx.x == 0) totals[sl] = carry;
+    const uint32_t sl = blockIdx.x;
+    uint32_t* row = blockSlabCounts + (size_t)sl * numBlocks;
+    uint32_t carry = 0;
+    for (uint32_t base = 0; base < numBlocks; base += 1024) {
+        const uint32_t i = base + threadIdx.x;
+        const uint32_t v = i < numBlocks ? row[i] : 0u;
+        uint32_t tot;
+        const uint32_t ex = block_exclusive_scan<1024>(v, lds, &tot);
+        if (i < numBlocks) row[i] = carry + ex;
+        carry += tot;
+        __syncthreads();
     }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        uint32_t run = 0;
-        for (uint32_t sl = 0; sl < numSlabs; ++sl) {
-            slabBase[sl] = run;
-            sendCounts[sl] = totals[sl];
-            run += totals[sl];
-        }
-    }
+    if (threadIdx.x == 0) sendCounts[sl] = carry;
 }
 
-__global__ __launch_bounds__(kProjectBlock) void k_part_pack(
-    const SplatRecord* __restrict__ records, const uint32_t* __restrict__ masks, uint32_t count,
-    uint32_t numSlabs, const uint32_t* __restrict__ blockSlabOffsets,
-    const uint32_t* __restrict__ slabBase, SplatRecord* __restrict__ send, uint64_t capacity) {
+// Writes the block's records of every slab it meets as one contiguous run of the destination
+// (slab-local rank order = ascending id): the 48-B records go through LDS so that consecutive
+// threads store consecutive 16-B words -- whole 64-B segments into uncached or peer memory instead
+// of three 16-B pieces per record 48 B apart.  dst(sl) = the run's first record, cap(sl) = records
+// the destination holds (nothing is written past it).  slabRows: the slab table (record masks).
+template <class Dst, class Cap>
+__device__ __forceinline__ void write_slab_runs(const SplatRecord* __restrict__ records, uint32_t slabBits,
+                                                uint32_t gid, uint32_t numSlabs, const uint32_t* slabRows,
+                                                Dst&& dst, Cap&& cap) {
     __shared__ uint32_t wcnt[kProjectBlock / 64][kMaxSlabs];
-    const uint32_t gid = blockIdx.x * kProjectBlock + threadIdx.x;
+    __shared__ uint4 sOut[kProjectBlock * 3];
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const uint32_t mask = gid < count ? masks[gid] : 0u;
     const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-    uint32_t rank[kMaxSlabs];
+    uint32_t rnk[kMaxSlabs];
     for (uint32_t sl = 0; sl < numSlabs; ++sl) {
-        const uint64_t b = __ballot((mask >> sl) & 1u);
-        rank[sl] = (uint32_t)__popcll(b & lt);
+        const uint64_t b = __ballot((slabBits >> sl) & 1u);
+        rnk[sl] = (uint32_t)__popcll(b & lt);
         if (lane == 0) wcnt[wave][sl] = (uint32_t)__popcll(b);
     }
-    __syncthreads();
-    if (!mask) return;
-    const SplatRecord r = records[gid];
-    for (uint32_t sl = 0; sl < numSlabs; ++sl) {
-        if (!((mask >> sl) & 1u)) continue;
-        uint32_t before = 0;
-        for (uint32_t w = 0; w < wave; ++w) before += wcnt[w][sl];
-        const uint64_t pos = (uint64_t)slabBase[sl] + blockSlabOffsets[(size_t)sl * gridDim.x + blockIdx.x] +
-                             before + rank[sl];
-        if (pos < capacity) send[pos] = r;
+    uint4 a = make_uint4(0, 0, 0, 0), b = a, c = a;
+    if (slabBits) {
+        const uint4* src = (const uint4*)(records + gid);
+        a = src[0];
+        b = src[1];
+        c = src[2];
     }
+    const short4 bounds = __builtin_bit_cast(short4, make_uint2(c.x, c.y));
+    __syncthreads();
+    for (uint32_t sl = 0; sl < numSlabs; ++sl) {
+        uint32_t before = 0, n = 0;
+#pragma unroll
+        for (uint32_t w = 0; w < kProjectBlock / 64; ++w) {
+            const uint32_t x = wcnt[w][sl];
+            before += w < wave ? x : 0u;
+            n += x;
+        }
+        if (n == 0) continue;  // (uniform)
+        if ((slabBits >> sl) & 1u) {
+            uint4* o = sOut + 3u * (before + rnk[sl]);
+            o[0] = a;
+            o[1] = b;
+            o[2] = make_uint4(c.x, c.y, c.z, slab_tile_mask(bounds, c.w, (int)slabRows[sl], (int)slabRows[sl + 1]));
+        }
+        __syncthreads();
+        uint4* d = (uint4*)dst(sl);
+        const uint64_t room = cap(sl);
+        for (uint32_t j = threadIdx.x; j < 3u * n; j += kProjectBlock)
+            if (j / 3u < room) d[j] = sOut[j];
+        __syncthreads();
+    }
+}
+
+// slabs packed one after another into the caller's send buffer (gsm_global_project_partition)
+__global__ __launch_bounds__(kProjectBlock) void k_part_pack(
+    const SplatRecord* __restrict__ records, const uint32_t* __restrict__ masks, uint32_t count,
+    SlabTable slabs, const uint32_t* __restrict__ blockSlabOffsets, const uint32_t* __restrict__ sendCounts,
+    SplatRecord* __restrict__ send, uint64_t capacity) {
+    const uint32_t gid = blockIdx.x * kProjectBlock + threadIdx.x;
+    const uint32_t mask = gid < count ? masks[gid] : 0u;
+    write_slab_runs(
+        records, mask, gid, slabs.n, slabs.rows,
+        [&](uint32_t sl) {
+            uint64_t base = 0;
+            for (uint32_t t = 0; t < sl; ++t) base += sendCounts[t];
+            return send + base + blockSlabOffsets[(size_t)sl * gridDim.x + blockIdx.x];
+        },
+        [&](uint32_t sl) {
+            uint64_t base = 0;
+            for (uint32_t t = 0; t < sl; ++t) base += sendCounts[t];
+            const uint64_t at = base + blockSlabOffsets[(size_t)sl * gridDim.x + blockIdx.x];
+            return at < capacity ? capacity - at : 0ull;
+        });
 }
 
 // slab owner: received records -> the renderer's per-gaussian arrays + tile counts for its rows.
 // devCount (may be null): the record count on the device (multi-GPU exchange); P.count is then the
-// capacity the grid covers and the ids past the count get no tiles.
+// capacity the grid covers, and blocks past the count leave at once (the scan and the scatter read
+// the count too).  The block's records (256 x 48 B, contiguous) are loaded as 16-B words by
+// consecutive threads and exchanged through LDS (whole segments of the uncached receive buffer).
 __global__ __launch_bounds__(kProjectBlock) void k_records_in(
     const SplatRecord* __restrict__ in, ProjectArgs P, GaussianRenderData* __restrict__ outRD,
     short4* __restrict__ outBounds, BlendRecord* __restrict__ outRec,
@@ -483,6 +609,7 @@ __global__ __launch_bounds__(kProjectBlock) void k_records_in(
     const float2* __restrict__ sincos, const uint32_t* __restrict__ devCount, const uint16_t* __restrict__ unitCost,
     uint32_t* __restrict__ unitOrder, uint32_t* __restrict__ costMax) {
     __shared__ uint32_t lds[kProjectBlock / 64];
+    __shared__ uint4 sIn[kProjectBlock * 3];
     // block 0 of a scheduled launch orders the blend's units (as k_project's: no k_unit_order launch)
     if (P.schedUnits) {
         if (blockIdx.x == 0) {
@@ -494,28 +621,54 @@ __global__ __launch_bounds__(kProjectBlock) void k_records_in(
     const uint32_t blk = blockIdx.x - (P.schedUnits ? 1u : 0u);
     const uint32_t gid = blk * kProjectBlock + threadIdx.x;
     const uint32_t n = devCount ? min(*devCount, P.count) : P.count;
+    if (blk * kProjectBlock >= n) return;  // (uniform) nothing here; the scan stops at the count
+    {
+        const uint32_t words = 3u * (min(n - blk * kProjectBlock, (uint32_t)kProjectBlock));
+        const uint4* src = (const uint4*)(in + (size_t)blk * kProjectBlock);
+#pragma unroll
+        for (uint32_t j = 0; j < 3; ++j) {
+            const uint32_t i = threadIdx.x + j * kProjectBlock;
+            if (i < words) sIn[i] = src[i];
+        }
+    }
+    __syncthreads();
     uint32_t ntiles = 0;
-    if (gid >= n && gid < P.count) counts[gid] = 0;
     if (gid < n) {
-        const SplatRecord r = in[gid];
+        const uint4 w0 = sIn[3 * threadIdx.x], w1 = sIn[3 * threadIdx.x + 1], w2 = sIn[3 * threadIdx.x + 2];
+        SplatRecord r;
+        r.rd = w0;
+        r.ra.x = w1.x;
+        r.ra.y = w1.y;
+        r.ra.z = w1.z;
+        r.ra.w = w1.w;
+        r.bounds = __builtin_bit_cast(short4, make_uint2(w2.x, w2.y));
+        r.rb = w2.z;
+        r.pad = w2.w;
+        const int rw = (int)r.bounds.y - (int)r.bounds.x + 1;
         const int ry0 = max((int)r.bounds.z, (int)P.rowBegin), ry1 = min((int)r.bounds.w, (int)P.rowEnd - 1);
-        if (P.keepRenderData || (ry1 - ry0 + 1) * ((int)r.bounds.y - (int)r.bounds.x + 1) > kMaskTiles)
-            *(uint4*)(outRD + gid) = r.rd;
+        if (P.keepRenderData || (ry1 - ry0 + 1) * rw > kMaskTiles) *(uint4*)(outRD + gid) = r.rd;
         outBounds[gid] = r.bounds;
         uint4* rp = (uint4*)(outRec + gid);
         rp[0] = make_uint4(r.ra.x, r.ra.y, r.ra.z, r.ra.w);
-        // the values k_project had in registers, rebuilt from the record exactly as k_scatter does
-        ProjOut o;
-        o.bounds = r.bounds;
-        o.cmx = hbits_to_f((uint16_t)(r.rd.x & 0xFFFFu));
-        o.cmy = hbits_to_f((uint16_t)(r.rd.x >> 16));
-        o.k = conic_from_quant(sincos, (uint16_t)(r.rd.y & 0xFFFFu), hbits_to_f((uint16_t)(r.rd.y >> 16)),
-                               hbits_to_f((uint16_t)(r.rd.z & 0xFFFFu)));
-        const float alpha = (float)(r.rd.w >> 24);
-        o.countable = alpha >= 1e-4f && r.bounds.x <= r.bounds.y && r.bounds.z <= r.bounds.w;
-        o.w = o.countable ? 2.0f * compute_power(alpha) : 0.0f;
         uint32_t mask;
-        ntiles = count_tiles(o, (int)P.rowBegin, (int)P.rowEnd, &mask);
+        if (((int)r.bounds.w - (int)r.bounds.z + 1) * rw <= kMaskTiles) {
+            // the sender's answers for this slab's rows (slab_tile_mask)
+            mask = r.pad;
+            ntiles = (uint32_t)__builtin_popcount(mask);
+        } else {
+            // a rect of more than 32 tiles: the values k_project had in registers, rebuilt from the
+            // record exactly as k_scatter does, and the tests of the slab's rows repeated
+            ProjOut o;
+            o.bounds = r.bounds;
+            o.cmx = hbits_to_f((uint16_t)(r.rd.x & 0xFFFFu));
+            o.cmy = hbits_to_f((uint16_t)(r.rd.x >> 16));
+            o.k = conic_from_quant(sincos, (uint16_t)(r.rd.y & 0xFFFFu), hbits_to_f((uint16_t)(r.rd.y >> 16)),
+                                   hbits_to_f((uint16_t)(r.rd.z & 0xFFFFu)));
+            const float alpha = (float)(r.rd.w >> 24);
+            o.countable = alpha >= 1e-4f && r.bounds.x <= r.bounds.y && r.bounds.z <= r.bounds.w;
+            o.w = o.countable ? 2.0f * compute_power(alpha) : 0.0f;
+            ntiles = count_tiles(o, (int)P.rowBegin, (int)P.rowEnd, &mask);
+        }
         counts[gid] = ntiles;
         masks[gid] = mask;
         const float2 band = ntiles ? band_of(r.ra, r.bounds, (int)P.rowBegin, (int)P.rowEnd) : make_float2(0.f, -1.f);
@@ -533,8 +686,10 @@ constexpr int kScanThreads = 1024;
 __global__ __launch_bounds__(kScanThreads) void k_scan_blocks(uint32_t* __restrict__ sums,
                                                               uint32_t nb, uint32_t maxAssignments,
                                                               TileAssignmentHeader* __restrict__ hdr,
-                                                              uint32_t* __restrict__ blendQueue) {
+                                                              uint32_t* __restrict__ blendQueue,
+                                                              const uint32_t* __restrict__ devCount) {
     __shared__ uint32_t lds[kScanThreads / 64];
+    if (devCount) nb = min(nb, (*devCount + (uint32_t)kProjectBlock - 1u) / (uint32_t)kProjectBlock);
     // rows of 4 * kScanThreads block sums, kScanRows rows in flight: thread t holds sums
     // [row * 4096 + 4t, +4) as one 16-byte load, so every load of a pass is issued before the
     // first scan (the sums are read once and written once)
@@ -620,7 +775,7 @@ __global__ __launch_bounds__(kProjectBlock) void k_scatter(
     ProjectArgs P, const GaussianRenderData* __restrict__ rd, const short4* __restrict__ bounds,
     const uint32_t* __restrict__ counts, const uint32_t* __restrict__ masks,
     const uint32_t* __restrict__ blockOffsets, uint32_t* __restrict__ keys, uint32_t* __restrict__ vals,
-    const float2* __restrict__ sincos, const BlendRecord* __restrict__ rec) {
+    const float2* __restrict__ sincos, const BlendRecord* __restrict__ rec, const uint32_t* __restrict__ devCount) {
     __shared__ uint32_t lds[kProjectBlock / 64];
     __shared__ uint32_t sOff[kProjectBlock];
     __shared__ uint32_t sMask[kProjectBlock];  // 0: no cooperative slots (large rect or no tiles)
@@ -634,7 +789,10 @@ __global__ __launch_bounds__(kProjectBlock) void k_scatter(
     constexpr uint16_t kNoOwner = 0xFFFFu;
     __shared__ uint16_t sOwn[kOwnCap];
     const uint32_t gid = blockIdx.x * kProjectBlock + threadIdx.x;
-    uint32_t c = (gid < P.count) ? counts[gid] : 0u;
+    // records path: the count lives on the device and the grid covers the capacity
+    const uint32_t n = devCount ? min(*devCount, P.count) : P.count;
+    if (blockIdx.x * kProjectBlock >= n) return;  // (uniform; the scan stopped at the count too)
+    uint32_t c = (gid < n) ? counts[gid] : 0u;
     uint32_t total;
     const uint32_t off = block_exclusive_scan<kProjectBlock>(c, lds, &total);
     const uint32_t base = blockOffsets[blockIdx.x];
@@ -760,19 +918,17 @@ __global__ __launch_bounds__(256) void k_tile_starts(const uint32_t* __restrict_
     }
 }
 
-// The multi-GPU frame's direct exchange (gsm_multigpu.hip): k_part_pack with every slab's records
-// written straight into the slab owner's receive buffer (peer pointers over xGMI) at the offset the
-// all-gathered count matrix gives -- counts[r * world + s] = records rank r holds for slab s, so
-// rank r's records of slab s start after those of ranks 0..r-1 (ascending id order at the owner).
-// Block 0 also leaves the rank's own receive count in *recvCount.
+// The multi-GPU frame's direct exchange (gsm_multigpu.hip): every slab's records written straight
+// into the slab owner's receive buffer (peer pointers over xGMI) at the offset the count matrix
+// gives -- counts[r * world + s] = records rank r holds for slab s, so rank r's records of slab s
+// start after those of ranks 0..r-1 (ascending id order at the owner).  Block 0 also leaves the
+// rank's own receive count in *recvCount.
 __global__ __launch_bounds__(kProjectBlock) void k_part_push(
     const SplatRecord* __restrict__ records, const uint32_t* __restrict__ masks, uint32_t count,
     uint32_t world, uint32_t rank, const uint32_t* __restrict__ blockSlabOffsets,
-    const uint32_t* __restrict__ counts, SlabPeers peers, uint32_t* __restrict__ recvCount) {
-    __shared__ uint32_t wcnt[kProjectBlock / 64][kMaxSlabs];
+    const uint32_t* __restrict__ counts, SlabPeers peers, uint32_t* __restrict__ recvCount, SlabTable slabs) {
     __shared__ uint32_t dstOff[kMaxSlabs];
     const uint32_t gid = blockIdx.x * kProjectBlock + threadIdx.x;
-    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     if (threadIdx.x < world) {
         uint32_t before = 0;
         for (uint32_t r = 0; r < rank; ++r) before += counts[r * world + threadIdx.x];
@@ -784,29 +940,16 @@ __global__ __launch_bounds__(kProjectBlock) void k_part_push(
         *recvCount = min(mine, peers.cap[rank]);
     }
     const uint32_t mask = gid < count ? masks[gid] : 0u;
-    const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-    uint32_t rnk[kMaxSlabs];
-    for (uint32_t sl = 0; sl < world; ++sl) {
-        const uint64_t b = __ballot((mask >> sl) & 1u);
-        rnk[sl] = (uint32_t)__popcll(b & lt);
-        if (lane == 0) wcnt[wave][sl] = (uint32_t)__popcll(b);
-    }
-    __syncthreads();
-    if (!mask) return;
-    const uint4* src = (const uint4*)(records + gid);
-    const uint4 a = src[0], b = src[1], c = src[2];
-    for (uint32_t sl = 0; sl < world; ++sl) {
-        if (!((mask >> sl) & 1u)) continue;
-        uint32_t before = 0;
-        for (uint32_t w = 0; w < wave; ++w) before += wcnt[w][sl];
-        const uint64_t pos =
-            (uint64_t)dstOff[sl] + blockSlabOffsets[(size_t)sl * gridDim.x + blockIdx.x] + before + rnk[sl];
-        if (pos >= peers.cap[sl]) continue;  // never past an owner's receive buffer
-        uint4* dst = (uint4*)(peers.recv[sl] + pos);
-        dst[0] = a;
-        dst[1] = b;
-        dst[2] = c;
-    }
+    __syncthreads();  // (dstOff)
+    write_slab_runs(
+        records, mask, gid, world, slabs.rows,
+        [&](uint32_t sl) {
+            return peers.recv[sl] + (uint64_t)dstOff[sl] + blockSlabOffsets[(size_t)sl * gridDim.x + blockIdx.x];
+        },
+        [&](uint32_t sl) {  // never past an owner's receive buffer
+            const uint64_t at = (uint64_t)dstOff[sl] + blockSlabOffsets[(size_t)sl * gridDim.x + blockIdx.x];
+            return at < peers.cap[sl] ? (uint64_t)peers.cap[sl] - at : 0ull;
+        });
 }
 
 // ---------------------------------------------------------------------------
@@ -937,10 +1080,9 @@ void launch_partition(bool halfInput, uint32_t deg, const void* world, const voi
     }
     if (halfInput) launch_project_part_t<true>(deg, world, harm, a, slabs, B, sincos, s);
     else launch_project_part_t<false>(deg, world, harm, a, slabs, B, sincos, s);
-    hipLaunchKernelGGL(k_part_scan, dim3(1), dim3(1024), 0, s, B.blockSlabCounts, blocks, slabs.n,
-                       sendCounts, B.slabBase);
-    hipLaunchKernelGGL(k_part_pack, dim3(blocks), dim3(kProjectBlock), 0, s, B.records, B.masks, a.count,
-                       slabs.n, B.blockSlabCounts, B.slabBase, (SplatRecord*)send, capacity);
+    hipLaunchKernelGGL(k_part_scan, dim3(slabs.n), dim3(1024), 0, s, B.blockSlabCounts, blocks, sendCounts);
+    hipLaunchKernelGGL(k_part_pack, dim3(blocks), dim3(kProjectBlock), 0, s, B.records, B.masks, a.count, slabs,
+                       B.blockSlabCounts, sendCounts, (SplatRecord*)send, capacity);
 }
 
 void launch_partition_counts(bool halfInput, uint32_t deg, const void* world, const void* harm, const ProjectArgs& a,
@@ -953,20 +1095,16 @@ void launch_partition_counts(bool halfInput, uint32_t deg, const void* world, co
     }
     if (halfInput) launch_project_part_t<true>(deg, world, harm, a, slabs, B, sincos, s);
     else launch_project_part_t<false>(deg, world, harm, a, slabs, B, sincos, s);
-    hipLaunchKernelGGL(k_part_scan, dim3(1), dim3(1024), 0, s, B.blockSlabCounts, blocks, slabs.n, sendCounts,
-                       B.slabBase);
+    hipLaunchKernelGGL(k_part_scan, dim3(slabs.n), dim3(1024), 0, s, B.blockSlabCounts, blocks, sendCounts);
 }
 
 void launch_partition_push(const ProjectArgs& a, uint32_t world, uint32_t rank, const PartitionBuffers& B,
-                           const uint32_t* counts, const SlabPeers& peers, uint32_t* recvCount, hipStream_t s) {
+                           const uint32_t* counts, const SlabPeers& peers, uint32_t* recvCount, const SlabTable& slabs,
+                           hipStream_t s) {
     const uint32_t blocks = (a.count + kProjectBlock - 1) / kProjectBlock;
-    if (blocks == 0) {  // no ids here: the receive count still comes from the matrix
-        hipLaunchKernelGGL(k_part_push, dim3(1), dim3(kProjectBlock), 0, s, B.records, B.masks, 0u, world, rank,
-                           B.blockSlabCounts, counts, peers, recvCount);
-        return;
-    }
-    hipLaunchKernelGGL(k_part_push, dim3(blocks), dim3(kProjectBlock), 0, s, B.records, B.masks, a.count, world,
-                       rank, B.blockSlabCounts, counts, peers, recvCount);
+    // (no ids here: one block still takes the receive count from the matrix)
+    hipLaunchKernelGGL(k_part_push, dim3(blocks ? blocks : 1u), dim3(kProjectBlock), 0, s, B.records, B.masks, a.count,
+                       world, rank, B.blockSlabCounts, counts, peers, recvCount, slabs);
 }
 
 void launch_records_in(const void* records, const ProjectArgs& a, const DeviceArena& A, hipStream_t s,
@@ -980,19 +1118,21 @@ void launch_records_in(const void* records, const ProjectArgs& a, const DeviceAr
 
 void launch_scan_sums(uint32_t* sums, uint32_t nb, uint32_t cap, TileAssignmentHeader* hdr, uint32_t* queue,
                       hipStream_t s) {
-    hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(kScanThreads), 0, s, sums, nb, cap, hdr, queue);
+    hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(kScanThreads), 0, s, sums, nb, cap, hdr, queue,
+                       (const uint32_t*)nullptr);
 }
 
-void launch_scan_blocks(uint32_t nb, const ProjectArgs& a, const DeviceArena& A, hipStream_t s) {
+void launch_scan_blocks(uint32_t nb, const ProjectArgs& a, const DeviceArena& A, hipStream_t s,
+                        const uint32_t* devCount) {
     hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(kScanThreads), 0, s, A.blockSums, nb,
-                       a.maxAssignments, A.header, A.tileQueue);
+                       a.maxAssignments, A.header, A.tileQueue, devCount);
 }
 
-void launch_scatter(const ProjectArgs& a, const DeviceArena& A, hipStream_t s) {
+void launch_scatter(const ProjectArgs& a, const DeviceArena& A, hipStream_t s, const uint32_t* devCount) {
     const uint32_t blocks = (a.count + kProjectBlock - 1) / kProjectBlock;
     if (blocks == 0) return;
     hipLaunchKernelGGL(k_scatter, dim3(blocks), dim3(kProjectBlock), 0, s, a, A.renderData, A.bounds,
-                       A.tileCounts, A.tileMasks, A.blockSums, A.keys[0], A.vals[0], A.sincosTable, A.rec);
+                       A.tileCounts, A.tileMasks, A.blockSums, A.keys[0], A.vals[0], A.sincosTable, A.rec, devCount);
 }
 
 void launch_headers(const uint32_t* sortedKeys, const FrameGeometry& g, const DeviceArena& A,

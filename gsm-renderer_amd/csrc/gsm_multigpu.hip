@@ -30,6 +30,7 @@
 #include <rccl/rccl.h>
 #include <unistd.h>
 
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <new>
@@ -156,6 +157,12 @@ class MultiGpu {
         return GSM_OK;
     }
     gsm_status counts(uint32_t* hostCounts);  // world x world, after the frame's stream work
+    gsm_status copyExchange(void* dst, size_t bytes) {
+        hipSetDevice(device_);
+        return hipMemcpy(dst, mem_, bytes < memBytes_ ? bytes : memBytes_, hipMemcpyDeviceToHost) == hipSuccess
+                   ? GSM_OK
+                   : GSM_ERR_RENDER_FAILED;
+    }
     gsm_status copyFrame(void* dst, size_t pitch, uint32_t width, uint32_t height) {
         if (rank_ != 0 || !frame0_ || !dst || width > r_->maxWidth() || height > r_->maxHeight() ||
             pitch < (size_t)width * bpp_)
@@ -224,7 +231,17 @@ gsm_status MultiGpu::prepare(GlobalRenderer* r, int rank, int world, MultiGpu** 
     m->framePitch_ = (size_t)r->maxWidth() * m->bpp_;
     m->frameOff_ = rank == 0 ? align_up(kRecordsOff + recBytes, 4096) : 0;
     m->memBytes_ = rank == 0 ? m->frameOff_ + m->framePitch_ * r->maxHeight() : kRecordsOff + recBytes;
-    bool ok = hipExtMallocWithFlags((void**)&m->mem_, m->memBytes_, hipDeviceMallocUncached) == hipSuccess &&
+    // fine-grained device memory (GSM_MG_MEM=uncached|cached: the A/B of DESIGN.md 7, create-time only):
+    // uncached exchange memory rendered wrong slabs on MI355X (tools/dbg/mg_ab2.sh: 30 of 36 virtual-rank
+    // frames, fine-grained and ordinary memory 0 of 36)
+    const char* mode = getenv("GSM_MG_MEM");
+    hipError_t ae = mode && !strcmp(mode, "cached")
+                        ? hipMalloc((void**)&m->mem_, m->memBytes_)
+                        : hipExtMallocWithFlags((void**)&m->mem_, m->memBytes_,
+                                                mode && !strcmp(mode, "uncached") ? hipDeviceMallocUncached
+                                                                                  : hipDeviceMallocFinegrained);
+    bool ok = ae == hipSuccess &&
+              (!getenv("GSM_MG_POISON") || hipMemset(m->mem_, 0xAB, m->memBytes_) == hipSuccess) &&
               hipMemset(m->mem_, 0, kRecordsOff) == hipSuccess &&
               hipMalloc(&m->sendCounts_, kMaxSlabs * 4) == hipSuccess && hipMalloc(&m->recvCount_, 4) == hipSuccess &&
               hipMemset(m->sendCounts_, 0, kMaxSlabs * 4) == hipSuccess && hipMemset(m->recvCount_, 0, 4) == hipSuccess;
@@ -516,6 +533,11 @@ gsm_status gsm_multigpu_debug_copy_frame(gsm_multigpu* m, void* host_dst, size_t
                                          uint32_t height) {
     if (!m || !m->impl) return GSM_ERR_INVALID_ARGUMENT;
     return m->impl->copyFrame(host_dst, dst_pitch_bytes, width, height);
+}
+
+gsm_status gsm_multigpu_debug_copy_exchange(gsm_multigpu* m, void* host_dst, size_t bytes) {
+    if (!m || !m->impl || !host_dst) return GSM_ERR_INVALID_ARGUMENT;
+    return m->impl->copyExchange(host_dst, bytes);
 }
 
 gsm_status gsm_multigpu_debug_counts(gsm_multigpu* m, uint32_t* host_counts) {

@@ -264,7 +264,7 @@ gsm_status GlobalRenderer::renderRecords(hipStream_t s, const void* records, uin
     return runFrame(s, a, width, height, color, colorPitch, depth, depthPitch,
                     [&](const ProjectArgs& pa) {
                         launch_records_in(records, pa, arena_, s, devCount);
-                    });
+                    }, devCount);
 }
 
 gsm_status GlobalRenderer::preparePartition(const gsm_gaussian_input& in, const gsm_camera_params& camp,
@@ -290,7 +290,6 @@ gsm_status GlobalRenderer::preparePartition(const gsm_gaussian_input& in, const 
         gsm_status st = alloc((void**)&part_.records, (size_t)maxGaussians_ * sizeof(SplatRecord));
         if (st == GSM_OK) st = alloc((void**)&part_.masks, (size_t)maxGaussians_ * 4);
         if (st == GSM_OK) st = alloc((void**)&part_.blockSlabCounts, kMaxSlabs * (blocks + 1) * 4);
-        if (st == GSM_OK) st = alloc((void**)&part_.slabBase, kMaxSlabs * 4);
         if (st != GSM_OK) {
             part_ = PartitionBuffers();
             return st;
@@ -333,6 +332,7 @@ gsm_status GlobalRenderer::partitionCounts(hipStream_t s, const gsm_gaussian_inp
     if (st != GSM_OK) return st;
     launch_partition_counts(f.half, f.deg, f.world, f.harm, f.a, f.slabs, part_, arena_.sincosTable, sendCounts, s);
     partCount_ = count;
+    partSlabs_ = f.slabs;
     if (hipGetLastError() != hipSuccess) return GSM_ERR_RENDER_FAILED;
     return GSM_OK;
 }
@@ -342,7 +342,8 @@ gsm_status GlobalRenderer::partitionPush(hipStream_t s, uint32_t world, uint32_t
     ProjectArgs a;
     std::memset(&a, 0, sizeof(a));
     a.count = partCount_;
-    launch_partition_push(a, world, rank, part_, counts, peers, recvCount, s);
+    if (world != partSlabs_.n) return GSM_ERR_INVALID_ARGUMENT;  // one slab per rank, as partitionCounts split
+    launch_partition_push(a, world, rank, part_, counts, peers, recvCount, partSlabs_, s);
     if (hipGetLastError() != hipSuccess) return GSM_ERR_RENDER_FAILED;
     return GSM_OK;
 }
@@ -350,7 +351,7 @@ gsm_status GlobalRenderer::partitionPush(hipStream_t s, uint32_t world, uint32_t
 template <class Front>
 gsm_status GlobalRenderer::runFrame(hipStream_t s, const ProjectArgs& a, uint32_t width, uint32_t height,
                                     void* color, size_t colorPitch, void* depth, size_t depthPitch,
-                                    Front&& front) {
+                                    Front&& front, const uint32_t* devCount) {
     const bool prof = (profiling_ & 1) != 0;         // every stage bracketed by events
     // only the blend (2 events per frame), on every frame or every period-th (bits 8-15)
     const uint32_t period = ((uint32_t)profiling_ >> 8) & 0xFFu;
@@ -387,9 +388,9 @@ gsm_status GlobalRenderer::runFrame(hipStream_t s, const ProjectArgs& a, uint32_
     if (prof) hipEventRecord(ev[0], s);
     front(fa);  // the projection (or records) launch; its block 0 orders the blend units (fa.schedUnits)
     if (prof) hipEventRecord(ev[1], s);
-    launch_scan_blocks(nb, a, arena_, s);
+    launch_scan_blocks(nb, a, arena_, s, devCount);
     if (prof) hipEventRecord(ev[2], s);
-    launch_scatter(a, arena_, s);
+    launch_scatter(a, arena_, s, devCount);
     if (keep) {  // preserve the unsorted assignment arrays for readback
         hipMemcpyAsync(arena_.keysKeep, arena_.keys[0], (size_t)maxAssignments_ * 4, hipMemcpyDeviceToDevice, s);
         hipMemcpyAsync(arena_.valsKeep, arena_.vals[0], (size_t)maxAssignments_ * 4, hipMemcpyDeviceToDevice, s);

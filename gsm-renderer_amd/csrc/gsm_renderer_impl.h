@@ -66,9 +66,11 @@ class GlobalRenderer {
     // scan, scatter, sort, headers and blend after `front` filled the per-gaussian arrays
     template <class Front>
     gsm_status runFrame(hipStream_t s, const ProjectArgs& a, uint32_t width, uint32_t height, void* color,
-                        size_t colorPitch, void* depth, size_t depthPitch, Front&& front);
+                        size_t colorPitch, void* depth, size_t depthPitch, Front&& front,
+                        const uint32_t* devCount = nullptr);
     PartitionBuffers part_;
     uint32_t partCount_ = 0;  // ids of the last partitionCounts
+    SlabTable partSlabs_{};   // its slab table (partitionPush cuts each record's tile answers by it)
     struct PartitionFrame {
         ProjectArgs a;
         SlabTable slabs;

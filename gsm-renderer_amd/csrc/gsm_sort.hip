@@ -813,15 +813,20 @@ bool sort_lane_ordered_atomics(int device) {
     uint32_t* d = nullptr;
     int prev = 0;
     hipGetDevice(&prev);
-    if (hipSetDevice(device) == hipSuccess && hipMalloc(&d, 4) == hipSuccess) {
+    // on a private non-blocking stream, synchronised alone: no other stream of the caller's process
+    // waits for the probe (a renderer create or a first gsm_sort_pairs_u32 call never stalls the device)
+    hipStream_t ps = nullptr;
+    if (hipSetDevice(device) == hipSuccess && hipStreamCreateWithFlags(&ps, hipStreamNonBlocking) == hipSuccess &&
+        hipMalloc(&d, 4) == hipSuccess) {
         uint32_t h = 1;
-        if (hipMemset(d, 0, 4) == hipSuccess) {
-            hipLaunchKernelGGL(k_rank_probe, dim3(64), dim3(256), 0, 0, d);
-            if (hipDeviceSynchronize() == hipSuccess && hipMemcpy(&h, d, 4, hipMemcpyDeviceToHost) == hipSuccess)
+        if (hipMemsetAsync(d, 0, 4, ps) == hipSuccess) {
+            hipLaunchKernelGGL(k_rank_probe, dim3(64), dim3(256), 0, ps, d);
+            if (hipMemcpyAsync(&h, d, 4, hipMemcpyDeviceToHost, ps) == hipSuccess && hipStreamSynchronize(ps) == hipSuccess)
                 ok = h == 0;
         }
-        hipFree(d);
     }
+    if (d) hipFree(d);
+    if (ps) hipStreamDestroy(ps);
     (void)hipGetLastError();
     hipSetDevice(prev);
     cache[device] = ok;

@@ -26,7 +26,8 @@ except Exception:  # pragma: no cover - torch is always present in this image
 from .types import RENDER_DATA, WORLD16, WORLD32  # noqa: F401
 
 _PKG_DIR = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(os.path.dirname(_PKG_DIR), "lib", "libgsm_amd.so")
+# GSM_AMD_LIB: another in-tree build of the same library (A/B experiments, tools/); default lib/
+LIB_PATH = os.environ.get("GSM_AMD_LIB") or os.path.join(os.path.dirname(_PKG_DIR), "lib", "libgsm_amd.so")
 INCLUDE_DIR = os.path.join(os.path.dirname(os.path.dirname(_PKG_DIR)), "include")
 
 
@@ -250,6 +251,7 @@ _SIGNATURES = {
     "gsm_multigpu_frame": ([C.c_void_p, C.POINTER(C.c_void_p), C.POINTER(C.c_size_t)], C.c_int),
     "gsm_multigpu_status": ([C.c_void_p, C.POINTER(C.c_uint32), C.c_int], C.c_int),
     "gsm_multigpu_set_timeout_ms": ([C.c_void_p, C.c_uint32], C.c_int),
+    "gsm_multigpu_debug_copy_exchange": ([C.c_void_p, C.c_void_p, C.c_size_t], C.c_int),
     "gsm_multigpu_debug_copy_frame": ([C.c_void_p, C.c_void_p, C.c_size_t, C.c_uint32, C.c_uint32], C.c_int),
 }
 
@@ -727,6 +729,14 @@ class MultiGpuRenderer:
         out = np.empty((int(height), int(width), 4), np.uint16)
         _check(_lib().gsm_multigpu_debug_copy_frame(self._h, out.ctypes.data_as(C.c_void_p), int(width) * 8,
                                                     int(width), int(height)), "gsm_multigpu_debug_copy_frame")
+        return out
+
+    def copy_exchange(self, nbytes: int) -> np.ndarray:
+        """The first nbytes of this rank's exchange memory (control, counts from byte 1024, records
+        from byte 4096), synchronous."""
+        out = np.empty(int(nbytes), np.uint8)
+        _check(_lib().gsm_multigpu_debug_copy_exchange(self._h, out.ctypes.data_as(C.c_void_p), out.size),
+               "gsm_multigpu_debug_copy_exchange")
         return out
 
     def status(self, clear: bool = False) -> int:

@@ -126,6 +126,10 @@ gsm_status gsm_multigpu_set_timeout_ms(gsm_multigpu *multigpu, uint32_t ms);
 gsm_status gsm_multigpu_debug_copy_frame(gsm_multigpu *multigpu, void *host_dst, size_t dst_pitch_bytes,
                                          uint32_t width, uint32_t height);
 
+/* The first `bytes` of this rank's exchange allocation (control words from byte 0, the count matrix
+ * from byte 1024, the received records from byte 4096), synchronous. */
+gsm_status gsm_multigpu_debug_copy_exchange(gsm_multigpu *multigpu, void *host_dst, size_t bytes);
+
 /* The last frame's world x world record counts (row = source rank, column = slab), synchronous. */
 gsm_status gsm_multigpu_debug_counts(gsm_multigpu *multigpu, uint32_t *host_counts);
 

@@ -1,16 +1,18 @@
-"""Per-rank device time of the native multi-GPU frame at world W, from W virtual ranks on one GPU
-(gsm_debug_partition_* , include/gsm_debug.h): each rank's partition projection + count, its push
-into the slab owners' receive buffers, and each owner's slab render from the received records,
-timed with HIP events on one stream (ranks run one after another, so each step sees the whole
-GPU -- an upper bound for a rank's own GPU).  No collectives and no xGMI: the push writes local
-memory.  Prints JSON: per-step times per rank and max_proj_push + max_render, the device part of
-one N-GPU frame.
+"""Per-rank device time of the multi-GPU frame at world W, from W virtual ranks on one GPU driven
+through the product path (gsm_multigpu_render_phase, include/gsm_multigpu.h): every rank's phase p
+is issued before any rank's phase p + 1 on ONE stream, so the ranks run one after another and each
+phase sees the whole GPU (an upper bound for a rank's own GPU).  Exchange memory is the product's
+(uncached, the flag barriers run); the pushes and the gathered pixels go to local memory instead of
+crossing xGMI.  HIP events bracket each rank's phase; the renderers' stage events split the slab
+render (records in, scan, scatter, sort, gap, blend).
+
+Prints JSON: per-phase times per rank, and device_frame_ms = max phase 0 + max phase 1 + max phase 2
+(+ phase 3), the device part of one N-GPU frame without the fabric.
 
 usage: python tools/exp_virtual_ranks.py [--config cfg3_5m_sh3_4k_f16] [--world 8] [--frames 5]
 """
 import argparse
 import json
-import math
 import os
 import sys
 
@@ -25,6 +27,7 @@ def main():
     ap.add_argument("--config", default="cfg3_5m_sh3_4k_f16")
     ap.add_argument("--world", type=int, default=8)
     ap.add_argument("--frames", type=int, default=5)
+    ap.add_argument("--stages", type=int, default=1, help="also time the slab render's stages")
     a = ap.parse_args()
     import torch
     import gsm_amd as gsm
@@ -39,70 +42,61 @@ def main():
     del wnp, hnp
     inp = gsm.GaussianInput(wt, ht, n, sh)
     cam = gsm.CameraParams.from_dict(cam_d)
-    tiles_y = (h + 15) // 16
-    per_rows = math.ceil(tiles_y / W)
-    rows = [min(i * per_rows, tiles_y) for i in range(W + 1)]
-    per_ids = math.ceil(n / W)
     cfg = gsm.RendererConfig(max_gaussians=n, max_width=w, max_height=h, precision=prec, gaussian_color_space=0)
-    ranks = [gsm.GlobalRenderer(device=0, config=cfg) for _ in range(W)]
-    send = [torch.zeros(W, dtype=torch.int32, device=dev) for _ in range(W)]
-    recv = [torch.zeros(n * gsm.SPLAT_RECORD_BYTES, dtype=torch.uint8, device=dev) for _ in range(W)]
-    rcnt = [torch.zeros(1, dtype=torch.int32, device=dev) for _ in range(W)]
-    color = torch.zeros((h, w, 4), dtype=torch.float16, device=dev)
-    depth = torch.zeros((h, w), dtype=torch.float16, device=dev)
-    for d in range(W):
-        ranks[d].set_tile_rows(rows[d], rows[d + 1])
+    rends = [gsm.GlobalRenderer(device=0, config=cfg) for _ in range(W)]
+    pre = [gsm.MultiGpuRenderer.prepare(r, k, W) for k, r in enumerate(rends)]
+    handles = [hd for _, hd in pre]
+    mgs = [m.connect_handles(handles) for m, _ in pre]
+    frame_ptr = mgs[0].frame()[0]
+    stream = torch.cuda.current_stream(dev)
     ev = lambda: torch.cuda.Event(enable_timing=True)  # noqa: E731
-    proj = np.zeros((a.frames, W))
-    push = np.zeros((a.frames, W))
-    rend = np.zeros((a.frames, W))
-    for f in range(a.frames + 2):
+    ph = np.zeros((a.frames, 4, W))
+
+    def frame(record):
         marks = []
-        for rk in range(W):
-            first = min(rk * per_ids, n)
-            e0, e1 = ev(), ev()
-            e0.record()
-            ranks[rk].debug_partition_counts(inp, cam, w, h, first, min(per_ids, n - first), rows, send[rk])
-            e1.record()
-            marks.append(("p", rk, e0, e1))
-        counts = torch.stack(send).contiguous()
-        for rk in range(W):
-            e0, e1 = ev(), ev()
-            e0.record()
-            ranks[rk].debug_partition_push(W, rk, counts, recv, rcnt[rk])
-            e1.record()
-            marks.append(("u", rk, e0, e1))
-        for d in range(W):
-            if rows[d] == rows[d + 1]:
-                continue
-            e0, e1 = ev(), ev()
-            e0.record()
-            ranks[d].debug_render_records_device_count(color, depth, recv[d], n, rcnt[d], w, h)
-            e1.record()
-            marks.append(("r", d, e0, e1))
+        for p in range(4):
+            for k, m in enumerate(mgs):
+                e0, e1 = ev(), ev()
+                e0.record(stream)
+                m.render_phases([p], None, None, inp, cam, w, h, gather=True, stream=stream,
+                                gather_target=frame_ptr if k == 0 else None)
+                e1.record(stream)
+                marks.append((p, k, e0, e1))
+        return marks
+
+    for f in range(a.frames + 2):
+        marks = frame(True)
         torch.cuda.synchronize()
-        if f < 2:
-            continue
-        for kind, rk, e0, e1 in marks:
-            t = e0.elapsed_time(e1)
-            {"p": proj, "u": push, "r": rend}[kind][f - 2, rk] = t
-    cm = counts.cpu().numpy().astype(np.int64)
-    out = {"config": a.config, "world": W, "records_per_slab": [int(x) for x in cm.sum(axis=0)],
-           "records_total": int(cm.sum()), "project_count_ms": proj.mean(0).round(4).tolist(),
-           "push_ms": push.mean(0).round(4).tolist(), "render_ms": rend.mean(0).round(4).tolist(),
-           "max_project_push_ms": float((proj + push).mean(0).max()), "max_render_ms": float(rend.mean(0).max()),
-           "note": "ranks timed one after another on one GPU (each step has the whole GPU); no collectives, no xGMI"}
-    out["device_frame_ms"] = out["max_project_push_ms"] + out["max_render_ms"]
-    # stage breakdown of the slowest slab render (stage events on that renderer, 5 more frames)
-    d = int(np.argmax(rend.mean(0)))
-    ranks[d].set_profiling(stage_events=True)
-    for _ in range(5):
-        ranks[d].debug_render_records_device_count(color, depth, recv[d], n, rcnt[d], w, h)
-    torch.cuda.synchronize()
-    out["slowest_slab"] = d
-    out["slowest_slab_stages_ms"] = {k: round(v, 4) for k, v in ranks[d].stage_times_ms().items()}
+        if f >= 2:
+            for p, k, e0, e1 in marks:
+                ph[f - 2, p, k] = e0.elapsed_time(e1)
+    stages = None
+    if a.stages:
+        for r in rends:
+            r.set_profiling(stage_events=True)
+        for _ in range(3):
+            frame(False)
+        torch.cuda.synchronize()
+        names = ["records_in", "scan", "scatter", "sort", "gap", "blend"]
+        stages = []
+        for r in rends:
+            try:
+                t = r.stage_times_ms()
+                stages.append({nm: round(float(t[k]), 4) for nm, k in zip(names, ["project", "scan", "scatter", "sort", "headers", "blend"])})
+            except gsm.RendererError:
+                stages.append(None)  # a rank without rows renders nothing
+    med = np.median(ph, axis=0)  # [phase][rank]
+    out = {"config": a.config, "world": W, "frames": a.frames, "timeouts": [m.status() for m in mgs],
+           "counts": mgs[0].counts().tolist(),
+           "phase_ms": {f"phase{p}": [round(float(x), 4) for x in med[p]] for p in range(4)},
+           "max_phase_ms": [round(float(med[p].max()), 4) for p in range(4)],
+           "device_frame_ms": round(float(sum(med[p].max() for p in range(4))), 4),
+           "slab_stages_ms": stages,
+           "note": "virtual ranks on one GPU, product kernels, one stream; no xGMI (pushes and pixels stay local)"}
     print(json.dumps(out))
-    for r in ranks:
+    for m in mgs:
+        m.close()
+    for r in rends:
         r.close()
 
 

@@ -129,9 +129,10 @@ void launch_partition(bool halfInput, uint32_t shDegree, const void* world, cons
                       hipStream_t stream);
 // the first half of launch_partition (projection + per-slab counts, no packing), then the records
 // written straight to every slab owner from the all-gathered count matrix (gsm_multigpu.hip)
+// (args.schedUnits > 0: one extra workgroup orders the blend units of the renderer's own rows, A)
 void launch_partition_counts(bool halfInput, uint32_t shDegree, const void* world, const void* harmonics,
                              const ProjectArgs& args, const SlabTable& slabs, const PartitionBuffers& B,
-                             const float2* sincos, uint32_t* sendCounts, hipStream_t stream);
+                             const float2* sincos, uint32_t* sendCounts, const DeviceArena& A, hipStream_t stream);
 void launch_partition_push(const ProjectArgs& args, uint32_t world, uint32_t rank, const PartitionBuffers& B,
                            const uint32_t* counts, const SlabPeers& peers, uint32_t* recvCount, const SlabTable& slabs,
                            hipStream_t stream);

@@ -446,7 +446,18 @@ template <bool HALF, int DEG>
 __global__ __launch_bounds__(kProjectBlock) void k_project_part(
     const void* __restrict__ world, const void* __restrict__ harm, ProjectArgs P, SlabTable slabs,
     SplatRecord* __restrict__ records, uint32_t* __restrict__ masks,
-    uint32_t* __restrict__ blockSlabCounts, const float2* __restrict__ sincos) {
+    uint32_t* __restrict__ blockSlabCounts, const float2* __restrict__ sincos, const uint16_t* __restrict__ unitCost,
+    uint32_t* __restrict__ unitOrder, uint32_t* __restrict__ costMax) {
+    // block 0 of a scheduled launch orders the blend units of the rank's own slab (the owner renders
+    // it later in the frame) while the other blocks project -- as k_project's block 0 does
+    if (P.schedUnits) {
+        if (blockIdx.x == 0) {
+            __shared__ uint32_t uoBase[kUoBuckets], uoMax[kProjectBlock / 64];
+            unit_order_block<kProjectBlock>(unitCost, unitOrder, P.schedUnits, uoBase, uoMax, costMax);
+            return;
+        }
+    }
+    const uint32_t blk = blockIdx.x - (P.schedUnits ? 1u : 0u);
     __shared__ uint32_t wcnt[kProjectBlock / 64][kMaxSlabs];
     __shared__ uint16_t div255[256];
     __shared__ TileTestLds L;
@@ -455,7 +466,7 @@ __global__ __launch_bounds__(kProjectBlock) void k_project_part(
     __shared__ uint32_t sRows[kMaxSlabs + 1];
     fill_div255(div255);
     const uint32_t tid = threadIdx.x;
-    const uint32_t gid = blockIdx.x * kProjectBlock + tid;
+    const uint32_t gid = blk * kProjectBlock + tid;
     const uint32_t lane = tid & 63, wave = tid >> 6;
     if (tid <= slabs.n) sRows[tid] = slabs.rows[tid];
     sTile[tid] = 0;
@@ -500,7 +511,7 @@ __global__ __launch_bounds__(kProjectBlock) void k_project_part(
         uint32_t t = 0;
 #pragma unroll
         for (int w = 0; w < kProjectBlock / 64; ++w) t += wcnt[w][tid];
-        blockSlabCounts[(size_t)tid * gridDim.x + blockIdx.x] = t;
+        blockSlabCounts[(size_t)tid * (gridDim.x - (P.schedUnits ? 1u : 0u)) + blk] = t;
     }
 }
 
@@ -1055,11 +1066,13 @@ void launch_project(bool halfInput, uint32_t deg, const void* world, const void*
 template <bool HALF>
 static void launch_project_part_t(uint32_t deg, const void* world, const void* harm, const ProjectArgs& a,
                                   const SlabTable& slabs, const PartitionBuffers& B, const float2* sincos,
-                                  hipStream_t s) {
+                                  const DeviceArena* A, hipStream_t s) {
     const uint32_t blocks = (a.count + kProjectBlock - 1) / kProjectBlock;
-#define GSM_LAUNCH_PPART(D)                                                                        \
-    hipLaunchKernelGGL((k_project_part<HALF, D>), dim3(blocks), dim3(kProjectBlock), 0, s, world,  \
-                       harm, a, slabs, B.records, B.masks, B.blockSlabCounts, sincos)
+    const uint32_t sched = (A && a.schedUnits) ? 1u : 0u;
+#define GSM_LAUNCH_PPART(D)                                                                                 \
+    hipLaunchKernelGGL((k_project_part<HALF, D>), dim3(blocks + sched), dim3(kProjectBlock), 0, s, world,   \
+                       harm, a, slabs, B.records, B.masks, B.blockSlabCounts, sincos,                       \
+                       sched ? A->unitCost : nullptr, sched ? A->unitOrder : nullptr, sched ? A->costMax : nullptr)
     switch (deg) {
         case 0: GSM_LAUNCH_PPART(0); break;
         case 1: GSM_LAUNCH_PPART(1); break;
@@ -1078,8 +1091,10 @@ void launch_partition(bool halfInput, uint32_t deg, const void* world, const voi
         hipMemsetAsync(sendCounts, 0, slabs.n * sizeof(uint32_t), s);
         return;
     }
-    if (halfInput) launch_project_part_t<true>(deg, world, harm, a, slabs, B, sincos, s);
-    else launch_project_part_t<false>(deg, world, harm, a, slabs, B, sincos, s);
+    ProjectArgs pa = a;
+    pa.schedUnits = 0;  // (the send-buffer path leaves the schedule to the receiving renderer)
+    if (halfInput) launch_project_part_t<true>(deg, world, harm, pa, slabs, B, sincos, nullptr, s);
+    else launch_project_part_t<false>(deg, world, harm, pa, slabs, B, sincos, nullptr, s);
     hipLaunchKernelGGL(k_part_scan, dim3(slabs.n), dim3(1024), 0, s, B.blockSlabCounts, blocks, sendCounts);
     hipLaunchKernelGGL(k_part_pack, dim3(blocks), dim3(kProjectBlock), 0, s, B.records, B.masks, a.count, slabs,
                        B.blockSlabCounts, sendCounts, (SplatRecord*)send, capacity);
@@ -1087,14 +1102,13 @@ void launch_partition(bool halfInput, uint32_t deg, const void* world, const voi
 
 void launch_partition_counts(bool halfInput, uint32_t deg, const void* world, const void* harm, const ProjectArgs& a,
                              const SlabTable& slabs, const PartitionBuffers& B, const float2* sincos,
-                             uint32_t* sendCounts, hipStream_t s) {
+                             uint32_t* sendCounts, const DeviceArena& A, hipStream_t s) {
     const uint32_t blocks = (a.count + kProjectBlock - 1) / kProjectBlock;
-    if (blocks == 0) {
-        hipMemsetAsync(sendCounts, 0, slabs.n * sizeof(uint32_t), s);
-        return;
-    }
-    if (halfInput) launch_project_part_t<true>(deg, world, harm, a, slabs, B, sincos, s);
-    else launch_project_part_t<false>(deg, world, harm, a, slabs, B, sincos, s);
+    if (blocks == 0) hipMemsetAsync(sendCounts, 0, slabs.n * sizeof(uint32_t), s);
+    if (blocks == 0 && a.schedUnits == 0) return;  // (no ids: the schedule block may still run)
+    if (halfInput) launch_project_part_t<true>(deg, world, harm, a, slabs, B, sincos, &A, s);
+    else launch_project_part_t<false>(deg, world, harm, a, slabs, B, sincos, &A, s);
+    if (blocks == 0) return;
     hipLaunchKernelGGL(k_part_scan, dim3(slabs.n), dim3(1024), 0, s, B.blockSlabCounts, blocks, sendCounts);
 }
 

@@ -361,7 +361,11 @@ gsm_status MultiGpu::phase(int p, hipStream_t s, const gsm_gaussian_input& in, c
             const uint32_t perIds = (N + world - 1) / world;
             const uint32_t first = rank * perIds < N ? rank * perIds : N;
             const uint32_t cnt = perIds < N - first ? perIds : N - first;
-            st = r_->partitionCounts(s, in, cam, width, height, first, cnt, rows, world, sendCounts_);
+            // the slab's blend units are ordered inside this launch (the long kernel of the frame's
+            // first half), not in the short records-in launch of phase 2
+            const bool mine = rows[rank] < rows[rank + 1];
+            if (mine && (st = r_->setTileRows(rows[rank], rows[rank + 1])) != GSM_OK) return st;
+            st = r_->partitionCounts(s, in, cam, width, height, first, cnt, rows, world, sendCounts_, mine);
             if (st != GSM_OK) return st;
             ++frame_;
             sync(s, 0, sendCounts_, true, false);  // counts into every rank's matrix, then arrive
@@ -381,7 +385,7 @@ gsm_status MultiGpu::phase(int p, hipStream_t s, const gsm_gaussian_input& in, c
                 void* target = gather ? (void*)frame0_ : color;
                 const size_t pitch = gather ? framePitch_ : colorPitch;
                 st = r_->renderRecords(s, mem_ + kRecordsOff, capacity_, width, height, target, pitch, depth,
-                                       depthPitch, recvCount_);
+                                       depthPitch, recvCount_, /*preOrdered=*/true);
                 if (st != GSM_OK) return st;
             }
             if (gather && world > 1) sync(s, 2, nullptr, true, false);  // my band is in rank 0's frame

@@ -253,7 +253,7 @@ gsm_status GlobalRenderer::render(hipStream_t s, const gsm_gaussian_input& in,
 
 gsm_status GlobalRenderer::renderRecords(hipStream_t s, const void* records, uint32_t count, uint32_t width,
                                          uint32_t height, void* color, size_t colorPitch, void* depth,
-                                         size_t depthPitch, const uint32_t* devCount) {
+                                         size_t depthPitch, const uint32_t* devCount, bool preOrdered) {
     // devCount: the count lives on the device (multi-GPU exchange, gsm_multigpu_render); `count` is
     // then the capacity the grids cover
     gsm_status st = validateFrame(count, !records, width, height, color, colorPitch, depth, depthPitch);
@@ -264,7 +264,7 @@ gsm_status GlobalRenderer::renderRecords(hipStream_t s, const void* records, uin
     return runFrame(s, a, width, height, color, colorPitch, depth, depthPitch,
                     [&](const ProjectArgs& pa) {
                         launch_records_in(records, pa, arena_, s, devCount);
-                    }, devCount);
+                    }, devCount, preOrdered);
 }
 
 gsm_status GlobalRenderer::preparePartition(const gsm_gaussian_input& in, const gsm_camera_params& camp,
@@ -325,12 +325,16 @@ gsm_status GlobalRenderer::projectPartition(hipStream_t s, const gsm_gaussian_in
 
 gsm_status GlobalRenderer::partitionCounts(hipStream_t s, const gsm_gaussian_input& in, const gsm_camera_params& camp,
                                            uint32_t width, uint32_t height, uint32_t first, uint32_t count,
-                                           const uint32_t* slabRows, uint32_t numSlabs, uint32_t* sendCounts) {
+                                           const uint32_t* slabRows, uint32_t numSlabs, uint32_t* sendCounts,
+                                           bool orderUnits) {
     PartitionFrame f;
     gsm_status st = preparePartition(in, camp, width, height, first, count, slabRows, numSlabs, false, nullptr,
                                      sendCounts, &f);
     if (st != GSM_OK) return st;
-    launch_partition_counts(f.half, f.deg, f.world, f.harm, f.a, f.slabs, part_, arena_.sincosTable, sendCounts, s);
+    // the blend units of this renderer's rows (its slab), ordered by one extra workgroup of the launch
+    f.a.schedUnits = orderUnits ? scheduleUnits(s, width, height) : 0u;
+    launch_partition_counts(f.half, f.deg, f.world, f.harm, f.a, f.slabs, part_, arena_.sincosTable, sendCounts,
+                            arena_, s);
     partCount_ = count;
     partSlabs_ = f.slabs;
     if (hipGetLastError() != hipSuccess) return GSM_ERR_RENDER_FAILED;
@@ -348,10 +352,23 @@ gsm_status GlobalRenderer::partitionPush(hipStream_t s, uint32_t world, uint32_t
     return GSM_OK;
 }
 
+uint32_t GlobalRenderer::scheduleUnits(hipStream_t s, uint32_t width, uint32_t height) {
+    const uint32_t upt = blend_units_per_tile((rowEnd_ - rowBegin_) * tilesX_, numCUs_);
+    const uint32_t units = (rowEnd_ - rowBegin_) * tilesX_ * upt;
+    const uint64_t key = ((uint64_t)upt << 60) ^ ((uint64_t)width << 40) ^ ((uint64_t)height << 20) ^
+                         ((uint64_t)rowBegin_ << 10) ^ rowEnd_;
+    if (key != schedKey_) {  // new geometry: no walks to order by yet
+        hipMemsetAsync(arena_.unitCost, 0, (size_t)units * sizeof(uint16_t), s);
+        hipMemsetAsync(arena_.costMax, 0, kCostMaxSlots * sizeof(uint32_t), s);
+        schedKey_ = key;
+    }
+    return tuning_.costOrder ? units : 0u;
+}
+
 template <class Front>
 gsm_status GlobalRenderer::runFrame(hipStream_t s, const ProjectArgs& a, uint32_t width, uint32_t height,
                                     void* color, size_t colorPitch, void* depth, size_t depthPitch,
-                                    Front&& front, const uint32_t* devCount) {
+                                    Front&& front, const uint32_t* devCount, bool preOrdered) {
     const bool prof = (profiling_ & 1) != 0;         // every stage bracketed by events
     // only the blend (2 events per frame), on every frame or every period-th (bits 8-15)
     const uint32_t period = ((uint32_t)profiling_ >> 8) & 0xFFu;
@@ -371,18 +388,11 @@ gsm_status GlobalRenderer::runFrame(hipStream_t s, const ProjectArgs& a, uint32_
     // Blend schedule: the units ordered by the walk lengths the previous frame of the same
     // geometry measured (the image does not depend on the order, only the load balance does).
     // The ordering only needs those costs: one extra workgroup of the projection launch does it
-    // (unit_order_block) while the others project (k_project, or k_records_in on the records path).
-    const uint32_t upt = blend_units_per_tile((rowEnd_ - rowBegin_) * tilesX_, numCUs_);
-    const uint32_t units = (rowEnd_ - rowBegin_) * tilesX_ * upt;
-    const uint64_t key = ((uint64_t)upt << 60) ^ ((uint64_t)width << 40) ^ ((uint64_t)height << 20) ^
-                         ((uint64_t)rowBegin_ << 10) ^ rowEnd_;
-    if (key != schedKey_) {
-        hipMemsetAsync(arena_.unitCost, 0, (size_t)units * sizeof(uint16_t), s);
-        hipMemsetAsync(arena_.costMax, 0, kCostMaxSlots * sizeof(uint32_t), s);
-        schedKey_ = key;
-    }
-    const bool costOrder = units > 0 && tuning_.costOrder;
-    fa.schedUnits = costOrder ? units : 0u;
+    // (unit_order_block) while the others project (k_project, or k_records_in on the records path;
+    // the multi-GPU frame orders them earlier, in its partition projection: preOrdered).
+    const uint32_t units = preOrdered ? 0u : scheduleUnits(s, width, height);
+    const bool costOrder = preOrdered ? tuning_.costOrder : units > 0;
+    fa.schedUnits = units;
 
     hipEvent_t* ev = (prof || blendOnly) ? frameEvents(profFrames_) : nullptr;
     if (prof) hipEventRecord(ev[0], s);

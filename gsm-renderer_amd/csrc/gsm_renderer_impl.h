@@ -30,14 +30,17 @@ class GlobalRenderer {
                                 void* send, uint64_t capacity, uint32_t* sendCounts);
     // the same projection for the direct exchange: per-slab counts first, then the records written
     // into every slab owner's receive buffer once the count matrix is on the device (gsm_multigpu.hip)
+    // orderUnits: the launch also orders the blend units of the renderer's own rows (set_tile_rows) for a
+    // later renderRecords(..., preOrdered = true) of the same frame
     gsm_status partitionCounts(hipStream_t stream, const gsm_gaussian_input& input, const gsm_camera_params& camera,
                                uint32_t width, uint32_t height, uint32_t first, uint32_t count,
-                               const uint32_t* slabRows, uint32_t numSlabs, uint32_t* sendCounts);
+                               const uint32_t* slabRows, uint32_t numSlabs, uint32_t* sendCounts,
+                               bool orderUnits = false);
     gsm_status partitionPush(hipStream_t stream, uint32_t world, uint32_t rank, const uint32_t* counts,
                              const SlabPeers& peers, uint32_t* recvCount);
     gsm_status renderRecords(hipStream_t stream, const void* records, uint32_t count, uint32_t width,
                              uint32_t height, void* color, size_t colorPitch, void* depth, size_t depthPitch,
-                             const uint32_t* devCount = nullptr);
+                             const uint32_t* devCount = nullptr, bool preOrdered = false);
     uint32_t maxGaussians() const { return maxGaussians_; }
     uint32_t tilesY() const { return tilesY_; }
     uint32_t maxWidth() const { return maxWidth_; }
@@ -67,7 +70,10 @@ class GlobalRenderer {
     template <class Front>
     gsm_status runFrame(hipStream_t s, const ProjectArgs& a, uint32_t width, uint32_t height, void* color,
                         size_t colorPitch, void* depth, size_t depthPitch, Front&& front,
-                        const uint32_t* devCount = nullptr);
+                        const uint32_t* devCount = nullptr, bool preOrdered = false);
+    // the blend schedule's unit count for the current rows (0 when cost order is off), its cost
+    // arrays cleared when the geometry changed
+    uint32_t scheduleUnits(hipStream_t s, uint32_t width, uint32_t height);
     PartitionBuffers part_;
     uint32_t partCount_ = 0;  // ids of the last partitionCounts
     SlabTable partSlabs_{};   // its slab table (partitionPush cuts each record's tile answers by it)

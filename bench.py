@@ -46,6 +46,39 @@ BLEND_EVENT_PERIOD = 5  # timed frames per bracketed blend (HIP events), see the
 VALU_PEAK_GIPS = 566.0
 VALU_PEAK_SPEC_GIPS = 1024 * 2.4 / 4
 VALU_PEAK_2WPS_GIPS = 508.5
+# Mix-weighted VALU roofline (r03): each class of the blend's VALU instructions (SQ_INSTS_VALU_*
+# counters, tools/traffic.py valu_mix_per_launch) priced at its issue cost in cycles per
+# wave-instruction per SIMD, measured with 8 independent waves per SIMD by tools/exp/valu_peak.hip
+# (profiles/r03_valu_peak.txt): packed 16-bit ops, v_perm_b32, DPP moves, v_max_u32, v_pk_max_u16 and
+# v_cvt_f32_f16 issue at half the 32-bit rate (4.1-4.3 cycles against 2.25), v_exp_f32 at a quarter.
+# "other" = the instructions no SQ_INSTS_VALU_* class counts; in the blends these are v_pk_min_f16,
+# v_perm_b32 (exp-table pairing), DPP / SDWA max (group break), v_pk_max_u16, readlane and moves (static
+# ISA histogram), priced at the half rate; roofline_valu also reports the fraction with "other" at the
+# full 32-bit rate (a lower bound).  Minimal issue time of a launch = sum(n_c * cost_c) / (SIMDs * clock).
+VALU_ISSUE_CYCLES = {"f16": 4.20, "f32": 2.28, "int32": 2.25, "int64": 4.5, "cvt": 4.11, "trans": 8.14, "other": 4.2}
+VALU_SIMDS = 1024
+VALU_CLOCK_GHZ = 2.3  # held under load (s_memtime against s_memrealtime in the probe)
+
+
+def valu_roofline(kernel, insts, mix, t_blend):
+    """roofline_valu of a blend launch: issue rate against the mix-weighted peak (None without PMC)."""
+    if not insts or t_blend <= 0:
+        return None
+    out = {"bound": "valu", "kernel": kernel, "unit": "G wave-instr/s", "achieved": insts / t_blend / 1e9,
+           "insts_per_launch": insts, "frac_of_packed_fp16_peak": insts / t_blend / 1e9 / VALU_PEAK_GIPS,
+           "peak_source": "tools/exp/valu_peak.hip, profiles/r03_valu_peak.txt"}
+    if mix:
+        cycles = sum(n * VALU_ISSUE_CYCLES[c] for c, n in mix.items())
+        t_min = cycles / (VALU_SIMDS * VALU_CLOCK_GHZ * 1e9)
+        lower = (cycles - mix.get("other", 0) * (VALU_ISSUE_CYCLES["other"] - 2.25)) / (VALU_SIMDS * VALU_CLOCK_GHZ * 1e9)
+        out.update({"peak": insts / t_min / 1e9, "frac": t_min / t_blend, "issue_time_us": t_min * 1e6,
+                    "frac_if_other_full_rate": lower / t_blend,
+                    "mix_per_launch": mix, "issue_cycles": VALU_ISSUE_CYCLES, "clock_ghz": VALU_CLOCK_GHZ,
+                    "peak_note": "mix-weighted: each instruction class at its measured issue cost (8 waves/SIMD)"})
+    else:
+        out.update({"peak": VALU_PEAK_GIPS, "frac": insts / t_blend / 1e9 / VALU_PEAK_GIPS,
+                    "peak_note": "no instruction mix measured: every instruction priced as packed fp16 (upper bound)"})
+    return out
 # FETCH_SIZE corrections calibrated on MI355X (tools/exp/fetch_calib.hip, profiles/r02_fetch_calibration.json)
 FETCH_TABLE_RAW_BYTES = 514.5 * 1024  # the blend's 128 KiB LDS table load: 8 XCD L2 misses, tallied at 1/2
 
@@ -65,7 +98,7 @@ def parse():
     p.add_argument("--traffic-json", default=None,
                    help="blend PMC numbers per launch (tools/traffic.py), used when measured on --config; "
                         "default profiles/PMC_TAG_pmc_blend_<cfgN>.json")
-    p.add_argument("--pmc-tag", default="r02", help="round tag of the default PMC files in profiles/")
+    p.add_argument("--pmc-tag", default="r03", help="round tag of the default PMC files in profiles/")
     p.add_argument("--stereo-path", choices=("depthfirst", "global"), default="depthfirst",
                    help="stereo configs: DepthFirst semantics (SURVEY 8f rank 1) or two Global views")
     p.add_argument("--df-max-gaussians", type=int, default=6_000_000,
@@ -311,7 +344,7 @@ def main():
     # outnumber 8 waves x CUs, quadrants otherwise; every unit reads the tile's whole list
     n_cus = torch.cuda.get_device_properties(dev).multi_processor_count
     units_per_tile = 2 if T > 8 * n_cus else 4
-    traffic = valu_insts = traffic_note = None
+    traffic = valu_insts = traffic_note = valu_mix = None
     tj = load_pmc(args.traffic_json, args.config, world_size, "k_blend_px")
     if tj:
         raw_fetch = tj["fetch_size_kib"] * 1024
@@ -327,6 +360,7 @@ def main():
                         f"lists {list_bytes // 2} B; gathers as counted (profiles/r02_fetch_calibration.json); "
                         f"upper bound if every gather segment were 128 B: {int(2 * raw_fetch + write)} B")
         valu_insts = tj.get("valu_insts_per_launch")
+        valu_mix = tj.get("valu_mix_per_launch")
     stage_sum = sum(v for k, v in stage_ms.items() if k != "blend_timed_region")
     sort_gkeys = A / (stage_ms["sort"] * 1e-3) / 1e9 if stage_ms["sort"] > 0 else 0.0
 
@@ -403,14 +437,7 @@ def main():
                      "algorithmic_bytes": b_blend, "launch_timing": f"HIP events around the blend on every {BLEND_EVENT_PERIOD}th frame of the timed region", "avg_launch_ms": blend_ms_timed,
                      "note": "blend is bound by packed-fp16 VALU issue (roofline_valu); HBM fraction "
                              "reported per the metric"},
-        "roofline_valu": ({"bound": "valu", "kernel": "k_blend_px", "unit": "G wave-instr/s",
-                           "achieved": valu_insts / t_blend / 1e9, "peak": VALU_PEAK_GIPS,
-                           "frac": valu_insts / t_blend / 1e9 / VALU_PEAK_GIPS,
-                           "frac_of_peak_at_2_waves_per_simd": valu_insts / t_blend / 1e9 / VALU_PEAK_2WPS_GIPS,
-                           "frac_of_spec_peak": valu_insts / t_blend / 1e9 / VALU_PEAK_SPEC_GIPS,
-                           "insts_per_launch": valu_insts,
-                           "peak_source": "tools/exp/valu_peak.hip, profiles/r02_valu_peak.txt"}
-                          if (valu_insts and t_blend > 0) else None),
+        "roofline_valu": valu_roofline("k_blend_px", valu_insts, valu_mix, t_blend),
         "roofline_frame": {"bound": "hbm", "achieved": b_frame / (ms_per_step * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
                            "unit": "GB/s", "frac": b_frame / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS,
                            "algorithmic_bytes": b_frame,
@@ -590,7 +617,7 @@ def run_depthfirst(args, c, world_np, harm_np, world, harm, dev):
     b_blend = A * 36 + P * 8 + T * 8
     t_blend = blend_ms_timed * 1e-3
     achieved = b_blend / t_blend / 1e9 if t_blend > 0 else 0.0
-    traffic = valu_insts = traffic_note = None
+    traffic = valu_insts = traffic_note = valu_mix = None
     tj = load_pmc(args.traffic_json, args.config, 1, "k_df_blend_eye")
     if tj:
         raw_fetch, write = tj["fetch_size_kib"] * 1024, tj["write_size_kib"] * 1024
@@ -600,6 +627,7 @@ def run_depthfirst(args, c, world_np, harm_np, world, harm, dev):
                         f"launch; wide parts doubled (table, lists), gathers as counted "
                         f"(profiles/r02_fetch_calibration.json); upper bound {int(2 * raw_fetch + write)} B")
         valu_insts = tj.get("valu_insts_per_launch")
+        valu_mix = tj.get("valu_mix_per_launch")
     parity, cpu = None, None
     if args.parity or args.cpu_baseline:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -635,10 +663,7 @@ def run_depthfirst(args, c, world_np, harm_np, world, harm, dev):
                      "traffic_over_algorithmic": (traffic / b_blend) if traffic else None, "traffic_note": traffic_note,
                      "algorithmic_bytes": b_blend, "launch_timing": f"HIP events around the blend on every {BLEND_EVENT_PERIOD}th frame of the timed region", "avg_launch_ms": blend_ms_timed,
                      "note": "blend is bound by packed-fp16 VALU issue (fp16 math per pixel per (tile, eye) unit)"},
-        "roofline_valu": ({"bound": "valu", "kernel": "k_df_blend_eye", "unit": "G wave-instr/s",
-                           "achieved": valu_insts / t_blend / 1e9, "peak": VALU_PEAK_GIPS,
-                           "frac": valu_insts / t_blend / 1e9 / VALU_PEAK_GIPS, "insts_per_launch": valu_insts}
-                          if (valu_insts and t_blend > 0) else None),
+        "roofline_valu": valu_roofline("k_df_blend_eye", valu_insts, valu_mix, t_blend),
         "blend_walk": {"walked": walk[0], "with_mean": walk[1], "blended": walk[2], "list_entries": walk[3]},
         "cpu_baseline": cpu, "stages_ms": stage_ms, "blend_gb_per_s": achieved, "parity_vs_oracle": parity,
     }

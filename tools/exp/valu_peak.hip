@@ -37,7 +37,14 @@ __global__ void k_peak(unsigned* out, unsigned long long* clk) {
     if (OP == 5) asm volatile("v_add_u32 %0, %0, %1" : "+v"(a##i) : "v"(m));                                 \
     if (OP == 6) asm volatile("v_pk_max_u16 %0, %0, %1" : "+v"(a##i) : "v"(m));                              \
     if (OP == 7) asm volatile("v_pk_mul_f32 %0, %0, %1" : "+v"(p##i) : "v"(pm));                             \
-    if (OP == 8) asm volatile("v_pk_fma_f32 %0, %0, %1, %2" : "+v"(p##i) : "v"(pm), "v"(pc));
+    if (OP == 8) asm volatile("v_pk_fma_f32 %0, %0, %1, %2" : "+v"(p##i) : "v"(pm), "v"(pc));               \
+    if (OP == 9) asm volatile("v_add_f16 %0, %0, %1" : "+v"(a##i) : "v"(m));                                 \
+    if (OP == 10) asm volatile("v_perm_b32 %0, %0, %1, %2" : "+v"(a##i) : "v"(m), "v"(c));                   \
+    if (OP == 11) asm volatile("v_cndmask_b32 %0, %0, %1, vcc" : "+v"(a##i) : "v"(m));                       \
+    if (OP == 12) asm volatile("v_mov_b32_dpp %0, %0 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf" : "+v"(a##i)); \
+    if (OP == 13) asm volatile("v_cvt_f32_f16 %0, %0" : "+v"(a##i));                                          \
+    if (OP == 14) asm volatile("v_exp_f32 %0, %0" : "+v"(a##i));                                              \
+    if (OP == 15) asm volatile("v_max_u32 %0, %0, %1" : "+v"(a##i) : "v"(m));
             REP8(ACC)
 #undef ACC
         }
@@ -109,5 +116,12 @@ int main() {
     run<6>("v_pk_max_u16", cus, out, clk);
     run<7>("v_pk_mul_f32", cus, out, clk);
     run<8>("v_pk_fma_f32", cus, out, clk);
+    run<9>("v_add_f16", cus, out, clk);
+    run<10>("v_perm_b32", cus, out, clk);
+    run<11>("v_cndmask_b32", cus, out, clk);
+    run<12>("v_mov_b32_dpp", cus, out, clk);
+    run<13>("v_cvt_f32_f16", cus, out, clk);
+    run<14>("v_exp_f32", cus, out, clk);
+    run<15>("v_max_u32", cus, out, clk);
     return 0;
 }

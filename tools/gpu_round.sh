@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round artefacts on one MI355X: GPU parity tests, smoke, PMC passes (blend traffic and VALU count)
+# Round artefacts on one MI355X: GPU parity tests, smoke, PMC passes (blend traffic, VALU count and mix)
 # of configs 2, 3 and 5, the bench lines of every single-GPU config, and rocprofv3 kernel-trace
 # summaries.  Everything lands in gpurun_out/round/; tools/round_copy.sh TAG copies what is judged
 # into profiles/.  Env: TESTS=0 skips the tests, PMC=0 the counter passes, CFGS limits the configs.
@@ -29,7 +29,9 @@ if [ "${PMC:-1}" = 1 ]; then
     i=0
     for set in "FETCH_SIZE" "WRITE_SIZE" \
                "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE" \
-               "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM"; do
+               "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM" \
+               "SQ_INSTS_VALU_ADD_F16 SQ_INSTS_VALU_MUL_F16 SQ_INSTS_VALU_FMA_F16 SQ_INSTS_VALU_TRANS_F16 SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_CVT SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_MUL_F32" \
+               "SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_VALU_INT64 SQ_THREAD_CYCLES_VALU"; do
       i=$((i+1))
       step pmc_${c}_$i 180 rocprofv3 --pmc $set --output-format csv -d $OUT/pmc_$c/p$i -o p$i -- $CMD
     done

@@ -44,4 +44,14 @@ for k, cs in acc.items():
         "valu_insts_per_launch": int(round(mean(cs, "SQ_INSTS_VALU"))) if "SQ_INSTS_VALU" in cs else None,
         "grbm_gui_active": mean(cs, "GRBM_GUI_ACTIVE"),
     }
+    # the VALU instruction mix by issue class (SQ_INSTS_VALU_* passes): bench.py prices each class at
+    # its measured issue cost (tools/exp/valu_peak.hip) for the mix-weighted roofline_valu
+    cls = {n: mean(cs, "SQ_INSTS_VALU_" + n) for n in ("ADD_F16", "MUL_F16", "FMA_F16", "TRANS_F16", "ADD_F32",
+                                                      "MUL_F32", "FMA_F32", "TRANS_F32", "INT32", "INT64", "CVT")}
+    if all(v is not None for v in cls.values()) and out["valu_insts_per_launch"]:
+        mix = {"f16": cls["ADD_F16"] + cls["MUL_F16"] + cls["FMA_F16"], "trans": cls["TRANS_F16"] + cls["TRANS_F32"],
+               "f32": cls["ADD_F32"] + cls["MUL_F32"] + cls["FMA_F32"], "int32": cls["INT32"], "int64": cls["INT64"],
+               "cvt": cls["CVT"]}
+        mix["other"] = max(0.0, out["valu_insts_per_launch"] - sum(mix.values()))
+        out["valu_mix_per_launch"] = {k: int(round(v)) for k, v in mix.items()}
 print(json.dumps(out, indent=1))

@@ -95,6 +95,8 @@ def parse():
     p.add_argument("--orbit-steps", type=int, default=50,
                    help="moving-camera frames timed after the static ones (single GPU, mono); 0 = off")
     p.add_argument("--parity", type=int, default=1, help="compare the frame with the oracle")
+    p.add_argument("--inflight-steps", type=int, default=50,
+                   help="frames timed with two renderers on two streams (single GPU, mono); 0 = off")
     p.add_argument("--traffic-json", default=None,
                    help="blend PMC numbers per launch (tools/traffic.py), used when measured on --config; "
                         "default profiles/PMC_TAG_pmc_blend_<cfgN>.json")
@@ -280,6 +282,44 @@ def main():
     counters = renderer.counters()
     ms_per_step = elapsed / args.steps * 1e3
     fps = 1e3 / ms_per_step
+    # two frames in flight (single GPU, mono): a second renderer handle on a second stream, frames
+    # alternating between the two -- the double-buffered use of the public API, so one frame's
+    # sort and projection overlap the other's blend tail.  A separate line, not `value`.
+    inflight = None
+    inflight_color = None
+    if world_size == 1 and not stereo and not native_multi and args.inflight_steps > 0:
+        r2 = gsm_amd.GlobalRenderer(device=dev.index, config=cfg)
+        streams = [torch.cuda.Stream(dev), torch.cuda.Stream(dev)]
+        tg = [(color, depth, cptr, dptr), None]
+        c2 = torch.zeros_like(color)
+        d2 = torch.zeros_like(depth)
+        tg[1] = (c2, d2, c2.data_ptr() - slab.y0 * pitch_c, d2.data_ptr() - slab.y0 * pitch_d)
+        rs = [renderer, r2]
+        renderer.set_profiling(stage_events=False)
+        k = [0]
+
+        def step_inflight():
+            i = k[0] & 1
+            k[0] += 1
+            rs[i].render(tg[i][2], tg[i][3], inp, cam, W, H, stream=streams[i], color_pitch=pitch_c,
+                         depth_pitch=pitch_d)
+        torch.cuda.synchronize()
+        for _ in range(args.warmup * 2):
+            step_inflight()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.inflight_steps):
+            step_inflight()
+        torch.cuda.synchronize()
+        t_if = time.perf_counter() - t0
+        inflight = {"value": args.inflight_steps / t_if, "unit": "frames/s", "steps": args.inflight_steps,
+                    "ms_per_step": t_if / args.inflight_steps * 1e3, "renderers": 2, "streams": 2,
+                    "note": "two renderer handles on two HIP streams, frames alternating (double-buffered "
+                            "targets); frames overlap across the handles, each frame is the full hot path",
+                    "parity_both_targets": None}
+        inflight_color = c2
+        r2.close()
+
     # the same frame under camera motion (single GPU, mono): every step a new view, 0.25 degrees
     # further along an orbit about the scene centre, so the blend schedule (last frame's walk
     # lengths, k_unit_order) is always one frame stale -- what the static `value` cannot show
@@ -388,6 +428,9 @@ def main():
             got = color[:H].view(torch.int16).cpu().numpy().view(np.uint16)
             parity = all(bool(np.array_equal(got[:, v * W:(v + 1) * W], r["color"])) for v, r in enumerate(refs)) \
                 and int(refs[-1]["total_assignments"]) == A
+            if inflight is not None and inflight_color is not None:
+                got2 = inflight_color[:H].view(torch.int16).cpu().numpy().view(np.uint16)
+                inflight["parity_both_targets"] = bool(np.array_equal(got2, refs[-1]["color"]))
         if args.cpu_baseline:
             med = float(np.median(times))
             cpu = cpu_baseline_entry(med, threads, f"{reps} full frames of {args.config} ({n} gaussians, "
@@ -448,6 +491,7 @@ def main():
         "sort_gkeys_per_s": sort_gkeys,
         "blend_gb_per_s": achieved,
         "orbit": orbit,
+        "inflight2": inflight,
         "parity_vs_oracle": multi_parity if native_multi else parity,
     }
     if multi_fallback:

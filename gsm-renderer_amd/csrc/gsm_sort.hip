@@ -82,10 +82,10 @@ __global__ __launch_bounds__(kRadixBlock) void k_radix_upsweep(const uint32_t* _
     __syncthreads();
     uint32_t begin, end;
     block_range(*nPtr, gridDim.x, blockIdx.x, &begin, &end);
-    // a chunk's keys are all loaded before any is counted (16 loads in flight per thread);
+    // a chunk's keys are all loaded before any is counted (16 loads in flight per thread), and the
+    // next chunk's loads are issued before this chunk's counting starts (its LDS atomics hide them);
     // order does not matter for a histogram, so they come as 16-byte vectors
-    for (uint32_t cbase = begin; cbase < end; cbase += kRadixChunk) {
-        uint4 q[kRadixItems / 4];
+    auto load_chunk = [&](uint32_t cbase, uint4 (&q)[kRadixItems / 4]) {
 #pragma unroll
         for (int i = 0; i < kRadixItems / 4; ++i) {
             const uint32_t idx = cbase + (uint32_t)(i * kRadixBlock + threadIdx.x) * 4u;
@@ -93,6 +93,13 @@ __global__ __launch_bounds__(kRadixBlock) void k_radix_upsweep(const uint32_t* _
                                   : make_uint4(idx < end ? keys[idx] : 0u, idx + 1u < end ? keys[idx + 1u] : 0u,
                                                idx + 2u < end ? keys[idx + 2u] : 0u, 0u);
         }
+    };
+    uint4 q[kRadixItems / 4];
+    if (begin < end) load_chunk(begin, q);
+    for (uint32_t cbase = begin; cbase < end; cbase += kRadixChunk) {
+        uint4 nq[kRadixItems / 4];
+        const bool more = cbase + kRadixChunk < end;
+        if (more) load_chunk(cbase + kRadixChunk, nq);
 #pragma unroll
         for (int i = 0; i < kRadixItems / 4; ++i) {
             const uint32_t idx = cbase + (uint32_t)(i * kRadixBlock + threadIdx.x) * 4u;
@@ -100,6 +107,10 @@ __global__ __launch_bounds__(kRadixBlock) void k_radix_upsweep(const uint32_t* _
 #pragma unroll
             for (int c = 0; c < 4; ++c)  // per-wave LDS counters: one ds_add per key
                 if (idx + (uint32_t)c < end) atomicAdd(&cnt[wave][(kk[c] >> shift) & (R - 1u)], 1u);
+        }
+        if (more) {
+#pragma unroll
+            for (int i = 0; i < kRadixItems / 4; ++i) q[i] = nq[i];
         }
     }
     __syncthreads();

@@ -44,7 +44,16 @@ __global__ void k_peak(unsigned* out, unsigned long long* clk) {
     if (OP == 12) asm volatile("v_mov_b32_dpp %0, %0 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf" : "+v"(a##i)); \
     if (OP == 13) asm volatile("v_cvt_f32_f16 %0, %0" : "+v"(a##i));                                          \
     if (OP == 14) asm volatile("v_exp_f32 %0, %0" : "+v"(a##i));                                              \
-    if (OP == 15) asm volatile("v_max_u32 %0, %0, %1" : "+v"(a##i) : "v"(m));
+    if (OP == 15) asm volatile("v_max_u32 %0, %0, %1" : "+v"(a##i) : "v"(m));                                \
+    if (OP == 16) asm volatile("v_div_scale_f32 %0, vcc, %0, %1, %0" : "+v"(a##i) : "v"(m) : "vcc");         \
+    if (OP == 17) asm volatile("v_div_fmas_f32 %0, %0, %1, %2" : "+v"(a##i) : "v"(m), "v"(c));               \
+    if (OP == 18) asm volatile("v_div_fixup_f32 %0, %0, %1, %2" : "+v"(a##i) : "v"(m), "v"(c));              \
+    if (OP == 19) asm volatile("v_rcp_f32 %0, %0" : "+v"(a##i));                                              \
+    if (OP == 20) asm volatile("v_sqrt_f32 %0, %0" : "+v"(a##i));                                             \
+    if (OP == 21) asm volatile("v_fma_mix_f32 %0, %0, %1, %2 op_sel_hi:[0,1,0]" : "+v"(a##i) : "v"(m), "v"(c)); \
+    if (OP == 22) asm volatile("v_cvt_f16_f32 %0, %0" : "+v"(a##i));                                          \
+    if (OP == 23) asm volatile("v_cndmask_b32 %0, %0, %1, s[0:1]" : "+v"(a##i) : "v"(m) : "s0", "s1");        \
+    if (OP == 24) asm volatile("v_cmp_gt_f32 s[0:1], %0, %1" : : "v"(a##i), "v"(m) : "s0", "s1");
             REP8(ACC)
 #undef ACC
         }
@@ -123,5 +132,14 @@ int main() {
     run<13>("v_cvt_f32_f16", cus, out, clk);
     run<14>("v_exp_f32", cus, out, clk);
     run<15>("v_max_u32", cus, out, clk);
+    run<16>("v_div_scale_f32", cus, out, clk);
+    run<17>("v_div_fmas_f32", cus, out, clk);
+    run<18>("v_div_fixup_f32", cus, out, clk);
+    run<19>("v_rcp_f32", cus, out, clk);
+    run<20>("v_sqrt_f32", cus, out, clk);
+    run<21>("v_fma_mix_f32", cus, out, clk);
+    run<22>("v_cvt_f16_f32", cus, out, clk);
+    run<23>("v_cndmask_b32_sgpr", cus, out, clk);
+    run<24>("v_cmp_gt_f32", cus, out, clk);
     return 0;
 }

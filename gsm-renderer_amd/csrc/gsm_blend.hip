@@ -205,6 +205,12 @@ __global__ __launch_bounds__(NT) void k_blend_px(
                          : (wv < NTOP ? blockIdx.x * NTOP + wv
                                       : gridDim.x * NTOP + blockIdx.x * (NW - NTOP) + (wv - NTOP));
     bool topPrio = split && wv < NTOP;
+    // When a wave claims its next unit from the queue (flags bits 8-9): 1 (default) after the current
+    // unit, 0 at its start, 2 one 64-entry batch before the walk it made last frame ends (unitCost).
+    // A claim made at the start hides the atomic's latency but hands the next position of the
+    // longest-first order to a wave that stays busy for the rest of its unit, so mid-length units
+    // started late and ran past the end of the work (r03, config 2: blend 140.4 -> 116.8 us late).
+    const uint32_t claimMode = ((uint32_t)flags >> 8) & 3u;
     uint32_t waveMax = 0;  // this wave's longest walk, for the next frame's schedule (costMax)
     // dynamic units: positions gridWaves + stripe + stripes * k from this workgroup's counter
     const uint32_t stripes = (gridDim.x % kQueueStripes) == 0 ? kQueueStripes : 1u;
@@ -228,6 +234,15 @@ __global__ __launch_bounds__(NT) void k_blend_px(
         uint32_t nproc = 0;
         uint32_t ncomp = 0;  // entry at which the unit moved to one pair per lane (trace only)
         uint32_t nextQ = 0;
+        bool claimed = false;
+        // claimMode 2: the walk this unit made last frame (before this frame's walk overwrites it)
+        const uint32_t expWalk = (claimMode == 2 && unitCost) ? __builtin_amdgcn_readfirstlane((uint32_t)unitCost[u]) : 0u;
+        auto claim = [&]() {
+            if (!claimed) {
+                if (lane == 0) nextQ = atomicAdd(myQueue, 1u);
+                claimed = true;
+            }
+        };
 
         h2 T[P], R[P], G[P], B[P], D[P];
 #pragma unroll
@@ -260,7 +275,7 @@ __global__ __launch_bounds__(NT) void k_blend_px(
             uint4 mA = *(const uint4*)(rec + gi2);
             uint32_t mB = rec[gi2].b;
             uint32_t nI = lst[min(192u + lane, last)];
-            if (lane == 0) nextQ = atomicAdd(myQueue, 1u);
+            if (claimMode == 0 || (claimMode == 2 && expWalk <= 64u)) claim();
             if (lane >= count) {
                 bA = pad;
                 bB = 0u;
@@ -312,6 +327,7 @@ __global__ __launch_bounds__(NT) void k_blend_px(
                 }
             }
             for (uint32_t b0 = 0;; b0 += 64u) {
+                if (claimMode == 2 && b0 + 64u >= expWalk) claim();
 #pragma unroll UNROLL
                 for (uint32_t gi = 0; gi < NG; ++gi) {
                     // stage 1: the next group's table words go in flight (independent of T)
@@ -487,6 +503,7 @@ __global__ __launch_bounds__(NT) void k_blend_px(
                     om1[k] = ONE - ac1[k];
                 }
                 for (;;) {
+                    if (claimMode == 2 && e + 64u >= expWalk) claim();
                     // stage 1: the next group's records and table words
                     {
                         const uint32_t jn = e + U1 - bb;  // 4..64
@@ -544,7 +561,7 @@ __global__ __launch_bounds__(NT) void k_blend_px(
             }
         unit_done:;
         } else {
-            if (lane == 0) nextQ = atomicAdd(myQueue, 1u);
+            if (claimMode != 1) claim();
         }
         // write (GlobalShaders.metal:1152-1186); empty tiles keep the clear colour (0,0,0,1)
 #pragma unroll
@@ -564,6 +581,7 @@ __global__ __launch_bounds__(NT) void k_blend_px(
         }
         if (agePrio || topPrio) __builtin_amdgcn_s_setprio(0);
         topPrio = false;
+        claim();  // (no-op when claimed during the walk)
         qi = gridWaves + stripe + stripes * __builtin_amdgcn_readfirstlane(nextQ);
     }
     if (unitCost && lane == 0 && waveMax) atomicMax(&costMax[(blockIdx.x * NW + wv) % kCostMaxSlots], waveMax);
@@ -600,7 +618,7 @@ static int blend_waves_per_wg(uint32_t numTiles, int numCUs) {
 // SIMD (flags bit 2), later units' priority rising with the age of their walk (flags bit 1).
 void launch_blend(const FrameGeometry& g, const DeviceArena& A, void* color,
                   size_t colorPitch, void* depth, size_t depthPitch, int numCUs, bool costOrder, int colorFormat,
-                  hipStream_t s, int wavesOverride) {
+                  hipStream_t s, int wavesOverride, int claim) {
     const uint32_t t0 = g.rowBegin * g.tilesX, t1 = g.rowEnd * g.tilesX;
     if (t1 <= t0) return;
     const uint32_t numTiles = t1 - t0;
@@ -608,7 +626,7 @@ void launch_blend(const FrameGeometry& g, const DeviceArena& A, void* color,
                      (depth == nullptr || ((((uintptr_t)depth) & 7u) == 0 && (depthPitch & 7u) == 0)))
                         ? 1
                         : 0;
-    const int flags = vec | 2 | (costOrder ? 4 : 0) | ((colorFormat & 15) << 4);
+    const int flags = vec | 2 | (costOrder ? 4 : 0) | ((colorFormat & 15) << 4) | ((claim & 3) << 8);
     // A.tileQueue was zeroed by k_scan_blocks earlier in the frame
     const int P = blend_pairs_per_lane(numTiles, numCUs);
     const int waves = wavesOverride ? wavesOverride : blend_waves_per_wg(numTiles, numCUs);

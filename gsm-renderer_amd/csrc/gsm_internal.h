@@ -89,6 +89,8 @@ struct Tuning {
                               // or forced by GSM_SORT_RANK=ballot
     bool costOrder = true;    // GSM_BLEND_SCHED=0: blend units in index order instead of last frame's walks
     int blendWaves = 0;       // GSM_BLEND_WAVES=8|12|16: waves per blend workgroup (0: by frame size)
+    int tileLoBits = 0;       // GSM_SORT_LOBITS=4..8: width of the first tile pass (0: half the tile field)
+    int blendClaim = 1;       // GSM_BLEND_CLAIM=early|late|auto (0/1/2): when a blend wave claims its next unit
 };
 // the environment's settings plus the device probe; `device` is a HIP device id
 Tuning tuning_from_env(int device);
@@ -158,7 +160,7 @@ void launch_headers(const uint32_t* sortedKeys, const FrameGeometry& geo, const 
 // front-to-back fp16 blend + clear (GlobalShaders.metal:140-154, 1030-1187)
 void launch_blend(const FrameGeometry& geo, const DeviceArena& A,
                   void* color, size_t colorPitch, void* depth, size_t depthPitch, int numCUs,
-                  bool costOrder, int colorFormat, hipStream_t stream, int waves = 0);
+                  bool costOrder, int colorFormat, hipStream_t stream, int waves = 0, int claim = 1);
 // blend kernel shape: pixel pairs per lane (0 = quadrant kernel) and blend units per tile
 int blend_pairs_per_lane(uint32_t numTiles, int numCUs);
 uint32_t blend_units_per_tile(uint32_t numTiles, int numCUs);
@@ -178,7 +180,7 @@ int radix_sort_bits(uint32_t* keys[2], uint32_t* vals[2], const uint32_t* nPtr, 
 // (tileStart[0..numTiles], lower bounds for empty tiles); binTotals: kSortTotalsWords words
 int radix_sort_tiles(uint32_t* keys[2], uint32_t* vals[2], const uint32_t* nPtr, uint32_t capacity, uint32_t shift,
                      uint32_t bits, uint32_t* hist, uint32_t* binTotals, uint32_t* tileStart, uint32_t numTiles,
-                     hipStream_t stream, bool ballot);
+                     hipStream_t stream, bool ballot, int loBits = 0);
 uint32_t radix_grid_for_capacity(uint32_t capacity);
 // bytes of the sort workspace (`hist` argument above) for a capacity; zero it once at allocation
 size_t radix_workspace_bytes(uint32_t capacity);

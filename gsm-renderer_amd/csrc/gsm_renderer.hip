@@ -429,7 +429,7 @@ gsm_status GlobalRenderer::runFrame(hipStream_t s, const ProjectArgs& a, uint32_
         // the last tile pass also writes the tile starts (radix_sort_tiles: no pass over the keys)
         const int res = radix_sort_tiles(kb, vb, &arena_.header->totalAssignments, maxAssignments_, 16, tileBits,
                                          arena_.radixHist, arena_.radixBinTotals, arena_.tileStart, tileCount_, s,
-                                         ballot);
+                                         ballot, tuning_.tileLoBits);
         tile_depth_sort(kb[res], vb[res], kb[res ^ 1], vb[res ^ 1], arena_.tileStart, rowBegin_ * tilesX_,
                         (rowEnd_ - rowBegin_) * tilesX_, s, ballot, arena_.halfVals[0], arena_.halfVals[1],
                         arena_.halfCount, tileCount_, capture, numCUs_);
@@ -453,7 +453,7 @@ gsm_status GlobalRenderer::runFrame(hipStream_t s, const ProjectArgs& a, uint32_
     // the schedule from the walks the previous frame's blend recorded (same stream: no join)
     if (prof || blendOnly) hipEventRecord(ev[5], s);
     launch_blend(g, arena_, color, colorPitch, depth, depthPitch, numCUs_, costOrder,
-                 (int)config_.color_format, s, tuning_.blendWaves);
+                 (int)config_.color_format, s, tuning_.blendWaves, tuning_.blendClaim);
     if (prof || blendOnly) hipEventRecord(ev[6], s);
     if (prof || blendOnly) profFrames_++;
     haveTimes_ = profFrames_ > 0;

@@ -449,7 +449,7 @@ int radix_sort_bits(uint32_t* keys[2], uint32_t* vals[2], const uint32_t* nPtr, 
 // starts at +512.
 int radix_sort_tiles(uint32_t* keys[2], uint32_t* vals[2], const uint32_t* nPtr, uint32_t capacity, uint32_t shift,
                      uint32_t bits, uint32_t* hist, uint32_t* binTotals, uint32_t* tileStart, uint32_t numTiles,
-                     hipStream_t s, bool ballot) {
+                     hipStream_t s, bool ballot, int loBits) {
     const uint32_t grid = radix_grid_for_capacity(capacity);
     if (bits > 16) bits = 16;
     TileStarts ts{};
@@ -460,7 +460,9 @@ int radix_sort_tiles(uint32_t* keys[2], uint32_t* vals[2], const uint32_t* nPtr,
                    binTotals, s, ballot, &ts, true);
         return 1;
     }
-    const uint32_t lo = (bits + 1u) / 2u, hi = bits - lo;  // radix_sort_bits' digit widths
+    uint32_t lo = (bits + 1u) / 2u;  // radix_sort_bits' digit widths unless a create-time width is set
+    if (loBits >= 4 && loBits <= 8 && bits - (uint32_t)loBits >= 1u && bits - (uint32_t)loBits <= 8u) lo = (uint32_t)loBits;
+    const uint32_t hi = bits - lo < 4u ? 4u : bits - lo;  // (a digit wider than the bits left reads zeros)
     TileStarts first{};
     first.bucketStartOut = binTotals + 512;
     radix_pass(keys[0], vals[0], keys[1], vals[1], nPtr, grid, shift, (int)lo, hist, binTotals + 256, s, ballot,
@@ -855,6 +857,10 @@ Tuning tuning_from_env(int device) {
     const char* wv = getenv("GSM_BLEND_WAVES");
     const int w = wv ? atoi(wv) : 0;
     t.blendWaves = (w == 8 || w == 12 || w == 16) ? w : 0;
+    const char* lb = getenv("GSM_SORT_LOBITS");
+    t.tileLoBits = lb ? atoi(lb) : 0;
+    const char* cv = getenv("GSM_BLEND_CLAIM");
+    t.blendClaim = !cv ? 1 : std::strcmp(cv, "early") == 0 ? 0 : std::strcmp(cv, "auto") == 0 ? 2 : 1;
     return t;
 }
 

@@ -28,6 +28,8 @@ def main():
     ap.add_argument("--world", type=int, default=8)
     ap.add_argument("--frames", type=int, default=5)
     ap.add_argument("--stages", type=int, default=1, help="also time the slab render's stages")
+    ap.add_argument("--trace-rank", type=int, default=-1,
+                    help="per-unit blend trace of this rank's slab (profiling bit 2) -> gpurun_out/vr_trace_*.npz")
     a = ap.parse_args()
     import torch
     import gsm_amd as gsm
@@ -85,13 +87,34 @@ def main():
                 stages.append({nm: round(float(t[k]), 4) for nm, k in zip(names, ["project", "scan", "scatter", "sort", "headers", "blend"])})
             except gsm.RendererError:
                 stages.append(None)  # a rank without rows renders nothing
+    trace = None
+    if a.trace_rank >= 0:
+        r = rends[a.trace_rank]
+        r.set_profiling(stage_events=False, blend_trace=True)
+        for _ in range(2):
+            frame(False)
+        torch.cuda.synchronize()
+        tr = r.copy_buffer(gsm.BufferId.BLEND_TRACE).astype(np.int64)
+        tr = tr[tr[:, 1] > 0]
+        os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+        np.savez(os.path.join(ROOT, "gpurun_out", f"vr_trace_{a.config}_w{W}_r{a.trace_rank}.npz"), trace=tr)
+        t0 = tr[:, 0].min()
+        st, en = (tr[:, 0] - t0) * 0.01, (tr[:, 1] - t0) * 0.01  # 100 MHz ticks -> us
+        dur, walk = en - st, tr[:, 2] & 0xFFFFFFFF
+        span = float(en.max())
+        grid = np.linspace(0, span, 11)[:-1] + span / 20
+        trace = {"units": int(tr.shape[0]), "span_us": round(span, 1), "max_unit_us": round(float(dur.max()), 1),
+                 "mean_unit_us": round(float(dur.mean()), 1), "sum_unit_us": round(float(dur.sum()), 1),
+                 "max_walk": int(walk.max()), "mean_walk": round(float(walk.mean()), 1),
+                 "occupancy_deciles": [int(((st <= x) & (en > x)).sum()) for x in grid],
+                 "first_start_spread_us": round(float(np.sort(st)[min(len(st) - 1, 3000)]), 1)}
     med = np.median(ph, axis=0)  # [phase][rank]
     out = {"config": a.config, "world": W, "frames": a.frames, "timeouts": [m.status() for m in mgs],
            "counts": mgs[0].counts().tolist(),
            "phase_ms": {f"phase{p}": [round(float(x), 4) for x in med[p]] for p in range(4)},
            "max_phase_ms": [round(float(med[p].max()), 4) for p in range(4)],
            "device_frame_ms": round(float(sum(med[p].max() for p in range(4))), 4),
-           "slab_stages_ms": stages,
+           "slab_stages_ms": stages, "blend_trace": trace,
            "note": "virtual ranks on one GPU, product kernels, one stream; no xGMI (pushes and pixels stay local)"}
     print(json.dumps(out))
     for m in mgs:

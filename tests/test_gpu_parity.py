@@ -403,11 +403,13 @@ def test_stereo_is_unsupported_like_the_reference(gsm, cuda):
 
 
 @pytest.mark.parametrize("env", [{"GSM_SORT_RANK": "ballot"}, {"GSM_BLEND_SCHED": "0"},
-                                 {"GSM_SORT": "radix4"}])
+                                 {"GSM_SORT": "radix4"}, {"GSM_BLEND_CLAIM": "early"},
+                                 {"GSM_BLEND_CLAIM": "auto"}])
 def test_create_time_switches_frames_match(gsm, cuda, oracle, monkeypatch, env):
     """The A/B switches read once at create (Tuning, gsm_internal.h) -- ballot sort ranks, index-order
-    blend schedule, the 4 x 8-bit full-key sort -- render the same frames bit for bit, first and
-    later frames (later ones take last frame's cost order when the schedule is on)."""
+    blend schedule, the 4 x 8-bit full-key sort, the blend queue's claim point -- render the same
+    frames bit for bit, first and later frames (later ones take last frame's cost order when the
+    schedule is on)."""
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     case = _synth(200_000, 1280, 720, 16, 1, 33)

@@ -602,12 +602,12 @@ uint32_t blend_units_per_tile(uint32_t numTiles, int numCUs) {
 }
 
 static int blend_waves_per_wg(uint32_t numTiles, int numCUs) {
-    // 16 waves per CU hide more latency once every wave slot gets >= 4 units (4K: 32400 units; two
-    // 1440x1600 views: 18000, r03 with the late queue claim 1166 -> 1192 frames/s against 12 waves);
+    // 16 waves per CU hide more latency once every wave slot gets >= 6 units (4K: 16200 tiles);
     // with fewer units per slot the tail weighs more: 12 waves from 2 units per slot (1080p: 8160
-    // units, r03: 3823 frames/s against 3672 at 16 and 3683 at 8), 8 below
+    // units, 3213 -> 3268 frames/s; two 1440x1600 views 1046 -> 1086, r02 fused-accumulate blend),
+    // 8 below (r03, late queue claim: DESIGN.md 10)
     const uint64_t units = (uint64_t)numTiles * blend_units_per_tile(numTiles, numCUs);
-    if (units >= 4ull * (uint64_t)numCUs * 16u) return 16;
+    if (units >= 6ull * (uint64_t)numCUs * 16u) return 16;
     return units >= 2ull * (uint64_t)numCUs * 12u ? 12 : 8;
 }
 

@@ -256,20 +256,20 @@ gsm_status DepthFirstRenderer::renderStereoSbs(hipStream_t s, const gsm_gaussian
     launch_scan_sums(A_.blockSums, nb, maxGaussians_, A_.visHdr, A_.queue, s);
     df_launch_compact(a, A_, s);
     if (prof) hipEventRecord(ev[1], s);
-    // DepthRadixSortEncoder, 32-bit keys (DepthFirstRenderer.swift:664-681): stable LSD, 4 x 8 bits
+    // DepthRadixSortEncoder, 32-bit keys (DepthFirstRenderer.swift:664-681): stable LSD
+    // (3 wide passes of 11/11/10 bits unless GSM_SORT_WIDE=0: the same stable order)
     const int dc = radix_sort_bits(A_.dkeys, A_.dvals, &A_.visHdr->totalAssignments, maxGaussians_, 0, 32,
-                                   A_.radixHist, A_.radixBinTotals, s, tuning_.ballotRank);
+                                   A_.radixHist, A_.radixBinTotals, s, tuning_.ballotRank, tuning_.wideSort);
     if (prof) hipEventRecord(ev[2], s);
     df_launch_instance_counts(A_.dvals[dc], a, A_, s);
     launch_scan_sums(A_.instSums, nb, maxInstances_, A_.instHdr, A_.queue, s);
     df_launch_instances(A_.dvals[dc], a, A_, s);  // with the blend's skip flags
     if (prof) hipEventRecord(ev[3], s);
     // TileSortEncoder (DepthFirstRenderer.swift:683-768): stable sort by the 16-bit tile id
-    uint32_t tileBits = 0;
-    while (tileBits < 16 && ((a.tileCount - 1u) >> tileBits)) tileBits++;
     // the last pass also writes the tile ranges' starts (radix_sort_tiles: no pass over the instances)
-    const int ic = radix_sort_tiles(A_.ikeys, A_.ivals, &A_.instHdr->totalAssignments, maxInstances_, 0, tileBits,
-                                    A_.radixHist, A_.radixBinTotals, A_.starts, a.tileCount, s, tuning_.ballotRank);
+    const int ic = radix_sort_tiles(A_.ikeys, A_.ivals, &A_.instHdr->totalAssignments, maxInstances_, 0, A_.radixHist,
+                                    A_.radixBinTotals, A_.starts, 0u, a.tileCount, a.tileCount, s, tuning_.ballotRank,
+                                    0, tuning_.wideSort);
     // Blend schedule: (tile, eye) units handed out longest first by the walk lengths the previous
     // frame of the same geometry measured (the image does not depend on the order, only the load
     // balance does).  Tuning::costOrder false (GSM_BLEND_SCHED=0 at create): index order.

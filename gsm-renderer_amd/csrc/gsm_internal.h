@@ -91,6 +91,7 @@ struct Tuning {
     int blendWaves = 0;       // GSM_BLEND_WAVES=8|12|16: waves per blend workgroup (0: by frame size)
     int tileLoBits = 0;       // GSM_SORT_LOBITS=4..8: width of the first tile pass (0: half the tile field)
     int blendClaim = 1;       // GSM_BLEND_CLAIM=early|late|auto (0/1/2): when a blend wave claims its next unit
+    bool wideSort = true;     // GSM_SORT_WIDE=0: no wide (9..11-bit) radix passes (radix_sort_bits / _tiles)
 };
 // the environment's settings plus the device probe; `device` is a HIP device id
 Tuning tuning_from_env(int device);
@@ -116,8 +117,11 @@ constexpr int kRadixBlock = 256;
 #endif
 constexpr int kRadixItems = GSM_RADIX_ITEMS;  // keys per thread per chunk (4096-key chunks)
 constexpr int kRadixChunk = kRadixBlock * kRadixItems;
+// wide radix digits (gsm_sort.hip): up to 11 bits, 2048 bins
+constexpr uint32_t kWideMaxBits = 11, kWideBins = 1u << kWideMaxBits;
 // radix_sort_tiles' workspace beside the histogram: two passes' digit totals + the bucket starts
-constexpr size_t kSortTotalsWords = 768;
+// (narrow passes, 768 words), or one wide pass's 2048 digit totals
+constexpr size_t kSortTotalsWords = kWideBins;
 
 // project + cull + SH + tile count + per-block count sums (GlobalShaders.metal:19-123, 563-616)
 void launch_project(bool halfInput, uint32_t shDegree, const void* world, const void* harmonics,
@@ -172,15 +176,17 @@ int radix_sort_pairs(uint32_t* keys[2], uint32_t* vals[2], const uint32_t* nPtr,
                      int firstDigit, int numDigits, uint32_t* hist, uint32_t* binTotals,
                      hipStream_t stream, bool ballot);
 // Stable LSD radix sort by bits [shift, shift + bits) only, in ceil(bits / 8) passes of
-// near-equal digit widths (4..8 bits).  Returns the ping-pong index of the result.
+// near-equal digit widths (4..8 bits), or -- `wide` and where that saves a pass -- ceil(bits / 11)
+// passes of 9..11 bits.  binTotals: kSortTotalsWords words.  Returns the ping-pong index of the result.
 int radix_sort_bits(uint32_t* keys[2], uint32_t* vals[2], const uint32_t* nPtr, uint32_t capacity,
                     uint32_t shift, uint32_t bits, uint32_t* hist, uint32_t* binTotals, hipStream_t stream,
-                    bool ballot);
-// the frame sort's tile field (bits <= 16) with the tile starts written by its last pass
-// (tileStart[0..numTiles], lower bounds for empty tiles); binTotals: kSortTotalsWords words
+                    bool ballot, bool wide = true);
+// the frame sort's tile field (tiles [tileBase, tileBase + numTiles) of allTiles, bits <= 16) with
+// the tile starts written by its last pass (tileStart[0..allTiles], lower bounds for empty tiles);
+// one wide pass relative to tileBase when numTiles <= 2048 and `wide`; binTotals: kSortTotalsWords words
 int radix_sort_tiles(uint32_t* keys[2], uint32_t* vals[2], const uint32_t* nPtr, uint32_t capacity, uint32_t shift,
-                     uint32_t bits, uint32_t* hist, uint32_t* binTotals, uint32_t* tileStart, uint32_t numTiles,
-                     hipStream_t stream, bool ballot, int loBits = 0);
+                     uint32_t* hist, uint32_t* binTotals, uint32_t* tileStart, uint32_t tileBase, uint32_t numTiles,
+                     uint32_t allTiles, hipStream_t stream, bool ballot, int loBits = 0, bool wide = true);
 uint32_t radix_grid_for_capacity(uint32_t capacity);
 // bytes of the sort workspace (`hist` argument above) for a capacity; zero it once at allocation
 size_t radix_workspace_bytes(uint32_t capacity);

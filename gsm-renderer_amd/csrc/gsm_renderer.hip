@@ -424,12 +424,12 @@ gsm_status GlobalRenderer::runFrame(hipStream_t s, const ProjectArgs& a, uint32_
     const bool fullRadix = tuning_.fullRadix;
     const bool ballot = tuning_.ballotRank;
     if (!fullRadix) {
-        uint32_t tileBits = 1;
-        while (tileBits < 16 && (tileCount_ - 1u) >> tileBits) tileBits++;
-        // the last tile pass also writes the tile starts (radix_sort_tiles: no pass over the keys)
-        const int res = radix_sort_tiles(kb, vb, &arena_.header->totalAssignments, maxAssignments_, 16, tileBits,
-                                         arena_.radixHist, arena_.radixBinTotals, arena_.tileStart, tileCount_, s,
-                                         ballot, tuning_.tileLoBits);
+        // the last tile pass also writes the tile starts (radix_sort_tiles: no pass over the keys); a
+        // slab of <= 2048 tiles (multi-GPU) takes one wide pass over its tiles' ids
+        const int res = radix_sort_tiles(kb, vb, &arena_.header->totalAssignments, maxAssignments_, 16,
+                                         arena_.radixHist, arena_.radixBinTotals, arena_.tileStart, rowBegin_ * tilesX_,
+                                         (rowEnd_ - rowBegin_) * tilesX_, tileCount_, s, ballot, tuning_.tileLoBits,
+                                         tuning_.wideSort);
         tile_depth_sort(kb[res], vb[res], kb[res ^ 1], vb[res ^ 1], arena_.tileStart, rowBegin_ * tilesX_,
                         (rowEnd_ - rowBegin_) * tilesX_, s, ballot, arena_.halfVals[0], arena_.halfVals[1],
                         arena_.halfCount, tileCount_, capture, numCUs_);

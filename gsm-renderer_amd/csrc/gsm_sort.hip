@@ -366,9 +366,298 @@ __global__ __launch_bounds__(kRadixBlock) void k_radix_downsweep(
     }
 }
 
+// ---------------------------------------------------------------------------
+// Wide digits (9..11 bits, up to 2048 bins): one pass where the narrow kernels need two.  Used
+// where the bits to sort drop by a whole pass: the DepthFirst depth sort's 32-bit keys (3 passes
+// of 11/11/10 bits instead of 4 of 8) and the tile field of a frame with <= 2048 tiles in its rows
+// (a multi-GPU slab, keys counted relative to the slab's first tile: one pass instead of two).
+// Same chunks, block ranges and stable ranks as the narrow downsweep; what changes is the
+// per-chunk digit bookkeeping: thread t owns the 2^BITS / 256 contiguous digits [t * DPT, +DPT)
+// (registers for their running global bases), and the per-wave counters are padded one word in
+// eight so those contiguous reads hit distinct LDS banks.
+// digit(k) = ((k >> shift) - base) & (2^BITS - 1): base = the slab's first tile (0 otherwise).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t wide_pad(uint32_t d) { return d + (d >> 3); }
+// block-major count rows of 2^BITS words, padded by 256 B (rows of a power-of-two stride all start on
+// the same HBM channel group)
+constexpr uint32_t kWideRowPad = 64;
+
+template <int BITS>
+__global__ __launch_bounds__(kRadixBlock) void k_wide_upsweep(const uint32_t* __restrict__ keys,
+                                                              const uint32_t* __restrict__ nPtr, uint32_t shift,
+                                                              uint32_t base, uint32_t* __restrict__ hist) {
+    constexpr uint32_t R = 1u << BITS;
+    // one counter array: a histogram needs no order, and 2^BITS bins spread the atomics
+    __shared__ uint32_t cnt[R];
+    for (uint32_t i = threadIdx.x; i < R; i += kRadixBlock) cnt[i] = 0;
+    __syncthreads();
+    uint32_t begin, end;
+    block_range(*nPtr, gridDim.x, blockIdx.x, &begin, &end);
+    auto load_chunk = [&](uint32_t cbase, uint4 (&q)[kRadixItems / 4]) {
+#pragma unroll
+        for (int i = 0; i < kRadixItems / 4; ++i) {
+            const uint32_t idx = cbase + (uint32_t)(i * kRadixBlock + threadIdx.x) * 4u;
+            q[i] = idx + 3u < end ? *(const uint4*)(keys + idx)
+                                  : make_uint4(idx < end ? keys[idx] : 0u, idx + 1u < end ? keys[idx + 1u] : 0u,
+                                               idx + 2u < end ? keys[idx + 2u] : 0u, 0u);
+        }
+    };
+    uint4 q[kRadixItems / 4];
+    if (begin < end) load_chunk(begin, q);
+    for (uint32_t cbase = begin; cbase < end; cbase += kRadixChunk) {
+        uint4 nq[kRadixItems / 4];
+        const bool more = cbase + kRadixChunk < end;
+        if (more) load_chunk(cbase + kRadixChunk, nq);
+#pragma unroll
+        for (int i = 0; i < kRadixItems / 4; ++i) {
+            const uint32_t idx = cbase + (uint32_t)(i * kRadixBlock + threadIdx.x) * 4u;
+            const uint32_t kk[4] = {q[i].x, q[i].y, q[i].z, q[i].w};
+#pragma unroll
+            for (int c = 0; c < 4; ++c)
+                if (idx + (uint32_t)c < end) atomicAdd(&cnt[((kk[c] >> shift) - base) & (R - 1u)], 1u);
+        }
+        if (more) {
+#pragma unroll
+            for (int i = 0; i < kRadixItems / 4; ++i) q[i] = nq[i];
+        }
+    }
+    __syncthreads();
+    // block-major counts (hist[b][d]): coalesced here, and the downsweep reads its row contiguously
+    for (uint32_t d = threadIdx.x; d < R; d += kRadixBlock) hist[(size_t)blockIdx.x * (R + kWideRowPad) + d] = cnt[d];
+}
+
+// Exclusive scan over blocks of the block-major wide counts, in place, digit totals out.  Workgroup g
+// owns digits [16g, 16g + 16); thread t scans digit 16g + (t & 15) over the (t >> 4)-th sixteenth of
+// the blocks (16 loads in flight), the 16 segment sums meet in LDS, then each thread writes its
+// running prefix back (the re-read hits L2).  16 digits per workgroup: 128 workgroups at 11 bits.
+constexpr uint32_t kWideScanDigits = 16;
+template <int BITS>
+__global__ __launch_bounds__(256) void k_wide_scan(uint32_t* __restrict__ hist, uint32_t grid,
+                                                   uint32_t* __restrict__ binTotals) {
+    constexpr uint32_t R = 1u << BITS;
+    constexpr uint32_t S = 256 / kWideScanDigits;  // segments
+    __shared__ uint32_t ss[S][kWideScanDigits];
+    const uint32_t j = threadIdx.x % kWideScanDigits, sg = threadIdx.x / kWideScanDigits;
+    const uint32_t d = blockIdx.x * kWideScanDigits + j;
+    const uint32_t q = (grid + S - 1) / S;
+    const uint32_t b0 = min(sg * q, grid), b1 = min(b0 + q, grid);
+    uint32_t* col = hist + d;
+    uint32_t sum = 0;
+    for (uint32_t b = b0; b < b1; b += 16u) {
+        uint32_t v[16];
+#pragma unroll
+        for (uint32_t i = 0; i < 16; ++i) v[i] = b + i < b1 ? col[(size_t)(b + i) * (R + kWideRowPad)] : 0u;
+#pragma unroll
+        for (uint32_t i = 0; i < 16; ++i) sum += v[i];
+    }
+    ss[sg][j] = sum;
+    __syncthreads();
+    uint32_t run = 0, tot = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < S; ++w) {
+        const uint32_t x = ss[w][j];
+        if (w < sg) run += x;
+        tot += x;
+    }
+    if (sg == 0) binTotals[d] = tot;
+    for (uint32_t b = b0; b < b1; b += 16u) {
+        uint32_t v[16];
+#pragma unroll
+        for (uint32_t i = 0; i < 16; ++i) v[i] = b + i < b1 ? col[(size_t)(b + i) * (R + kWideRowPad)] : 0u;
+#pragma unroll
+        for (uint32_t i = 0; i < 16; ++i)
+            if (b + i < b1) {
+                col[(size_t)(b + i) * (R + kWideRowPad)] = run;
+                run += v[i];
+            }
+    }
+}
+
+// Exclusive scan over the block of one value per thread (4 waves); returns this thread's offset.
+__device__ __forceinline__ uint32_t wide_block_scan(uint32_t x, uint32_t* part, uint32_t* total) {
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    uint32_t inc = x;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t t = __shfl_up(inc, o, 64);
+        if (lane >= (uint32_t)o) inc += t;
+    }
+    if (lane == 63) part[wave] = inc;
+    __syncthreads();
+    uint32_t off = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < kWaves; ++w) {
+        if ((uint32_t)w < wave) off += part[w];
+        tot += part[w];
+    }
+    *total = tot;
+    return off + inc - x;
+}
+
+// STARTS (one pass over a frame's tile field, radix_sort_tiles): block 0 writes every tile's start
+// -- the exclusive scan of the digit totals, i.e. its digit's global base -- tiles before the
+// slab start at 0 and those after it at n (no keys there), tileStart[allTiles] = n.
+template <int BITS, bool BALLOT, bool STARTS>
+__global__ __launch_bounds__(kRadixBlock) void k_wide_downsweep(
+    const uint32_t* __restrict__ keysIn, const uint32_t* __restrict__ valsIn, uint32_t* __restrict__ keysOut,
+    uint32_t* __restrict__ valsOut, const uint32_t* __restrict__ nPtr, uint32_t shift, uint32_t base,
+    const uint32_t* __restrict__ hist, const uint32_t* __restrict__ binTotals, uint32_t* __restrict__ tileStart,
+    uint32_t numTiles, uint32_t allTiles) {
+    constexpr uint32_t R = 1u << BITS;
+    constexpr uint32_t DPT = R / kRadixBlock;  // digits per thread
+    constexpr uint32_t RP = (R + R / 8 + 255u) / 256u * 256u;  // padded counter rows (whole uint4 zeroing rounds)
+    static_assert(DPT >= 2 && DPT <= 8, "wide digits: 9..11 bits");
+    __shared__ __attribute__((aligned(16))) uint32_t waveCnt[kWaves][RP];  // ranks, then each wave's LDS start per digit
+    __shared__ uint32_t adj[RP];               // per digit: global destination minus LDS start
+    __shared__ uint32_t sKeys[kRadixChunk];
+    __shared__ uint32_t sVals[kRadixChunk];
+    __shared__ uint32_t part[kWaves];
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+    const uint32_t n = *nPtr;
+    uint32_t begin, end;
+    block_range(n, gridDim.x, blockIdx.x, &begin, &end);
+    const uint32_t d0 = tid * DPT;  // this thread's digits
+    auto zero_counters = [&]() {    // 16-byte stores
+        static_assert((kWaves * RP) % (4 * kRadixBlock) == 0, "counter rows in whole uint4 rounds");
+        uint4* z = (uint4*)&waveCnt[0][0];
+#pragma unroll
+        for (uint32_t i = 0; i < kWaves * RP / 4 / kRadixBlock; ++i) z[i * kRadixBlock + tid] = make_uint4(0u, 0u, 0u, 0u);
+    };
+
+    // global base of this thread's digits: exclusive scan of the digit totals + the block's column
+    uint32_t gbase[DPT];
+    {
+        uint32_t run = 0;
+#pragma unroll
+        for (uint32_t i = 0; i < DPT; ++i) {
+            gbase[i] = run;
+            run += binTotals[d0 + i];
+        }
+        uint32_t tot;
+        const uint32_t off = wide_block_scan(run, part, &tot);
+#pragma unroll
+        for (uint32_t i = 0; i < DPT; ++i) gbase[i] += off;
+        if (STARTS && blockIdx.x == 0) {
+            // tiles [base, base + numTiles) of allTiles: their digits' global bases
+            for (uint32_t t = tid; t < base; t += kRadixBlock) tileStart[t] = 0u;
+#pragma unroll
+            for (uint32_t i = 0; i < DPT; ++i)
+                if (d0 + i < numTiles) tileStart[base + d0 + i] = gbase[i];
+            for (uint32_t t = base + numTiles + tid; t <= allTiles; t += kRadixBlock) tileStart[t] = n;
+        }
+        if (begin >= end) return;
+        const uint32_t* row = hist + (size_t)blockIdx.x * (R + kWideRowPad) + d0;  // block-major (k_wide_scan)
+#pragma unroll
+        for (uint32_t i = 0; i < DPT; ++i) gbase[i] += row[i];
+        zero_counters();
+        __syncthreads();
+    }
+
+    const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    for (uint32_t cbase = begin; cbase < end; cbase += kRadixChunk) {
+        uint32_t k[kRadixItems], v[kRadixItems], rank[kRadixItems];
+#pragma unroll
+        for (int j = 0; j < kRadixItems; ++j) {
+            const uint32_t idx = cbase + wave * (64 * kRadixItems) + j * 64 + lane;
+            const bool valid = idx < end;
+            k[j] = valid ? keysIn[idx] : 0u;
+            v[j] = valid ? valsIn[idx] : 0u;
+        }
+#pragma unroll
+        for (int j = 0; j < kRadixItems; ++j) {
+            const uint32_t idx = cbase + wave * (64 * kRadixItems) + j * 64 + lane;
+            const bool valid = idx < end;
+            const uint32_t d = ((k[j] >> shift) - base) & (R - 1u);
+            if constexpr (BALLOT) {
+                const uint64_t peers = match_digit<BITS>(d, valid);
+                const uint32_t before = waveCnt[wave][wide_pad(d)];
+                if (valid && (peers & lt) == 0) waveCnt[wave][wide_pad(d)] = before + (uint32_t)__popcll(peers);
+                rank[j] = before + (uint32_t)__popcll(peers & lt);
+            } else {
+                rank[j] = valid ? atomicAdd(&waveCnt[wave][wide_pad(d)], 1u) : 0u;
+            }
+        }
+        __syncthreads();
+        // per digit: chunk total, its LDS start (scan over digits), each wave's start within it
+        {
+            uint32_t c[DPT][kWaves], tot[DPT], run = 0;
+#pragma unroll
+            for (uint32_t i = 0; i < DPT; ++i) {
+                tot[i] = 0;
+#pragma unroll
+                for (int w = 0; w < kWaves; ++w) {
+                    c[i][w] = waveCnt[w][wide_pad(d0 + i)];
+                    tot[i] += c[i][w];
+                }
+                run += tot[i];
+            }
+            uint32_t all;
+            uint32_t ls = wide_block_scan(run, part, &all);
+#pragma unroll
+            for (uint32_t i = 0; i < DPT; ++i) {
+                const uint32_t pd = wide_pad(d0 + i);
+                adj[pd] = gbase[i] - ls;
+                gbase[i] += tot[i];
+#pragma unroll
+                for (int w = 0; w < kWaves; ++w) {
+                    waveCnt[w][pd] = ls;
+                    ls += c[i][w];
+                }
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < kRadixItems; ++j) {
+            const uint32_t idx = cbase + wave * (64 * kRadixItems) + j * 64 + lane;
+            if (idx < end) {
+                const uint32_t pos = waveCnt[wave][wide_pad(((k[j] >> shift) - base) & (R - 1u))] + rank[j];
+                sKeys[pos] = k[j];
+                sVals[pos] = v[j];
+            }
+        }
+        __syncthreads();
+        zero_counters();
+        const uint32_t cn = min((uint32_t)kRadixChunk, end - cbase);
+        for (uint32_t p = tid; p < cn; p += kRadixBlock) {
+            const uint32_t key = sKeys[p];
+            const uint32_t dst = adj[wide_pad(((key >> shift) - base) & (R - 1u))] + p;
+            keysOut[dst] = key;
+            valsOut[dst] = sVals[p];
+        }
+        __syncthreads();
+    }
+}
+
+static void wide_pass(uint32_t* kin, uint32_t* vin, uint32_t* kout, uint32_t* vout, const uint32_t* nPtr,
+                      uint32_t grid, uint32_t shift, uint32_t base, int bits, uint32_t* hist, uint32_t* binTotals,
+                      hipStream_t s, bool ballot, bool starts, uint32_t* tileStart, uint32_t numTiles,
+                      uint32_t allTiles) {
+#define GSM_WIDE_DOWN(B, BAL, S)                                                                              \
+    hipLaunchKernelGGL((k_wide_downsweep<B, BAL, S>), dim3(grid), dim3(kRadixBlock), 0, s, kin, vin, kout, vout, \
+                       nPtr, shift, base, hist, binTotals, tileStart, numTiles, allTiles)
+#define GSM_WIDE_PASS(B)                                                                                         \
+    hipLaunchKernelGGL(k_wide_upsweep<B>, dim3(grid), dim3(kRadixBlock), 0, s, kin, nPtr, shift, base, hist);    \
+    hipLaunchKernelGGL(k_wide_scan<B>, dim3((1u << B) / kWideScanDigits), dim3(256), 0, s, hist, grid, binTotals); \
+    if (ballot) {                                                                                                \
+        if (starts) GSM_WIDE_DOWN(B, true, true);                                                                \
+        else GSM_WIDE_DOWN(B, true, false);                                                                      \
+    } else {                                                                                                     \
+        if (starts) GSM_WIDE_DOWN(B, false, true);                                                               \
+        else GSM_WIDE_DOWN(B, false, false);                                                                     \
+    }
+    switch (bits) {
+        case 9: GSM_WIDE_PASS(9); break;
+        case 10: GSM_WIDE_PASS(10); break;
+        default: GSM_WIDE_PASS(11); break;
+    }
+#undef GSM_WIDE_PASS
+#undef GSM_WIDE_DOWN
+}
+
 size_t radix_workspace_bytes(uint32_t capacity) {
-    (void)capacity;  // per-block digit counts: <= 1024 blocks x 256 digits
-    return (size_t)256 * 1024 * sizeof(uint32_t);
+    // per-block digit counts: <= 1024 blocks x 256 digits (narrow), x 2048 digits (wide)
+    const size_t wide = (size_t)(kWideBins + kWideRowPad) * radix_grid_for_capacity(capacity) * sizeof(uint32_t);
+    return wide > (size_t)256 * 1024 * 4 ? wide : (size_t)256 * 1024 * sizeof(uint32_t);
 }
 
 uint32_t radix_grid_for_capacity(uint32_t capacity) {
@@ -426,34 +715,57 @@ int radix_sort_pairs(uint32_t* keys[2], uint32_t* vals[2], const uint32_t* nPtr,
 
 int radix_sort_bits(uint32_t* keys[2], uint32_t* vals[2], const uint32_t* nPtr, uint32_t capacity,
                     uint32_t shift, uint32_t bits, uint32_t* hist, uint32_t* binTotals, hipStream_t s,
-                    bool ballot) {
+                    bool ballot, bool wide) {
     const uint32_t grid = radix_grid_for_capacity(capacity);
-    const uint32_t passes = (bits + 7) / 8;
+    const uint32_t narrowPasses = (bits + 7) / 8;
+    const uint32_t widePasses = (bits + kWideMaxBits - 1) / kWideMaxBits;
+    // wide digits where they save a whole pass (32-bit keys: 3 passes of 11/11/10 bits instead of 4)
+    const bool useWide = wide && widePasses < narrowPasses;
+    const uint32_t passes = useWide ? widePasses : narrowPasses;
     int cur = 0;
     uint32_t done = 0;
     for (uint32_t p = 0; p < passes; ++p) {
         // near-equal digit widths; a digit wider than the bits left reads zero bits above the field
         uint32_t b = (bits - done + (passes - p) - 1) / (passes - p);
-        if (b < 4) b = 4;
-        radix_pass(keys[cur], vals[cur], keys[cur ^ 1], vals[cur ^ 1], nPtr, grid, shift + done, (int)b, hist,
-                   binTotals, s, ballot);
+        if (useWide) {
+            if (b < 9) b = 9;
+            wide_pass(keys[cur], vals[cur], keys[cur ^ 1], vals[cur ^ 1], nPtr, grid, shift + done, 0u, (int)b, hist,
+                      binTotals, s, ballot, false, nullptr, 0u, 0u);
+        } else {
+            if (b < 4) b = 4;
+            radix_pass(keys[cur], vals[cur], keys[cur ^ 1], vals[cur ^ 1], nPtr, grid, shift + done, (int)b, hist,
+                       binTotals, s, ballot);
+        }
         done += b;
         cur ^= 1;
     }
     return cur;
 }
 
-// The frame sort's tile passes (radix_sort_bits over the tile field, bits <= 16: one or two
-// passes) with the tile starts written by the last pass (TileStarts above).  binTotals holds
-// kSortTotalsWords words: the last pass's digit totals, the first pass's at +256, its bucket
-// starts at +512.
+// The frame sort's tile passes with the tile starts written by the last pass (TileStarts above).
+// The keys' tile field holds tiles [tileBase, tileBase + numTiles) of allTiles.  With <= 2048 tiles
+// in that range (a multi-GPU slab) and wide digits on, one wide pass sorts it, digits counted
+// from tileBase; otherwise radix_sort_bits' narrow passes over the whole tile field (bits <= 16:
+// one or two passes).  binTotals holds kSortTotalsWords words: the last pass's digit totals, the
+// first pass's at +256, its bucket starts at +512 (narrow); the wide pass's 2048 totals.
 int radix_sort_tiles(uint32_t* keys[2], uint32_t* vals[2], const uint32_t* nPtr, uint32_t capacity, uint32_t shift,
-                     uint32_t bits, uint32_t* hist, uint32_t* binTotals, uint32_t* tileStart, uint32_t numTiles,
-                     hipStream_t s, bool ballot, int loBits) {
+                     uint32_t* hist, uint32_t* binTotals, uint32_t* tileStart, uint32_t tileBase, uint32_t numTiles,
+                     uint32_t allTiles, hipStream_t s, bool ballot, int loBits, bool wide) {
     const uint32_t grid = radix_grid_for_capacity(capacity);
-    if (bits > 16) bits = 16;
+    auto bitsFor = [](uint32_t tiles) {
+        uint32_t b = 1;
+        while (b < 16 && ((tiles - 1u) >> b)) b++;
+        return b;
+    };
+    uint32_t bits = bitsFor(allTiles);
+    const uint32_t localBits = bitsFor(numTiles);
+    if (wide && bits > 8 && localBits <= kWideMaxBits) {
+        wide_pass(keys[0], vals[0], keys[1], vals[1], nPtr, grid, shift, tileBase, (int)(localBits < 9 ? 9 : localBits),
+                  hist, binTotals, s, ballot, true, tileStart, numTiles, allTiles);
+        return 1;
+    }
     TileStarts ts{};
-    ts.numTiles = numTiles;
+    ts.numTiles = allTiles;
     ts.tileStart = tileStart;
     if (bits <= 8) {  // one pass, one bucket
         radix_pass(keys[0], vals[0], keys[1], vals[1], nPtr, grid, shift, (int)(bits < 4 ? 4 : bits), hist,
@@ -861,6 +1173,8 @@ Tuning tuning_from_env(int device) {
     t.tileLoBits = lb ? atoi(lb) : 0;
     const char* cv = getenv("GSM_BLEND_CLAIM");
     t.blendClaim = !cv ? 1 : std::strcmp(cv, "early") == 0 ? 0 : std::strcmp(cv, "auto") == 0 ? 2 : 1;
+    const char* ws = getenv("GSM_SORT_WIDE");
+    t.wideSort = !(ws && ws[0] == '0');
     return t;
 }
 

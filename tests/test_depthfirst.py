@@ -227,6 +227,24 @@ def test_df_bit_exact(gsm, cuda, oracle, name):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("env", [{"GSM_SORT_WIDE": "0"}, {"GSM_SORT_RANK": "ballot"},
+                                 {"GSM_SORT_WIDE": "0", "GSM_SORT_RANK": "ballot"}])
+def test_df_sort_switches(gsm, cuda, oracle, monkeypatch, env):
+    """The create-time sort switches (gsm_internal.h Tuning): narrow 4 x 8-bit depth passes and two
+    tile passes instead of the wide ones (3 x 11/11/10 bits; one pass for this frame's 575 tiles),
+    ballot ranks -- every intermediate stays bit-exact."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    n, w, h, sh, prec, cs, seed, kw = DF_CASES["sh2_f16_config5_shape"]
+    world, harm = _scene(n, w, h, sh, prec, seed, **kw)
+    L, R = _cams(w, h)
+    r = oracle.df_render_stereo(world, harm, sh, L, R, w, h, color_space=cs)
+    g = gpu_df(gsm, cuda, world, harm, sh, L, R, w, h, color_space=cs)
+    assert_df_equal(g, r)
+    g["renderer"].close()
+
+
+@pytest.mark.gpu
 def test_df_scene_transform(gsm, cuda, oracle):
     n, w, h = 15000, 240, 200
     world, harm = _scene(n, w, h, 9, 1, 12)

@@ -404,10 +404,12 @@ def test_stereo_is_unsupported_like_the_reference(gsm, cuda):
 
 @pytest.mark.parametrize("env", [{"GSM_SORT_RANK": "ballot"}, {"GSM_BLEND_SCHED": "0"},
                                  {"GSM_SORT": "radix4"}, {"GSM_BLEND_CLAIM": "early"},
-                                 {"GSM_BLEND_CLAIM": "auto"}])
+                                 {"GSM_BLEND_CLAIM": "auto"}, {"GSM_SORT_WIDE": "0"},
+                                 {"GSM_SORT_WIDE": "0", "GSM_SORT_RANK": "ballot"}])
 def test_create_time_switches_frames_match(gsm, cuda, oracle, monkeypatch, env):
     """The A/B switches read once at create (Tuning, gsm_internal.h) -- ballot sort ranks, index-order
-    blend schedule, the 4 x 8-bit full-key sort, the blend queue's claim point -- render the same
+    blend schedule, the 4 x 8-bit full-key sort, the blend queue's claim point, narrow tile passes
+    instead of the one wide pass of this frame's 1800 tiles -- render the same
     frames bit for bit, first and later frames (later ones take last frame's cost order when the
     schedule is on)."""
     for k, v in env.items():

@@ -367,10 +367,9 @@ __global__ __launch_bounds__(kRadixBlock) void k_radix_downsweep(
 }
 
 // ---------------------------------------------------------------------------
-// Wide digits (9..11 bits, up to 2048 bins): one pass where the narrow kernels need two.  Used
-// where the bits to sort drop by a whole pass: the DepthFirst depth sort's 32-bit keys (3 passes
-// of 11/11/10 bits instead of 4 of 8) and the tile field of a frame with <= 2048 tiles in its rows
-// (a multi-GPU slab, keys counted relative to the slab's first tile: one pass instead of two).
+// Wide digits (9..11 bits, up to 2048 bins): one pass where the narrow kernels need two -- the tile
+// field of a frame with <= 2048 tiles in its rows (a multi-GPU slab, keys counted relative to the
+// slab's first tile).
 // Same chunks, block ranges and stable ranks as the narrow downsweep; what changes is the
 // per-chunk digit bookkeeping: thread t owns the 2^BITS / 256 contiguous digits [t * DPT, +DPT)
 // (registers for their running global bases), and the per-wave counters are padded one word in
@@ -715,27 +714,19 @@ int radix_sort_pairs(uint32_t* keys[2], uint32_t* vals[2], const uint32_t* nPtr,
 
 int radix_sort_bits(uint32_t* keys[2], uint32_t* vals[2], const uint32_t* nPtr, uint32_t capacity,
                     uint32_t shift, uint32_t bits, uint32_t* hist, uint32_t* binTotals, hipStream_t s,
-                    bool ballot, bool wide) {
+                    bool ballot) {
+    // (3 wide passes of 11/11/10 bits for the DepthFirst depth sort's 32-bit keys were measured
+    // slower than these 4 narrow ones: 89 against 85 us of kernels at config 5)
     const uint32_t grid = radix_grid_for_capacity(capacity);
-    const uint32_t narrowPasses = (bits + 7) / 8;
-    const uint32_t widePasses = (bits + kWideMaxBits - 1) / kWideMaxBits;
-    // wide digits where they save a whole pass (32-bit keys: 3 passes of 11/11/10 bits instead of 4)
-    const bool useWide = wide && widePasses < narrowPasses;
-    const uint32_t passes = useWide ? widePasses : narrowPasses;
+    const uint32_t passes = (bits + 7) / 8;
     int cur = 0;
     uint32_t done = 0;
     for (uint32_t p = 0; p < passes; ++p) {
         // near-equal digit widths; a digit wider than the bits left reads zero bits above the field
         uint32_t b = (bits - done + (passes - p) - 1) / (passes - p);
-        if (useWide) {
-            if (b < 9) b = 9;
-            wide_pass(keys[cur], vals[cur], keys[cur ^ 1], vals[cur ^ 1], nPtr, grid, shift + done, 0u, (int)b, hist,
-                      binTotals, s, ballot, false, nullptr, 0u, 0u);
-        } else {
-            if (b < 4) b = 4;
-            radix_pass(keys[cur], vals[cur], keys[cur ^ 1], vals[cur ^ 1], nPtr, grid, shift + done, (int)b, hist,
-                       binTotals, s, ballot);
-        }
+        if (b < 4) b = 4;
+        radix_pass(keys[cur], vals[cur], keys[cur ^ 1], vals[cur ^ 1], nPtr, grid, shift + done, (int)b, hist,
+                   binTotals, s, ballot);
         done += b;
         cur ^= 1;
     }

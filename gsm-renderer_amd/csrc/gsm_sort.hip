@@ -23,6 +23,9 @@
 namespace gsm {
 
 constexpr int kWaves = kRadixBlock / 64;
+#ifndef GSM_UPSWEEP_COPIES
+#define GSM_UPSWEEP_COPIES 4
+#endif
 
 __device__ __forceinline__ void block_range(uint32_t n, uint32_t grid, uint32_t b, uint32_t* begin,
                                             uint32_t* end) {
@@ -76,9 +79,14 @@ __global__ __launch_bounds__(kRadixBlock) void k_radix_upsweep(const uint32_t* _
                                                                uint32_t shift,
                                                                uint32_t* __restrict__ hist) {
     constexpr uint32_t R = 1u << BITS;
-    __shared__ uint32_t cnt[kWaves][R];
+    // GSM_UPSWEEP_COPIES counter copies per wave (lane & (copies - 1) picks one), rows padded by a
+    // word so one digit's copies sit in different LDS banks: fewer same-address collisions among
+    // the 64 lanes of one ds_add
+    constexpr uint32_t CP = GSM_UPSWEEP_COPIES, RS = R + (CP > 1 ? 1u : 0u);
+    __shared__ uint32_t cnt[kWaves * CP][RS];
     const uint32_t wave = threadIdx.x >> 6;
-    for (int i = threadIdx.x; i < kWaves * (int)R; i += kRadixBlock) (&cnt[0][0])[i] = 0;
+    const uint32_t row = wave * CP + (threadIdx.x & (CP - 1u));
+    for (int i = threadIdx.x; i < (int)(kWaves * CP * RS); i += kRadixBlock) (&cnt[0][0])[i] = 0;
     __syncthreads();
     uint32_t begin, end;
     block_range(*nPtr, gridDim.x, blockIdx.x, &begin, &end);
@@ -106,7 +114,7 @@ __global__ __launch_bounds__(kRadixBlock) void k_radix_upsweep(const uint32_t* _
             const uint32_t kk[4] = {q[i].x, q[i].y, q[i].z, q[i].w};
 #pragma unroll
             for (int c = 0; c < 4; ++c)  // per-wave LDS counters: one ds_add per key
-                if (idx + (uint32_t)c < end) atomicAdd(&cnt[wave][(kk[c] >> shift) & (R - 1u)], 1u);
+                if (idx + (uint32_t)c < end) atomicAdd(&cnt[row][(kk[c] >> shift) & (R - 1u)], 1u);
         }
         if (more) {
 #pragma unroll
@@ -117,7 +125,7 @@ __global__ __launch_bounds__(kRadixBlock) void k_radix_upsweep(const uint32_t* _
     for (uint32_t d = threadIdx.x; d < R; d += kRadixBlock) {
         uint32_t s = 0;
 #pragma unroll
-        for (int w = 0; w < kWaves; ++w) s += cnt[w][d];
+        for (uint32_t w = 0; w < kWaves * CP; ++w) s += cnt[w][d];
         hist[(size_t)d * gridDim.x + blockIdx.x] = s;
     }
 }

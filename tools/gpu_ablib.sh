@@ -36,6 +36,11 @@ PY
       --traffic-json /dev/null > $OUT/bench_${v}_$cfg.log 2>&1 || { echo "bench failed: $v $cfg"; tail -n 5 $OUT/bench_${v}_$cfg.log; use A; exit 1; }
     grep '"metric"' $OUT/bench_${v}_$cfg.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('  bench', '$v', round(d['value'],1), 'parity', d.get('parity_vs_oracle'), 'inflight2', (d.get('inflight2') or {}).get('value'), (d.get('inflight2') or {}).get('parity_both_targets'), {k: round(x*1e3,1) for k,x in d['stages_ms'].items()})"
   done
+  if [ "${VR:-0}" = 1 ]; then  # virtual-rank multi-GPU frame (config 4: 5M / 4K / 8 ranks)
+    timeout -k 10 300 python tools/exp_virtual_ranks.py --config cfg3_5m_sh3_4k_f16 --world 8 --frames 5 \
+      > $OUT/vr_$v.log 2>&1 || { echo "vr failed: $v"; tail -n 5 $OUT/vr_$v.log; use A; exit 1; }
+    grep '^{' $OUT/vr_$v.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('  vr', '$v', d['device_frame_ms'], d['max_phase_ms'], {k: round(max(s[k] for s in d['slab_stages_ms'])*1e3,1) for k in d['slab_stages_ms'][0]})"
+  fi
 done
 use A
 echo "=== done"

@@ -256,9 +256,10 @@ gsm_status DepthFirstRenderer::renderStereoSbs(hipStream_t s, const gsm_gaussian
     launch_scan_sums(A_.blockSums, nb, maxGaussians_, A_.visHdr, A_.queue, s);
     df_launch_compact(a, A_, s);
     if (prof) hipEventRecord(ev[1], s);
-    // DepthRadixSortEncoder, 32-bit keys (DepthFirstRenderer.swift:664-681): stable LSD, 4 x 8 bits
+    // DepthRadixSortEncoder, 32-bit keys (DepthFirstRenderer.swift:664-681): stable LSD
+    // (3 wide passes of 11/11/10 bits unless GSM_SORT_WIDE=0: the same stable order)
     const int dc = radix_sort_bits(A_.dkeys, A_.dvals, &A_.visHdr->totalAssignments, maxGaussians_, 0, 32,
-                                   A_.radixHist, A_.radixBinTotals, s, tuning_.ballotRank);
+                                   A_.radixHist, A_.radixBinTotals, s, tuning_.ballotRank, tuning_.wideSort);
     if (prof) hipEventRecord(ev[2], s);
     df_launch_instance_counts(A_.dvals[dc], a, A_, s);
     launch_scan_sums(A_.instSums, nb, maxInstances_, A_.instHdr, A_.queue, s);

@@ -91,7 +91,7 @@ struct Tuning {
     int blendWaves = 0;       // GSM_BLEND_WAVES=8|12|16: waves per blend workgroup (0: by frame size)
     int tileLoBits = 0;       // GSM_SORT_LOBITS=4..8: width of the first tile pass (0: half the tile field)
     int blendClaim = 1;       // GSM_BLEND_CLAIM=early|late|auto (0/1/2): when a blend wave claims its next unit
-    bool wideSort = true;     // GSM_SORT_WIDE=0: two narrow tile passes instead of one wide (9..11-bit) pass
+    bool wideSort = true;     // GSM_SORT_WIDE=0: narrow passes only (no wide 9..11-bit tile or depth passes)
 };
 // the environment's settings plus the device probe; `device` is a HIP device id
 Tuning tuning_from_env(int device);
@@ -176,10 +176,11 @@ int radix_sort_pairs(uint32_t* keys[2], uint32_t* vals[2], const uint32_t* nPtr,
                      int firstDigit, int numDigits, uint32_t* hist, uint32_t* binTotals,
                      hipStream_t stream, bool ballot);
 // Stable LSD radix sort by bits [shift, shift + bits) only, in ceil(bits / 8) passes of
-// near-equal digit widths (4..8 bits).  Returns the ping-pong index of the result.
+// near-equal digit widths (4..8 bits), or -- `wide` and where that saves a pass -- ceil(bits / 11)
+// passes of 9..11 bits.  binTotals: kSortTotalsWords words.  Returns the ping-pong index of the result.
 int radix_sort_bits(uint32_t* keys[2], uint32_t* vals[2], const uint32_t* nPtr, uint32_t capacity,
                     uint32_t shift, uint32_t bits, uint32_t* hist, uint32_t* binTotals, hipStream_t stream,
-                    bool ballot);
+                    bool ballot, bool wide = false);
 // the frame sort's tile field (tiles [tileBase, tileBase + numTiles) of allTiles, bits <= 16) with
 // the tile starts written by its last pass (tileStart[0..allTiles], lower bounds for empty tiles);
 // one wide pass relative to tileBase when numTiles <= 2048 and `wide`; binTotals: kSortTotalsWords words

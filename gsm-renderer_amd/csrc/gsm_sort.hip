@@ -377,7 +377,7 @@ __global__ __launch_bounds__(kRadixBlock) void k_radix_downsweep(
 // ---------------------------------------------------------------------------
 // Wide digits (9..11 bits, up to 2048 bins): one pass where the narrow kernels need two -- the tile
 // field of a frame with <= 2048 tiles in its rows (a multi-GPU slab, keys counted relative to the
-// slab's first tile).
+// slab's first tile), and the DepthFirst depth sort's 32-bit keys (3 passes of 11/11/10 bits).
 // Same chunks, block ranges and stable ranks as the narrow downsweep; what changes is the
 // per-chunk digit bookkeeping: thread t owns the 2^BITS / 256 contiguous digits [t * DPT, +DPT)
 // (registers for their running global bases), and the per-wave counters are padded one word in
@@ -396,10 +396,11 @@ __global__ __launch_bounds__(kRadixBlock) void k_wide_upsweep(const uint32_t* __
     constexpr uint32_t R = 1u << BITS;
     // one counter array: a histogram needs no order, and 2^BITS bins spread the atomics
     __shared__ uint32_t cnt[R];
-    for (uint32_t i = threadIdx.x; i < R; i += kRadixBlock) cnt[i] = 0;
-    __syncthreads();
     uint32_t begin, end;
     block_range(*nPtr, gridDim.x, blockIdx.x, &begin, &end);
+    if (begin >= end) return;  // no row: k_wide_scan reads the active blocks' rows only
+    for (uint32_t i = threadIdx.x; i < R; i += kRadixBlock) cnt[i] = 0;
+    __syncthreads();
     auto load_chunk = [&](uint32_t cbase, uint4 (&q)[kRadixItems / 4]) {
 #pragma unroll
         for (int i = 0; i < kRadixItems / 4; ++i) {
@@ -433,29 +434,37 @@ __global__ __launch_bounds__(kRadixBlock) void k_wide_upsweep(const uint32_t* __
     for (uint32_t d = threadIdx.x; d < R; d += kRadixBlock) hist[(size_t)blockIdx.x * (R + kWideRowPad) + d] = cnt[d];
 }
 
-// Exclusive scan over blocks of the block-major wide counts, in place, digit totals out.  Workgroup g
-// owns digits [16g, 16g + 16); thread t scans digit 16g + (t & 15) over the (t >> 4)-th sixteenth of
-// the blocks (16 loads in flight), the 16 segment sums meet in LDS, then each thread writes its
-// running prefix back (the re-read hits L2).  16 digits per workgroup: 128 workgroups at 11 bits.
-constexpr uint32_t kWideScanDigits = 16;
+// Exclusive scan over blocks of the block-major wide counts, in place, digit totals out -- over the
+// blocks that hold keys (block_range: the grid is sized for the capacity, a frame fills a part of
+// it).  Workgroup g owns digits [16g, 16g + 16); thread t scans digit 16g + (t & 15) over the
+// (t >> 4)-th sixteenth of those blocks: up to 32 rows loaded at once and kept in registers (one
+// memory round trip; more rows loop and re-read), the 16 segment sums meet in LDS.
+constexpr uint32_t kWideScanDigits = 16, kWideScanRegs = 32;
 template <int BITS>
 __global__ __launch_bounds__(256) void k_wide_scan(uint32_t* __restrict__ hist, uint32_t grid,
-                                                   uint32_t* __restrict__ binTotals) {
-    constexpr uint32_t R = 1u << BITS;
+                                                   const uint32_t* __restrict__ nPtr, uint32_t* __restrict__ binTotals) {
+    constexpr uint32_t R = 1u << BITS, RS = R + kWideRowPad;
     constexpr uint32_t S = 256 / kWideScanDigits;  // segments
     __shared__ uint32_t ss[S][kWideScanDigits];
+    // active blocks, as block_range splits n: block b holds keys iff b * per < n
+    const uint32_t n = *nPtr;
+    uint32_t per = (n + grid - 1) / grid;
+    per = (per + kRadixChunk - 1) / kRadixChunk * kRadixChunk;
+    const uint32_t active = per ? min(grid, (n + per - 1) / per) : 0u;
     const uint32_t j = threadIdx.x % kWideScanDigits, sg = threadIdx.x / kWideScanDigits;
     const uint32_t d = blockIdx.x * kWideScanDigits + j;
-    const uint32_t q = (grid + S - 1) / S;
-    const uint32_t b0 = min(sg * q, grid), b1 = min(b0 + q, grid);
+    const uint32_t q = (active + S - 1) / S;
+    const uint32_t b0 = min(sg * q, active), b1 = min(b0 + q, active);
     uint32_t* col = hist + d;
+    uint32_t v[kWideScanRegs];
     uint32_t sum = 0;
-    for (uint32_t b = b0; b < b1; b += 16u) {
-        uint32_t v[16];
+    if (q <= kWideScanRegs) {
 #pragma unroll
-        for (uint32_t i = 0; i < 16; ++i) v[i] = b + i < b1 ? col[(size_t)(b + i) * (R + kWideRowPad)] : 0u;
+        for (uint32_t i = 0; i < kWideScanRegs; ++i) v[i] = b0 + i < b1 ? col[(size_t)(b0 + i) * RS] : 0u;
 #pragma unroll
-        for (uint32_t i = 0; i < 16; ++i) sum += v[i];
+        for (uint32_t i = 0; i < kWideScanRegs; ++i) sum += v[i];
+    } else {
+        for (uint32_t b = b0; b < b1; ++b) sum += col[(size_t)b * RS];
     }
     ss[sg][j] = sum;
     __syncthreads();
@@ -467,16 +476,19 @@ __global__ __launch_bounds__(256) void k_wide_scan(uint32_t* __restrict__ hist, 
         tot += x;
     }
     if (sg == 0) binTotals[d] = tot;
-    for (uint32_t b = b0; b < b1; b += 16u) {
-        uint32_t v[16];
+    if (q <= kWideScanRegs) {
 #pragma unroll
-        for (uint32_t i = 0; i < 16; ++i) v[i] = b + i < b1 ? col[(size_t)(b + i) * (R + kWideRowPad)] : 0u;
-#pragma unroll
-        for (uint32_t i = 0; i < 16; ++i)
-            if (b + i < b1) {
-                col[(size_t)(b + i) * (R + kWideRowPad)] = run;
+        for (uint32_t i = 0; i < kWideScanRegs; ++i)
+            if (b0 + i < b1) {
+                col[(size_t)(b0 + i) * RS] = run;
                 run += v[i];
             }
+    } else {
+        for (uint32_t b = b0; b < b1; ++b) {
+            const uint32_t x = col[(size_t)b * RS];
+            col[(size_t)b * RS] = run;
+            run += x;
+        }
     }
 }
 
@@ -644,7 +656,7 @@ static void wide_pass(uint32_t* kin, uint32_t* vin, uint32_t* kout, uint32_t* vo
                        nPtr, shift, base, hist, binTotals, tileStart, numTiles, allTiles)
 #define GSM_WIDE_PASS(B)                                                                                         \
     hipLaunchKernelGGL(k_wide_upsweep<B>, dim3(grid), dim3(kRadixBlock), 0, s, kin, nPtr, shift, base, hist);    \
-    hipLaunchKernelGGL(k_wide_scan<B>, dim3((1u << B) / kWideScanDigits), dim3(256), 0, s, hist, grid, binTotals); \
+    hipLaunchKernelGGL(k_wide_scan<B>, dim3((1u << B) / kWideScanDigits), dim3(256), 0, s, hist, grid, nPtr, binTotals); \
     if (ballot) {                                                                                                \
         if (starts) GSM_WIDE_DOWN(B, true, true);                                                                \
         else GSM_WIDE_DOWN(B, true, false);                                                                      \
@@ -722,19 +734,27 @@ int radix_sort_pairs(uint32_t* keys[2], uint32_t* vals[2], const uint32_t* nPtr,
 
 int radix_sort_bits(uint32_t* keys[2], uint32_t* vals[2], const uint32_t* nPtr, uint32_t capacity,
                     uint32_t shift, uint32_t bits, uint32_t* hist, uint32_t* binTotals, hipStream_t s,
-                    bool ballot) {
-    // (3 wide passes of 11/11/10 bits for the DepthFirst depth sort's 32-bit keys were measured
-    // slower than these 4 narrow ones: 89 against 85 us of kernels at config 5)
+                    bool ballot, bool wide) {
     const uint32_t grid = radix_grid_for_capacity(capacity);
-    const uint32_t passes = (bits + 7) / 8;
+    const uint32_t narrowPasses = (bits + 7) / 8;
+    const uint32_t widePasses = (bits + kWideMaxBits - 1) / kWideMaxBits;
+    // wide digits where they save a whole pass (32-bit keys: 3 passes of 11/11/10 bits instead of 4)
+    const bool useWide = wide && widePasses < narrowPasses;
+    const uint32_t passes = useWide ? widePasses : narrowPasses;
     int cur = 0;
     uint32_t done = 0;
     for (uint32_t p = 0; p < passes; ++p) {
         // near-equal digit widths; a digit wider than the bits left reads zero bits above the field
         uint32_t b = (bits - done + (passes - p) - 1) / (passes - p);
-        if (b < 4) b = 4;
-        radix_pass(keys[cur], vals[cur], keys[cur ^ 1], vals[cur ^ 1], nPtr, grid, shift + done, (int)b, hist,
-                   binTotals, s, ballot);
+        if (useWide) {
+            if (b < 9) b = 9;
+            wide_pass(keys[cur], vals[cur], keys[cur ^ 1], vals[cur ^ 1], nPtr, grid, shift + done, 0u, (int)b, hist,
+                      binTotals, s, ballot, false, nullptr, 0u, 0u);
+        } else {
+            if (b < 4) b = 4;
+            radix_pass(keys[cur], vals[cur], keys[cur ^ 1], vals[cur ^ 1], nPtr, grid, shift + done, (int)b, hist,
+                       binTotals, s, ballot);
+        }
         done += b;
         cur ^= 1;
     }

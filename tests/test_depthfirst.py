@@ -230,8 +230,9 @@ def test_df_bit_exact(gsm, cuda, oracle, name):
 @pytest.mark.parametrize("env", [{"GSM_SORT_WIDE": "0"}, {"GSM_SORT_RANK": "ballot"},
                                  {"GSM_SORT_WIDE": "0", "GSM_SORT_RANK": "ballot"}])
 def test_df_sort_switches(gsm, cuda, oracle, monkeypatch, env):
-    """The create-time sort switches (gsm_internal.h Tuning): two narrow tile passes instead of the
-    one wide pass of this frame's 575 tiles, ballot ranks -- every intermediate stays bit-exact."""
+    """The create-time sort switches (gsm_internal.h Tuning): narrow 4 x 8-bit depth passes and two
+    tile passes instead of the wide ones (3 x 11/11/10 bits; one pass for this frame's 575 tiles),
+    ballot ranks -- every intermediate stays bit-exact."""
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     n, w, h, sh, prec, cs, seed, kw = DF_CASES["sh2_f16_config5_shape"]

@@ -81,7 +81,7 @@ __global__ __launch_bounds__(NT) void k_blend_px(
     const uint32_t* __restrict__ order, uint16_t* __restrict__ unitCost,
     unsigned long long* __restrict__ trace, const uint32_t* __restrict__ half0,
     const uint32_t* __restrict__ half1, const uint32_t* __restrict__ halfCount, uint32_t tileCount,
-    uint32_t* __restrict__ costMax) {
+    uint32_t* __restrict__ costMax, uint32_t rowBegin, uint32_t rowStride) {
     static_assert(P == 1 || P == 2, "pairs per lane: quadrant or half-tile units (half-tile lists)");
     static_assert(!COMPACT || P == 2, "compaction: half tiles");
     constexpr uint32_t U = 4 / P;  // entries per pipeline group
@@ -220,7 +220,7 @@ __global__ __launch_bounds__(NT) void k_blend_px(
         uint32_t u = order ? __builtin_amdgcn_readfirstlane(order[qi]) : qi;
         if (u >= numUnits) u = qi;  // a schedule is a permutation of [0, numUnits); never trust it further
         const uint32_t tile = tileBegin + u / UPT, part = u % UPT;
-        const uint32_t tileX = tile % tilesX, tileY = tile / tilesX;
+        const uint32_t tileX = tile % tilesX, tileY = rowBegin + (tile / tilesX) * rowStride;
         const uint32_t ux = tileX * kTileWidth + (part & 1u) * 16u;
         const uint32_t uy = tileY * kTileHeight + (P == 1 ? (part >> 1) * 8u : 0u);
         // the unit walks its half's list: the tile's sorted entries without those whose skip flag for
@@ -619,9 +619,10 @@ static int blend_waves_per_wg(uint32_t numTiles, int numCUs) {
 void launch_blend(const FrameGeometry& g, const DeviceArena& A, void* color,
                   size_t colorPitch, void* depth, size_t depthPitch, int numCUs, bool costOrder, int colorFormat,
                   hipStream_t s, int wavesOverride, int claim) {
-    const uint32_t t0 = g.rowBegin * g.tilesX, t1 = g.rowEnd * g.tilesX;
-    if (t1 <= t0) return;
-    const uint32_t numTiles = t1 - t0;
+    // local tile ids: tile t = k * tilesX + tx of the renderer's row k (pixel row rowBegin + k * rowStride)
+    const uint32_t numTiles = g.rowCount * g.tilesX;
+    if (numTiles == 0) return;
+    const uint32_t t0 = 0;
     const int vec = ((((uintptr_t)color) & 15u) == 0 && (colorPitch & 15u) == 0 &&
                      (depth == nullptr || ((((uintptr_t)depth) & 7u) == 0 && (depthPitch & 7u) == 0)))
                         ? 1
@@ -638,7 +639,8 @@ void launch_blend(const FrameGeometry& g, const DeviceArena& A, void* color,
     hipLaunchKernelGGL((k_blend_px<NTH, PP, CMP>), dim3(grid), dim3(NTH), 0, s, A.tileStart, A.rec, \
                        A.expTable, A.tileQueue, t0, numTiles, g.tilesX, g.width, g.height,          \
                        (uint8_t*)color, colorPitch, (uint8_t*)depth, depthPitch, flags, order, A.unitCost,  \
-                       A.blendTrace, A.halfVals[0], A.halfVals[1], A.halfCount, g.tileCount, A.costMax)
+                       A.blendTrace, A.halfVals[0], A.halfVals[1], A.halfCount, g.tileCount, A.costMax, \
+                       g.rowBegin, g.rowStride)
     // half tiles compact to one pair per lane once <= 16 of their 32 groups are alive
     if (P == 1) {
         if (waves == 16) GSM_LAUNCH_BLEND(1024, 1, false);

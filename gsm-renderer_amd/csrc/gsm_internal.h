@@ -12,7 +12,11 @@ namespace gsm {
 struct ProjectArgs {
     CameraUniforms cam;
     TileBinningParams bin;
-    uint32_t rowBegin, rowEnd;  // slab of tile rows; full frame = [0, tilesY)
+    // the renderer's tile rows: rowBegin, rowBegin + rowStride, ... < rowEnd -- a
+    // contiguous slab (stride 1; full frame [0, tilesY)) or a multi-GPU rank's interleaved rows
+    // (stride = world).  Tile ids of keys, tile starts and blend units count the set's rows only:
+    // local tile = k * tilesX + tx for row rowBegin + k * rowStride.
+    uint32_t rowBegin, rowEnd, rowStride;
     uint32_t count;
     uint32_t maxAssignments;
     uint32_t keepRenderData;  // write GaussianRenderData of every visible gaussian (debug readback);
@@ -29,8 +33,9 @@ struct ProjectArgs {
 // record a slab owner receives per gaussian (GaussianRenderData + blend record + tile rect).
 constexpr uint32_t kMaxSlabs = 16;
 struct SlabTable {
-    uint32_t rows[kMaxSlabs + 1];
+    uint32_t rows[kMaxSlabs + 1];  // contiguous: slab s = rows [rows[s], rows[s + 1])
     uint32_t n;
+    uint32_t interleave;  // 1: slab s = rows s, s + n, s + 2n, ... < rows[n] (rows[n] = tilesY)
 };
 struct SplatRecord {
     uint4 rd;         // GaussianRenderData

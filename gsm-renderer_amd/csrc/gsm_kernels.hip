@@ -192,19 +192,35 @@ __device__ __forceinline__ ProjOut project_gaussian(const void* __restrict__ wor
     return o;
 }
 
-// tiles of a projected gaussian's rect in rows [rowBegin, rowEnd) that its ellipse meets
+// The renderer's tile rows (ProjectArgs::rowBegin / rowEnd / rowStride): rows b, b + s, ... < e,
+// row index k = (ty - b) / s; a contiguous slab has s = 1, a multi-GPU rank's interleaved rows s = W.
+struct RowSet {
+    int b, e, s;
+};
+__device__ __forceinline__ RowSet rows_of(const ProjectArgs& P) {
+    return RowSet{(int)P.rowBegin, (int)P.rowEnd, P.rowStride > 1u ? (int)P.rowStride : 1};
+}
+// row indices [*k0, *k1] of the set inside tile rows [y0, y1] (empty when *k0 > *k1)
+__device__ __forceinline__ void rows_within(const RowSet& R, int y0, int y1, int* k0, int* k1) {
+    const int lo = max(y0, R.b), hi = min(y1, R.e - 1);
+    *k0 = (lo - R.b + R.s - 1) / R.s;
+    *k1 = hi < R.b ? -1 : (hi - R.b) / R.s;
+}
+
+// tiles of a projected gaussian's rect in the renderer's rows that its ellipse meets
 // (tileCountIndirectKernel, GlobalShaders.metal:563-616).  For rects of at most 32 tiles the
-// answers are also returned as a bit mask in scan order (bit (ty - ty0) * width + (tx - tx0)),
-// so the scatter reuses them instead of repeating the tests.
+// answers are also returned as a bit mask in scan order (bit (k - k0) * width + (tx - tx0) for
+// row index k), so the scatter reuses them instead of repeating the tests.
 constexpr int kMaskTiles = 32;
-__device__ __forceinline__ uint32_t count_tiles(const ProjOut& o, int rowBegin, int rowEnd, uint32_t* maskOut) {
+__device__ __forceinline__ uint32_t count_tiles(const ProjOut& o, const RowSet& R, uint32_t* maskOut) {
     uint32_t n = 0, mask = 0;
     *maskOut = 0;
     if (!o.countable) return 0;
-    const int ty0 = max((int)o.bounds.z, rowBegin), ty1 = min((int)o.bounds.w, rowEnd - 1);
+    int k0, k1;
+    rows_within(R, (int)o.bounds.z, (int)o.bounds.w, &k0, &k1);
     uint32_t bit = 0;
-    for (int ty = ty0; ty <= ty1; ++ty)
-        for (int tx = (int)o.bounds.x; tx <= (int)o.bounds.y; ++tx, ++bit)
+    for (int k = k0; k <= k1; ++k)
+        for (int tx = (int)o.bounds.x, ty = R.b + k * R.s; tx <= (int)o.bounds.y; ++tx, ++bit)
             if (intersects_tile(tx, ty, o.cmx, o.cmy, o.k, o.w)) {
                 n++;
                 if (bit < (uint32_t)kMaskTiles) mask |= 1u << bit;
@@ -214,8 +230,9 @@ __device__ __forceinline__ uint32_t count_tiles(const ProjOut& o, int rowBegin, 
 }
 
 // The blend's half-tile skip band of a projected gaussian (BandSkip of its fp16 blend record),
-// checked once against its tile rect within rows [rowBegin, rowEnd): (mean x, half width), or a
-// negative width when the band may not be used.  Stored in the blend record's padding for k_scatter.
+// checked once against its tile rect within the renderer's rows (from its first to its last row in
+// the rect: a superset for interleaved rows): (mean x, half width), or a negative width when the
+// band may not be used.  Stored in the blend record's padding for k_scatter.
 __device__ __forceinline__ bool band_rect_ok(const BandSkip& b, int x0, int x1, int y0, int y1) {
     if (!b.valid) return false;
     const int mxm = fp16_coord_margin(x1), mym = fp16_coord_margin(y1);
@@ -224,9 +241,11 @@ __device__ __forceinline__ bool band_rect_ok(const BandSkip& b, int x0, int x1, 
     const float ay = __builtin_fmaxf(__builtin_fabsf((float)(y0 - mym) - b.my), __builtin_fabsf((float)(y1 + mym) - b.my));
     return ax <= 200.0f && ay <= 200.0f && b.cxx * (ax * ax) + b.cyy * (ay * ay) <= 16000.0f;
 }
-__device__ __forceinline__ float2 band_of(const BlendRecordA& ra, short4 r, int rowBegin, int rowEnd) {
+__device__ __forceinline__ float2 band_of(const BlendRecordA& ra, short4 r, const RowSet& R) {
     const BandSkip b = band_skip_setup(ra.x, ra.y, ra.z, kBlendZeroP);
-    const int by0 = max((int)r.z, rowBegin), by1 = min((int)r.w, rowEnd - 1);
+    int k0, k1;
+    rows_within(R, (int)r.z, (int)r.w, &k0, &k1);
+    const int by0 = R.b + k0 * R.s, by1 = R.b + k1 * R.s;
     if (band_rect_ok(b, (int)r.x * (int)kTileWidth, (int)r.y * (int)kTileWidth + (int)kTileWidth - 1,
                      by0 * (int)kTileHeight, by1 * (int)kTileHeight + (int)kTileHeight - 1))
         return make_float2(b.mx, b.ex);
@@ -347,7 +366,7 @@ __global__ __launch_bounds__(kProjectBlock) void k_project(
         const uint32_t mask = sMask[tid];
         ntiles = (uint32_t)__builtin_popcount(mask) + sMore[tid];
         masks[gid] = mask;
-        const float2 band = ntiles ? band_of(o.ra, o.bounds, (int)P.rowBegin, (int)P.rowEnd) : make_float2(0.f, -1.f);
+        const float2 band = ntiles ? band_of(o.ra, o.bounds, rows_of(P)) : make_float2(0.f, -1.f);
         uint4* rp = (uint4*)(outRec + gid);
         rp[0] = make_uint4(o.ra.x, o.ra.y, o.ra.z, o.ra.w);
         rp[1] = make_uint4(o.rb, __float_as_uint(band.x), __float_as_uint(band.y), 0u);
@@ -430,16 +449,26 @@ __device__ __forceinline__ void block_tile_tests(TileTestLds& L, const ProjOut& 
     __syncthreads();
 }
 
-// the slab's part of a record's tile answers: rows [rb, re) of the rect, scan order (ty - max(ty0,
-// rb)) * rw + tx - tx0 -- k_scatter's mask order for the slab -- when the whole rect has <= 32 tiles
-// (full = the rect's answers, bit (ty - ty0) * rw + tx - tx0); 0 otherwise (the owner re-tests)
-__device__ __forceinline__ uint32_t slab_tile_mask(short4 b, uint32_t full, int rb, int re) {
+// the rows of slab sl (SlabTable: contiguous blocks or interleaved rows)
+__device__ __forceinline__ RowSet slab_rows(const SlabTable& t, const uint32_t* rows, uint32_t sl) {
+    return t.interleave ? RowSet{(int)sl, (int)rows[t.n], (int)t.n} : RowSet{(int)rows[sl], (int)rows[sl + 1], 1};
+}
+
+// the slab's part of a record's tile answers: the slab's rows of the rect, scan order (k - k0) * rw
+// + tx - tx0 over the slab's row indices k -- k_scatter's mask order for the slab -- when the whole
+// rect has <= 32 tiles (full = the rect's answers, bit (ty - ty0) * rw + tx - tx0); 0 otherwise (the
+// owner re-tests)
+__device__ __forceinline__ uint32_t slab_tile_mask(short4 b, uint32_t full, const RowSet& R) {
     const int rw = (int)b.y - (int)b.x + 1;
     if (((int)b.w - (int)b.z + 1) * rw > kMaskTiles) return 0u;
-    const int y0 = max((int)b.z, rb), y1 = min((int)b.w, re - 1);
-    if (y1 < y0) return 0u;
-    const uint32_t shift = (uint32_t)((y0 - (int)b.z) * rw), bits = (uint32_t)((y1 - y0 + 1) * rw);
-    return (full >> shift) & (bits >= 32u ? 0xFFFFFFFFu : ((1u << bits) - 1u));
+    int k0, k1;
+    rows_within(R, (int)b.z, (int)b.w, &k0, &k1);
+    if (k1 < k0) return 0u;
+    const uint32_t rowBits = rw >= 32 ? 0xFFFFFFFFu : ((1u << rw) - 1u);
+    uint32_t out = 0, at = 0;
+    for (int k = k0; k <= k1; ++k, at += (uint32_t)rw)  // (<= 32 rows: the rect has <= 32 tiles)
+        out |= ((full >> (uint32_t)((R.b + k * R.s - (int)b.z) * rw)) & rowBits) << at;
+    return out;
 }
 
 template <bool HALF, int DEG>
@@ -484,9 +513,14 @@ __global__ __launch_bounds__(kProjectBlock) void k_project_part(
     const uint32_t nSlabs = slabs.n;
     block_tile_tests(L, o, area, (int)o.bounds.z, [&](uint32_t lo, uint32_t k, int ty) {
         if (k < (uint32_t)kMaskTiles) atomicOr(&sTile[lo], 1u << k);
-        uint32_t sl = 0;  // the slab of row ty: slabs.rows is non-decreasing, at most 16 slabs
-        while (sl + 1u < nSlabs && (uint32_t)ty >= sRows[sl + 1u]) ++sl;
-        if ((uint32_t)ty >= sRows[sl] && (uint32_t)ty < sRows[sl + 1u]) atomicOr(&sSlab[lo], 1u << sl);
+        uint32_t sl = 0;  // the slab of row ty: row ty mod n (interleaved), or the block holding it
+        if (slabs.interleave) {
+            sl = (uint32_t)ty % nSlabs;
+            if ((uint32_t)ty < sRows[nSlabs]) atomicOr(&sSlab[lo], 1u << sl);
+        } else {  // slabs.rows is non-decreasing, at most 16 slabs
+            while (sl + 1u < nSlabs && (uint32_t)ty >= sRows[sl + 1u]) ++sl;
+            if ((uint32_t)ty >= sRows[sl] && (uint32_t)ty < sRows[sl + 1u]) atomicOr(&sSlab[lo], 1u << sl);
+        }
     });
     uint32_t mask = 0;
     if (gid < P.count) {
@@ -538,10 +572,10 @@ __global__ __launch_bounds__(1024) void k_part_scan(uint32_t* __restrict__ block
 // (slab-local rank order = ascending id): the 48-B records go through LDS so that consecutive
 // threads store consecutive 16-B words -- whole 64-B segments into uncached or peer memory instead
 // of three 16-B pieces per record 48 B apart.  dst(sl) = the run's first record, cap(sl) = records
-// the destination holds (nothing is written past it).  slabRows: the slab table (record masks).
+// the destination holds (nothing is written past it).  slabs: the slab table (record masks).
 template <class Dst, class Cap>
 __device__ __forceinline__ void write_slab_runs(const SplatRecord* __restrict__ records, uint32_t slabBits,
-                                                uint32_t gid, uint32_t numSlabs, const uint32_t* slabRows,
+                                                uint32_t gid, uint32_t numSlabs, const SlabTable& slabs,
                                                 Dst&& dst, Cap&& cap) {
     __shared__ uint32_t wcnt[kProjectBlock / 64][kMaxSlabs];
     __shared__ uint4 sOut[kProjectBlock * 3];
@@ -575,7 +609,7 @@ __device__ __forceinline__ void write_slab_runs(const SplatRecord* __restrict__ 
             uint4* o = sOut + 3u * (before + rnk[sl]);
             o[0] = a;
             o[1] = b;
-            o[2] = make_uint4(c.x, c.y, c.z, slab_tile_mask(bounds, c.w, (int)slabRows[sl], (int)slabRows[sl + 1]));
+            o[2] = make_uint4(c.x, c.y, c.z, slab_tile_mask(bounds, c.w, slab_rows(slabs, slabs.rows, sl)));
         }
         __syncthreads();
         uint4* d = (uint4*)dst(sl);
@@ -594,7 +628,7 @@ __global__ __launch_bounds__(kProjectBlock) void k_part_pack(
     const uint32_t gid = blockIdx.x * kProjectBlock + threadIdx.x;
     const uint32_t mask = gid < count ? masks[gid] : 0u;
     write_slab_runs(
-        records, mask, gid, slabs.n, slabs.rows,
+        records, mask, gid, slabs.n, slabs,
         [&](uint32_t sl) {
             uint64_t base = 0;
             for (uint32_t t = 0; t < sl; ++t) base += sendCounts[t];
@@ -656,8 +690,10 @@ __global__ __launch_bounds__(kProjectBlock) void k_records_in(
         r.rb = w2.z;
         r.pad = w2.w;
         const int rw = (int)r.bounds.y - (int)r.bounds.x + 1;
-        const int ry0 = max((int)r.bounds.z, (int)P.rowBegin), ry1 = min((int)r.bounds.w, (int)P.rowEnd - 1);
-        if (P.keepRenderData || (ry1 - ry0 + 1) * rw > kMaskTiles) *(uint4*)(outRD + gid) = r.rd;
+        const RowSet R = rows_of(P);
+        int k0, k1;
+        rows_within(R, (int)r.bounds.z, (int)r.bounds.w, &k0, &k1);
+        if (P.keepRenderData || (k1 - k0 + 1) * rw > kMaskTiles) *(uint4*)(outRD + gid) = r.rd;
         outBounds[gid] = r.bounds;
         uint4* rp = (uint4*)(outRec + gid);
         rp[0] = make_uint4(r.ra.x, r.ra.y, r.ra.z, r.ra.w);
@@ -678,11 +714,11 @@ __global__ __launch_bounds__(kProjectBlock) void k_records_in(
             const float alpha = (float)(r.rd.w >> 24);
             o.countable = alpha >= 1e-4f && r.bounds.x <= r.bounds.y && r.bounds.z <= r.bounds.w;
             o.w = o.countable ? 2.0f * compute_power(alpha) : 0.0f;
-            ntiles = count_tiles(o, (int)P.rowBegin, (int)P.rowEnd, &mask);
+            ntiles = count_tiles(o, R, &mask);
         }
         counts[gid] = ntiles;
         masks[gid] = mask;
-        const float2 band = ntiles ? band_of(r.ra, r.bounds, (int)P.rowBegin, (int)P.rowEnd) : make_float2(0.f, -1.f);
+        const float2 band = ntiles ? band_of(r.ra, r.bounds, R) : make_float2(0.f, -1.f);
         rp[1] = make_uint4(r.rb, __float_as_uint(band.x), __float_as_uint(band.y), 0u);
     }
     uint32_t s = block_reduce_add<kProjectBlock>(ntiles, lds);
@@ -791,7 +827,7 @@ __global__ __launch_bounds__(kProjectBlock) void k_scatter(
     __shared__ uint32_t sOff[kProjectBlock];
     __shared__ uint32_t sMask[kProjectBlock];  // 0: no cooperative slots (large rect or no tiles)
     __shared__ uint32_t sRect[kProjectBlock];  // x0 | rw << 16 (rw <= 32)
-    __shared__ int sTy0[kProjectBlock];
+    __shared__ int sTy0[kProjectBlock];        // first row index of the rect in the renderer's rows
     __shared__ uint32_t sD[kProjectBlock];     // depth bits of the key
     __shared__ float2 sBand[kProjectBlock];    // skip-flag band of each gaussian: mean x, half width (< 0: none)
     // the block's first kOwnCap slots: owner << 5 | tile bit of each small-rect slot, kNoOwner for the
@@ -820,8 +856,9 @@ __global__ __launch_bounds__(kProjectBlock) void k_scatter(
         // the key's depth: the fp16 depth bits of the blend record (b = colB | depth << 16, the same
         // bits as GaussianRenderData.depth), so the scatter reads one 16-B slot per gaussian
         dbits = ((r1.x >> 16) ^ 0x8000u) & 0xFFFFu;
-        ty0 = max((int)r.z, (int)P.rowBegin);
-        ty1 = min((int)r.w, (int)P.rowEnd - 1);
+        // row indices of the renderer's rows inside the rect (the keys carry local tile ids,
+        // k * tilesX + tx: the sort, the tile starts and the blend count the renderer's rows only)
+        rows_within(rows_of(P), (int)r.z, (int)r.w, &ty0, &ty1);
         const int rw = (int)r.y - (int)r.x + 1;
         large = (ty1 - ty0 + 1) * rw > kMaskTiles;
         if (!large) mask = masks[gid];
@@ -868,8 +905,8 @@ __global__ __launch_bounds__(kProjectBlock) void k_scatter(
         if (wp >= P.maxAssignments) continue;
         const uint32_t rect = sRect[lo];
         const uint32_t rwo = rect >> 16;
-        const int ty = sTy0[lo] + (int)(bit / rwo), tx = (int)(rect & 0xFFFFu) + (int)(bit % rwo);
-        keys[wp] = ((uint32_t)(ty * (int)P.bin.tilesX + tx) << 16) | sD[lo];
+        const int k = sTy0[lo] + (int)(bit / rwo), tx = (int)(rect & 0xFFFFu) + (int)(bit % rwo);
+        keys[wp] = ((uint32_t)(k * (int)P.bin.tilesX + tx) << 16) | sD[lo];
         const float2 bd = sBand[lo];
         vals[wp] = (blockIdx.x * kProjectBlock + lo) | (half_skip_flags(bd.x, bd.y, tx) << kHalfSkipShift);
     }
@@ -885,11 +922,12 @@ __global__ __launch_bounds__(kProjectBlock) void k_scatter(
     float cx = hbits_to_f(hmx), cy = hbits_to_f(hmy);
     Conic k = conic_from_quant(sincos, thq, hbits_to_f(hs1), hbits_to_f(hs2));
     float w = 2.0f * compute_power((float)opac);
-    for (int ty = ty0; ty <= ty1; ++ty)
-        for (int tx = (int)r.x; tx <= (int)r.y; ++tx)
+    const RowSet R = rows_of(P);
+    for (int kr = ty0; kr <= ty1; ++kr)
+        for (int tx = (int)r.x, ty = R.b + kr * R.s; tx <= (int)r.y; ++tx)
             if (intersects_tile(tx, ty, cx, cy, k, w)) {
                 if (wp < P.maxAssignments) {
-                    uint32_t tile = (uint32_t)(ty * (int)P.bin.tilesX + tx);
+                    uint32_t tile = (uint32_t)(kr * (int)P.bin.tilesX + tx);
                     keys[wp] = (tile << 16) | dbits;
                     vals[wp] = gid | (half_skip_flags(band.x, band.y, tx) << kHalfSkipShift);
                     wp++;
@@ -953,7 +991,7 @@ __global__ __launch_bounds__(kProjectBlock) void k_part_push(
     const uint32_t mask = gid < count ? masks[gid] : 0u;
     __syncthreads();  // (dstOff)
     write_slab_runs(
-        records, mask, gid, world, slabs.rows,
+        records, mask, gid, world, slabs,
         [&](uint32_t sl) {
             return peers.recv[sl] + (uint64_t)dstOff[sl] + blockSlabOffsets[(size_t)sl * gridDim.x + blockIdx.x];
         },
@@ -1151,7 +1189,7 @@ void launch_scatter(const ProjectArgs& a, const DeviceArena& A, hipStream_t s, c
 
 void launch_headers(const uint32_t* sortedKeys, const FrameGeometry& g, const DeviceArena& A,
                     hipStream_t s) {
-    const uint32_t t0 = g.rowBegin * g.tilesX, t1 = g.rowEnd * g.tilesX;
+    const uint32_t t0 = 0, t1 = g.rowCount * g.tilesX;  // the keys hold local tile ids (k_scatter)
     if (t1 <= t0) return;
     uint32_t blocks = (g.maxAssignments + 1u + 1023u) / 1024u;  // grid-stride over the device-side total
     if (blocks > 4096u) blocks = 4096u;

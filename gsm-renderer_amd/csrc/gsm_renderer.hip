@@ -197,6 +197,7 @@ ProjectArgs GlobalRenderer::frameArgs(const gsm_camera_params& camp, uint32_t wi
     a.bin.totalInkThreshold = 2.0f;
     a.rowBegin = rowBegin_;
     a.rowEnd = rowEnd_;
+    a.rowStride = rowStride_;
     a.count = count;
     a.maxAssignments = maxAssignments_;
     // uniform terms of the projection, same operation order as the per-gaussian code
@@ -240,6 +241,9 @@ gsm_status GlobalRenderer::render(hipStream_t s, const gsm_gaussian_input& in,
     gsm_status st = validateFrame(in.gaussian_count, !in.gaussians || !in.harmonics, width, height, color,
                                   colorPitch, depth, depthPitch);
     if (st != GSM_OK) return st;
+    // the projection's tile tests walk contiguous rows; interleaved row sets come from the records
+    // path only (gsm_multigpu)
+    if (rowStride_ != 1) return GSM_ERR_INVALID_ARGUMENT;
     const ProjectArgs a = frameArgs(camp, width, height, in.gaussian_count, in.sh_components);
     // GlobalProjectCullEncoder.swift:19-26 SH_DEGREE selection
     const uint32_t k = in.sh_components;
@@ -270,7 +274,8 @@ gsm_status GlobalRenderer::renderRecords(hipStream_t s, const void* records, uin
 gsm_status GlobalRenderer::preparePartition(const gsm_gaussian_input& in, const gsm_camera_params& camp,
                                             uint32_t width, uint32_t height, uint32_t first, uint32_t count,
                                             const uint32_t* slabRows, uint32_t numSlabs, bool needSend,
-                                            const void* send, const uint32_t* sendCounts, PartitionFrame* f) {
+                                            const void* send, const uint32_t* sendCounts, PartitionFrame* f,
+                                            bool interleave) {
     if ((uint64_t)first + count > in.gaussian_count || count > maxGaussians_)
         return GSM_ERR_INVALID_GAUSSIAN_COUNT;
     if (width == 0 || height == 0 || width > maxWidth_ || height > maxHeight_)
@@ -280,8 +285,10 @@ gsm_status GlobalRenderer::preparePartition(const gsm_gaussian_input& in, const 
         return GSM_ERR_MISSING_REQUIRED_BUFFER;
     std::memset(&f->slabs, 0, sizeof(f->slabs));
     f->slabs.n = numSlabs;
+    f->slabs.interleave = interleave ? 1u : 0u;  // slab s = rows s, s + n, ... < slabRows[n]
     for (uint32_t i = 0; i <= numSlabs; ++i) {
-        if (slabRows[i] > tilesY_ || (i > 0 && slabRows[i] < slabRows[i - 1])) return GSM_ERR_INVALID_ARGUMENT;
+        if (slabRows[i] > tilesY_ || (!interleave && i > 0 && slabRows[i] < slabRows[i - 1]))
+            return GSM_ERR_INVALID_ARGUMENT;
         f->slabs.rows[i] = slabRows[i];
     }
     if (hipSetDevice(device_) != hipSuccess) return GSM_ERR_DEVICE_NOT_AVAILABLE;
@@ -297,8 +304,9 @@ gsm_status GlobalRenderer::preparePartition(const gsm_gaussian_input& in, const 
     }
     f->half = config_.precision == GSM_PRECISION_FLOAT16;
     f->a = frameArgs(camp, width, height, count, in.sh_components);
-    f->a.rowBegin = 0;
+    f->a.rowBegin = 0;  // the rank's ids are projected against the whole frame
     f->a.rowEnd = tilesY_;
+    f->a.rowStride = 1;
     const size_t ws = f->half ? sizeof(PackedWorldGaussianHalf) : sizeof(PackedWorldGaussian);
     const size_t hs = (size_t)in.sh_components * 3 * (f->half ? 2 : 4);
     f->world = (const char*)in.gaussians + (size_t)first * ws;
@@ -326,10 +334,10 @@ gsm_status GlobalRenderer::projectPartition(hipStream_t s, const gsm_gaussian_in
 gsm_status GlobalRenderer::partitionCounts(hipStream_t s, const gsm_gaussian_input& in, const gsm_camera_params& camp,
                                            uint32_t width, uint32_t height, uint32_t first, uint32_t count,
                                            const uint32_t* slabRows, uint32_t numSlabs, uint32_t* sendCounts,
-                                           bool orderUnits) {
+                                           bool orderUnits, bool interleave) {
     PartitionFrame f;
     gsm_status st = preparePartition(in, camp, width, height, first, count, slabRows, numSlabs, false, nullptr,
-                                     sendCounts, &f);
+                                     sendCounts, &f, interleave);
     if (st != GSM_OK) return st;
     // the blend units of this renderer's rows (its slab), ordered by one extra workgroup of the launch
     f.a.schedUnits = orderUnits ? scheduleUnits(s, width, height) : 0u;
@@ -353,10 +361,10 @@ gsm_status GlobalRenderer::partitionPush(hipStream_t s, uint32_t world, uint32_t
 }
 
 uint32_t GlobalRenderer::scheduleUnits(hipStream_t s, uint32_t width, uint32_t height) {
-    const uint32_t upt = blend_units_per_tile((rowEnd_ - rowBegin_) * tilesX_, numCUs_);
-    const uint32_t units = (rowEnd_ - rowBegin_) * tilesX_ * upt;
+    const uint32_t upt = blend_units_per_tile(rowCount() * tilesX_, numCUs_);
+    const uint32_t units = rowCount() * tilesX_ * upt;
     const uint64_t key = ((uint64_t)upt << 60) ^ ((uint64_t)width << 40) ^ ((uint64_t)height << 20) ^
-                         ((uint64_t)rowBegin_ << 10) ^ rowEnd_;
+                         ((uint64_t)rowStride_ << 30) ^ ((uint64_t)rowBegin_ << 10) ^ rowEnd_;
     if (key != schedKey_) {  // new geometry: no walks to order by yet
         hipMemsetAsync(arena_.unitCost, 0, (size_t)units * sizeof(uint16_t), s);
         hipMemsetAsync(arena_.costMax, 0, kCostMaxSlots * sizeof(uint32_t), s);
@@ -414,6 +422,8 @@ gsm_status GlobalRenderer::runFrame(hipStream_t s, const ProjectArgs& a, uint32_
     g.tileCount = tileCount_;
     g.rowBegin = rowBegin_;
     g.rowEnd = rowEnd_;
+    g.rowStride = rowStride_;
+    g.rowCount = rowCount();
     g.width = width;
     g.height = height;
     g.maxAssignments = maxAssignments_;
@@ -424,14 +434,15 @@ gsm_status GlobalRenderer::runFrame(hipStream_t s, const ProjectArgs& a, uint32_
     const bool fullRadix = tuning_.fullRadix;
     const bool ballot = tuning_.ballotRank;
     if (!fullRadix) {
-        // the last tile pass also writes the tile starts (radix_sort_tiles: no pass over the keys); a
-        // slab of <= 2048 tiles (multi-GPU) takes one wide pass over its tiles' ids
+        // the last tile pass also writes the tile starts (radix_sort_tiles: no pass over the keys); the
+        // keys hold local tile ids of the renderer's rows (k_scatter): a slab of <= 2048 tiles
+        // (multi-GPU) takes one wide pass
+        const uint32_t localTiles = rowCount() * tilesX_;
         const int res = radix_sort_tiles(kb, vb, &arena_.header->totalAssignments, maxAssignments_, 16,
-                                         arena_.radixHist, arena_.radixBinTotals, arena_.tileStart, rowBegin_ * tilesX_,
-                                         (rowEnd_ - rowBegin_) * tilesX_, tileCount_, s, ballot, tuning_.tileLoBits,
-                                         tuning_.wideSort);
-        tile_depth_sort(kb[res], vb[res], kb[res ^ 1], vb[res ^ 1], arena_.tileStart, rowBegin_ * tilesX_,
-                        (rowEnd_ - rowBegin_) * tilesX_, s, ballot, arena_.halfVals[0], arena_.halfVals[1],
+                                         arena_.radixHist, arena_.radixBinTotals, arena_.tileStart, 0u, localTiles,
+                                         tileCount_, s, ballot, tuning_.tileLoBits, tuning_.wideSort);
+        tile_depth_sort(kb[res], vb[res], kb[res ^ 1], vb[res ^ 1], arena_.tileStart, 0u, localTiles, s, ballot,
+                        arena_.halfVals[0], arena_.halfVals[1],
                         arena_.halfCount, tileCount_, capture, numCUs_);
         sortedKeys_ = capture ? kb[res ^ 1] : nullptr;
         sortedVals_ = capture ? vb[res ^ 1] : nullptr;
@@ -448,7 +459,7 @@ gsm_status GlobalRenderer::runFrame(hipStream_t s, const ProjectArgs& a, uint32_
     // the blend walks per-half lists without the entries its half provably skips (k_scatter flags);
     // the tile sort writes them, the 4-pass sort needs the separate pass
     if (fullRadix)
-        launch_half_lists(sortedVals_, rowBegin_ * tilesX_, (rowEnd_ - rowBegin_) * tilesX_, arena_, tileCount_, s);
+        launch_half_lists(sortedVals_, 0u, rowCount() * tilesX_, arena_, tileCount_, s);
     arena_.blendTrace = (profiling_ & 4) ? traceBuf_ : nullptr;
     // the schedule from the walks the previous frame's blend recorded (same stream: no join)
     if (prof || blendOnly) hipEventRecord(ev[5], s);
@@ -587,15 +598,17 @@ gsm_status GlobalRenderer::debugCopy(int which, void* dst, size_t bytes, size_t*
     return GSM_OK;
 }
 
-gsm_status GlobalRenderer::setTileRows(uint32_t b, uint32_t e) {
+gsm_status GlobalRenderer::setTileRows(uint32_t b, uint32_t e, uint32_t stride) {
     if (b == 0 && e == 0) {
         rowBegin_ = 0;
         rowEnd_ = tilesY_;
+        rowStride_ = 1;
         return GSM_OK;
     }
-    if (b >= e || e > tilesY_) return GSM_ERR_INVALID_ARGUMENT;
+    if (b >= e || e > tilesY_ || stride == 0) return GSM_ERR_INVALID_ARGUMENT;
     rowBegin_ = b;
     rowEnd_ = e;
+    rowStride_ = stride;
     return GSM_OK;
 }
 

@@ -35,7 +35,7 @@ class GlobalRenderer {
     gsm_status partitionCounts(hipStream_t stream, const gsm_gaussian_input& input, const gsm_camera_params& camera,
                                uint32_t width, uint32_t height, uint32_t first, uint32_t count,
                                const uint32_t* slabRows, uint32_t numSlabs, uint32_t* sendCounts,
-                               bool orderUnits = false);
+                               bool orderUnits = false, bool interleave = false);
     gsm_status partitionPush(hipStream_t stream, uint32_t world, uint32_t rank, const uint32_t* counts,
                              const SlabPeers& peers, uint32_t* recvCount);
     gsm_status renderRecords(hipStream_t stream, const void* records, uint32_t count, uint32_t width,
@@ -56,7 +56,9 @@ class GlobalRenderer {
     gsm_status setProfiling(int flags);  // bit0: stage events, bit1: keep unsorted keys
     gsm_status stageTimes(float* ms, int n);
     gsm_status lastGpuTime(double* seconds);
-    gsm_status setTileRows(uint32_t begin, uint32_t end);
+    // the renderer's tile rows: begin, begin + stride, ... < end (0, 0: the whole frame)
+    gsm_status setTileRows(uint32_t begin, uint32_t end, uint32_t stride = 1);
+    uint32_t rowCount() const { return rowEnd_ > rowBegin_ ? (rowEnd_ - rowBegin_ + rowStride_ - 1) / rowStride_ : 0u; }
     int device() const { return device_; }
 
    private:
@@ -88,7 +90,7 @@ class GlobalRenderer {
     gsm_status preparePartition(const gsm_gaussian_input& in, const gsm_camera_params& camera, uint32_t width,
                                 uint32_t height, uint32_t first, uint32_t count, const uint32_t* slabRows,
                                 uint32_t numSlabs, bool needSend, const void* send, const uint32_t* sendCounts,
-                                PartitionFrame* f);
+                                PartitionFrame* f, bool interleave = false);
     void release();
     int sortPassCount() const;
 
@@ -98,7 +100,7 @@ class GlobalRenderer {
     Tuning tuning_{};  // A/B switches, read once at create
     uint32_t maxGaussians_ = 1, maxWidth_ = 1, maxHeight_ = 1;
     uint32_t tilesX_ = 1, tilesY_ = 1, tileCount_ = 1;
-    uint32_t rowBegin_ = 0, rowEnd_ = 1;
+    uint32_t rowBegin_ = 0, rowEnd_ = 1, rowStride_ = 1;
     uint32_t maxAssignments_ = 4;
     DeviceArena arena_;
     std::vector<void*> allocations_;

@@ -131,7 +131,8 @@ static_assert(offsetof(StereoTiledRenderData, colorR) == 24, "layout");
 // Tile-slab bookkeeping for one frame.
 struct FrameGeometry {
     uint32_t tilesX, tilesY, tileCount;
-    uint32_t rowBegin, rowEnd;  // tile rows owned by this renderer (slab)
+    uint32_t rowBegin, rowEnd;  // tile rows owned by this renderer: rowBegin, + rowStride, ... < rowEnd
+    uint32_t rowStride, rowCount;
     uint32_t width, height;     // frame (camera) size
     uint32_t maxAssignments;
 };

@@ -37,6 +37,16 @@ def slab_rows(tiles_y: int, height: int, world_size: int) -> List[int]:
     return [s.row_begin for s in ss] + [ss[-1].row_end]
 
 
+def rank_tile_rows(tiles_y: int, world_size: int, rank: int, interleave: bool = False) -> List[int]:
+    """Tile rows rank owns in the native multi-GPU frame (gsm_multigpu_render): its contiguous
+    block of ceil(tiles_y / W) rows (the default), or rows rank, rank + W, rank + 2W, ... when the
+    ranks were prepared with GSM_MG_ROWS=interleaved."""
+    if interleave:
+        return list(range(rank, tiles_y, world_size))
+    per = -(-tiles_y // world_size)
+    return list(range(min(rank * per, tiles_y), min((rank + 1) * per, tiles_y)))
+
+
 def exchange(send, send_counts, recv, group=None, staged: bool = False) -> int:
     """all_to_all of per-slab record counts, then of the records themselves.
 

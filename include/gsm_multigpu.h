@@ -90,7 +90,10 @@ void gsm_multigpu_destroy(gsm_multigpu *multigpu);
 /* One frame of gsm_global_render (GlobalRenderer.swift:201-238) across the ranks.  Collective:
  * every rank calls it once per frame with the same input (device pointers on its own GPU; it
  * reads only its id range [r * ceil(N / W), +ceil(N / W))), camera, size and gather choice.
- * Rank r owns tile rows [r * ceil(tiles_y / W), +ceil(tiles_y / W)).  Per frame, on `stream`:
+ * Rank r owns tile rows [r * ceil(tiles_y / W), +ceil(tiles_y / W)), or -- when every rank's
+ * process has GSM_MG_ROWS=interleaved in its environment at gsm_multigpu_prepare -- rows r, r + W,
+ * r + 2W, ... (balances content off the frame's centre; a record then travels to every rank one of
+ * its rect's rows maps to).  Per frame, on `stream`:
  *   1. projection of the rank's ids, per-slab record counts written into every rank's count
  *      matrix, flag barrier;
  *   2. every record written straight into its slab owner's receive buffer (offsets from the

@@ -12,7 +12,6 @@ DESIGN.md 7 -- which is one reason the frame uses no collective library.)
 The same kernels run for W virtual ranks in one process (phases issued rank by rank on one stream,
 include/gsm_multigpu.h gsm_multigpu_render_phase) up to config 4, 5M / SH3 / 4K over 8 ranks."""
 import json
-import math
 import os
 import socket
 import subprocess
@@ -52,9 +51,11 @@ def _run_ranks(tmp_path, world, extra=(), timeout=150):
     return [json.load(open(os.path.join(tmp_path, f"status_{r}.json"))) for r in range(world)]
 
 
-@pytest.mark.parametrize("world,n,w,h,sh,prec", [(2, 40_000, 640, 360, 16, 1), (3, 30_000, 1280, 720, 4, 0)])
-def test_processes_on_one_gpu_render_the_oracle_frame(oracle, tmp_path, world, n, w, h, sh, prec):
+@pytest.mark.parametrize("world,n,w,h,sh,prec,rows", [(2, 40_000, 640, 360, 16, 1, "contiguous"),
+                                                      (3, 30_000, 1280, 720, 4, 0, "interleaved")])
+def test_processes_on_one_gpu_render_the_oracle_frame(oracle, tmp_path, monkeypatch, world, n, w, h, sh, prec, rows):
     from gsm_amd import scenes
+    monkeypatch.setenv("GSM_MG_ROWS", rows)  # (the rank processes inherit it)
     st = _run_ranks(tmp_path, world, ["--n", str(n), "--width", str(w), "--height", str(h), "--sh", str(sh),
                                       "--precision", str(prec)])
     assert all(s["timeouts"] == 0 for s in st)
@@ -65,17 +66,18 @@ def test_processes_on_one_gpu_render_the_oracle_frame(oracle, tmp_path, world, n
     # B: next camera, the library's copy into the caller's tensor
     ref_b = oracle.render(world_np, harm_np, sh, scenes.orbit_camera(w, h, 3.0), w, h, max_gaussians=n)
     assert np.array_equal(np.load(tmp_path / "frame_b.npy"), ref_b["color"])
-    # C: bands in each rank's own targets, composed here
+    # C: each rank's tile rows (a contiguous block, or r, r + W, ... interleaved) in its own targets
+    from gsm_amd import exchange
     tiles_y = (h + 15) // 16
-    per = math.ceil(tiles_y / world)
     for r in range(world):
-        y0, y1 = min(r * per * 16, h), min((r + 1) * per * 16, h)
+        own = np.zeros(h, bool)
+        for t in exchange.rank_tile_rows(tiles_y, world, r, interleave=rows == "interleaved"):
+            own[16 * t:min(16 * t + 16, h)] = True
         col = np.load(tmp_path / f"band_c_color_{r}.npy")
         dep = np.load(tmp_path / f"band_c_depth_{r}.npy")
-        assert np.array_equal(col[y0:y1], ref["color"][y0:y1])
-        assert np.array_equal(dep[y0:y1], ref["depth"][y0:y1])
-        nan_rows = np.concatenate([col[:y0], col[y1:]]).reshape(-1)
-        assert np.all((nan_rows & 0x7C00) == 0x7C00)  # rows of other slabs untouched (NaN)
+        assert np.array_equal(col[own], ref["color"][own])
+        assert np.array_equal(dep[own], ref["depth"][own])
+        assert np.all((col[~own].reshape(-1) & 0x7C00) == 0x7C00)  # rows of other ranks untouched (NaN)
     # every rank holds the same count matrix; its column sums are the slabs' receive counts
     cm = np.array(st[0]["counts"], np.int64)
     assert all(np.array_equal(np.array(s["counts"]), cm) for s in st)
@@ -122,12 +124,19 @@ def _virtual_frame(gsm, cuda, world, n, w, h, sh, prec, seed, cams):
     return frames, counts, timeouts
 
 
-@pytest.mark.parametrize("world,n,w,h,prec", [(2, 40_000, 640, 360, 1), (3, 60_000, 1280, 720, 1),
-                                              (8, 50_000, 640, 360, 0), (16, 30_000, 640, 360, 1)])
-def test_virtual_ranks_product_path(gsm, cuda, oracle, world, n, w, h, prec):
+@pytest.mark.parametrize("world,n,w,h,prec,rows", [(2, 40_000, 640, 360, 1, "contiguous"),
+                                                   (3, 60_000, 1280, 720, 1, "contiguous"),
+                                                   (8, 50_000, 640, 360, 0, "contiguous"),
+                                                   (16, 30_000, 640, 360, 1, "contiguous"),
+                                                   (3, 60_000, 1280, 720, 1, "interleaved"),
+                                                   (8, 50_000, 640, 360, 0, "interleaved"),
+                                                   (16, 30_000, 640, 360, 1, "interleaved")])
+def test_virtual_ranks_product_path(gsm, cuda, oracle, monkeypatch, world, n, w, h, prec, rows):
     """W ranks of one process through the product kernels (barriers, pushes, gather into rank 0's
-    frame), two cameras: the second frame reuses the parity-double-buffered count matrix."""
+    frame), two cameras: the second frame reuses the parity-double-buffered count matrix.  Rows in
+    contiguous blocks (the default) or interleaved over the ranks (GSM_MG_ROWS=interleaved)."""
     from gsm_amd import scenes
+    monkeypatch.setenv("GSM_MG_ROWS", rows)
     sh = 16 if prec else 4
     cams = [scenes.make_camera(w, h), scenes.orbit_camera(w, h, 5.0)]
     frames, counts, timeouts = _virtual_frame(gsm, cuda, world, n, w, h, sh, prec, 78, cams)

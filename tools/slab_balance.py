@@ -37,11 +37,30 @@ def splits(ty, w, prev_load):
     per = math.ceil(ty / w)
     contiguous = [list(range(r * per, min(ty, (r + 1) * per))) for r in range(w)]
     interleaved = [list(range(r, ty, w)) for r in range(w)]
+    cyclic = {b: [[y for y in range(ty) if (y // b) % w == r] for r in range(w)] for b in (2, 4)}
     cum = np.cumsum(prev_load) / max(prev_load.sum(), 1)
     cuts = [0] + [int(np.searchsorted(cum, k / w)) + 1 for k in range(1, w)] + [ty]
     cuts = np.maximum.accumulate(np.minimum(cuts, ty))
     adaptive = [list(range(cuts[r], cuts[r + 1])) for r in range(w)]
-    return {"contiguous": contiguous, "interleaved": interleaved, "adaptive": adaptive}
+    return {"contiguous": contiguous, "interleaved": interleaved, "cyclic2": cyclic[2], "cyclic4": cyclic[4],
+            "adaptive": adaptive}
+
+
+def records(fr, parts):
+    """(gaussian, rank) records the exchange moves: a gaussian with tiles goes to every rank owning a
+    row of its rect (the rect rows bound the rows its tile tests hit)"""
+    b = fr["bounds"]
+    live = fr["tile_counts"] > 0
+    y0, y1 = b[live, 2], b[live, 3]
+    owner = np.full(fr["tiles_y"], -1)
+    for r, rows in enumerate(parts):
+        owner[rows] = r
+    tot = 0
+    for r in range(len(parts)):
+        mine = np.zeros(fr["tiles_y"] + 1, np.int64)
+        mine[1:] = np.cumsum(owner == r)
+        tot += int(np.count_nonzero(mine[y1 + 1] - mine[y0] > 0))
+    return tot
 
 
 def imbalance(load, parts):
@@ -80,8 +99,8 @@ def main():
             case = {"scene": sname, "orbit_deg": ang, "assignments": int(assign.sum()), "by_world": {}}
             for w in (2, 4, 8):
                 sp = splits(fr["tiles_y"], w, ref)
-                case["by_world"][w] = {k: {"assign": imbalance(assign, v), "blend": imbalance(blend, v)}
-                                       for k, v in sp.items()}
+                case["by_world"][w] = {k: {"assign": imbalance(assign, v), "blend": imbalance(blend, v),
+                                           "records": records(fr, v)} for k, v in sp.items()}
             out["cases"].append(case)
             print(json.dumps(case))
             prev = blend

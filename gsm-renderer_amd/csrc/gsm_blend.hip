@@ -15,6 +15,10 @@
 #include "gsm_internal.h"
 #include "gsm_types.h"
 
+#ifndef GSM_BLEND_P1_TILES_PER_CU
+#define GSM_BLEND_P1_TILES_PER_CU 8u
+#endif
+
 namespace gsm {
 
 typedef _Float16 h1;
@@ -594,7 +598,7 @@ int blend_pairs_per_lane(uint32_t numTiles, int numCUs) {
     // or a slab of a multi-GPU frame has fewer units than slots, its blend time is its longest
     // unit's walk, and quadrant units (1 pair per lane, ~38 instead of ~61 VALU per entry)
     // shorten that (measured on 1/2, 1/4, 1/8 of the 1080p rows: 149/130/118 -> 138/105/96 us)
-    return numTiles <= (uint32_t)numCUs * 8u ? 1 : 2;
+    return numTiles <= (uint32_t)numCUs * GSM_BLEND_P1_TILES_PER_CU ? 1 : 2;
 }
 
 uint32_t blend_units_per_tile(uint32_t numTiles, int numCUs) {

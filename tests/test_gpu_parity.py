@@ -186,8 +186,9 @@ def _synth(n, w, h, sh, prec, seed, **kw):
     return dict(world=world, harm=harm, sh=sh, cam=cam, width=w, height=h, max_gaussians=max(n, 1))
 
 
-def test_empty_frame_is_clear(gsm, cuda, oracle):
-    case = _synth(64, 320, 180, 1, 0, 1)
+@pytest.mark.parametrize("w,h", [(320, 180), (1280, 720)])  # 120 tiles: one narrow pass; 1800: one wide pass
+def test_empty_frame_is_clear(gsm, cuda, oracle, w, h):
+    case = _synth(64, w, h, 1, 0, 1)
     case["count"] = 0
     g = gpu_render(gsm, cuda, case)
     r = oracle_render(oracle, case)

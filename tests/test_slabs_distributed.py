@@ -27,6 +27,24 @@ def test_partition_covers_rows_once(tiles_y, height, n):
     assert np.all(rows == 1) and np.all(pix == 1)
 
 
+@pytest.mark.parametrize("tiles_y,n", [(23, 2), (68, 8), (135, 8), (5, 8), (5, 16), (68, 3)])
+@pytest.mark.parametrize("interleave", [False, True])
+def test_native_rank_rows_cover_rows_once(tiles_y, n, interleave):
+    """The native multi-GPU frame's row ownership (gsm_amd.exchange.rank_tile_rows, the rule of
+    csrc/gsm_multigpu.hip): contiguous blocks or interleaved rows, every tile row owned once."""
+    from gsm_amd import exchange
+    owned = np.zeros(tiles_y, int)
+    for r in range(n):
+        rows = exchange.rank_tile_rows(tiles_y, n, r, interleave=interleave)
+        assert rows == sorted(rows)
+        if interleave:
+            assert all(t % n == r for t in rows)
+        elif rows:
+            assert rows == list(range(rows[0], rows[-1] + 1))
+        owned[rows] += 1
+    assert np.all(owned == 1)
+
+
 def _free_port():
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))

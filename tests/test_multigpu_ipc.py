@@ -52,7 +52,8 @@ def _run_ranks(tmp_path, world, extra=(), timeout=150):
 
 
 @pytest.mark.parametrize("world,n,w,h,sh,prec,rows", [(2, 40_000, 640, 360, 16, 1, "contiguous"),
-                                                      (3, 30_000, 1280, 720, 4, 0, "interleaved")])
+                                                      (3, 30_000, 1280, 720, 4, 0, "interleaved"),
+                                                      (4, 30_000, 640, 360, 9, 1, "contiguous")])
 def test_processes_on_one_gpu_render_the_oracle_frame(oracle, tmp_path, monkeypatch, world, n, w, h, sh, prec, rows):
     from gsm_amd import scenes
     monkeypatch.setenv("GSM_MG_ROWS", rows)  # (the rank processes inherit it)

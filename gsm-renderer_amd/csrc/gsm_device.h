@@ -134,6 +134,31 @@ __device__ __forceinline__ float load_harm(const void* __restrict__ h, size_t i)
     }
 }
 
+#ifndef GSM_SH_FMAMIX
+#define GSM_SH_FMAMIX 1
+#endif
+// fp32(h) * b for the fp16 in the low / high half of w: one v_fma_mix_f32 (the fp16 operand widened
+// exactly inside the instruction, fma(h, b, -0) = the correctly rounded product) instead of a
+// v_cvt_f32_f16 and a v_mul_f32 -- the same bits as the contract's convert-then-multiply
+__device__ __forceinline__ float mul_h_lo(uint32_t w, float b) {
+#if GSM_SH_FMAMIX
+    float r;
+    asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel_hi:[1,0,0]" : "=v"(r) : "v"(w), "v"(b), "v"(-0.0f));
+    return r;
+#else
+    return hbits_to_f((uint16_t)(w & 0xFFFFu)) * b;
+#endif
+}
+__device__ __forceinline__ float mul_h_hi(uint32_t w, float b) {
+#if GSM_SH_FMAMIX
+    float r;
+    asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "=v"(r) : "v"(w), "v"(b), "v"(-0.0f));
+    return r;
+#else
+    return hbits_to_f((uint16_t)(w >> 16)) * b;
+#endif
+}
+
 // computeSHColor (GaussianShared.h:38-116) specialised by degree like the
 // SH_DEGREE function constant (GlobalProjectCullEncoder.swift:19-45).
 template <bool HALF, int DEG>
@@ -181,24 +206,23 @@ __device__ __forceinline__ void sh_color(const void* __restrict__ harm, uint32_t
     if constexpr (HALF && DEG == 3) {
         // 96 B per gaussian, 16-B aligned: six dwordx4 loads.
         const uint4* p = (const uint4*)((const uint16_t*)harm + base);
-        uint16_t hv[48];
+        uint32_t hw[24];  // coefficient 2k in the low half of hw[k], 2k + 1 in the high half
 #pragma unroll
         for (int q = 0; q < 6; ++q) {
             uint4 v = p[q];
-            uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-            for (int t = 0; t < 4; ++t) {
-                hv[q * 8 + 2 * t] = (uint16_t)(w[t] & 0xFFFFu);
-                hv[q * 8 + 2 * t + 1] = (uint16_t)(w[t] >> 16);
-            }
+            hw[4 * q] = v.x;
+            hw[4 * q + 1] = v.y;
+            hw[4 * q + 2] = v.z;
+            hw[4 * q + 3] = v.w;
         }
+        auto mulc = [&](int c, float bb) { return (c & 1) ? mul_h_hi(hw[c >> 1], bb) : mul_h_lo(hw[c >> 1], bb); };
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
-            cr = cr + hbits_to_f(hv[i]) * b[i];
-            cg = cg + hbits_to_f(hv[16 + i]) * b[i];
-            cb = cb + hbits_to_f(hv[32 + i]) * b[i];
+            cr = cr + mulc(i, b[i]);
+            cg = cg + mulc(16 + i, b[i]);
+            cb = cb + mulc(32 + i, b[i]);
         }
-    } else {
+    } else {  // (v_fma_mix here, on 2-byte loads: DepthFirst SH2 projection 60.3 -> 63.5 us, not kept)
 #pragma unroll
         for (int i = 0; i < K; ++i) {
             cr = cr + load_harm<HALF>(harm, base + i) * b[i];

@@ -12,6 +12,10 @@
 #include "gsm_internal.h"
 #include "gsm_types.h"
 
+#ifndef GSM_SCAN_RUNS
+#define GSM_SCAN_RUNS 1
+#endif
+
 namespace gsm {
 
 // ---------------------------------------------------------------------------
@@ -743,6 +747,53 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_blocks(uint32_t* __restri
     constexpr uint32_t kRow = 4u * kScanThreads, kScanRows = 8;
     const uint32_t t4 = threadIdx.x * 4u;
     uint64_t carry = 0;
+    // up to 32 sums per thread (nb <= 32768: config 3's 19.5K blocks): thread t scans its own
+    // contiguous run of `per` sums (16-byte loads, all in flight), then ONE block scan of the run
+    // totals -- instead of one block scan per 4096-sum row (config 3: 5)
+    const uint32_t per = ((nb + kScanThreads - 1) / kScanThreads + 3u) & ~3u;
+    if (GSM_SCAN_RUNS && nb > kRow && per <= 32u) {
+        constexpr uint32_t kV = 8;
+        uint4 v[kV];
+        const uint32_t b0 = threadIdx.x * per;
+#pragma unroll
+        for (uint32_t r = 0; r < kV; ++r) {
+            const uint32_t i = b0 + 4u * r;
+            v[r] = (4u * r < per && i + 3u < nb) ? *(const uint4*)(sums + i)
+                   : (4u * r < per ? make_uint4(i < nb ? sums[i] : 0u, i + 1u < nb ? sums[i + 1u] : 0u,
+                                                i + 2u < nb ? sums[i + 2u] : 0u, 0u)
+                                   : make_uint4(0u, 0u, 0u, 0u));
+        }
+        uint64_t local = 0;
+#pragma unroll
+        for (uint32_t r = 0; r < kV; ++r) local += (uint64_t)v[r].x + v[r].y + v[r].z + v[r].w;
+        // run totals fit 32 bits unless the frame overflows anyway (clamped below); the block scan
+        // takes them saturated, the carry is exact
+        uint32_t tot;
+        const uint32_t off = block_exclusive_scan<kScanThreads>(local > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)local,
+                                                                lds, &tot);
+        uint64_t run = off;
+#pragma unroll
+        for (uint32_t r = 0; r < kV; ++r) {
+            const uint32_t i = b0 + 4u * r;
+            if (4u * r >= per || i >= nb) break;
+            const uint32_t in[4] = {v[r].x, v[r].y, v[r].z, v[r].w};
+            uint32_t o[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                o[j] = run > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)run;
+                run += in[j];
+            }
+            if (i + 3u < nb) {
+                *(uint4*)(sums + i) = make_uint4(o[0], o[1], o[2], o[3]);
+            } else {
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    if (i + (uint32_t)j < nb) sums[i + j] = o[j];
+            }
+        }
+        carry = tot;
+        nb = 0;  // (the row loop below has nothing left)
+    }
     for (uint32_t base = 0; base < nb; base += kScanRows * kRow) {
         uint4 v[kScanRows];
 #pragma unroll

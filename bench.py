@@ -105,6 +105,10 @@ def parse():
                    help="stereo configs: DepthFirst semantics (SURVEY 8f rank 1) or two Global views")
     p.add_argument("--df-max-gaussians", type=int, default=6_000_000,
                    help="DepthFirst RendererConfig.maxGaussians (reference default 6M -> 24M instances)")
+    p.add_argument("--virtual-ranks", type=int, default=8,
+                   help="N=1: also run BASELINE config 4's frame (5M/SH3/4K) split over this many virtual "
+                        "ranks on the one GPU (tools/exp_virtual_ranks.py, a child process): per-rank device "
+                        "frame and its speedup over the same frame on one renderer; 0 = off")
     p.add_argument("--multi", choices=("alltoall", "replicas"), default="alltoall",
                    help="N>1 partition: all-to-all of projected records (8e) or projection replicas")
     p.add_argument("--multi-extra-config", default="cfg3_5m_sh3_4k_f16",
@@ -135,6 +139,29 @@ def launch_ranks(args) -> int:
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
     return subprocess.call(cmd)
+
+
+def virtual_ranks_entry(world: int):
+    """BASELINE config 4 (5M / SH3 / 3840x2160 over `world` ranks) measured without a multi-GPU node:
+    the product's multi-GPU frame (gsm_multigpu_render_phase) for `world` virtual ranks on this GPU,
+    each rank's phases timed alone with the whole GPU -- the device part of one rank's frame, no xGMI
+    -- against the same frame on one renderer (tools/exp_virtual_ranks.py, run as a child process so
+    this process's GPU state stays as it is).  None when the child fails."""
+    import subprocess
+    cmd = [sys.executable, os.path.join(ROOT, "tools", "exp_virtual_ranks.py"), "--config", "cfg3_5m_sh3_4k_f16",
+           "--world", str(world), "--frames", "5", "--stages", "0", "--single", "1"]
+    try:
+        p = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+        d = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
+    except Exception as e:  # noqa: BLE001 -- reported, never fatal for the bench line
+        return {"error": f"{type(e).__name__}: {str(e)[:200]}"}
+    return {"workload": "cfg3_5m_sh3_4k_f16 frame (BASELINE configs[3]) over %d virtual ranks" % world,
+            "world": world, "device_frame_ms": d["device_frame_ms"], "max_phase_ms": d["max_phase_ms"],
+            "one_gpu_frame_ms": d.get("one_gpu_frame_ms"), "device_speedup": d.get("device_speedup"),
+            "barrier_timeouts": d.get("timeouts"),
+            "note": "each rank's phases run alone on this GPU (an upper bound for a rank's own GPU); the pushes "
+                    "and the gathered pixels stay local (no xGMI time); device_speedup = one-renderer frame / "
+                    "per-rank device frame"}
 
 
 def main():
@@ -500,6 +527,8 @@ def main():
         out["barrier_timeouts"] = barrier_timeouts
     if multi_4k:
         out["config4"] = multi_4k
+    if world_size == 1 and not stereo and args.virtual_ranks > 1:
+        out["virtual_ranks_config4"] = virtual_ranks_entry(args.virtual_ranks)
     print(json.dumps(out))
     renderer.close()
     if world_size > 1:

@@ -28,6 +28,8 @@ def main():
     ap.add_argument("--world", type=int, default=8)
     ap.add_argument("--frames", type=int, default=5)
     ap.add_argument("--stages", type=int, default=1, help="also time the slab render's stages")
+    ap.add_argument("--single", type=int, default=0,
+                    help="also time the whole frame on one renderer (same scene, same box): one_gpu_frame_ms")
     ap.add_argument("--trace-rank", type=int, default=-1,
                     help="per-unit blend trace of this rank's slab (profiling bit 2) -> gpurun_out/vr_trace_*.npz")
     a = ap.parse_args()
@@ -108,6 +110,22 @@ def main():
                  "max_walk": int(walk.max()), "mean_walk": round(float(walk.mean()), 1),
                  "occupancy_deciles": [int(((st <= x) & (en > x)).sum()) for x in grid],
                  "first_start_spread_us": round(float(np.sort(st)[min(len(st) - 1, 3000)]), 1)}
+    one_gpu = None
+    if a.single:  # the same frame on one renderer with the whole frame's rows (bench.py's 1-GPU path)
+        one = gsm.GlobalRenderer(device=0, config=cfg)
+        color = torch.empty((h, w, 4), dtype=torch.float16, device=dev)
+        depth = torch.empty((h, w), dtype=torch.float16, device=dev)
+        for _ in range(3):
+            one.render(color, depth, inp, cam, w, h, stream=stream)
+        torch.cuda.synchronize()
+        e0, e1 = ev(), ev()
+        e0.record(stream)
+        for _ in range(a.frames * 4):
+            one.render(color, depth, inp, cam, w, h, stream=stream)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        one_gpu = e0.elapsed_time(e1) / (a.frames * 4)
+        one.close()
     med = np.median(ph, axis=0)  # [phase][rank]
     out = {"config": a.config, "world": W, "frames": a.frames, "timeouts": [m.status() for m in mgs],
            "counts": mgs[0].counts().tolist(),
@@ -115,6 +133,8 @@ def main():
            "max_phase_ms": [round(float(med[p].max()), 4) for p in range(4)],
            "device_frame_ms": round(float(sum(med[p].max() for p in range(4))), 4),
            "slab_stages_ms": stages, "blend_trace": trace,
+           "one_gpu_frame_ms": round(one_gpu, 4) if one_gpu else None,
+           "device_speedup": round(one_gpu / float(sum(med[p].max() for p in range(4))), 3) if one_gpu else None,
            "note": "virtual ranks on one GPU, product kernels, one stream; no xGMI (pushes and pixels stay local)"}
     print(json.dumps(out))
     for m in mgs:

@@ -22,7 +22,7 @@ for v in A ${VARIANTS:-}; do
   for cfg in ${CFGS:-cfg2_1m_sh3_1080p_f16 cfg3_5m_sh3_4k_f16}; do
     rm -rf $OUT/kt_${v}_$cfg
     timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/kt_${v}_$cfg -o run -- \
-      python bench.py --config $cfg --steps 20 --warmup 3 --cpu-baseline 0 --parity 0 --orbit-steps 0 --inflight-steps 0 \
+      python bench.py --config $cfg --steps 20 --warmup 3 --cpu-baseline 0 --parity 0 --orbit-steps 0 --inflight-steps 0 --virtual-ranks 0 \
       > $OUT/kt_${v}_$cfg.log 2>&1 || { echo "rocprof failed: $v $cfg"; tail -n 5 $OUT/kt_${v}_$cfg.log; use A; exit 1; }
     f=$(find $OUT/kt_${v}_$cfg -name '*kernel_stats.csv' | head -n 1)
     python3 - "$f" "$v $cfg" <<'PY'
@@ -32,7 +32,7 @@ print(sys.argv[2])
 for r in sorted(rows, key=lambda r: -float(r["TotalDurationNs"]))[:12]:
     print(f"  {r['Name'].split('(')[0][:52]:52s} calls={int(r['Calls']):5d} avg_us={float(r['AverageNs'])/1e3:8.1f}")
 PY
-    timeout -k 10 300 python bench.py --config $cfg --steps 50 --warmup 5 --cpu-baseline 0 --orbit-steps ${ORBIT:-0} \
+    timeout -k 10 300 python bench.py --config $cfg --steps 50 --warmup 5 --cpu-baseline 0 --orbit-steps ${ORBIT:-0} --virtual-ranks 0 \
       --traffic-json /dev/null > $OUT/bench_${v}_$cfg.log 2>&1 || { echo "bench failed: $v $cfg"; tail -n 5 $OUT/bench_${v}_$cfg.log; use A; exit 1; }
     grep '"metric"' $OUT/bench_${v}_$cfg.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('  bench', '$v', round(d['value'],1), 'parity', d.get('parity_vs_oracle'), 'inflight2', (d.get('inflight2') or {}).get('value'), (d.get('inflight2') or {}).get('parity_both_targets'), {k: round(x*1e3,1) for k,x in d['stages_ms'].items()})"
   done

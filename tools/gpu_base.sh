@@ -8,7 +8,7 @@ T=${TAG:-base}
 mkdir -p gpurun_out/$T
 for cfg in ${CFGS:-cfg2_1m_sh3_1080p_f16 cfg3_5m_sh3_4k_f16}; do
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/$T/kt_$cfg -o run -- \
-    python bench.py --config $cfg --steps 20 --warmup 3 --cpu-baseline 0 --parity 0 --orbit-steps 0 --inflight-steps 0 \
+    python bench.py --config $cfg --steps 20 --warmup 3 --cpu-baseline 0 --parity 0 --orbit-steps 0 --inflight-steps 0 --virtual-ranks 0 \
     > gpurun_out/$T/kt_$cfg.log 2>&1 || { echo "trace failed $cfg"; tail -5 gpurun_out/$T/kt_$cfg.log; exit 1; }
   echo "== $cfg"; tail -1 gpurun_out/$T/kt_$cfg.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('fps', round(d['value'],1), {k: round(v*1e3,1) for k,v in d['stages_ms'].items()})"
   python3 tools/timeline.py $(find gpurun_out/$T/kt_$cfg -name '*kernel_trace.csv' | head -1) | tee gpurun_out/$T/timeline_$cfg.txt
@@ -20,7 +20,7 @@ if [ "${PMC:-1}" = "1" ]; then
              "SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_LDS_ADDR_CONFLICT SQ_INSTS_SALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_BUSY_CYCLES"; do
     i=$((i+1))
     timeout -s KILL 120 rocprofv3 --pmc $set --output-format csv -d gpurun_out/$T/pmc$i -o p -- \
-      python bench.py --steps 5 --warmup 2 --cpu-baseline 0 --parity 0 --orbit-steps 0 --inflight-steps 0 > gpurun_out/$T/pmc$i.log 2>&1 || { echo "pmc $i failed"; tail -5 gpurun_out/$T/pmc$i.log; exit 1; }
+      python bench.py --steps 5 --warmup 2 --cpu-baseline 0 --parity 0 --orbit-steps 0 --inflight-steps 0 --virtual-ranks 0 > gpurun_out/$T/pmc$i.log 2>&1 || { echo "pmc $i failed"; tail -5 gpurun_out/$T/pmc$i.log; exit 1; }
   done
   python3 tools/pmc_summary.py gpurun_out/$T > gpurun_out/$T/pmc_summary.txt 2>&1; grep -A26 "k_blend" gpurun_out/$T/pmc_summary.txt | head -30
 fi

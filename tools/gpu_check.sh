@@ -19,7 +19,7 @@ step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 step bench 600 python bench.py --steps ${BENCH_STEPS:-50} --warmup 5
 if [ "${PROFILE:-1}" = "1" ]; then
   step rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- \
-       python bench.py --steps 20 --warmup 3 --cpu-baseline 0 --parity 0 --orbit-steps 0 --inflight-steps 0
+       python bench.py --steps 20 --warmup 3 --cpu-baseline 0 --parity 0 --orbit-steps 0 --inflight-steps 0 --virtual-ranks 0
   find gpurun_out/prof -name "*kernel_stats.csv" -exec cp {} gpurun_out/kernel_stats.csv \; 2>/dev/null
   head -n 30 gpurun_out/kernel_stats.csv 2>/dev/null
 fi

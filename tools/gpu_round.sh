@@ -25,7 +25,7 @@ if [ "${PMC:-1}" = 1 ]; then
   for cfg in $CFGS; do
     c=${cfg%%_*}
     kern=k_blend_px; [ $c = cfg5 ] && kern=k_df_blend_eye
-    CMD="python bench.py --config $cfg --steps 5 --warmup 2 --cpu-baseline 0 --parity 0 --orbit-steps 0 --inflight-steps 0"
+    CMD="python bench.py --config $cfg --steps 5 --warmup 2 --cpu-baseline 0 --parity 0 --orbit-steps 0 --inflight-steps 0 --virtual-ranks 0"
     i=0
     for set in "FETCH_SIZE" "WRITE_SIZE" \
                "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE" \
@@ -46,6 +46,6 @@ for cfg in $CFGS; do
   [ $c = cfg5 ] && step bench_${c}_global 600 python bench.py --config $cfg --stereo-path global --cpu-baseline 0 \
        --traffic-json /dev/null
   step kt_$c 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/kt_$c -o run -- \
-       python bench.py --config $cfg --steps 50 --warmup 5 --cpu-baseline 0 --parity 0 --orbit-steps 0 --inflight-steps 0
+       python bench.py --config $cfg --steps 50 --warmup 5 --cpu-baseline 0 --parity 0 --orbit-steps 0 --inflight-steps 0 --virtual-ranks 0
 done
 echo "=== done"

@@ -19,7 +19,7 @@ step pytest_gpu 600 python -u -m pytest tests -m gpu -x -q -rf --timeout 120 --t
 for w in ${WIDE_AB:-1 0}; do
   export GSM_SORT_WIDE=$w
   step kt_cfg5_w$w 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/wide/kt5_w$w -o run -- \
-       python bench.py --config cfg5_1m_sh2_stereo_2x1440x1600_f16 --steps 20 --warmup 3 --cpu-baseline 0 --parity 0 --orbit-steps 0 --inflight-steps 0
+       python bench.py --config cfg5_1m_sh2_stereo_2x1440x1600_f16 --steps 20 --warmup 3 --cpu-baseline 0 --parity 0 --orbit-steps 0 --inflight-steps 0 --virtual-ranks 0
   step vr_cfg3_w$w 300 python tools/exp_virtual_ranks.py --config cfg3_5m_sh3_4k_f16 --world 8 --frames 5
   step vr_cfg2_w$w 300 python tools/exp_virtual_ranks.py --config cfg2_1m_sh3_1080p_f16 --world 8 --frames 5
   step vr2_cfg2_w$w 300 python tools/exp_virtual_ranks.py --config cfg2_1m_sh3_1080p_f16 --world 2 --frames 5

@@ -8,7 +8,7 @@ mkdir -p gpurun_out/kt
 for cfg in ${CFGS:-cfg2_1m_sh3_1080p_f16 cfg3_5m_sh3_4k_f16}; do
   rm -rf gpurun_out/kt/$cfg
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/kt/$cfg -o run -- \
-    python bench.py --config $cfg --steps 20 --warmup 3 --cpu-baseline 0 --parity 0 --orbit-steps 0 --inflight-steps 0 \
+    python bench.py --config $cfg --steps 20 --warmup 3 --cpu-baseline 0 --parity 0 --orbit-steps 0 --inflight-steps 0 --virtual-ranks 0 \
     > gpurun_out/kt/$cfg.log 2>&1 || { echo "rocprof failed for $cfg"; tail -5 gpurun_out/kt/$cfg.log; exit 1; }
   f=$(find gpurun_out/kt/$cfg -name '*kernel_stats.csv' | head -1)
   python3 - "$f" "$cfg" <<'PY' | tee gpurun_out/kt/$cfg.txt

@@ -7,7 +7,7 @@ cfg=${CFG:-cfg2_1m_sh3_1080p_f16}
 kern=${KERN:-k_blend_px}
 OUT=gpurun_out/pmcq
 rm -rf $OUT; mkdir -p $OUT
-CMD="python bench.py --config $cfg --steps 5 --warmup 2 --cpu-baseline 0 --parity 0 --orbit-steps 0 --inflight-steps 0"
+CMD="python bench.py --config $cfg --steps 5 --warmup 2 --cpu-baseline 0 --parity 0 --orbit-steps 0 --inflight-steps 0 --virtual-ranks 0"
 i=0
 for set in FETCH_SIZE WRITE_SIZE "SQ_INSTS_VALU SQ_WAVES GRBM_GUI_ACTIVE"; do
   i=$((i+1))

@@ -15,6 +15,9 @@
 #include "gsm_internal.h"
 #include "gsm_types.h"
 
+#ifndef GSM_COMPACT_LDS
+#define GSM_COMPACT_LDS 1
+#endif
 #ifndef GSM_BLEND_P1_TILES_PER_CU
 #define GSM_BLEND_P1_TILES_PER_CU 8u
 #endif
@@ -496,13 +499,25 @@ __global__ __launch_bounds__(NT) void k_blend_px(
                 h2 ac1[U1], om1[U1];
                 uint32_t rgc1[U1], bdc1[U1], rgn1[U1], bdn1[U1], opn1[U1];
                 u16x2 en1[U1];
+                // The records come from the LDS stage of the current batch (uniform-address reads, as
+                // in the half-tile walk; GSM_COMPACT_LDS) -- it holds batch bb here: the walk staged it,
+                // or staged the next one and the rotation above made that batch bb -- instead of five
+                // v_readlane per entry from the batch registers.
 #pragma unroll
                 for (uint32_t k = 0; k < U1; ++k) {  // prime the group at e
                     const uint32_t j = e - bb + k;
+#if GSM_COMPACT_LDS
+                    const uint4 ra = lrecA[wv][j];
+                    const uint32_t r2 = ra.z;
+                    const h2 pq = quad1(ra.x, ra.y, r2);
+                    rgc1[k] = ra.w;
+                    bdc1[k] = lrecB[wv][j];
+#else
                     const uint32_t r2 = __builtin_amdgcn_readlane(bA.z, j);
                     const h2 pq = quad1(__builtin_amdgcn_readlane(bA.x, j), __builtin_amdgcn_readlane(bA.y, j), r2);
                     rgc1[k] = __builtin_amdgcn_readlane(bA.w, j);
                     bdc1[k] = __builtin_amdgcn_readlane(bB, j);
+#endif
                     ac1[k] = __builtin_elementwise_min(splat_hi(as_h2(r2)) * lookup2(tbl, pq), C099);
                     om1[k] = ONE - ac1[k];
                 }
@@ -512,6 +527,25 @@ __global__ __launch_bounds__(NT) void k_blend_px(
                     {
                         const uint32_t jn = e + U1 - bb;  // 4..64
                         const bool nb = jn >= 64u;
+#if GSM_COMPACT_LDS
+                        if (nb) {  // the next group opens the next batch: stage it (this batch is all read)
+                            lrecA[wv][lane] = nA;
+                            lrecB[wv][lane] = nB;
+                            blend_wave_sync();
+                        }
+#pragma unroll
+                        for (uint32_t k = 0; k < U1; ++k) {
+                            const uint32_t j = (jn + k) & 63u;
+                            const uint4 ra = lrecA[wv][j];
+                            opn1[k] = ra.z;
+                            const h2 pq = quad1(ra.x, ra.y, opn1[k]);
+                            rgn1[k] = ra.w;
+                            bdn1[k] = lrecB[wv][j];
+                            const uint32_t pb = as_u32(pq);
+                            en1[k].x = tbl[pb & 0xFFFFu];
+                            en1[k].y = tbl[pb >> 16];
+                        }
+#else
                         const uint32_t sx = nb ? nA.x : bA.x, sy = nb ? nA.y : bA.y;
                         const uint32_t sz = nb ? nA.z : bA.z, sw = nb ? nA.w : bA.w;
                         const uint32_t sb = nb ? nB : bB;
@@ -526,6 +560,7 @@ __global__ __launch_bounds__(NT) void k_blend_px(
                             en1[k].x = tbl[pb & 0xFFFFu];
                             en1[k].y = tbl[pb >> 16];
                         }
+#endif
                     }
                     // stage 2: blend the current group
 #pragma unroll

@@ -22,6 +22,10 @@
 #include "gsm_internal.h"
 #include "gsm_types.h"
 
+#ifndef GSM_DF_EXEC_ALIVE
+#define GSM_DF_EXEC_ALIVE 1
+#endif
+
 namespace gsm {
 
 // ---------------------------------------------------------------------------
@@ -473,6 +477,11 @@ __device__ __forceinline__ void df_blend_eye_w(DfEyeState& st, bool alive, h2 p0
     const h2 ONE = {(h1)1.0f, (h1)1.0f};
     const h1 c099 = (h1)0.99;
     const h2 C099 = {c099, c099};
+#if GSM_DF_EXEC_ALIVE
+    // a lane whose eye is done keeps C and T (alpha 0 would leave the same bits: C + c * 0 == C,
+    // T * 1 == T): its updates run under an EXEC mask of the live lanes instead of zeroing its alphas
+    if (!alive) return;
+#endif
     const uint32_t b0 = df_u32(p0), b1 = df_u32(p1);
     df_u16x2 e0, e1;
     e0.x = tbl[b0 & 0xFFFFu];
@@ -482,10 +491,12 @@ __device__ __forceinline__ void df_blend_eye_w(DfEyeState& st, bool alive, h2 p0
     const h2 op = df_hi(df_h2(zw));
     h2 a0 = __builtin_elementwise_min(op * __builtin_bit_cast(h2, e0), C099);
     h2 a1 = __builtin_elementwise_min(op * __builtin_bit_cast(h2, e1), C099);
+#if !GSM_DF_EXEC_ALIVE
     if (!alive) {
         a0 = df_h2(0u);
         a1 = df_h2(0u);
     }
+#endif
     const h2 w0 = a0 * st.T[0], w1 = a1 * st.T[1];
     const h2 r = df_lo(df_h2(rg)), g = df_hi(df_h2(rg)), b = df_lo(df_h2(bw));
     st.Cr[0] = df_acc(st.Cr[0], r, w0);

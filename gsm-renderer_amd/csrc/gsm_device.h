@@ -137,21 +137,6 @@ __device__ __forceinline__ float load_harm(const void* __restrict__ h, size_t i)
 #ifndef GSM_SH_FMAMIX
 #define GSM_SH_FMAMIX 1
 #endif
-// The projection's inputs (world records, SH coefficients) are read once per frame: with
-// GSM_PROJ_NT they are loaded non-temporally, so they do not displace the projection's outputs
-// (records, bounds, counts) that the scatter and the blend read back.
-#ifndef GSM_PROJ_NT
-#define GSM_PROJ_NT 0
-#endif
-typedef unsigned int gsm_u32x4 __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ uint4 load_stream16(const uint4* p) {
-#if GSM_PROJ_NT
-    const gsm_u32x4 v = __builtin_nontemporal_load((const gsm_u32x4*)p);
-    return make_uint4(v.x, v.y, v.z, v.w);
-#else
-    return *p;
-#endif
-}
 // fp32(h) * b for the fp16 in the low / high half of w: one v_fma_mix_f32 (the fp16 operand widened
 // exactly inside the instruction, fma(h, b, -0) = the correctly rounded product) instead of a
 // v_cvt_f32_f16 and a v_mul_f32 -- the same bits as the contract's convert-then-multiply
@@ -224,7 +209,7 @@ __device__ __forceinline__ void sh_color(const void* __restrict__ harm, uint32_t
         uint32_t hw[24];  // coefficient 2k in the low half of hw[k], 2k + 1 in the high half
 #pragma unroll
         for (int q = 0; q < 6; ++q) {
-            uint4 v = load_stream16(p + q);
+            uint4 v = p[q];
             hw[4 * q] = v.x;
             hw[4 * q + 1] = v.y;
             hw[4 * q + 2] = v.z;

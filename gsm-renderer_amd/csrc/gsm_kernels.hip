@@ -57,7 +57,7 @@ __device__ __forceinline__ ProjOut project_gaussian(const void* __restrict__ wor
         float pos[3], scale[3], rot[4], opacity;
         if constexpr (HALF) {
             const uint4* wp = (const uint4*)((const PackedWorldGaussianHalf*)world + gid);
-            uint4 w0 = load_stream16(wp), w1 = load_stream16(wp + 1);
+            uint4 w0 = wp[0], w1 = wp[1];
             pos[0] = __builtin_bit_cast(float, w0.x);
             pos[1] = __builtin_bit_cast(float, w0.y);
             pos[2] = __builtin_bit_cast(float, w0.z);

@@ -6,13 +6,15 @@ radix sort -> tile headers -> front-to-back fp16 blend) over one synthetic scene
 resident in HBM.  Default workload = BASELINE.json configs[1]: 1M gaussians, SH3,
 1920x1080, PackedWorldGaussianHalf (fp16).
 
-N>1 (torch.distributed.run, one rank per GPU, RCCL over xGMI), --multi:
+N>1 (torch.distributed.run, one rank per GPU), --multi:
   alltoall (default): the whole partitioned frame inside libgsm_amd.so
-      (gsm_multigpu_render over torch's RCCL communicator): rank r projects ids
-      [r*N/n, (r+1)*N/n) once, per-slab counts are all-gathered, each 48-byte record is
-      written straight into its slab owner's receive buffer over xGMI, every rank renders its
-      band of tile rows; if any rank cannot create that frame, every rank falls back to the
-      RCCL all-to-all of gsm_amd.exchange ("multi_fallback" in the line);
+      (gsm_multigpu_render; exchange handles all-gathered once at set-up over torch.distributed,
+      no collective in a frame): rank r projects ids [r*N/n, (r+1)*N/n) once, its per-slab counts
+      are stored into every rank's count matrix by the scan kernel, each 48-byte record is written
+      straight into its slab owner's receive buffer over xGMI, every rank renders its band of tile
+      rows into rank 0's frame, ordered by device-side flag barriers the producing kernels arrive
+      at themselves; if any rank cannot create that frame, every rank falls back to
+      the RCCL all-to-all of gsm_amd.exchange ("multi_fallback" in the line);
   replicas: every rank projects all gaussians and keeps its band's assignments.
 Either way the bands are gathered on rank 0 inside the timed step.  The frame is fixed as N
 grows -> "scaling": "strong".  The line also carries "config4": BASELINE configs[3], the 4K
@@ -90,7 +92,8 @@ def parse():
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--config", default="cfg2_1m_sh3_1080p_f16")
     p.add_argument("--cpu-baseline", type=int, default=1, help="time the C oracle (rank 0, N=1)")
-    p.add_argument("--cpu-threads", type=int, default=16)
+    p.add_argument("--cpu-threads", type=int, default=0,
+                   help="oracle threads of cpu_baseline (0: every CPU of this process's affinity mask)")
     p.add_argument("--cpu-one-thread", type=int, default=1, help="also time one oracle frame on 1 thread (<= 1M)")
     p.add_argument("--orbit-steps", type=int, default=50,
                    help="moving-camera frames timed after the static ones (single GPU, mono); 0 = off")
@@ -158,7 +161,9 @@ def virtual_ranks_entry(world: int):
     return {"workload": "cfg3_5m_sh3_4k_f16 frame (BASELINE configs[3]) over %d virtual ranks" % world,
             "world": world, "device_frame_ms": d["device_frame_ms"], "max_phase_ms": d["max_phase_ms"],
             "one_gpu_frame_ms": d.get("one_gpu_frame_ms"), "device_speedup": d.get("device_speedup"),
-            "barrier_timeouts": d.get("timeouts"),
+            "barrier_timeouts": d.get("timeouts"), "xgmi_model": d.get("xgmi_model"),
+            "modelled_speedup_with_xgmi": (round(d["one_gpu_frame_ms"] / d["xgmi_model"]["modelled_frame_ms"], 3)
+                                           if d.get("one_gpu_frame_ms") and d.get("xgmi_model") else None),
             "note": "each rank's phases run alone on this GPU (an upper bound for a rank's own GPU); the pushes "
                     "and the gathered pixels stay local (no xGMI time); device_speedup = one-renderer frame / "
                     "per-rank device frame"}
@@ -234,11 +239,11 @@ def main():
     stream = torch.cuda.current_stream(dev)
 
     alltoall = (world_size > 1 or force_multi) and args.multi == "alltoall"
-    # N > 1 over RCCL: the whole partitioned frame runs inside libgsm_amd.so (gsm_multigpu_render,
-    # include/gsm_multigpu.h): counts all-gathered on the device, records pushed to their slab
-    # owners over xGMI, bands sent to rank 0 -- no host round trip in a frame.  The gloo rehearsal
-    # (BENCH_DIST_BACKEND=gloo, several ranks on one GPU) has no RCCL communicator and moves the
-    # records through gsm_amd.exchange instead.
+    # N > 1: the whole partitioned frame runs inside libgsm_amd.so (gsm_multigpu_render,
+    # include/gsm_multigpu.h): counts stored into every rank's count matrix by the scan kernel,
+    # records pushed to their slab owners over xGMI, bands written into rank 0's frame by the slab
+    # blends, device flag barriers -- no host round trip and no collective in a frame (the exchange
+    # handles travel once, at set-up, over torch.distributed with any backend).
     native_multi = alltoall
     multi_fallback = None
     if native_multi:
@@ -377,8 +382,7 @@ def main():
         if rank == 0:
             sys.path.insert(0, os.path.join(ROOT, "oracle"))
             import oracle as O  # parity checker only
-            ref = O.render(world_np, harm_np, sh, cam_d, W, H, max_gaussians=n,
-                           nthreads=max(1, min(args.cpu_threads, os.cpu_count() or 1)))
+            ref = O.render(world_np, harm_np, sh, cam_d, W, H, max_gaussians=n, nthreads=min(16, cpu_threads(args)))
             multi_parity = bool(np.array_equal(mg.copy_frame(W, H), ref["color"]))
     # BASELINE config 4 (the 4K scene of config 3 on N GPUs): timed the same way after `value`
     multi_4k = None
@@ -436,7 +440,7 @@ def main():
     if world_size == 1 and not native_multi and (args.parity or args.cpu_baseline):
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import oracle as O  # CPU baseline + parity checker only
-        threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+        threads = cpu_threads(args)
         views = [scenes.make_camera(W, H, -stereo), scenes.make_camera(W, H, stereo)] if stereo else [cam_d]
         times = []
         refs = None
@@ -463,6 +467,12 @@ def main():
             cpu = cpu_baseline_entry(med, threads, f"{reps} full frames of {args.config} ({n} gaussians, "
                                      f"{len(views)} view(s) of {W}x{H}) with the C oracle (oracle/gsm_oracle.c, "
                                      f"pthreads), median {med:.2f} s/frame", refs[-1]["times"])
+            if threads != 16:  # the r01-r03 figure (16 threads), for comparison
+                t = time.perf_counter()
+                O.render(world_np, harm_np, sh, cam_d, W, H, max_gaussians=n, nthreads=16)
+                t16 = time.perf_counter() - t
+                cpu["threads_16"] = {"value": 1.0 / t16, "unit": "frames/s", "cores": 16,
+                                     "sample": f"1 full frame of {args.config}, 16 threads, {t16:.2f} s"}
             if args.cpu_one_thread and not stereo and n <= 1_000_000:
                 t = time.perf_counter()
                 O.render(world_np, harm_np, sh, cam_d, W, H, max_gaussians=n, nthreads=1)
@@ -636,10 +646,39 @@ def cpu_model():
     return None
 
 
+def cpu_threads(args) -> int:
+    """Oracle threads of cpu_baseline: --cpu-threads, or every CPU this process may run on."""
+    if args.cpu_threads > 0:
+        return args.cpu_threads
+    try:
+        return max(1, len(os.sched_getaffinity(0)))
+    except (AttributeError, OSError):
+        return max(1, os.cpu_count() or 1)
+
+
+def cgroup_cpu_quota():
+    """CPUs' worth of time the cgroup grants (cpu.max quota / period), None when unlimited."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        return None if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        return None
+
+
 def cpu_baseline_entry(median_s, threads, sample, stage_times):
-    return {"value": 1.0 / median_s, "unit": "frames/s", "cores": threads, "kind": "port",
-            "host_cpus": os.cpu_count(), "cpu_model": cpu_model(), "sample": sample,
-            "stages_s": {k: round(v, 4) for k, v in stage_times.items()}}
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        affinity = None
+    quota = cgroup_cpu_quota()
+    out = {"value": 1.0 / median_s, "unit": "frames/s", "cores": threads, "kind": "port",
+           "host_cpus": os.cpu_count(), "affinity_cpus": affinity, "cgroup_cpu_quota": quota,
+           "cpu_model": cpu_model(), "sample": sample, "stages_s": {k: round(v, 4) for k, v in stage_times.items()}}
+    if quota is not None and quota < threads:
+        out["note"] = (f"{threads} oracle threads (every CPU of the affinity mask) under a cgroup quota of {quota} "
+                       f"CPUs: the box grants this process {quota} CPUs' worth of time")
+    return out
 
 
 def run_depthfirst(args, c, world_np, harm_np, world, harm, dev):
@@ -705,7 +744,7 @@ def run_depthfirst(args, c, world_np, harm_np, world, harm, dev):
     if args.parity or args.cpu_baseline:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import oracle as O  # CPU baseline + parity checker only
-        threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+        threads = cpu_threads(args)
         times, ref = [], None
         for _ in range(2 if args.cpu_baseline else 1):
             t = time.perf_counter()

@@ -88,7 +88,7 @@ __global__ __launch_bounds__(NT) void k_blend_px(
     const uint32_t* __restrict__ order, uint16_t* __restrict__ unitCost,
     unsigned long long* __restrict__ trace, const uint32_t* __restrict__ half0,
     const uint32_t* __restrict__ half1, const uint32_t* __restrict__ halfCount, uint32_t tileCount,
-    uint32_t* __restrict__ costMax, uint32_t rowBegin, uint32_t rowStride) {
+    uint32_t* __restrict__ costMax, uint32_t rowBegin, uint32_t rowStride, MgArrive arrive) {
     static_assert(P == 1 || P == 2, "pairs per lane: quadrant or half-tile units (half-tile lists)");
     static_assert(!COMPACT || P == 2, "compaction: half tiles");
     constexpr uint32_t U = 4 / P;  // entries per pipeline group
@@ -624,6 +624,10 @@ __global__ __launch_bounds__(NT) void k_blend_px(
         qi = gridWaves + stripe + stripes * __builtin_amdgcn_readfirstlane(nextQ);
     }
     if (unitCost && lane == 0 && waveMax) atomicMax(&costMax[(blockIdx.x * NW + wv) % kCostMaxSlots], waveMax);
+    // multi-GPU frame gathered on rank 0 (gsm_multigpu.hip): the pixels this wave stored into rank
+    // 0's frame are released at system scope, and the wave arrives at barrier 2 (the last one raises
+    // the flags) -- every wave of the grid arrives exactly once, here
+    if (arrive.done) mg_arrive_wave(arrive);
 }
 
 
@@ -657,7 +661,7 @@ static int blend_waves_per_wg(uint32_t numTiles, int numCUs) {
 // SIMD (flags bit 2), later units' priority rising with the age of their walk (flags bit 1).
 void launch_blend(const FrameGeometry& g, const DeviceArena& A, void* color,
                   size_t colorPitch, void* depth, size_t depthPitch, int numCUs, bool costOrder, int colorFormat,
-                  hipStream_t s, int wavesOverride, int claim) {
+                  hipStream_t s, int wavesOverride, int claim, const MgArrive* arrive) {
     // local tile ids: tile t = k * tilesX + tx of the renderer's row k (pixel row rowBegin + k * rowStride)
     const uint32_t numTiles = g.rowCount * g.tilesX;
     if (numTiles == 0) return;
@@ -674,12 +678,17 @@ void launch_blend(const FrameGeometry& g, const DeviceArena& A, void* color,
     uint32_t grid = (units + (uint32_t)waves - 1) / (uint32_t)waves;
     if (grid > (uint32_t)numCUs) grid = (uint32_t)numCUs;
     const uint32_t* order = costOrder ? A.unitOrder : nullptr;
+    MgArrive ar{};
+    if (arrive) {
+        ar = *arrive;
+        ar.total = grid * (uint32_t)waves;  // every wave arrives once, at its exit
+    }
 #define GSM_LAUNCH_BLEND(NTH, PP, CMP)                                                                       \
     hipLaunchKernelGGL((k_blend_px<NTH, PP, CMP>), dim3(grid), dim3(NTH), 0, s, A.tileStart, A.rec, \
                        A.expTable, A.tileQueue, t0, numTiles, g.tilesX, g.width, g.height,          \
                        (uint8_t*)color, colorPitch, (uint8_t*)depth, depthPitch, flags, order, A.unitCost,  \
                        A.blendTrace, A.halfVals[0], A.halfVals[1], A.halfCount, g.tileCount, A.costMax, \
-                       g.rowBegin, g.rowStride)
+                       g.rowBegin, g.rowStride, ar)
     // half tiles compact to one pair per lane once <= 16 of their 32 groups are alive
     if (P == 1) {
         if (waves == 16) GSM_LAUNCH_BLEND(1024, 1, false);

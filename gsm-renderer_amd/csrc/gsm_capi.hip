@@ -240,7 +240,7 @@ gsm_status gsm_debug_partition_push(gsm_renderer* r, void* stream, uint32_t worl
         peers.recv[p] = (gsm::SplatRecord*)recv_buffers[p];
         peers.cap[p] = r->impl->maxGaussians();  // (gsm_debug.h: each holds max_gaussians records)
     }
-    return r->impl->partitionPush((hipStream_t)stream, world, rank, d_counts, peers, d_recv_count);
+    return r->impl->partitionPush((hipStream_t)stream, world, rank, d_counts, peers, d_recv_count, gsm::MgArrive{});
 }
 
 gsm_status gsm_debug_render_records_device_count(gsm_renderer* r, void* stream, const void* records,

@@ -56,6 +56,65 @@ struct PartitionBuffers {
     uint32_t* blockSlabCounts = nullptr;  // [kMaxSlabs * blocks]
 };
 
+// ---------------------------------------------------------------------------
+// Multi-GPU frame (gsm_multigpu.hip): memory model of the exchange.
+// A producing kernel arrives at a barrier itself: every unit of it that stored exchange data (a
+// wave, or a workgroup after a barrier) ends with a SYSTEM-scope release -- `buffer_wbl2 sc0 sc1`
+// writes back its XCD's L2, the wait makes it complete -- and one device-scope add to the rank's
+// arrival counter; the unit whose add completes the count raises this rank's flag word of the
+// barrier in every rank's control block (system-scope stores) and re-arms the counter.  Every
+// consumer load of exchange data is system-coherent (`sc0 sc1`: ld_sys32 / ld_sys128 below), so
+// no L1 or L2 line that predates the flag can serve it, on any XCD of any GPU.
+// ---------------------------------------------------------------------------
+struct MgArrive {
+    uint32_t* flag[kMaxSlabs];  // this rank's word of the barrier in rank p's control block (peer mappings)
+    uint32_t* done;             // this rank's arrival counter of the barrier (own memory, 0 between frames)
+    uint32_t total;             // arriving units of the launch
+    uint32_t epoch;             // the frame number the flags receive
+    uint32_t world;
+};
+
+// One arriving unit: called by every lane of ONE wave, after every store the unit signals for
+// (a workgroup arriving as one unit: every wave's `s_waitcnt vmcnt(0)`, then a workgroup barrier,
+// then one wave calls this).
+__device__ __forceinline__ void mg_arrive_wave(const MgArrive& a) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");      // system scope: buffer_wbl2 sc0 sc1
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the write-back is complete before the add
+    uint32_t last = 0;
+    if ((threadIdx.x & 63u) == 0)
+        last = __hip_atomic_fetch_add(a.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == a.total - 1u ? 1u : 0u;
+    if (__builtin_amdgcn_readfirstlane(last)) {
+        // every other unit released its stores before its add: acquire them, release to the peers
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "");
+        const uint32_t lane = threadIdx.x & 63u;
+        if (lane == 0) __hip_atomic_store(a.done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (lane < a.world) __hip_atomic_store(a.flag[lane], a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+// a workgroup of NT threads arriving as one unit (see mg_arrive_wave); ends the kernel's use of it
+__device__ __forceinline__ void mg_arrive_block(const MgArrive& a) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x < 64u) mg_arrive_wave(a);
+}
+// k_part_scan's count publication: row `rank` of rank p's count matrix (this frame's parity), and
+// the arrival at barrier 0 (arrive.done == null: no publication, the send-buffer path)
+struct CountPublish {
+    uint32_t* row[kMaxSlabs];
+    MgArrive arrive;
+};
+// system-coherent loads of exchange data (sc0 sc1: no cached copy can answer them)
+__device__ __forceinline__ uint32_t ld_sys32(const uint32_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+// 16-B word i of a wave-uniform base of `bytes` bytes
+__device__ __forceinline__ uint4 ld_sys128(const void* base, uint32_t bytes, uint32_t i) {
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)bytes, 0x00020000);
+    const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)(i * 16u), 0, 17 /* sc0 | sc1 */);
+    return make_uint4(v[0], v[1], v[2], v[3]);
+}
+
 // Device buffers of one renderer (the GlobalViewResources analogue, GlobalResources.swift:6-362).
 struct DeviceArena {
     GaussianRenderData* renderData = nullptr;  // [maxG]
@@ -143,10 +202,11 @@ void launch_partition(bool halfInput, uint32_t shDegree, const void* world, cons
 // (args.schedUnits > 0: one extra workgroup orders the blend units of the renderer's own rows, A)
 void launch_partition_counts(bool halfInput, uint32_t shDegree, const void* world, const void* harmonics,
                              const ProjectArgs& args, const SlabTable& slabs, const PartitionBuffers& B,
-                             const float2* sincos, uint32_t* sendCounts, const DeviceArena& A, hipStream_t stream);
+                             const float2* sincos, uint32_t* sendCounts, const DeviceArena& A,
+                             const CountPublish& publish, hipStream_t stream);
 void launch_partition_push(const ProjectArgs& args, uint32_t world, uint32_t rank, const PartitionBuffers& B,
                            const uint32_t* counts, const SlabPeers& peers, uint32_t* recvCount, const SlabTable& slabs,
-                           hipStream_t stream);
+                           const MgArrive& arrive, hipStream_t stream);
 // received records -> per-gaussian arrays + tile counts of the renderer's rows (replaces project)
 void launch_records_in(const void* records, const ProjectArgs& args, const DeviceArena& A,
                        hipStream_t stream, const uint32_t* devCount = nullptr);
@@ -169,7 +229,8 @@ void launch_headers(const uint32_t* sortedKeys, const FrameGeometry& geo, const 
 // front-to-back fp16 blend + clear (GlobalShaders.metal:140-154, 1030-1187)
 void launch_blend(const FrameGeometry& geo, const DeviceArena& A,
                   void* color, size_t colorPitch, void* depth, size_t depthPitch, int numCUs,
-                  bool costOrder, int colorFormat, hipStream_t stream, int waves = 0, int claim = 1);
+                  bool costOrder, int colorFormat, hipStream_t stream, int waves = 0, int claim = 1,
+                  const MgArrive* arrive = nullptr);
 // blend kernel shape: pixel pairs per lane (0 = quadrant kernel) and blend units per tile
 int blend_pairs_per_lane(uint32_t numTiles, int numCUs);
 uint32_t blend_units_per_tile(uint32_t numTiles, int numCUs);

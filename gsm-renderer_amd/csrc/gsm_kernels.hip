@@ -553,9 +553,12 @@ __global__ __launch_bounds__(kProjectBlock) void k_project_part(
     }
 }
 
-// one workgroup per slab: exclusive scan of the slab's block counts (in place) and its total
+// one workgroup per slab: exclusive scan of the slab's block counts (in place) and its total.
+// Multi-GPU frame (pub.arrive.done != null): the total also goes into column `slab` of row `rank` of
+// every rank's count matrix (pub.row[p], peer mappings), and the workgroups arrive at barrier 0 --
+// the count publication needs no kernel of its own (gsm_multigpu.hip)
 __global__ __launch_bounds__(1024) void k_part_scan(uint32_t* __restrict__ blockSlabCounts, uint32_t numBlocks,
-                                                    uint32_t* __restrict__ sendCounts) {
+                                                    uint32_t* __restrict__ sendCounts, CountPublish pub) {
     __shared__ uint32_t lds[1024 / 64];
     const uint32_t sl = blockIdx.x;
     uint32_t* row = blockSlabCounts + (size_t)sl * numBlocks;
@@ -570,6 +573,11 @@ __global__ __launch_bounds__(1024) void k_part_scan(uint32_t* __restrict__ block
         __syncthreads();
     }
     if (threadIdx.x == 0) sendCounts[sl] = carry;
+    if (pub.arrive.done && threadIdx.x < 64u) {  // (carry is uniform over the workgroup)
+        if (threadIdx.x < pub.arrive.world)
+            __hip_atomic_store(pub.row[threadIdx.x] + sl, carry, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        mg_arrive_wave(pub.arrive);  // wave 0 made every store of the workgroup that crosses ranks
+    }
 }
 
 // Writes the block's records of every slab it meets as one contiguous run of the destination
@@ -672,12 +680,14 @@ __global__ __launch_bounds__(kProjectBlock) void k_records_in(
     const uint32_t n = devCount ? min(*devCount, P.count) : P.count;
     if (blk * kProjectBlock >= n) return;  // (uniform) nothing here; the scan stops at the count
     {
+        // system-coherent 16-B loads (ld_sys128): on the multi-GPU path the records were stored by the
+        // peers' k_part_push over xGMI; no L1 / L2 line of an earlier frame may answer
         const uint32_t words = 3u * (min(n - blk * kProjectBlock, (uint32_t)kProjectBlock));
-        const uint4* src = (const uint4*)(in + (size_t)blk * kProjectBlock);
+        const SplatRecord* src = in + (size_t)blk * kProjectBlock;
 #pragma unroll
         for (uint32_t j = 0; j < 3; ++j) {
             const uint32_t i = threadIdx.x + j * kProjectBlock;
-            if (i < words) sIn[i] = src[i];
+            if (i < words) sIn[i] = ld_sys128(src, words * 16u, i);
         }
     }
     __syncthreads();
@@ -734,6 +744,23 @@ __global__ __launch_bounds__(kProjectBlock) void k_records_in(
 //    (prefix sum: TwoPassTileAssignEncoder.swift:91-196; clamp GlobalShaders.metal:694-712)
 // ---------------------------------------------------------------------------
 constexpr int kScanThreads = 1024;
+// Exclusive scan of one 64-bit value per thread (< 2^37 each) over the workgroup, exact: one 32-bit
+// block scan while every value is < 2^22 (1024 of them stay below 2^32), otherwise two 32-bit scans of
+// the high (>> 16, < 2^21 each) and low 16-bit parts.  A frame far over its capacity thus never wraps
+// its total below maxAssignments, and the overflow flag is raised.  Ends with the lds free.
+__device__ __forceinline__ uint64_t scan_exact64(uint64_t v, uint32_t* lds, uint64_t* total) {
+    if (!__syncthreads_or(v >= (1ull << 22))) {
+        uint32_t t32;
+        const uint32_t off = block_exclusive_scan<kScanThreads>((uint32_t)v, lds, &t32);
+        *total = t32;
+        return off;
+    }
+    uint32_t hiTot, loTot;
+    const uint32_t hiOff = block_exclusive_scan<kScanThreads>((uint32_t)(v >> 16), lds, &hiTot);
+    const uint32_t loOff = block_exclusive_scan<kScanThreads>((uint32_t)(v & 0xFFFFu), lds, &loTot);
+    *total = ((uint64_t)hiTot << 16) + loTot;
+    return ((uint64_t)hiOff << 16) + loOff;
+}
 __global__ __launch_bounds__(kScanThreads) void k_scan_blocks(uint32_t* __restrict__ sums,
                                                               uint32_t nb, uint32_t maxAssignments,
                                                               TileAssignmentHeader* __restrict__ hdr,
@@ -766,12 +793,8 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_blocks(uint32_t* __restri
         uint64_t local = 0;
 #pragma unroll
         for (uint32_t r = 0; r < kV; ++r) local += (uint64_t)v[r].x + v[r].y + v[r].z + v[r].w;
-        // run totals fit 32 bits unless the frame overflows anyway (clamped below); the block scan
-        // takes them saturated, the carry is exact
-        uint32_t tot;
-        const uint32_t off = block_exclusive_scan<kScanThreads>(local > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)local,
-                                                                lds, &tot);
-        uint64_t run = off;
+        uint64_t tot;
+        uint64_t run = scan_exact64(local, lds, &tot);
 #pragma unroll
         for (uint32_t r = 0; r < kV; ++r) {
             const uint32_t i = b0 + 4u * r;
@@ -807,9 +830,8 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_blocks(uint32_t* __restri
         for (uint32_t r = 0; r < kScanRows; ++r) {
             const uint32_t row0 = base + r * kRow;
             if (row0 >= nb) break;
-            uint32_t tot;
-            const uint32_t off = block_exclusive_scan<kScanThreads>(v[r].x + v[r].y + v[r].z + v[r].w, lds, &tot);
-            uint64_t run = carry + off;
+            uint64_t tot;
+            uint64_t run = carry + scan_exact64((uint64_t)v[r].x + v[r].y + v[r].z + v[r].w, lds, &tot);
             const uint32_t in[4] = {v[r].x, v[r].y, v[r].z, v[r].w};
             uint32_t o[4];
 #pragma unroll
@@ -1026,17 +1048,19 @@ __global__ __launch_bounds__(256) void k_tile_starts(const uint32_t* __restrict_
 __global__ __launch_bounds__(kProjectBlock) void k_part_push(
     const SplatRecord* __restrict__ records, const uint32_t* __restrict__ masks, uint32_t count,
     uint32_t world, uint32_t rank, const uint32_t* __restrict__ blockSlabOffsets,
-    const uint32_t* __restrict__ counts, SlabPeers peers, uint32_t* __restrict__ recvCount, SlabTable slabs) {
+    const uint32_t* __restrict__ counts, SlabPeers peers, uint32_t* __restrict__ recvCount, SlabTable slabs,
+    MgArrive arrive) {
     __shared__ uint32_t dstOff[kMaxSlabs];
     const uint32_t gid = blockIdx.x * kProjectBlock + threadIdx.x;
+    // the count matrix was stored by every rank's k_part_scan (system-coherent loads, no cached copy)
     if (threadIdx.x < world) {
         uint32_t before = 0;
-        for (uint32_t r = 0; r < rank; ++r) before += counts[r * world + threadIdx.x];
+        for (uint32_t r = 0; r < rank; ++r) before += ld_sys32(counts + r * world + threadIdx.x);
         dstOff[threadIdx.x] = before;
     }
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         uint32_t mine = 0;
-        for (uint32_t r = 0; r < world; ++r) mine += counts[r * world + rank];
+        for (uint32_t r = 0; r < world; ++r) mine += ld_sys32(counts + r * world + rank);
         *recvCount = min(mine, peers.cap[rank]);
     }
     const uint32_t mask = gid < count ? masks[gid] : 0u;
@@ -1050,6 +1074,8 @@ __global__ __launch_bounds__(kProjectBlock) void k_part_push(
             const uint64_t at = (uint64_t)dstOff[sl] + blockSlabOffsets[(size_t)sl * gridDim.x + blockIdx.x];
             return at < peers.cap[sl] ? (uint64_t)peers.cap[sl] - at : 0ull;
         });
+    // every workgroup arrives once (barrier 1) after all its waves' record stores
+    if (arrive.done) mg_arrive_block(arrive);
 }
 
 // ---------------------------------------------------------------------------
@@ -1184,30 +1210,35 @@ void launch_partition(bool halfInput, uint32_t deg, const void* world, const voi
     pa.schedUnits = 0;  // (the send-buffer path leaves the schedule to the receiving renderer)
     if (halfInput) launch_project_part_t<true>(deg, world, harm, pa, slabs, B, sincos, nullptr, s);
     else launch_project_part_t<false>(deg, world, harm, pa, slabs, B, sincos, nullptr, s);
-    hipLaunchKernelGGL(k_part_scan, dim3(slabs.n), dim3(1024), 0, s, B.blockSlabCounts, blocks, sendCounts);
+    hipLaunchKernelGGL(k_part_scan, dim3(slabs.n), dim3(1024), 0, s, B.blockSlabCounts, blocks, sendCounts,
+                       CountPublish{});
     hipLaunchKernelGGL(k_part_pack, dim3(blocks), dim3(kProjectBlock), 0, s, B.records, B.masks, a.count, slabs,
                        B.blockSlabCounts, sendCounts, (SplatRecord*)send, capacity);
 }
 
 void launch_partition_counts(bool halfInput, uint32_t deg, const void* world, const void* harm, const ProjectArgs& a,
                              const SlabTable& slabs, const PartitionBuffers& B, const float2* sincos,
-                             uint32_t* sendCounts, const DeviceArena& A, hipStream_t s) {
+                             uint32_t* sendCounts, const DeviceArena& A, const CountPublish& pub, hipStream_t s) {
     const uint32_t blocks = (a.count + kProjectBlock - 1) / kProjectBlock;
-    if (blocks == 0) hipMemsetAsync(sendCounts, 0, slabs.n * sizeof(uint32_t), s);
-    if (blocks == 0 && a.schedUnits == 0) return;  // (no ids: the schedule block may still run)
-    if (halfInput) launch_project_part_t<true>(deg, world, harm, a, slabs, B, sincos, &A, s);
-    else launch_project_part_t<false>(deg, world, harm, a, slabs, B, sincos, &A, s);
-    if (blocks == 0) return;
-    hipLaunchKernelGGL(k_part_scan, dim3(slabs.n), dim3(1024), 0, s, B.blockSlabCounts, blocks, sendCounts);
+    if (blocks > 0 || a.schedUnits > 0) {  // (no ids: the schedule block may still run)
+        if (halfInput) launch_project_part_t<true>(deg, world, harm, a, slabs, B, sincos, &A, s);
+        else launch_project_part_t<false>(deg, world, harm, a, slabs, B, sincos, &A, s);
+    }
+    // with no ids the scan still runs: zero counts, published, and the arrival at barrier 0
+    CountPublish p = pub;
+    if (p.arrive.done) p.arrive.total = slabs.n;
+    hipLaunchKernelGGL(k_part_scan, dim3(slabs.n), dim3(1024), 0, s, B.blockSlabCounts, blocks, sendCounts, p);
 }
 
 void launch_partition_push(const ProjectArgs& a, uint32_t world, uint32_t rank, const PartitionBuffers& B,
                            const uint32_t* counts, const SlabPeers& peers, uint32_t* recvCount, const SlabTable& slabs,
-                           hipStream_t s) {
+                           const MgArrive& arrive, hipStream_t s) {
     const uint32_t blocks = (a.count + kProjectBlock - 1) / kProjectBlock;
-    // (no ids here: one block still takes the receive count from the matrix)
+    // (no ids here: one block still takes the receive count from the matrix and arrives)
+    MgArrive ar = arrive;
+    ar.total = blocks ? blocks : 1u;
     hipLaunchKernelGGL(k_part_push, dim3(blocks ? blocks : 1u), dim3(kProjectBlock), 0, s, B.records, B.masks, a.count,
-                       world, rank, B.blockSlabCounts, counts, peers, recvCount, slabs);
+                       world, rank, B.blockSlabCounts, counts, peers, recvCount, slabs, ar);
 }
 
 void launch_records_in(const void* records, const ProjectArgs& a, const DeviceArena& A, hipStream_t s,

@@ -1,30 +1,39 @@
 // gsm_multigpu.hip -- one frame partitioned across the GPUs of a node by screen slab, behind the
 // C ABI (include/gsm_multigpu.h).
 //
-// One process and one GlobalRenderer per GPU.  Every rank owns one uncached "exchange"
+// One process and one GlobalRenderer per GPU.  Every rank owns one fine-grained "exchange"
 // allocation; at set-up the ranks open each other's (IPC handles exchanged by the caller, or over
 // an RCCL communicator).  Per frame, enqueue-only on the caller's stream, no host synchronisation
 // and no collective library:
 //   phase 0  project the rank's id range once and count its records per destination slab
-//            (GlobalRenderer::partitionCounts: k_project_part, k_part_scan); k_mg_sync writes the
-//            counts into row `rank` of every rank's count matrix and arrives at barrier 0;
+//            (GlobalRenderer::partitionCounts: k_project_part, k_part_scan); k_part_scan's workgroup
+//            for slab s stores its total into column s of row `rank` of every rank's count matrix and
+//            arrives at barrier 0;
 //   phase 1  wait at barrier 0; k_part_push: every record goes straight from the projection into
 //            its slab owner's receive buffer, at the offset the count matrix gives -- rank order, so
-//            the receiver's records are in ascending id order (the stable sort's tie order); arrive
-//            at barrier 1;
+//            the receiver's records are in ascending id order (the stable sort's tie order); its
+//            workgroups arrive at barrier 1;
 //   phase 2  wait at barrier 1; the owner renders its tile rows from the received records, their
-//            count read on the device; when gathering, the blend writes its pixels straight into
-//            rank 0's frame, and the rank arrives at barrier 2;
+//            count read on the device; when gathering, the blend writes its pixels (colour, and
+//            depth when asked) straight into rank 0's frame and its waves arrive at barrier 2;
 //   phase 3  rank 0 waits at barrier 2 for every slab (then copies the frame to the caller's
-//            gather target unless the caller renders into the library frame itself).
-// A barrier is an arrival and a wait, each one 64-lane workgroup: the arrival is a system-scope
-// release and one flag word per peer written with the frame number (lane p -> rank p's flag of this
-// rank); the wait is lane p spinning, bounded by a timeout, on this rank's flag of rank p, and a
-// system-scope acquire.  Flags, counts, records and the
-// gathered frame all live in uncached memory, so the owner's reads never meet a stale L2 line of
-// a peer's write.  Ordering across frames: a rank arrives at frame k + 1's barrier 0 only after
-// its stream finished frame k, so no record or pixel of frame k + 1 is written into a rank before
-// it is done reading frame k; the count matrix is double-buffered by frame parity.
+//            targets unless the caller renders into the library frame itself).
+//
+// Memory model (gsm_internal.h MgArrive): the kernels that store exchange data arrive
+// at the barrier themselves -- every storing unit releases at system scope (`buffer_wbl2 sc0 sc1` on
+// its own XCD's L2, then the wait), then adds to the rank's arrival counter, and the last unit raises
+// the rank's flag in every rank's control block.  A wait is k_mg_sync: kSyncWaitBlocks workgroups,
+// each polling the W flags (relaxed system-scope loads, bounded by a timeout) and then acquiring at
+// system scope, so every XCD's L1/L2 drops what it held of the exchange memory; every consumer load
+// of exchange data is system-coherent besides (ld_sys32 / ld_sys128).  Nothing relies on the fence
+// scope HIP puts between two kernels.
+// Errors: a rank whose frame is refused (check: validated before anything is enqueued) still
+// performs every barrier of the frame, arriving with the failure bit set and zero counts, so the
+// epochs of all ranks stay aligned; a peer waiting on such an arrival counts it (peer_errors) and
+// the next frame is unaffected.  A wait that times out skips the remaining waits of that frame only.
+// Ordering across frames: a rank arrives at frame k + 1's barrier 0 only after its stream finished
+// frame k, so no record or pixel of frame k + 1 is written into a rank before it is done reading
+// frame k; the count matrix is double-buffered by frame parity.
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
@@ -69,12 +78,15 @@ const Rccl& rccl() {
 // exchange allocation layout (bytes from its base)
 constexpr uint32_t kBarriers = 3;
 constexpr size_t kFlagWords = 0;      // u32 flag[kBarriers][kMaxSlabs]: [b][src] = last frame src reached b
-constexpr size_t kStatusWord = 64;    // u32: this rank's barrier timeouts
+constexpr size_t kStatusWord = 64;    // u32 [0] barrier timeouts, [1] failed peer arrivals, [2] epoch of the last timeout
 constexpr size_t kCountsWord = 256;   // u32 counts[2][kMaxSlabs * kMaxSlabs] (frame parity; row = source)
 constexpr size_t kRecordsOff = 4096;  // SplatRecord[capacity]
 static_assert(kFlagWords + kBarriers * kMaxSlabs <= kStatusWord, "flags before the status word");
+constexpr uint32_t kFailBit = 0x80000000u;  // a flag's epoch with this bit: that rank's frame failed
+constexpr uint32_t kEpochMask = 0x7FFFFFFFu;
+constexpr uint32_t kSyncWaitBlocks = 32;    // workgroups of a wait: >= 4 per XCD (blocks are dealt round robin)
 constexpr uint32_t kHandleMagic = 0x58534D47u;  // "GMSX"
-constexpr uint32_t kHandleVersion = 1;
+constexpr uint32_t kHandleVersion = 2;
 
 struct ExchangeFields {
     uint32_t magic, version;
@@ -84,7 +96,10 @@ struct ExchangeFields {
     int32_t pid, device;
     uint64_t base;      // device address in the owner's process (a same-process peer uses it directly)
     uint64_t bytes;
-    uint64_t frameOff;  // rank 0: the gathered frame; 0 elsewhere
+    uint64_t frameOff;  // rank 0: the gathered colour frame; 0 elsewhere
+    uint64_t depthOff;  // rank 0: the gathered r16f depth frame; 0 elsewhere
+    uint32_t interleave;  // slab rows interleaved (GSM_MG_ROWS=interleaved): every rank must agree
+    uint32_t memKind;     // exchange memory kind (0 fine-grained, 2 device)
     char busId[32];
     hipIpcMemHandle_t ipc;
 };
@@ -100,41 +115,76 @@ struct SyncPeers {
 size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 }  // namespace
 
-// One barrier of the multi-GPU frame (header comment).  publish (nullable): this rank's per-slab
-// record counts, written into row `rank` of every rank's count matrix before the arrival.
+// A barrier step outside the producing kernels:
+//  * wait (kSyncWaitBlocks workgroups of 64): lane p of every workgroup spins on this rank's flag of
+//    rank p (relaxed system-scope loads, s_sleep, bounded by timeoutTicks), then the workgroup acquires
+//    at system scope (its CU's L1 and its XCD's L2 drop their lines of the exchange memory).  Block 0
+//    counts a timeout (status[0], and the frame's epoch in status[2]: the frame's later waits skip)
+//    and every arrival carrying the failure bit (status[1]).
+//  * arrive (one workgroup; a rank that renders nothing, or one whose frame failed): zero counts
+//    into row `rank` of every count matrix when `publishZero`, a system-scope release, then this
+//    rank's flag in every rank's control block (with kFailBit when `fail`).
 __global__ __launch_bounds__(64) void k_mg_sync(SyncPeers peers, uint32_t* __restrict__ mine, uint32_t rank,
-                                                uint32_t world, uint32_t barrier, uint32_t epoch,
-                                                const uint32_t* __restrict__ publish, uint32_t parity, int arrive,
-                                                int wait, unsigned long long timeoutTicks) {
+                                                uint32_t world, uint32_t barrier, uint32_t epoch, int publishZero,
+                                                uint32_t parity, int arrive, int fail, unsigned long long timeoutTicks) {
     const uint32_t lane = threadIdx.x;
-    if (publish && lane < world) {
-        uint32_t* row = peers.ctl[lane] + kCountsWord + parity * kMaxSlabs * kMaxSlabs + rank * world;
-        for (uint32_t s = 0; s < world; ++s) row[s] = publish[s];
-    }
     if (arrive) {
-        // every store of this rank's earlier kernels (records, pixels) and of this wave (counts)
-        // is visible at system scope before any peer can see the flag
+        if (publishZero && lane < world) {
+            uint32_t* row = peers.ctl[lane] + kCountsWord + parity * kMaxSlabs * kMaxSlabs + rank * world;
+            for (uint32_t s = 0; s < world; ++s) __hip_atomic_store(row + s, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (lane < world)
-            __hip_atomic_store(peers.ctl[lane] + kFlagWords + barrier * kMaxSlabs + rank, epoch, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(peers.ctl[lane] + kFlagWords + barrier * kMaxSlabs + rank, epoch | (fail ? kFailBit : 0u),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        return;
     }
-    if (!wait) return;
     uint32_t* status = mine + kStatusWord;
-    // after a timeout every later wait is skipped: a missing peer costs one timeout, not one per barrier
-    const bool skip = __hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u;
+    // after a timeout the frame's remaining waits are skipped (a missing peer costs one timeout per
+    // frame, and the next frame waits again)
+    const bool skip = ld_sys32(status + 2) == epoch;
+    bool failed = false;
     if (!skip && lane < world) {
         const uint32_t* flag = mine + kFlagWords + barrier * kMaxSlabs + lane;
         const unsigned long long t0 = wall_clock64();
-        while ((int)(__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - epoch) < 0) {
+        for (;;) {
+            const uint32_t f = ld_sys32(flag);
+            if ((int)((f & kEpochMask) - epoch) >= 0) {
+                failed = (f & kFailBit) != 0u && (f & kEpochMask) == epoch;
+                break;
+            }
             if (wall_clock64() - t0 > timeoutTicks) {
-                __hip_atomic_fetch_add(status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                if (blockIdx.x == 0) {
+                    __hip_atomic_fetch_add(status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    __hip_atomic_store(status + 2, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                }
                 break;
             }
             __builtin_amdgcn_s_sleep(1);
         }
     }
+    if (failed && blockIdx.x == 0) __hip_atomic_fetch_add(status + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+}
+
+// rank 0's copy of the gathered frame into the caller's target (rows of `rowBytes`, a multiple of 2):
+// system-coherent loads (the peers stored the frame over xGMI), 4-byte words where aligned
+__global__ __launch_bounds__(256) void k_mg_copy2d(uint8_t* __restrict__ dst, size_t dpitch, const uint8_t* src,
+                                                   size_t spitch, uint32_t rowBytes, uint32_t rows) {
+    const uint32_t y = blockIdx.y;
+    if (y >= rows) return;
+    const uint8_t* s = src + (size_t)y * spitch;
+    uint8_t* d = dst + (size_t)y * dpitch;
+    const bool w4 = ((((uintptr_t)s) | ((uintptr_t)d) | rowBytes) & 3u) == 0;
+    if (w4) {
+        for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < rowBytes / 4u; i += gridDim.x * 256u)
+            ((uint32_t*)d)[i] = ld_sys32((const uint32_t*)s + i);
+    } else {
+        for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < rowBytes / 2u; i += gridDim.x * 256u)
+            ((uint16_t*)d)[i] = __hip_atomic_load((const uint16_t*)s + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
 }
 
 class MultiGpu {
@@ -150,7 +200,12 @@ class MultiGpu {
         *pitch = rank_ == 0 ? framePitch_ : 0;
         return GSM_OK;
     }
-    gsm_status status(uint32_t* timeouts, bool clear);
+    gsm_status frameDepth(void** depth, size_t* pitch) const {
+        *depth = rank_ == 0 ? depth0_ : nullptr;
+        *pitch = rank_ == 0 ? depthPitch0_ : 0;
+        return GSM_OK;
+    }
+    gsm_status status(uint32_t* timeouts, uint32_t* peerErrors, bool clear);
     gsm_status setTimeout(uint32_t ms) {
         if (ms == 0) return GSM_ERR_INVALID_ARGUMENT;
         timeoutTicks_ = (unsigned long long)ms * wallKHz_;
@@ -163,40 +218,67 @@ class MultiGpu {
                    ? GSM_OK
                    : GSM_ERR_RENDER_FAILED;
     }
-    gsm_status copyFrame(void* dst, size_t pitch, uint32_t width, uint32_t height) {
-        if (rank_ != 0 || !frame0_ || !dst || width > r_->maxWidth() || height > r_->maxHeight() ||
-            pitch < (size_t)width * bpp_)
+    gsm_status copyFrame(void* dst, size_t pitch, uint32_t width, uint32_t height, bool depth) {
+        const char* src = depth ? depth0_ : frame0_;
+        const size_t bpp = depth ? 2u : bpp_;
+        if (rank_ != 0 || !src || !dst || width > r_->maxWidth() || height > r_->maxHeight() || pitch < (size_t)width * bpp)
             return GSM_ERR_INVALID_ARGUMENT;
         hipSetDevice(device_);
-        if (hipMemcpy2D(dst, pitch, frame0_, framePitch_, (size_t)width * bpp_, height, hipMemcpyDeviceToHost) !=
-            hipSuccess)
+        if (hipMemcpy2D(dst, pitch, src, depth ? depthPitch0_ : framePitch_, (size_t)width * bpp, height,
+                        hipMemcpyDeviceToHost) != hipSuccess)
             return GSM_ERR_RENDER_FAILED;
         return GSM_OK;
     }
 
    private:
+    // the targets phase 2 renders into and what phase 3 copies (one frame's call arguments)
+    struct Targets {
+        bool gather = false, gatherDepth = false;
+        void* color = nullptr;  // the blend's colour target
+        size_t colorPitch = 0;
+        void* depth = nullptr;  // the blend's depth target (nullable)
+        size_t depthPitch = 0;
+    };
     void release();
     gsm_status check(const gsm_gaussian_input& in, uint32_t width, uint32_t height, void* color, size_t colorPitch,
-                     void* gatherColor) const;
+                     void* depth, size_t depthPitch, void* gatherColor, Targets* t) const;
     uint32_t* ctl() const { return (uint32_t*)mem_; }
-    void sync(hipStream_t s, uint32_t barrier, const uint32_t* publish, bool arrive, bool wait) {
-        hipLaunchKernelGGL(k_mg_sync, dim3(1), dim3(64), 0, s, sync_, ctl(), (uint32_t)rank_, (uint32_t)world_,
-                           barrier, frame_, publish, frame_ & 1u, arrive ? 1 : 0, wait ? 1 : 0, timeoutTicks_);
+    uint32_t* done(uint32_t barrier) const { return done_ + barrier * 16u; }  // 64 B apart
+    MgArrive arrival(uint32_t barrier) const {
+        MgArrive a{};
+        for (int p = 0; p < world_; ++p) a.flag[p] = sync_.ctl[p] + kFlagWords + barrier * kMaxSlabs + rank_;
+        a.done = done(barrier);
+        a.epoch = frame_;
+        a.world = (uint32_t)world_;
+        return a;
+    }
+    void wait(hipStream_t s, uint32_t barrier) {
+        hipLaunchKernelGGL(k_mg_sync, dim3(kSyncWaitBlocks), dim3(64), 0, s, sync_, ctl(), (uint32_t)rank_,
+                           (uint32_t)world_, barrier, frame_, 0, frame_ & 1u, 0, 0, timeoutTicks_);
+    }
+    void arrive(hipStream_t s, uint32_t barrier, bool publishZero, bool fail) {
+        hipLaunchKernelGGL(k_mg_sync, dim3(1), dim3(64), 0, s, sync_, ctl(), (uint32_t)rank_, (uint32_t)world_, barrier,
+                           frame_, publishZero ? 1 : 0, frame_ & 1u, 1, fail ? 1 : 0, timeoutTicks_);
     }
 
     GlobalRenderer* r_ = nullptr;
     int rank_ = 0, world_ = 1, device_ = 0;
-    char* mem_ = nullptr;  // this rank's exchange allocation (uncached)
-    size_t memBytes_ = 0, frameOff_ = 0, framePitch_ = 0;
+    char* mem_ = nullptr;  // this rank's exchange allocation (fine-grained)
+    size_t memBytes_ = 0, frameOff_ = 0, framePitch_ = 0, depthOff_ = 0, depthPitch0_ = 0;
     uint32_t bpp_ = 8, capacity_ = 0, minCap_ = 0;
     uint32_t* sendCounts_ = nullptr;  // this rank's per-slab counts (k_part_scan)
     uint32_t* recvCount_ = nullptr;   // records this rank receives (k_part_push, block 0)
+    uint32_t* done_ = nullptr;        // arrival counters, one 64-B line per barrier (own device memory)
     SyncPeers sync_{};
     SlabPeers recs_{};
-    char* frame0_ = nullptr;  // rank 0's gathered frame (peer mapping on the other ranks)
+    char* frame0_ = nullptr;  // rank 0's gathered colour frame (peer mapping on the other ranks)
+    char* depth0_ = nullptr;  // rank 0's gathered depth frame
     bool connected_ = false;
-    uint32_t frame_ = 0;  // frames begun (phase 0); the barriers' epoch
+    uint32_t frame_ = 0;       // frames begun (phase 0); the barriers' epoch
+    int nextPhase_ = 0;        // phases run in order 0..3
+    gsm_status frameErr_ = GSM_OK;  // this rank's error of the current frame (barrier-only phases after it)
     bool interleave_ = false;  // slab rows interleaved (GSM_MG_ROWS=interleaved at prepare)
+    uint32_t memKind_ = 0;
     uint32_t wallKHz_ = 100000;
     unsigned long long timeoutTicks_ = 0;
     std::vector<void*> opened_;  // IPC mappings of peer allocations
@@ -206,16 +288,21 @@ void MultiGpu::release() {
     hipSetDevice(device_);
     for (void* p : opened_) hipIpcCloseMemHandle(p);
     opened_.clear();
-    for (void* p : {(void*)mem_, (void*)sendCounts_, (void*)recvCount_})
+    for (void* p : {(void*)mem_, (void*)sendCounts_, (void*)recvCount_, (void*)done_})
         if (p) hipFree(p);
     mem_ = nullptr;
-    sendCounts_ = recvCount_ = nullptr;
+    sendCounts_ = recvCount_ = done_ = nullptr;
 }
 
 gsm_status MultiGpu::prepare(GlobalRenderer* r, int rank, int world, MultiGpu** out, void* handle) {
     *out = nullptr;
     if (!handle || world < 1 || world > (int)kMaxSlabs || rank < 0 || rank >= world) return GSM_ERR_INVALID_ARGUMENT;
     if (hipSetDevice(r->device()) != hipSuccess) return GSM_ERR_DEVICE_NOT_AVAILABLE;
+    // exchange memory kind (create-time): fine-grained device memory (default) or ordinary
+    // device memory (GSM_MG_MEM=cached, one GPU only).  Uncached memory is refused: on MI355X its
+    // stores and loads rendered wrong virtual-rank frames (profiles/r03_mg_exchange_memory_ab.log; the
+    // cause, measured in r04, is in DESIGN.md 7)
+    const char* mode = getenv("GSM_MG_MEM");
     MultiGpu* m = new (std::nothrow) MultiGpu();
     if (!m) return GSM_ERR_FAILED_TO_ALLOCATE_BUFFER;
     m->r_ = r;
@@ -224,30 +311,31 @@ gsm_status MultiGpu::prepare(GlobalRenderer* r, int rank, int world, MultiGpu** 
     m->device_ = r->device();
     m->capacity_ = r->maxGaussians();
     m->bpp_ = r->colorBytesPerPixel();
+    m->memKind_ = mode && !strcmp(mode, "cached") ? 2u : (mode && !strcmp(mode, "uncached") ? 1u : 0u);
     int khz = 0;
     if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, m->device_) == hipSuccess && khz > 0)
         m->wallKHz_ = (uint32_t)khz;
     m->timeoutTicks_ = 10000ull * m->wallKHz_;
-    const char* rv = getenv("GSM_MG_ROWS");  // every rank must agree (the same environment)
+    const char* rv = getenv("GSM_MG_ROWS");  // every rank must agree: checked at connect (the handle)
     m->interleave_ = rv && std::strcmp(rv, "interleaved") == 0;
     const size_t recBytes = (size_t)m->capacity_ * sizeof(SplatRecord);
-    m->framePitch_ = (size_t)r->maxWidth() * m->bpp_;
+    m->framePitch_ = align_up((size_t)r->maxWidth() * m->bpp_, 16);
+    m->depthPitch0_ = align_up((size_t)r->maxWidth() * 2u, 16);
     m->frameOff_ = rank == 0 ? align_up(kRecordsOff + recBytes, 4096) : 0;
-    m->memBytes_ = rank == 0 ? m->frameOff_ + m->framePitch_ * r->maxHeight() : kRecordsOff + recBytes;
-    // fine-grained device memory (GSM_MG_MEM=uncached|cached: the A/B of DESIGN.md 7, create-time only):
-    // uncached exchange memory rendered wrong slabs on MI355X (tools/dbg/mg_ab2.sh: 30 of 36 virtual-rank
-    // frames, fine-grained and ordinary memory 0 of 36)
-    const char* mode = getenv("GSM_MG_MEM");
-    hipError_t ae = mode && !strcmp(mode, "cached")
-                        ? hipMalloc((void**)&m->mem_, m->memBytes_)
-                        : hipExtMallocWithFlags((void**)&m->mem_, m->memBytes_,
-                                                mode && !strcmp(mode, "uncached") ? hipDeviceMallocUncached
-                                                                                  : hipDeviceMallocFinegrained);
-    bool ok = ae == hipSuccess &&
+    m->depthOff_ = rank == 0 ? align_up(m->frameOff_ + m->framePitch_ * r->maxHeight(), 4096) : 0;
+    m->memBytes_ = rank == 0 ? m->depthOff_ + m->depthPitch0_ * r->maxHeight() : kRecordsOff + recBytes;
+    hipError_t ae = m->memKind_ == 2u ? hipMalloc((void**)&m->mem_, m->memBytes_)
+                                      : hipExtMallocWithFlags((void**)&m->mem_, m->memBytes_,
+                                                              m->memKind_ == 1u ? hipDeviceMallocUncached
+                                                                                : hipDeviceMallocFinegrained);
+    // the partition buffers now, so that no frame can fail on an allocation
+    bool ok = ae == hipSuccess && r->ensurePartitionBuffers() == GSM_OK &&
               (!getenv("GSM_MG_POISON") || hipMemset(m->mem_, 0xAB, m->memBytes_) == hipSuccess) &&
               hipMemset(m->mem_, 0, kRecordsOff) == hipSuccess &&
               hipMalloc(&m->sendCounts_, kMaxSlabs * 4) == hipSuccess && hipMalloc(&m->recvCount_, 4) == hipSuccess &&
-              hipMemset(m->sendCounts_, 0, kMaxSlabs * 4) == hipSuccess && hipMemset(m->recvCount_, 0, 4) == hipSuccess;
+              hipMalloc(&m->done_, kBarriers * 64) == hipSuccess &&
+              hipMemset(m->sendCounts_, 0, kMaxSlabs * 4) == hipSuccess && hipMemset(m->recvCount_, 0, 4) == hipSuccess &&
+              hipMemset(m->done_, 0, kBarriers * 64) == hipSuccess && hipDeviceSynchronize() == hipSuccess;
     ExchangeHandle h;
     std::memset(&h, 0, sizeof(h));
     if (ok) ok = hipIpcGetMemHandle(&h.ipc, m->mem_) == hipSuccess;
@@ -270,6 +358,9 @@ gsm_status MultiGpu::prepare(GlobalRenderer* r, int rank, int world, MultiGpu** 
     h.base = (uint64_t)(uintptr_t)m->mem_;
     h.bytes = m->memBytes_;
     h.frameOff = m->frameOff_;
+    h.depthOff = m->depthOff_;
+    h.interleave = m->interleave_ ? 1u : 0u;
+    h.memKind = m->memKind_;
     std::memcpy(handle, &h, sizeof(h));
     *out = m;
     return GSM_OK;
@@ -284,10 +375,13 @@ gsm_status MultiGpu::connect(const void* all) {
     uint32_t minCap = 0xFFFFFFFFu;
     for (int p = 0; p < world_; ++p) {
         const ExchangeHandle& h = hs[(size_t)p];
+        // the ranks agree on the world, the frame limits and the row layout (a rank with another
+        // GSM_MG_ROWS would send records with the wrong slab masks: refused here)
         if (h.magic != kHandleMagic || h.version != kHandleVersion || h.rank != p || h.world != world_ ||
-            h.maxWidth != r_->maxWidth() || h.maxHeight != r_->maxHeight() || h.bytesPerPixel != bpp_)
+            h.maxWidth != r_->maxWidth() || h.maxHeight != r_->maxHeight() || h.bytesPerPixel != bpp_ ||
+            h.interleave != (interleave_ ? 1u : 0u))
             return GSM_ERR_INVALID_ARGUMENT;
-        if (p == 0 && h.frameOff == 0) return GSM_ERR_INVALID_ARGUMENT;
+        if (p == 0 && (h.frameOff == 0 || h.depthOff == 0)) return GSM_ERR_INVALID_ARGUMENT;
         if (h.capacity < minCap) minCap = h.capacity;
     }
     if (hs[(size_t)rank_].base != (uint64_t)(uintptr_t)mem_) return GSM_ERR_INVALID_ARGUMENT;  // not our handle
@@ -307,6 +401,8 @@ gsm_status MultiGpu::connect(const void* all) {
             }
             base[p] = (char*)(uintptr_t)h.base;
         } else {
+            // ordinary device memory is coherent only inside one GPU: refused across processes
+            if (h.memKind == 2u) return GSM_ERR_UNSUPPORTED;
             void* ptr = nullptr;
             if (hipIpcOpenMemHandle(&ptr, h.ipc, hipIpcMemLazyEnablePeerAccess) != hipSuccess) {
                 (void)hipGetLastError();
@@ -320,34 +416,63 @@ gsm_status MultiGpu::connect(const void* all) {
         recs_.cap[p] = h.capacity;
     }
     frame0_ = base[0] + hs[0].frameOff;
+    depth0_ = base[0] + hs[0].depthOff;
     minCap_ = minCap;
     connected_ = true;
     return GSM_OK;
 }
 
+// Everything any phase of this rank's frame could refuse, before anything is enqueued.
 gsm_status MultiGpu::check(const gsm_gaussian_input& in, uint32_t width, uint32_t height, void* color,
-                           size_t colorPitch, void* gatherColor) const {
-    if (!connected_) return GSM_ERR_INVALID_ARGUMENT;
-    // the same answer on every rank (same N, size and limits): no rank is left waiting at a barrier
+                           size_t colorPitch, void* depth, size_t depthPitch, void* gatherColor, Targets* t) const {
+    // which barrier steps the frame has (gather, and so barrier 2) follows from the arguments alone:
+    // a refused frame still performs them
+    t->gather = gatherColor != nullptr;
+    t->gatherDepth = t->gather && depth != nullptr;
+    // the frame capacity is the smallest rank's: the same answer on every rank for the same frame
     if (in.gaussian_count > minCap_) return GSM_ERR_INVALID_GAUSSIAN_COUNT;
     if (width == 0 || height == 0 || width > r_->maxWidth() || height > r_->maxHeight())
         return GSM_ERR_INVALID_DIMENSIONS;
     if (in.gaussian_count > 0 && (!in.gaussians || !in.harmonics)) return GSM_ERR_MISSING_REQUIRED_BUFFER;
-    if (rank_ == 0 && gatherColor && gatherColor != frame0_) {
-        if (colorPitch < (size_t)width * bpp_) return GSM_ERR_INVALID_BUFFER_SIZE;
-    } else if (!gatherColor && !color) {
-        return GSM_ERR_MISSING_REQUIRED_BUFFER;
+    if (t->gather) {
+        t->color = frame0_;
+        t->colorPitch = framePitch_;
+        t->depth = t->gatherDepth ? (void*)depth0_ : nullptr;
+        t->depthPitch = depthPitch0_;
+        if (rank_ == 0) {  // the copies of phase 3 into the caller's targets
+            if (gatherColor != frame0_ && colorPitch < (size_t)width * bpp_) return GSM_ERR_INVALID_BUFFER_SIZE;
+            if (t->gatherDepth && depth != depth0_ && (depthPitch < (size_t)width * 2u || (depthPitch & 1u) ||
+                                                       (((uintptr_t)depth) & 1u)))
+                return GSM_ERR_INVALID_BUFFER_SIZE;
+        }
+    } else {
+        t->color = color;
+        t->colorPitch = colorPitch;
+        t->depth = depth;
+        t->depthPitch = depthPitch;
     }
-    if (hipSetDevice(device_) != hipSuccess) return GSM_ERR_DEVICE_NOT_AVAILABLE;
-    return GSM_OK;
+    // what the slab render (GlobalRenderer::renderRecords) would refuse
+    return r_->validateFrame(0, false, width, height, t->color, t->colorPitch, t->depth, t->depthPitch);
 }
 
 gsm_status MultiGpu::phase(int p, hipStream_t s, const gsm_gaussian_input& in, const gsm_camera_params& cam,
                            uint32_t width, uint32_t height, void* color, size_t colorPitch, void* depth,
                            size_t depthPitch, void* gatherColor) {
     if (p < 0 || p > 3) return GSM_ERR_INVALID_ARGUMENT;
-    gsm_status st = check(in, width, height, color, colorPitch, gatherColor);
-    if (st != GSM_OK) return st;
+    if (!connected_) return GSM_ERR_INVALID_ARGUMENT;  // no peers to stay in step with
+    if (p != nextPhase_) return GSM_ERR_INVALID_ARGUMENT;  // phases in order: nothing enqueued
+    if (hipSetDevice(device_) != hipSuccess) return GSM_ERR_DEVICE_NOT_AVAILABLE;
+    Targets t;
+    gsm_status cst = check(in, width, height, color, colorPitch, depth, depthPitch, gatherColor, &t);
+    if (p == 0) {
+        ++frame_;
+        frame_ &= kEpochMask;
+        if (frame_ == 0) frame_ = 1;  // (epoch 0 is the flags' initial value)
+        frameErr_ = cst;
+    } else if (frameErr_ == GSM_OK) {
+        frameErr_ = cst;  // (the same arguments as phase 0's for a caller that follows the protocol)
+    }
+    nextPhase_ = (p + 1) & 3;
     const uint32_t world = (uint32_t)world_, rank = (uint32_t)rank_;
     // slabs: contiguous blocks of ceil(tilesY / world) tile rows (default: each record travels to the
     // fewest ranks -- interleaving sends a gaussian to every rank one of its rect rows maps to, +71 %
@@ -363,64 +488,92 @@ gsm_status MultiGpu::phase(int p, hipStream_t s, const gsm_gaussian_input& in, c
     auto setRows = [&]() {
         return interleave_ ? r_->setTileRows(rank, tilesY, world) : r_->setTileRows(rows[rank], rows[rank + 1]);
     };
-    const bool gather = gatherColor != nullptr;
-    // every phase ends with an arrival and the next begins with the matching wait, so a barrier
-    // only ever waits for work enqueued in an earlier phase (virtual ranks on one stream)
+    gsm_status st = GSM_OK;
+    // Every phase performs its barrier steps whatever happened before in this frame on this rank: a
+    // failed frame arrives with the failure bit (and zero counts), so every rank's epochs stay equal.
     switch (p) {
         case 0: {
-            // the rank's id range (gsm_amd.exchange.id_range)
-            const uint32_t N = in.gaussian_count;
-            const uint32_t perIds = (N + world - 1) / world;
-            const uint32_t first = rank * perIds < N ? rank * perIds : N;
-            const uint32_t cnt = perIds < N - first ? perIds : N - first;
-            // the slab's blend units are ordered inside this launch (the long kernel of the frame's
-            // first half), not in the short records-in launch of phase 2
-            if (mine && (st = setRows()) != GSM_OK) return st;
-            st = r_->partitionCounts(s, in, cam, width, height, first, cnt, rows, world, sendCounts_, mine, interleave_);
-            if (st != GSM_OK) return st;
-            ++frame_;
-            sync(s, 0, sendCounts_, true, false);  // counts into every rank's matrix, then arrive
+            if (frameErr_ == GSM_OK) {
+                // the rank's id range (gsm_amd.exchange.id_range)
+                const uint32_t N = in.gaussian_count;
+                const uint32_t perIds = (N + world - 1) / world;
+                const uint32_t first = rank * perIds < N ? rank * perIds : N;
+                const uint32_t cnt = perIds < N - first ? perIds : N - first;
+                CountPublish pub{};
+                for (uint32_t q = 0; q < world; ++q)
+                    pub.row[q] = sync_.ctl[q] + kCountsWord + (frame_ & 1u) * kMaxSlabs * kMaxSlabs + rank * world;
+                pub.arrive = arrival(0);
+                // the slab's blend units are ordered inside this launch (the long kernel of the frame's
+                // first half), not in the short records-in launch of phase 2
+                if (mine && (st = setRows()) != GSM_OK) frameErr_ = st;
+                if (frameErr_ == GSM_OK &&
+                    (st = r_->partitionCounts(s, in, cam, width, height, first, cnt, rows, world, sendCounts_, mine,
+                                              interleave_, &pub)) != GSM_OK)
+                    frameErr_ = st;  // (refused before any launch)
+            }
+            if (frameErr_ != GSM_OK) arrive(s, 0, /*publishZero=*/true, /*fail=*/true);
             break;
         }
         case 1: {
-            sync(s, 0, nullptr, false, true);  // every rank's counts are in my matrix
-            const uint32_t* counts = ctl() + kCountsWord + (frame_ & 1u) * kMaxSlabs * kMaxSlabs;
-            if ((st = r_->partitionPush(s, world, rank, counts, recs_, recvCount_)) != GSM_OK) return st;
-            sync(s, 1, nullptr, true, false);
+            wait(s, 0);  // every rank's counts are in my matrix
+            if (frameErr_ == GSM_OK) {
+                const uint32_t* counts = ctl() + kCountsWord + (frame_ & 1u) * kMaxSlabs * kMaxSlabs;
+                if ((st = r_->partitionPush(s, world, rank, counts, recs_, recvCount_, arrival(1))) != GSM_OK)
+                    frameErr_ = st;
+            }
+            if (frameErr_ != GSM_OK) arrive(s, 1, false, true);
             break;
         }
         case 2: {
-            sync(s, 1, nullptr, false, true);  // every record of my slab has arrived
-            if (mine) {
-                if ((st = setRows()) != GSM_OK) return st;
-                void* target = gather ? (void*)frame0_ : color;
-                const size_t pitch = gather ? framePitch_ : colorPitch;
-                st = r_->renderRecords(s, mem_ + kRecordsOff, capacity_, width, height, target, pitch, depth,
-                                       depthPitch, recvCount_, /*preOrdered=*/true);
-                if (st != GSM_OK) return st;
+            wait(s, 1);  // every record of my slab has arrived
+            const bool signal = t.gather && world > 1;  // rank 0 waits for every slab's pixels
+            bool arrived = false;
+            if (frameErr_ == GSM_OK && mine) {
+                if ((st = setRows()) == GSM_OK) {
+                    const MgArrive ba = arrival(2);
+                    st = r_->renderRecords(s, mem_ + kRecordsOff, capacity_, width, height, t.color, t.colorPitch,
+                                           t.depth, t.depthPitch, recvCount_, /*preOrdered=*/true,
+                                           signal ? &ba : nullptr);
+                    arrived = signal && st == GSM_OK;  // the blend's waves arrive
+                }
+                if (st != GSM_OK) frameErr_ = st;
             }
-            if (gather && world > 1) sync(s, 2, nullptr, true, false);  // my band is in rank 0's frame
+            if (signal && !arrived) arrive(s, 2, false, frameErr_ != GSM_OK);
             break;
         }
         case 3: {
-            if (gather && rank == 0) {
-                if (world > 1) sync(s, 2, nullptr, false, true);  // every band is in my frame
-                if (gatherColor != frame0_ &&
-                    hipMemcpy2DAsync(gatherColor, colorPitch, frame0_, framePitch_, (size_t)width * bpp_, height,
-                                     hipMemcpyDeviceToDevice, s) != hipSuccess)
-                    return GSM_ERR_RENDER_FAILED;
+            if (t.gather && rank == 0) {
+                if (world > 1) wait(s, 2);  // every band is in my frame
+                if (frameErr_ == GSM_OK) {
+                    const uint32_t gy = height;
+                    if (gatherColor != frame0_) {
+                        const uint32_t rowBytes = width * bpp_;
+                        hipLaunchKernelGGL(k_mg_copy2d, dim3((rowBytes / 4u + 255u) / 256u, gy), dim3(256), 0, s,
+                                           (uint8_t*)gatherColor, colorPitch, (const uint8_t*)frame0_, framePitch_,
+                                           rowBytes, gy);
+                    }
+                    if (t.gatherDepth && depth != depth0_) {
+                        const uint32_t rowBytes = width * 2u;
+                        hipLaunchKernelGGL(k_mg_copy2d, dim3((rowBytes / 4u + 255u) / 256u, gy), dim3(256), 0, s,
+                                           (uint8_t*)depth, depthPitch, (const uint8_t*)depth0_, depthPitch0_, rowBytes,
+                                           gy);
+                    }
+                }
             }
             break;
         }
     }
     if (hipGetLastError() != hipSuccess) return GSM_ERR_RENDER_FAILED;
-    return GSM_OK;
+    return frameErr_;
 }
 
-gsm_status MultiGpu::status(uint32_t* timeouts, bool clear) {
+gsm_status MultiGpu::status(uint32_t* timeouts, uint32_t* peerErrors, bool clear) {
     hipSetDevice(device_);
-    if (hipMemcpy(timeouts, ctl() + kStatusWord, 4, hipMemcpyDeviceToHost) != hipSuccess) return GSM_ERR_RENDER_FAILED;
-    if (clear && hipMemset(ctl() + kStatusWord, 0, 4) != hipSuccess) return GSM_ERR_RENDER_FAILED;
+    uint32_t w[2] = {0, 0};
+    if (hipMemcpy(w, ctl() + kStatusWord, 8, hipMemcpyDeviceToHost) != hipSuccess) return GSM_ERR_RENDER_FAILED;
+    if (timeouts) *timeouts = w[0];
+    if (peerErrors) *peerErrors = w[1];
+    if (clear && hipMemset(ctl() + kStatusWord, 0, 12) != hipSuccess) return GSM_ERR_RENDER_FAILED;
     return GSM_OK;
 }
 
@@ -521,12 +674,14 @@ gsm_status gsm_multigpu_render_phase(gsm_multigpu* m, int phase, void* stream, c
 gsm_status gsm_multigpu_render(gsm_multigpu* m, void* stream, const gsm_gaussian_input* input,
                                const gsm_camera_params* camera, uint32_t width, uint32_t height, void* color,
                                size_t color_pitch_bytes, void* depth, size_t depth_pitch_bytes, void* gather_color) {
+    // every phase runs even after a refusal: its barrier steps keep the ranks' epochs in step
+    gsm_status first = GSM_OK;
     for (int p = 0; p < 4; ++p) {
         gsm_status st = gsm_multigpu_render_phase(m, p, stream, input, camera, width, height, color, color_pitch_bytes,
                                                   depth, depth_pitch_bytes, gather_color);
-        if (st != GSM_OK) return st;
+        if (first == GSM_OK) first = st;
     }
-    return GSM_OK;
+    return first;
 }
 
 gsm_status gsm_multigpu_frame(gsm_multigpu* m, void** color, size_t* pitch_bytes) {
@@ -534,9 +689,19 @@ gsm_status gsm_multigpu_frame(gsm_multigpu* m, void** color, size_t* pitch_bytes
     return m->impl->frame(color, pitch_bytes);
 }
 
+gsm_status gsm_multigpu_frame_depth(gsm_multigpu* m, void** depth, size_t* pitch_bytes) {
+    if (!m || !m->impl || !depth || !pitch_bytes) return GSM_ERR_INVALID_ARGUMENT;
+    return m->impl->frameDepth(depth, pitch_bytes);
+}
+
 gsm_status gsm_multigpu_status(gsm_multigpu* m, uint32_t* timeouts, int clear) {
     if (!m || !m->impl || !timeouts) return GSM_ERR_INVALID_ARGUMENT;
-    return m->impl->status(timeouts, clear != 0);
+    return m->impl->status(timeouts, nullptr, clear != 0);
+}
+
+gsm_status gsm_multigpu_errors(gsm_multigpu* m, uint32_t* timeouts, uint32_t* failed_peer_arrivals, int clear) {
+    if (!m || !m->impl || !timeouts || !failed_peer_arrivals) return GSM_ERR_INVALID_ARGUMENT;
+    return m->impl->status(timeouts, failed_peer_arrivals, clear != 0);
 }
 
 gsm_status gsm_multigpu_set_timeout_ms(gsm_multigpu* m, uint32_t ms) {
@@ -547,7 +712,13 @@ gsm_status gsm_multigpu_set_timeout_ms(gsm_multigpu* m, uint32_t ms) {
 gsm_status gsm_multigpu_debug_copy_frame(gsm_multigpu* m, void* host_dst, size_t dst_pitch_bytes, uint32_t width,
                                          uint32_t height) {
     if (!m || !m->impl) return GSM_ERR_INVALID_ARGUMENT;
-    return m->impl->copyFrame(host_dst, dst_pitch_bytes, width, height);
+    return m->impl->copyFrame(host_dst, dst_pitch_bytes, width, height, false);
+}
+
+gsm_status gsm_multigpu_debug_copy_depth(gsm_multigpu* m, void* host_dst, size_t dst_pitch_bytes, uint32_t width,
+                                         uint32_t height) {
+    if (!m || !m->impl) return GSM_ERR_INVALID_ARGUMENT;
+    return m->impl->copyFrame(host_dst, dst_pitch_bytes, width, height, true);
 }
 
 gsm_status gsm_multigpu_debug_copy_exchange(gsm_multigpu* m, void* host_dst, size_t bytes) {

@@ -257,7 +257,8 @@ gsm_status GlobalRenderer::render(hipStream_t s, const gsm_gaussian_input& in,
 
 gsm_status GlobalRenderer::renderRecords(hipStream_t s, const void* records, uint32_t count, uint32_t width,
                                          uint32_t height, void* color, size_t colorPitch, void* depth,
-                                         size_t depthPitch, const uint32_t* devCount, bool preOrdered) {
+                                         size_t depthPitch, const uint32_t* devCount, bool preOrdered,
+                                         const MgArrive* blendArrive) {
     // devCount: the count lives on the device (multi-GPU exchange, gsm_multigpu_render); `count` is
     // then the capacity the grids cover
     gsm_status st = validateFrame(count, !records, width, height, color, colorPitch, depth, depthPitch);
@@ -268,7 +269,7 @@ gsm_status GlobalRenderer::renderRecords(hipStream_t s, const void* records, uin
     return runFrame(s, a, width, height, color, colorPitch, depth, depthPitch,
                     [&](const ProjectArgs& pa) {
                         launch_records_in(records, pa, arena_, s, devCount);
-                    }, devCount, preOrdered);
+                    }, devCount, preOrdered, blendArrive);
 }
 
 gsm_status GlobalRenderer::preparePartition(const gsm_gaussian_input& in, const gsm_camera_params& camp,
@@ -292,16 +293,8 @@ gsm_status GlobalRenderer::preparePartition(const gsm_gaussian_input& in, const 
         f->slabs.rows[i] = slabRows[i];
     }
     if (hipSetDevice(device_) != hipSuccess) return GSM_ERR_DEVICE_NOT_AVAILABLE;
-    if (!part_.records) {  // lazily: only ranks of a partitioned frame need these
-        const size_t blocks = ((size_t)maxGaussians_ + kProjectBlock - 1) / kProjectBlock;
-        gsm_status st = alloc((void**)&part_.records, (size_t)maxGaussians_ * sizeof(SplatRecord));
-        if (st == GSM_OK) st = alloc((void**)&part_.masks, (size_t)maxGaussians_ * 4);
-        if (st == GSM_OK) st = alloc((void**)&part_.blockSlabCounts, kMaxSlabs * (blocks + 1) * 4);
-        if (st != GSM_OK) {
-            part_ = PartitionBuffers();
-            return st;
-        }
-    }
+    gsm_status st = ensurePartitionBuffers();
+    if (st != GSM_OK) return st;
     f->half = config_.precision == GSM_PRECISION_FLOAT16;
     f->a = frameArgs(camp, width, height, count, in.sh_components);
     f->a.rowBegin = 0;  // the rank's ids are projected against the whole frame
@@ -314,6 +307,17 @@ gsm_status GlobalRenderer::preparePartition(const gsm_gaussian_input& in, const 
     const uint32_t k = in.sh_components;
     f->deg = k <= 1 ? 0u : (k <= 4 ? 1u : (k <= 9 ? 2u : 3u));
     return GSM_OK;
+}
+
+gsm_status GlobalRenderer::ensurePartitionBuffers() {
+    if (part_.records) return GSM_OK;  // lazily: only ranks of a partitioned frame need these
+    if (hipSetDevice(device_) != hipSuccess) return GSM_ERR_DEVICE_NOT_AVAILABLE;
+    const size_t blocks = ((size_t)maxGaussians_ + kProjectBlock - 1) / kProjectBlock;
+    gsm_status st = alloc((void**)&part_.records, (size_t)maxGaussians_ * sizeof(SplatRecord));
+    if (st == GSM_OK) st = alloc((void**)&part_.masks, (size_t)maxGaussians_ * 4);
+    if (st == GSM_OK) st = alloc((void**)&part_.blockSlabCounts, kMaxSlabs * (blocks + 1) * 4);
+    if (st != GSM_OK) part_ = PartitionBuffers();
+    return st;
 }
 
 gsm_status GlobalRenderer::projectPartition(hipStream_t s, const gsm_gaussian_input& in,
@@ -334,7 +338,7 @@ gsm_status GlobalRenderer::projectPartition(hipStream_t s, const gsm_gaussian_in
 gsm_status GlobalRenderer::partitionCounts(hipStream_t s, const gsm_gaussian_input& in, const gsm_camera_params& camp,
                                            uint32_t width, uint32_t height, uint32_t first, uint32_t count,
                                            const uint32_t* slabRows, uint32_t numSlabs, uint32_t* sendCounts,
-                                           bool orderUnits, bool interleave) {
+                                           bool orderUnits, bool interleave, const CountPublish* publish) {
     PartitionFrame f;
     gsm_status st = preparePartition(in, camp, width, height, first, count, slabRows, numSlabs, false, nullptr,
                                      sendCounts, &f, interleave);
@@ -342,7 +346,7 @@ gsm_status GlobalRenderer::partitionCounts(hipStream_t s, const gsm_gaussian_inp
     // the blend units of this renderer's rows (its slab), ordered by one extra workgroup of the launch
     f.a.schedUnits = orderUnits ? scheduleUnits(s, width, height) : 0u;
     launch_partition_counts(f.half, f.deg, f.world, f.harm, f.a, f.slabs, part_, arena_.sincosTable, sendCounts,
-                            arena_, s);
+                            arena_, publish ? *publish : CountPublish{}, s);
     partCount_ = count;
     partSlabs_ = f.slabs;
     if (hipGetLastError() != hipSuccess) return GSM_ERR_RENDER_FAILED;
@@ -350,12 +354,12 @@ gsm_status GlobalRenderer::partitionCounts(hipStream_t s, const gsm_gaussian_inp
 }
 
 gsm_status GlobalRenderer::partitionPush(hipStream_t s, uint32_t world, uint32_t rank, const uint32_t* counts,
-                                         const SlabPeers& peers, uint32_t* recvCount) {
+                                         const SlabPeers& peers, uint32_t* recvCount, const MgArrive& arrive) {
     ProjectArgs a;
     std::memset(&a, 0, sizeof(a));
     a.count = partCount_;
     if (world != partSlabs_.n) return GSM_ERR_INVALID_ARGUMENT;  // one slab per rank, as partitionCounts split
-    launch_partition_push(a, world, rank, part_, counts, peers, recvCount, partSlabs_, s);
+    launch_partition_push(a, world, rank, part_, counts, peers, recvCount, partSlabs_, arrive, s);
     if (hipGetLastError() != hipSuccess) return GSM_ERR_RENDER_FAILED;
     return GSM_OK;
 }
@@ -376,7 +380,8 @@ uint32_t GlobalRenderer::scheduleUnits(hipStream_t s, uint32_t width, uint32_t h
 template <class Front>
 gsm_status GlobalRenderer::runFrame(hipStream_t s, const ProjectArgs& a, uint32_t width, uint32_t height,
                                     void* color, size_t colorPitch, void* depth, size_t depthPitch,
-                                    Front&& front, const uint32_t* devCount, bool preOrdered) {
+                                    Front&& front, const uint32_t* devCount, bool preOrdered,
+                                    const MgArrive* blendArrive) {
     const bool prof = (profiling_ & 1) != 0;         // every stage bracketed by events
     // only the blend (2 events per frame), on every frame or every period-th (bits 8-15)
     const uint32_t period = ((uint32_t)profiling_ >> 8) & 0xFFu;
@@ -464,7 +469,7 @@ gsm_status GlobalRenderer::runFrame(hipStream_t s, const ProjectArgs& a, uint32_
     // the schedule from the walks the previous frame's blend recorded (same stream: no join)
     if (prof || blendOnly) hipEventRecord(ev[5], s);
     launch_blend(g, arena_, color, colorPitch, depth, depthPitch, numCUs_, costOrder,
-                 (int)config_.color_format, s, tuning_.blendWaves, tuning_.blendClaim);
+                 (int)config_.color_format, s, tuning_.blendWaves, tuning_.blendClaim, blendArrive);
     if (prof || blendOnly) hipEventRecord(ev[6], s);
     if (prof || blendOnly) profFrames_++;
     haveTimes_ = profFrames_ > 0;

@@ -32,15 +32,26 @@ class GlobalRenderer {
     // into every slab owner's receive buffer once the count matrix is on the device (gsm_multigpu.hip)
     // orderUnits: the launch also orders the blend units of the renderer's own rows (set_tile_rows) for a
     // later renderRecords(..., preOrdered = true) of the same frame
+    // publish (multi-GPU frame): the per-slab totals also go into every rank's count matrix and the
+    // scan's workgroups arrive at barrier 0 (gsm_multigpu.hip); null: counts only
     gsm_status partitionCounts(hipStream_t stream, const gsm_gaussian_input& input, const gsm_camera_params& camera,
                                uint32_t width, uint32_t height, uint32_t first, uint32_t count,
                                const uint32_t* slabRows, uint32_t numSlabs, uint32_t* sendCounts,
-                               bool orderUnits = false, bool interleave = false);
+                               bool orderUnits = false, bool interleave = false, const CountPublish* publish = nullptr);
+    // the push's workgroups arrive at `arrive`'s barrier after their record stores
     gsm_status partitionPush(hipStream_t stream, uint32_t world, uint32_t rank, const uint32_t* counts,
-                             const SlabPeers& peers, uint32_t* recvCount);
+                             const SlabPeers& peers, uint32_t* recvCount, const MgArrive& arrive);
+    // blendArrive (nullable): the blend's waves arrive at that barrier after their pixel stores
     gsm_status renderRecords(hipStream_t stream, const void* records, uint32_t count, uint32_t width,
                              uint32_t height, void* color, size_t colorPitch, void* depth, size_t depthPitch,
-                             const uint32_t* devCount = nullptr, bool preOrdered = false);
+                             const uint32_t* devCount = nullptr, bool preOrdered = false,
+                             const MgArrive* blendArrive = nullptr);
+    // what renderRecords / the multi-GPU frame would refuse, checked before anything is enqueued
+    gsm_status validateFrame(uint32_t count, bool inputMissing, uint32_t width, uint32_t height,
+                             const void* color, size_t colorPitch, const void* depth, size_t depthPitch) const;
+    // the partition buffers (allocated lazily by the first partition frame; the multi-GPU frame
+    // allocates them at prepare so that no frame can fail on an allocation)
+    gsm_status ensurePartitionBuffers();
     uint32_t maxGaussians() const { return maxGaussians_; }
     uint32_t tilesY() const { return tilesY_; }
     uint32_t maxWidth() const { return maxWidth_; }
@@ -66,13 +77,12 @@ class GlobalRenderer {
     gsm_status alloc(void** p, size_t bytes);
     ProjectArgs frameArgs(const gsm_camera_params& camera, uint32_t width, uint32_t height, uint32_t count,
                           uint32_t shComponents) const;
-    gsm_status validateFrame(uint32_t count, bool inputMissing, uint32_t width, uint32_t height,
-                             const void* color, size_t colorPitch, const void* depth, size_t depthPitch) const;
     // scan, scatter, sort, headers and blend after `front` filled the per-gaussian arrays
     template <class Front>
     gsm_status runFrame(hipStream_t s, const ProjectArgs& a, uint32_t width, uint32_t height, void* color,
                         size_t colorPitch, void* depth, size_t depthPitch, Front&& front,
-                        const uint32_t* devCount = nullptr, bool preOrdered = false);
+                        const uint32_t* devCount = nullptr, bool preOrdered = false,
+                        const MgArrive* blendArrive = nullptr);
     // the blend schedule's unit count for the current rows (0 when cost order is off), its cost
     // arrays cleared when the geometry changed
     uint32_t scheduleUnits(hipStream_t s, uint32_t width, uint32_t height);

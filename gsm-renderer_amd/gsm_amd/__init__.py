@@ -253,6 +253,9 @@ _SIGNATURES = {
     "gsm_multigpu_set_timeout_ms": ([C.c_void_p, C.c_uint32], C.c_int),
     "gsm_multigpu_debug_copy_exchange": ([C.c_void_p, C.c_void_p, C.c_size_t], C.c_int),
     "gsm_multigpu_debug_copy_frame": ([C.c_void_p, C.c_void_p, C.c_size_t, C.c_uint32, C.c_uint32], C.c_int),
+    "gsm_multigpu_debug_copy_depth": ([C.c_void_p, C.c_void_p, C.c_size_t, C.c_uint32, C.c_uint32], C.c_int),
+    "gsm_multigpu_frame_depth": ([C.c_void_p, C.POINTER(C.c_void_p), C.POINTER(C.c_size_t)], C.c_int),
+    "gsm_multigpu_errors": ([C.c_void_p, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.c_int], C.c_int),
 }
 
 SPLAT_RECORD_BYTES = 48  # include/gsm_multigpu.h GSM_SPLAT_RECORD_BYTES
@@ -689,20 +692,24 @@ class MultiGpuRenderer:
 
     def render(self, color_texture, depth_texture, input: GaussianInput, camera: CameraParams, width: int,
                height: int, gather: bool = True, stream=None, color_pitch: Optional[int] = None,
-               depth_pitch: Optional[int] = None, gather_target=None):
+               depth_pitch: Optional[int] = None, gather_target=None, gather_depth: bool = False):
         """One frame.  gather: rank 0 receives the whole frame -- in color_texture (a copy of the
         library frame), or, with gather_target = self.frame()[0], in the library frame itself; the
-        other ranks' color_texture is then unused (may be None)."""
+        other ranks' color_texture is then unused (may be None).  gather_depth (with gather): rank 0
+        also receives the r16f depth -- in depth_texture (a copy) or, when depth_texture is None, in
+        the library depth frame (self.frame_depth())."""
         self.render_phases(range(4), color_texture, depth_texture, input, camera, width, height, gather, stream,
-                           color_pitch, depth_pitch, gather_target)
+                           color_pitch, depth_pitch, gather_target, gather_depth)
 
     def render_phases(self, phases, color_texture, depth_texture, input: GaussianInput, camera: CameraParams,
                       width: int, height: int, gather: bool = True, stream=None, color_pitch: Optional[int] = None,
-                      depth_pitch: Optional[int] = None, gather_target=None):
+                      depth_pitch: Optional[int] = None, gather_target=None, gather_depth: bool = False):
         """gsm_multigpu_render_phase for each phase in `phases` (virtual ranks: phase p of every rank
-        before phase p + 1 of any, include/gsm_multigpu.h)."""
+        before phase p + 1 of any, include/gsm_multigpu.h).  Every phase is issued even after one
+        returned an error (the ranks stay in step); the first error is raised after the last."""
         inp, cam, cp, dp = self._args(input, camera, color_texture, depth_texture, width, color_pitch, depth_pitch)
         col = _ptr(color_texture)
+        dep = _ptr(depth_texture)
         if gather:  # rank 0: the caller's target (a copy) or else the library frame; others: any non-NULL
             if gather_target is not None:
                 g = _ptr(gather_target)
@@ -710,12 +717,23 @@ class MultiGpuRenderer:
                 g = col if col is not None else self.frame()[0]
             else:
                 g = 1
+            if not gather_depth:
+                dep = None
+            elif self.rank == 0:
+                if dep is None:
+                    dep, dp = self.frame_depth()
+            else:
+                dep = 1
         else:
             g = None
+        first = None
         for p in phases:
             st = _lib().gsm_multigpu_render_phase(self._h, int(p), _stream_handle(stream), C.byref(inp), C.byref(cam),
-                                                  int(width), int(height), col, cp, _ptr(depth_texture), dp, g)
-            _check(st, f"gsm_multigpu_render_phase({p})")
+                                                  int(width), int(height), col, cp, dep, dp, g)
+            if st != 0 and first is None:
+                first = (st, p)
+        if first is not None:
+            _check(first[0], f"gsm_multigpu_render_phase({first[1]})")
 
     def frame(self):
         """(device pointer, pitch bytes) of rank 0's gathered frame; (None, 0) elsewhere."""
@@ -723,6 +741,26 @@ class MultiGpuRenderer:
         pitch = C.c_size_t()
         _check(_lib().gsm_multigpu_frame(self._h, C.byref(p), C.byref(pitch)), "gsm_multigpu_frame")
         return p.value, int(pitch.value)
+
+    def frame_depth(self):
+        """(device pointer, pitch bytes) of rank 0's gathered r16f depth frame; (None, 0) elsewhere."""
+        p = C.c_void_p()
+        pitch = C.c_size_t()
+        _check(_lib().gsm_multigpu_frame_depth(self._h, C.byref(p), C.byref(pitch)), "gsm_multigpu_frame_depth")
+        return p.value, int(pitch.value)
+
+    def copy_depth(self, width: int, height: int) -> np.ndarray:
+        """Rank 0: the gathered r16f depth frame as uint16 bits [height, width] (synchronous)."""
+        out = np.empty((int(height), int(width)), np.uint16)
+        _check(_lib().gsm_multigpu_debug_copy_depth(self._h, out.ctypes.data_as(C.c_void_p), int(width) * 2,
+                                                    int(width), int(height)), "gsm_multigpu_debug_copy_depth")
+        return out
+
+    def errors(self, clear: bool = False):
+        """(barrier timeouts, failed peer arrivals) since create or the last clear."""
+        t, f = C.c_uint32(0), C.c_uint32(0)
+        _check(_lib().gsm_multigpu_errors(self._h, C.byref(t), C.byref(f), 1 if clear else 0), "gsm_multigpu_errors")
+        return int(t.value), int(f.value)
 
     def copy_frame(self, width: int, height: int) -> np.ndarray:
         """Rank 0: the gathered rgba16f frame as uint16 bits [height, width, 4] (synchronous)."""

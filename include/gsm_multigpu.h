@@ -16,11 +16,13 @@
  * stable-sort tie order (determinism contract).
  *
  * gsm_multigpu_* run the whole protocol inside the library with no host round trip and no
- * collective library in the frame: every rank owns one uncached "exchange" allocation (control
- * words, the count matrix, its receive buffer of records and, on rank 0, the gathered frame),
- * the ranks open each other's exchange allocations once (IPC handles), and per frame the
- * counts, the records and the slab pixels are written straight into the owners' memory by the
- * producing kernels (xGMI stores between GPUs), ordered by device-side flag barriers.
+ * collective library in the frame: every rank owns one fine-grained "exchange" allocation
+ * (control words, the count matrix, its receive buffer of records and, on rank 0, the gathered
+ * colour and depth frames), the ranks open each other's exchange allocations once (IPC handles),
+ * and per frame the counts, the records and the slab pixels are written straight into the owners'
+ * memory by the producing kernels (xGMI stores between GPUs), which then arrive at a device-side
+ * flag barrier themselves: every storing unit releases at system scope before its arrival, every
+ * consumer load of exchange data is system-coherent.
  * gsm_global_project_partition / gsm_global_render_records remain for callers that move the
  * records themselves.
  */
@@ -63,14 +65,19 @@ gsm_status gsm_global_render_records(gsm_renderer *renderer, void *stream, const
  * One renderer per rank (gsm_global_create on that rank's GPU; every rank with the same
  * max_width / max_height).  Set-up is collective and happens once, in two steps around an
  * exchange the caller performs with any transport (torch.distributed, MPI, sockets, ...):
- *   gsm_multigpu_prepare   allocates this rank's exchange memory (uncached device memory:
+ *   gsm_multigpu_prepare   allocates this rank's exchange memory (fine-grained device memory:
  *                          control words, 2 x W x W counts, max_gaussians x 48-B records,
- *                          and on rank 0 the gathered frame, max_width x max_height pixels)
- *                          and writes its GSM_MULTIGPU_HANDLE_BYTES handle into `handle`;
+ *                          and on rank 0 the gathered colour frame and r16f depth frame,
+ *                          max_width x max_height pixels each) and the renderer's partition
+ *                          buffers, and writes its GSM_MULTIGPU_HANDLE_BYTES handle into `handle`.
+ *                          GSM_MG_MEM=cached (ordinary device memory; one GPU only: refused at
+ *                          connect across processes) is the A/B of DESIGN.md 7;
+ *                          GSM_MG_MEM=uncached returns GSM_ERR_UNSUPPORTED;
  *   (caller)               all-gathers the handles: all[r * GSM_MULTIGPU_HANDLE_BYTES] = rank r's;
  *   gsm_multigpu_connect   opens every peer's exchange memory (hipIpcOpenMemHandle; a handle
  *                          from the same process is used directly) and checks that the ranks
- *                          agree on the world and the frame limits.
+ *                          agree on the world, the frame limits and the row layout
+ *                          (GSM_MG_ROWS): GSM_ERR_INVALID_ARGUMENT otherwise.
  * The frame capacity is the smallest max_gaussians of all ranks (a slab receives every id at
  * most once): a frame with more gaussians returns GSM_ERR_INVALID_GAUSSIAN_COUNT on every rank
  * alike, before anything is enqueued.
@@ -99,16 +106,25 @@ void gsm_multigpu_destroy(gsm_multigpu *multigpu);
  *   2. every record written straight into its slab owner's receive buffer (offsets from the
  *      count matrix: rank order), flag barrier;
  *   3. the owner renders its rows from the received records (their count read on the device);
- *      colour goes to rank 0's gathered frame when gathering, else to the rank's own color
- *      target (full-frame addressed, rows outside the slab untouched); depth always to the
- *      rank's own depth target (nullable);
- *   4. gathering: every rank signals rank 0, whose stream waits for all slabs; a gather_color
- *      other than gsm_multigpu_frame's buffer then receives a copy of the frame.
+ *      when gathering, colour goes to rank 0's gathered frame and -- when depth_r16f is non-NULL
+ *      -- depth to rank 0's gathered depth frame (GlobalRenderer.swift:350 writes depth with
+ *      every frame); without gathering both go to the rank's own targets (full-frame addressed,
+ *      rows outside the slab untouched; depth nullable);
+ *   4. gathering: every rank's blend signals rank 0, whose stream waits for all slabs; a
+ *      gather_color other than gsm_multigpu_frame's buffer (a depth_r16f other than
+ *      gsm_multigpu_frame_depth's) then receives a copy of the frame.
  * Gathering: gather_color non-NULL on every rank (ranks other than 0 pass any non-NULL value;
- * their color may then be NULL).  No host synchronisation anywhere in the frame.  A barrier
- * that waits longer than the timeout (default 10 s; a peer that never calls) gives up, counts
- * the event (gsm_multigpu_status) and lets the frame finish with undefined pixels: no wait on
- * the device is unbounded. */
+ * their color may then be NULL); depth gathered when depth_r16f is non-NULL, the same choice on
+ * every rank (ranks other than 0 pass any non-NULL value).  No host synchronisation anywhere in
+ * the frame.
+ * Errors: everything a rank could refuse is checked before it enqueues anything; a refused rank
+ * returns the error but still performs every barrier step of the frame (zero counts, arrivals
+ * marked failed), so the ranks stay in step and the next frame renders normally; its peers finish
+ * the frame without its records or band and count a failed peer arrival (gsm_multigpu_errors).
+ * A barrier that waits longer than the timeout (default 10 s; a peer that never calls) gives up,
+ * counts the event (gsm_multigpu_status) and lets the frame finish with undefined pixels (the
+ * frame's later waits are skipped; the next frame waits again): no wait on the device is
+ * unbounded. */
 gsm_status gsm_multigpu_render(gsm_multigpu *multigpu, void *stream, const gsm_gaussian_input *input,
                                const gsm_camera_params *camera, uint32_t width, uint32_t height,
                                void *color_rgba16f, size_t color_pitch_bytes, void *depth_r16f,
@@ -118,15 +134,26 @@ gsm_status gsm_multigpu_render(gsm_multigpu *multigpu, void *stream, const gsm_g
  * *pitch_bytes = max_width x bytes per pixel of the configured colour format.  Passing it as
  * gather_color skips the copy.  Other ranks: *color = NULL. */
 gsm_status gsm_multigpu_frame(gsm_multigpu *multigpu, void **color, size_t *pitch_bytes);
+/* Rank 0's gathered r16f depth frame (library memory): *depth = its device pointer, *pitch_bytes its
+ * row pitch.  Passing it as depth_r16f skips the copy.  Other ranks: *depth = NULL. */
+gsm_status gsm_multigpu_frame_depth(gsm_multigpu *multigpu, void **depth, size_t *pitch_bytes);
 
 /* Barrier timeouts since create (or the last clear), synchronous: 0 on a healthy run. */
 gsm_status gsm_multigpu_status(gsm_multigpu *multigpu, uint32_t *timeouts, int clear);
+/* Barrier timeouts and failed peer arrivals (a peer's frame was refused: its arrival carried the
+ * failure mark) since create or the last clear, synchronous: 0 and 0 on a healthy run. */
+gsm_status gsm_multigpu_errors(gsm_multigpu *multigpu, uint32_t *timeouts, uint32_t *failed_peer_arrivals,
+                               int clear);
 /* Barrier timeout in milliseconds (default 10000, at least 1). */
 gsm_status gsm_multigpu_set_timeout_ms(gsm_multigpu *multigpu, uint32_t ms);
 
 /* Rank 0: copy rows [0, height) x width pixels of the gathered frame into host memory (dst_pitch
  * bytes per row), synchronous (after the frame's stream work); GSM_ERR_INVALID_ARGUMENT elsewhere. */
 gsm_status gsm_multigpu_debug_copy_frame(gsm_multigpu *multigpu, void *host_dst, size_t dst_pitch_bytes,
+                                         uint32_t width, uint32_t height);
+
+/* Rank 0: the same for the gathered r16f depth frame (dst_pitch >= 2 x width). */
+gsm_status gsm_multigpu_debug_copy_depth(gsm_multigpu *multigpu, void *host_dst, size_t dst_pitch_bytes,
                                          uint32_t width, uint32_t height);
 
 /* The first `bytes` of this rank's exchange allocation (control words from byte 0, the count matrix
@@ -137,7 +164,9 @@ gsm_status gsm_multigpu_debug_copy_exchange(gsm_multigpu *multigpu, void *host_d
 gsm_status gsm_multigpu_debug_counts(gsm_multigpu *multigpu, uint32_t *host_counts);
 
 /* gsm_multigpu_render in four phases (0: projection + counts + barrier; 1: records + barrier;
- * 2: slab render + the gather signal; 3: rank 0's gather wait + copy); render = phases 0..3.
+ * 2: slab render + the gather signal; 3: rank 0's gather wait + copy); render = phases 0..3, each
+ * called even after an earlier phase of the frame returned an error (GSM_ERR_INVALID_ARGUMENT and
+ * nothing enqueued for a phase out of order).
  * For W ranks driven from ONE host thread (virtual ranks of a test or a timing tool, e.g. W
  * renderers on one GPU sharing one stream): issue phase p of every rank before phase p + 1 of
  * any, so that every barrier waits only for work enqueued before it. */

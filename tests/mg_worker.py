@@ -5,10 +5,14 @@ through their IPC mappings, the flag barriers across the processes, the slab ren
 straight into rank 0's gathered frame -- is the product path of libgsm_amd.so.
 
 Frames (same scene every rank, generated from the seed):
-  A  gathered into the library frame (gather_target = MultiGpuRenderer.frame()), read back on rank 0
-  B  the next camera, gathered into a caller tensor (the library's copy)
+  A  gathered with depth into the library frames (MultiGpuRenderer.frame() / frame_depth()), read
+     back on rank 0
+  B  the next camera, gathered with depth into caller tensors (the library's copies)
   C  not gathered: every rank writes its band into its own colour/depth targets
-Rank 0 writes A and B, and every rank its band of C, as .npy files into --out, plus status.json."""
+  D  rank 1 passes a width over the maximum: it alone refuses the frame, but still performs every
+     barrier step (arrivals marked failed); the others finish it
+  E  the frame of A again on every rank: bit-exact, the ranks still in step after D
+Rank 0 writes A, B and E, and every rank its band of C, as .npy files into --out, plus status.json."""
 import argparse
 import json
 import os
@@ -66,21 +70,25 @@ def main():
                 result["refused"] = e.status == gsm_amd.Status.INVALID_GAUSSIAN_COUNT
             return
         frame_ptr, _ = mg.frame()
-        # A: into the library frame (zero copy)
+        # A: into the library frames (zero copy), colour and depth
         for _ in range(2):  # a second frame reuses every mapping and flag
             mg.render(None, None, inp, gsm_amd.CameraParams.from_dict(cam_d), w, h, gather=True, stream=stream,
-                      gather_target=frame_ptr if a.rank == 0 else None)
+                      gather_target=frame_ptr if a.rank == 0 else None, gather_depth=True)
         torch.cuda.synchronize()
         dist.barrier()
         if a.rank == 0:
             np.save(os.path.join(a.out, "frame_a.npy"), mg.copy_frame(w, h))
-        # B: the next camera, gathered into a caller tensor on rank 0
+            np.save(os.path.join(a.out, "depth_a.npy"), mg.copy_depth(w, h))
+        # B: the next camera, gathered into caller tensors on rank 0
         cam_b = scenes.orbit_camera(w, h, 3.0)
         color = torch.full((h, w, 4), float("nan"), dtype=torch.float16, device=dev) if a.rank == 0 else None
-        mg.render(color, None, inp, gsm_amd.CameraParams.from_dict(cam_b), w, h, gather=True, stream=stream)
+        depth = torch.full((h, w), float("nan"), dtype=torch.float16, device=dev) if a.rank == 0 else None
+        mg.render(color, depth, inp, gsm_amd.CameraParams.from_dict(cam_b), w, h, gather=True, stream=stream,
+                  gather_depth=True)
         torch.cuda.synchronize()
         if a.rank == 0:
             np.save(os.path.join(a.out, "frame_b.npy"), color.view(torch.int16).cpu().numpy().view(np.uint16))
+            np.save(os.path.join(a.out, "depth_b.npy"), depth.view(torch.int16).cpu().numpy().view(np.uint16))
         # C: no gather -- every rank's band in its own targets
         color = torch.full((h, w, 4), float("nan"), dtype=torch.float16, device=dev)
         depth = torch.full((h, w), float("nan"), dtype=torch.float16, device=dev)
@@ -90,6 +98,26 @@ def main():
         np.save(os.path.join(a.out, f"band_c_depth_{a.rank}.npy"), depth.view(torch.int16).cpu().numpy().view(np.uint16))
         result["counts"] = mg.counts().tolist()
         result["timeouts"] = mg.status()
+        if a.world > 1:
+            # D: rank 1 alone refuses the frame (width over the maximum); every rank stays in step
+            torch.cuda.synchronize()
+            dist.barrier()
+            try:
+                mg.render(None, None, inp, gsm_amd.CameraParams.from_dict(cam_d), w + (1 if a.rank == 1 else 0), h,
+                          gather=True, stream=stream, gather_target=frame_ptr if a.rank == 0 else None,
+                          gather_depth=True)
+                result["d_status"] = 0
+            except gsm_amd.RendererError as e:
+                result["d_status"] = int(e.status)
+            torch.cuda.synchronize()
+            # E: the frame of A on every rank again
+            mg.render(None, None, inp, gsm_amd.CameraParams.from_dict(cam_d), w, h, gather=True, stream=stream,
+                      gather_target=frame_ptr if a.rank == 0 else None, gather_depth=True)
+            torch.cuda.synchronize()
+            if a.rank == 0:
+                np.save(os.path.join(a.out, "frame_e.npy"), mg.copy_frame(w, h))
+                np.save(os.path.join(a.out, "depth_e.npy"), mg.copy_depth(w, h))
+            result["timeouts_de"], result["failed_peer_arrivals"] = mg.errors()
     finally:
         torch.cuda.synchronize()
         dist.barrier()  # no rank unmaps its exchange memory while a peer may still write into it

@@ -480,3 +480,31 @@ def test_color_formats(gsm, cuda, oracle, fmt):
         r.render(color, dep, inp, gsm.CameraParams.from_dict(case["cam"]), w, h,
                  color_pitch=w * gsm.ColorFormat(fmt).bytes_per_pixel + 2)
     r.close()
+
+
+def test_assignment_total_past_2_32_clamps_with_overflow(gsm, cuda):
+    """A frame whose assignment total passes 2^32 by less than its capacity (265 126 screen-covering
+    gaussians x 16 200 tiles of 3840x2160 = 2^32 + 73 904): a 32-bit scan of the block sums would wrap
+    the total to 73 904 < 4N and sort a garbage frame without the overflow flag.  The exact scan
+    (k_scan_blocks) clamps it to 4N with overflow = 1, as the reference's clamp does
+    (GlobalShaders.metal:696-701).  No oracle: 4.3G tile tests are out of reach on the CPU."""
+    from gsm_amd.types import WORLD32
+    n, w, h = 265_126, 3840, 2160
+    assert n * 120 * 135 - 2 ** 32 == 73_904
+    world = np.zeros(n, WORLD32)
+    world["pz"], world["opacity"] = 5.0, 0.99
+    world["sx"] = world["sy"] = world["sz"] = 50.0  # sigma clamped to 2 * 3840 / 3 px: every tile
+    world["rot"][:, 3] = 1.0
+    harm = np.tile(np.array([0.3, 0.2, 0.1], np.float32), n)
+    from gsm_amd import scenes
+    cam = scenes.make_camera(w, h)
+    rend = gsm.GlobalRenderer(config=gsm.RendererConfig(max_gaussians=n, max_width=w, max_height=h, precision=0,
+                                                        gaussian_color_space=0))
+    color = cuda.empty((h, w, 4), dtype=cuda.float16, device="cuda")
+    rend.render(color, None, gsm.GaussianInput(to_dev(cuda, world), to_dev(cuda, harm), n, 1),
+                gsm.CameraParams.from_dict(cam), w, h)
+    cuda.cuda.synchronize()
+    c = rend.counters()
+    assert c["overflow"] == 1
+    assert c["total_assignments"] == 4 * n
+    rend.close()

@@ -1,6 +1,6 @@
 """The N > 1 product path of include/gsm_multigpu.h with real processes, on one MI355X.
 
-Two (three) rank processes share GPU 0 (tests/mg_worker.py): each owns an uncached exchange
+Two to four rank processes share GPU 0 (tests/mg_worker.py): each owns a fine-grained exchange
 allocation, the handles go over torch.distributed (gloo) and every rank opens its peers' allocations
 with hipIpcOpenMemHandle -- the set-up the 8-GPU node runs, where the mappings cross xGMI.  Per frame
 every record is stored by k_part_push straight into another process's receive buffer, the count
@@ -62,11 +62,20 @@ def test_processes_on_one_gpu_render_the_oracle_frame(oracle, tmp_path, monkeypa
     assert all(s["timeouts"] == 0 for s in st)
     world_np, harm_np, cam_d = scenes.gen_scene(n, w, h, sh, prec, seed=11)
     ref = oracle.render(world_np, harm_np, sh, cam_d, w, h, max_gaussians=n)
-    # A: gathered into the library frame across the processes
+    # A: gathered into the library frames (colour and depth) across the processes
     assert np.array_equal(np.load(tmp_path / "frame_a.npy"), ref["color"])
-    # B: next camera, the library's copy into the caller's tensor
+    assert np.array_equal(np.load(tmp_path / "depth_a.npy"), ref["depth"])
+    # B: next camera, the library's copies into the caller's tensors
     ref_b = oracle.render(world_np, harm_np, sh, scenes.orbit_camera(w, h, 3.0), w, h, max_gaussians=n)
     assert np.array_equal(np.load(tmp_path / "frame_b.npy"), ref_b["color"])
+    assert np.array_equal(np.load(tmp_path / "depth_b.npy"), ref_b["depth"])
+    # D / E: rank 1 alone refused frame D (INVALID_DIMENSIONS) but kept every barrier step; the others
+    # finished it without timing out and counted its failed arrivals; frame E is bit-exact again
+    assert st[1]["d_status"] == 7 and all(s["d_status"] == 0 for r, s in enumerate(st) if r != 1)
+    assert all(s["timeouts_de"] == 0 for s in st)
+    assert st[0]["failed_peer_arrivals"] >= 1
+    assert np.array_equal(np.load(tmp_path / "frame_e.npy"), ref["color"])
+    assert np.array_equal(np.load(tmp_path / "depth_e.npy"), ref["depth"])
     # C: each rank's tile rows (a contiguous block, or r, r + W, ... interleaved) in its own targets
     from gsm_amd import exchange
     tiles_y = (h + 15) // 16
@@ -87,8 +96,9 @@ def test_processes_on_one_gpu_render_the_oracle_frame(oracle, tmp_path, monkeypa
 
 
 def test_processes_refuse_a_frame_over_the_smallest_capacity(tmp_path):
-    """A rank sized for less than the frame: every rank returns INVALID_GAUSSIAN_COUNT before any
-    barrier (no rank waits, no peer's receive buffer is overrun)."""
+    """A rank sized for less than the frame: every rank returns INVALID_GAUSSIAN_COUNT before it
+    enqueues any work of the frame (its barrier steps still run, marked failed: no rank waits for a
+    peer that stopped, no peer's receive buffer is overrun)."""
     st = _run_ranks(tmp_path, 2, ["--n", "20000", "--cap", "15000"])
     assert all(s["refused"] for s in st)
 
@@ -107,22 +117,23 @@ def _virtual_frame(gsm, cuda, world, n, w, h, sh, prec, seed, cams):
     mgs = [m.connect_handles(handles) for m, _ in pre]
     frame_ptr, _ = mgs[0].frame()
     stream = cuda.cuda.current_stream()
-    frames = []
+    frames, depths = [], []
     for cam in cams:
         cp = gsm.CameraParams.from_dict(cam)
         for ph in range(4):  # phase p of every rank before phase p + 1 of any (one stream)
             for k, m in enumerate(mgs):
                 m.render_phases([ph], None, None, inp, cp, w, h, gather=True, stream=stream,
-                                gather_target=frame_ptr if k == 0 else None)
+                                gather_target=frame_ptr if k == 0 else None, gather_depth=True)
         cuda.cuda.synchronize()
         frames.append(mgs[0].copy_frame(w, h))
+        depths.append(mgs[0].copy_depth(w, h))
     counts = mgs[0].counts()
     timeouts = [m.status() for m in mgs]
     for m in mgs:
         m.close()
     for r in rends:
         r.close()
-    return frames, counts, timeouts
+    return frames, counts, timeouts, depths
 
 
 @pytest.mark.parametrize("world,n,w,h,prec,rows", [(2, 40_000, 640, 360, 1, "contiguous"),
@@ -140,25 +151,28 @@ def test_virtual_ranks_product_path(gsm, cuda, oracle, monkeypatch, world, n, w,
     monkeypatch.setenv("GSM_MG_ROWS", rows)
     sh = 16 if prec else 4
     cams = [scenes.make_camera(w, h), scenes.orbit_camera(w, h, 5.0)]
-    frames, counts, timeouts = _virtual_frame(gsm, cuda, world, n, w, h, sh, prec, 78, cams)
+    frames, counts, timeouts, depths = _virtual_frame(gsm, cuda, world, n, w, h, sh, prec, 78, cams)
     assert timeouts == [0] * world
     world_np, harm_np, _ = scenes.gen_scene(n, w, h, sh, prec, seed=78)
-    for i, (got, cam) in enumerate(zip(frames, cams)):
+    for i, (got, gd, cam) in enumerate(zip(frames, depths, cams)):
         ref = oracle.render(world_np, harm_np, sh, cam, w, h, max_gaussians=n)
         bad = np.nonzero(np.any(got != ref["color"], axis=(1, 2)))[0]
         assert len(bad) == 0, f"frame {i}: {len(bad)} rows differ, first {bad[:16].tolist()}"
+        assert np.array_equal(gd, ref["depth"]), f"frame {i}: gathered depth differs"
     assert counts.shape == (world, world)
 
 
 def test_config4_virtual_ranks_full_size(gsm, cuda, oracle):
     """BASELINE config 4: 5M gaussians, SH3, 3840x2160, fp16, partitioned over 8 ranks (virtual ranks
-    on one GPU, the product kernels and uncached exchange buffers) -- bit-exact with the oracle."""
+    on one GPU, the product kernels and fine-grained exchange memory) -- colour and gathered depth
+    bit-exact with the oracle."""
     from gsm_amd import scenes
     c = scenes.CONFIGS["cfg3_5m_sh3_4k_f16"]
     n, w, h, sh, prec = c["count"], c["width"], c["height"], c["sh"], c["precision"]
     world_np, harm_np, cam_d = scenes.gen_scene(n, w, h, sh, prec, seed=42)
-    frames, counts, timeouts = _virtual_frame(gsm, cuda, 8, n, w, h, sh, prec, 42, [cam_d])
+    frames, counts, timeouts, depths = _virtual_frame(gsm, cuda, 8, n, w, h, sh, prec, 42, [cam_d])
     assert timeouts == [0] * 8
     ref = oracle.render(world_np, harm_np, sh, cam_d, w, h, max_gaussians=n, nthreads=min(16, os.cpu_count() or 1))
     assert np.array_equal(frames[0], ref["color"])
+    assert np.array_equal(depths[0], ref["depth"])
     assert counts.sum() >= int(np.count_nonzero(ref["tile_counts"]))

@@ -62,7 +62,7 @@ def main():
             for k, m in enumerate(mgs):
                 e0, e1 = ev(), ev()
                 e0.record(stream)
-                m.render_phases([p], None, None, inp, cam, w, h, gather=True, stream=stream,
+                m.render_phases([p], None, None, inp, cam, w, h, gather=True, gather_depth=True, stream=stream,
                                 gather_target=frame_ptr if k == 0 else None)
                 e1.record(stream)
                 marks.append((p, k, e0, e1))
@@ -127,12 +127,38 @@ def main():
         one_gpu = e0.elapsed_time(e1) / (a.frames * 4)
         one.close()
     med = np.median(ph, axis=0)  # [phase][rank]
+    # xGMI model (not a measurement: the virtual ranks' pushes and pixels stay in one GPU's HBM).
+    # counts[r][s] = records rank r sends to slab s; every cross-rank record is 48 B (SplatRecord)
+    # over the (r, s) link; rank 0 receives every other band's pixels (rgba16f + r16f = 10 B) over
+    # that rank's link.  MI355X: 7 xGMI links per GPU, ~153 GB/s each, point to point,
+    # all links concurrently; the stores stream while the producing kernel runs, so a phase takes
+    # at least max(its device time, its busiest link's bytes / 153 GB/s).
+    link_gbs = 153.0
+    cm = mgs[0].counts().astype(np.int64)
+    rec_link = cm * 48
+    np.fill_diagonal(rec_link, 0)
+    tiles_y = (h + 15) // 16
+    per_rows = (tiles_y + W - 1) // W
+    band_px = [max(0, min(h, min(tiles_y, (r + 1) * per_rows) * 16) - min(h, min(tiles_y, r * per_rows) * 16)) * w
+               for r in range(W)]
+    pix_link = [band_px[r] * 10 if r else 0 for r in range(W)]
+    t_push = float(rec_link.max()) / (link_gbs * 1e9) * 1e3
+    t_pix = float(max(pix_link)) / (link_gbs * 1e9) * 1e3
+    mp = [float(med[p].max()) for p in range(4)]
+    model_frame = mp[0] + max(mp[1], t_push) + max(mp[2], t_pix) + mp[3]
+    xgmi = {"link_gb_per_s": link_gbs, "records_out_bytes_per_rank": [int(x) for x in rec_link.sum(axis=1)],
+            "busiest_link_records_bytes": int(rec_link.max()), "rank0_pixel_in_bytes": int(sum(pix_link)),
+            "busiest_link_pixel_bytes": int(max(pix_link)), "push_link_ms": round(t_push, 4),
+            "pixel_link_ms": round(t_pix, 4), "modelled_frame_ms": round(model_frame, 4),
+            "note": "MODEL, not measured: each phase >= its busiest link's bytes at 153 GB/s (7 concurrent "
+                    "point-to-point links per GPU); device phases measured on one GPU"}
     out = {"config": a.config, "world": W, "frames": a.frames, "timeouts": [m.status() for m in mgs],
            "counts": mgs[0].counts().tolist(),
            "phase_ms": {f"phase{p}": [round(float(x), 4) for x in med[p]] for p in range(4)},
            "max_phase_ms": [round(float(med[p].max()), 4) for p in range(4)],
            "device_frame_ms": round(float(sum(med[p].max() for p in range(4))), 4),
            "slab_stages_ms": stages, "blend_trace": trace,
+           "xgmi_model": xgmi,
            "one_gpu_frame_ms": round(one_gpu, 4) if one_gpu else None,
            "device_speedup": round(one_gpu / float(sum(med[p].max() for p in range(4))), 3) if one_gpu else None,
            "note": "virtual ranks on one GPU, product kernels, one stream; no xGMI (pushes and pixels stay local)"}

@@ -113,6 +113,26 @@ __global__ __launch_bounds__(NT) void k_blend_px(
     // write (GlobalShaders.metal:1152-1186): one pixel pair (px, py), (px + 1, py) in the target's
     // format (flags bits 4-7, gsm_color_format; conversion rules in include/gsm_renderer.h)
     const int colorFmt = (flags >> 4) & 15;
+    // flags bit 10: the targets are rank 0's gathered frame of a multi-GPU frame -- every pixel store
+    // system-coherent write-through (gsm_internal.h: the wave's arrival at the end then only drains)
+    const bool wt = (flags & 1024) != 0;
+    const uint32_t colorBytes = (uint32_t)(colorPitch * H), depthBytes = (uint32_t)(depthPitch * H);
+    auto st128 = [&](uint8_t* p, uint4 v) {
+        if (wt) st_sys128_at(color, colorBytes, (uint32_t)(p - color), v);
+        else *(uint4*)p = v;
+    };
+    auto st32 = [&](uint8_t* p, uint32_t v) {
+        if (wt) st_sys32_at(color, colorBytes, (uint32_t)(p - color), v);
+        else *(uint32_t*)p = v;
+    };
+    auto std32 = [&](uint8_t* p, uint32_t v) {
+        if (wt) st_sys32_at(depth, depthBytes, (uint32_t)(p - depth), v);
+        else *(uint32_t*)p = v;
+    };
+    auto std16 = [&](uint8_t* p, uint16_t v) {
+        if (wt) st_sys16_at(depth, depthBytes, (uint32_t)(p - depth), v);
+        else *(uint16_t*)p = v;
+    };
     auto write_pair = [&](uint32_t px, uint32_t py, h2 Av, h2 Rq, h2 Gq, h2 Bq, h2 Dq) {
         if (py >= H) return;
         uint8_t* crow = color + (size_t)py * colorPitch;
@@ -125,15 +145,15 @@ __global__ __launch_bounds__(NT) void k_blend_px(
             const uint32_t p1a = (ur >> 16) | (ug & 0xFFFF0000u);
             const uint32_t p1b = (ub >> 16) | (ua & 0xFFFF0000u);
             if ((flags & 1) && px + 1 < W) {
-                *(uint4*)(crow + (size_t)px * 8) = make_uint4(p0a, p0b, p1a, p1b);
+                st128(crow + (size_t)px * 8, make_uint4(p0a, p0b, p1a, p1b));
             } else {
                 if (px < W) {  // 4-byte stores: any 4-byte aligned pitch
-                    ((uint32_t*)(crow + (size_t)px * 8))[0] = p0a;
-                    ((uint32_t*)(crow + (size_t)px * 8))[1] = p0b;
+                    st32(crow + (size_t)px * 8, p0a);
+                    st32(crow + (size_t)px * 8 + 4, p0b);
                 }
                 if (px + 1 < W) {
-                    ((uint32_t*)(crow + (size_t)(px + 1) * 8))[0] = p1a;
-                    ((uint32_t*)(crow + (size_t)(px + 1) * 8))[1] = p1b;
+                    st32(crow + (size_t)(px + 1) * 8, p1a);
+                    st32(crow + (size_t)(px + 1) * 8 + 4, p1b);
                 }
             }
         } else {
@@ -144,14 +164,13 @@ __global__ __launch_bounds__(NT) void k_blend_px(
                 float c[4] = {h_bits_to_f((uint16_t)(ur >> sh)), h_bits_to_f((uint16_t)(ug >> sh)),
                               h_bits_to_f((uint16_t)(ub >> sh)), h_bits_to_f((uint16_t)(ua >> sh))};
                 if (colorFmt == GSM_COLOR_FORMAT_RGBA32F) {
-                    float* o = (float*)(crow + (size_t)(px + i) * 16);
+                    uint8_t* o = crow + (size_t)(px + i) * 16;
                     if (flags & 1) {
-                        *(float4*)o = make_float4(c[0], c[1], c[2], c[3]);
+                        st128(o, make_uint4(__float_as_uint(c[0]), __float_as_uint(c[1]), __float_as_uint(c[2]),
+                                            __float_as_uint(c[3])));
                     } else {
-                        o[0] = c[0];
-                        o[1] = c[1];
-                        o[2] = c[2];
-                        o[3] = c[3];
+#pragma unroll
+                        for (int k = 0; k < 4; ++k) st32(o + 4 * k, __float_as_uint(c[k]));
                     }
                     continue;
                 }
@@ -166,15 +185,15 @@ __global__ __launch_bounds__(NT) void k_blend_px(
                 }
                 const bool bgra = colorFmt >= GSM_COLOR_FORMAT_BGRA8_UNORM;
                 const uint32_t px32 = (bgra ? u8[2] : u8[0]) | (u8[1] << 8) | ((bgra ? u8[0] : u8[2]) << 16) | (u8[3] << 24);
-                *(uint32_t*)(crow + (size_t)(px + i) * 4) = px32;
+                st32(crow + (size_t)(px + i) * 4, px32);
             }
         }
         if (depth) {
             if ((flags & 1) && px + 1 < W) {
-                *(uint32_t*)(depth + (size_t)py * depthPitch + (size_t)px * 2) = ud;
+                std32(depth + (size_t)py * depthPitch + (size_t)px * 2, ud);
             } else {
-                if (px < W) *(uint16_t*)(depth + (size_t)py * depthPitch + (size_t)px * 2) = (uint16_t)(ud & 0xFFFFu);
-                if (px + 1 < W) *(uint16_t*)(depth + (size_t)py * depthPitch + (size_t)(px + 1) * 2) = (uint16_t)(ud >> 16);
+                if (px < W) std16(depth + (size_t)py * depthPitch + (size_t)px * 2, (uint16_t)(ud & 0xFFFFu));
+                if (px + 1 < W) std16(depth + (size_t)py * depthPitch + (size_t)(px + 1) * 2, (uint16_t)(ud >> 16));
             }
         }
     };
@@ -625,8 +644,8 @@ __global__ __launch_bounds__(NT) void k_blend_px(
     }
     if (unitCost && lane == 0 && waveMax) atomicMax(&costMax[(blockIdx.x * NW + wv) % kCostMaxSlots], waveMax);
     // multi-GPU frame gathered on rank 0 (gsm_multigpu.hip): the pixels this wave stored into rank
-    // 0's frame are released at system scope, and the wave arrives at barrier 2 (the last one raises
-    // the flags) -- every wave of the grid arrives exactly once, here
+    // 0's frame (write-through, flags bit 10) are drained and the wave arrives at barrier 2 (the last
+    // one raises the flags) -- every wave of the grid arrives exactly once, here
     if (arrive.done) mg_arrive_wave(arrive);
 }
 
@@ -670,7 +689,8 @@ void launch_blend(const FrameGeometry& g, const DeviceArena& A, void* color,
                      (depth == nullptr || ((((uintptr_t)depth) & 7u) == 0 && (depthPitch & 7u) == 0)))
                         ? 1
                         : 0;
-    const int flags = vec | 2 | (costOrder ? 4 : 0) | ((colorFormat & 15) << 4) | ((claim & 3) << 8);
+    const int flags = vec | 2 | (costOrder ? 4 : 0) | ((colorFormat & 15) << 4) | ((claim & 3) << 8) |
+                      (arrive ? 1024 : 0);  // (a gathered multi-GPU frame: write-through pixel stores)
     // A.tileQueue was zeroed by k_scan_blocks earlier in the frame
     const int P = blend_pairs_per_lane(numTiles, numCUs);
     const int waves = wavesOverride ? wavesOverride : blend_waves_per_wg(numTiles, numCUs);

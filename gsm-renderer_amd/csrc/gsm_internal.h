@@ -58,13 +58,16 @@ struct PartitionBuffers {
 
 // ---------------------------------------------------------------------------
 // Multi-GPU frame (gsm_multigpu.hip): memory model of the exchange.
-// A producing kernel arrives at a barrier itself: every unit of it that stored exchange data (a
-// wave, or a workgroup after a barrier) ends with a SYSTEM-scope release -- `buffer_wbl2 sc0 sc1`
-// writes back its XCD's L2, the wait makes it complete -- and one device-scope add to the rank's
-// arrival counter; the unit whose add completes the count raises this rank's flag word of the
-// barrier in every rank's control block (system-scope stores) and re-arms the counter.  Every
-// consumer load of exchange data is system-coherent (`sc0 sc1`: ld_sys32 / ld_sys128 below), so
-// no L1 or L2 line that predates the flag can serve it, on any XCD of any GPU.
+// Every store of exchange data (counts, records, the gathered pixels) is a SYSTEM-coherent
+// write-through store (`sc0 sc1`: st_sys* below) -- it leaves no dirty line in any L2 and is
+// acknowledged only once it is visible at system scope.  A producing kernel arrives at a barrier
+// itself: every storing unit (a wave, or a workgroup after a barrier) drains its stores
+// (`s_waitcnt vmcnt(0)`), then makes one device-scope add to the rank's arrival counter; the unit
+// whose add completes the count raises this rank's flag word of the barrier in every rank's control
+// block (system-coherent stores) and re-arms the counter.  Every consumer load of exchange data is
+// system-coherent (`sc0 sc1`: ld_sys*), so no L1 or L2 line that predates the flag can serve it, on
+// any XCD of any GPU.  (r04: a system-scope release -- buffer_wbl2 sc0 sc1 -- in every storing unit
+// instead of write-through stores cost the config-4 virtual-rank frame 0.272 -> 0.372 ms.)
 // ---------------------------------------------------------------------------
 struct MgArrive {
     uint32_t* flag[kMaxSlabs];  // this rank's word of the barrier in rank p's control block (peer mappings)
@@ -74,45 +77,84 @@ struct MgArrive {
     uint32_t world;
 };
 
-// One arriving unit: called by every lane of ONE wave, after every store the unit signals for
-// (a workgroup arriving as one unit: every wave's `s_waitcnt vmcnt(0)`, then a workgroup barrier,
-// then one wave calls this).
+// One arriving unit: called by every lane of ONE wave, after every exchange store the unit signals
+// for (a workgroup arriving as one unit: every wave's `s_waitcnt vmcnt(0)`, then a workgroup
+// barrier, then one wave calls this).
 __device__ __forceinline__ void mg_arrive_wave(const MgArrive& a) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");      // system scope: buffer_wbl2 sc0 sc1
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the write-back is complete before the add
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's write-through stores are acknowledged
     uint32_t last = 0;
     if ((threadIdx.x & 63u) == 0)
         last = __hip_atomic_fetch_add(a.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == a.total - 1u ? 1u : 0u;
     if (__builtin_amdgcn_readfirstlane(last)) {
-        // every other unit released its stores before its add: acquire them, release to the peers
-        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "");
+        // every other unit drained its stores before its add: the flags go out after all of them
         const uint32_t lane = threadIdx.x & 63u;
         if (lane == 0) __hip_atomic_store(a.done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (lane < a.world) __hip_atomic_store(a.flag[lane], a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
-// a workgroup of NT threads arriving as one unit (see mg_arrive_wave); ends the kernel's use of it
+// a workgroup arriving as one unit (see mg_arrive_wave); ends the kernel's use of it
 __device__ __forceinline__ void mg_arrive_block(const MgArrive& a) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x < 64u) mg_arrive_wave(a);
 }
+// The multi-GPU frame's direct push (k_project_part, gsm_multigpu.hip): the receive slots of every
+// rank are indexed by GLOBAL gaussian id -- rank r projects ids [first, first + count), first a multiple
+// of 256 -- so a record needs no offset from a count exchange: gaussian g's record for slab s goes to
+// slot g of rank s's receive buffer, and bit g of rank s's slot mask says whether it is there (every
+// wave writes the 64-bit mask word of its 64 ids for every slab, also when it is zero).  The owner
+// renders its slots in id order: the stable sort's tie order without any gather.
+struct MgPush {
+    SplatRecord* recv[kMaxSlabs];             // slot 0 of rank s's receive buffer (peer mappings)
+    unsigned long long* mask[kMaxSlabs];      // word 0 of rank s's slot mask
+    uint32_t first;                           // this rank's first id (the launch's gid 0)
+    uint32_t slots;                           // slots of every receive buffer (the frame's N)
+    MgArrive arrive;                          // barrier 1: every workgroup after its stores
+};
+// The owner's view of its slots (k_records_in): which ids hold a record this frame
+struct SlotIn {
+    const unsigned long long* mask;  // bit g: slot g holds a record (null: dense records)
+    const uint32_t* failedEpoch;     // [world]: == epoch when that source's frame failed (its slots are void)
+    uint32_t epoch, perIds;          // the frame; ids per source rank (a multiple of 256)
+};
 // k_part_scan's count publication: row `rank` of rank p's count matrix (this frame's parity), and
 // the arrival at barrier 0 (arrive.done == null: no publication, the send-buffer path)
 struct CountPublish {
     uint32_t* row[kMaxSlabs];
     MgArrive arrive;
 };
-// system-coherent loads of exchange data (sc0 sc1: no cached copy can answer them)
+// system-coherent access to exchange data (sc0 sc1): loads no cached copy can answer, write-through
+// stores; `base` wave-uniform, `bytes` its extent (the buffer descriptor's range), i in elements
+constexpr int kSysCoherent = 17;  // cache-policy bits sc0 | sc1
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t sys_rsrc(const void* base, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)bytes, 0x00020000);
+}
 __device__ __forceinline__ uint32_t ld_sys32(const uint32_t* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
-// 16-B word i of a wave-uniform base of `bytes` bytes
+__device__ __forceinline__ unsigned long long ld_sys64(const unsigned long long* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 __device__ __forceinline__ uint4 ld_sys128(const void* base, uint32_t bytes, uint32_t i) {
-    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)bytes, 0x00020000);
-    const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)(i * 16u), 0, 17 /* sc0 | sc1 */);
+    const auto v = __builtin_amdgcn_raw_buffer_load_b128(sys_rsrc(base, bytes), (int)(i * 16u), 0, kSysCoherent);
     return make_uint4(v[0], v[1], v[2], v[3]);
+}
+__device__ __forceinline__ void st_sys128(void* base, uint32_t bytes, uint32_t i, uint4 v) {
+    typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+    const v4u w = {v.x, v.y, v.z, v.w};
+    __builtin_amdgcn_raw_buffer_store_b128(w, sys_rsrc(base, bytes), (int)(i * 16u), 0, kSysCoherent);
+}
+// byte offset `off` from a wave-uniform base
+__device__ __forceinline__ void st_sys32_at(void* base, uint32_t bytes, uint32_t off, uint32_t v) {
+    __builtin_amdgcn_raw_buffer_store_b32(v, sys_rsrc(base, bytes), (int)off, 0, kSysCoherent);
+}
+__device__ __forceinline__ void st_sys16_at(void* base, uint32_t bytes, uint32_t off, uint16_t v) {
+    __builtin_amdgcn_raw_buffer_store_b16(v, sys_rsrc(base, bytes), (int)off, 0, kSysCoherent);
+}
+__device__ __forceinline__ void st_sys128_at(void* base, uint32_t bytes, uint32_t off, uint4 v) {
+    typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+    const v4u w = {v.x, v.y, v.z, v.w};
+    __builtin_amdgcn_raw_buffer_store_b128(w, sys_rsrc(base, bytes), (int)off, 0, kSysCoherent);
 }
 
 // Device buffers of one renderer (the GlobalViewResources analogue, GlobalResources.swift:6-362).
@@ -156,6 +198,8 @@ struct Tuning {
     int tileLoBits = 0;       // GSM_SORT_LOBITS=4..8: width of the first tile pass (0: half the tile field)
     int blendClaim = 1;       // GSM_BLEND_CLAIM=early|late|auto (0/1/2): when a blend wave claims its next unit
     bool wideSort = true;     // GSM_SORT_WIDE=0: narrow passes only (no wide 9..11-bit tile or depth passes)
+    bool wide12 = true;       // GSM_SORT_WIDE12=0: a 12-bit tile field (2049..4096 tiles) in two narrow
+                              // passes instead of one 12-bit wide pass
 };
 // the environment's settings plus the device probe; `device` is a HIP device id
 Tuning tuning_from_env(int device);
@@ -183,9 +227,11 @@ constexpr int kRadixItems = GSM_RADIX_ITEMS;  // keys per thread per chunk (4096
 constexpr int kRadixChunk = kRadixBlock * kRadixItems;
 // wide radix digits (gsm_sort.hip): up to 11 bits, 2048 bins
 constexpr uint32_t kWideMaxBits = 11, kWideBins = 1u << kWideMaxBits;
+// one 12-bit pass for a tile field of 2049..4096 tiles (1080p: 4080) -- Tuning::wide12
+constexpr uint32_t kWide12Bits = 12, kWide12Bins = 1u << kWide12Bits;
 // radix_sort_tiles' workspace beside the histogram: two passes' digit totals + the bucket starts
 // (narrow passes, 768 words), or one wide pass's 2048 digit totals
-constexpr size_t kSortTotalsWords = kWideBins;
+constexpr size_t kSortTotalsWords = kWide12Bins;
 
 // project + cull + SH + tile count + per-block count sums (GlobalShaders.metal:19-123, 563-616)
 void launch_project(bool halfInput, uint32_t shDegree, const void* world, const void* harmonics,
@@ -209,7 +255,12 @@ void launch_partition_push(const ProjectArgs& args, uint32_t world, uint32_t ran
                            const MgArrive& arrive, hipStream_t stream);
 // received records -> per-gaussian arrays + tile counts of the renderer's rows (replaces project)
 void launch_records_in(const void* records, const ProjectArgs& args, const DeviceArena& A,
-                       hipStream_t stream, const uint32_t* devCount = nullptr);
+                       hipStream_t stream, const uint32_t* devCount = nullptr, const SlotIn* slots = nullptr);
+// the multi-GPU frame's projection with the direct push (MgPush): records and slot-mask words into
+// every slab owner's receive buffer, the workgroups arriving at barrier 1
+void launch_partition_direct(bool halfInput, uint32_t shDegree, const void* world, const void* harmonics,
+                             const ProjectArgs& args, const SlabTable& slabs, const PartitionBuffers& B,
+                             const float2* sincos, const DeviceArena& A, const MgPush& push, hipStream_t stream);
 // devCount (nullable): the gaussian count on the device (records path); only its blocks are scanned
 void launch_scan_blocks(uint32_t numBlocks, const ProjectArgs& args, const DeviceArena& A,
                         hipStream_t stream, const uint32_t* devCount = nullptr);
@@ -252,7 +303,8 @@ int radix_sort_bits(uint32_t* keys[2], uint32_t* vals[2], const uint32_t* nPtr, 
 // one wide pass relative to tileBase when numTiles <= 2048 and `wide`; binTotals: kSortTotalsWords words
 int radix_sort_tiles(uint32_t* keys[2], uint32_t* vals[2], const uint32_t* nPtr, uint32_t capacity, uint32_t shift,
                      uint32_t* hist, uint32_t* binTotals, uint32_t* tileStart, uint32_t tileBase, uint32_t numTiles,
-                     uint32_t allTiles, hipStream_t stream, bool ballot, int loBits = 0, bool wide = true);
+                     uint32_t allTiles, hipStream_t stream, bool ballot, int loBits = 0, bool wide = true,
+                     bool wide12 = false);
 uint32_t radix_grid_for_capacity(uint32_t capacity);
 // bytes of the sort workspace (`hist` argument above) for a capacity; zero it once at allocation
 size_t radix_workspace_bytes(uint32_t capacity);

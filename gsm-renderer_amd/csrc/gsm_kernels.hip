@@ -475,18 +475,23 @@ __device__ __forceinline__ uint32_t slab_tile_mask(short4 b, uint32_t full, cons
     return out;
 }
 
-template <bool HALF, int DEG>
+// DIRECT (the multi-GPU frame, MgPush): instead of keeping the records and per-slab counts for a
+// later push, every wave writes its records straight into the slab owners' receive slots (slot =
+// global id, system-coherent write-through) with the slot-mask word of its 64 ids for every slab, and
+// every workgroup (the schedule block too) arrives at barrier 1.
+template <bool HALF, int DEG, bool DIRECT>
 __global__ __launch_bounds__(kProjectBlock) void k_project_part(
     const void* __restrict__ world, const void* __restrict__ harm, ProjectArgs P, SlabTable slabs,
     SplatRecord* __restrict__ records, uint32_t* __restrict__ masks,
     uint32_t* __restrict__ blockSlabCounts, const float2* __restrict__ sincos, const uint16_t* __restrict__ unitCost,
-    uint32_t* __restrict__ unitOrder, uint32_t* __restrict__ costMax) {
+    uint32_t* __restrict__ unitOrder, uint32_t* __restrict__ costMax, MgPush push) {
     // block 0 of a scheduled launch orders the blend units of the rank's own slab (the owner renders
     // it later in the frame) while the other blocks project -- as k_project's block 0 does
     if (P.schedUnits) {
         if (blockIdx.x == 0) {
             __shared__ uint32_t uoBase[kUoBuckets], uoMax[kProjectBlock / 64];
             unit_order_block<kProjectBlock>(unitCost, unitOrder, P.schedUnits, uoBase, uoMax, costMax);
+            if constexpr (DIRECT) mg_arrive_block(push.arrive);
             return;
         }
     }
@@ -527,6 +532,32 @@ __global__ __launch_bounds__(kProjectBlock) void k_project_part(
         }
     });
     uint32_t mask = 0;
+    if constexpr (DIRECT) {
+        if (gid < P.count && o.vis) mask = sSlab[tid];
+        const uint32_t w0 = blk * kProjectBlock + wave * 64u;  // the wave's first id of the range
+        if (w0 < P.count) {  // (uniform) the wave's 64 slots, every slab: mask word, then records
+            const uint32_t slot0 = push.first + w0;
+            const uint4 a = make_uint4(o.rd.x, o.rd.y, o.rd.z, o.rd.w);
+            const uint4 b = make_uint4(o.ra.x, o.ra.y, o.ra.z, o.ra.w);
+            const uint2 bb = __builtin_bit_cast(uint2, o.bounds);
+            for (uint32_t sl = 0; sl < nSlabs; ++sl) {
+                const bool has = (mask >> sl) & 1u;
+                const unsigned long long word = __ballot(has);
+                if (lane == 0)
+                    __hip_atomic_store(push.mask[sl] + slot0 / 64u, word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                if (has) {
+                    SplatRecord* dst = push.recv[sl] + slot0;  // (wave-uniform base)
+                    const uint4 c = make_uint4(bb.x, bb.y, o.rb,
+                                               slab_tile_mask(o.bounds, sTile[tid], slab_rows(slabs, slabs.rows, sl)));
+                    st_sys128(dst, 64u * 48u, 3u * lane, a);
+                    st_sys128(dst, 64u * 48u, 3u * lane + 1u, b);
+                    st_sys128(dst, 64u * 48u, 3u * lane + 2u, c);
+                }
+            }
+        }
+        mg_arrive_block(push.arrive);
+        return;
+    }
     if (gid < P.count) {
         mask = sSlab[tid];
         if (o.vis) {
@@ -585,7 +616,7 @@ __global__ __launch_bounds__(1024) void k_part_scan(uint32_t* __restrict__ block
 // threads store consecutive 16-B words -- whole 64-B segments into uncached or peer memory instead
 // of three 16-B pieces per record 48 B apart.  dst(sl) = the run's first record, cap(sl) = records
 // the destination holds (nothing is written past it).  slabs: the slab table (record masks).
-template <class Dst, class Cap>
+template <bool WT, class Dst, class Cap>
 __device__ __forceinline__ void write_slab_runs(const SplatRecord* __restrict__ records, uint32_t slabBits,
                                                 uint32_t gid, uint32_t numSlabs, const SlabTable& slabs,
                                                 Dst&& dst, Cap&& cap) {
@@ -626,8 +657,13 @@ __device__ __forceinline__ void write_slab_runs(const SplatRecord* __restrict__ 
         __syncthreads();
         uint4* d = (uint4*)dst(sl);
         const uint64_t room = cap(sl);
-        for (uint32_t j = threadIdx.x; j < 3u * n; j += kProjectBlock)
-            if (j / 3u < room) d[j] = sOut[j];
+        if constexpr (WT) {  // exchange memory: system-coherent write-through stores (gsm_internal.h)
+            const uint32_t nw = 3u * (uint32_t)min((uint64_t)n, room);
+            for (uint32_t j = threadIdx.x; j < nw; j += kProjectBlock) st_sys128(d, nw * 16u, j, sOut[j]);
+        } else {
+            for (uint32_t j = threadIdx.x; j < 3u * n; j += kProjectBlock)
+                if (j / 3u < room) d[j] = sOut[j];
+        }
         __syncthreads();
     }
 }
@@ -639,7 +675,7 @@ __global__ __launch_bounds__(kProjectBlock) void k_part_pack(
     SplatRecord* __restrict__ send, uint64_t capacity) {
     const uint32_t gid = blockIdx.x * kProjectBlock + threadIdx.x;
     const uint32_t mask = gid < count ? masks[gid] : 0u;
-    write_slab_runs(
+    write_slab_runs<false>(
         records, mask, gid, slabs.n, slabs,
         [&](uint32_t sl) {
             uint64_t base = 0;
@@ -664,7 +700,7 @@ __global__ __launch_bounds__(kProjectBlock) void k_records_in(
     short4* __restrict__ outBounds, BlendRecord* __restrict__ outRec,
     uint32_t* __restrict__ counts, uint32_t* __restrict__ masks, uint32_t* __restrict__ blockSums,
     const float2* __restrict__ sincos, const uint32_t* __restrict__ devCount, const uint16_t* __restrict__ unitCost,
-    uint32_t* __restrict__ unitOrder, uint32_t* __restrict__ costMax) {
+    uint32_t* __restrict__ unitOrder, uint32_t* __restrict__ costMax, SlotIn slots) {
     __shared__ uint32_t lds[kProjectBlock / 64];
     __shared__ uint4 sIn[kProjectBlock * 3];
     // block 0 of a scheduled launch orders the blend's units (as k_project's: no k_unit_order launch)
@@ -679,7 +715,23 @@ __global__ __launch_bounds__(kProjectBlock) void k_records_in(
     const uint32_t gid = blk * kProjectBlock + threadIdx.x;
     const uint32_t n = devCount ? min(*devCount, P.count) : P.count;
     if (blk * kProjectBlock >= n) return;  // (uniform) nothing here; the scan stops at the count
-    {
+    bool present = gid < n;
+    if (slots.mask) {
+        // slots indexed by global id (MgPush): the slot mask says which hold a record this frame --
+        // a source whose frame failed wrote none, its range is void -- and each present record is
+        // loaded by its own lane (system-coherent: the sources stored them over xGMI)
+        const uint32_t w0 = gid & ~63u;
+        const unsigned long long word = ld_sys64(slots.mask + w0 / 64u);
+        const uint32_t src = gid / slots.perIds;
+        present = present && ((word >> (threadIdx.x & 63u)) & 1ull) && ld_sys32(slots.failedEpoch + src) != slots.epoch;
+        if (present) {
+            const SplatRecord* base = in + w0;
+            const uint32_t l = threadIdx.x & 63u;
+            sIn[3 * threadIdx.x] = ld_sys128(base, 64u * 48u, 3u * l);
+            sIn[3 * threadIdx.x + 1] = ld_sys128(base, 64u * 48u, 3u * l + 1u);
+            sIn[3 * threadIdx.x + 2] = ld_sys128(base, 64u * 48u, 3u * l + 2u);
+        }
+    } else {
         // system-coherent 16-B loads (ld_sys128): on the multi-GPU path the records were stored by the
         // peers' k_part_push over xGMI; no L1 / L2 line of an earlier frame may answer
         const uint32_t words = 3u * (min(n - blk * kProjectBlock, (uint32_t)kProjectBlock));
@@ -692,7 +744,7 @@ __global__ __launch_bounds__(kProjectBlock) void k_records_in(
     }
     __syncthreads();
     uint32_t ntiles = 0;
-    if (gid < n) {
+    if (present) {
         const uint4 w0 = sIn[3 * threadIdx.x], w1 = sIn[3 * threadIdx.x + 1], w2 = sIn[3 * threadIdx.x + 2];
         SplatRecord r;
         r.rd = w0;
@@ -734,6 +786,8 @@ __global__ __launch_bounds__(kProjectBlock) void k_records_in(
         masks[gid] = mask;
         const float2 band = ntiles ? band_of(r.ra, r.bounds, R) : make_float2(0.f, -1.f);
         rp[1] = make_uint4(r.rb, __float_as_uint(band.x), __float_as_uint(band.y), 0u);
+    } else if (gid < n) {
+        counts[gid] = 0;  // an empty slot (the scatter reads nothing else of it)
     }
     uint32_t s = block_reduce_add<kProjectBlock>(ntiles, lds);
     if (threadIdx.x == 0) blockSums[blk] = s;
@@ -1065,7 +1119,7 @@ __global__ __launch_bounds__(kProjectBlock) void k_part_push(
     }
     const uint32_t mask = gid < count ? masks[gid] : 0u;
     __syncthreads();  // (dstOff)
-    write_slab_runs(
+    write_slab_runs<true>(
         records, mask, gid, world, slabs,
         [&](uint32_t sl) {
             return peers.recv[sl] + (uint64_t)dstOff[sl] + blockSlabOffsets[(size_t)sl * gridDim.x + blockIdx.x];
@@ -1178,16 +1232,23 @@ void launch_project(bool halfInput, uint32_t deg, const void* world, const void*
     else launch_project_t<false>(deg, world, harm, a, A, s);
 }
 
-template <bool HALF>
+template <bool HALF, bool DIRECT = false>
 static void launch_project_part_t(uint32_t deg, const void* world, const void* harm, const ProjectArgs& a,
                                   const SlabTable& slabs, const PartitionBuffers& B, const float2* sincos,
-                                  const DeviceArena* A, hipStream_t s) {
+                                  const DeviceArena* A, hipStream_t s, const MgPush* push = nullptr) {
     const uint32_t blocks = (a.count + kProjectBlock - 1) / kProjectBlock;
     const uint32_t sched = (A && a.schedUnits) ? 1u : 0u;
+    // the direct push: every workgroup arrives, and a rank with no ids still runs one that does
+    const uint32_t grid = DIRECT ? (blocks + sched > 0 ? blocks + sched : 1u) : blocks + sched;
+    MgPush pu{};
+    if (DIRECT) {
+        pu = *push;
+        pu.arrive.total = grid;
+    }
 #define GSM_LAUNCH_PPART(D)                                                                                 \
-    hipLaunchKernelGGL((k_project_part<HALF, D>), dim3(blocks + sched), dim3(kProjectBlock), 0, s, world,   \
+    hipLaunchKernelGGL((k_project_part<HALF, D, DIRECT>), dim3(grid), dim3(kProjectBlock), 0, s, world,     \
                        harm, a, slabs, B.records, B.masks, B.blockSlabCounts, sincos,                       \
-                       sched ? A->unitCost : nullptr, sched ? A->unitOrder : nullptr, sched ? A->costMax : nullptr)
+                       sched ? A->unitCost : nullptr, sched ? A->unitOrder : nullptr, sched ? A->costMax : nullptr, pu)
     switch (deg) {
         case 0: GSM_LAUNCH_PPART(0); break;
         case 1: GSM_LAUNCH_PPART(1); break;
@@ -1195,6 +1256,13 @@ static void launch_project_part_t(uint32_t deg, const void* world, const void* h
         default: GSM_LAUNCH_PPART(3); break;
     }
 #undef GSM_LAUNCH_PPART
+}
+
+void launch_partition_direct(bool halfInput, uint32_t deg, const void* world, const void* harm, const ProjectArgs& a,
+                             const SlabTable& slabs, const PartitionBuffers& B, const float2* sincos,
+                             const DeviceArena& A, const MgPush& push, hipStream_t s) {
+    if (halfInput) launch_project_part_t<true, true>(deg, world, harm, a, slabs, B, sincos, &A, s, &push);
+    else launch_project_part_t<false, true>(deg, world, harm, a, slabs, B, sincos, &A, s, &push);
 }
 
 void launch_partition(bool halfInput, uint32_t deg, const void* world, const void* harm,
@@ -1242,12 +1310,13 @@ void launch_partition_push(const ProjectArgs& a, uint32_t world, uint32_t rank, 
 }
 
 void launch_records_in(const void* records, const ProjectArgs& a, const DeviceArena& A, hipStream_t s,
-                       const uint32_t* devCount) {
+                       const uint32_t* devCount, const SlotIn* slots) {
     const uint32_t blocks = (a.count + kProjectBlock - 1) / kProjectBlock;
     if (blocks == 0 && a.schedUnits == 0) return;  // (an empty frame still orders its blend units)
     hipLaunchKernelGGL(k_records_in, dim3(blocks + (a.schedUnits ? 1u : 0u)), dim3(kProjectBlock), 0, s,
                        (const SplatRecord*)records, a, A.renderData, A.bounds, A.rec, A.tileCounts, A.tileMasks,
-                       A.blockSums, A.sincosTable, devCount, A.unitCost, A.unitOrder, A.costMax);
+                       A.blockSums, A.sincosTable, devCount, A.unitCost, A.unitOrder, A.costMax,
+                       slots ? *slots : SlotIn{});
 }
 
 void launch_scan_sums(uint32_t* sums, uint32_t nb, uint32_t cap, TileAssignmentHeader* hdr, uint32_t* queue,

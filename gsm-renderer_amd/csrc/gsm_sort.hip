@@ -525,7 +525,7 @@ __global__ __launch_bounds__(kRadixBlock) void k_wide_downsweep(
     constexpr uint32_t R = 1u << BITS;
     constexpr uint32_t DPT = R / kRadixBlock;  // digits per thread
     constexpr uint32_t RP = (R + R / 8 + 255u) / 256u * 256u;  // padded counter rows (whole uint4 zeroing rounds)
-    static_assert(DPT >= 2 && DPT <= 8, "wide digits: 9..11 bits");
+    static_assert(DPT >= 2 && DPT <= 16, "wide digits: 9..12 bits");
     __shared__ __attribute__((aligned(16))) uint32_t waveCnt[kWaves][RP];  // ranks, then each wave's LDS start per digit
     __shared__ uint32_t adj[RP];               // per digit: global destination minus LDS start
     __shared__ uint32_t sKeys[kRadixChunk];
@@ -667,6 +667,7 @@ static void wide_pass(uint32_t* kin, uint32_t* vin, uint32_t* kout, uint32_t* vo
     switch (bits) {
         case 9: GSM_WIDE_PASS(9); break;
         case 10: GSM_WIDE_PASS(10); break;
+        case 12: GSM_WIDE_PASS(12); break;
         default: GSM_WIDE_PASS(11); break;
     }
 #undef GSM_WIDE_PASS
@@ -675,7 +676,7 @@ static void wide_pass(uint32_t* kin, uint32_t* vin, uint32_t* kout, uint32_t* vo
 
 size_t radix_workspace_bytes(uint32_t capacity) {
     // per-block digit counts: <= 1024 blocks x 256 digits (narrow), x 2048 digits (wide)
-    const size_t wide = (size_t)(kWideBins + kWideRowPad) * radix_grid_for_capacity(capacity) * sizeof(uint32_t);
+    const size_t wide = (size_t)(kWide12Bins + kWideRowPad) * radix_grid_for_capacity(capacity) * sizeof(uint32_t);
     return wide > (size_t)256 * 1024 * 4 ? wide : (size_t)256 * 1024 * sizeof(uint32_t);
 }
 
@@ -769,7 +770,7 @@ int radix_sort_bits(uint32_t* keys[2], uint32_t* vals[2], const uint32_t* nPtr, 
 // first pass's at +256, its bucket starts at +512 (narrow); the wide pass's 2048 totals.
 int radix_sort_tiles(uint32_t* keys[2], uint32_t* vals[2], const uint32_t* nPtr, uint32_t capacity, uint32_t shift,
                      uint32_t* hist, uint32_t* binTotals, uint32_t* tileStart, uint32_t tileBase, uint32_t numTiles,
-                     uint32_t allTiles, hipStream_t s, bool ballot, int loBits, bool wide) {
+                     uint32_t allTiles, hipStream_t s, bool ballot, int loBits, bool wide, bool wide12) {
     const uint32_t grid = radix_grid_for_capacity(capacity);
     auto bitsFor = [](uint32_t tiles) {
         uint32_t b = 1;
@@ -778,7 +779,7 @@ int radix_sort_tiles(uint32_t* keys[2], uint32_t* vals[2], const uint32_t* nPtr,
     };
     uint32_t bits = bitsFor(allTiles);
     const uint32_t localBits = bitsFor(numTiles);
-    if (wide && bits > 8 && localBits <= kWideMaxBits) {
+    if (wide && bits > 8 && (localBits <= kWideMaxBits || (wide12 && localBits == kWide12Bits))) {
         wide_pass(keys[0], vals[0], keys[1], vals[1], nPtr, grid, shift, tileBase, (int)(localBits < 9 ? 9 : localBits),
                   hist, binTotals, s, ballot, true, tileStart, numTiles, allTiles);
         return 1;
@@ -1194,6 +1195,8 @@ Tuning tuning_from_env(int device) {
     t.blendClaim = !cv ? 1 : std::strcmp(cv, "early") == 0 ? 0 : std::strcmp(cv, "auto") == 0 ? 2 : 1;
     const char* ws = getenv("GSM_SORT_WIDE");
     t.wideSort = !(ws && ws[0] == '0');
+    const char* w12 = getenv("GSM_SORT_WIDE12");
+    t.wide12 = !(w12 && w12[0] == '0');
     return t;
 }
 

@@ -280,8 +280,10 @@ def main():
             renderer.render_stereo_sbs(cptr, dptr, inp, cam_l, cam_r, W, H, stream=stream,
                                        color_pitch=pitch_c, depth_pitch=pitch_d)
         elif native_multi:
+            # colour and depth gathered into rank 0's library frames (the reference writes depth with
+            # every frame, GlobalRenderer.swift:350; the one-GPU step renders both too)
             mg.render(None, None, inp, cam, W, H, gather=True, stream=stream,
-                      gather_target=frame_ptr if rank == 0 else None)
+                      gather_target=frame_ptr if rank == 0 else None, gather_depth=True)
             return
         elif alltoall:
             renderer.project_partition(inp, cam, W, H, first, cnt, rows, send, send_cap, send_counts,
@@ -383,16 +385,17 @@ def main():
             sys.path.insert(0, os.path.join(ROOT, "oracle"))
             import oracle as O  # parity checker only
             ref = O.render(world_np, harm_np, sh, cam_d, W, H, max_gaussians=n, nthreads=min(16, cpu_threads(args)))
-            multi_parity = bool(np.array_equal(mg.copy_frame(W, H), ref["color"]))
+            multi_parity = bool(np.array_equal(mg.copy_frame(W, H), ref["color"])) and \
+                bool(np.array_equal(mg.copy_depth(W, H), ref["depth"]))
     # BASELINE config 4 (the 4K scene of config 3 on N GPUs): timed the same way after `value`
     multi_4k = None
     if native_multi and args.multi_extra_config not in ("", "none", args.config):
         multi_4k = multi_extra_frame(args, gsm_amd, scenes, dev, gpu, rank, world_size, backend)
-    barrier_timeouts = None
+    barrier_timeouts = failed_arrivals = None
     if native_multi:
-        t = torch.tensor([mg.status()], dtype=torch.int64, device=dev if backend == "nccl" else "cpu")
-        dist.all_reduce(t)  # every rank's barrier timeouts (0 on a healthy run)
-        barrier_timeouts = int(t.item())
+        t = torch.tensor(list(mg.errors()), dtype=torch.int64, device=dev if backend == "nccl" else "cpu")
+        dist.all_reduce(t)  # every rank's barrier timeouts and failed peer arrivals (0, 0 when healthy)
+        barrier_timeouts, failed_arrivals = int(t[0].item()), int(t[1].item())
         torch.cuda.synchronize()
         dist.barrier()  # no rank unmaps its exchange memory while a peer may still write into it
         mg.close()
@@ -535,6 +538,7 @@ def main():
         out["multi_fallback"] = multi_fallback
     if barrier_timeouts is not None:
         out["barrier_timeouts"] = barrier_timeouts
+        out["failed_peer_arrivals"] = failed_arrivals
     if multi_4k:
         out["config4"] = multi_4k
     if world_size == 1 and not stereo and args.virtual_ranks > 1:
@@ -578,7 +582,8 @@ def multi_extra_frame(args, gsm_amd, scenes, dev, gpu, rank, world_size, backend
     stream = torch.cuda.current_stream(dev)
 
     def step():
-        mg.render(None, None, inp, cam, W, H, gather=True, stream=stream, gather_target=frame_ptr if rank == 0 else None)
+        mg.render(None, None, inp, cam, W, H, gather=True, stream=stream, gather_target=frame_ptr if rank == 0 else None,
+                  gather_depth=True)
     for _ in range(3):
         step()
     steps = max(1, min(args.steps, 20))

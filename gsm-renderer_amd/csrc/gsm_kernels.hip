@@ -613,7 +613,7 @@ __global__ __launch_bounds__(1024) void k_part_scan(uint32_t* __restrict__ block
 
 // Writes the block's records of every slab it meets as one contiguous run of the destination
 // (slab-local rank order = ascending id): the 48-B records go through LDS so that consecutive
-// threads store consecutive 16-B words -- whole 64-B segments into uncached or peer memory instead
+// threads store consecutive 16-B words -- whole 64-B segments into exchange or peer memory instead
 // of three 16-B pieces per record 48 B apart.  dst(sl) = the run's first record, cap(sl) = records
 // the destination holds (nothing is written past it).  slabs: the slab table (record masks).
 template <bool WT, class Dst, class Cap>
@@ -694,7 +694,9 @@ __global__ __launch_bounds__(kProjectBlock) void k_part_pack(
 // devCount (may be null): the record count on the device (multi-GPU exchange); P.count is then the
 // capacity the grid covers, and blocks past the count leave at once (the scan and the scatter read
 // the count too).  The block's records (256 x 48 B, contiguous) are loaded as 16-B words by
-// consecutive threads and exchanged through LDS (whole segments of the uncached receive buffer).
+// consecutive threads and exchanged through LDS (whole segments of the receive buffer).  With a slot
+// mask (SlotIn: the multi-GPU frame's receive slots, indexed by global id) each present slot is
+// loaded by its own lane and the empty ones count no tiles.
 __global__ __launch_bounds__(kProjectBlock) void k_records_in(
     const SplatRecord* __restrict__ in, ProjectArgs P, GaussianRenderData* __restrict__ outRD,
     short4* __restrict__ outBounds, BlendRecord* __restrict__ outRec,

@@ -316,10 +316,11 @@ gsm_status MultiGpu::prepare(GlobalRenderer* r, int rank, int world, MultiGpu** 
     if (!handle || world < 1 || world > (int)kMaxSlabs || rank < 0 || rank >= world) return GSM_ERR_INVALID_ARGUMENT;
     if (hipSetDevice(r->device()) != hipSuccess) return GSM_ERR_DEVICE_NOT_AVAILABLE;
     // exchange memory kind (create-time): fine-grained device memory (default) or ordinary
-    // device memory (GSM_MG_MEM=cached, one GPU only).  Uncached memory is refused: on MI355X its
-    // stores and loads rendered wrong virtual-rank frames (profiles/r03_mg_exchange_memory_ab.log; the
-    // cause, measured in r04, is in DESIGN.md 7)
+    // device memory (GSM_MG_MEM=cached, one GPU only)
     const char* mode = getenv("GSM_MG_MEM");
+    // uncached exchange memory renders wrong slabs on MI355X: refused; the A/B script
+    // (tools/exp/mg_memkind_ab.py) reaches it as "uncached-ab"
+    if (mode && !strcmp(mode, "uncached")) return GSM_ERR_UNSUPPORTED;
     MultiGpu* m = new (std::nothrow) MultiGpu();
     if (!m) return GSM_ERR_FAILED_TO_ALLOCATE_BUFFER;
     m->r_ = r;
@@ -328,7 +329,7 @@ gsm_status MultiGpu::prepare(GlobalRenderer* r, int rank, int world, MultiGpu** 
     m->device_ = r->device();
     m->capacity_ = r->maxGaussians();
     m->bpp_ = r->colorBytesPerPixel();
-    m->memKind_ = mode && !strcmp(mode, "cached") ? 2u : (mode && !strcmp(mode, "uncached") ? 1u : 0u);
+    m->memKind_ = mode && !strcmp(mode, "cached") ? 2u : (mode && !strcmp(mode, "uncached-ab") ? 1u : 0u);
     int khz = 0;
     if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, m->device_) == hipSuccess && khz > 0)
         m->wallKHz_ = (uint32_t)khz;

@@ -525,7 +525,7 @@ __global__ __launch_bounds__(kRadixBlock) void k_wide_downsweep(
     constexpr uint32_t R = 1u << BITS;
     constexpr uint32_t DPT = R / kRadixBlock;  // digits per thread
     constexpr uint32_t RP = (R + R / 8 + 255u) / 256u * 256u;  // padded counter rows (whole uint4 zeroing rounds)
-    static_assert(DPT >= 2 && DPT <= 16, "wide digits: 9..12 bits");
+    static_assert(DPT >= 2 && DPT <= 8, "wide digits: 9..11 bits (12: k_wide12_downsweep)");
     __shared__ __attribute__((aligned(16))) uint32_t waveCnt[kWaves][RP];  // ranks, then each wave's LDS start per digit
     __shared__ uint32_t adj[RP];               // per digit: global destination minus LDS start
     __shared__ uint32_t sKeys[kRadixChunk];
@@ -647,13 +647,163 @@ __global__ __launch_bounds__(kRadixBlock) void k_wide_downsweep(
     }
 }
 
+// 12-bit wide downsweep (a tile field of 2049..4096 tiles: 1080p's 4080): k_wide_downsweep's
+// algorithm with the per-wave digit counters packed two 16-bit halves per word (a wave ranks at most
+// 1024 keys of a chunk, so a half never carries into its neighbour; lanes of one ds_add_rtn_u32 on the
+// same word are still served in lane order, so a lane's old half is its stable rank), and the
+// per-digit global offsets written over the counters once the chunk sits in LDS: 69 KB of LDS, two
+// workgroups per CU (the unpacked layout needs 125 KB: one).
+template <bool BALLOT, bool STARTS>
+__global__ __launch_bounds__(kRadixBlock) void k_wide12_downsweep(
+    const uint32_t* __restrict__ keysIn, const uint32_t* __restrict__ valsIn, uint32_t* __restrict__ keysOut,
+    uint32_t* __restrict__ valsOut, const uint32_t* __restrict__ nPtr, uint32_t shift, uint32_t base,
+    const uint32_t* __restrict__ hist, const uint32_t* __restrict__ binTotals, uint32_t* __restrict__ tileStart,
+    uint32_t numTiles, uint32_t allTiles) {
+    constexpr uint32_t R = kWide12Bins, DPT = R / kRadixBlock, WPT = DPT / 2;  // 16 digits, 8 words per thread
+    constexpr uint32_t RWP = (R / 2 + R / 16 + 255u) / 256u * 256u;           // padded words per wave: 2304
+    static_assert(kWaves * RWP >= R + R / 8, "the digits' offsets fit over the counters");
+    static_assert((kWaves * RWP) % (4 * kRadixBlock) == 0, "counter rows in whole uint4 rounds");
+    static_assert(kRadixItems * 64 < 65536, "a wave's count of one digit fits 16 bits");
+    __shared__ __attribute__((aligned(16))) uint32_t cnt[kWaves][RWP];
+    __shared__ uint32_t sKeys[kRadixChunk];
+    __shared__ uint32_t sVals[kRadixChunk];
+    __shared__ uint32_t part[kWaves];
+    uint32_t* adj = &cnt[0][0];  // after the LDS scatter: digit d's global destination minus LDS start, at wide_pad(d)
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+    const uint32_t n = *nPtr;
+    uint32_t begin, end;
+    block_range(n, gridDim.x, blockIdx.x, &begin, &end);
+    const uint32_t d0 = tid * DPT, w0 = tid * WPT;  // this thread's digits and counter words
+    auto zero_counters = [&]() {
+        uint4* z = (uint4*)&cnt[0][0];
+#pragma unroll
+        for (uint32_t i = 0; i < kWaves * RWP / 4 / kRadixBlock; ++i) z[i * kRadixBlock + tid] = make_uint4(0u, 0u, 0u, 0u);
+    };
+    uint32_t gbase[DPT];
+    {
+        uint32_t run = 0;
+#pragma unroll
+        for (uint32_t i = 0; i < DPT; ++i) {
+            gbase[i] = run;
+            run += binTotals[d0 + i];
+        }
+        uint32_t tot;
+        const uint32_t off = wide_block_scan(run, part, &tot);
+#pragma unroll
+        for (uint32_t i = 0; i < DPT; ++i) gbase[i] += off;
+        if (STARTS && blockIdx.x == 0) {
+            for (uint32_t t = tid; t < base; t += kRadixBlock) tileStart[t] = 0u;
+#pragma unroll
+            for (uint32_t i = 0; i < DPT; ++i)
+                if (d0 + i < numTiles) tileStart[base + d0 + i] = gbase[i];
+            for (uint32_t t = base + numTiles + tid; t <= allTiles; t += kRadixBlock) tileStart[t] = n;
+        }
+        if (begin >= end) return;
+        const uint32_t* row = hist + (size_t)blockIdx.x * (R + kWideRowPad) + d0;  // block-major (k_wide_scan)
+#pragma unroll
+        for (uint32_t i = 0; i < DPT; ++i) gbase[i] += row[i];
+        zero_counters();
+        __syncthreads();
+    }
+    const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    for (uint32_t cbase = begin; cbase < end; cbase += kRadixChunk) {
+        uint32_t k[kRadixItems], v[kRadixItems], rank[kRadixItems];
+#pragma unroll
+        for (int j = 0; j < kRadixItems; ++j) {
+            const uint32_t idx = cbase + wave * (64 * kRadixItems) + j * 64 + lane;
+            const bool valid = idx < end;
+            k[j] = valid ? keysIn[idx] : 0u;
+            v[j] = valid ? valsIn[idx] : 0u;
+        }
+#pragma unroll
+        for (int j = 0; j < kRadixItems; ++j) {
+            const uint32_t idx = cbase + wave * (64 * kRadixItems) + j * 64 + lane;
+            const bool valid = idx < end;
+            const uint32_t d = ((k[j] >> shift) - base) & (R - 1u);
+            uint32_t* word = &cnt[wave][wide_pad(d >> 1)];
+            const uint32_t sh = (d & 1u) * 16u;
+            if constexpr (BALLOT) {
+                const uint64_t peers = match_digit<kWide12Bits>(d, valid);
+                const uint32_t before = (*word >> sh) & 0xFFFFu;
+                // one leader per digit; the two digits of a word add to different halves
+                if (valid && (peers & lt) == 0) atomicAdd(word, (uint32_t)__popcll(peers) << sh);
+                rank[j] = before + (uint32_t)__popcll(peers & lt);
+            } else {
+                rank[j] = valid ? ((atomicAdd(word, 1u << sh) >> sh) & 0xFFFFu) : 0u;
+            }
+        }
+        __syncthreads();
+        // per digit: chunk total, its LDS start (scan over digits), each wave's start within it
+        uint32_t adjR[DPT];
+        {
+            uint32_t x[WPT][kWaves], run = 0;
+#pragma unroll
+            for (uint32_t i = 0; i < WPT; ++i)
+#pragma unroll
+                for (int w = 0; w < kWaves; ++w) {
+                    x[i][w] = cnt[w][wide_pad(w0 + i)];
+                    run += (x[i][w] & 0xFFFFu) + (x[i][w] >> 16);
+                }
+            uint32_t all;
+            uint32_t ls = wide_block_scan(run, part, &all);
+#pragma unroll
+            for (uint32_t i = 0; i < WPT; ++i) {
+                uint32_t lo[kWaves], hi[kWaves];
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {  // digit d0 + 2i + h
+                    const uint32_t dd = 2u * i + (uint32_t)h;
+                    adjR[dd] = gbase[dd] - ls;
+#pragma unroll
+                    for (int w = 0; w < kWaves; ++w) {
+                        const uint32_t c = h ? (x[i][w] >> 16) : (x[i][w] & 0xFFFFu);
+                        (h ? hi : lo)[w] = ls;
+                        ls += c;
+                        gbase[dd] += c;
+                    }
+                }
+#pragma unroll
+                for (int w = 0; w < kWaves; ++w) cnt[w][wide_pad(w0 + i)] = lo[w] | (hi[w] << 16);
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < kRadixItems; ++j) {
+            const uint32_t idx = cbase + wave * (64 * kRadixItems) + j * 64 + lane;
+            if (idx < end) {
+                const uint32_t d = ((k[j] >> shift) - base) & (R - 1u);
+                const uint32_t pos = ((cnt[wave][wide_pad(d >> 1)] >> ((d & 1u) * 16u)) & 0xFFFFu) + rank[j];
+                sKeys[pos] = k[j];
+                sVals[pos] = v[j];
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (uint32_t i = 0; i < DPT; ++i) adj[wide_pad(d0 + i)] = adjR[i];
+        __syncthreads();
+        const uint32_t cn = min((uint32_t)kRadixChunk, end - cbase);
+        for (uint32_t p = tid; p < cn; p += kRadixBlock) {
+            const uint32_t key = sKeys[p];
+            const uint32_t dst = adj[wide_pad(((key >> shift) - base) & (R - 1u))] + p;
+            keysOut[dst] = key;
+            valsOut[dst] = sVals[p];
+        }
+        __syncthreads();
+        zero_counters();
+        __syncthreads();
+    }
+}
+
 static void wide_pass(uint32_t* kin, uint32_t* vin, uint32_t* kout, uint32_t* vout, const uint32_t* nPtr,
                       uint32_t grid, uint32_t shift, uint32_t base, int bits, uint32_t* hist, uint32_t* binTotals,
                       hipStream_t s, bool ballot, bool starts, uint32_t* tileStart, uint32_t numTiles,
                       uint32_t allTiles) {
 #define GSM_WIDE_DOWN(B, BAL, S)                                                                              \
-    hipLaunchKernelGGL((k_wide_downsweep<B, BAL, S>), dim3(grid), dim3(kRadixBlock), 0, s, kin, vin, kout, vout, \
-                       nPtr, shift, base, hist, binTotals, tileStart, numTiles, allTiles)
+    if (B == kWide12Bits)                                                                                     \
+        hipLaunchKernelGGL((k_wide12_downsweep<BAL, S>), dim3(grid), dim3(kRadixBlock), 0, s, kin, vin, kout, \
+                           vout, nPtr, shift, base, hist, binTotals, tileStart, numTiles, allTiles);          \
+    else                                                                                                      \
+        hipLaunchKernelGGL((k_wide_downsweep<(B < 12 ? B : 11), BAL, S>), dim3(grid), dim3(kRadixBlock), 0, s, kin, vin, \
+                           kout, vout, nPtr, shift, base, hist, binTotals, tileStart, numTiles, allTiles)
 #define GSM_WIDE_PASS(B)                                                                                         \
     hipLaunchKernelGGL(k_wide_upsweep<B>, dim3(grid), dim3(kRadixBlock), 0, s, kin, nPtr, shift, base, hist);    \
     hipLaunchKernelGGL(k_wide_scan<B>, dim3((1u << B) / kWideScanDigits), dim3(256), 0, s, hist, grid, nPtr, binTotals); \

@@ -73,7 +73,8 @@ gsm_status gsm_global_render_records(gsm_renderer *renderer, void *stream, const
  *                          buffers, and writes its GSM_MULTIGPU_HANDLE_BYTES handle into `handle`.
  *                          GSM_MG_MEM=cached (ordinary device memory; one GPU only: refused at
  *                          connect across processes) is the A/B of DESIGN.md 7;
- *                          GSM_MG_MEM=uncached returns GSM_ERR_UNSUPPORTED;
+ *                          GSM_MG_MEM=uncached returns GSM_ERR_UNSUPPORTED: uncached memory
+ *                          renders wrong slabs on MI355X;
  *   (caller)               all-gathers the handles: all[r * GSM_MULTIGPU_HANDLE_BYTES] = rank r's;
  *   gsm_multigpu_connect   opens every peer's exchange memory (hipIpcOpenMemHandle; a handle
  *                          from the same process is used directly) and checks that the ranks

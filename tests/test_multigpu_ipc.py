@@ -176,3 +176,15 @@ def test_config4_virtual_ranks_full_size(gsm, cuda, oracle):
     assert np.array_equal(frames[0], ref["color"])
     assert np.array_equal(depths[0], ref["depth"])
     assert counts.sum() >= int(np.count_nonzero(ref["tile_counts"]))
+
+
+def test_uncached_exchange_memory_is_refused(gsm, cuda, monkeypatch):
+    """GSM_MG_MEM=uncached: refused at gsm_multigpu_prepare (GSM_ERR_UNSUPPORTED) -- uncached memory
+    renders wrong virtual-rank slabs on MI355X even with write-through stores and system-coherent
+    loads (profiles/r04_mg_memkind_uncached.log)."""
+    monkeypatch.setenv("GSM_MG_MEM", "uncached")
+    r = gsm.GlobalRenderer(device=0, config=gsm.RendererConfig(max_gaussians=1024, max_width=64, max_height=32))
+    with pytest.raises(gsm.RendererError) as e:
+        gsm.MultiGpuRenderer.prepare(r, 0, 2)
+    assert e.value.status == gsm.Status.UNSUPPORTED
+    r.close()

@@ -2,9 +2,10 @@
 (tests/test_multigpu_ipc.py _virtual_frame: W renderers of one process, the product kernels, barriers
 and gather into rank 0's frame) repeated `rounds` times over three cases and two cameras, each frame
 compared with the oracle (colour and gathered depth).  The exchange memory kind comes from the
-environment at prepare: GSM_MG_MEM=fine (default) | cached | uncached.
+environment at prepare: GSM_MG_MEM=fine (default) | cached | uncached-ab (uncached memory; the product
+refuses GSM_MG_MEM=uncached).
 
-usage: GSM_MG_MEM=uncached python tools/exp/mg_memkind_ab.py [rounds]   -> one line per frame, then
+usage: GSM_MG_MEM=uncached-ab python tools/exp/mg_memkind_ab.py [rounds]   -> one line per frame, then
        "bad frames: B of F" (the r03 log profiles/r03_mg_exchange_memory_ab.log came from its predecessor)"""
 import os
 import sys

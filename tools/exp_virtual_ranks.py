@@ -2,7 +2,7 @@
 through the product path (gsm_multigpu_render_phase, include/gsm_multigpu.h): every rank's phase p
 is issued before any rank's phase p + 1 on ONE stream, so the ranks run one after another and each
 phase sees the whole GPU (an upper bound for a rank's own GPU).  Exchange memory is the product's
-(uncached, the flag barriers run); the pushes and the gathered pixels go to local memory instead of
+(fine-grained, the flag barriers run); the pushes and the gathered pixels go to local memory instead of
 crossing xGMI.  HIP events bracket each rank's phase; the renderers' stage events split the slab
 render (records in, scan, scatter, sort, gap, blend).
 

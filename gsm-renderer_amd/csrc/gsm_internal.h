@@ -98,25 +98,6 @@ __device__ __forceinline__ void mg_arrive_block(const MgArrive& a) {
     __syncthreads();
     if (threadIdx.x < 64u) mg_arrive_wave(a);
 }
-// The multi-GPU frame's direct push (k_project_part, gsm_multigpu.hip): the receive slots of every
-// rank are indexed by GLOBAL gaussian id -- rank r projects ids [first, first + count), first a multiple
-// of 256 -- so a record needs no offset from a count exchange: gaussian g's record for slab s goes to
-// slot g of rank s's receive buffer, and bit g of rank s's slot mask says whether it is there (every
-// wave writes the 64-bit mask word of its 64 ids for every slab, also when it is zero).  The owner
-// renders its slots in id order: the stable sort's tie order without any gather.
-struct MgPush {
-    SplatRecord* recv[kMaxSlabs];             // slot 0 of rank s's receive buffer (peer mappings)
-    unsigned long long* mask[kMaxSlabs];      // word 0 of rank s's slot mask
-    uint32_t first;                           // this rank's first id (the launch's gid 0)
-    uint32_t slots;                           // slots of every receive buffer (the frame's N)
-    MgArrive arrive;                          // barrier 1: every workgroup after its stores
-};
-// The owner's view of its slots (k_records_in): which ids hold a record this frame
-struct SlotIn {
-    const unsigned long long* mask;  // bit g: slot g holds a record (null: dense records)
-    const uint32_t* failedEpoch;     // [world]: == epoch when that source's frame failed (its slots are void)
-    uint32_t epoch, perIds;          // the frame; ids per source rank (a multiple of 256)
-};
 // k_part_scan's count publication: row `rank` of rank p's count matrix (this frame's parity), and
 // the arrival at barrier 0 (arrive.done == null: no publication, the send-buffer path)
 struct CountPublish {
@@ -130,9 +111,6 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t sys_rsrc(const void* base, uin
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)bytes, 0x00020000);
 }
 __device__ __forceinline__ uint32_t ld_sys32(const uint32_t* p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-__device__ __forceinline__ unsigned long long ld_sys64(const unsigned long long* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 __device__ __forceinline__ uint4 ld_sys128(const void* base, uint32_t bytes, uint32_t i) {
@@ -198,8 +176,8 @@ struct Tuning {
     int tileLoBits = 0;       // GSM_SORT_LOBITS=4..8: width of the first tile pass (0: half the tile field)
     int blendClaim = 1;       // GSM_BLEND_CLAIM=early|late|auto (0/1/2): when a blend wave claims its next unit
     bool wideSort = true;     // GSM_SORT_WIDE=0: narrow passes only (no wide 9..11-bit tile or depth passes)
-    bool wide12 = true;       // GSM_SORT_WIDE12=0: a 12-bit tile field (2049..4096 tiles) in two narrow
-                              // passes instead of one 12-bit wide pass
+    bool wide12 = false;      // GSM_SORT_WIDE12=1: a 12-bit tile field (2049..4096 tiles) in one 12-bit
+                              // wide pass instead of two narrow passes (measured slower: DESIGN.md 4)
 };
 // the environment's settings plus the device probe; `device` is a HIP device id
 Tuning tuning_from_env(int device);
@@ -255,12 +233,7 @@ void launch_partition_push(const ProjectArgs& args, uint32_t world, uint32_t ran
                            const MgArrive& arrive, hipStream_t stream);
 // received records -> per-gaussian arrays + tile counts of the renderer's rows (replaces project)
 void launch_records_in(const void* records, const ProjectArgs& args, const DeviceArena& A,
-                       hipStream_t stream, const uint32_t* devCount = nullptr, const SlotIn* slots = nullptr);
-// the multi-GPU frame's projection with the direct push (MgPush): records and slot-mask words into
-// every slab owner's receive buffer, the workgroups arriving at barrier 1
-void launch_partition_direct(bool halfInput, uint32_t shDegree, const void* world, const void* harmonics,
-                             const ProjectArgs& args, const SlabTable& slabs, const PartitionBuffers& B,
-                             const float2* sincos, const DeviceArena& A, const MgPush& push, hipStream_t stream);
+                       hipStream_t stream, const uint32_t* devCount = nullptr);
 // devCount (nullable): the gaussian count on the device (records path); only its blocks are scanned
 void launch_scan_blocks(uint32_t numBlocks, const ProjectArgs& args, const DeviceArena& A,
                         hipStream_t stream, const uint32_t* devCount = nullptr);

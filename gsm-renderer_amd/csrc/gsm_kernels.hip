@@ -475,23 +475,18 @@ __device__ __forceinline__ uint32_t slab_tile_mask(short4 b, uint32_t full, cons
     return out;
 }
 
-// DIRECT (the multi-GPU frame, MgPush): instead of keeping the records and per-slab counts for a
-// later push, every wave writes its records straight into the slab owners' receive slots (slot =
-// global id, system-coherent write-through) with the slot-mask word of its 64 ids for every slab, and
-// every workgroup (the schedule block too) arrives at barrier 1.
-template <bool HALF, int DEG, bool DIRECT>
+template <bool HALF, int DEG>
 __global__ __launch_bounds__(kProjectBlock) void k_project_part(
     const void* __restrict__ world, const void* __restrict__ harm, ProjectArgs P, SlabTable slabs,
     SplatRecord* __restrict__ records, uint32_t* __restrict__ masks,
     uint32_t* __restrict__ blockSlabCounts, const float2* __restrict__ sincos, const uint16_t* __restrict__ unitCost,
-    uint32_t* __restrict__ unitOrder, uint32_t* __restrict__ costMax, MgPush push) {
+    uint32_t* __restrict__ unitOrder, uint32_t* __restrict__ costMax) {
     // block 0 of a scheduled launch orders the blend units of the rank's own slab (the owner renders
     // it later in the frame) while the other blocks project -- as k_project's block 0 does
     if (P.schedUnits) {
         if (blockIdx.x == 0) {
             __shared__ uint32_t uoBase[kUoBuckets], uoMax[kProjectBlock / 64];
             unit_order_block<kProjectBlock>(unitCost, unitOrder, P.schedUnits, uoBase, uoMax, costMax);
-            if constexpr (DIRECT) mg_arrive_block(push.arrive);
             return;
         }
     }
@@ -532,32 +527,6 @@ __global__ __launch_bounds__(kProjectBlock) void k_project_part(
         }
     });
     uint32_t mask = 0;
-    if constexpr (DIRECT) {
-        if (gid < P.count && o.vis) mask = sSlab[tid];
-        const uint32_t w0 = blk * kProjectBlock + wave * 64u;  // the wave's first id of the range
-        if (w0 < P.count) {  // (uniform) the wave's 64 slots, every slab: mask word, then records
-            const uint32_t slot0 = push.first + w0;
-            const uint4 a = make_uint4(o.rd.x, o.rd.y, o.rd.z, o.rd.w);
-            const uint4 b = make_uint4(o.ra.x, o.ra.y, o.ra.z, o.ra.w);
-            const uint2 bb = __builtin_bit_cast(uint2, o.bounds);
-            for (uint32_t sl = 0; sl < nSlabs; ++sl) {
-                const bool has = (mask >> sl) & 1u;
-                const unsigned long long word = __ballot(has);
-                if (lane == 0)
-                    __hip_atomic_store(push.mask[sl] + slot0 / 64u, word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                if (has) {
-                    SplatRecord* dst = push.recv[sl] + slot0;  // (wave-uniform base)
-                    const uint4 c = make_uint4(bb.x, bb.y, o.rb,
-                                               slab_tile_mask(o.bounds, sTile[tid], slab_rows(slabs, slabs.rows, sl)));
-                    st_sys128(dst, 64u * 48u, 3u * lane, a);
-                    st_sys128(dst, 64u * 48u, 3u * lane + 1u, b);
-                    st_sys128(dst, 64u * 48u, 3u * lane + 2u, c);
-                }
-            }
-        }
-        mg_arrive_block(push.arrive);
-        return;
-    }
     if (gid < P.count) {
         mask = sSlab[tid];
         if (o.vis) {
@@ -694,15 +663,13 @@ __global__ __launch_bounds__(kProjectBlock) void k_part_pack(
 // devCount (may be null): the record count on the device (multi-GPU exchange); P.count is then the
 // capacity the grid covers, and blocks past the count leave at once (the scan and the scatter read
 // the count too).  The block's records (256 x 48 B, contiguous) are loaded as 16-B words by
-// consecutive threads and exchanged through LDS (whole segments of the receive buffer).  With a slot
-// mask (SlotIn: the multi-GPU frame's receive slots, indexed by global id) each present slot is
-// loaded by its own lane and the empty ones count no tiles.
+// consecutive threads and exchanged through LDS (whole segments of the receive buffer).
 __global__ __launch_bounds__(kProjectBlock) void k_records_in(
     const SplatRecord* __restrict__ in, ProjectArgs P, GaussianRenderData* __restrict__ outRD,
     short4* __restrict__ outBounds, BlendRecord* __restrict__ outRec,
     uint32_t* __restrict__ counts, uint32_t* __restrict__ masks, uint32_t* __restrict__ blockSums,
     const float2* __restrict__ sincos, const uint32_t* __restrict__ devCount, const uint16_t* __restrict__ unitCost,
-    uint32_t* __restrict__ unitOrder, uint32_t* __restrict__ costMax, SlotIn slots) {
+    uint32_t* __restrict__ unitOrder, uint32_t* __restrict__ costMax) {
     __shared__ uint32_t lds[kProjectBlock / 64];
     __shared__ uint4 sIn[kProjectBlock * 3];
     // block 0 of a scheduled launch orders the blend's units (as k_project's: no k_unit_order launch)
@@ -717,23 +684,7 @@ __global__ __launch_bounds__(kProjectBlock) void k_records_in(
     const uint32_t gid = blk * kProjectBlock + threadIdx.x;
     const uint32_t n = devCount ? min(*devCount, P.count) : P.count;
     if (blk * kProjectBlock >= n) return;  // (uniform) nothing here; the scan stops at the count
-    bool present = gid < n;
-    if (slots.mask) {
-        // slots indexed by global id (MgPush): the slot mask says which hold a record this frame --
-        // a source whose frame failed wrote none, its range is void -- and each present record is
-        // loaded by its own lane (system-coherent: the sources stored them over xGMI)
-        const uint32_t w0 = gid & ~63u;
-        const unsigned long long word = ld_sys64(slots.mask + w0 / 64u);
-        const uint32_t src = gid / slots.perIds;
-        present = present && ((word >> (threadIdx.x & 63u)) & 1ull) && ld_sys32(slots.failedEpoch + src) != slots.epoch;
-        if (present) {
-            const SplatRecord* base = in + w0;
-            const uint32_t l = threadIdx.x & 63u;
-            sIn[3 * threadIdx.x] = ld_sys128(base, 64u * 48u, 3u * l);
-            sIn[3 * threadIdx.x + 1] = ld_sys128(base, 64u * 48u, 3u * l + 1u);
-            sIn[3 * threadIdx.x + 2] = ld_sys128(base, 64u * 48u, 3u * l + 2u);
-        }
-    } else {
+    {
         // system-coherent 16-B loads (ld_sys128): on the multi-GPU path the records were stored by the
         // peers' k_part_push over xGMI; no L1 / L2 line of an earlier frame may answer
         const uint32_t words = 3u * (min(n - blk * kProjectBlock, (uint32_t)kProjectBlock));
@@ -746,7 +697,7 @@ __global__ __launch_bounds__(kProjectBlock) void k_records_in(
     }
     __syncthreads();
     uint32_t ntiles = 0;
-    if (present) {
+    if (gid < n) {
         const uint4 w0 = sIn[3 * threadIdx.x], w1 = sIn[3 * threadIdx.x + 1], w2 = sIn[3 * threadIdx.x + 2];
         SplatRecord r;
         r.rd = w0;
@@ -788,8 +739,6 @@ __global__ __launch_bounds__(kProjectBlock) void k_records_in(
         masks[gid] = mask;
         const float2 band = ntiles ? band_of(r.ra, r.bounds, R) : make_float2(0.f, -1.f);
         rp[1] = make_uint4(r.rb, __float_as_uint(band.x), __float_as_uint(band.y), 0u);
-    } else if (gid < n) {
-        counts[gid] = 0;  // an empty slot (the scatter reads nothing else of it)
     }
     uint32_t s = block_reduce_add<kProjectBlock>(ntiles, lds);
     if (threadIdx.x == 0) blockSums[blk] = s;
@@ -1234,23 +1183,16 @@ void launch_project(bool halfInput, uint32_t deg, const void* world, const void*
     else launch_project_t<false>(deg, world, harm, a, A, s);
 }
 
-template <bool HALF, bool DIRECT = false>
+template <bool HALF>
 static void launch_project_part_t(uint32_t deg, const void* world, const void* harm, const ProjectArgs& a,
                                   const SlabTable& slabs, const PartitionBuffers& B, const float2* sincos,
-                                  const DeviceArena* A, hipStream_t s, const MgPush* push = nullptr) {
+                                  const DeviceArena* A, hipStream_t s) {
     const uint32_t blocks = (a.count + kProjectBlock - 1) / kProjectBlock;
     const uint32_t sched = (A && a.schedUnits) ? 1u : 0u;
-    // the direct push: every workgroup arrives, and a rank with no ids still runs one that does
-    const uint32_t grid = DIRECT ? (blocks + sched > 0 ? blocks + sched : 1u) : blocks + sched;
-    MgPush pu{};
-    if (DIRECT) {
-        pu = *push;
-        pu.arrive.total = grid;
-    }
 #define GSM_LAUNCH_PPART(D)                                                                                 \
-    hipLaunchKernelGGL((k_project_part<HALF, D, DIRECT>), dim3(grid), dim3(kProjectBlock), 0, s, world,     \
+    hipLaunchKernelGGL((k_project_part<HALF, D>), dim3(blocks + sched), dim3(kProjectBlock), 0, s, world,   \
                        harm, a, slabs, B.records, B.masks, B.blockSlabCounts, sincos,                       \
-                       sched ? A->unitCost : nullptr, sched ? A->unitOrder : nullptr, sched ? A->costMax : nullptr, pu)
+                       sched ? A->unitCost : nullptr, sched ? A->unitOrder : nullptr, sched ? A->costMax : nullptr)
     switch (deg) {
         case 0: GSM_LAUNCH_PPART(0); break;
         case 1: GSM_LAUNCH_PPART(1); break;
@@ -1258,13 +1200,6 @@ static void launch_project_part_t(uint32_t deg, const void* world, const void* h
         default: GSM_LAUNCH_PPART(3); break;
     }
 #undef GSM_LAUNCH_PPART
-}
-
-void launch_partition_direct(bool halfInput, uint32_t deg, const void* world, const void* harm, const ProjectArgs& a,
-                             const SlabTable& slabs, const PartitionBuffers& B, const float2* sincos,
-                             const DeviceArena& A, const MgPush& push, hipStream_t s) {
-    if (halfInput) launch_project_part_t<true, true>(deg, world, harm, a, slabs, B, sincos, &A, s, &push);
-    else launch_project_part_t<false, true>(deg, world, harm, a, slabs, B, sincos, &A, s, &push);
 }
 
 void launch_partition(bool halfInput, uint32_t deg, const void* world, const void* harm,
@@ -1312,13 +1247,12 @@ void launch_partition_push(const ProjectArgs& a, uint32_t world, uint32_t rank, 
 }
 
 void launch_records_in(const void* records, const ProjectArgs& a, const DeviceArena& A, hipStream_t s,
-                       const uint32_t* devCount, const SlotIn* slots) {
+                       const uint32_t* devCount) {
     const uint32_t blocks = (a.count + kProjectBlock - 1) / kProjectBlock;
     if (blocks == 0 && a.schedUnits == 0) return;  // (an empty frame still orders its blend units)
     hipLaunchKernelGGL(k_records_in, dim3(blocks + (a.schedUnits ? 1u : 0u)), dim3(kProjectBlock), 0, s,
                        (const SplatRecord*)records, a, A.renderData, A.bounds, A.rec, A.tileCounts, A.tileMasks,
-                       A.blockSums, A.sincosTable, devCount, A.unitCost, A.unitOrder, A.costMax,
-                       slots ? *slots : SlotIn{});
+                       A.blockSums, A.sincosTable, devCount, A.unitCost, A.unitOrder, A.costMax);
 }
 
 void launch_scan_sums(uint32_t* sums, uint32_t nb, uint32_t cap, TileAssignmentHeader* hdr, uint32_t* queue,

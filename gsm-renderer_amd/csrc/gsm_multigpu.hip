@@ -5,13 +5,16 @@
 // allocation; at set-up the ranks open each other's (IPC handles exchanged by the caller, or over
 // an RCCL communicator).  Per frame, enqueue-only on the caller's stream, no host synchronisation
 // and no collective library:
-//   phase 0  project the rank's id range once (GlobalRenderer::partitionDirect: k_project_part<DIRECT>)
-//            and write every record straight into each slab owner's receive slots -- slot = global
-//            gaussian id, so no count has to be exchanged first -- with the slot-mask word of every 64
-//            ids for every slab; the workgroups arrive at barrier 1;
-//   phase 1  nothing since r04 (the push is part of phase 0; the phase number stays for the ABI);
-//   phase 2  wait at barrier 1; the owner renders its tile rows from its slots in id order (the
-//            stable sort's tie order); when gathering, the blend writes its pixels (colour, and
+//   phase 0  project the rank's id range once and count its records per destination slab
+//            (GlobalRenderer::partitionCounts: k_project_part, k_part_scan); k_part_scan's workgroup
+//            for slab s stores its total into column s of row `rank` of every rank's count matrix and
+//            arrives at barrier 0;
+//   phase 1  wait at barrier 0; k_part_push: every record goes straight from the projection into
+//            its slab owner's receive buffer, at the offset the count matrix gives -- rank order, so
+//            the receiver's records are in ascending id order (the stable sort's tie order); its
+//            workgroups arrive at barrier 1;
+//   phase 2  wait at barrier 1; the owner renders its tile rows from the received records, their
+//            count read on the device; when gathering, the blend writes its pixels (colour, and
 //            depth when asked) straight into rank 0's frame and its waves arrive at barrier 2;
 //   phase 3  rank 0 waits at barrier 2 for every slab (then copies the frame to the caller's
 //            targets unless the caller renders into the library frame itself).
@@ -21,18 +24,16 @@
 // themselves -- every storing unit drains its stores, then adds to the rank's arrival counter, and the
 // last unit raises the rank's flag in every rank's control block.  A wait is k_mg_sync: lane p polls
 // the flag of rank p (relaxed system-scope loads, bounded by a timeout), then an acquire at system
-// scope; every consumer load of exchange data is system-coherent (ld_sys32 / ld_sys64 / ld_sys128),
-// and before the caller may read rank 0's gathered frame, kSyncWaitBlocks workgroups acquire so that
-// every XCD's L2 drops its lines of it.  Nothing relies on the fence scope HIP puts between kernels.
+// scope; every consumer load of exchange data is system-coherent (ld_sys32 / ld_sys128), and before
+// the caller may read rank 0's gathered frame, kSyncWaitBlocks workgroups acquire so that every XCD's
+// L2 drops its lines of it.  Nothing relies on the fence scope HIP puts between two kernels.
 // Errors: a rank whose frame is refused (check: validated before anything is enqueued) still
-// performs every barrier of the frame, arriving with the failure bit set (it pushed nothing: its
-// slots are void at every owner that frame), so the epochs of all ranks stay aligned; a peer waiting
-// on such an arrival counts it (peer_errors) and the next frame is unaffected.  A wait that times out
-// skips the remaining waits of that frame only.
-// Ordering across frames: the receive slots and their masks are double-buffered by frame parity.  A
-// rank pushes frame k + 2 into the parity of frame k only after its own wait at frame k + 1's
-// barrier 1, which needs every owner's arrival at that barrier -- made by the owner's frame k + 1
-// projection, after its stream finished reading frame k's slots.
+// performs every barrier of the frame, arriving with the failure bit set and zero counts, so the
+// epochs of all ranks stay aligned; a peer waiting on such an arrival counts it (peer_errors) and
+// the next frame is unaffected.  A wait that times out skips the remaining waits of that frame only.
+// Ordering across frames: a rank arrives at frame k + 1's barrier 0 only after its stream finished
+// frame k, so no record or pixel of frame k + 1 is written into a rank before it is done reading
+// frame k; the count matrix is double-buffered by frame parity.
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
@@ -74,21 +75,18 @@ const Rccl& rccl() {
     return R;
 }
 
-// exchange allocation layout (bytes from its base): control words, the slot masks (one bit per
-// gaussian id, two frame parities), the receive slots (one SplatRecord per gaussian id, two
-// parities), on rank 0 the gathered colour and depth frames
-constexpr uint32_t kBarriers = 3;     // barrier 0 is unused since r04 (the direct push exchanges no counts)
+// exchange allocation layout (bytes from its base)
+constexpr uint32_t kBarriers = 3;
 constexpr size_t kFlagWords = 0;      // u32 flag[kBarriers][kMaxSlabs]: [b][src] = last frame src reached b
 constexpr size_t kStatusWord = 64;    // u32 [0] barrier timeouts, [1] failed peer arrivals, [2] epoch of the last timeout
-constexpr size_t kFailedWord = 128;   // u32 [kMaxSlabs]: the epoch at which source p's frame failed (barrier 1)
-constexpr size_t kMaskOff = 4096;     // u64 slot-mask words, parity 0 then parity 1
+constexpr size_t kCountsWord = 256;   // u32 counts[2][kMaxSlabs * kMaxSlabs] (frame parity; row = source)
+constexpr size_t kRecordsOff = 4096;  // SplatRecord[capacity]
 static_assert(kFlagWords + kBarriers * kMaxSlabs <= kStatusWord, "flags before the status word");
-static_assert(kFailedWord + kMaxSlabs <= kMaskOff / 4, "control words in the first 4 KiB");
 constexpr uint32_t kFailBit = 0x80000000u;  // a flag's epoch with this bit: that rank's frame failed
 constexpr uint32_t kEpochMask = 0x7FFFFFFFu;
 constexpr uint32_t kSyncWaitBlocks = 32;    // workgroups of a wait: >= 4 per XCD (blocks are dealt round robin)
 constexpr uint32_t kHandleMagic = 0x58534D47u;  // "GMSX"
-constexpr uint32_t kHandleVersion = 3;
+constexpr uint32_t kHandleVersion = 2;
 
 struct ExchangeFields {
     uint32_t magic, version;
@@ -98,8 +96,6 @@ struct ExchangeFields {
     int32_t pid, device;
     uint64_t base;      // device address in the owner's process (a same-process peer uses it directly)
     uint64_t bytes;
-    uint64_t maskBytes; // bytes of one parity's slot mask (from kMaskOff)
-    uint64_t recOff;    // the receive slots of parity 0 (parity 1 follows after capacity records)
     uint64_t frameOff;  // rank 0: the gathered colour frame; 0 elsewhere
     uint64_t depthOff;  // rank 0: the gathered r16f depth frame; 0 elsewhere
     uint32_t interleave;  // slab rows interleaved (GSM_MG_ROWS=interleaved): every rank must agree
@@ -125,15 +121,19 @@ size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 //    at system scope (its CU's L1 and its XCD's L2 drop their lines of the exchange memory).  Block 0
 //    counts a timeout (status[0], and the frame's epoch in status[2]: the frame's later waits skip)
 //    and every arrival carrying the failure bit (status[1]).
-//    At barrier 1 block 0 also records which sources arrived failed (kFailedWord: their slots are
-//    void this frame).
-//  * arrive (one workgroup; a rank that renders nothing, or one whose frame failed): this rank's
-//    flag in every rank's control block (with kFailBit when `fail`).
+//  * arrive (one workgroup; a rank that renders nothing, or one whose frame failed): zero counts
+//    into row `rank` of every count matrix when `publishZero`, a system-scope release, then this
+//    rank's flag in every rank's control block (with kFailBit when `fail`).
 __global__ __launch_bounds__(64) void k_mg_sync(SyncPeers peers, uint32_t* __restrict__ mine, uint32_t rank,
-                                                uint32_t world, uint32_t barrier, uint32_t epoch, int arrive, int fail,
-                                                unsigned long long timeoutTicks) {
+                                                uint32_t world, uint32_t barrier, uint32_t epoch, int publishZero,
+                                                uint32_t parity, int arrive, int fail, unsigned long long timeoutTicks) {
     const uint32_t lane = threadIdx.x;
     if (arrive) {
+        if (publishZero && lane < world) {
+            uint32_t* row = peers.ctl[lane] + kCountsWord + parity * kMaxSlabs * kMaxSlabs + rank * world;
+            for (uint32_t s = 0; s < world; ++s) __hip_atomic_store(row + s, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (write-through stores, drained)
         if (lane < world)
             __hip_atomic_store(peers.ctl[lane] + kFlagWords + barrier * kMaxSlabs + rank, epoch | (fail ? kFailBit : 0u),
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -164,8 +164,6 @@ __global__ __launch_bounds__(64) void k_mg_sync(SyncPeers peers, uint32_t* __res
         }
     }
     if (failed && blockIdx.x == 0) __hip_atomic_fetch_add(status + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    if (barrier == 1 && blockIdx.x == 0 && lane < world)
-        __hip_atomic_store(mine + kFailedWord + lane, failed ? epoch : 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
 }
 
@@ -211,7 +209,7 @@ class MultiGpu {
         timeoutTicks_ = (unsigned long long)ms * wallKHz_;
         return GSM_OK;
     }
-    gsm_status counts(uint32_t* hostCounts);  // world x world from the slot masks, after the frame's work
+    gsm_status counts(uint32_t* hostCounts);  // world x world, after the frame's stream work
     gsm_status copyExchange(void* dst, size_t bytes) {
         hipSetDevice(device_);
         return hipMemcpy(dst, mem_, bytes < memBytes_ ? bytes : memBytes_, hipMemcpyDeviceToHost) == hipSuccess
@@ -257,37 +255,23 @@ class MultiGpu {
     // kSyncWaitBlocks workgroups acquire (every XCD's L2 drops its lines of the frame)
     void wait(hipStream_t s, uint32_t barrier) {
         hipLaunchKernelGGL(k_mg_sync, dim3(barrier == 2 ? kSyncWaitBlocks : 1u), dim3(64), 0, s, sync_, ctl(),
-                           (uint32_t)rank_, (uint32_t)world_, barrier, frame_, 0, 0, timeoutTicks_);
+                           (uint32_t)rank_, (uint32_t)world_, barrier, frame_, 0, frame_ & 1u, 0, 0, timeoutTicks_);
     }
-    void arrive(hipStream_t s, uint32_t barrier, bool fail) {
+    void arrive(hipStream_t s, uint32_t barrier, bool publishZero, bool fail) {
         hipLaunchKernelGGL(k_mg_sync, dim3(1), dim3(64), 0, s, sync_, ctl(), (uint32_t)rank_, (uint32_t)world_, barrier,
-                           frame_, 1, fail ? 1 : 0, timeoutTicks_);
-    }
-    // this frame's parity of rank p's slot mask / receive slots
-    unsigned long long* slotMask(int p) const {
-        return (unsigned long long*)((char*)sync_.ctl[p] + kMaskOff + (frame_ & 1u) * peerMaskBytes_[p]);
-    }
-    SplatRecord* slots(int p) const {
-        return (SplatRecord*)((char*)sync_.ctl[p] + peerRecOff_[p] +
-                              (size_t)(frame_ & 1u) * peerCap_[p] * sizeof(SplatRecord));
-    }
-    // ids per rank: a multiple of 256, so that no workgroup or mask word spans two ranks
-    static uint32_t idsPerRank(uint32_t n, uint32_t world) {
-        const uint32_t per = (n + world - 1) / world;
-        return (per + 255u) / 256u * 256u;
+                           frame_, publishZero ? 1 : 0, frame_ & 1u, 1, fail ? 1 : 0, timeoutTicks_);
     }
 
     GlobalRenderer* r_ = nullptr;
     int rank_ = 0, world_ = 1, device_ = 0;
     char* mem_ = nullptr;  // this rank's exchange allocation (fine-grained)
     size_t memBytes_ = 0, frameOff_ = 0, framePitch_ = 0, depthOff_ = 0, depthPitch0_ = 0;
-    size_t maskBytes_ = 0, recOff_ = 0;  // one parity's slot mask; the receive slots (all ranks alike)
     uint32_t bpp_ = 8, capacity_ = 0, minCap_ = 0;
-    uint32_t lastN_ = 0;              // gaussians of the last frame begun (counts())
+    uint32_t* sendCounts_ = nullptr;  // this rank's per-slab counts (k_part_scan)
+    uint32_t* recvCount_ = nullptr;   // records this rank receives (k_part_push, block 0)
     uint32_t* done_ = nullptr;        // arrival counters, one 64-B line per barrier (own device memory)
     SyncPeers sync_{};
-    size_t peerMaskBytes_[kMaxSlabs] = {}, peerRecOff_[kMaxSlabs] = {};  // every rank's layout (its handle)
-    uint32_t peerCap_[kMaxSlabs] = {};
+    SlabPeers recs_{};
     char* frame0_ = nullptr;  // rank 0's gathered colour frame (peer mapping on the other ranks)
     char* depth0_ = nullptr;  // rank 0's gathered depth frame
     bool connected_ = false;
@@ -305,10 +289,10 @@ void MultiGpu::release() {
     hipSetDevice(device_);
     for (void* p : opened_) hipIpcCloseMemHandle(p);
     opened_.clear();
-    for (void* p : {(void*)mem_, (void*)done_})
+    for (void* p : {(void*)mem_, (void*)sendCounts_, (void*)recvCount_, (void*)done_})
         if (p) hipFree(p);
     mem_ = nullptr;
-    done_ = nullptr;
+    sendCounts_ = recvCount_ = done_ = nullptr;
 }
 
 gsm_status MultiGpu::prepare(GlobalRenderer* r, int rank, int world, MultiGpu** out, void* handle) {
@@ -336,15 +320,12 @@ gsm_status MultiGpu::prepare(GlobalRenderer* r, int rank, int world, MultiGpu** 
     m->timeoutTicks_ = 10000ull * m->wallKHz_;
     const char* rv = getenv("GSM_MG_ROWS");  // every rank must agree: checked at connect (the handle)
     m->interleave_ = rv && std::strcmp(rv, "interleaved") == 0;
-    const size_t recBytes = (size_t)m->capacity_ * sizeof(SplatRecord);  // one parity's slots
-    m->maskBytes_ = align_up(((size_t)m->capacity_ + 63u) / 64u * 8u, 4096);
-    m->recOff_ = kMaskOff + 2 * m->maskBytes_;
-    const size_t slotsEnd = m->recOff_ + 2 * recBytes;
+    const size_t recBytes = (size_t)m->capacity_ * sizeof(SplatRecord);
     m->framePitch_ = align_up((size_t)r->maxWidth() * m->bpp_, 16);
     m->depthPitch0_ = align_up((size_t)r->maxWidth() * 2u, 16);
-    m->frameOff_ = rank == 0 ? align_up(slotsEnd, 4096) : 0;
+    m->frameOff_ = rank == 0 ? align_up(kRecordsOff + recBytes, 4096) : 0;
     m->depthOff_ = rank == 0 ? align_up(m->frameOff_ + m->framePitch_ * r->maxHeight(), 4096) : 0;
-    m->memBytes_ = rank == 0 ? m->depthOff_ + m->depthPitch0_ * r->maxHeight() : slotsEnd;
+    m->memBytes_ = rank == 0 ? m->depthOff_ + m->depthPitch0_ * r->maxHeight() : kRecordsOff + recBytes;
     hipError_t ae = m->memKind_ == 2u ? hipMalloc((void**)&m->mem_, m->memBytes_)
                                       : hipExtMallocWithFlags((void**)&m->mem_, m->memBytes_,
                                                               m->memKind_ == 1u ? hipDeviceMallocUncached
@@ -352,8 +333,10 @@ gsm_status MultiGpu::prepare(GlobalRenderer* r, int rank, int world, MultiGpu** 
     // the partition buffers now, so that no frame can fail on an allocation
     bool ok = ae == hipSuccess && r->ensurePartitionBuffers() == GSM_OK &&
               (!getenv("GSM_MG_POISON") || hipMemset(m->mem_, 0xAB, m->memBytes_) == hipSuccess) &&
-              hipMemset(m->mem_, 0, m->recOff_) == hipSuccess &&  // control words and both slot masks
+              hipMemset(m->mem_, 0, kRecordsOff) == hipSuccess &&
+              hipMalloc(&m->sendCounts_, kMaxSlabs * 4) == hipSuccess && hipMalloc(&m->recvCount_, 4) == hipSuccess &&
               hipMalloc(&m->done_, kBarriers * 64) == hipSuccess &&
+              hipMemset(m->sendCounts_, 0, kMaxSlabs * 4) == hipSuccess && hipMemset(m->recvCount_, 0, 4) == hipSuccess &&
               hipMemset(m->done_, 0, kBarriers * 64) == hipSuccess && hipDeviceSynchronize() == hipSuccess;
     ExchangeHandle h;
     std::memset(&h, 0, sizeof(h));
@@ -376,8 +359,6 @@ gsm_status MultiGpu::prepare(GlobalRenderer* r, int rank, int world, MultiGpu** 
     h.device = m->device_;
     h.base = (uint64_t)(uintptr_t)m->mem_;
     h.bytes = m->memBytes_;
-    h.maskBytes = m->maskBytes_;
-    h.recOff = m->recOff_;
     h.frameOff = m->frameOff_;
     h.depthOff = m->depthOff_;
     h.interleave = m->interleave_ ? 1u : 0u;
@@ -433,9 +414,8 @@ gsm_status MultiGpu::connect(const void* all) {
             base[p] = (char*)ptr;
         }
         sync_.ctl[p] = (uint32_t*)base[p];
-        peerMaskBytes_[p] = h.maskBytes;
-        peerRecOff_[p] = h.recOff;
-        peerCap_[p] = h.capacity;
+        recs_.recv[p] = (SplatRecord*)(base[p] + kRecordsOff);
+        recs_.cap[p] = h.capacity;
     }
     frame0_ = base[0] + hs[0].frameOff;
     depth0_ = base[0] + hs[0].depthOff;
@@ -515,54 +495,52 @@ gsm_status MultiGpu::phase(int p, hipStream_t s, const gsm_gaussian_input& in, c
     // failed frame arrives with the failure bit (and zero counts), so every rank's epochs stay equal.
     switch (p) {
         case 0: {
-            lastN_ = in.gaussian_count;
             if (frameErr_ == GSM_OK) {
-                // the rank's id range: a multiple of 256 ids per rank (idsPerRank)
+                // the rank's id range (gsm_amd.exchange.id_range)
                 const uint32_t N = in.gaussian_count;
-                const uint32_t perIds = idsPerRank(N, world);
+                const uint32_t perIds = (N + world - 1) / world;
                 const uint32_t first = rank * perIds < N ? rank * perIds : N;
                 const uint32_t cnt = perIds < N - first ? perIds : N - first;
-                MgPush push{};
-                for (uint32_t q = 0; q < world; ++q) {
-                    push.recv[q] = slots((int)q);
-                    push.mask[q] = slotMask((int)q);
-                }
-                push.first = first;
-                push.slots = N;
-                push.arrive = arrival(1);
+                CountPublish pub{};
+                for (uint32_t q = 0; q < world; ++q)
+                    pub.row[q] = sync_.ctl[q] + kCountsWord + (frame_ & 1u) * kMaxSlabs * kMaxSlabs + rank * world;
+                pub.arrive = arrival(0);
                 // the slab's blend units are ordered inside this launch (the long kernel of the frame's
-                // first half), not in the records-in launch of phase 2
+                // first half), not in the short records-in launch of phase 2
                 if (mine && (st = setRows()) != GSM_OK) frameErr_ = st;
                 if (frameErr_ == GSM_OK &&
-                    (st = r_->partitionDirect(s, in, cam, width, height, first, cnt, rows, world, mine, interleave_,
-                                              push)) != GSM_OK)
+                    (st = r_->partitionCounts(s, in, cam, width, height, first, cnt, rows, world, sendCounts_, mine,
+                                              interleave_, &pub)) != GSM_OK)
                     frameErr_ = st;  // (refused before any launch)
             }
-            if (frameErr_ != GSM_OK) arrive(s, 1, /*fail=*/true);  // pushed nothing: its slots are void
+            if (frameErr_ != GSM_OK) arrive(s, 0, /*publishZero=*/true, /*fail=*/true);
             break;
         }
-        case 1:  // (the push is part of phase 0)
+        case 1: {
+            wait(s, 0);  // every rank's counts are in my matrix
+            if (frameErr_ == GSM_OK) {
+                const uint32_t* counts = ctl() + kCountsWord + (frame_ & 1u) * kMaxSlabs * kMaxSlabs;
+                if ((st = r_->partitionPush(s, world, rank, counts, recs_, recvCount_, arrival(1))) != GSM_OK)
+                    frameErr_ = st;
+            }
+            if (frameErr_ != GSM_OK) arrive(s, 1, false, true);
             break;
+        }
         case 2: {
-            wait(s, 1);  // every rank's records of my slab are in my slots
+            wait(s, 1);  // every record of my slab has arrived
             const bool signal = t.gather && world > 1;  // rank 0 waits for every slab's pixels
             bool arrived = false;
             if (frameErr_ == GSM_OK && mine) {
                 if ((st = setRows()) == GSM_OK) {
                     const MgArrive ba = arrival(2);
-                    SlotIn si;
-                    si.mask = slotMask(rank_);
-                    si.failedEpoch = ctl() + kFailedWord;
-                    si.epoch = frame_;
-                    si.perIds = idsPerRank(in.gaussian_count, world);
-                    st = r_->renderRecords(s, slots(rank_), in.gaussian_count, width, height, t.color, t.colorPitch,
-                                           t.depth, t.depthPitch, nullptr, /*preOrdered=*/true, signal ? &ba : nullptr,
-                                           &si);
+                    st = r_->renderRecords(s, mem_ + kRecordsOff, capacity_, width, height, t.color, t.colorPitch,
+                                           t.depth, t.depthPitch, recvCount_, /*preOrdered=*/true,
+                                           signal ? &ba : nullptr);
                     arrived = signal && st == GSM_OK;  // the blend's waves arrive
                 }
                 if (st != GSM_OK) frameErr_ = st;
             }
-            if (signal && !arrived) arrive(s, 2, frameErr_ != GSM_OK);
+            if (signal && !arrived) arrive(s, 2, false, frameErr_ != GSM_OK);
             break;
         }
         case 3: {
@@ -602,17 +580,10 @@ gsm_status MultiGpu::status(uint32_t* timeouts, uint32_t* peerErrors, bool clear
 }
 
 gsm_status MultiGpu::counts(uint32_t* hostCounts) {
-    // counts[r][s] = records rank r pushed to slab s in the last frame: the set bits of rank s's slot
-    // mask over rank r's ids (every rank's mask through its mapping)
     hipSetDevice(device_);
-    const uint32_t N = lastN_, world = (uint32_t)world_, per = idsPerRank(N, world);
-    std::vector<unsigned long long> w(((size_t)N + 63u) / 64u);
-    std::memset(hostCounts, 0, (size_t)world * world * 4);
-    for (uint32_t sl = 0; sl < world && N > 0; ++sl) {
-        if (hipMemcpy(w.data(), slotMask((int)sl), w.size() * 8, hipMemcpyDeviceToHost) != hipSuccess)
-            return GSM_ERR_RENDER_FAILED;
-        for (size_t i = 0; i < w.size(); ++i) hostCounts[(uint32_t)(i * 64u / per) * world + sl] += (uint32_t)__builtin_popcountll(w[i]);
-    }
+    const uint32_t* c = ctl() + kCountsWord + (frame_ & 1u) * kMaxSlabs * kMaxSlabs;
+    if (hipMemcpy(hostCounts, c, (size_t)world_ * world_ * 4, hipMemcpyDeviceToHost) != hipSuccess)
+        return GSM_ERR_RENDER_FAILED;
     return GSM_OK;
 }
 

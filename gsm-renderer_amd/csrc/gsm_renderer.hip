@@ -258,7 +258,7 @@ gsm_status GlobalRenderer::render(hipStream_t s, const gsm_gaussian_input& in,
 gsm_status GlobalRenderer::renderRecords(hipStream_t s, const void* records, uint32_t count, uint32_t width,
                                          uint32_t height, void* color, size_t colorPitch, void* depth,
                                          size_t depthPitch, const uint32_t* devCount, bool preOrdered,
-                                         const MgArrive* blendArrive, const SlotIn* slots) {
+                                         const MgArrive* blendArrive) {
     // devCount: the count lives on the device (multi-GPU exchange, gsm_multigpu_render); `count` is
     // then the capacity the grids cover
     gsm_status st = validateFrame(count, !records, width, height, color, colorPitch, depth, depthPitch);
@@ -268,7 +268,7 @@ gsm_status GlobalRenderer::renderRecords(hipStream_t s, const void* records, uin
     const ProjectArgs a = frameArgs(cam, width, height, count, 1);
     return runFrame(s, a, width, height, color, colorPitch, depth, depthPitch,
                     [&](const ProjectArgs& pa) {
-                        launch_records_in(records, pa, arena_, s, devCount, slots);
+                        launch_records_in(records, pa, arena_, s, devCount);
                     }, devCount, preOrdered, blendArrive);
 }
 
@@ -282,7 +282,6 @@ gsm_status GlobalRenderer::preparePartition(const gsm_gaussian_input& in, const 
     if (width == 0 || height == 0 || width > maxWidth_ || height > maxHeight_)
         return GSM_ERR_INVALID_DIMENSIONS;
     if (!slabRows || numSlabs == 0 || numSlabs > kMaxSlabs) return GSM_ERR_INVALID_ARGUMENT;
-    // (sendCounts == kNoCounts: the direct push keeps no per-slab counts)
     if (!sendCounts || (count > 0 && ((needSend && !send) || !in.gaussians || !in.harmonics)))
         return GSM_ERR_MISSING_REQUIRED_BUFFER;
     std::memset(&f->slabs, 0, sizeof(f->slabs));
@@ -348,23 +347,6 @@ gsm_status GlobalRenderer::partitionCounts(hipStream_t s, const gsm_gaussian_inp
     f.a.schedUnits = orderUnits ? scheduleUnits(s, width, height) : 0u;
     launch_partition_counts(f.half, f.deg, f.world, f.harm, f.a, f.slabs, part_, arena_.sincosTable, sendCounts,
                             arena_, publish ? *publish : CountPublish{}, s);
-    partCount_ = count;
-    partSlabs_ = f.slabs;
-    if (hipGetLastError() != hipSuccess) return GSM_ERR_RENDER_FAILED;
-    return GSM_OK;
-}
-
-gsm_status GlobalRenderer::partitionDirect(hipStream_t s, const gsm_gaussian_input& in, const gsm_camera_params& camp,
-                                           uint32_t width, uint32_t height, uint32_t first, uint32_t count,
-                                           const uint32_t* slabRows, uint32_t numSlabs, bool orderUnits,
-                                           bool interleave, const MgPush& push) {
-    PartitionFrame f;
-    static const uint32_t kNoCounts = 0;
-    gsm_status st = preparePartition(in, camp, width, height, first, count, slabRows, numSlabs, false, nullptr,
-                                     &kNoCounts, &f, interleave);
-    if (st != GSM_OK) return st;
-    f.a.schedUnits = orderUnits ? scheduleUnits(s, width, height) : 0u;
-    launch_partition_direct(f.half, f.deg, f.world, f.harm, f.a, f.slabs, part_, arena_.sincosTable, arena_, push, s);
     partCount_ = count;
     partSlabs_ = f.slabs;
     if (hipGetLastError() != hipSuccess) return GSM_ERR_RENDER_FAILED;

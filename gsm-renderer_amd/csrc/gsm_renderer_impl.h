@@ -42,17 +42,10 @@ class GlobalRenderer {
     gsm_status partitionPush(hipStream_t stream, uint32_t world, uint32_t rank, const uint32_t* counts,
                              const SlabPeers& peers, uint32_t* recvCount, const MgArrive& arrive);
     // blendArrive (nullable): the blend's waves arrive at that barrier after their pixel stores
-    // slots (nullable): `count` receive slots indexed by global id with their slot mask (MgPush)
     gsm_status renderRecords(hipStream_t stream, const void* records, uint32_t count, uint32_t width,
                              uint32_t height, void* color, size_t colorPitch, void* depth, size_t depthPitch,
                              const uint32_t* devCount = nullptr, bool preOrdered = false,
-                             const MgArrive* blendArrive = nullptr, const SlotIn* slots = nullptr);
-    // the multi-GPU frame's projection of ids [first, first + count) with the direct push into every
-    // slab owner's receive slots (push: peer mappings, barrier 1); orderUnits as partitionCounts
-    gsm_status partitionDirect(hipStream_t stream, const gsm_gaussian_input& input, const gsm_camera_params& camera,
-                               uint32_t width, uint32_t height, uint32_t first, uint32_t count,
-                               const uint32_t* slabRows, uint32_t numSlabs, bool orderUnits, bool interleave,
-                               const MgPush& push);
+                             const MgArrive* blendArrive = nullptr);
     // what renderRecords / the multi-GPU frame would refuse, checked before anything is enqueued
     gsm_status validateFrame(uint32_t count, bool inputMissing, uint32_t width, uint32_t height,
                              const void* color, size_t colorPitch, const void* depth, size_t depthPitch) const;

@@ -1346,7 +1346,7 @@ Tuning tuning_from_env(int device) {
     const char* ws = getenv("GSM_SORT_WIDE");
     t.wideSort = !(ws && ws[0] == '0');
     const char* w12 = getenv("GSM_SORT_WIDE12");
-    t.wide12 = !(w12 && w12[0] == '0');
+    t.wide12 = w12 && w12[0] == '1';
     return t;
 }
 

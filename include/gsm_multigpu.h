@@ -17,12 +17,12 @@
  *
  * gsm_multigpu_* run the whole protocol inside the library with no host round trip and no
  * collective library in the frame: every rank owns one fine-grained "exchange" allocation
- * (control words, the slot masks, its receive slots of records and, on rank 0, the gathered
+ * (control words, the count matrix, its receive buffer of records and, on rank 0, the gathered
  * colour and depth frames), the ranks open each other's exchange allocations once (IPC handles),
- * and per frame the records and the slab pixels are written straight into the owners' memory by
- * the producing kernels (xGMI stores between GPUs) with system-coherent write-through stores; the
- * producers then arrive at a device-side flag barrier themselves, and every consumer load of
- * exchange data is system-coherent.
+ * and per frame the counts, the records and the slab pixels are written straight into the owners'
+ * memory by the producing kernels (xGMI stores between GPUs) with system-coherent write-through
+ * stores; the producers drain them and then arrive at a device-side flag barrier themselves, and
+ * every consumer load of exchange data is system-coherent.
  * gsm_global_project_partition / gsm_global_render_records remain for callers that move the
  * records themselves.
  */
@@ -66,8 +66,7 @@ gsm_status gsm_global_render_records(gsm_renderer *renderer, void *stream, const
  * max_width / max_height).  Set-up is collective and happens once, in two steps around an
  * exchange the caller performs with any transport (torch.distributed, MPI, sockets, ...):
  *   gsm_multigpu_prepare   allocates this rank's exchange memory (fine-grained device memory:
- *                          control words, 2 x max_gaussians slot-mask bits and 48-B record
- *                          slots (two frame parities),
+ *                          control words, 2 x W x W counts, max_gaussians x 48-B records,
  *                          and on rank 0 the gathered colour frame and r16f depth frame,
  *                          max_width x max_height pixels each) and the renderer's partition
  *                          buffers, and writes its GSM_MULTIGPU_HANDLE_BYTES handle into `handle`.
@@ -102,12 +101,12 @@ void gsm_multigpu_destroy(gsm_multigpu *multigpu);
  * Rank r owns tile rows [r * ceil(tiles_y / W), +ceil(tiles_y / W)), or -- when every rank's
  * process has GSM_MG_ROWS=interleaved in its environment at gsm_multigpu_prepare -- rows r, r + W,
  * r + 2W, ... (balances content off the frame's centre; a record then travels to every rank one of
- * its rect's rows maps to).  Rank r's ids are [r * P, (r + 1) * P), P = ceil(N / W) rounded up to
- * a multiple of 256.  Per frame, on `stream`:
- *   1+2. projection of the rank's ids; every record written straight into the receive slots of
- *      each slab owner it meets -- slot = the gaussian's id, so no count is exchanged first -- with
- *      one slot-mask bit per id (slots and masks double-buffered by frame parity), flag barrier;
- *   3. the owner renders its rows from its slots in id order (the stable sort's tie order);
+ * its rect's rows maps to).  Per frame, on `stream`:
+ *   1. projection of the rank's ids, per-slab record counts written into every rank's count
+ *      matrix, flag barrier;
+ *   2. every record written straight into its slab owner's receive buffer (offsets from the
+ *      count matrix: rank order), flag barrier;
+ *   3. the owner renders its rows from the received records (their count read on the device);
  *      when gathering, colour goes to rank 0's gathered frame and -- when depth_r16f is non-NULL
  *      -- depth to rank 0's gathered depth frame (GlobalRenderer.swift:350 writes depth with
  *      every frame); without gathering both go to the rank's own targets (full-frame addressed,
@@ -158,16 +157,15 @@ gsm_status gsm_multigpu_debug_copy_frame(gsm_multigpu *multigpu, void *host_dst,
 gsm_status gsm_multigpu_debug_copy_depth(gsm_multigpu *multigpu, void *host_dst, size_t dst_pitch_bytes,
                                          uint32_t width, uint32_t height);
 
-/* The first `bytes` of this rank's exchange allocation (control words from byte 0, the slot masks
- * from byte 4096, then the receive slots), synchronous. */
+/* The first `bytes` of this rank's exchange allocation (control words from byte 0, the count matrix
+ * from byte 1024, the received records from byte 4096), synchronous. */
 gsm_status gsm_multigpu_debug_copy_exchange(gsm_multigpu *multigpu, void *host_dst, size_t bytes);
 
-/* The last frame's world x world record counts (row = source rank, column = slab), from the slot
- * masks, synchronous. */
+/* The last frame's world x world record counts (row = source rank, column = slab), synchronous. */
 gsm_status gsm_multigpu_debug_counts(gsm_multigpu *multigpu, uint32_t *host_counts);
 
-/* gsm_multigpu_render in four phases (0: projection + records pushed + barrier; 1: nothing since
- * r04; 2: slab render + the gather signal; 3: rank 0's gather wait + copy); render = phases 0..3, each
+/* gsm_multigpu_render in four phases (0: projection + counts + barrier; 1: records + barrier;
+ * 2: slab render + the gather signal; 3: rank 0's gather wait + copy); render = phases 0..3, each
  * called even after an earlier phase of the frame returned an error (GSM_ERR_INVALID_ARGUMENT and
  * nothing enqueued for a phase out of order).
  * For W ranks driven from ONE host thread (virtual ranks of a test or a timing tool, e.g. W

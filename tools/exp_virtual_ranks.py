@@ -32,6 +32,7 @@ def main():
                     help="also time the whole frame on one renderer (same scene, same box): one_gpu_frame_ms")
     ap.add_argument("--trace-rank", type=int, default=-1,
                     help="per-unit blend trace of this rank's slab (profiling bit 2) -> gpurun_out/vr_trace_*.npz")
+    ap.add_argument("--depth", type=int, default=1, help="gather the r16f depth frame too (product default)")
     a = ap.parse_args()
     import torch
     import gsm_amd as gsm
@@ -62,7 +63,7 @@ def main():
             for k, m in enumerate(mgs):
                 e0, e1 = ev(), ev()
                 e0.record(stream)
-                m.render_phases([p], None, None, inp, cam, w, h, gather=True, gather_depth=True, stream=stream,
+                m.render_phases([p], None, None, inp, cam, w, h, gather=True, gather_depth=bool(a.depth), stream=stream,
                                 gather_target=frame_ptr if k == 0 else None)
                 e1.record(stream)
                 marks.append((p, k, e0, e1))
@@ -152,7 +153,7 @@ def main():
             "pixel_link_ms": round(t_pix, 4), "modelled_frame_ms": round(model_frame, 4),
             "note": "MODEL, not measured: each phase >= its busiest link's bytes at 153 GB/s (7 concurrent "
                     "point-to-point links per GPU); device phases measured on one GPU"}
-    out = {"config": a.config, "world": W, "frames": a.frames, "timeouts": [m.status() for m in mgs],
+    out = {"config": a.config, "world": W, "frames": a.frames, "gather_depth": bool(a.depth), "timeouts": [m.status() for m in mgs],
            "counts": mgs[0].counts().tolist(),
            "phase_ms": {f"phase{p}": [round(float(x), 4) for x in med[p]] for p in range(4)},
            "max_phase_ms": [round(float(med[p].max()), 4) for p in range(4)],

@@ -102,6 +102,13 @@ __global__ __launch_bounds__(NT) void k_blend_px(
     __shared__ uint32_t cscr[NW][16];  // compaction: the alive groups of each wave, in order
     __shared__ __attribute__((aligned(16))) uint4 lrecA[NW][64];  // current batch records
     __shared__ uint32_t lrecB[NW][64];
+    // a gathered multi-GPU frame (flags bit 10): the unit's r16f depth staged per wave, stored at the
+    // unit's end as 16-B write-through stores (2-B write-through stores cost ~12x a 16-B store per
+    // byte on gfx950: MI355X_MICROARCH.md, store flavours)
+    constexpr uint32_t UH = (P == 1) ? 8u : 16u;  // unit rows (units are 16 pixels wide)
+    __shared__ __attribute__((aligned(16))) uint32_t dstage[NW][UH * 8];
+    __shared__ uint32_t exitCount;  // GSM_MG_PIXELS=wb: waves of this workgroup past their last unit
+    if (threadIdx.x == 0) exitCount = 0;
     {
         const uint4* src = (const uint4*)expTable;
         uint4* dst = (uint4*)tbl;
@@ -117,6 +124,7 @@ __global__ __launch_bounds__(NT) void k_blend_px(
     // system-coherent write-through (gsm_internal.h: the wave's arrival at the end then only drains)
     const bool wt = (flags & 1024) != 0;
     const uint32_t colorBytes = (uint32_t)(colorPitch * H), depthBytes = (uint32_t)(depthPitch * H);
+    uint32_t* const dst = dstage[threadIdx.x >> 6];
     auto st128 = [&](uint8_t* p, uint4 v) {
         if (wt) st_sys128_at(color, colorBytes, (uint32_t)(p - color), v);
         else *(uint4*)p = v;
@@ -188,7 +196,9 @@ __global__ __launch_bounds__(NT) void k_blend_px(
                 st32(crow + (size_t)(px + i) * 4, px32);
             }
         }
-        if (depth) {
+        if (depth && wt) {
+            dst[((py & (UH - 1u)) * 16u + (px & 15u)) >> 1] = ud;  // (flush_depth at the unit's end)
+        } else if (depth) {
             if ((flags & 1) && px + 1 < W) {
                 std32(depth + (size_t)py * depthPitch + (size_t)px * 2, ud);
             } else {
@@ -626,6 +636,30 @@ __global__ __launch_bounds__(NT) void k_blend_px(
         for (int q = 0; q < P; ++q)
             write_pair(ux + offX[q], uy + offY[q], (full > 0) ? (ONE - T[q]) : ONE, R[q], G[q], B[q], D[q]);
     unit_end:
+        if (wt && depth) {
+            // every pixel pair of the unit was staged by the writes above (each exactly once); rows
+            // past H were not, and are not stored
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            if (lane < UH * 2u) {
+                const uint32_t r = lane >> 1, hx = (lane & 1u) * 8u;
+                const uint32_t py = uy + r, px = ux + hx;
+                const uint4 v = *(const uint4*)&dst[r * 8u + (hx >> 1)];
+                if (py < H) {
+                    const uint32_t off = (uint32_t)((size_t)py * depthPitch + (size_t)px * 2u);
+                    if ((flags & 2048) && px + 8u <= W) {
+                        st_sys128_at(depth, depthBytes, off, v);
+                    } else {
+                        const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+                        for (uint32_t i = 0; i < 8; ++i)
+                            if (px + i < W) st_sys16_at(depth, depthBytes, off + 2u * i, (uint16_t)(w4[i >> 1] >> (16u * (i & 1u))));
+                    }
+                }
+            }
+            __builtin_amdgcn_wave_barrier();  // the next unit's staging writes after these reads
+        }
         if (unitCost && lane == 0) unitCost[u] = (uint16_t)min(nproc, 65535u);
         waveMax = max(waveMax, min(nproc, 65535u));
         if (trace && lane == 0) {
@@ -646,7 +680,23 @@ __global__ __launch_bounds__(NT) void k_blend_px(
     // multi-GPU frame gathered on rank 0 (gsm_multigpu.hip): the pixels this wave stored into rank
     // 0's frame (write-through, flags bit 10) are drained and the wave arrives at barrier 2 (the last
     // one raises the flags) -- every wave of the grid arrives exactly once, here
-    if (arrive.done) mg_arrive_wave(arrive);
+    if (arrive.done) {
+        if (flags & 4096) {
+            // GSM_MG_PIXELS=wb: plain pixel stores; the workgroup's last exiting wave writes the XCD's
+            // L2 back at system scope (covering every wave of the workgroup: each drained its stores
+            // before its count) and arrives for the workgroup
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            uint32_t old = 0;
+            if (lane == 0) old = __hip_atomic_fetch_add(&exitCount, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (__builtin_amdgcn_readfirstlane(old) == NW - 1u) {
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                mg_arrive_unit(arrive, blockIdx.x);
+            }
+        } else {
+            mg_arrive_unit(arrive, blockIdx.x * NW + (threadIdx.x >> 6));
+        }
+    }
 }
 
 
@@ -680,7 +730,7 @@ static int blend_waves_per_wg(uint32_t numTiles, int numCUs) {
 // SIMD (flags bit 2), later units' priority rising with the age of their walk (flags bit 1).
 void launch_blend(const FrameGeometry& g, const DeviceArena& A, void* color,
                   size_t colorPitch, void* depth, size_t depthPitch, int numCUs, bool costOrder, int colorFormat,
-                  hipStream_t s, int wavesOverride, int claim, const MgArrive* arrive) {
+                  hipStream_t s, int wavesOverride, int claim, const MgArrive* arrive, bool arriveWB) {
     // local tile ids: tile t = k * tilesX + tx of the renderer's row k (pixel row rowBegin + k * rowStride)
     const uint32_t numTiles = g.rowCount * g.tilesX;
     if (numTiles == 0) return;
@@ -690,7 +740,9 @@ void launch_blend(const FrameGeometry& g, const DeviceArena& A, void* color,
                         ? 1
                         : 0;
     const int flags = vec | 2 | (costOrder ? 4 : 0) | ((colorFormat & 15) << 4) | ((claim & 3) << 8) |
-                      (arrive ? 1024 : 0);  // (a gathered multi-GPU frame: write-through pixel stores)
+                      (arrive ? (arriveWB ? 4096 : 1024) : 0) |  // (a gathered multi-GPU frame: write-through
+                                                                 // pixel stores, or the L2 write-back at exit)
+                      ((depth && (((uintptr_t)depth) & 15u) == 0 && (depthPitch & 15u) == 0) ? 2048 : 0);
     // A.tileQueue was zeroed by k_scan_blocks earlier in the frame
     const int P = blend_pairs_per_lane(numTiles, numCUs);
     const int waves = wavesOverride ? wavesOverride : blend_waves_per_wg(numTiles, numCUs);
@@ -701,7 +753,7 @@ void launch_blend(const FrameGeometry& g, const DeviceArena& A, void* color,
     MgArrive ar{};
     if (arrive) {
         ar = *arrive;
-        ar.total = grid * (uint32_t)waves;  // every wave arrives once, at its exit
+        ar.total = arriveWB ? grid : grid * (uint32_t)waves;  // every wave (workgroup) arrives once, at its exit
     }
 #define GSM_LAUNCH_BLEND(NTH, PP, CMP)                                                                       \
     hipLaunchKernelGGL((k_blend_px<NTH, PP, CMP>), dim3(grid), dim3(NTH), 0, s, A.tileStart, A.rec, \

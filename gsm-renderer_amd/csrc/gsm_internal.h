@@ -51,8 +51,10 @@ struct SlabPeers {
     uint32_t cap[kMaxSlabs];  // records each receive buffer holds (k_part_push writes no further)
 };
 struct PartitionBuffers {
-    SplatRecord* records = nullptr;     // [maxG] projected records of the rank's range
-    uint32_t* masks = nullptr;          // [maxG] slabs each gaussian meets
+    SplatRecord* runs = nullptr;        // [slabs][runStride]: the projection's block runs, block b of
+                                        // slab s at s * runStride + b * 256 (k_project_part)
+    uint32_t runStride = 0;             // records per slab: the blocks of maxG ids x 256
+    uint32_t runSlabs = 0;              // slabs `runs` holds
     uint32_t* blockSlabCounts = nullptr;  // [kMaxSlabs * blocks]
 };
 
@@ -80,11 +82,12 @@ struct MgArrive {
 // One arriving unit: called by every lane of ONE wave, after every exchange store the unit signals
 // for (a workgroup arriving as one unit: every wave's `s_waitcnt vmcnt(0)`, then a workgroup
 // barrier, then one wave calls this).
-__device__ __forceinline__ void mg_arrive_wave(const MgArrive& a) {
+// (total: the arriving units, a.total unless the caller counts them otherwise)
+__device__ __forceinline__ void mg_arrive_wave(const MgArrive& a, uint32_t total) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's write-through stores are acknowledged
     uint32_t last = 0;
     if ((threadIdx.x & 63u) == 0)
-        last = __hip_atomic_fetch_add(a.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == a.total - 1u ? 1u : 0u;
+        last = __hip_atomic_fetch_add(a.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == total - 1u ? 1u : 0u;
     if (__builtin_amdgcn_readfirstlane(last)) {
         // every other unit drained its stores before its add: the flags go out after all of them
         const uint32_t lane = threadIdx.x & 63u;
@@ -92,11 +95,38 @@ __device__ __forceinline__ void mg_arrive_wave(const MgArrive& a) {
         if (lane < a.world) __hip_atomic_store(a.flag[lane], a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
+__device__ __forceinline__ void mg_arrive_wave(const MgArrive& a) { mg_arrive_wave(a, a.total); }
 // a workgroup arriving as one unit (see mg_arrive_wave); ends the kernel's use of it
 __device__ __forceinline__ void mg_arrive_block(const MgArrive& a) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x < 64u) mg_arrive_wave(a);
+}
+// Arrivals of many units (thousands of workgroups) spread over kArriveShards counters, each on its
+// own 128-B line after the barrier's main counter (a.done[0]): unit u adds to shard u % kArriveShards;
+// the add completing a shard (its unit count is known from a.total) re-arms that shard and arrives at
+// the main counter for it, whose last add raises the flags (mg_arrive_wave).  Same-address atomics
+// serialize in one L2 channel: 2442 adds to one word cost more than the projection's tail.
+constexpr uint32_t kArriveShards = 16, kArriveLineWords = 32;
+constexpr uint32_t kArriveWordsPerBarrier = (1 + kArriveShards) * kArriveLineWords;
+// called by every lane of ONE wave, after every exchange store of the unit (as mg_arrive_wave)
+__device__ __forceinline__ void mg_arrive_unit(const MgArrive& a, uint32_t unit) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const uint32_t sh = unit % kArriveShards;
+    const uint32_t shTotal = (a.total - sh + kArriveShards - 1u) / kArriveShards;  // (unit < total)
+    uint32_t* c = a.done + (1u + sh) * kArriveLineWords;
+    uint32_t last = 0;
+    if ((threadIdx.x & 63u) == 0)
+        last = __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == shTotal - 1u ? 1u : 0u;
+    if (__builtin_amdgcn_readfirstlane(last)) {
+        if ((threadIdx.x & 63u) == 0) __hip_atomic_store(c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        mg_arrive_wave(a, a.total < kArriveShards ? a.total : kArriveShards);  // (the shards that have units)
+    }
+}
+__device__ __forceinline__ void mg_arrive_block_unit(const MgArrive& a, uint32_t unit) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x < 64u) mg_arrive_unit(a, unit);
 }
 // k_part_scan's count publication: row `rank` of rank p's count matrix (this frame's parity), and
 // the arrival at barrier 0 (arrive.done == null: no publication, the send-buffer path)
@@ -176,6 +206,12 @@ struct Tuning {
     int tileLoBits = 0;       // GSM_SORT_LOBITS=4..8: width of the first tile pass (0: half the tile field)
     int blendClaim = 1;       // GSM_BLEND_CLAIM=early|late|auto (0/1/2): when a blend wave claims its next unit
     bool wideSort = true;     // GSM_SORT_WIDE=0: narrow passes only (no wide 9..11-bit tile or depth passes)
+    bool mgPixelsWB = true;   // a gathered multi-GPU frame's blend stores its pixels plainly and the last
+                              // exiting wave of each workgroup writes the XCD's L2 back at system scope
+                              // before arriving; GSM_MG_PIXELS=wt: write-through pixel stores instead
+                              // (config 4 / W = 8 slab blend 96 -> 75 us with wb: DESIGN.md 7)
+    int mgPushPerCU = 4;      // GSM_MG_PUSH_GRID=k: the push (k_part_copy) runs k workgroups per CU over the
+                              // runs (0: one workgroup per 256-id block)
     bool wide12 = false;      // GSM_SORT_WIDE12=1: a 12-bit tile field (2049..4096 tiles) in one 12-bit
                               // wide pass instead of two narrow passes (measured slower: DESIGN.md 4)
 };
@@ -230,7 +266,7 @@ void launch_partition_counts(bool halfInput, uint32_t shDegree, const void* worl
                              const CountPublish& publish, hipStream_t stream);
 void launch_partition_push(const ProjectArgs& args, uint32_t world, uint32_t rank, const PartitionBuffers& B,
                            const uint32_t* counts, const SlabPeers& peers, uint32_t* recvCount, const SlabTable& slabs,
-                           const MgArrive& arrive, hipStream_t stream);
+                           const MgArrive& arrive, hipStream_t stream, uint32_t gridCap = 0);
 // received records -> per-gaussian arrays + tile counts of the renderer's rows (replaces project)
 void launch_records_in(const void* records, const ProjectArgs& args, const DeviceArena& A,
                        hipStream_t stream, const uint32_t* devCount = nullptr);
@@ -254,7 +290,7 @@ void launch_headers(const uint32_t* sortedKeys, const FrameGeometry& geo, const 
 void launch_blend(const FrameGeometry& geo, const DeviceArena& A,
                   void* color, size_t colorPitch, void* depth, size_t depthPitch, int numCUs,
                   bool costOrder, int colorFormat, hipStream_t stream, int waves = 0, int claim = 1,
-                  const MgArrive* arrive = nullptr);
+                  const MgArrive* arrive = nullptr, bool arriveWB = false);
 // blend kernel shape: pixel pairs per lane (0 = quadrant kernel) and blend units per tile
 int blend_pairs_per_lane(uint32_t numTiles, int numCUs);
 uint32_t blend_units_per_tile(uint32_t numTiles, int numCUs);

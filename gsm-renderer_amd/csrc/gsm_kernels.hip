@@ -478,7 +478,7 @@ __device__ __forceinline__ uint32_t slab_tile_mask(short4 b, uint32_t full, cons
 template <bool HALF, int DEG>
 __global__ __launch_bounds__(kProjectBlock) void k_project_part(
     const void* __restrict__ world, const void* __restrict__ harm, ProjectArgs P, SlabTable slabs,
-    SplatRecord* __restrict__ records, uint32_t* __restrict__ masks,
+    SplatRecord* __restrict__ runs, uint32_t runStride,
     uint32_t* __restrict__ blockSlabCounts, const float2* __restrict__ sincos, const uint16_t* __restrict__ unitCost,
     uint32_t* __restrict__ unitOrder, uint32_t* __restrict__ costMax) {
     // block 0 of a scheduled launch orders the blend units of the rank's own slab (the owner renders
@@ -526,30 +526,36 @@ __global__ __launch_bounds__(kProjectBlock) void k_project_part(
             if ((uint32_t)ty >= sRows[sl] && (uint32_t)ty < sRows[sl + 1u]) atomicOr(&sSlab[lo], 1u << sl);
         }
     });
-    uint32_t mask = 0;
-    if (gid < P.count) {
-        mask = sSlab[tid];
-        if (o.vis) {
-            SplatRecord r;
-            r.rd = o.rd;
-            r.ra = o.ra;
-            r.bounds = o.bounds;
-            r.rb = o.rb;
-            r.pad = sTile[tid];  // the whole rect's answers (slab_tile_mask cuts the slab's part)
-            records[gid] = r;
-        }
-        masks[gid] = mask;
-    }
+    const uint32_t mask = gid < P.count ? sSlab[tid] : 0u;  // (only visible gaussians meet a tile)
     for (uint32_t sl = 0; sl < nSlabs; ++sl) {
         const uint32_t c = (uint32_t)__popcll(__ballot((mask >> sl) & 1u));
         if (lane == 0) wcnt[wave][sl] = c;
     }
     __syncthreads();
+    const uint32_t nb = gridDim.x - (P.schedUnits ? 1u : 0u);
     if (tid < nSlabs) {
         uint32_t t = 0;
 #pragma unroll
         for (int w = 0; w < kProjectBlock / 64; ++w) t += wcnt[w][tid];
-        blockSlabCounts[(size_t)tid * (gridDim.x - (P.schedUnits ? 1u : 0u)) + blk] = t;
+        blockSlabCounts[(size_t)tid * nb + blk] = t;
+    }
+    // the block's run of slab sl: records [sl * runStride + blk * 256, + count), ascending id (lane
+    // order within a wave, wave order within the block), stored from the threads (assembling the runs
+    // in LDS first measured slower: 60.8 against 56.3 us at config 4 / W = 8); the record's last word
+    // is the slab's part of the rect's tile answers (slab_tile_mask)
+    const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    const uint2 bw = __builtin_bit_cast(uint2, o.bounds);
+    const uint32_t tileBits = sTile[tid];
+    for (uint32_t sl = 0; sl < nSlabs; ++sl) {
+        const uint64_t b = __ballot((mask >> sl) & 1u);
+        if ((mask >> sl) & 1u) {
+            uint32_t at = (uint32_t)__popcll(b & lt);
+            for (uint32_t w = 0; w < wave; ++w) at += wcnt[w][sl];
+            uint4* d = (uint4*)(runs + (size_t)sl * runStride + (size_t)blk * kProjectBlock + at);
+            d[0] = o.rd;
+            d[1] = make_uint4(o.ra.x, o.ra.y, o.ra.z, o.ra.w);
+            d[2] = make_uint4(bw.x, bw.y, o.rb, slab_tile_mask(o.bounds, tileBits, slab_rows(slabs, sRows, sl)));
+        }
     }
 }
 
@@ -580,83 +586,69 @@ __global__ __launch_bounds__(1024) void k_part_scan(uint32_t* __restrict__ block
     }
 }
 
-// Writes the block's records of every slab it meets as one contiguous run of the destination
-// (slab-local rank order = ascending id): the 48-B records go through LDS so that consecutive
-// threads store consecutive 16-B words -- whole 64-B segments into exchange or peer memory instead
-// of three 16-B pieces per record 48 B apart.  dst(sl) = the run's first record, cap(sl) = records
-// the destination holds (nothing is written past it).  slabs: the slab table (record masks).
-template <bool WT, class Dst, class Cap>
-__device__ __forceinline__ void write_slab_runs(const SplatRecord* __restrict__ records, uint32_t slabBits,
-                                                uint32_t gid, uint32_t numSlabs, const SlabTable& slabs,
-                                                Dst&& dst, Cap&& cap) {
-    __shared__ uint32_t wcnt[kProjectBlock / 64][kMaxSlabs];
-    __shared__ uint4 sOut[kProjectBlock * 3];
-    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-    uint32_t rnk[kMaxSlabs];
-    for (uint32_t sl = 0; sl < numSlabs; ++sl) {
-        const uint64_t b = __ballot((slabBits >> sl) & 1u);
-        rnk[sl] = (uint32_t)__popcll(b & lt);
-        if (lane == 0) wcnt[wave][sl] = (uint32_t)__popcll(b);
-    }
-    uint4 a = make_uint4(0, 0, 0, 0), b = a, c = a;
-    if (slabBits) {
-        const uint4* src = (const uint4*)(records + gid);
-        a = src[0];
-        b = src[1];
-        c = src[2];
-    }
-    const short4 bounds = __builtin_bit_cast(short4, make_uint2(c.x, c.y));
-    __syncthreads();
-    for (uint32_t sl = 0; sl < numSlabs; ++sl) {
-        uint32_t before = 0, n = 0;
-#pragma unroll
-        for (uint32_t w = 0; w < kProjectBlock / 64; ++w) {
-            const uint32_t x = wcnt[w][sl];
-            before += w < wave ? x : 0u;
-            n += x;
-        }
-        if (n == 0) continue;  // (uniform)
-        if ((slabBits >> sl) & 1u) {
-            uint4* o = sOut + 3u * (before + rnk[sl]);
-            o[0] = a;
-            o[1] = b;
-            o[2] = make_uint4(c.x, c.y, c.z, slab_tile_mask(bounds, c.w, slab_rows(slabs, slabs.rows, sl)));
-        }
-        __syncthreads();
-        uint4* d = (uint4*)dst(sl);
-        const uint64_t room = cap(sl);
-        if constexpr (WT) {  // exchange memory: system-coherent write-through stores (gsm_internal.h)
-            const uint32_t nw = 3u * (uint32_t)min((uint64_t)n, room);
-            for (uint32_t j = threadIdx.x; j < nw; j += kProjectBlock) st_sys128(d, nw * 16u, j, sOut[j]);
-        } else {
-            for (uint32_t j = threadIdx.x; j < 3u * n; j += kProjectBlock)
-                if (j / 3u < room) d[j] = sOut[j];
-        }
-        __syncthreads();
-    }
-}
-
-// slabs packed one after another into the caller's send buffer (gsm_global_project_partition)
-__global__ __launch_bounds__(kProjectBlock) void k_part_pack(
-    const SplatRecord* __restrict__ records, const uint32_t* __restrict__ masks, uint32_t count,
-    SlabTable slabs, const uint32_t* __restrict__ blockSlabOffsets, const uint32_t* __restrict__ sendCounts,
+// The block runs of every slab copied to their destination: one wave per (block, slab) run (waves
+// over runs, workgroups gridDim.x blocks apart), 16-B words, the run's records contiguous at both
+// ends.  The run of block b for slab s starts at blockSlabOffsets[s * nb + b] (k_part_scan) within
+// the slab's records; its length is the next block's offset less its own (the slab total after the
+// last block).
+//  PUSH (the multi-GPU frame, gsm_multigpu.hip): into slab s's owner's receive buffer, after the
+//    records of the ranks before this one (the count matrix: counts[r * world + s], system-coherent
+//    loads; row `rank` is this rank's totals), write-through stores; block 0 leaves the rank's receive
+//    count in *recvCount; every workgroup arrives (arrive.done) after its stores.
+//  !PUSH (gsm_global_project_partition): into the caller's send buffer, slab after slab.
+template <bool PUSH>
+__global__ __launch_bounds__(kProjectBlock) void k_part_copy(
+    const SplatRecord* __restrict__ runs, uint32_t runStride, uint32_t nb, uint32_t numSlabs,
+    const uint32_t* __restrict__ blockSlabOffsets, const uint32_t* __restrict__ totals, uint32_t rank,
+    const uint32_t* __restrict__ counts, SlabPeers peers, uint32_t* __restrict__ recvCount, MgArrive arrive,
     SplatRecord* __restrict__ send, uint64_t capacity) {
-    const uint32_t gid = blockIdx.x * kProjectBlock + threadIdx.x;
-    const uint32_t mask = gid < count ? masks[gid] : 0u;
-    write_slab_runs<false>(
-        records, mask, gid, slabs.n, slabs,
-        [&](uint32_t sl) {
-            uint64_t base = 0;
-            for (uint32_t t = 0; t < sl; ++t) base += sendCounts[t];
-            return send + base + blockSlabOffsets[(size_t)sl * gridDim.x + blockIdx.x];
-        },
-        [&](uint32_t sl) {
-            uint64_t base = 0;
-            for (uint32_t t = 0; t < sl; ++t) base += sendCounts[t];
-            const uint64_t at = base + blockSlabOffsets[(size_t)sl * gridDim.x + blockIdx.x];
-            return at < capacity ? capacity - at : 0ull;
-        });
+    __shared__ uint32_t sBase[kMaxSlabs], sTotal[kMaxSlabs];
+    if (threadIdx.x < numSlabs) {
+        const uint32_t sl = threadIdx.x;
+        uint32_t base = 0;
+        if constexpr (PUSH) {
+            for (uint32_t r = 0; r < rank; ++r) base += ld_sys32(counts + r * numSlabs + sl);
+            sTotal[sl] = ld_sys32(counts + rank * numSlabs + sl);
+        } else {
+            for (uint32_t t = 0; t < sl; ++t) base += totals[t];
+            sTotal[sl] = totals[sl];
+        }
+        sBase[sl] = base;
+    }
+    if constexpr (PUSH) {
+        if (blockIdx.x == 0 && threadIdx.x == 0) {
+            uint32_t mine = 0;
+            for (uint32_t r = 0; r < numSlabs; ++r) mine += ld_sys32(counts + r * numSlabs + rank);
+            *recvCount = min(mine, peers.cap[rank]);
+        }
+    }
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    constexpr uint32_t kWaves = kProjectBlock / 64;
+    const uint32_t runsTotal = nb * numSlabs;
+    for (uint32_t k = blockIdx.x * kWaves + wave; k < runsTotal; k += gridDim.x * kWaves) {
+        const uint32_t b = k / numSlabs, sl = k - b * numSlabs;
+        const uint32_t off = blockSlabOffsets[(size_t)sl * nb + b];
+        const uint32_t end = b + 1u < nb ? blockSlabOffsets[(size_t)sl * nb + b + 1u] : sTotal[sl];
+        const uint32_t n = end - off;
+        if (n == 0) continue;
+        const uint4* src = (const uint4*)(runs + (size_t)sl * runStride + (size_t)b * kProjectBlock);
+        const uint64_t at = (uint64_t)sBase[sl] + off;  // the run's first record at the destination
+        if constexpr (PUSH) {
+            const uint64_t cap = peers.cap[sl];
+            const uint32_t m = at >= cap ? 0u : (uint32_t)min((uint64_t)n, cap - at);  // never past it
+            uint4* d = (uint4*)(peers.recv[sl] + at);
+            for (uint32_t j = lane; j < 3u * m; j += 64u) st_sys128(d, 3u * m * 16u, j, src[j]);
+        } else {
+            const uint32_t m = at >= capacity ? 0u : (uint32_t)min((uint64_t)n, capacity - at);
+            uint4* d = (uint4*)(send + at);
+            for (uint32_t j = lane; j < 3u * m; j += 64u) d[j] = src[j];
+        }
+    }
+    if constexpr (PUSH) {
+        // every workgroup arrives once (barrier 1) after all its waves' record stores
+        if (arrive.done) mg_arrive_block_unit(arrive, blockIdx.x);
+    }
 }
 
 // slab owner: received records -> the renderer's per-gaussian arrays + tile counts for its rows.
@@ -680,13 +672,16 @@ __global__ __launch_bounds__(kProjectBlock) void k_records_in(
             return;
         }
     }
-    const uint32_t blk = blockIdx.x - (P.schedUnits ? 1u : 0u);
-    const uint32_t gid = blk * kProjectBlock + threadIdx.x;
+    uint32_t blk = blockIdx.x - (P.schedUnits ? 1u : 0u);
     const uint32_t n = devCount ? min(*devCount, P.count) : P.count;
-    if (blk * kProjectBlock >= n) return;  // (uniform) nothing here; the scan stops at the count
+    // blocks of 256 records, gridDim (less the schedule block) apart: the grid is capped when the count
+    // lives on the device (launch_records_in), so few blocks find nothing to do
+    const uint32_t stride = gridDim.x - (P.schedUnits ? 1u : 0u);
+    for (; blk * kProjectBlock < n; blk += stride) {  // (uniform)
+    const uint32_t gid = blk * kProjectBlock + threadIdx.x;
     {
         // system-coherent 16-B loads (ld_sys128): on the multi-GPU path the records were stored by the
-        // peers' k_part_push over xGMI; no L1 / L2 line of an earlier frame may answer
+        // peers' k_part_copy over xGMI; no L1 / L2 line of an earlier frame may answer
         const uint32_t words = 3u * (min(n - blk * kProjectBlock, (uint32_t)kProjectBlock));
         const SplatRecord* src = in + (size_t)blk * kProjectBlock;
 #pragma unroll
@@ -742,6 +737,8 @@ __global__ __launch_bounds__(kProjectBlock) void k_records_in(
     }
     uint32_t s = block_reduce_add<kProjectBlock>(ntiles, lds);
     if (threadIdx.x == 0) blockSums[blk] = s;
+    __syncthreads();  // (sIn and lds of the next block)
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -1045,43 +1042,6 @@ __global__ __launch_bounds__(256) void k_tile_starts(const uint32_t* __restrict_
     }
 }
 
-// The multi-GPU frame's direct exchange (gsm_multigpu.hip): every slab's records written straight
-// into the slab owner's receive buffer (peer pointers over xGMI) at the offset the count matrix
-// gives -- counts[r * world + s] = records rank r holds for slab s, so rank r's records of slab s
-// start after those of ranks 0..r-1 (ascending id order at the owner).  Block 0 also leaves the
-// rank's own receive count in *recvCount.
-__global__ __launch_bounds__(kProjectBlock) void k_part_push(
-    const SplatRecord* __restrict__ records, const uint32_t* __restrict__ masks, uint32_t count,
-    uint32_t world, uint32_t rank, const uint32_t* __restrict__ blockSlabOffsets,
-    const uint32_t* __restrict__ counts, SlabPeers peers, uint32_t* __restrict__ recvCount, SlabTable slabs,
-    MgArrive arrive) {
-    __shared__ uint32_t dstOff[kMaxSlabs];
-    const uint32_t gid = blockIdx.x * kProjectBlock + threadIdx.x;
-    // the count matrix was stored by every rank's k_part_scan (system-coherent loads, no cached copy)
-    if (threadIdx.x < world) {
-        uint32_t before = 0;
-        for (uint32_t r = 0; r < rank; ++r) before += ld_sys32(counts + r * world + threadIdx.x);
-        dstOff[threadIdx.x] = before;
-    }
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-        uint32_t mine = 0;
-        for (uint32_t r = 0; r < world; ++r) mine += ld_sys32(counts + r * world + rank);
-        *recvCount = min(mine, peers.cap[rank]);
-    }
-    const uint32_t mask = gid < count ? masks[gid] : 0u;
-    __syncthreads();  // (dstOff)
-    write_slab_runs<true>(
-        records, mask, gid, world, slabs,
-        [&](uint32_t sl) {
-            return peers.recv[sl] + (uint64_t)dstOff[sl] + blockSlabOffsets[(size_t)sl * gridDim.x + blockIdx.x];
-        },
-        [&](uint32_t sl) {  // never past an owner's receive buffer
-            const uint64_t at = (uint64_t)dstOff[sl] + blockSlabOffsets[(size_t)sl * gridDim.x + blockIdx.x];
-            return at < peers.cap[sl] ? (uint64_t)peers.cap[sl] - at : 0ull;
-        });
-    // every workgroup arrives once (barrier 1) after all its waves' record stores
-    if (arrive.done) mg_arrive_block(arrive);
-}
 
 // ---------------------------------------------------------------------------
 // 5. the blend's half-tile lists: per tile, the sorted ids whose skip flag for half h is clear, in
@@ -1191,7 +1151,7 @@ static void launch_project_part_t(uint32_t deg, const void* world, const void* h
     const uint32_t sched = (A && a.schedUnits) ? 1u : 0u;
 #define GSM_LAUNCH_PPART(D)                                                                                 \
     hipLaunchKernelGGL((k_project_part<HALF, D>), dim3(blocks + sched), dim3(kProjectBlock), 0, s, world,   \
-                       harm, a, slabs, B.records, B.masks, B.blockSlabCounts, sincos,                       \
+                       harm, a, slabs, B.runs, B.runStride, B.blockSlabCounts, sincos,                      \
                        sched ? A->unitCost : nullptr, sched ? A->unitOrder : nullptr, sched ? A->costMax : nullptr)
     switch (deg) {
         case 0: GSM_LAUNCH_PPART(0); break;
@@ -1202,6 +1162,7 @@ static void launch_project_part_t(uint32_t deg, const void* world, const void* h
 #undef GSM_LAUNCH_PPART
 }
 
+constexpr uint32_t kCopyMaxBlocks = 2048;  // k_part_copy<false>: workgroups loop over the runs
 void launch_partition(bool halfInput, uint32_t deg, const void* world, const void* harm,
                       const ProjectArgs& a, const SlabTable& slabs, const PartitionBuffers& B,
                       const float2* sincos, void* send, uint64_t capacity, uint32_t* sendCounts,
@@ -1217,8 +1178,9 @@ void launch_partition(bool halfInput, uint32_t deg, const void* world, const voi
     else launch_project_part_t<false>(deg, world, harm, pa, slabs, B, sincos, nullptr, s);
     hipLaunchKernelGGL(k_part_scan, dim3(slabs.n), dim3(1024), 0, s, B.blockSlabCounts, blocks, sendCounts,
                        CountPublish{});
-    hipLaunchKernelGGL(k_part_pack, dim3(blocks), dim3(kProjectBlock), 0, s, B.records, B.masks, a.count, slabs,
-                       B.blockSlabCounts, sendCounts, (SplatRecord*)send, capacity);
+    hipLaunchKernelGGL(k_part_copy<false>, dim3(min(blocks, kCopyMaxBlocks)), dim3(kProjectBlock), 0, s, B.runs,
+                       B.runStride, blocks, slabs.n, B.blockSlabCounts, sendCounts, 0u, nullptr, SlabPeers{},
+                       nullptr, MgArrive{}, (SplatRecord*)send, capacity);
 }
 
 void launch_partition_counts(bool halfInput, uint32_t deg, const void* world, const void* harm, const ProjectArgs& a,
@@ -1237,19 +1199,26 @@ void launch_partition_counts(bool halfInput, uint32_t deg, const void* world, co
 
 void launch_partition_push(const ProjectArgs& a, uint32_t world, uint32_t rank, const PartitionBuffers& B,
                            const uint32_t* counts, const SlabPeers& peers, uint32_t* recvCount, const SlabTable& slabs,
-                           const MgArrive& arrive, hipStream_t s) {
+                           const MgArrive& arrive, hipStream_t s, uint32_t gridCap) {
+    (void)slabs;
     const uint32_t blocks = (a.count + kProjectBlock - 1) / kProjectBlock;
-    // (no ids here: one block still takes the receive count from the matrix and arrives)
+    // (no ids here: one workgroup still takes the receive count from the matrix and arrives)
+    uint32_t grid = blocks ? blocks : 1u;
+    if (gridCap && grid > gridCap) grid = gridCap;
     MgArrive ar = arrive;
-    ar.total = blocks ? blocks : 1u;
-    hipLaunchKernelGGL(k_part_push, dim3(blocks ? blocks : 1u), dim3(kProjectBlock), 0, s, B.records, B.masks, a.count,
-                       world, rank, B.blockSlabCounts, counts, peers, recvCount, slabs, ar);
+    ar.total = grid;
+    hipLaunchKernelGGL(k_part_copy<true>, dim3(grid), dim3(kProjectBlock), 0, s, B.runs, B.runStride, blocks, world,
+                       B.blockSlabCounts, nullptr, rank, counts, peers, recvCount, ar, nullptr, 0ull);
 }
 
+// a grid covering a device-side count: 8 workgroups per CU of a 256-CU device, each looping over the
+// 256-record blocks (a grid for the whole capacity spent most of its workgroups finding nothing)
+constexpr uint32_t kRecordsInMaxBlocks = 2048;
 void launch_records_in(const void* records, const ProjectArgs& a, const DeviceArena& A, hipStream_t s,
                        const uint32_t* devCount) {
-    const uint32_t blocks = (a.count + kProjectBlock - 1) / kProjectBlock;
+    uint32_t blocks = (a.count + kProjectBlock - 1) / kProjectBlock;
     if (blocks == 0 && a.schedUnits == 0) return;  // (an empty frame still orders its blend units)
+    if (devCount && blocks > kRecordsInMaxBlocks) blocks = kRecordsInMaxBlocks;
     hipLaunchKernelGGL(k_records_in, dim3(blocks + (a.schedUnits ? 1u : 0u)), dim3(kProjectBlock), 0, s,
                        (const SplatRecord*)records, a, A.renderData, A.bounds, A.rec, A.tileCounts, A.tileMasks,
                        A.blockSums, A.sincosTable, devCount, A.unitCost, A.unitOrder, A.costMax);

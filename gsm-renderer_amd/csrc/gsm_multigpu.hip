@@ -19,10 +19,11 @@
 //   phase 3  rank 0 waits at barrier 2 for every slab (then copies the frame to the caller's
 //            targets unless the caller renders into the library frame itself).
 //
-// Memory model (gsm_internal.h MgArrive): every store of exchange data is a
-// system-coherent write-through store (sc0 sc1), and the kernels that make them arrive at the barrier
-// themselves -- every storing unit drains its stores, then adds to the rank's arrival counter, and the
-// last unit raises the rank's flag in every rank's control block.  A wait is k_mg_sync: lane p polls
+// Memory model (gsm_internal.h MgArrive): the records and counts are system-coherent
+// write-through stores (sc0 sc1); the gathered pixels are plain stores that the blend's workgroups
+// write back at system scope (their XCD's L2) before arriving.  The kernels that make them arrive at
+// the barrier themselves -- every storing unit drains its stores, then adds to the rank's arrival
+// counter, and the last unit raises the rank's flag in every rank's control block.  A wait is k_mg_sync: lane p polls
 // the flag of rank p (relaxed system-scope loads, bounded by a timeout), then an acquire at system
 // scope; every consumer load of exchange data is system-coherent (ld_sys32 / ld_sys128), and before
 // the caller may read rank 0's gathered frame, kSyncWaitBlocks workgroups acquire so that every XCD's
@@ -241,7 +242,7 @@ class MultiGpu {
     gsm_status check(const gsm_gaussian_input& in, uint32_t width, uint32_t height, void* color, size_t colorPitch,
                      void* depth, size_t depthPitch, void* gatherColor, Targets* t) const;
     uint32_t* ctl() const { return (uint32_t*)mem_; }
-    uint32_t* done(uint32_t barrier) const { return done_ + barrier * 16u; }  // 64 B apart
+    uint32_t* done(uint32_t barrier) const { return done_ + barrier * kArriveWordsPerBarrier; }
     MgArrive arrival(uint32_t barrier) const {
         MgArrive a{};
         for (int p = 0; p < world_; ++p) a.flag[p] = sync_.ctl[p] + kFlagWords + barrier * kMaxSlabs + rank_;
@@ -269,7 +270,7 @@ class MultiGpu {
     uint32_t bpp_ = 8, capacity_ = 0, minCap_ = 0;
     uint32_t* sendCounts_ = nullptr;  // this rank's per-slab counts (k_part_scan)
     uint32_t* recvCount_ = nullptr;   // records this rank receives (k_part_push, block 0)
-    uint32_t* done_ = nullptr;        // arrival counters, one 64-B line per barrier (own device memory)
+    uint32_t* done_ = nullptr;        // arrival counters per barrier: main + shards (own device memory)
     SyncPeers sync_{};
     SlabPeers recs_{};
     char* frame0_ = nullptr;  // rank 0's gathered colour frame (peer mapping on the other ranks)
@@ -331,13 +332,13 @@ gsm_status MultiGpu::prepare(GlobalRenderer* r, int rank, int world, MultiGpu** 
                                                               m->memKind_ == 1u ? hipDeviceMallocUncached
                                                                                 : hipDeviceMallocFinegrained);
     // the partition buffers now, so that no frame can fail on an allocation
-    bool ok = ae == hipSuccess && r->ensurePartitionBuffers() == GSM_OK &&
+    bool ok = ae == hipSuccess && r->ensurePartitionBuffers((uint32_t)world) == GSM_OK &&
               (!getenv("GSM_MG_POISON") || hipMemset(m->mem_, 0xAB, m->memBytes_) == hipSuccess) &&
               hipMemset(m->mem_, 0, kRecordsOff) == hipSuccess &&
               hipMalloc(&m->sendCounts_, kMaxSlabs * 4) == hipSuccess && hipMalloc(&m->recvCount_, 4) == hipSuccess &&
-              hipMalloc(&m->done_, kBarriers * 64) == hipSuccess &&
+              hipMalloc(&m->done_, kBarriers * kArriveWordsPerBarrier * 4) == hipSuccess &&
               hipMemset(m->sendCounts_, 0, kMaxSlabs * 4) == hipSuccess && hipMemset(m->recvCount_, 0, 4) == hipSuccess &&
-              hipMemset(m->done_, 0, kBarriers * 64) == hipSuccess && hipDeviceSynchronize() == hipSuccess;
+              hipMemset(m->done_, 0, kBarriers * kArriveWordsPerBarrier * 4) == hipSuccess && hipDeviceSynchronize() == hipSuccess;
     ExchangeHandle h;
     std::memset(&h, 0, sizeof(h));
     if (ok) ok = hipIpcGetMemHandle(&h.ipc, m->mem_) == hipSuccess;

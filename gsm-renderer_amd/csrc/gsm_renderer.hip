@@ -293,7 +293,7 @@ gsm_status GlobalRenderer::preparePartition(const gsm_gaussian_input& in, const 
         f->slabs.rows[i] = slabRows[i];
     }
     if (hipSetDevice(device_) != hipSuccess) return GSM_ERR_DEVICE_NOT_AVAILABLE;
-    gsm_status st = ensurePartitionBuffers();
+    gsm_status st = ensurePartitionBuffers(numSlabs);
     if (st != GSM_OK) return st;
     f->half = config_.precision == GSM_PRECISION_FLOAT16;
     f->a = frameArgs(camp, width, height, count, in.sh_components);
@@ -309,14 +309,18 @@ gsm_status GlobalRenderer::preparePartition(const gsm_gaussian_input& in, const 
     return GSM_OK;
 }
 
-gsm_status GlobalRenderer::ensurePartitionBuffers() {
-    if (part_.records) return GSM_OK;  // lazily: only ranks of a partitioned frame need these
+gsm_status GlobalRenderer::ensurePartitionBuffers(uint32_t numSlabs) {
+    // lazily: only ranks of a partitioned frame need these (the multi-GPU frame: at prepare)
+    if (part_.runs && part_.runSlabs >= numSlabs) return GSM_OK;
     if (hipSetDevice(device_) != hipSuccess) return GSM_ERR_DEVICE_NOT_AVAILABLE;
     const size_t blocks = ((size_t)maxGaussians_ + kProjectBlock - 1) / kProjectBlock;
-    gsm_status st = alloc((void**)&part_.records, (size_t)maxGaussians_ * sizeof(SplatRecord));
-    if (st == GSM_OK) st = alloc((void**)&part_.masks, (size_t)maxGaussians_ * 4);
-    if (st == GSM_OK) st = alloc((void**)&part_.blockSlabCounts, kMaxSlabs * (blocks + 1) * 4);
-    if (st != GSM_OK) part_ = PartitionBuffers();
+    PartitionBuffers b = part_;
+    b.runStride = (uint32_t)(blocks * kProjectBlock);
+    b.runSlabs = numSlabs;
+    // (a buffer for fewer slabs stays allocated until the renderer is destroyed)
+    gsm_status st = alloc((void**)&b.runs, (size_t)numSlabs * b.runStride * sizeof(SplatRecord));
+    if (st == GSM_OK && !b.blockSlabCounts) st = alloc((void**)&b.blockSlabCounts, kMaxSlabs * (blocks + 1) * 4);
+    if (st == GSM_OK) part_ = b;
     return st;
 }
 
@@ -359,7 +363,8 @@ gsm_status GlobalRenderer::partitionPush(hipStream_t s, uint32_t world, uint32_t
     std::memset(&a, 0, sizeof(a));
     a.count = partCount_;
     if (world != partSlabs_.n) return GSM_ERR_INVALID_ARGUMENT;  // one slab per rank, as partitionCounts split
-    launch_partition_push(a, world, rank, part_, counts, peers, recvCount, partSlabs_, arrive, s);
+    launch_partition_push(a, world, rank, part_, counts, peers, recvCount, partSlabs_, arrive, s,
+                          tuning_.mgPushPerCU > 0 ? (uint32_t)(tuning_.mgPushPerCU * numCUs_) : 0u);
     if (hipGetLastError() != hipSuccess) return GSM_ERR_RENDER_FAILED;
     return GSM_OK;
 }
@@ -470,7 +475,8 @@ gsm_status GlobalRenderer::runFrame(hipStream_t s, const ProjectArgs& a, uint32_
     // the schedule from the walks the previous frame's blend recorded (same stream: no join)
     if (prof || blendOnly) hipEventRecord(ev[5], s);
     launch_blend(g, arena_, color, colorPitch, depth, depthPitch, numCUs_, costOrder,
-                 (int)config_.color_format, s, tuning_.blendWaves, tuning_.blendClaim, blendArrive);
+                 (int)config_.color_format, s, tuning_.blendWaves, tuning_.blendClaim, blendArrive,
+                 tuning_.mgPixelsWB);
     if (prof || blendOnly) hipEventRecord(ev[6], s);
     if (prof || blendOnly) profFrames_++;
     haveTimes_ = profFrames_ > 0;

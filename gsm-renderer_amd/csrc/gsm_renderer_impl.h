@@ -51,7 +51,7 @@ class GlobalRenderer {
                              const void* color, size_t colorPitch, const void* depth, size_t depthPitch) const;
     // the partition buffers (allocated lazily by the first partition frame; the multi-GPU frame
     // allocates them at prepare so that no frame can fail on an allocation)
-    gsm_status ensurePartitionBuffers();
+    gsm_status ensurePartitionBuffers(uint32_t numSlabs);
     uint32_t maxGaussians() const { return maxGaussians_; }
     uint32_t tilesY() const { return tilesY_; }
     uint32_t maxWidth() const { return maxWidth_; }

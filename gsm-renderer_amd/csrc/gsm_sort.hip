@@ -1345,6 +1345,10 @@ Tuning tuning_from_env(int device) {
     t.blendClaim = !cv ? 1 : std::strcmp(cv, "early") == 0 ? 0 : std::strcmp(cv, "auto") == 0 ? 2 : 1;
     const char* ws = getenv("GSM_SORT_WIDE");
     t.wideSort = !(ws && ws[0] == '0');
+    const char* mp = getenv("GSM_MG_PIXELS");
+    t.mgPixelsWB = !(mp && std::strcmp(mp, "wt") == 0);
+    const char* mpg = getenv("GSM_MG_PUSH_GRID");
+    t.mgPushPerCU = mpg ? atoi(mpg) : 4;
     const char* w12 = getenv("GSM_SORT_WIDE12");
     t.wide12 = w12 && w12[0] == '1';
     return t;

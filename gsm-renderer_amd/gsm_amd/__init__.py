@@ -692,21 +692,25 @@ class MultiGpuRenderer:
 
     def render(self, color_texture, depth_texture, input: GaussianInput, camera: CameraParams, width: int,
                height: int, gather: bool = True, stream=None, color_pitch: Optional[int] = None,
-               depth_pitch: Optional[int] = None, gather_target=None, gather_depth: bool = False):
+               depth_pitch: Optional[int] = None, gather_target=None, gather_depth: Optional[bool] = None):
         """One frame.  gather: rank 0 receives the whole frame -- in color_texture (a copy of the
         library frame), or, with gather_target = self.frame()[0], in the library frame itself; the
         other ranks' color_texture is then unused (may be None).  gather_depth (with gather): rank 0
         also receives the r16f depth -- in depth_texture (a copy) or, when depth_texture is None, in
-        the library depth frame (self.frame_depth())."""
+        the library depth frame (self.frame_depth()); default: whether depth_texture is given (every
+        rank must make the same choice: pass it explicitly when only rank 0 holds a depth texture)."""
         self.render_phases(range(4), color_texture, depth_texture, input, camera, width, height, gather, stream,
                            color_pitch, depth_pitch, gather_target, gather_depth)
 
     def render_phases(self, phases, color_texture, depth_texture, input: GaussianInput, camera: CameraParams,
                       width: int, height: int, gather: bool = True, stream=None, color_pitch: Optional[int] = None,
-                      depth_pitch: Optional[int] = None, gather_target=None, gather_depth: bool = False):
+                      depth_pitch: Optional[int] = None, gather_target=None, gather_depth: Optional[bool] = None):
         """gsm_multigpu_render_phase for each phase in `phases` (virtual ranks: phase p of every rank
         before phase p + 1 of any, include/gsm_multigpu.h).  Every phase is issued even after one
-        returned an error (the ranks stay in step); the first error is raised after the last."""
+        returned an error (the ranks stay in step); the first error is raised after the last.
+        gather_depth as render's."""
+        if gather_depth is None:
+            gather_depth = depth_texture is not None
         inp, cam, cp, dp = self._args(input, camera, color_texture, depth_texture, width, color_pitch, depth_pitch)
         col = _ptr(color_texture)
         dep = _ptr(depth_texture)

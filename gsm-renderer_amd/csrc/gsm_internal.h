@@ -48,7 +48,7 @@ static_assert(sizeof(SplatRecord) == 48, "SplatRecord must be 48 B");
 // the receive buffer of every slab owner (peer device pointers; the multi-GPU exchange)
 struct SlabPeers {
     SplatRecord* recv[kMaxSlabs];
-    uint32_t cap[kMaxSlabs];  // records each receive buffer holds (k_part_push writes no further)
+    uint32_t cap[kMaxSlabs];  // records each receive buffer holds (k_part_copy writes no further)
 };
 struct PartitionBuffers {
     SplatRecord* runs = nullptr;        // [slabs][runStride]: the projection's block runs, block b of

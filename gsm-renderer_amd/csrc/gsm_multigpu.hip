@@ -9,7 +9,7 @@
 //            (GlobalRenderer::partitionCounts: k_project_part, k_part_scan); k_part_scan's workgroup
 //            for slab s stores its total into column s of row `rank` of every rank's count matrix and
 //            arrives at barrier 0;
-//   phase 1  wait at barrier 0; k_part_push: every record goes straight from the projection into
+//   phase 1  wait at barrier 0; k_part_copy: every block run of the projection (staged per slab) goes into
 //            its slab owner's receive buffer, at the offset the count matrix gives -- rank order, so
 //            the receiver's records are in ascending id order (the stable sort's tie order); its
 //            workgroups arrive at barrier 1;
@@ -269,7 +269,7 @@ class MultiGpu {
     size_t memBytes_ = 0, frameOff_ = 0, framePitch_ = 0, depthOff_ = 0, depthPitch0_ = 0;
     uint32_t bpp_ = 8, capacity_ = 0, minCap_ = 0;
     uint32_t* sendCounts_ = nullptr;  // this rank's per-slab counts (k_part_scan)
-    uint32_t* recvCount_ = nullptr;   // records this rank receives (k_part_push, block 0)
+    uint32_t* recvCount_ = nullptr;   // records this rank receives (k_part_copy, block 0)
     uint32_t* done_ = nullptr;        // arrival counters per barrier: main + shards (own device memory)
     SyncPeers sync_{};
     SlabPeers recs_{};

@@ -3,7 +3,7 @@
 Two to four rank processes share GPU 0 (tests/mg_worker.py): each owns a fine-grained exchange
 allocation, the handles go over torch.distributed (gloo) and every rank opens its peers' allocations
 with hipIpcOpenMemHandle -- the set-up the 8-GPU node runs, where the mappings cross xGMI.  Per frame
-every record is stored by k_part_push straight into another process's receive buffer, the count
+every record is stored by k_part_copy straight into another process's receive buffer, the count
 matrix rows and the barrier flags cross the processes, the slab blends write their pixels into rank
 0's gathered frame, and rank 0's stream waits for every slab.  The frames must equal the oracle's bit
 for bit, with no barrier timeout.  (RCCL cannot run two ranks on one GPU -- "Duplicate GPU detected",

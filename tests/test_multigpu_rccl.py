@@ -72,7 +72,7 @@ def test_native_exchange_virtual_ranks(gsm, cuda, oracle, world, n, w, h, prec):
     """The device steps of gsm_multigpu_render for world > 1 without RCCL (include/gsm_debug.h): W
     renderers on one GPU play the ranks -- each projects its id range and counts its records per slab
     (k_project_part), the count matrix is stacked on the device (the all-gather), every rank's
-    k_part_push writes its records straight into every slab owner's receive buffer at the matrix's
+    k_part_copy writes its records straight into every slab owner's receive buffer at the matrix's
     offsets, and each owner renders its rows from the count read on the device.  Ids and slab rows
     are split as gsm_multigpu.hip splits them.  The composed frame equals the oracle bit for bit:
     the push offsets, the receive counts and the rank-ordered ties of world > 1 (the world-1 RCCL

@@ -902,6 +902,7 @@ __global__ __launch_bounds__(kProjectBlock) void k_scatter(
     __shared__ uint32_t sOff[kProjectBlock];
     __shared__ uint32_t sMask[kProjectBlock];  // 0: no cooperative slots (large rect or no tiles)
     __shared__ uint32_t sRect[kProjectBlock];  // x0 | rw << 16 (rw <= 32)
+    __shared__ uint32_t sInv[kProjectBlock];   // ceil(2^16 / rw): bit / rw = (bit * inv) >> 16 for bit < 32
     __shared__ int sTy0[kProjectBlock];        // first row index of the rect in the renderer's rows
     __shared__ uint32_t sD[kProjectBlock];     // depth bits of the key
     __shared__ float2 sBand[kProjectBlock];    // skip-flag band of each gaussian: mean x, half width (< 0: none)
@@ -938,6 +939,10 @@ __global__ __launch_bounds__(kProjectBlock) void k_scatter(
         large = (ty1 - ty0 + 1) * rw > kMaskTiles;
         if (!large) mask = masks[gid];
         sRect[threadIdx.x] = ((uint32_t)(int)r.x & 0xFFFFu) | ((uint32_t)rw << 16);
+        // 2^16 / rw is a power of two (v_rcp_f32 exact) or >= 1/rw >= 1/32 away from an integer, and the
+        // 1-ulp reciprocal moves it by <= 2^16 * 2^-23 < 0.008: the ceiling is exact.  With inv = ceil(2^16
+        // / rw), (bit * inv) >> 16 = bit / rw for every bit < 32 and rw <= 32 (checked exhaustively)
+        sInv[threadIdx.x] = (uint32_t)__builtin_ceilf(65536.0f * __builtin_amdgcn_rcpf((float)rw));
     }
     sOff[threadIdx.x] = off;
     sMask[threadIdx.x] = mask;
@@ -980,7 +985,8 @@ __global__ __launch_bounds__(kProjectBlock) void k_scatter(
         if (wp >= P.maxAssignments) continue;
         const uint32_t rect = sRect[lo];
         const uint32_t rwo = rect >> 16;
-        const int k = sTy0[lo] + (int)(bit / rwo), tx = (int)(rect & 0xFFFFu) + (int)(bit % rwo);
+        const uint32_t row = (bit * sInv[lo]) >> 16;  // bit / rwo (bit < 32)
+        const int k = sTy0[lo] + (int)row, tx = (int)(rect & 0xFFFFu) + (int)(bit - row * rwo);
         keys[wp] = ((uint32_t)(k * (int)P.bin.tilesX + tx) << 16) | sD[lo];
         const float2 bd = sBand[lo];
         vals[wp] = (blockIdx.x * kProjectBlock + lo) | (half_skip_flags(bd.x, bd.y, tx) << kHalfSkipShift);

@@ -81,13 +81,13 @@ constexpr uint32_t kBarriers = 3;
 constexpr size_t kFlagWords = 0;      // u32 flag[kBarriers][kMaxSlabs]: [b][src] = last frame src reached b
 constexpr size_t kStatusWord = 64;    // u32 [0] barrier timeouts, [1] failed peer arrivals, [2] epoch of the last timeout
 constexpr size_t kCountsWord = 256;   // u32 counts[2][kMaxSlabs * kMaxSlabs] (frame parity; row = source)
-constexpr size_t kRecordsOff = 4096;  // SplatRecord[capacity]
+constexpr size_t kRecordsOff = 4096;  // SplatRecord[2][capacity] (frame parity)
 static_assert(kFlagWords + kBarriers * kMaxSlabs <= kStatusWord, "flags before the status word");
 constexpr uint32_t kFailBit = 0x80000000u;  // a flag's epoch with this bit: that rank's frame failed
 constexpr uint32_t kEpochMask = 0x7FFFFFFFu;
 constexpr uint32_t kSyncWaitBlocks = 32;    // workgroups of a wait: >= 4 per XCD (blocks are dealt round robin)
 constexpr uint32_t kHandleMagic = 0x58534D47u;  // "GMSX"
-constexpr uint32_t kHandleVersion = 2;
+constexpr uint32_t kHandleVersion = 3;
 
 struct ExchangeFields {
     uint32_t magic, version;
@@ -101,6 +101,7 @@ struct ExchangeFields {
     uint64_t depthOff;  // rank 0: the gathered r16f depth frame; 0 elsewhere
     uint32_t interleave;  // slab rows interleaved (GSM_MG_ROWS=interleaved): every rank must agree
     uint32_t memKind;     // exchange memory kind (0 fine-grained, 2 device)
+    uint32_t pipelined;   // GSM_MG_PIPELINE=1 (rank 0 holds two gathered frames): every rank must agree
     char busId[32];
     hipIpcMemHandle_t ipc;
 };
@@ -114,6 +115,8 @@ struct SyncPeers {
 };
 
 size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
+// bytes of one frame parity of a receive buffer of `capacity` records
+size_t recv_parity_bytes(uint32_t capacity) { return align_up((size_t)capacity * sizeof(SplatRecord), 4096); }
 }  // namespace
 
 // A barrier step outside the producing kernels:
@@ -195,12 +198,12 @@ class MultiGpu {
                      uint32_t height, void* color, size_t colorPitch, void* depth, size_t depthPitch,
                      void* gatherColor);
     gsm_status frame(void** color, size_t* pitch) const {
-        *color = rank_ == 0 ? frame0_ : nullptr;
+        *color = rank_ == 0 ? frameBuf(frame_) : nullptr;
         *pitch = rank_ == 0 ? framePitch_ : 0;
         return GSM_OK;
     }
     gsm_status frameDepth(void** depth, size_t* pitch) const {
-        *depth = rank_ == 0 ? depth0_ : nullptr;
+        *depth = rank_ == 0 ? depthBuf(frame_) : nullptr;
         *pitch = rank_ == 0 ? depthPitch0_ : 0;
         return GSM_OK;
     }
@@ -218,7 +221,7 @@ class MultiGpu {
                    : GSM_ERR_RENDER_FAILED;
     }
     gsm_status copyFrame(void* dst, size_t pitch, uint32_t width, uint32_t height, bool depth) {
-        const char* src = depth ? depth0_ : frame0_;
+        const char* src = depth ? depthBuf(frame_) : frameBuf(frame_);
         const size_t bpp = depth ? 2u : bpp_;
         if (rank_ != 0 || !src || !dst || width > r_->maxWidth() || height > r_->maxHeight() || pitch < (size_t)width * bpp)
             return GSM_ERR_INVALID_ARGUMENT;
@@ -242,6 +245,12 @@ class MultiGpu {
     gsm_status check(const gsm_gaussian_input& in, uint32_t width, uint32_t height, void* color, size_t colorPitch,
                      void* depth, size_t depthPitch, void* gatherColor, Targets* t) const;
     uint32_t* ctl() const { return (uint32_t*)mem_; }
+    // rank 0's gathered frames of frame f: one pair, or (pipelined) two alternating by frame parity
+    char* frameBuf(uint32_t f) const { return frame0_ ? frame0_ + (pipelined_ ? (f & 1u) * frameStride_ : 0) : nullptr; }
+    char* depthBuf(uint32_t f) const { return depth0_ ? depth0_ + (pipelined_ ? (f & 1u) * depthStride_ : 0) : nullptr; }
+    bool libraryFrame(const void* p) const {
+        return p && (p == frame0_ || p == depth0_ || (pipelined_ && (p == frame0_ + frameStride_ || p == depth0_ + depthStride_)));
+    }
     uint32_t* done(uint32_t barrier) const { return done_ + barrier * kArriveWordsPerBarrier; }
     MgArrive arrival(uint32_t barrier) const {
         MgArrive a{};
@@ -267,9 +276,10 @@ class MultiGpu {
     int rank_ = 0, world_ = 1, device_ = 0;
     char* mem_ = nullptr;  // this rank's exchange allocation (fine-grained)
     size_t memBytes_ = 0, frameOff_ = 0, framePitch_ = 0, depthOff_ = 0, depthPitch0_ = 0;
+    size_t frameStride_ = 0, depthStride_ = 0;  // rank 0: bytes of one gathered colour / depth frame
     uint32_t bpp_ = 8, capacity_ = 0, minCap_ = 0;
     uint32_t* sendCounts_ = nullptr;  // this rank's per-slab counts (k_part_scan)
-    uint32_t* recvCount_ = nullptr;   // records this rank receives (k_part_copy, block 0)
+    uint32_t* recvCount_ = nullptr;   // [2] records this rank receives, by frame parity (k_part_copy, block 0)
     uint32_t* done_ = nullptr;        // arrival counters per barrier: main + shards (own device memory)
     SyncPeers sync_{};
     SlabPeers recs_{};
@@ -280,6 +290,14 @@ class MultiGpu {
     int nextPhase_ = 0;        // phases run in order 0..3
     gsm_status frameErr_ = GSM_OK;  // this rank's error of the current frame (barrier-only phases after it)
     bool interleave_ = false;  // slab rows interleaved (GSM_MG_ROWS=interleaved at prepare)
+    // Pipelined (GSM_MG_PIPELINE=1 at prepare, every rank alike): phases 0-1 on the library's own stream
+    // (front_), phases 2-3 on the caller's, joined by events -- frame f + 1's projection and push run
+    // beside frame f's slab render.  front_ starts frame f only after the caller's stream finished frame
+    // f - 2 (evEnd_[f & 1]): the receive buffer, receive count, blend schedule and rank 0's gathered
+    // frames of parity f & 1 are then free.
+    bool pipelined_ = false;
+    hipStream_t front_ = nullptr;
+    hipEvent_t evFront_[2] = {nullptr, nullptr}, evEnd_[2] = {nullptr, nullptr};
     uint32_t memKind_ = 0;
     uint32_t wallKHz_ = 100000;
     unsigned long long timeoutTicks_ = 0;
@@ -292,6 +310,11 @@ void MultiGpu::release() {
     opened_.clear();
     for (void* p : {(void*)mem_, (void*)sendCounts_, (void*)recvCount_, (void*)done_})
         if (p) hipFree(p);
+    for (hipEvent_t& e : evFront_)
+        if (e) hipEventDestroy(e), e = nullptr;
+    for (hipEvent_t& e : evEnd_)
+        if (e) hipEventDestroy(e), e = nullptr;
+    if (front_) hipStreamDestroy(front_), front_ = nullptr;
     mem_ = nullptr;
     sendCounts_ = recvCount_ = done_ = nullptr;
 }
@@ -321,12 +344,20 @@ gsm_status MultiGpu::prepare(GlobalRenderer* r, int rank, int world, MultiGpu** 
     m->timeoutTicks_ = 10000ull * m->wallKHz_;
     const char* rv = getenv("GSM_MG_ROWS");  // every rank must agree: checked at connect (the handle)
     m->interleave_ = rv && std::strcmp(rv, "interleaved") == 0;
-    const size_t recBytes = (size_t)m->capacity_ * sizeof(SplatRecord);
+    const char* pv = getenv("GSM_MG_PIPELINE");  // every rank must agree: checked at connect (the handle)
+    m->pipelined_ = pv && pv[0] == '1';
+    // two frame parities of the receive buffer (a source pushes frame f + 2 into the parity of frame f
+    // only after its barrier 0 of frame f + 2, which needs this rank's arrival there -- made after this
+    // rank finished reading frame f's records: in stream order, or, pipelined, after evEnd_)
+    const size_t recBytes = 2 * recv_parity_bytes(m->capacity_);
     m->framePitch_ = align_up((size_t)r->maxWidth() * m->bpp_, 16);
     m->depthPitch0_ = align_up((size_t)r->maxWidth() * 2u, 16);
+    m->frameStride_ = align_up(m->framePitch_ * r->maxHeight(), 4096);
+    m->depthStride_ = align_up(m->depthPitch0_ * r->maxHeight(), 4096);
+    const size_t nFrames = m->pipelined_ ? 2 : 1;
     m->frameOff_ = rank == 0 ? align_up(kRecordsOff + recBytes, 4096) : 0;
-    m->depthOff_ = rank == 0 ? align_up(m->frameOff_ + m->framePitch_ * r->maxHeight(), 4096) : 0;
-    m->memBytes_ = rank == 0 ? m->depthOff_ + m->depthPitch0_ * r->maxHeight() : kRecordsOff + recBytes;
+    m->depthOff_ = rank == 0 ? m->frameOff_ + nFrames * m->frameStride_ : 0;
+    m->memBytes_ = rank == 0 ? m->depthOff_ + nFrames * m->depthStride_ : kRecordsOff + recBytes;
     hipError_t ae = m->memKind_ == 2u ? hipMalloc((void**)&m->mem_, m->memBytes_)
                                       : hipExtMallocWithFlags((void**)&m->mem_, m->memBytes_,
                                                               m->memKind_ == 1u ? hipDeviceMallocUncached
@@ -335,10 +366,16 @@ gsm_status MultiGpu::prepare(GlobalRenderer* r, int rank, int world, MultiGpu** 
     bool ok = ae == hipSuccess && r->ensurePartitionBuffers((uint32_t)world) == GSM_OK &&
               (!getenv("GSM_MG_POISON") || hipMemset(m->mem_, 0xAB, m->memBytes_) == hipSuccess) &&
               hipMemset(m->mem_, 0, kRecordsOff) == hipSuccess &&
-              hipMalloc(&m->sendCounts_, kMaxSlabs * 4) == hipSuccess && hipMalloc(&m->recvCount_, 4) == hipSuccess &&
+              hipMalloc(&m->sendCounts_, kMaxSlabs * 4) == hipSuccess && hipMalloc(&m->recvCount_, 8) == hipSuccess &&
               hipMalloc(&m->done_, kBarriers * kArriveWordsPerBarrier * 4) == hipSuccess &&
-              hipMemset(m->sendCounts_, 0, kMaxSlabs * 4) == hipSuccess && hipMemset(m->recvCount_, 0, 4) == hipSuccess &&
+              hipMemset(m->sendCounts_, 0, kMaxSlabs * 4) == hipSuccess && hipMemset(m->recvCount_, 0, 8) == hipSuccess &&
               hipMemset(m->done_, 0, kBarriers * kArriveWordsPerBarrier * 4) == hipSuccess && hipDeviceSynchronize() == hipSuccess;
+    if (ok && m->pipelined_)
+        ok = hipStreamCreateWithFlags(&m->front_, hipStreamNonBlocking) == hipSuccess &&
+             hipEventCreateWithFlags(&m->evFront_[0], hipEventDisableTiming) == hipSuccess &&
+             hipEventCreateWithFlags(&m->evFront_[1], hipEventDisableTiming) == hipSuccess &&
+             hipEventCreateWithFlags(&m->evEnd_[0], hipEventDisableTiming) == hipSuccess &&
+             hipEventCreateWithFlags(&m->evEnd_[1], hipEventDisableTiming) == hipSuccess;
     ExchangeHandle h;
     std::memset(&h, 0, sizeof(h));
     if (ok) ok = hipIpcGetMemHandle(&h.ipc, m->mem_) == hipSuccess;
@@ -364,6 +401,7 @@ gsm_status MultiGpu::prepare(GlobalRenderer* r, int rank, int world, MultiGpu** 
     h.depthOff = m->depthOff_;
     h.interleave = m->interleave_ ? 1u : 0u;
     h.memKind = m->memKind_;
+    h.pipelined = m->pipelined_ ? 1u : 0u;
     std::memcpy(handle, &h, sizeof(h));
     *out = m;
     return GSM_OK;
@@ -382,7 +420,7 @@ gsm_status MultiGpu::connect(const void* all) {
         // GSM_MG_ROWS would send records with the wrong slab masks: refused here)
         if (h.magic != kHandleMagic || h.version != kHandleVersion || h.rank != p || h.world != world_ ||
             h.maxWidth != r_->maxWidth() || h.maxHeight != r_->maxHeight() || h.bytesPerPixel != bpp_ ||
-            h.interleave != (interleave_ ? 1u : 0u))
+            h.interleave != (interleave_ ? 1u : 0u) || h.pipelined != (pipelined_ ? 1u : 0u))
             return GSM_ERR_INVALID_ARGUMENT;
         if (p == 0 && (h.frameOff == 0 || h.depthOff == 0)) return GSM_ERR_INVALID_ARGUMENT;
         if (h.capacity < minCap) minCap = h.capacity;
@@ -443,6 +481,9 @@ gsm_status MultiGpu::check(const gsm_gaussian_input& in, uint32_t width, uint32_
         t->depth = t->gatherDepth ? (void*)depth0_ : nullptr;
         t->depthPitch = depthPitch0_;
         if (rank_ == 0) {  // the copies of phase 3 into the caller's targets
+            // pipelined: the library frames alternate and a peer may be writing the other one
+            if (pipelined_ && (libraryFrame(gatherColor) || (t->gatherDepth && libraryFrame(depth))))
+                return GSM_ERR_INVALID_ARGUMENT;
             if (gatherColor != frame0_ && colorPitch < (size_t)width * bpp_) return GSM_ERR_INVALID_BUFFER_SIZE;
             if (t->gatherDepth && depth != depth0_ && (depthPitch < (size_t)width * 2u || (depthPitch & 1u) ||
                                                        (((uintptr_t)depth) & 1u)))
@@ -477,6 +518,20 @@ gsm_status MultiGpu::phase(int p, hipStream_t s, const gsm_gaussian_input& in, c
     }
     nextPhase_ = (p + 1) & 3;
     const uint32_t world = (uint32_t)world_, rank = (uint32_t)rank_;
+    const uint32_t par = frame_ & 1u;  // the frame's parity: count matrix, receive buffer, schedule set
+    if (t.gather) {  // rank 0's gathered frames of this frame (two alternating ones when pipelined)
+        t.color = frameBuf(frame_);
+        t.depth = t.gatherDepth ? (void*)depthBuf(frame_) : nullptr;
+    }
+    // pipelined: phases 0-1 on front_ after the caller's stream finished frame f - 2, phases 2-3 on the
+    // caller's stream after this frame's phase 1
+    const hipStream_t cs = s;
+    if (pipelined_ && p <= 1) s = front_;
+    if (pipelined_ && p == 0) hipStreamWaitEvent(front_, evEnd_[par], 0);
+    if (pipelined_ && p == 2) hipStreamWaitEvent(cs, evFront_[par], 0);
+    SlabPeers recv = recs_;  // this frame's parity of every owner's receive buffer
+    for (uint32_t q = 0; q < world; ++q)
+        recv.recv[q] = (SplatRecord*)((char*)recs_.recv[q] + par * recv_parity_bytes(recs_.cap[q]));
     // slabs: contiguous blocks of ceil(tilesY / world) tile rows (default: each record travels to the
     // fewest ranks -- interleaving sends a gaussian to every rank one of its rect rows maps to, +71 %
     // records at 1080p / W = 8, device frame +3.5-5 % on the benchmark's uniform cloud), or interleaved
@@ -509,6 +564,7 @@ gsm_status MultiGpu::phase(int p, hipStream_t s, const gsm_gaussian_input& in, c
                 // the slab's blend units are ordered inside this launch (the long kernel of the frame's
                 // first half), not in the short records-in launch of phase 2
                 if (mine && (st = setRows()) != GSM_OK) frameErr_ = st;
+                r_->selectSchedule(par);
                 if (frameErr_ == GSM_OK &&
                     (st = r_->partitionCounts(s, in, cam, width, height, first, cnt, rows, world, sendCounts_, mine,
                                               interleave_, &pub)) != GSM_OK)
@@ -521,10 +577,11 @@ gsm_status MultiGpu::phase(int p, hipStream_t s, const gsm_gaussian_input& in, c
             wait(s, 0);  // every rank's counts are in my matrix
             if (frameErr_ == GSM_OK) {
                 const uint32_t* counts = ctl() + kCountsWord + (frame_ & 1u) * kMaxSlabs * kMaxSlabs;
-                if ((st = r_->partitionPush(s, world, rank, counts, recs_, recvCount_, arrival(1))) != GSM_OK)
+                if ((st = r_->partitionPush(s, world, rank, counts, recv, recvCount_ + par, arrival(1))) != GSM_OK)
                     frameErr_ = st;
             }
             if (frameErr_ != GSM_OK) arrive(s, 1, false, true);
+            if (pipelined_) hipEventRecord(evFront_[par], front_);
             break;
         }
         case 2: {
@@ -534,9 +591,10 @@ gsm_status MultiGpu::phase(int p, hipStream_t s, const gsm_gaussian_input& in, c
             if (frameErr_ == GSM_OK && mine) {
                 if ((st = setRows()) == GSM_OK) {
                     const MgArrive ba = arrival(2);
-                    st = r_->renderRecords(s, mem_ + kRecordsOff, capacity_, width, height, t.color, t.colorPitch,
-                                           t.depth, t.depthPitch, recvCount_, /*preOrdered=*/true,
-                                           signal ? &ba : nullptr);
+                    r_->selectSchedule(par);
+                    st = r_->renderRecords(s, mem_ + kRecordsOff + par * recv_parity_bytes(capacity_), capacity_, width,
+                                           height, t.color, t.colorPitch, t.depth, t.depthPitch, recvCount_ + par,
+                                           /*preOrdered=*/true, signal ? &ba : nullptr);
                     arrived = signal && st == GSM_OK;  // the blend's waves arrive
                 }
                 if (st != GSM_OK) frameErr_ = st;
@@ -549,20 +607,21 @@ gsm_status MultiGpu::phase(int p, hipStream_t s, const gsm_gaussian_input& in, c
                 if (world > 1) wait(s, 2);  // every band is in my frame
                 if (frameErr_ == GSM_OK) {
                     const uint32_t gy = height;
-                    if (gatherColor != frame0_) {
+                    if (gatherColor != t.color) {
                         const uint32_t rowBytes = width * bpp_;
                         hipLaunchKernelGGL(k_mg_copy2d, dim3((rowBytes / 4u + 255u) / 256u, gy), dim3(256), 0, s,
-                                           (uint8_t*)gatherColor, colorPitch, (const uint8_t*)frame0_, framePitch_,
+                                           (uint8_t*)gatherColor, colorPitch, (const uint8_t*)t.color, framePitch_,
                                            rowBytes, gy);
                     }
-                    if (t.gatherDepth && depth != depth0_) {
+                    if (t.gatherDepth && depth != t.depth) {
                         const uint32_t rowBytes = width * 2u;
                         hipLaunchKernelGGL(k_mg_copy2d, dim3((rowBytes / 4u + 255u) / 256u, gy), dim3(256), 0, s,
-                                           (uint8_t*)depth, depthPitch, (const uint8_t*)depth0_, depthPitch0_, rowBytes,
+                                           (uint8_t*)depth, depthPitch, (const uint8_t*)t.depth, depthPitch0_, rowBytes,
                                            gy);
                     }
                 }
             }
+            if (pipelined_) hipEventRecord(evEnd_[par], s);
             break;
         }
     }

@@ -130,6 +130,7 @@ gsm_status GlobalRenderer::create(const gsm_renderer_config& cfg, int hipDevice,
         delete r;
         return st;
     }
+    r->sched_[0] = {A.unitCost, A.unitOrder, A.costMax};
     // numeric-contract tables (gsm_detmath.h)
     std::vector<uint16_t> expt(65536);
     for (uint32_t i = 0; i < 65536; ++i) expt[i] = blend_exp_table_entry((uint16_t)i);
@@ -321,7 +322,25 @@ gsm_status GlobalRenderer::ensurePartitionBuffers(uint32_t numSlabs) {
     gsm_status st = alloc((void**)&b.runs, (size_t)numSlabs * b.runStride * sizeof(SplatRecord));
     if (st == GSM_OK && !b.blockSlabCounts) st = alloc((void**)&b.blockSlabCounts, kMaxSlabs * (blocks + 1) * 4);
     if (st == GSM_OK) part_ = b;
+    if (st == GSM_OK && !sched_[1].unitOrder) {
+        ScheduleSet t;
+        st = alloc((void**)&t.unitCost, (size_t)tileCount_ * 4 * sizeof(uint16_t));
+        if (st == GSM_OK) st = alloc((void**)&t.unitOrder, (size_t)tileCount_ * 4 * sizeof(uint32_t));
+        if (st == GSM_OK) st = alloc((void**)&t.costMax, kCostMaxSlots * sizeof(uint32_t));
+        if (st == GSM_OK && (hipMemset(t.unitCost, 0, (size_t)tileCount_ * 4 * sizeof(uint16_t)) != hipSuccess ||
+                             hipMemset(t.costMax, 0, kCostMaxSlots * sizeof(uint32_t)) != hipSuccess ||
+                             hipDeviceSynchronize() != hipSuccess))
+            st = GSM_ERR_FAILED_TO_ALLOCATE_BUFFER;
+        if (st == GSM_OK) sched_[1] = t;
+    }
     return st;
+}
+
+void GlobalRenderer::selectSchedule(uint32_t parity) {
+    const ScheduleSet& t = sched_[(parity & 1u) && sched_[1].unitOrder ? 1 : 0];
+    arena_.unitCost = t.unitCost;
+    arena_.unitOrder = t.unitOrder;
+    arena_.costMax = t.costMax;
 }
 
 gsm_status GlobalRenderer::projectPartition(hipStream_t s, const gsm_gaussian_input& in,
@@ -374,9 +393,12 @@ uint32_t GlobalRenderer::scheduleUnits(hipStream_t s, uint32_t width, uint32_t h
     const uint32_t units = rowCount() * tilesX_ * upt;
     const uint64_t key = ((uint64_t)upt << 60) ^ ((uint64_t)width << 40) ^ ((uint64_t)height << 20) ^
                          ((uint64_t)rowStride_ << 30) ^ ((uint64_t)rowBegin_ << 10) ^ rowEnd_;
-    if (key != schedKey_) {  // new geometry: no walks to order by yet
-        hipMemsetAsync(arena_.unitCost, 0, (size_t)units * sizeof(uint16_t), s);
-        hipMemsetAsync(arena_.costMax, 0, kCostMaxSlots * sizeof(uint32_t), s);
+    if (key != schedKey_) {  // new geometry: no walks to order by yet (either schedule set)
+        for (const ScheduleSet& t : sched_) {
+            if (!t.unitCost) continue;
+            hipMemsetAsync(t.unitCost, 0, (size_t)units * sizeof(uint16_t), s);
+            hipMemsetAsync(t.costMax, 0, kCostMaxSlots * sizeof(uint32_t), s);
+        }
         schedKey_ = key;
     }
     return tuning_.costOrder ? units : 0u;

@@ -52,6 +52,12 @@ class GlobalRenderer {
     // the partition buffers (allocated lazily by the first partition frame; the multi-GPU frame
     // allocates them at prepare so that no frame can fail on an allocation)
     gsm_status ensurePartitionBuffers(uint32_t numSlabs);
+    // The multi-GPU frame's two sets of blend-schedule buffers (unit costs, order, longest walk):
+    // frame f uses set f & 1 in its projection (ordering) and in its blend, so with frame f + 1's
+    // projection running beside frame f's blend (gsm_multigpu pipelined) neither reads what the other
+    // writes; the ordering then follows the walks of frame f - 2.  Set 1 is allocated by
+    // ensurePartitionBuffers.
+    void selectSchedule(uint32_t parity);
     uint32_t maxGaussians() const { return maxGaussians_; }
     uint32_t tilesY() const { return tilesY_; }
     uint32_t maxWidth() const { return maxWidth_; }
@@ -88,7 +94,12 @@ class GlobalRenderer {
     uint32_t scheduleUnits(hipStream_t s, uint32_t width, uint32_t height);
     PartitionBuffers part_;
     uint32_t partCount_ = 0;  // ids of the last partitionCounts
-    SlabTable partSlabs_{};   // its slab table (partitionPush cuts each record's tile answers by it)
+    SlabTable partSlabs_{};
+    struct ScheduleSet {
+        uint16_t* unitCost = nullptr;
+        uint32_t* unitOrder = nullptr;
+        uint32_t* costMax = nullptr;
+    } sched_[2];   // its slab table (partitionPush cuts each record's tile answers by it)
     struct PartitionFrame {
         ProjectArgs a;
         SlabTable slabs;

@@ -74,6 +74,12 @@ gsm_status gsm_global_render_records(gsm_renderer *renderer, void *stream, const
  *                          connect across processes) is the A/B of DESIGN.md 7;
  *                          GSM_MG_MEM=uncached returns GSM_ERR_UNSUPPORTED: uncached memory
  *                          renders wrong slabs on MI355X;
+ *                          GSM_MG_PIPELINE=1 (every rank alike, checked at connect): phases 0-1 of a
+ *                          frame run on a stream of the library's own and phases 2-3 on the caller's,
+ *                          joined by events, so frame f + 1's projection and record push run beside
+ *                          frame f's slab render (rank 0 then holds two gathered frames that alternate,
+ *                          and a gather target must be the caller's own memory: the library frames
+ *                          are refused with GSM_ERR_INVALID_ARGUMENT);
  *   (caller)               all-gathers the handles: all[r * GSM_MULTIGPU_HANDLE_BYTES] = rank r's;
  *   gsm_multigpu_connect   opens every peer's exchange memory (hipIpcOpenMemHandle; a handle
  *                          from the same process is used directly) and checks that the ranks
@@ -133,7 +139,8 @@ gsm_status gsm_multigpu_render(gsm_multigpu *multigpu, void *stream, const gsm_g
 
 /* Rank 0's gathered frame (library memory, valid until destroy): *color = its device pointer,
  * *pitch_bytes = max_width x bytes per pixel of the configured colour format.  Passing it as
- * gather_color skips the copy.  Other ranks: *color = NULL. */
+ * gather_color skips the copy.  Other ranks: *color = NULL.  Pipelined (GSM_MG_PIPELINE=1): the
+ * frame of the last frame issued (two alternate); not a valid gather target. */
 gsm_status gsm_multigpu_frame(gsm_multigpu *multigpu, void **color, size_t *pitch_bytes);
 /* Rank 0's gathered r16f depth frame (library memory): *depth = its device pointer, *pitch_bytes its
  * row pitch.  Passing it as depth_r16f skips the copy.  Other ranks: *depth = NULL. */

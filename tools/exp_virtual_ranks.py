@@ -33,6 +33,9 @@ def main():
     ap.add_argument("--trace-rank", type=int, default=-1,
                     help="per-unit blend trace of this rank's slab (profiling bit 2) -> gpurun_out/vr_trace_*.npz")
     ap.add_argument("--depth", type=int, default=1, help="gather the r16f depth frame too (product default)")
+    ap.add_argument("--interval", type=int, default=0,
+                    help="also time N frames issued back to back (no events between phases): the group's frame "
+                         "interval; run with GSM_MG_PIPELINE=1 in the environment for the pipelined frame")
     a = ap.parse_args()
     import torch
     import gsm_amd as gsm
@@ -69,7 +72,10 @@ def main():
                 marks.append((p, k, e0, e1))
         return marks
 
-    for f in range(a.frames + 2):
+    piped = os.environ.get("GSM_MG_PIPELINE") == "1"
+    if piped:  # phases 0-1 run on the ranks' own streams: per-phase events on the caller's stream see none
+        a.frames, a.stages, a.trace_rank = 0, 0, -1
+    for f in range(a.frames + 2 if a.frames else 0):
         marks = frame(True)
         torch.cuda.synchronize()
         if f >= 2:
@@ -111,6 +117,33 @@ def main():
                  "max_walk": int(walk.max()), "mean_walk": round(float(walk.mean()), 1),
                  "occupancy_deciles": [int(((st <= x) & (en > x)).sum()) for x in grid],
                  "first_start_spread_us": round(float(np.sort(st)[min(len(st) - 1, 3000)]), 1)}
+    interval = None
+    if a.interval:
+        # every phase of every rank of N frames, one caller stream, rank 0 gathering into caller tensors
+        # (pipelined ranks refuse the library frames as targets); one event pair around all N frames
+        cbuf = torch.empty((h, w, 4), dtype=torch.float16, device=dev)
+        dbuf = torch.empty((h, w), dtype=torch.float16, device=dev)
+        cams = [gsm.CameraParams.from_dict(scenes.orbit_camera(w, h, 0.25 * i)) for i in range(a.interval + 3)]
+
+        def issue(cm):
+            for p in range(4):
+                for k, m in enumerate(mgs):
+                    m.render_phases([p], cbuf if k == 0 else None, dbuf if k == 0 else None, inp, cm, w, h,
+                                    gather=True, gather_depth=bool(a.depth), stream=stream)
+        for cm in cams[:3]:
+            issue(cm)
+        torch.cuda.synchronize()
+        e0, e1 = ev(), ev()
+        e0.record(stream)
+        for cm in cams[3:]:
+            issue(cm)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        g = e0.elapsed_time(e1) / a.interval
+        interval = {"frames": a.interval, "pipelined": os.environ.get("GSM_MG_PIPELINE") == "1",
+                    "group_interval_ms": round(g, 4), "per_rank_interval_ms": round(g / W, 4),
+                    "note": "W virtual ranks share one GPU: the group's frame interval / W models one rank's "
+                            "interval on its own GPU (moving camera, 0.25 deg per frame)"}
     one_gpu = None
     if a.single:  # the same frame on one renderer with the whole frame's rows (bench.py's 1-GPU path)
         one = gsm.GlobalRenderer(device=0, config=cfg)
@@ -121,13 +154,14 @@ def main():
         torch.cuda.synchronize()
         e0, e1 = ev(), ev()
         e0.record(stream)
-        for _ in range(a.frames * 4):
+        reps = max(a.frames, 5) * 4
+        for _ in range(reps):
             one.render(color, depth, inp, cam, w, h, stream=stream)
         e1.record(stream)
         torch.cuda.synchronize()
-        one_gpu = e0.elapsed_time(e1) / (a.frames * 4)
+        one_gpu = e0.elapsed_time(e1) / reps
         one.close()
-    med = np.median(ph, axis=0)  # [phase][rank]
+    med = np.median(ph, axis=0) if ph.shape[0] else np.zeros((4, W))  # [phase][rank]
     # xGMI model (not a measurement: the virtual ranks' pushes and pixels stay in one GPU's HBM).
     # counts[r][s] = records rank r sends to slab s; every cross-rank record is 48 B (SplatRecord)
     # over the (r, s) link; rank 0 receives every other band's pixels (rgba16f + r16f = 10 B) over
@@ -158,10 +192,10 @@ def main():
            "phase_ms": {f"phase{p}": [round(float(x), 4) for x in med[p]] for p in range(4)},
            "max_phase_ms": [round(float(med[p].max()), 4) for p in range(4)],
            "device_frame_ms": round(float(sum(med[p].max() for p in range(4))), 4),
-           "slab_stages_ms": stages, "blend_trace": trace,
+           "slab_stages_ms": stages, "blend_trace": trace, "interval": interval,
            "xgmi_model": xgmi,
            "one_gpu_frame_ms": round(one_gpu, 4) if one_gpu else None,
-           "device_speedup": round(one_gpu / float(sum(med[p].max() for p in range(4))), 3) if one_gpu else None,
+           "device_speedup": round(one_gpu / float(sum(med[p].max() for p in range(4))), 3) if one_gpu and not piped else None,
            "note": "virtual ranks on one GPU, product kernels, one stream; no xGMI (pushes and pixels stay local)"}
     print(json.dumps(out))
     for m in mgs:

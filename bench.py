@@ -152,21 +152,32 @@ def virtual_ranks_entry(world: int):
     this process's GPU state stays as it is).  None when the child fails."""
     import subprocess
     cmd = [sys.executable, os.path.join(ROOT, "tools", "exp_virtual_ranks.py"), "--config", "cfg3_5m_sh3_4k_f16",
-           "--world", str(world), "--frames", "5", "--stages", "0", "--single", "1"]
+           "--world", str(world), "--frames", "5", "--stages", "0", "--single", "1", "--interval", "20"]
     try:
         p = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
         d = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
     except Exception as e:  # noqa: BLE001 -- reported, never fatal for the bench line
         return {"error": f"{type(e).__name__}: {str(e)[:200]}"}
+    # the pipelined frame (GSM_MG_PIPELINE=1): frames issued back to back, phases 0-1 of frame f + 1
+    # beside phases 2-3 of frame f; only the frame interval is meaningful there
+    pipe = None
+    try:
+        pp = subprocess.run(cmd[:4] + ["--world", str(world), "--interval", "20"], capture_output=True, text=True,
+                            timeout=300, env=dict(os.environ, GSM_MG_PIPELINE="1"))
+        pipe = json.loads([ln for ln in pp.stdout.splitlines() if ln.startswith("{")][-1]).get("interval")
+    except Exception as e:  # noqa: BLE001
+        pipe = {"error": f"{type(e).__name__}: {str(e)[:200]}"}
     return {"workload": "cfg3_5m_sh3_4k_f16 frame (BASELINE configs[3]) over %d virtual ranks" % world,
             "world": world, "device_frame_ms": d["device_frame_ms"], "max_phase_ms": d["max_phase_ms"],
+            "interval_serial": d.get("interval"), "interval_pipelined": pipe,
             "one_gpu_frame_ms": d.get("one_gpu_frame_ms"), "device_speedup": d.get("device_speedup"),
             "barrier_timeouts": d.get("timeouts"), "xgmi_model": d.get("xgmi_model"),
             "modelled_speedup_with_xgmi": (round(d["one_gpu_frame_ms"] / d["xgmi_model"]["modelled_frame_ms"], 3)
                                            if d.get("one_gpu_frame_ms") and d.get("xgmi_model") else None),
             "note": "each rank's phases run alone on this GPU (an upper bound for a rank's own GPU); the pushes "
                     "and the gathered pixels stay local (no xGMI time); device_speedup = one-renderer frame / "
-                    "per-rank device frame"}
+                    "per-rank device frame (one-frame latency); interval_*: the group's frame interval / world "
+                    "for frames issued back to back under a moving camera, serial and pipelined (GSM_MG_PIPELINE=1)"}
 
 
 def main():

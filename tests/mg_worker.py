@@ -12,7 +12,9 @@ Frames (same scene every rank, generated from the seed):
   D  rank 1 passes a width over the maximum: it alone refuses the frame, but still performs every
      barrier step (arrivals marked failed); the others finish it
   E  the frame of A again on every rank: bit-exact, the ranks still in step after D
-Rank 0 writes A, B and E, and every rank its band of C, as .npy files into --out, plus status.json."""
+With --pipelined 1 (GSM_MG_PIPELINE=1) instead: P0-P3, three views issued back to back without host
+synchronisation, each gathered with depth into its own caller tensors on rank 0.
+Rank 0 writes A, B and E (or P0-P3), and every rank its band of C, as .npy files into --out, plus status.json."""
 import argparse
 import json
 import os
@@ -37,7 +39,12 @@ def main():
     p.add_argument("--precision", type=int, default=1)
     p.add_argument("--seed", type=int, default=11)
     p.add_argument("--cap", type=int, default=0, help="max_gaussians of this rank (0: n)")
+    p.add_argument("--pipelined", type=int, default=0,
+                   help="GSM_MG_PIPELINE=1: only frames P0-P3 (three views, issued back to back, gathered with "
+                        "depth into caller tensors on rank 0)")
     a = p.parse_args()
+    if a.pipelined:
+        os.environ["GSM_MG_PIPELINE"] = "1"  # read at gsm_multigpu_prepare
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(a.port)
     import torch
@@ -68,6 +75,20 @@ def main():
                 result["refused"] = False
             except gsm_amd.RendererError as e:
                 result["refused"] = e.status == gsm_amd.Status.INVALID_GAUSSIAN_COUNT
+            return
+        if a.pipelined:
+            cams = [cam_d, scenes.orbit_camera(w, h, 3.0), scenes.orbit_camera(w, h, 6.0), cam_d]
+            cols = [torch.full((h, w, 4), float("nan"), dtype=torch.float16, device=dev) for _ in cams]
+            deps = [torch.full((h, w), float("nan"), dtype=torch.float16, device=dev) for _ in cams]
+            for i, cm in enumerate(cams):  # no host synchronisation between the frames
+                mg.render(cols[i] if a.rank == 0 else None, deps[i] if a.rank == 0 else None, inp,
+                          gsm_amd.CameraParams.from_dict(cm), w, h, gather=True, stream=stream, gather_depth=True)
+            torch.cuda.synchronize()
+            if a.rank == 0:
+                for i in range(len(cams)):
+                    np.save(os.path.join(a.out, f"frame_p{i}.npy"), cols[i].view(torch.int16).cpu().numpy().view(np.uint16))
+                    np.save(os.path.join(a.out, f"depth_p{i}.npy"), deps[i].view(torch.int16).cpu().numpy().view(np.uint16))
+            result["timeouts"] = mg.status()
             return
         frame_ptr, _ = mg.frame()
         # A: into the library frames (zero copy), colour and depth

@@ -66,7 +66,8 @@ gsm_status gsm_global_render_records(gsm_renderer *renderer, void *stream, const
  * max_width / max_height).  Set-up is collective and happens once, in two steps around an
  * exchange the caller performs with any transport (torch.distributed, MPI, sockets, ...):
  *   gsm_multigpu_prepare   allocates this rank's exchange memory (fine-grained device memory:
- *                          control words, 2 x W x W counts, max_gaussians x 48-B records,
+ *                          control words, 2 x W x W counts, 2 x max_gaussians x 48-B records
+ *                          (frame parity),
  *                          and on rank 0 the gathered colour frame and r16f depth frame,
  *                          max_width x max_height pixels each) and the renderer's partition
  *                          buffers, and writes its GSM_MULTIGPU_HANDLE_BYTES handle into `handle`.
@@ -165,7 +166,8 @@ gsm_status gsm_multigpu_debug_copy_depth(gsm_multigpu *multigpu, void *host_dst,
                                          uint32_t width, uint32_t height);
 
 /* The first `bytes` of this rank's exchange allocation (control words from byte 0, the count matrix
- * from byte 1024, the received records from byte 4096), synchronous. */
+ * from byte 1024, the received records of even frames from byte 4096, of odd frames after them at the
+ * next 4096-byte boundary), synchronous. */
 gsm_status gsm_multigpu_debug_copy_exchange(gsm_multigpu *multigpu, void *host_dst, size_t bytes);
 
 /* The last frame's world x world record counts (row = source rank, column = slab), synchronous. */

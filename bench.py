@@ -112,6 +112,9 @@ def parse():
                    help="N=1: also run BASELINE config 4's frame (5M/SH3/4K) split over this many virtual "
                         "ranks on the one GPU (tools/exp_virtual_ranks.py, a child process): per-rank device "
                         "frame and its speedup over the same frame on one renderer; 0 = off")
+    p.add_argument("--mg-pipeline", type=int, default=0,
+                   help="N > 1: the pipelined multi-GPU frame (GSM_MG_PIPELINE=1: a frame's projection and push "
+                        "beside the previous frame's slab render; rank 0 gathers into its own tensors)")
     p.add_argument("--multi", choices=("alltoall", "replicas"), default="alltoall",
                    help="N>1 partition: all-to-all of projected records (8e) or projection replicas")
     p.add_argument("--multi-extra-config", default="cfg3_5m_sh3_4k_f16",
@@ -257,11 +260,17 @@ def main():
     # handles travel once, at set-up, over torch.distributed with any backend).
     native_multi = alltoall
     multi_fallback = None
+    if native_multi and args.mg_pipeline:
+        os.environ["GSM_MG_PIPELINE"] = "1"  # read by gsm_multigpu_prepare on every rank
+    gtargets = (None, None)
     if native_multi:
         mg = None
         try:  # exchange handles over torch.distributed (any backend); the frame needs no collective
             mg = gsm_amd.MultiGpuRenderer.connect(renderer, rank, world_size, gsm_amd.MultiGpuRenderer.torch_allgather)
             frame_ptr = mg.frame()[0]  # rank 0: the gathered frame (library memory, zero copy)
+            if args.mg_pipeline and rank == 0:  # pipelined: the library frames alternate, gather into ours
+                gtargets = (torch.empty((H, W, 4), dtype=torch.float16, device=dev),
+                            torch.empty((H, W), dtype=torch.float16, device=dev))
         except gsm_amd.RendererError as e:  # e.g. exchange memory that cannot be opened on this node
             multi_fallback = f"rank {rank}: {e}"
         # create is collective: every rank takes the native frame or none does
@@ -293,8 +302,11 @@ def main():
         elif native_multi:
             # colour and depth gathered into rank 0's library frames (the reference writes depth with
             # every frame, GlobalRenderer.swift:350; the one-GPU step renders both too)
-            mg.render(None, None, inp, cam, W, H, gather=True, stream=stream,
-                      gather_target=frame_ptr if rank == 0 else None, gather_depth=True)
+            if gtargets[0] is not None:
+                mg.render(gtargets[0], gtargets[1], inp, cam, W, H, gather=True, stream=stream, gather_depth=True)
+            else:
+                mg.render(None, None, inp, cam, W, H, gather=True, stream=stream,
+                          gather_target=frame_ptr if rank == 0 else None, gather_depth=True)
             return
         elif alltoall:
             renderer.project_partition(inp, cam, W, H, first, cnt, rows, send, send_cap, send_counts,
@@ -549,6 +561,7 @@ def main():
         out["multi_fallback"] = multi_fallback
     if barrier_timeouts is not None:
         out["barrier_timeouts"] = barrier_timeouts
+        out["mg_pipelined"] = bool(args.mg_pipeline)
         out["failed_peer_arrivals"] = failed_arrivals
     if multi_4k:
         out["config4"] = multi_4k
@@ -591,8 +604,15 @@ def multi_extra_frame(args, gsm_amd, scenes, dev, gpu, rank, world_size, backend
     inp = gsm_amd.GaussianInput(world, harm, n, sh)
     cam = gsm_amd.CameraParams.from_dict(cam_d)
     stream = torch.cuda.current_stream(dev)
+    gcol = gdep = None
+    if args.mg_pipeline and rank == 0:  # pipelined: rank 0 gathers into its own tensors
+        gcol = torch.empty((H, W, 4), dtype=torch.float16, device=dev)
+        gdep = torch.empty((H, W), dtype=torch.float16, device=dev)
 
     def step():
+        if gcol is not None:
+            mg.render(gcol, gdep, inp, cam, W, H, gather=True, stream=stream, gather_depth=True)
+            return
         mg.render(None, None, inp, cam, W, H, gather=True, stream=stream, gather_target=frame_ptr if rank == 0 else None,
                   gather_depth=True)
     for _ in range(3):

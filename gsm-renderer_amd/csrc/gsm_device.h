@@ -23,6 +23,36 @@ __device__ __forceinline__ float clampf(float v, float lo, float hi) {
 }
 
 // ---------------------------------------------------------------------------
+// Correctly rounded a[k] / b for K numerators over one divisor -- bit for bit the IEEE a[k] / b of the
+// oracle -- at one division's cost: y = RN(1 / b), then per numerator q = RN(a y), r = RN(a - b q) (exact
+// by the fma), q' = RN(q + r y): Markstein's correction, correctly rounded when y is the correctly
+// rounded reciprocal and r does not underflow (Muller et al., Handbook of Floating-Point Arithmetic,
+// division via fma).  r = 0 keeps q (so a = -0 gives -0).  A wave holding a numerator below 2^-96
+// (nonzero: r could underflow) or a divisor outside [2^-100, 2^100] takes the divisions themselves.
+// Checked on 9e8 random and fp16-valued pairs against IEEE division (tools/exp/markstein_div.c,
+// tests/test_markstein_div.py).  b > 0 (norms).
+template <int K>
+__device__ __forceinline__ void div_many(float (&a)[K], float b) {
+    bool slow = !(b >= 0x1p-100f && b <= 0x1p100f);
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const uint32_t x = __float_as_uint(a[k]) & 0x7FFFFFFFu;
+        slow = slow || (x - 1u) < (31u << 23) - 1u;
+    }
+    if (__ballot(slow) != 0ull) {  // (rare; wave-uniform)
+#pragma unroll
+        for (int k = 0; k < K; ++k) a[k] = a[k] / b;
+        return;
+    }
+    const float y = 1.0f / b;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const float q = a[k] * y;
+        const float r = __builtin_fmaf(-q, b, a[k]);
+        a[k] = r == 0.0f ? q : __builtin_fmaf(r, y, q);
+    }
+}
+
 // small column-major matrix helpers (simd / Metal layout)
 // ---------------------------------------------------------------------------
 struct M3 {
@@ -177,7 +207,9 @@ __device__ __forceinline__ void sh_color(const void* __restrict__ harm, uint32_t
     float dd = d0 * d0 + d1 * d1;
     dd = dd + d2 * d2;
     float n = __builtin_sqrtf(dd);
-    float x = d0 / n, y = d1 / n, z = d2 / n;
+    float dn3[3] = {d0, d1, d2};
+    div_many(dn3, n);  // d / n, each correctly rounded
+    float x = dn3[0], y = dn3[1], z = dn3[2];
     float xx = x * x, yy = y * y, zz = z * z;
     float xy = x * y, yz = y * z, xz = x * z;
     float b[16];
@@ -265,7 +297,7 @@ __device__ __forceinline__ M3 build_cov3d(const float scale[3], const float rot[
         if (nrm < 1e-8f) {
             q[0] = 1.0f; q[1] = 0.0f; q[2] = 0.0f; q[3] = 0.0f;
         } else {
-            q[0] = q[0] / nrm; q[1] = q[1] / nrm; q[2] = q[2] / nrm; q[3] = q[3] / nrm;
+            div_many(q, nrm);  // q / nrm, each correctly rounded
         }
     }
     float x = q[0], y = q[1], z = q[2], r = q[3];
@@ -351,8 +383,10 @@ __device__ __forceinline__ Cov2 stabilize_cov2d(Cov2 cov, float maxEig) {
     if (__builtin_fabsf(b) > 1e-8f) {
         float vx = b, vy = l1 - a;
         float dn = __builtin_fmaxf(__builtin_sqrtf(vx * vx + vy * vy), 1e-8f);
-        v1x = vx / dn;
-        v1y = vy / dn;
+        float v2[2] = {vx, vy};
+        div_many(v2, dn);
+        v1x = v2[0];
+        v1y = v2[1];
     } else if (a >= d) {
         v1x = 1.0f; v1y = 0.0f;
     } else {
@@ -384,8 +418,10 @@ __device__ __forceinline__ bool theta_sigmas(const Cov2& cov, float* theta, floa
     if (__builtin_fabsf(b) > 1e-8f) {
         float tx = b, ty = l1 - a;
         float nn = __builtin_sqrtf(tx * tx + ty * ty);
-        v1x = tx / nn;
-        v1y = ty / nn;
+        float v2[2] = {tx, ty};
+        div_many(v2, nn);
+        v1x = v2[0];
+        v1y = v2[1];
     } else if (a >= d) {
         v1x = 1.0f; v1y = 0.0f;
     } else {
@@ -415,8 +451,10 @@ __device__ __forceinline__ void obb_extents(const Cov2& cov, float* ex, float* e
     if (__builtin_fabsf(b) > 1e-6f) {
         float vx = b, vy = l1 - a;
         float dn = __builtin_fmaxf(__builtin_sqrtf(vx * vx + vy * vy), 1e-6f);
-        v1x = vx / dn;
-        v1y = vy / dn;
+        float v2[2] = {vx, vy};
+        div_many(v2, dn);
+        v1x = v2[0];
+        v1y = v2[1];
     } else if (a >= d) {
         v1x = 1.0f; v1y = 0.0f;
     } else {

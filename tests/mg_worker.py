@@ -13,8 +13,9 @@ Frames (same scene every rank, generated from the seed):
      barrier step (arrivals marked failed); the others finish it
   E  the frame of A again on every rank: bit-exact, the ranks still in step after D
 With --pipelined 1 (GSM_MG_PIPELINE=1) instead: P0-P3, three views issued back to back without host
-synchronisation, each gathered with depth into its own caller tensors on rank 0.
-Rank 0 writes A, B and E (or P0-P3), and every rank its band of C, as .npy files into --out, plus status.json."""
+synchronisation, each gathered with depth into its own caller tensors on rank 0; then PD (rank 1
+alone refuses, as D) and PE (the view of P0) issued back to back after them.
+Rank 0 writes A, B and E (or P0-P3 and PE), and every rank its band of C, as .npy files into --out, plus status.json."""
 import argparse
 import json
 import os
@@ -89,6 +90,22 @@ def main():
                     np.save(os.path.join(a.out, f"frame_p{i}.npy"), cols[i].view(torch.int16).cpu().numpy().view(np.uint16))
                     np.save(os.path.join(a.out, f"depth_p{i}.npy"), deps[i].view(torch.int16).cpu().numpy().view(np.uint16))
             result["timeouts"] = mg.status()
+            if a.world > 1:
+                # D (rank 1 refuses: width over the maximum) then E (the first view again), pipelined and
+                # back to back: the ranks stay in step, E is bit-exact
+                for i, wd in enumerate((w + (1 if a.rank == 1 else 0), w)):
+                    try:
+                        mg.render(cols[i] if a.rank == 0 else None, deps[i] if a.rank == 0 else None, inp,
+                                  gsm_amd.CameraParams.from_dict(cam_d), wd, h, gather=True, stream=stream,
+                                  gather_depth=True)
+                        result[f"pd{i}_status"] = 0
+                    except gsm_amd.RendererError as e:
+                        result[f"pd{i}_status"] = int(e.status)
+                torch.cuda.synchronize()
+                if a.rank == 0:
+                    np.save(os.path.join(a.out, "frame_pe.npy"), cols[1].view(torch.int16).cpu().numpy().view(np.uint16))
+                    np.save(os.path.join(a.out, "depth_pe.npy"), deps[1].view(torch.int16).cpu().numpy().view(np.uint16))
+                result["timeouts_de"], result["failed_peer_arrivals"] = mg.errors()
             return
         frame_ptr, _ = mg.frame()
         # A: into the library frames (zero copy), colour and depth

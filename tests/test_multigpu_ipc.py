@@ -99,7 +99,9 @@ def test_processes_on_one_gpu_render_the_oracle_frame(oracle, tmp_path, monkeypa
 def test_processes_pipelined(oracle, tmp_path, monkeypatch, world, rows):
     """GSM_MG_PIPELINE=1 across rank processes (IPC-mapped exchange memory): four frames over three
     views issued back to back, each rank's projection and push of frame f + 1 on its own stream beside
-    its slab render of frame f -- every gathered frame (colour and depth) bit-exact with the oracle."""
+    its slab render of frame f -- every gathered frame (colour and depth) bit-exact with the oracle;
+    then a frame that rank 1 alone refuses and the next one, back to back: the ranks stay in step and
+    the next frame is bit-exact (pipelined)."""
     from gsm_amd import scenes
     monkeypatch.setenv("GSM_MG_ROWS", rows)
     n, w, h, sh, prec = 40_000, 640, 360, 16, 1
@@ -111,6 +113,13 @@ def test_processes_pipelined(oracle, tmp_path, monkeypatch, world, rows):
         ref = oracle.render(world_np, harm_np, sh, cam, w, h, max_gaussians=n)
         assert np.array_equal(np.load(os.path.join(tmp_path, f"frame_p{i}.npy")), ref["color"]), f"frame {i}"
         assert np.array_equal(np.load(os.path.join(tmp_path, f"depth_p{i}.npy")), ref["depth"]), f"depth {i}"
+    # then D (rank 1 alone refuses) and E (the first view), pipelined back to back: E bit-exact
+    assert st[1]["pd0_status"] == 7 and all(s["pd0_status"] == 0 for k, s in enumerate(st) if k != 1)
+    assert all(s["pd1_status"] == 0 and s["timeouts_de"] == 0 for s in st)
+    assert st[0]["failed_peer_arrivals"] >= 1
+    ref = oracle.render(world_np, harm_np, sh, cams[0], w, h, max_gaussians=n)
+    assert np.array_equal(np.load(os.path.join(tmp_path, "frame_pe.npy")), ref["color"])
+    assert np.array_equal(np.load(os.path.join(tmp_path, "depth_pe.npy")), ref["depth"])
 
 
 def test_processes_refuse_a_frame_over_the_smallest_capacity(tmp_path):

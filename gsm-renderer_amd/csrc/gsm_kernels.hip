@@ -466,7 +466,12 @@ __device__ __forceinline__ uint32_t slab_tile_mask(short4 b, uint32_t full, cons
     const int rw = (int)b.y - (int)b.x + 1;
     if (((int)b.w - (int)b.z + 1) * rw > kMaskTiles) return 0u;
     int k0, k1;
-    rows_within(R, (int)b.z, (int)b.w, &k0, &k1);
+    if (R.s == 1) {  // contiguous slab (wave-uniform): rows_within without its divisions
+        k0 = max((int)b.z, R.b) - R.b;
+        k1 = min((int)b.w, R.e - 1) - R.b;
+    } else {
+        rows_within(R, (int)b.z, (int)b.w, &k0, &k1);
+    }
     if (k1 < k0) return 0u;
     const uint32_t rowBits = rw >= 32 ? 0xFFFFFFFFu : ((1u << rw) - 1u);
     uint32_t out = 0, at = 0;
@@ -492,18 +497,33 @@ __global__ __launch_bounds__(kProjectBlock) void k_project_part(
     }
     const uint32_t blk = blockIdx.x - (P.schedUnits ? 1u : 0u);
     __shared__ uint32_t wcnt[kProjectBlock / 64][kMaxSlabs];
+    __shared__ uint64_t wbal[kProjectBlock / 64][kMaxSlabs];  // the wave's ballot of each slab
     __shared__ uint16_t div255[256];
     __shared__ TileTestLds L;
     __shared__ uint32_t sTile[kProjectBlock];  // answers of candidates < 32
     __shared__ uint32_t sSlab[kProjectBlock];  // slabs with a hit
     __shared__ uint32_t sRows[kMaxSlabs + 1];
+    // the slab of tile row ty < kRowTab (0xFF: none), so a hit costs one LDS byte instead of a search
+    // over the slab bounds (contiguous) or a division (interleaved)
+    constexpr uint32_t kRowTab = 512;
+    __shared__ uint8_t sRowSlab[kRowTab];
     fill_div255(div255);
     const uint32_t tid = threadIdx.x;
     const uint32_t gid = blk * kProjectBlock + tid;
     const uint32_t lane = tid & 63, wave = tid >> 6;
-    if (tid <= slabs.n) sRows[tid] = slabs.rows[tid];
+    const uint32_t nSlabs = slabs.n;
+    if (tid <= nSlabs) sRows[tid] = slabs.rows[tid];
     sTile[tid] = 0;
     sSlab[tid] = 0;
+    auto slabOf = [&](uint32_t ty) -> uint32_t {  // (reads sRows)
+        if (ty >= sRows[nSlabs]) return 0xFFu;
+        if (slabs.interleave) return ty % nSlabs;
+        uint32_t sl = 0;  // slabs.rows is non-decreasing, at most 16 slabs
+        while (sl + 1u < nSlabs && ty >= sRows[sl + 1u]) ++sl;
+        return ty >= sRows[sl] ? sl : 0xFFu;
+    };
+    __syncthreads();
+    for (uint32_t r = tid; r < kRowTab; r += kProjectBlock) sRowSlab[r] = (uint8_t)slabOf(r);
     ProjOut o;
     o.vis = false;
     o.countable = false;
@@ -514,22 +534,19 @@ __global__ __launch_bounds__(kProjectBlock) void k_project_part(
         if (o.vis && o.countable)
             area = (uint32_t)(((int)o.bounds.w - (int)o.bounds.z + 1) * ((int)o.bounds.y - (int)o.bounds.x + 1));
     }
-    const uint32_t nSlabs = slabs.n;
     block_tile_tests(L, o, area, (int)o.bounds.z, [&](uint32_t lo, uint32_t k, int ty) {
         if (k < (uint32_t)kMaskTiles) atomicOr(&sTile[lo], 1u << k);
-        uint32_t sl = 0;  // the slab of row ty: row ty mod n (interleaved), or the block holding it
-        if (slabs.interleave) {
-            sl = (uint32_t)ty % nSlabs;
-            if ((uint32_t)ty < sRows[nSlabs]) atomicOr(&sSlab[lo], 1u << sl);
-        } else {  // slabs.rows is non-decreasing, at most 16 slabs
-            while (sl + 1u < nSlabs && (uint32_t)ty >= sRows[sl + 1u]) ++sl;
-            if ((uint32_t)ty >= sRows[sl] && (uint32_t)ty < sRows[sl + 1u]) atomicOr(&sSlab[lo], 1u << sl);
-        }
+        // the slab of row ty: row ty mod n (interleaved), or the block holding it
+        const uint32_t sl = (uint32_t)ty < kRowTab ? (uint32_t)sRowSlab[ty] : slabOf((uint32_t)ty);
+        if (sl != 0xFFu) atomicOr(&sSlab[lo], 1u << sl);
     });
     const uint32_t mask = gid < P.count ? sSlab[tid] : 0u;  // (only visible gaussians meet a tile)
     for (uint32_t sl = 0; sl < nSlabs; ++sl) {
-        const uint32_t c = (uint32_t)__popcll(__ballot((mask >> sl) & 1u));
-        if (lane == 0) wcnt[wave][sl] = c;
+        const uint64_t b = __ballot((mask >> sl) & 1u);
+        if (lane == 0) {
+            wcnt[wave][sl] = (uint32_t)__popcll(b);
+            wbal[wave][sl] = b;
+        }
     }
     __syncthreads();
     const uint32_t nb = gridDim.x - (P.schedUnits ? 1u : 0u);
@@ -543,19 +560,19 @@ __global__ __launch_bounds__(kProjectBlock) void k_project_part(
     // order within a wave, wave order within the block), stored from the threads (assembling the runs
     // in LDS first measured slower: 60.8 against 56.3 us at config 4 / W = 8); the record's last word
     // is the slab's part of the rect's tile answers (slab_tile_mask)
+    // each lane walks only its own slabs (one or two for most gaussians; a wave-uniform loop over all
+    // slabs ran the store body once per slab any lane of the wave had -- every slab, for scattered ids)
     const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     const uint2 bw = __builtin_bit_cast(uint2, o.bounds);
     const uint32_t tileBits = sTile[tid];
-    for (uint32_t sl = 0; sl < nSlabs; ++sl) {
-        const uint64_t b = __ballot((mask >> sl) & 1u);
-        if ((mask >> sl) & 1u) {
-            uint32_t at = (uint32_t)__popcll(b & lt);
-            for (uint32_t w = 0; w < wave; ++w) at += wcnt[w][sl];
-            uint4* d = (uint4*)(runs + (size_t)sl * runStride + (size_t)blk * kProjectBlock + at);
-            d[0] = o.rd;
-            d[1] = make_uint4(o.ra.x, o.ra.y, o.ra.z, o.ra.w);
-            d[2] = make_uint4(bw.x, bw.y, o.rb, slab_tile_mask(o.bounds, tileBits, slab_rows(slabs, sRows, sl)));
-        }
+    for (uint32_t m = mask; m != 0u; m &= m - 1u) {
+        const uint32_t sl = (uint32_t)__builtin_ctz(m);
+        uint32_t at = (uint32_t)__popcll(wbal[wave][sl] & lt);
+        for (uint32_t w = 0; w < wave; ++w) at += wcnt[w][sl];
+        uint4* d = (uint4*)(runs + (size_t)sl * runStride + (size_t)blk * kProjectBlock + at);
+        d[0] = o.rd;
+        d[1] = make_uint4(o.ra.x, o.ra.y, o.ra.z, o.ra.w);
+        d[2] = make_uint4(bw.x, bw.y, o.rb, slab_tile_mask(o.bounds, tileBits, slab_rows(slabs, sRows, sl)));
     }
 }
 

@@ -2,11 +2,12 @@
 # PMC passes (counters only with --kernel-trace/--stats; never with sys/runtime traces).
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-# CFG=<bench config> (default config 2), OUT=<dir under gpurun_out> (default pmc)
+# CFG=<bench config> (default config 2), OUT=<dir under gpurun_out> (default pmc), PMC_CMD=<another
+# program, e.g. tools/exp_virtual_ranks.py> instead of the bench line
 OUT=gpurun_out/${OUT:-pmc}
 mkdir -p $OUT
 export TMPDIR=/tmp
-CMD="python bench.py --config ${CFG:-cfg2_1m_sh3_1080p_f16} --steps 5 --warmup 2 --cpu-baseline 0 --parity 0 --orbit-steps 0 --inflight-steps 0 --virtual-ranks 0"
+CMD=${PMC_CMD:-"python bench.py --config ${CFG:-cfg2_1m_sh3_1080p_f16} --steps 5 --warmup 2 --cpu-baseline 0 --parity 0 --orbit-steps 0 --inflight-steps 0 --virtual-ranks 0"}
 i=0
 for set in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE" \
            "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM" \

@@ -586,12 +586,24 @@ __global__ __launch_bounds__(1024) void k_part_scan(uint32_t* __restrict__ block
     const uint32_t sl = blockIdx.x;
     uint32_t* row = blockSlabCounts + (size_t)sl * numBlocks;
     uint32_t carry = 0;
-    for (uint32_t base = 0; base < numBlocks; base += 1024) {
-        const uint32_t i = base + threadIdx.x;
-        const uint32_t v = i < numBlocks ? row[i] : 0u;
+    // IT consecutive counts per thread: one pass (one load latency) up to 4096 blocks (config 4's ranks
+    // have 2442), where one count per thread took three dependent passes
+    constexpr uint32_t IT = 4;
+    for (uint32_t base = 0; base < numBlocks; base += 1024u * IT) {
+        const uint32_t i0 = base + threadIdx.x * IT;
+        uint32_t v[IT], sum = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < IT; ++k) {
+            v[k] = i0 + k < numBlocks ? row[i0 + k] : 0u;
+            sum += v[k];
+        }
         uint32_t tot;
-        const uint32_t ex = block_exclusive_scan<1024>(v, lds, &tot);
-        if (i < numBlocks) row[i] = carry + ex;
+        uint32_t run = carry + block_exclusive_scan<1024>(sum, lds, &tot);
+#pragma unroll
+        for (uint32_t k = 0; k < IT; ++k) {
+            if (i0 + k < numBlocks) row[i0 + k] = run;
+            run += v[k];
+        }
         carry += tot;
         __syncthreads();
     }

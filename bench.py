@@ -103,7 +103,7 @@ def parse():
     p.add_argument("--traffic-json", default=None,
                    help="blend PMC numbers per launch (tools/traffic.py), used when measured on --config; "
                         "default profiles/PMC_TAG_pmc_blend_<cfgN>.json")
-    p.add_argument("--pmc-tag", default="r03", help="round tag of the default PMC files in profiles/")
+    p.add_argument("--pmc-tag", default="r04", help="round tag of the default PMC files in profiles/")
     p.add_argument("--stereo-path", choices=("depthfirst", "global"), default="depthfirst",
                    help="stereo configs: DepthFirst semantics (SURVEY 8f rank 1) or two Global views")
     p.add_argument("--df-max-gaussians", type=int, default=6_000_000,

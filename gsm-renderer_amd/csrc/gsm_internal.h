@@ -214,7 +214,11 @@ struct Tuning {
                               // runs (0: one workgroup per 256-id block)
     bool wide12 = false;      // GSM_SORT_WIDE12=1: a 12-bit tile field (2049..4096 tiles) in one 12-bit
                               // wide pass instead of two narrow passes (measured slower: DESIGN.md 4)
+    bool fusedScan = true;    // frames of <= kFusedScanMaxBlocks projection blocks: every scatter workgroup
+                              // sums the block counts before its own (no k_scan_blocks launch);
+                              // GSM_SCAN_FUSED=0: the separate scan
 };
+constexpr uint32_t kFusedScanMaxBlocks = 8192;
 // the environment's settings plus the device probe; `device` is a HIP device id
 Tuning tuning_from_env(int device);
 // Create-time probe of the one undocumented hardware property the default sort ranks rely on:
@@ -278,8 +282,10 @@ void launch_scan_blocks(uint32_t numBlocks, const ProjectArgs& args, const Devic
 void launch_scan_sums(uint32_t* sums, uint32_t nb, uint32_t cap, TileAssignmentHeader* hdr, uint32_t* queue,
                       hipStream_t stream);
 // duplicate-with-keys (GlobalShaders.metal:623-678 fused with :266-295)
+// fusedScan: A.blockSums holds the unscanned block counts (no launch_scan_blocks before it); each
+// workgroup adds up the counts before its own, workgroup 0 also the total (header, blend queue)
 void launch_scatter(const ProjectArgs& args, const DeviceArena& A, hipStream_t stream,
-                    const uint32_t* devCount = nullptr);
+                    const uint32_t* devCount = nullptr, bool fusedScan = false);
 // the blend's half-tile lists from the sorted values (skip flags, k_scatter), tiles [tileBegin, +numTiles)
 void launch_half_lists(const uint32_t* sortedVals, uint32_t tileBegin, uint32_t numTiles, const DeviceArena& A,
                        uint32_t tileCount, hipStream_t stream);

@@ -922,12 +922,48 @@ __device__ __forceinline__ uint32_t half_skip_flags(float mx, float ex, int tx) 
     return (l ? 1u : 0u) | (r ? 2u : 0u);
 }
 
+// Sum of sums[0, n) over the workgroup, exact in 64 bits (16-B loads where the array allows).
+__device__ __forceinline__ uint64_t block_sum_prefix(const uint32_t* __restrict__ sums, uint32_t n,
+                                                     unsigned long long* lds64) {
+    uint64_t v = 0;
+    const uint32_t n4 = n & ~3u;
+    constexpr uint32_t kStep = kProjectBlock * 4u;
+    uint32_t i = threadIdx.x * 4u;
+    for (; i + 3u * kStep < n4; i += 4u * kStep) {  // four 16-B loads in flight per thread
+        uint4 q[4];
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k) q[k] = *(const uint4*)(sums + i + k * kStep);
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k) v += (uint64_t)q[k].x + q[k].y + q[k].z + q[k].w;
+    }
+    for (; i < n4; i += kStep) {
+        const uint4 q = *(const uint4*)(sums + i);
+        v += (uint64_t)q.x + q.y + q.z + q.w;
+    }
+    if (threadIdx.x < n - n4) v += sums[n4 + threadIdx.x];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += (uint64_t)__shfl_xor((unsigned long long)v, o, 64);
+    if ((threadIdx.x & 63u) == 0) lds64[threadIdx.x >> 6] = v;
+    __syncthreads();
+    uint64_t t = 0;
+#pragma unroll
+    for (int w = 0; w < kProjectBlock / 64; ++w) t += lds64[w];
+    __syncthreads();
+    return t;
+}
+
+// fusedScan (frames of <= kFusedScanMaxBlocks blocks): blockOffsets holds the unscanned block counts;
+// each workgroup adds up those before its own -- the offset k_scan_blocks would have written, with
+// its saturation at 2^32 - 1 -- and workgroup 0 adds up all of them for the header and resets the
+// blend's queue (k_scan_blocks' other duties), so the frame needs no scan launch
 __global__ __launch_bounds__(kProjectBlock) void k_scatter(
     ProjectArgs P, const GaussianRenderData* __restrict__ rd, const short4* __restrict__ bounds,
     const uint32_t* __restrict__ counts, const uint32_t* __restrict__ masks,
     const uint32_t* __restrict__ blockOffsets, uint32_t* __restrict__ keys, uint32_t* __restrict__ vals,
-    const float2* __restrict__ sincos, const BlendRecord* __restrict__ rec, const uint32_t* __restrict__ devCount) {
+    const float2* __restrict__ sincos, const BlendRecord* __restrict__ rec, const uint32_t* __restrict__ devCount,
+    uint32_t fusedScan, TileAssignmentHeader* __restrict__ hdr, uint32_t* __restrict__ blendQueue) {
     __shared__ uint32_t lds[kProjectBlock / 64];
+    __shared__ unsigned long long lds64[kProjectBlock / 64];
     __shared__ uint32_t sOff[kProjectBlock];
     __shared__ uint32_t sMask[kProjectBlock];  // 0: no cooperative slots (large rect or no tiles)
     __shared__ uint32_t sRect[kProjectBlock];  // x0 | rw << 16 (rw <= 32)
@@ -943,11 +979,33 @@ __global__ __launch_bounds__(kProjectBlock) void k_scatter(
     const uint32_t gid = blockIdx.x * kProjectBlock + threadIdx.x;
     // records path: the count lives on the device and the grid covers the capacity
     const uint32_t n = devCount ? min(*devCount, P.count) : P.count;
+    if (fusedScan && blockIdx.x == 0) {  // (before any exit: an empty frame still gets its header)
+        const uint64_t all = block_sum_prefix(blockOffsets, (n + kProjectBlock - 1u) / kProjectBlock, lds64);
+        if (threadIdx.x == 0) {
+            uint32_t tot = all > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)all;
+            uint32_t ovf = 0;
+            if (tot > P.maxAssignments) {
+                tot = P.maxAssignments;
+                ovf = 1;
+            }
+            hdr->totalAssignments = tot;
+            hdr->maxCapacity = P.maxAssignments;
+            hdr->paddedCount = ((tot + 1023u) / 1024u) * 1024u;
+            hdr->overflow = ovf;
+            for (uint32_t q = 0; q < kQueueStripes; ++q) blendQueue[q * kQueueStride] = 0;
+        }
+    }
     if (blockIdx.x * kProjectBlock >= n) return;  // (uniform; the scan stopped at the count too)
-    uint32_t c = (gid < n) ? counts[gid] : 0u;
+    uint32_t c = (gid < n) ? counts[gid] : 0u;  // (in flight while the block counts are added up)
+    uint32_t base;
+    if (fusedScan) {
+        const uint64_t before = blockIdx.x ? block_sum_prefix(blockOffsets, blockIdx.x, lds64) : 0ull;
+        base = before > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)before;
+    } else {
+        base = blockOffsets[blockIdx.x];
+    }
     uint32_t total;
     const uint32_t off = block_exclusive_scan<kProjectBlock>(c, lds, &total);
-    const uint32_t base = blockOffsets[blockIdx.x];
     bool large = false;
     short4 r = make_short4(0, -1, 0, -1);
     uint32_t dbits = 0;
@@ -1271,11 +1329,13 @@ void launch_scan_blocks(uint32_t nb, const ProjectArgs& a, const DeviceArena& A,
                        a.maxAssignments, A.header, A.tileQueue, devCount);
 }
 
-void launch_scatter(const ProjectArgs& a, const DeviceArena& A, hipStream_t s, const uint32_t* devCount) {
+void launch_scatter(const ProjectArgs& a, const DeviceArena& A, hipStream_t s, const uint32_t* devCount,
+                    bool fusedScan) {
     const uint32_t blocks = (a.count + kProjectBlock - 1) / kProjectBlock;
-    if (blocks == 0) return;
+    if (blocks == 0) return;  // (the caller scans such a frame with launch_scan_blocks)
     hipLaunchKernelGGL(k_scatter, dim3(blocks), dim3(kProjectBlock), 0, s, a, A.renderData, A.bounds,
-                       A.tileCounts, A.tileMasks, A.blockSums, A.keys[0], A.vals[0], A.sincosTable, A.rec, devCount);
+                       A.tileCounts, A.tileMasks, A.blockSums, A.keys[0], A.vals[0], A.sincosTable, A.rec, devCount,
+                       fusedScan ? 1u : 0u, A.header, A.tileQueue);
 }
 
 void launch_headers(const uint32_t* sortedKeys, const FrameGeometry& g, const DeviceArena& A,

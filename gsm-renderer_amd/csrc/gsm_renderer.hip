@@ -438,9 +438,11 @@ gsm_status GlobalRenderer::runFrame(hipStream_t s, const ProjectArgs& a, uint32_
     if (prof) hipEventRecord(ev[0], s);
     front(fa);  // the projection (or records) launch; its block 0 orders the blend units (fa.schedUnits)
     if (prof) hipEventRecord(ev[1], s);
-    launch_scan_blocks(nb, a, arena_, s, devCount);
+    // (a frame of few blocks: the scatter's workgroups add up the block counts themselves)
+    const bool fusedScan = tuning_.fusedScan && nb > 0 && nb <= kFusedScanMaxBlocks;
+    if (!fusedScan) launch_scan_blocks(nb, a, arena_, s, devCount);
     if (prof) hipEventRecord(ev[2], s);
-    launch_scatter(a, arena_, s, devCount);
+    launch_scatter(a, arena_, s, devCount, fusedScan);
     if (keep) {  // preserve the unsorted assignment arrays for readback
         hipMemcpyAsync(arena_.keysKeep, arena_.keys[0], (size_t)maxAssignments_ * 4, hipMemcpyDeviceToDevice, s);
         hipMemcpyAsync(arena_.valsKeep, arena_.vals[0], (size_t)maxAssignments_ * 4, hipMemcpyDeviceToDevice, s);

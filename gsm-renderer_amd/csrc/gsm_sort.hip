@@ -1351,6 +1351,8 @@ Tuning tuning_from_env(int device) {
     t.mgPushPerCU = mpg ? atoi(mpg) : 4;
     const char* w12 = getenv("GSM_SORT_WIDE12");
     t.wide12 = w12 && w12[0] == '1';
+    const char* fs = getenv("GSM_SCAN_FUSED");
+    t.fusedScan = !(fs && fs[0] == '0');
     return t;
 }
 

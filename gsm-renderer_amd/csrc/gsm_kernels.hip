@@ -655,23 +655,38 @@ __global__ __launch_bounds__(kProjectBlock) void k_part_copy(
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
     constexpr uint32_t kWaves = kProjectBlock / 64;
     const uint32_t runsTotal = nb * numSlabs;
-    for (uint32_t k = blockIdx.x * kWaves + wave; k < runsTotal; k += gridDim.x * kWaves) {
-        const uint32_t b = k / numSlabs, sl = k - b * numSlabs;
-        const uint32_t off = blockSlabOffsets[(size_t)sl * nb + b];
-        const uint32_t end = b + 1u < nb ? blockSlabOffsets[(size_t)sl * nb + b + 1u] : sTotal[sl];
-        const uint32_t n = end - off;
-        if (n == 0) continue;
-        const uint4* src = (const uint4*)(runs + (size_t)sl * runStride + (size_t)b * kProjectBlock);
-        const uint64_t at = (uint64_t)sBase[sl] + off;  // the run's first record at the destination
-        if constexpr (PUSH) {
-            const uint64_t cap = peers.cap[sl];
-            const uint32_t m = at >= cap ? 0u : (uint32_t)min((uint64_t)n, cap - at);  // never past it
-            uint4* d = (uint4*)(peers.recv[sl] + at);
-            for (uint32_t j = lane; j < 3u * m; j += 64u) st_sys128(d, 3u * m * 16u, j, src[j]);
-        } else {
-            const uint32_t m = at >= capacity ? 0u : (uint32_t)min((uint64_t)n, capacity - at);
-            uint4* d = (uint4*)(send + at);
-            for (uint32_t j = lane; j < 3u * m; j += 64u) d[j] = src[j];
+    // the wave's runs k0, k0 + S, k0 + 2S, ...: lane j loads the bounds of its j-th run up front (one
+    // load round trip for up to 64 runs instead of one per run), the copy loop reads them by readlane
+    const uint32_t S = gridDim.x * kWaves, k0 = blockIdx.x * kWaves + wave;
+    const uint32_t nRuns = k0 < runsTotal ? (runsTotal - k0 + S - 1u) / S : 0u;
+    for (uint32_t c0 = 0; c0 < nRuns; c0 += 64u) {
+        uint32_t offL = 0, nL = 0;
+        if (c0 + lane < nRuns) {
+            const uint32_t kL = k0 + (c0 + lane) * S;
+            const uint32_t bL = kL / numSlabs, slL = kL - bL * numSlabs;
+            offL = blockSlabOffsets[(size_t)slL * nb + bL];
+            const uint32_t endL = bL + 1u < nb ? blockSlabOffsets[(size_t)slL * nb + bL + 1u] : sTotal[slL];
+            nL = endL - offL;
+        }
+        const uint32_t cnt = min(64u, nRuns - c0);
+        for (uint32_t j = 0; j < cnt; ++j) {
+            const uint32_t n = (uint32_t)__builtin_amdgcn_readlane((int)nL, (int)j);
+            if (n == 0) continue;
+            const uint32_t off = (uint32_t)__builtin_amdgcn_readlane((int)offL, (int)j);
+            const uint32_t k = k0 + (c0 + j) * S;
+            const uint32_t b = k / numSlabs, sl = k - b * numSlabs;
+            const uint4* src = (const uint4*)(runs + (size_t)sl * runStride + (size_t)b * kProjectBlock);
+            const uint64_t at = (uint64_t)sBase[sl] + off;  // the run's first record at the destination
+            if constexpr (PUSH) {
+                const uint64_t cap = peers.cap[sl];
+                const uint32_t m = at >= cap ? 0u : (uint32_t)min((uint64_t)n, cap - at);  // never past it
+                uint4* d = (uint4*)(peers.recv[sl] + at);
+                for (uint32_t w = lane; w < 3u * m; w += 64u) st_sys128(d, 3u * m * 16u, w, src[w]);
+            } else {
+                const uint32_t m = at >= capacity ? 0u : (uint32_t)min((uint64_t)n, capacity - at);
+                uint4* d = (uint4*)(send + at);
+                for (uint32_t w = lane; w < 3u * m; w += 64u) d[w] = src[w];
+            }
         }
     }
     if constexpr (PUSH) {

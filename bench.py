@@ -28,6 +28,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
 import sys
 import time
@@ -407,7 +408,7 @@ def main():
         if rank == 0:
             sys.path.insert(0, os.path.join(ROOT, "oracle"))
             import oracle as O  # parity checker only
-            ref = O.render(world_np, harm_np, sh, cam_d, W, H, max_gaussians=n, nthreads=min(16, cpu_threads(args)))
+            ref = O.render(world_np, harm_np, sh, cam_d, W, H, max_gaussians=n, nthreads=min(16, cpu_thread_candidates(args)[0]))
             multi_parity = bool(np.array_equal(mg.copy_frame(W, H), ref["color"])) and \
                 bool(np.array_equal(mg.copy_depth(W, H), ref["depth"]))
     # BASELINE config 4 (the 4K scene of config 3 on N GPUs): timed the same way after `value`
@@ -466,15 +467,13 @@ def main():
     if world_size == 1 and not native_multi and (args.parity or args.cpu_baseline):
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import oracle as O  # CPU baseline + parity checker only
-        threads = cpu_threads(args)
+        cands = cpu_thread_candidates(args)
         views = [scenes.make_camera(W, H, -stereo), scenes.make_camera(W, H, stereo)] if stereo else [cam_d]
-        times = []
-        refs = None
         reps = 3 if args.cpu_baseline else 1
-        for _ in range(reps):  # one frame = every view (both eyes for config 5)
-            t = time.perf_counter()
-            refs = [O.render(world_np, harm_np, sh, cv, W, H, max_gaussians=n, nthreads=threads) for cv in views]
-            times.append(time.perf_counter() - t)
+        # one frame = every view (both eyes for config 5); the baseline is the best thread count the box grants
+        threads, times, per_threads, refs = time_oracle(
+            lambda nt: [O.render(world_np, harm_np, sh, cv, W, H, max_gaussians=n, nthreads=nt) for cv in views],
+            cands if args.cpu_baseline else cands[:1], reps)
         if args.parity:
             if orbit is not None:  # the buffer holds the last orbit frame: check it, then redo the static one
                 ro = O.render(world_np, harm_np, sh, orbit_last_cam, W, H, max_gaussians=n, nthreads=threads)
@@ -492,8 +491,8 @@ def main():
             med = float(np.median(times))
             cpu = cpu_baseline_entry(med, threads, f"{reps} full frames of {args.config} ({n} gaussians, "
                                      f"{len(views)} view(s) of {W}x{H}) with the C oracle (oracle/gsm_oracle.c, "
-                                     f"pthreads), median {med:.2f} s/frame", refs[-1]["times"])
-            if threads != 16:  # the r01-r03 figure (16 threads), for comparison
+                                     f"pthreads), median {med:.2f} s/frame", refs[-1]["times"], per_threads)
+            if 16 not in per_threads:  # the r01-r03 figure (16 threads), for comparison
                 t = time.perf_counter()
                 O.render(world_np, harm_np, sh, cam_d, W, H, max_gaussians=n, nthreads=16)
                 t16 = time.perf_counter() - t
@@ -682,14 +681,37 @@ def cpu_model():
     return None
 
 
-def cpu_threads(args) -> int:
-    """Oracle threads of cpu_baseline: --cpu-threads, or every CPU this process may run on."""
+def cpu_thread_candidates(args):
+    """Oracle thread counts to time for cpu_baseline: --cpu-threads alone, else the CPUs of this
+    process's affinity mask and the cgroup quota rounded up (on the GPU box 256 affine CPUs share a
+    16-CPU quota: 256 threads there measure the throttling, not the host) -- the best one is `value`."""
     if args.cpu_threads > 0:
-        return args.cpu_threads
+        return [args.cpu_threads]
     try:
-        return max(1, len(os.sched_getaffinity(0)))
+        aff = max(1, len(os.sched_getaffinity(0)))
     except (AttributeError, OSError):
-        return max(1, os.cpu_count() or 1)
+        aff = max(1, os.cpu_count() or 1)
+    quota = cgroup_cpu_quota()
+    cands = [aff]
+    if quota is not None and math.ceil(quota) < aff:
+        cands.insert(0, max(1, math.ceil(quota)))
+    return cands
+
+
+def time_oracle(render, cands, reps):
+    """Median seconds per frame of `render(nthreads)` over `reps` frames for each thread count;
+    returns (best thread count, its frame times, {threads: frames/s}, the last frame's result)."""
+    best, per, out = None, {}, None
+    for nt in cands:
+        times = []
+        for _ in range(reps):
+            t = time.perf_counter()
+            out = render(nt)
+            times.append(time.perf_counter() - t)
+        per[nt] = 1.0 / float(np.median(times))
+        if best is None or per[nt] > per[best[0]]:
+            best = (nt, times)
+    return best[0], best[1], per, out
 
 
 def cgroup_cpu_quota():
@@ -702,7 +724,7 @@ def cgroup_cpu_quota():
         return None
 
 
-def cpu_baseline_entry(median_s, threads, sample, stage_times):
+def cpu_baseline_entry(median_s, threads, sample, stage_times, per_threads=None):
     try:
         affinity = len(os.sched_getaffinity(0))
     except (AttributeError, OSError):
@@ -711,9 +733,11 @@ def cpu_baseline_entry(median_s, threads, sample, stage_times):
     out = {"value": 1.0 / median_s, "unit": "frames/s", "cores": threads, "kind": "port",
            "host_cpus": os.cpu_count(), "affinity_cpus": affinity, "cgroup_cpu_quota": quota,
            "cpu_model": cpu_model(), "sample": sample, "stages_s": {k: round(v, 4) for k, v in stage_times.items()}}
-    if quota is not None and quota < threads:
-        out["note"] = (f"{threads} oracle threads (every CPU of the affinity mask) under a cgroup quota of {quota} "
-                       f"CPUs: the box grants this process {quota} CPUs' worth of time")
+    for nt, v in sorted((per_threads or {}).items()):
+        out[f"threads_{nt}"] = {"value": v, "unit": "frames/s", "cores": nt}
+    if per_threads and len(per_threads) > 1:
+        out["note"] = (f"oracle timed at {sorted(per_threads)} threads (affinity mask {affinity} CPUs, cgroup quota "
+                       f"{quota} CPUs); value = the best, {threads} threads")
     return out
 
 
@@ -780,13 +804,11 @@ def run_depthfirst(args, c, world_np, harm_np, world, harm, dev):
     if args.parity or args.cpu_baseline:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import oracle as O  # CPU baseline + parity checker only
-        threads = cpu_threads(args)
-        times, ref = [], None
-        for _ in range(2 if args.cpu_baseline else 1):
-            t = time.perf_counter()
-            ref = O.df_render_stereo(world_np, harm_np, sh, cams[0], cams[1], W, H,
-                                     max_gaussians=max(n, args.df_max_gaussians), nthreads=threads)
-            times.append(time.perf_counter() - t)
+        cands = cpu_thread_candidates(args)
+        threads, times, per_threads, ref = time_oracle(
+            lambda nt: O.df_render_stereo(world_np, harm_np, sh, cams[0], cams[1], W, H,
+                                          max_gaussians=max(n, args.df_max_gaussians), nthreads=nt),
+            cands if args.cpu_baseline else cands[:1], 2 if args.cpu_baseline else 1)
         if args.parity:
             got = color.view(torch.int16).cpu().numpy().view(np.uint16)
             parity = bool(np.array_equal(got, ref["color"])) and int(ref["total_instances"]) == A
@@ -794,7 +816,7 @@ def run_depthfirst(args, c, world_np, harm_np, world, harm, dev):
             med = float(np.median(times))
             cpu = cpu_baseline_entry(med, threads, f"{len(times)} full DepthFirst stereo frames of {args.config} "
                                      f"with the C oracle (og_df_render_stereo, pthreads), median {med:.2f} s/frame",
-                                     ref["times"])
+                                     ref["times"], per_threads)
     out = {
         "metric": "frames/sec @ N Gaussians × W×H (1/2/4/8 GPU); sort Gkeys/s; blend HBM GB/s",
         "value": 1e3 / ms_per_step, "unit": "frames/s", "n_gpus": 1, "steps": args.steps,

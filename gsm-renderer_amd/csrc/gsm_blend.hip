@@ -41,10 +41,43 @@ __device__ __forceinline__ uint32_t as_u32(h2 v) { return __builtin_bit_cast(uin
 __device__ __forceinline__ h2 splat_lo(h2 v) { return h2{v.x, v.x}; }
 __device__ __forceinline__ h2 splat_hi(h2 v) { return h2{v.y, v.y}; }
 
+// The table index of a packed pair of quadratic forms.  GSM_BLEND_PCLAMP: every p above 34.65625 (the
+// largest p with a nonzero entry, +inf included) reads the one zero entry of 34.6875 (0x5056), so the
+// lanes of a gaussian's far field broadcast one LDS word instead of gathering scattered zeros
+// (bank conflicts); v_pk_minimum3_f16 (IEEE 754-2019 minimum) keeps negative p and NaN p (whose entries
+// are NaN) -- the entry read is the same value for every p.
+#ifndef GSM_BLEND_PCLAMP
+#define GSM_BLEND_PCLAMP 0
+#endif
+// GSM_BLEND_DEADX: a lane whose group broke walks on with its columns moved to x = 65504, so its p is
+// +-inf or NaN (one of three table words) instead of a live-looking scattered index
+#ifndef GSM_BLEND_DEADX
+#define GSM_BLEND_DEADX 0
+#endif
+// GSM_BLEND_DUPTBL (attribution builds only): every table read of the walk issued twice, the second
+// result folded into nothing observable -- the difference of SQ_LDS_BANK_CONFLICT to the plain build
+// is the conflict count of the table reads themselves
+// GSM_BLEND_ZSTATS (statistics builds only): the trace's t[3] holds per unit the entries on which no
+// live pixel has a nonzero alpha and the sum over entries of the live pixels; t[0]'s top 16 bits ncomp
+#ifndef GSM_BLEND_ZSTATS
+#define GSM_BLEND_ZSTATS 0
+#endif
+#ifndef GSM_BLEND_DUPTBL
+#define GSM_BLEND_DUPTBL 0
+#endif
+__device__ __forceinline__ uint32_t tbl_bits(h2 p) {
+#if GSM_BLEND_PCLAMP
+    const h2 c = {(h1)34.6875f, (h1)34.6875f};
+    return as_u32(__builtin_elementwise_minimum(p, c));
+#else
+    return as_u32(p);
+#endif
+}
+
 // exp table lookup for a packed pair of quadratic forms: the table is indexed by the fp16 bits
 // of p and holds fp16(exp(fp16(-0.5 * p))), correctly rounded (gsm_detmath.h)
 __device__ __forceinline__ h2 lookup2(const uint16_t* tbl, h2 p) {
-    const uint32_t pb = as_u32(p);
+    const uint32_t pb = tbl_bits(p);
     const uint32_t lo = tbl[pb & 0xFFFFu];
     const uint32_t hi = tbl[pb >> 16];
     return as_h2(lo | (hi << 16));
@@ -224,6 +257,11 @@ __global__ __launch_bounds__(NT) void k_blend_px(
     }
     const h2 ONE = {(h1)1.0f, (h1)1.0f};
     const h2 ZERO = {(h1)0.0f, (h1)0.0f};
+    const h2 FAR = {(h1)65504.0f, (h1)65504.0f};  // (GSM_BLEND_DEADX)
+    (void)FAR;
+#if GSM_BLEND_DUPTBL
+    uint32_t dupSink = 0;
+#endif
     const uint32_t thrBits = (uint32_t)__builtin_bit_cast(uint16_t, (h1)(1.0f / 255.0f));
     const h1 c099 = (h1)0.99;
     const h2 C099 = {c099, c099};
@@ -269,6 +307,9 @@ __global__ __launch_bounds__(NT) void k_blend_px(
         if (trace) tStart = __builtin_amdgcn_s_memrealtime();
         uint32_t nproc = 0;
         uint32_t ncomp = 0;  // entry at which the unit moved to one pair per lane (trace only)
+#if GSM_BLEND_ZSTATS
+        uint32_t zeroEntries = 0, alivePx = 0;  // (statistics build: entries no live pixel takes, live pixels)
+#endif
         uint32_t nextQ = 0;
         bool claimed = false;
         // claimMode 2: the walk this unit made last frame (before this frame's walk overwrites it)
@@ -387,13 +428,20 @@ __global__ __launch_bounds__(NT) void k_blend_px(
                             for (int q = 0; q < P; ++q) {
                                 // raw table words: first used in stage 3, after the current
                                 // group's blend, so the LDS latency hides behind it
-                                const uint32_t pb = as_u32(pq[q]);
+                                const uint32_t pb = tbl_bits(pq[q]);
                                 en[k][q].x = tbl[pb & 0xFFFFu];
                                 en[k][q].y = tbl[pb >> 16];
+#if GSM_BLEND_DUPTBL
+                                dupSink ^= (uint32_t)((volatile uint16_t*)tbl)[pb & 0xFFFFu] ^
+                                           ((uint32_t)((volatile uint16_t*)tbl)[pb >> 16] << 16);
+#endif
                             }
                         }
                     }
                     // stage 2: blend the current group
+#if GSM_BLEND_ZSTATS
+                    const uint32_t g1s = b0 + gi * U;
+#endif
 #pragma unroll
                     for (uint32_t k = 0; k < U; ++k) {
                         // group break (GlobalShaders.metal:1086-1088): max T of the 4x2 group
@@ -410,6 +458,17 @@ __global__ __launch_bounds__(NT) void k_blend_px(
                             gm = max(gm, o);
                         }
                         alive = alive && !(gm < thrBits);  // T >= 0: fp16 order == bit order
+#if GSM_BLEND_ZSTATS
+                        {
+                            uint32_t nz = 0;
+#pragma unroll
+                            for (int q = 0; q < P; ++q) nz |= as_u32(ac[k][q]);
+                            if (g1s + k < count) {
+                                zeroEntries += __ballot(alive && nz != 0) == 0 ? 1u : 0u;
+                                alivePx += (uint32_t)__popcll(__ballot(alive)) * (2u * P);
+                            }
+                        }
+#endif
                         const h2 rgv = as_h2(rgc[k]), bdv = as_h2(bdc[k]);
                         // a dead lane keeps T and C (alpha 0 would give the same bits: C + c*0 == C,
                         // T*1 == T): the updates run under an EXEC mask of the live lanes
@@ -439,6 +498,10 @@ __global__ __launch_bounds__(NT) void k_blend_px(
                             b0C = b0;
                             goto compact_phase;
                         }
+#if GSM_BLEND_DEADX
+#pragma unroll
+                        for (int k = 0; k < P; ++k) X[k] = alive ? X[k] : FAR;
+#endif
                     }
                     // stage 3: the next group's alphas
 #pragma unroll
@@ -497,7 +560,10 @@ __global__ __launch_bounds__(NT) void k_blend_px(
                 h2 T1 = pick(T[0], T[1]), R1 = pick(R[0], R[1]), G1 = pick(G[0], G[1]);
                 h2 B1 = pick(B[0], B[1]), D1 = pick(D[0], D[1]);
                 const uint32_t px1 = ux + (sg & 3u) * 4u + 2u * kk, py1 = uy + (sg >> 2) * 2u + rr;
-                const h2 X1 = h2{(h1)(float)px1, (h1)(float)(px1 + 1u)};
+                h2 X1 = h2{(h1)(float)px1, (h1)(float)(px1 + 1u)};
+#if GSM_BLEND_DEADX
+                if (!valid1) X1 = FAR;
+#endif
                 const h2 Y1 = h2{(h1)(float)py1, (h1)(float)py1};
                 bool alive1 = valid1;
                 // the same per-pixel operations as the half-tile walk (quadform above)
@@ -570,9 +636,13 @@ __global__ __launch_bounds__(NT) void k_blend_px(
                             const h2 pq = quad1(ra.x, ra.y, opn1[k]);
                             rgn1[k] = ra.w;
                             bdn1[k] = lrecB[wv][j];
-                            const uint32_t pb = as_u32(pq);
+                            const uint32_t pb = tbl_bits(pq);
                             en1[k].x = tbl[pb & 0xFFFFu];
                             en1[k].y = tbl[pb >> 16];
+#if GSM_BLEND_DUPTBL
+                            dupSink ^= (uint32_t)((volatile uint16_t*)tbl)[pb & 0xFFFFu] ^
+                                       ((uint32_t)((volatile uint16_t*)tbl)[pb >> 16] << 16);
+#endif
                         }
 #else
                         const uint32_t sx = nb ? nA.x : bA.x, sy = nb ? nA.y : bA.y;
@@ -597,6 +667,12 @@ __global__ __launch_bounds__(NT) void k_blend_px(
                         const uint32_t tb = as_u32(T1);
                         const uint32_t gm = quad_max_u32(max(tb & 0xFFFFu, tb >> 16));
                         alive1 = alive1 && !(gm < thrBits);
+#if GSM_BLEND_ZSTATS
+                        if (e + k < count) {
+                            zeroEntries += __ballot(alive1 && as_u32(ac1[k]) != 0) == 0 ? 1u : 0u;
+                            alivePx += (uint32_t)__popcll(__ballot(alive1)) * 2u;
+                        }
+#endif
                         if (alive1) {
                             const h2 rgv = as_h2(rgc1[k]), bdv = as_h2(bdc1[k]);
                             const h2 w = ac1[k] * T1;  // (GlobalShaders.metal:1137-1149)
@@ -608,7 +684,12 @@ __global__ __launch_bounds__(NT) void k_blend_px(
                         }
                     }
                     e += U1;
-                    if ((e & 15u) == 0 && (e >= count || __ballot(alive1) == 0)) break;
+                    if ((e & 15u) == 0) {
+                        if (e >= count || __ballot(alive1) == 0) break;
+#if GSM_BLEND_DEADX
+                        X1 = alive1 ? X1 : FAR;
+#endif
+                    }
                     // stage 3: the next group's alphas
 #pragma unroll
                     for (uint32_t k = 0; k < U1; ++k) {
@@ -668,6 +749,11 @@ __global__ __launch_bounds__(NT) void k_blend_px(
             t[1] = __builtin_amdgcn_s_memrealtime();
             t[2] = ((unsigned long long)count << 32) | nproc;
             const unsigned long long xcc = (unsigned long long)__builtin_amdgcn_s_getreg(20 | (3 << 11));  // XCC_ID
+#if GSM_BLEND_ZSTATS
+            t[0] = ((unsigned long long)ncomp << 48) | (tStart & 0xFFFFFFFFFFFFull);
+            t[3] = ((unsigned long long)alivePx << 32) | zeroEntries;
+            if (false)
+#endif
             t[3] = (xcc << 48) | ((unsigned long long)(ncomp & 0xFFFFu) << 32) |
                    (unsigned long long)__builtin_amdgcn_s_getreg(4 | (31 << 11));
         }
@@ -676,6 +762,9 @@ __global__ __launch_bounds__(NT) void k_blend_px(
         claim();  // (no-op when claimed during the walk)
         qi = gridWaves + stripe + stripes * __builtin_amdgcn_readfirstlane(nextQ);
     }
+#if GSM_BLEND_DUPTBL
+    if (dupSink == 0x9E3779B9u && flags == -1) queue[0] = dupSink;  // keeps the duplicate reads alive
+#endif
     if (unitCost && lane == 0 && waveMax) atomicMax(&costMax[(blockIdx.x * NW + wv) % kCostMaxSlots], waveMax);
     // multi-GPU frame gathered on rank 0 (gsm_multigpu.hip): the pixels this wave stored into rank
     // 0's frame (write-through, flags bit 10) are drained and the wave arrives at barrier 2 (the last

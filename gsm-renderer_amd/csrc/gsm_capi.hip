@@ -34,6 +34,7 @@ const char* gsm_status_string(gsm_status s) {
         case GSM_ERR_MISSING_REQUIRED_BUFFER: return "Missing required buffer";
         case GSM_ERR_INVALID_ARGUMENT: return "Invalid argument";
         case GSM_ERR_UNSUPPORTED: return "GlobalRenderer does not support stereo rendering";
+        case GSM_ERR_PHASE_ORDER: return "Multi-GPU frame phase called out of order (gsm_multigpu_finish_frame)";
     }
     return "unknown status";
 }

@@ -26,18 +26,21 @@ __device__ __forceinline__ float clampf(float v, float lo, float hi) {
 // Correctly rounded a[k] / b for K numerators over one divisor -- bit for bit the IEEE a[k] / b of the
 // oracle -- at one division's cost: y = RN(1 / b), then per numerator q = RN(a y), r = RN(a - b q) (exact
 // by the fma), q' = RN(q + r y): Markstein's correction, correctly rounded when y is the correctly
-// rounded reciprocal and r does not underflow (Muller et al., Handbook of Floating-Point Arithmetic,
-// division via fma).  r = 0 keeps q (so a = -0 gives -0).  A wave holding a numerator below 2^-96
-// (nonzero: r could underflow) or a divisor outside [2^-100, 2^100] takes the divisions themselves.
-// Checked on 9e8 random and fp16-valued pairs against IEEE division (tools/exp/markstein_div.c,
-// tests/test_markstein_div.py).  b > 0 (norms).
+// rounded reciprocal, q is normal and r does not underflow (Muller et al., Handbook of Floating-Point
+// Arithmetic, division via fma).  r = 0 keeps q (so a = -0 gives -0).  The fast path takes numerators
+// that are zero or of magnitude in [2^-96, 2^96] (finite; below 2^-96 r could underflow) over divisors
+// in [2^-29, 2^29], so every quotient lies in [2^-125, 2^125]: normal, no overflow (r05, ADVICE r04: the
+// earlier [2^-100, 2^100] divisor range let quotients go subnormal or overflow).  A wave holding any
+// other operand takes the divisions themselves.  Checked on random, signed-zero, fp16-valued and
+// arbitrary-bit-pattern pairs against IEEE division (tools/exp/markstein_div.c, tests/test_markstein_div.py).
+// b > 0 (norms).
 template <int K>
 __device__ __forceinline__ void div_many(float (&a)[K], float b) {
-    bool slow = !(b >= 0x1p-100f && b <= 0x1p100f);
+    bool slow = !(b >= 0x1p-29f && b <= 0x1p29f);
 #pragma unroll
     for (int k = 0; k < K; ++k) {
         const uint32_t x = __float_as_uint(a[k]) & 0x7FFFFFFFu;
-        slow = slow || (x - 1u) < (31u << 23) - 1u;
+        slow = slow || (x != 0u && x - (31u << 23) > (192u << 23));  // 0 < |a| < 2^-96, |a| > 2^96, inf, NaN
     }
     if (__ballot(slow) != 0ull) {  // (rare; wave-uniform)
 #pragma unroll

@@ -153,7 +153,8 @@ __global__ __launch_bounds__(64) void k_mg_sync(SyncPeers peers, uint32_t* __res
         const unsigned long long t0 = wall_clock64();
         for (;;) {
             const uint32_t f = ld_sys32(flag);
-            if ((int)((f & kEpochMask) - epoch) >= 0) {
+            // f at or after epoch, modulo 2^31 (epochs wrap from 2^31 - 1 to 1)
+            if ((int)(((f & kEpochMask) - epoch) << 1) >= 0) {
                 failed = (f & kFailBit) != 0u && (f & kEpochMask) == epoch;
                 break;
             }
@@ -197,13 +198,21 @@ class MultiGpu {
     gsm_status phase(int p, hipStream_t s, const gsm_gaussian_input& in, const gsm_camera_params& cam, uint32_t width,
                      uint32_t height, void* color, size_t colorPitch, void* depth, size_t depthPitch,
                      void* gatherColor);
+    // gsm_multigpu_finish_frame: the remaining phases of a frame left unfinished (barrier steps only
+    // from the slab render on; phase 1's push still runs when phase 0 published this rank's counts)
+    gsm_status finishFrame(hipStream_t s);
+    // gsm_multigpu_wait_event: the next phase 0 waits for `ev` on the stream its projection runs on
+    gsm_status waitEvent(hipEvent_t ev) {
+        inputEvent_ = ev;
+        return GSM_OK;
+    }
     gsm_status frame(void** color, size_t* pitch) const {
-        *color = rank_ == 0 ? frameBuf(frame_) : nullptr;
+        *color = rank_ == 0 ? frameBuf(par_) : nullptr;
         *pitch = rank_ == 0 ? framePitch_ : 0;
         return GSM_OK;
     }
     gsm_status frameDepth(void** depth, size_t* pitch) const {
-        *depth = rank_ == 0 ? depthBuf(frame_) : nullptr;
+        *depth = rank_ == 0 ? depthBuf(par_) : nullptr;
         *pitch = rank_ == 0 ? depthPitch0_ : 0;
         return GSM_OK;
     }
@@ -221,7 +230,7 @@ class MultiGpu {
                    : GSM_ERR_RENDER_FAILED;
     }
     gsm_status copyFrame(void* dst, size_t pitch, uint32_t width, uint32_t height, bool depth) {
-        const char* src = depth ? depthBuf(frame_) : frameBuf(frame_);
+        const char* src = depth ? depthBuf(par_) : frameBuf(par_);
         const size_t bpp = depth ? 2u : bpp_;
         if (rank_ != 0 || !src || !dst || width > r_->maxWidth() || height > r_->maxHeight() || pitch < (size_t)width * bpp)
             return GSM_ERR_INVALID_ARGUMENT;
@@ -245,9 +254,11 @@ class MultiGpu {
     gsm_status check(const gsm_gaussian_input& in, uint32_t width, uint32_t height, void* color, size_t colorPitch,
                      void* depth, size_t depthPitch, void* gatherColor, Targets* t) const;
     uint32_t* ctl() const { return (uint32_t*)mem_; }
-    // rank 0's gathered frames of frame f: one pair, or (pipelined) two alternating by frame parity
-    char* frameBuf(uint32_t f) const { return frame0_ ? frame0_ + (pipelined_ ? (f & 1u) * frameStride_ : 0) : nullptr; }
-    char* depthBuf(uint32_t f) const { return depth0_ ? depth0_ + (pipelined_ ? (f & 1u) * depthStride_ : 0) : nullptr; }
+    // rank 0's gathered frames of a frame of parity `par`: one pair, or (pipelined) two alternating
+    char* frameBuf(uint32_t par) const { return frame0_ ? frame0_ + (pipelined_ ? par * frameStride_ : 0) : nullptr; }
+    char* depthBuf(uint32_t par) const { return depth0_ ? depth0_ + (pipelined_ ? par * depthStride_ : 0) : nullptr; }
+    gsm_status run(int p, hipStream_t s, const gsm_gaussian_input* in, const gsm_camera_params* cam, uint32_t width,
+                   uint32_t height, Targets t, size_t colorPitch, void* depth, size_t depthPitch, void* gatherColor);
     bool libraryFrame(const void* p) const {
         return p && (p == frame0_ || p == depth0_ || (pipelined_ && (p == frame0_ + frameStride_ || p == depth0_ + depthStride_)));
     }
@@ -265,11 +276,11 @@ class MultiGpu {
     // kSyncWaitBlocks workgroups acquire (every XCD's L2 drops its lines of the frame)
     void wait(hipStream_t s, uint32_t barrier) {
         hipLaunchKernelGGL(k_mg_sync, dim3(barrier == 2 ? kSyncWaitBlocks : 1u), dim3(64), 0, s, sync_, ctl(),
-                           (uint32_t)rank_, (uint32_t)world_, barrier, frame_, 0, frame_ & 1u, 0, 0, timeoutTicks_);
+                           (uint32_t)rank_, (uint32_t)world_, barrier, frame_, 0, par_, 0, 0, timeoutTicks_);
     }
     void arrive(hipStream_t s, uint32_t barrier, bool publishZero, bool fail) {
         hipLaunchKernelGGL(k_mg_sync, dim3(1), dim3(64), 0, s, sync_, ctl(), (uint32_t)rank_, (uint32_t)world_, barrier,
-                           frame_, publishZero ? 1 : 0, frame_ & 1u, 1, fail ? 1 : 0, timeoutTicks_);
+                           frame_, publishZero ? 1 : 0, par_, 1, fail ? 1 : 0, timeoutTicks_);
     }
 
     GlobalRenderer* r_ = nullptr;
@@ -286,8 +297,11 @@ class MultiGpu {
     char* frame0_ = nullptr;  // rank 0's gathered colour frame (peer mapping on the other ranks)
     char* depth0_ = nullptr;  // rank 0's gathered depth frame
     bool connected_ = false;
-    uint32_t frame_ = 0;       // frames begun (phase 0); the barriers' epoch
+    uint32_t frame_ = 0;       // frames begun (phase 0); the barriers' epoch: 1 .. 2^31 - 1, then 1 again
+    uint32_t par_ = 0;         // the frame's parity, alternating every frame (also across the epoch's wrap)
     int nextPhase_ = 0;        // phases run in order 0..3
+    Targets frameT_{};         // phase 0's targets (gathering or not: the barrier steps of finishFrame)
+    hipEvent_t inputEvent_ = nullptr;  // gsm_multigpu_wait_event (one-shot, the next phase 0)
     gsm_status frameErr_ = GSM_OK;  // this rank's error of the current frame (barrier-only phases after it)
     bool interleave_ = false;  // slab rows interleaved (GSM_MG_ROWS=interleaved at prepare)
     // Pipelined (GSM_MG_PIPELINE=1 at prepare, every rank alike): phases 0-1 on the library's own stream
@@ -306,6 +320,8 @@ class MultiGpu {
 
 void MultiGpu::release() {
     hipSetDevice(device_);
+    // pipelined: the library's stream may still run a frame's projection or push into peer memory
+    if (front_) hipStreamSynchronize(front_);
     for (void* p : opened_) hipIpcCloseMemHandle(p);
     opened_.clear();
     for (void* p : {(void*)mem_, (void*)sendCounts_, (void*)recvCount_, (void*)done_})
@@ -504,7 +520,8 @@ gsm_status MultiGpu::phase(int p, hipStream_t s, const gsm_gaussian_input& in, c
                            size_t depthPitch, void* gatherColor) {
     if (p < 0 || p > 3) return GSM_ERR_INVALID_ARGUMENT;
     if (!connected_) return GSM_ERR_INVALID_ARGUMENT;  // no peers to stay in step with
-    if (p != nextPhase_) return GSM_ERR_INVALID_ARGUMENT;  // phases in order: nothing enqueued
+    // phases in order, nothing enqueued otherwise (a frame left unfinished: gsm_multigpu_finish_frame)
+    if (p != nextPhase_) return GSM_ERR_PHASE_ORDER;
     if (hipSetDevice(device_) != hipSuccess) return GSM_ERR_DEVICE_NOT_AVAILABLE;
     Targets t;
     gsm_status cst = check(in, width, height, color, colorPitch, depth, depthPitch, gatherColor, &t);
@@ -512,22 +529,51 @@ gsm_status MultiGpu::phase(int p, hipStream_t s, const gsm_gaussian_input& in, c
         ++frame_;
         frame_ &= kEpochMask;
         if (frame_ == 0) frame_ = 1;  // (epoch 0 is the flags' initial value)
+        par_ ^= 1u;
         frameErr_ = cst;
+        frameT_ = t;
     } else if (frameErr_ == GSM_OK) {
         frameErr_ = cst;  // (the same arguments as phase 0's for a caller that follows the protocol)
     }
+    return run(p, s, &in, &cam, width, height, t, colorPitch, depth, depthPitch, gatherColor);
+}
+
+gsm_status MultiGpu::finishFrame(hipStream_t s) {
+    if (!connected_) return GSM_ERR_INVALID_ARGUMENT;
+    if (nextPhase_ == 0) return GSM_OK;  // no frame pending
+    if (hipSetDevice(device_) != hipSuccess) return GSM_ERR_DEVICE_NOT_AVAILABLE;
+    gsm_status first = GSM_OK;
+    while (nextPhase_ != 0) {
+        const int p = nextPhase_;
+        // phase 1 needs no caller argument: the push runs when phase 0 published this rank's counts (the
+        // owners expect those records); from phase 2 on the frame is abandoned -- barrier steps only,
+        // a failed arrival at barrier 2 when gathering
+        if (p >= 2 && frameErr_ == GSM_OK) frameErr_ = GSM_ERR_RENDER_FAILED;
+        const gsm_status st = run(p, s, nullptr, nullptr, 0, 0, frameT_, 0, nullptr, 0, nullptr);
+        if (first == GSM_OK && p == 1) first = st;
+    }
+    return first;
+}
+
+gsm_status MultiGpu::run(int p, hipStream_t s, const gsm_gaussian_input* in, const gsm_camera_params* cam,
+                         uint32_t width, uint32_t height, Targets t, size_t colorPitch, void* depth,
+                         size_t depthPitch, void* gatherColor) {
     nextPhase_ = (p + 1) & 3;
     const uint32_t world = (uint32_t)world_, rank = (uint32_t)rank_;
-    const uint32_t par = frame_ & 1u;  // the frame's parity: count matrix, receive buffer, schedule set
+    const uint32_t par = par_;  // the frame's parity: count matrix, receive buffer, schedule set
     if (t.gather) {  // rank 0's gathered frames of this frame (two alternating ones when pipelined)
-        t.color = frameBuf(frame_);
-        t.depth = t.gatherDepth ? (void*)depthBuf(frame_) : nullptr;
+        t.color = frameBuf(par);
+        t.depth = t.gatherDepth ? (void*)depthBuf(par) : nullptr;
     }
     // pipelined: phases 0-1 on front_ after the caller's stream finished frame f - 2, phases 2-3 on the
     // caller's stream after this frame's phase 1
     const hipStream_t cs = s;
     if (pipelined_ && p <= 1) s = front_;
     if (pipelined_ && p == 0) hipStreamWaitEvent(front_, evEnd_[par], 0);
+    if (p == 0 && inputEvent_) {  // the caller's inputs of this frame are complete (gsm_multigpu_wait_event)
+        hipStreamWaitEvent(s, inputEvent_, 0);
+        inputEvent_ = nullptr;
+    }
     if (pipelined_ && p == 2) hipStreamWaitEvent(cs, evFront_[par], 0);
     SlabPeers recv = recs_;  // this frame's parity of every owner's receive buffer
     for (uint32_t q = 0; q < world; ++q)
@@ -553,20 +599,20 @@ gsm_status MultiGpu::phase(int p, hipStream_t s, const gsm_gaussian_input& in, c
         case 0: {
             if (frameErr_ == GSM_OK) {
                 // the rank's id range (gsm_amd.exchange.id_range)
-                const uint32_t N = in.gaussian_count;
+                const uint32_t N = in->gaussian_count;
                 const uint32_t perIds = (N + world - 1) / world;
                 const uint32_t first = rank * perIds < N ? rank * perIds : N;
                 const uint32_t cnt = perIds < N - first ? perIds : N - first;
                 CountPublish pub{};
                 for (uint32_t q = 0; q < world; ++q)
-                    pub.row[q] = sync_.ctl[q] + kCountsWord + (frame_ & 1u) * kMaxSlabs * kMaxSlabs + rank * world;
+                    pub.row[q] = sync_.ctl[q] + kCountsWord + par * kMaxSlabs * kMaxSlabs + rank * world;
                 pub.arrive = arrival(0);
                 // the slab's blend units are ordered inside this launch (the long kernel of the frame's
                 // first half), not in the short records-in launch of phase 2
                 if (mine && (st = setRows()) != GSM_OK) frameErr_ = st;
                 r_->selectSchedule(par);
                 if (frameErr_ == GSM_OK &&
-                    (st = r_->partitionCounts(s, in, cam, width, height, first, cnt, rows, world, sendCounts_, mine,
+                    (st = r_->partitionCounts(s, *in, *cam, width, height, first, cnt, rows, world, sendCounts_, mine,
                                               interleave_, &pub)) != GSM_OK)
                     frameErr_ = st;  // (refused before any launch)
             }
@@ -576,7 +622,7 @@ gsm_status MultiGpu::phase(int p, hipStream_t s, const gsm_gaussian_input& in, c
         case 1: {
             wait(s, 0);  // every rank's counts are in my matrix
             if (frameErr_ == GSM_OK) {
-                const uint32_t* counts = ctl() + kCountsWord + (frame_ & 1u) * kMaxSlabs * kMaxSlabs;
+                const uint32_t* counts = ctl() + kCountsWord + par * kMaxSlabs * kMaxSlabs;
                 if ((st = r_->partitionPush(s, world, rank, counts, recv, recvCount_ + par, arrival(1))) != GSM_OK)
                     frameErr_ = st;
             }
@@ -641,7 +687,7 @@ gsm_status MultiGpu::status(uint32_t* timeouts, uint32_t* peerErrors, bool clear
 
 gsm_status MultiGpu::counts(uint32_t* hostCounts) {
     hipSetDevice(device_);
-    const uint32_t* c = ctl() + kCountsWord + (frame_ & 1u) * kMaxSlabs * kMaxSlabs;
+    const uint32_t* c = ctl() + kCountsWord + par_ * kMaxSlabs * kMaxSlabs;
     if (hipMemcpy(hostCounts, c, (size_t)world_ * world_ * 4, hipMemcpyDeviceToHost) != hipSuccess)
         return GSM_ERR_RENDER_FAILED;
     return GSM_OK;
@@ -731,6 +777,16 @@ gsm_status gsm_multigpu_render_phase(gsm_multigpu* m, int phase, void* stream, c
     if (!m || !m->impl || !input || !camera) return GSM_ERR_INVALID_ARGUMENT;
     return m->impl->phase(phase, (hipStream_t)stream, *input, *camera, width, height, color, color_pitch_bytes, depth,
                           depth_pitch_bytes, gather_color);
+}
+
+gsm_status gsm_multigpu_finish_frame(gsm_multigpu* m, void* stream) {
+    if (!m || !m->impl) return GSM_ERR_INVALID_ARGUMENT;
+    return m->impl->finishFrame((hipStream_t)stream);
+}
+
+gsm_status gsm_multigpu_wait_event(gsm_multigpu* m, void* event) {
+    if (!m || !m->impl) return GSM_ERR_INVALID_ARGUMENT;
+    return m->impl->waitEvent((hipEvent_t)event);
 }
 
 gsm_status gsm_multigpu_render(gsm_multigpu* m, void* stream, const gsm_gaussian_input* input,

@@ -49,6 +49,7 @@ class Status(enum.IntEnum):
     MISSING_REQUIRED_BUFFER = 13
     INVALID_ARGUMENT = 14
     UNSUPPORTED = 15
+    PHASE_ORDER = 16
 
 
 class RendererError(RuntimeError):
@@ -256,6 +257,8 @@ _SIGNATURES = {
     "gsm_multigpu_debug_copy_depth": ([C.c_void_p, C.c_void_p, C.c_size_t, C.c_uint32, C.c_uint32], C.c_int),
     "gsm_multigpu_frame_depth": ([C.c_void_p, C.POINTER(C.c_void_p), C.POINTER(C.c_size_t)], C.c_int),
     "gsm_multigpu_errors": ([C.c_void_p, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.c_int], C.c_int),
+    "gsm_multigpu_finish_frame": ([C.c_void_p, C.c_void_p], C.c_int),
+    "gsm_multigpu_wait_event": ([C.c_void_p, C.c_void_p], C.c_int),
 }
 
 SPLAT_RECORD_BYTES = 48  # include/gsm_multigpu.h GSM_SPLAT_RECORD_BYTES
@@ -738,6 +741,18 @@ class MultiGpuRenderer:
                 first = (st, p)
         if first is not None:
             _check(first[0], f"gsm_multigpu_render_phase({first[1]})")
+
+    def finish_frame(self, stream=None):
+        """gsm_multigpu_finish_frame: the phases a caller left unfinished (barrier steps; the slab is
+        abandoned from phase 2 on), so the ranks stay in step; a no-op when no frame is pending."""
+        _check(_lib().gsm_multigpu_finish_frame(self._h, _stream_handle(stream)), "gsm_multigpu_finish_frame")
+
+    def wait_event(self, event):
+        """gsm_multigpu_wait_event: the next frame's projection (phase 0) waits for `event` (a
+        torch.cuda.Event recorded after the caller wrote this frame's gaussians / harmonics) -- needed
+        when pipelined (GSM_MG_PIPELINE=1), where phase 0 runs on the library's own stream."""
+        h = event.cuda_event if hasattr(event, "cuda_event") else int(event)
+        _check(_lib().gsm_multigpu_wait_event(self._h, C.c_void_p(h)), "gsm_multigpu_wait_event")
 
     def frame(self):
         """(device pointer, pitch bytes) of rank 0's gathered frame; (None, 0) elsewhere."""

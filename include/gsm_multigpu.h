@@ -175,8 +175,9 @@ gsm_status gsm_multigpu_debug_counts(gsm_multigpu *multigpu, uint32_t *host_coun
 
 /* gsm_multigpu_render in four phases (0: projection + counts + barrier; 1: records + barrier;
  * 2: slab render + the gather signal; 3: rank 0's gather wait + copy); render = phases 0..3, each
- * called even after an earlier phase of the frame returned an error (GSM_ERR_INVALID_ARGUMENT and
- * nothing enqueued for a phase out of order).
+ * called even after an earlier phase of the frame returned an error.  A phase called out of order
+ * returns GSM_ERR_PHASE_ORDER and enqueues nothing (r05; GSM_ERR_INVALID_ARGUMENT before): a caller
+ * that stopped part way through a frame calls gsm_multigpu_finish_frame before the next phase 0.
  * For W ranks driven from ONE host thread (virtual ranks of a test or a timing tool, e.g. W
  * renderers on one GPU sharing one stream): issue phase p of every rank before phase p + 1 of
  * any, so that every barrier waits only for work enqueued before it. */
@@ -185,6 +186,21 @@ gsm_status gsm_multigpu_render_phase(gsm_multigpu *multigpu, int phase, void *st
                                      uint32_t width, uint32_t height, void *color_rgba16f,
                                      size_t color_pitch_bytes, void *depth_r16f, size_t depth_pitch_bytes,
                                      void *gather_color);
+
+/* The phases a caller left unfinished in the current frame (r05): phase 1's record push
+ * still runs when phase 0 published this rank's counts (the owners expect the records); from phase 2
+ * on the frame is abandoned on this rank -- barrier steps only, its arrival at the gather barrier
+ * marked failed -- so every rank's epochs stay in step and the next frame renders normally.
+ * Enqueued on `stream`; GSM_OK and nothing enqueued when no frame is pending. */
+gsm_status gsm_multigpu_finish_frame(gsm_multigpu *multigpu, void *stream);
+
+/* Inputs written on another stream (r05): the next frame's phase 0 makes the stream its
+ * projection runs on wait for `event` (a hipEvent_t the caller recorded after writing that frame's
+ * gaussians / harmonics).  Pipelined (GSM_MG_PIPELINE=1) phases 0-1 run on the library's own stream,
+ * which is otherwise ordered only after the caller's stream finished frame f - 2: without this call
+ * the caller must not change the input buffers of a frame it has issued until that frame's phase 1
+ * completed.  One-shot (the next phase 0 consumes it); NULL clears it. */
+gsm_status gsm_multigpu_wait_event(gsm_multigpu *multigpu, void *event);
 
 #ifdef __cplusplus
 }

@@ -40,7 +40,8 @@ typedef enum {
     GSM_ERR_ENCODER_CREATION_FAILED = 12,    /* .encoderCreationFailed */
     GSM_ERR_MISSING_REQUIRED_BUFFER = 13,    /* .missingRequiredBuffer */
     GSM_ERR_INVALID_ARGUMENT = 14,           /* null handle / pointer (no Swift analogue) */
-    GSM_ERR_UNSUPPORTED = 15                 /* renderStereo on Global: fatalError in the reference */
+    GSM_ERR_UNSUPPORTED = 15,                /* renderStereo on Global: fatalError in the reference */
+    GSM_ERR_PHASE_ORDER = 16                 /* gsm_multigpu_render_phase out of order (gsm_multigpu.h) */
 } gsm_status;
 
 /* RenderPrecision (GaussianRendererProtocol.swift:4-7). */

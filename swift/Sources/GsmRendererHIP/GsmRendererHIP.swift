@@ -232,6 +232,7 @@ public enum RendererError: Error, Sendable, Equatable {
         case GSM_ERR_ENCODER_CREATION_FAILED: self = .encoderCreationFailed
         case GSM_ERR_MISSING_REQUIRED_BUFFER: self = .missingRequiredBuffer
         case GSM_ERR_UNSUPPORTED: self = .unsupported
+        case GSM_ERR_PHASE_ORDER: self = .invalidArgument
         default: self = .invalidArgument
         }
     }

@@ -257,3 +257,100 @@ def test_virtual_ranks_pipelined(gsm, cuda, oracle, monkeypatch, world, n, w, h,
         m.close()
     for r in rends:
         r.close()
+
+
+def test_virtual_ranks_pipelined_inputs_written_between_frames(gsm, cuda, oracle, monkeypatch):
+    """pipelined phases 0-1 run on the library's own stream, so a frame's projection is not
+    ordered after the caller's stream by itself.  The caller rewrites the one input buffer on its own
+    stream between frames (scenes A, B, A, B), records an event after each write and hands it to every
+    rank with gsm_multigpu_wait_event; every frame is bit-exact with the oracle of the scene written
+    for it."""
+    from gsm_amd import scenes
+    monkeypatch.setenv("GSM_MG_PIPELINE", "1")
+    world, n, w, h, sh, prec = 3, 40_000, 1280, 720, 16, 1
+    sc = [scenes.gen_scene(n, w, h, sh, prec, seed=s) for s in (91, 92)]
+    srcw = [cuda.from_numpy(x[0].view(np.uint8).reshape(-1).copy()).cuda() for x in sc]
+    srch = [cuda.from_numpy(x[1].view(np.uint8).reshape(-1).copy()).cuda() for x in sc]
+    wt, ht = cuda.empty_like(srcw[0]), cuda.empty_like(srch[0])
+    inp = gsm.GaussianInput(wt, ht, n, sh)
+    cfg = gsm.RendererConfig(max_gaussians=n, max_width=w, max_height=h, precision=prec, gaussian_color_space=0)
+    rends = [gsm.GlobalRenderer(device=0, config=cfg) for _ in range(world)]
+    pre = [gsm.MultiGpuRenderer.prepare(r, k, world) for k, r in enumerate(rends)]
+    mgs = [m.connect_handles([hd for _, hd in pre]) for m, _ in pre]
+    stream = cuda.cuda.current_stream()
+    order = [0, 1, 0, 1]
+    cam = sc[0][2]
+    cp = gsm.CameraParams.from_dict(cam)
+    colors = [cuda.full((h, w, 4), float("nan"), dtype=cuda.float16, device="cuda") for _ in order]
+    evs = []
+    for f, s in enumerate(order):
+        wt.copy_(srcw[s])  # on the caller's stream, after frame f - 1's phases were issued
+        ht.copy_(srch[s])
+        ev = cuda.cuda.Event()
+        ev.record(stream)
+        evs.append(ev)
+        for m in mgs:
+            m.wait_event(ev)
+        for ph in range(4):
+            for k, m in enumerate(mgs):
+                m.render_phases([ph], colors[f] if k == 0 else None, None, inp, cp, w, h, gather=True, stream=stream,
+                                gather_depth=False)
+    cuda.cuda.synchronize()
+    assert [m.status() for m in mgs] == [0] * world
+    refs = [oracle.render(sc[s][0], sc[s][1], sh, cam, w, h, max_gaussians=n) for s in (0, 1)]
+    for f, s in enumerate(order):
+        got = colors[f].view(cuda.int16).cpu().numpy().view(np.uint16)
+        bad = np.nonzero(np.any(got != refs[s]["color"], axis=(1, 2)))[0]
+        assert len(bad) == 0, f"frame {f} (scene {s}): {len(bad)} rows differ, first {bad[:16].tolist()}"
+    for m in mgs:
+        m.close()
+    for r in rends:
+        r.close()
+
+
+def test_virtual_ranks_phase_order_and_finish_frame(gsm, cuda, oracle):
+    """a phase out of order returns GSM_ERR_PHASE_ORDER (nothing enqueued); a caller that
+    stopped after phase 1 calls gsm_multigpu_finish_frame (barrier steps, the slabs abandoned with
+    failed arrivals at the gather barrier), and the next frame renders bit-exact with no timeout."""
+    from gsm_amd import scenes
+    world, n, w, h, sh, prec = 2, 30_000, 640, 360, 16, 1
+    world_np, harm_np, cam = scenes.gen_scene(n, w, h, sh, prec, seed=17)
+    wt = cuda.from_numpy(world_np.view(np.uint8).reshape(-1).copy()).cuda()
+    ht = cuda.from_numpy(harm_np.view(np.uint8).reshape(-1).copy()).cuda()
+    inp = gsm.GaussianInput(wt, ht, n, sh)
+    cfg = gsm.RendererConfig(max_gaussians=n, max_width=w, max_height=h, precision=prec, gaussian_color_space=0)
+    rends = [gsm.GlobalRenderer(device=0, config=cfg) for _ in range(world)]
+    pre = [gsm.MultiGpuRenderer.prepare(r, k, world) for k, r in enumerate(rends)]
+    mgs = [m.connect_handles([hd for _, hd in pre]) for m, _ in pre]
+    frame_ptr, _ = mgs[0].frame()
+    stream = cuda.cuda.current_stream()
+    cp = gsm.CameraParams.from_dict(cam)
+
+    def phases(phs, k):
+        mgs[k].render_phases(phs, None, None, inp, cp, w, h, gather=True, stream=stream,
+                             gather_target=frame_ptr if k == 0 else None, gather_depth=False)
+
+    for ph in (0, 1):
+        for k in range(world):
+            phases([ph], k)
+    with pytest.raises(gsm.RendererError) as e:  # phase 0 while phase 2 is pending
+        phases([0], 0)
+    assert e.value.status == gsm.Status.PHASE_ORDER
+    # one stream for both ranks: rank 1's remaining steps (its failed gather arrival) before rank 0's
+    # gather wait
+    mgs[1].finish_frame(stream)
+    mgs[0].finish_frame(stream)
+    mgs[0].finish_frame(stream)  # nothing pending: a no-op
+    for ph in range(4):
+        for k in range(world):
+            phases([ph], k)
+    cuda.cuda.synchronize()
+    ref = oracle.render(world_np, harm_np, sh, cam, w, h, max_gaussians=n)
+    assert np.array_equal(mgs[0].copy_frame(w, h), ref["color"])
+    errs = [m.errors() for m in mgs]
+    assert all(t == 0 for t, _ in errs), errs
+    assert errs[0][1] >= 1  # rank 1's abandoned slab arrived failed at rank 0's gather barrier
+    for m in mgs:
+        m.close()
+    for r in rends:
+        r.close()

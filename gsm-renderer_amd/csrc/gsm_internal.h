@@ -22,6 +22,9 @@ struct ProjectArgs {
     uint32_t keepRenderData;  // write GaussianRenderData of every visible gaussian (debug readback);
                               // otherwise only where the scatter needs it (rects over kMaskTiles tiles)
     uint32_t schedUnits;      // > 0: the projection launch also orders this many blend units
+    uint32_t pairBucket;      // the pair-walk blend (k_blend_pw): units of the schedule's walk buckets below this
+                              // one (walk > (256 - pairBucket) / 256 of the longest) run alone, the rest in pairs;
+                              // the split position goes to costMax[kCostMaxSlots] (0: not written)
                               // (unit_order_block in one extra workgroup, block 0)
     // per-frame constants of projectCovariance2D / stabilizeCovariance2D / computeDepthFactor,
     // evaluated once on the host with the same IEEE fp32 operations the kernels would repeat
@@ -214,6 +217,10 @@ struct Tuning {
                               // runs (0: one workgroup per 256-id block)
     bool wide12 = false;      // GSM_SORT_WIDE12=1: a 12-bit tile field (2049..4096 tiles) in one 12-bit
                               // wide pass instead of two narrow passes (measured slower: DESIGN.md 4)
+    bool blendPairs = true;   // half-tile frames on one GPU: two units per blend wave (k_blend_pw, r05);
+                              // GSM_BLEND_PAIRS=0: one unit per wave (k_blend_px)
+    int pairBucket = 128;     // GSM_BLEND_PAIR_SPLIT=b (0..256): the units whose last walk exceeds (256 - b) / 256
+                              // of the longest run alone, the others in pairs (ProjectArgs::pairBucket)
     bool fusedScan = true;    // frames of <= kFusedScanMaxBlocks projection blocks: every scatter workgroup
                               // sums the block counts before its own (no k_scan_blocks launch);
                               // GSM_SCAN_FUSED=0: the separate scan
@@ -296,7 +303,10 @@ void launch_headers(const uint32_t* sortedKeys, const FrameGeometry& geo, const 
 void launch_blend(const FrameGeometry& geo, const DeviceArena& A,
                   void* color, size_t colorPitch, void* depth, size_t depthPitch, int numCUs,
                   bool costOrder, int colorFormat, hipStream_t stream, int waves = 0, int claim = 1,
-                  const MgArrive* arrive = nullptr, bool arriveWB = false);
+                  const MgArrive* arrive = nullptr, bool arriveWB = false, bool pairs = false);
+// k_blend_pw (gsm_blend_pw.hip): two half-tile units per wave, one GPU's frame
+void launch_blend_pw(const FrameGeometry& g, const DeviceArena& A, void* color, size_t colorPitch, void* depth,
+                     size_t depthPitch, int numCUs, bool costOrder, int colorFormat, hipStream_t s, int waves);
 // blend kernel shape: pixel pairs per lane (0 = quadrant kernel) and blend units per tile
 int blend_pairs_per_lane(uint32_t numTiles, int numCUs);
 uint32_t blend_units_per_tile(uint32_t numTiles, int numCUs);
@@ -346,10 +356,11 @@ constexpr uint32_t kUoBuckets = 256;
 // average gap between a wave's units at 4K was 7.7 us of queueing).
 constexpr uint32_t kQueueStripes = 8, kQueueStride = 16;
 constexpr uint32_t kCostMaxSlots = 64;  // words of the longest-walk maximum (spread atomics)
+// (+ 1 word after them in the Global renderer's schedule sets: the pair walk's split position)
 template <int NT>
 __device__ __forceinline__ void unit_order_block(const uint16_t* __restrict__ cost, uint32_t* __restrict__ order,
                                                  uint32_t n, uint32_t* base, uint32_t* wmax,
-                                                 uint32_t* __restrict__ costMax) {
+                                                 uint32_t* __restrict__ costMax, uint32_t splitBucket = 0) {
     static_assert(NT >= (int)kUoBuckets && NT % 64 == 0, "one thread per bucket");
     constexpr uint32_t UN = 8;
     const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
@@ -392,6 +403,9 @@ __device__ __forceinline__ void unit_order_block(const uint16_t* __restrict__ co
         *(uint4*)(base + lane * 4u) = make_uint4(e, e + c.x, e + c.x + c.y, e + c.x + c.y + c.z);
     }
     __syncthreads();
+    // the pair walk's split: the units of buckets [0, splitBucket) -- the longest walks -- run alone
+    if (splitBucket && t == 0) costMax[kCostMaxSlots] = splitBucket >= kUoBuckets ? n : base[splitBucket];
+
     for (uint32_t b0 = 0; b0 < n; b0 += (uint32_t)NT * UN) {
         uint32_t c[UN];
         load(b0, c);

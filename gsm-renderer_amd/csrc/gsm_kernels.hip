@@ -276,7 +276,7 @@ __global__ __launch_bounds__(kProjectBlock) void k_project(
     if (P.schedUnits) {
         if (blockIdx.x == 0) {
             __shared__ uint32_t uoBase[kUoBuckets], uoMax[kProjectBlock / 64];
-            unit_order_block<kProjectBlock>(unitCost, unitOrder, P.schedUnits, uoBase, uoMax, costMax);
+            unit_order_block<kProjectBlock>(unitCost, unitOrder, P.schedUnits, uoBase, uoMax, costMax, P.pairBucket);
             return;
         }
     }
@@ -491,7 +491,7 @@ __global__ __launch_bounds__(kProjectBlock) void k_project_part(
     if (P.schedUnits) {
         if (blockIdx.x == 0) {
             __shared__ uint32_t uoBase[kUoBuckets], uoMax[kProjectBlock / 64];
-            unit_order_block<kProjectBlock>(unitCost, unitOrder, P.schedUnits, uoBase, uoMax, costMax);
+            unit_order_block<kProjectBlock>(unitCost, unitOrder, P.schedUnits, uoBase, uoMax, costMax, P.pairBucket);
             return;
         }
     }
@@ -712,7 +712,7 @@ __global__ __launch_bounds__(kProjectBlock) void k_records_in(
     if (P.schedUnits) {
         if (blockIdx.x == 0) {
             __shared__ uint32_t uoBase[kUoBuckets], uoMax[kProjectBlock / 64];
-            unit_order_block<kProjectBlock>(unitCost, unitOrder, P.schedUnits, uoBase, uoMax, costMax);
+            unit_order_block<kProjectBlock>(unitCost, unitOrder, P.schedUnits, uoBase, uoMax, costMax, P.pairBucket);
             return;
         }
     }

@@ -1351,6 +1351,10 @@ Tuning tuning_from_env(int device) {
     t.mgPushPerCU = mpg ? atoi(mpg) : 4;
     const char* w12 = getenv("GSM_SORT_WIDE12");
     t.wide12 = w12 && w12[0] == '1';
+    const char* bp = getenv("GSM_BLEND_PAIRS");
+    t.blendPairs = !(bp && bp[0] == '0');
+    const char* ps = getenv("GSM_BLEND_PAIR_SPLIT");
+    if (ps) t.pairBucket = std::min(256, std::max(0, atoi(ps)));
     const char* fs = getenv("GSM_SCAN_FUSED");
     t.fusedScan = !(fs && fs[0] == '0');
     return t;

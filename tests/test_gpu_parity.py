@@ -428,6 +428,32 @@ def test_create_time_switches_frames_match(gsm, cuda, oracle, monkeypatch, env):
     g["renderer"].close()
 
 
+@pytest.mark.parametrize("env", [{"GSM_BLEND_WAVES": "16"}, {"GSM_BLEND_WAVES": "16", "GSM_BLEND_PAIR_SPLIT": "1"},
+                                 {"GSM_BLEND_WAVES": "16", "GSM_BLEND_PAIR_SPLIT": "256"},
+                                 {"GSM_BLEND_WAVES": "16", "GSM_BLEND_PAIR_SPLIT": "200"},
+                                 {"GSM_BLEND_WAVES": "16", "GSM_BLEND_SCHED": "0"},
+                                 {"GSM_BLEND_WAVES": "16", "GSM_BLEND_PAIRS": "0"}])
+def test_pair_walk_blend_frames_match(gsm, cuda, oracle, monkeypatch, env):
+    """The pair-walk blend (k_blend_pw, r05): a 1080p frame of half-tile units at 16 waves per workgroup
+    -- two units per wave in the 8- / 4- / 2-pixels-per-lane layouts, single units beside them (the
+    schedule's split: 1 = almost all units paired, 256 = none, 200 = most alone), with and without the
+    schedule, and one unit per wave (GSM_BLEND_PAIRS=0) -- renders the oracle's frame bit for bit, first
+    and later frames (later ones are paired by last frame's walks)."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    case = _synth(300_000, 1920, 1080, 4, 1, 35)
+    r = oracle_render(oracle, case)
+    g = gpu_render(gsm, cuda, case, keep=False)
+    for k in env:
+        monkeypatch.delenv(k)
+    assert_frame_equal(g, r)
+    for _ in range(3):
+        g2 = gpu_render(gsm, cuda, case, renderer=g["renderer"], keep=False)
+        assert np.array_equal(g["color"], g2["color"])
+        assert np.array_equal(g["depth"], g2["depth"])
+    g["renderer"].close()
+
+
 @pytest.mark.parametrize("cfg_name,precision", [
     ("cfg2_1m_sh3_1080p_f16", None),
     # the same 1M / SH3 / 1080p frame from PackedWorldGaussian (48 B) + fp32 SH
@@ -472,11 +498,16 @@ def test_1080p_tile_field_one_12bit_pass(gsm, cuda, oracle, monkeypatch, wide12,
     g["renderer"].close()
 
 
-@pytest.mark.parametrize("fmt", [1, 2, 3, 4, 5])
-def test_color_formats(gsm, cuda, oracle, fmt):
+@pytest.mark.parametrize("fmt,pairs", [(1, False), (2, False), (3, False), (4, False), (5, False),
+                                      (1, True), (3, True), (5, True)])
+def test_color_formats(gsm, cuda, oracle, monkeypatch, fmt, pairs):
     """The colour target in every gsm_color_format equals the oracle's rgba16f frame converted by
-    the declared rules (include/gsm_renderer.h; oracle.convert_color); depth stays r16f."""
-    case = _synth(20000, 320, 180, 9, 1, 21)
+    the declared rules (include/gsm_renderer.h; oracle.convert_color); depth stays r16f.  pairs: the
+    pair-walk blend's own pixel writes (k_blend_pw: a 1080p frame of half-tile units at 16 waves per
+    workgroup)."""
+    if pairs:
+        monkeypatch.setenv("GSM_BLEND_WAVES", "16")
+    case = _synth(60000, 1920, 1080, 4, 1, 21) if pairs else _synth(20000, 320, 180, 9, 1, 21)
     w, h = case["width"], case["height"]
     ref = oracle_render(oracle, case)
     want = oracle.convert_color(ref["color"], fmt)

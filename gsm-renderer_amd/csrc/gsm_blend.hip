@@ -309,16 +309,6 @@ __global__ __launch_bounds__(NT) void k_blend_px(
         uint32_t ncomp = 0;  // entry at which the unit moved to one pair per lane (trace only)
 #if GSM_BLEND_ZSTATS
         uint32_t zeroEntries = 0, alivePx = 0;  // (statistics build: entries no live pixel takes, live pixels)
-        // GSM_BLEND_ZSTATS == 2: the first entry after which at most kThr[i] groups are alive (10 bits each)
-        constexpr uint32_t kThr[11] = {30, 28, 24, 20, 16, 12, 8, 6, 4, 2, 0};
-        uint32_t thrE[11];
-#pragma unroll
-        for (int i = 0; i < 11; ++i) thrE[i] = 1023u;
-        auto curve = [&](uint32_t groupsAlive, uint32_t e) {
-#pragma unroll
-            for (int i = 0; i < 11; ++i)
-                if (thrE[i] == 1023u && groupsAlive <= kThr[i]) thrE[i] = min(e, 1022u);
-        };
 #endif
         uint32_t nextQ = 0;
         bool claimed = false;
@@ -477,7 +467,6 @@ __global__ __launch_bounds__(NT) void k_blend_px(
                                 zeroEntries += __ballot(alive && nz != 0) == 0 ? 1u : 0u;
                                 alivePx += (uint32_t)__popcll(__ballot(alive)) * (2u * P);
                             }
-                            curve((uint32_t)__popcll(__ballot(alive) & (P == 2 ? 0x5555555555555555ull : 0x1111111111111111ull)), g1s + k);
                         }
 #endif
                         const h2 rgv = as_h2(rgc[k]), bdv = as_h2(bdc[k]);
@@ -683,7 +672,6 @@ __global__ __launch_bounds__(NT) void k_blend_px(
                             zeroEntries += __ballot(alive1 && as_u32(ac1[k]) != 0) == 0 ? 1u : 0u;
                             alivePx += (uint32_t)__popcll(__ballot(alive1)) * 2u;
                         }
-                        curve((uint32_t)__popcll(__ballot(alive1) & 0x1111111111111111ull), e + k);
 #endif
                         if (alive1) {
                             const h2 rgv = as_h2(rgc1[k]), bdv = as_h2(bdc1[k]);
@@ -761,18 +749,7 @@ __global__ __launch_bounds__(NT) void k_blend_px(
             t[1] = __builtin_amdgcn_s_memrealtime();
             t[2] = ((unsigned long long)count << 32) | nproc;
             const unsigned long long xcc = (unsigned long long)__builtin_amdgcn_s_getreg(20 | (3 << 11));  // XCC_ID
-#if GSM_BLEND_ZSTATS == 2
-            {
-                unsigned long long lo = 0, hi = 0;
-#pragma unroll
-                for (int i = 0; i < 6; ++i) lo |= (unsigned long long)thrE[i] << (10 * i);
-#pragma unroll
-                for (int i = 6; i < 11; ++i) hi |= (unsigned long long)thrE[i] << (10 * (i - 6));
-                t[0] = lo;
-                t[3] = hi | ((unsigned long long)min(ncomp, 1023u) << 50);
-            }
-            if (false)
-#elif GSM_BLEND_ZSTATS
+#if GSM_BLEND_ZSTATS
             t[0] = ((unsigned long long)ncomp << 48) | (tStart & 0xFFFFFFFFFFFFull);
             t[3] = ((unsigned long long)alivePx << 32) | zeroEntries;
             if (false)

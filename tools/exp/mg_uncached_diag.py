@@ -74,11 +74,17 @@ def run(kind, gather, world, n, w, h, sh, prec, cams, seed=78):
                 y0, y1 = min(h, k * per * 16), min(h, (k + 1) * per * 16)
                 pix[y0:y1] = own[k][y0:y1].view(torch.int16).cpu().numpy().view(np.uint16)
         out.append({"ex": ex, "pix": pix, "timeouts": [m.status() for m in mgs]})
-    for m in mgs:
-        m.close()
-    for r in rends:
-        r.close()
+    if os.environ.get("DIAG_KEEP") == "1":  # keep every allocation alive: no virtual address is reused
+        KEEP.append((mgs, rends, wt, ht, own))
+    else:
+        for m in mgs:
+            m.close()
+        for r in rends:
+            r.close()
     return out
+
+
+KEEP = []
 
 
 def counts_of(ex, par, world):
@@ -130,20 +136,44 @@ def compare(label, ref, got, refs_img, world, n, h):
 
 
 def main():
-    rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 3
+    """usage: mg_uncached_diag.py ROUNDS KINDS OUT  -- KINDS: comma list of fine | uc | uc_own run in this
+    order in ONE process (each run a fresh set of renderers and exchange allocations); every frame's
+    counts, received records and pixels are saved to OUT (npz) and its pixels compared with the oracle."""
+    rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 2
+    kinds = (sys.argv[2] if len(sys.argv) > 2 else "fine,uc,uc_own").split(",")
+    outp = sys.argv[3] if len(sys.argv) > 3 else None
     O.build()
     cases = [(8, 50_000, 640, 360, 0), (3, 60_000, 1280, 720, 1)]
+    spec = {"fine": ("fine", True), "uc": ("uncached-ab", True), "uc_own": ("uncached-ab", False)}
+    save = {}
+    refs = {}
     for it in range(rounds):
         for world, n, w, h, prec in cases:
             sh = 16 if prec else 4
             cams = [scenes.make_camera(w, h), scenes.orbit_camera(w, h, 5.0)]
-            wn, hn, _ = scenes.gen_scene(n, w, h, sh, prec, seed=78)
-            refs = [O.render(wn, hn, sh, c, w, h, max_gaussians=n)["color"] for c in cams]
-            fine = run("fine", True, world, n, w, h, sh, prec, cams)
-            for label, kind, gather in (("fine", "fine", True), ("uc", "uncached-ab", True), ("uc_own", "uncached-ab", False)):
-                got = fine if label == "fine" else run(kind, gather, world, n, w, h, sh, prec, cams)
-                for line in compare(label, fine, got, refs, world, n, h):
-                    print(it, (world, n, w, h, prec), line, flush=True)
+            key = (world, n, w, h, prec)
+            if key not in refs:
+                wn, hn, _ = scenes.gen_scene(n, w, h, sh, prec, seed=78)
+                refs[key] = [O.render(wn, hn, sh, c, w, h, max_gaussians=n)["color"] for c in cams]
+            for label in kinds:
+                kind, gather = spec[label]
+                got = run(kind, gather, world, n, w, h, sh, prec, cams)
+                for f, fr in enumerate(got):
+                    par = 1 if f % 2 == 0 else 0
+                    bad = np.nonzero(np.any(fr["pix"] != refs[key][f], axis=(1, 2)))[0]
+                    cts = [counts_of(x, par, world) for x in fr["ex"]]
+                    consistent = all(np.array_equal(cts[0], c) for c in cts)
+                    print(it, key, label, "frame", f, "timeouts", sum(fr["timeouts"]), "bad rows", len(bad),
+                          (f"{bad.min()}-{bad.max()}" if len(bad) else ""), "count matrices equal on all ranks", consistent,
+                          flush=True)
+                    tag = f"{it}_{world}_{label}_{f}"
+                    save[tag + "_counts"] = np.stack(cts)
+                    save[tag + "_pix"] = fr["pix"]
+                    for r in range(world):
+                        nrec = int(cts[0][:, r].sum())
+                        save[tag + f"_rec{r}"] = records_of(fr["ex"][r], par, n, nrec).copy()
+    if outp:
+        np.savez_compressed(outp, **save)
 
 
 if __name__ == "__main__":

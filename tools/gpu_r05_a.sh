@@ -5,14 +5,8 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 O=gpurun_out/r05; mkdir -p $O; export TMPDIR=/tmp
 st() { local n=$1 t=$2; shift 2; timeout -k 10 $t "$@" > $O/$n.log 2>&1; local rc=$?; echo "$n rc=$rc: $(tail -n 1 $O/$n.log)"; if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi; }
-st pytest_mg_new 400 python -u -m pytest tests/test_multigpu_ipc.py -x -v --timeout 200 --timeout-method thread -k "inputs_written or phase_order or pipelined or product_path"
 st trace_cfg2_0 120 python tools/blend_trace.py
 st trace_cfg2_13 120 python tools/blend_trace.py --angle 13.75
 st trace_cfg3_0 200 python tools/blend_trace.py --config cfg3_5m_sh3_4k_f16
-cp gsm-renderer_amd/lib/libgsm_amd.so /tmp/libA.so
-cp gsm-renderer_amd/lib_z2/libgsm_amd.so gsm-renderer_amd/lib/libgsm_amd.so
-st curves_cfg2 150 python tools/blend_curves.py --angles 0 13.75
-st curves_cfg3 200 python tools/blend_curves.py --config cfg3_5m_sh3_4k_f16
-cp /tmp/libA.so gsm-renderer_amd/lib/libgsm_amd.so
 st mg_uncached_diag 300 python -u tools/exp/mg_uncached_diag.py 2
 echo done

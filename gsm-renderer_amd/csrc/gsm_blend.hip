@@ -8,7 +8,9 @@
 // every list entry.  Numeric contract: DESIGN.md.
 #include <hip/hip_runtime.h>
 
+#include <cstdio>
 #include <cstdlib>
+#include <cstring>
 
 #include "../../include/gsm_renderer.h"
 #include "gsm_detmath.h"
@@ -121,7 +123,7 @@ __global__ __launch_bounds__(NT) void k_blend_px(
     const uint32_t* __restrict__ order, uint16_t* __restrict__ unitCost,
     unsigned long long* __restrict__ trace, const uint32_t* __restrict__ half0,
     const uint32_t* __restrict__ half1, const uint32_t* __restrict__ halfCount, uint32_t tileCount,
-    uint32_t* __restrict__ costMax, uint32_t rowBegin, uint32_t rowStride, MgArrive arrive) {
+    uint32_t* __restrict__ costMax, uint32_t rowBegin, uint32_t rowStride, MgArrive arrive, float4 prioFrac) {
     static_assert(P == 1 || P == 2, "pairs per lane: quadrant or half-tile units (half-tile lists)");
     static_assert(!COMPACT || P == 2, "compaction: half tiles");
     constexpr uint32_t U = 4 / P;  // entries per pipeline group
@@ -131,6 +133,17 @@ __global__ __launch_bounds__(NT) void k_blend_px(
     constexpr uint32_t NW = NT / 64;
     constexpr uint32_t UNROLL = NG;
     const bool agePrio = (flags & 2) != 0;
+    // flags bit 12 (GSM_BLEND_PRIO=lrpt): priority by the unit's predicted REMAINING walk (last frame's
+    // walk minus the entries done), levels at prioT[0..2] x the longest walk of last frame -- longest
+    // remaining processing time first; otherwise the age priority below
+    const bool lrpt = (flags & 8192) != 0 && unitCost != nullptr;
+    uint32_t prioT3 = 0, prioT2 = 0, prioT1 = 0;
+    if (lrpt) {
+        const uint32_t M = __builtin_amdgcn_readfirstlane(costMax[kCostMaxSlots + 1]);
+        prioT3 = (uint32_t)((float)M * prioFrac.x);
+        prioT2 = (uint32_t)((float)M * prioFrac.y);
+        prioT1 = (uint32_t)((float)M * prioFrac.z);
+    }
     __shared__ __attribute__((aligned(16))) uint16_t tbl[65536];
     __shared__ uint32_t cscr[NW][16];  // compaction: the alive groups of each wave, in order
     __shared__ __attribute__((aligned(16))) uint4 lrecA[NW][64];  // current batch records
@@ -313,7 +326,15 @@ __global__ __launch_bounds__(NT) void k_blend_px(
         uint32_t nextQ = 0;
         bool claimed = false;
         // claimMode 2: the walk this unit made last frame (before this frame's walk overwrites it)
-        const uint32_t expWalk = (claimMode == 2 && unitCost) ? __builtin_amdgcn_readfirstlane((uint32_t)unitCost[u]) : 0u;
+        const uint32_t expWalk = ((claimMode == 2 || lrpt) && unitCost) ? __builtin_amdgcn_readfirstlane((uint32_t)unitCost[u]) : 0u;
+        auto lrptPrio = [&](uint32_t done) {  // (flags bit 12)
+            const uint32_t rem = expWalk > done ? expWalk - done : 0u;
+            if (rem >= prioT3) __builtin_amdgcn_s_setprio(3);
+            else if (rem >= prioT2) __builtin_amdgcn_s_setprio(2);
+            else if (rem >= prioT1) __builtin_amdgcn_s_setprio(1);
+            else __builtin_amdgcn_s_setprio(0);
+        };
+        if (lrpt) lrptPrio(0u);
         auto claim = [&]() {
             if (!claimed) {
                 if (lane == 0) nextQ = atomicAdd(myQueue, 1u);
@@ -516,7 +537,9 @@ __global__ __launch_bounds__(NT) void k_blend_px(
                         bdc[k] = bdn[k];
                     }
                 }
-                if (topPrio) {
+                if (lrpt) {
+                    lrptPrio(b0 + 64u);
+                } else if (topPrio) {
                     if (b0 == 0) __builtin_amdgcn_s_setprio(3);
                 } else if (agePrio) {
                     if (b0 == 0) __builtin_amdgcn_s_setprio(1);
@@ -702,6 +725,7 @@ __global__ __launch_bounds__(NT) void k_blend_px(
                     if (e - bb == 64u) {
                         rotate(bb);
                         bb += 64u;
+                        if (lrpt) lrptPrio(e);
                     }
                 }
                 nproc = e;
@@ -757,7 +781,7 @@ __global__ __launch_bounds__(NT) void k_blend_px(
             t[3] = (xcc << 48) | ((unsigned long long)(ncomp & 0xFFFFu) << 32) |
                    (unsigned long long)__builtin_amdgcn_s_getreg(4 | (31 << 11));
         }
-        if (agePrio || topPrio) __builtin_amdgcn_s_setprio(0);
+        if (agePrio || topPrio || lrpt) __builtin_amdgcn_s_setprio(0);
         topPrio = false;
         claim();  // (no-op when claimed during the walk)
         qi = gridWaves + stripe + stripes * __builtin_amdgcn_readfirstlane(nextQ);
@@ -828,7 +852,17 @@ void launch_blend(const FrameGeometry& g, const DeviceArena& A, void* color,
                      (depth == nullptr || ((((uintptr_t)depth) & 7u) == 0 && (depthPitch & 7u) == 0)))
                         ? 1
                         : 0;
+    // GSM_BLEND_PRIO=lrpt[:a,b,c] (A/B): remaining-walk priorities at a / b / c of the longest walk
+    static const char* pv = getenv("GSM_BLEND_PRIO");
+    static const bool lrptMode = pv && !strncmp(pv, "lrpt", 4);
+    static float4 prioFrac = [] {
+        float4 f = make_float4(0.6f, 0.35f, 0.15f, 0.0f);
+        const char* p = getenv("GSM_BLEND_PRIO");
+        if (p && p[0] && p[4] == ':') sscanf(p + 5, "%f,%f,%f", &f.x, &f.y, &f.z);
+        return f;
+    }();
     const int flags = vec | 2 | (costOrder ? 4 : 0) | ((colorFormat & 15) << 4) | ((claim & 3) << 8) |
+                      ((lrptMode && costOrder) ? 8192 : 0) |
                       (arrive ? (arriveWB ? 4096 : 1024) : 0) |  // (a gathered multi-GPU frame: write-through
                                                                  // pixel stores, or the L2 write-back at exit)
                       ((depth && (((uintptr_t)depth) & 15u) == 0 && (depthPitch & 15u) == 0) ? 2048 : 0);
@@ -839,7 +873,8 @@ void launch_blend(const FrameGeometry& g, const DeviceArena& A, void* color,
     // per wave (r05, k_blend_pw).  The pairs cut the VALU work (-10 %) but halve the waves walking: a gain
     // where the walk is VALU-bound (config 3: blend 370 -> 327 us), a loss where it is bound by its
     // longest units and latency (config 2: 121 -> 129-147 us at every split tried).
-    if (pairs && P == 2 && !arrive && waves == 16) {
+    static const bool forcePairs = getenv("GSM_BLEND_PAIRS") && getenv("GSM_BLEND_PAIRS")[0] == '2';  // (A/B)
+    if (pairs && P == 2 && !arrive && (waves == 16 || forcePairs)) {
         launch_blend_pw(g, A, color, colorPitch, depth, depthPitch, numCUs, costOrder, colorFormat, s, waves);
         return;
     }
@@ -857,7 +892,7 @@ void launch_blend(const FrameGeometry& g, const DeviceArena& A, void* color,
                        A.expTable, A.tileQueue, t0, numTiles, g.tilesX, g.width, g.height,          \
                        (uint8_t*)color, colorPitch, (uint8_t*)depth, depthPitch, flags, order, A.unitCost,  \
                        A.blendTrace, A.halfVals[0], A.halfVals[1], A.halfCount, g.tileCount, A.costMax, \
-                       g.rowBegin, g.rowStride, ar)
+                       g.rowBegin, g.rowStride, ar, prioFrac)
     // half tiles compact to one pair per lane once <= 16 of their 32 groups are alive
     if (P == 1) {
         if (waves == 16) GSM_LAUNCH_BLEND(1024, 1, false);

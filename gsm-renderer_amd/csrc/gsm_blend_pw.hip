@@ -18,6 +18,7 @@
 // longest job is no longer than before.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
 #include <type_traits>
 
 #include "../../include/gsm_renderer.h"
@@ -137,7 +138,7 @@ __global__ __launch_bounds__(NT) void k_blend_pw(
     PwTarget tg, const uint32_t* __restrict__ order, uint16_t* __restrict__ unitCost,
     unsigned long long* __restrict__ trace, const uint32_t* __restrict__ half0, const uint32_t* __restrict__ half1,
     const uint32_t* __restrict__ halfCount, uint32_t tileCount, uint32_t* __restrict__ costMax, uint32_t rowBegin,
-    uint32_t rowStride, int flags) {
+    uint32_t rowStride, int flags, uint32_t tailSingles, int staticSingles) {
     constexpr uint32_t NW = NT / 64;
     constexpr uint32_t NTOP = 4;  // one top-priority single unit per SIMD (the schedule's longest)
     static_assert(NW > NTOP, "pairs need waves beyond the top-priority ones");
@@ -170,14 +171,27 @@ __global__ __launch_bounds__(NT) void k_blend_pw(
     // first job of every wave is static -- with the schedule on, waves 0-3 of each workgroup (one per SIMD)
     // take jobs 0 .. 4 gridDim.x - 1 at top priority -- then jobs come from the striped queue (claimed
     // after a job ends).
-    const uint32_t NS = order ? min(__builtin_amdgcn_readfirstlane(costMax[kCostMaxSlots]), numUnits) : 0u;
     const uint32_t gridWaves = gridDim.x * NW;
+    uint32_t NS = order ? min(__builtin_amdgcn_readfirstlane(costMax[kCostMaxSlots]), numUnits) : 0u;
+    if (staticSingles) NS = min(max(NS, gridWaves), numUnits);  // (A/B: every wave's first job alone)
+    // (A/B: the last tailSingles positions -- the shortest walks -- alone again)
+    const uint32_t PE = max(NS, numUnits > tailSingles ? numUnits - tailSingles : 0u);
+    const uint32_t NPJ = (PE - NS + 1u) / 2u;
     uint32_t job = !split ? blockIdx.x * NW + wv
                           : (wv < NTOP ? blockIdx.x * NTOP + wv : gridDim.x * NTOP + blockIdx.x * (NW - NTOP) + (wv - NTOP));
     bool topPrio = split && wv < NTOP;
     auto jobPos = [&](uint32_t J, bool& single) {
-        single = J < NS;
-        return single ? J : NS + 2u * (J - NS);
+        if (J < NS) {
+            single = true;
+            return J;
+        }
+        if (J < NS + NPJ) {
+            const uint32_t p = NS + 2u * (J - NS);
+            single = p + 1u >= PE;  // (an odd pair range ends with one unit)
+            return p;
+        }
+        single = true;
+        return PE + (J - NS - NPJ);
     };
     bool single;
     uint32_t pos = jobPos(job, single);
@@ -187,7 +201,7 @@ __global__ __launch_bounds__(NT) void k_blend_pw(
     uint32_t waveMax = 0;
 
     while (pos < numUnits) {
-        const bool pair = !single && pos + 1u < numUnits;
+        const bool pair = !single && pos + 1u < PE;
         // the two units (scalars, not arrays: a lane-dependent pick from an array would go to scratch)
         uint32_t Uu0 = 0, Uu1 = 0, UX0 = 0, UX1 = 0, UY0 = 0, UY1 = 0, CNT0 = 0, CNT1 = 0, FULL0 = 0, FULL1 = 0;
         const uint32_t *LST0 = half0, *LST1 = half0;
@@ -582,6 +596,10 @@ __global__ __launch_bounds__(NT) void k_blend_pw(
 // the pair walk for a frame of half-tile units on one GPU (no multi-GPU gather); `waves` per workgroup
 void launch_blend_pw(const FrameGeometry& g, const DeviceArena& A, void* color, size_t colorPitch, void* depth,
                      size_t depthPitch, int numCUs, bool costOrder, int colorFormat, hipStream_t s, int waves) {
+    // A/B knobs (read per launch, experiments only): GSM_BLEND_PAIR_TAIL=k -- the k shortest units alone;
+    // GSM_BLEND_PAIR_STATIC=1 -- every wave's first job alone
+    static const uint32_t tailSingles = getenv("GSM_BLEND_PAIR_TAIL") ? (uint32_t)atoi(getenv("GSM_BLEND_PAIR_TAIL")) : 0u;
+    static const int staticSingles = getenv("GSM_BLEND_PAIR_STATIC") ? atoi(getenv("GSM_BLEND_PAIR_STATIC")) : 0;
     const uint32_t numTiles = g.rowCount * g.tilesX;
     if (numTiles == 0) return;
     const int vec = ((((uintptr_t)color) & 15u) == 0 && (colorPitch & 15u) == 0 &&
@@ -600,7 +618,7 @@ void launch_blend_pw(const FrameGeometry& g, const DeviceArena& A, void* color, 
 #define GSM_LAUNCH_PW(NTH)                                                                                          \
     hipLaunchKernelGGL((k_blend_pw<NTH>), dim3(grid), dim3(NTH), 0, s, A.tileStart, A.rec, A.expTable, A.tileQueue, \
                        numTiles, g.tilesX, tg, order, A.unitCost, A.blendTrace, A.halfVals[0], A.halfVals[1],      \
-                       A.halfCount, g.tileCount, A.costMax, g.rowBegin, g.rowStride, flags)
+                       A.halfCount, g.tileCount, A.costMax, g.rowBegin, g.rowStride, flags, tailSingles, staticSingles)
     if (waves >= 16) GSM_LAUNCH_PW(1024);
     else if (waves >= 12) GSM_LAUNCH_PW(768);
     else GSM_LAUNCH_PW(512);

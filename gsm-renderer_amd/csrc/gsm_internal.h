@@ -356,7 +356,8 @@ constexpr uint32_t kUoBuckets = 256;
 // average gap between a wave's units at 4K was 7.7 us of queueing).
 constexpr uint32_t kQueueStripes = 8, kQueueStride = 16;
 constexpr uint32_t kCostMaxSlots = 64;  // words of the longest-walk maximum (spread atomics)
-// (+ 1 word after them in the Global renderer's schedule sets: the pair walk's split position)
+// (+ 2 words after them in the Global renderer's schedule sets: the pair walk's split position and the
+// longest walk of the previous frame, which the blend's remaining-work priorities scale by)
 template <int NT>
 __device__ __forceinline__ void unit_order_block(const uint16_t* __restrict__ cost, uint32_t* __restrict__ order,
                                                  uint32_t n, uint32_t* base, uint32_t* wmax,
@@ -404,7 +405,10 @@ __device__ __forceinline__ void unit_order_block(const uint16_t* __restrict__ co
     }
     __syncthreads();
     // the pair walk's split: the units of buckets [0, splitBucket) -- the longest walks -- run alone
-    if (splitBucket && t == 0) costMax[kCostMaxSlots] = splitBucket >= kUoBuckets ? n : base[splitBucket];
+    if (splitBucket && t == 0) {
+        costMax[kCostMaxSlots] = splitBucket >= kUoBuckets ? n : base[splitBucket];
+        costMax[kCostMaxSlots + 1] = mx;
+    }
 
     for (uint32_t b0 = 0; b0 < n; b0 += (uint32_t)NT * UN) {
         uint32_t c[UN];

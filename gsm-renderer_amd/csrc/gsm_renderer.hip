@@ -119,7 +119,7 @@ gsm_status GlobalRenderer::create(const gsm_renderer_config& cfg, int hipDevice,
     GSM_ALLOC(A.tileQueue, kQueueStripes * kQueueStride * sizeof(uint32_t));
     GSM_ALLOC(A.unitCost, (size_t)r->tileCount_ * 4 * sizeof(uint16_t));
     GSM_ALLOC(A.unitOrder, (size_t)r->tileCount_ * 4 * sizeof(uint32_t));
-    GSM_ALLOC(A.costMax, (kCostMaxSlots + 1) * sizeof(uint32_t));
+    GSM_ALLOC(A.costMax, (kCostMaxSlots + 2) * sizeof(uint32_t));
     GSM_ALLOC(A.halfVals[0], cap * sizeof(uint32_t));
     GSM_ALLOC(A.halfVals[1], cap * sizeof(uint32_t));
     GSM_ALLOC(A.halfCount, (size_t)r->tileCount_ * 2 * sizeof(uint32_t));
@@ -141,7 +141,7 @@ gsm_status GlobalRenderer::create(const gsm_renderer_config& cfg, int hipDevice,
         hipMemset(A.header, 0, sizeof(TileAssignmentHeader)) != hipSuccess ||
         hipMemset(A.tileStart, 0, ((size_t)r->tileCount_ + 1) * sizeof(uint32_t)) != hipSuccess ||
         hipMemset(A.unitCost, 0, (size_t)r->tileCount_ * 4 * sizeof(uint16_t)) != hipSuccess ||
-        hipMemset(A.costMax, 0, (kCostMaxSlots + 1) * sizeof(uint32_t)) != hipSuccess ||
+        hipMemset(A.costMax, 0, (kCostMaxSlots + 2) * sizeof(uint32_t)) != hipSuccess ||
         // every entry of the value buffers is a valid gaussian id at all times (the blend's
         // clamped, unpredicated gathers may read entry 0 of an empty frame)
         hipMemset(A.vals[0], 0, cap * sizeof(uint32_t)) != hipSuccess ||
@@ -326,9 +326,9 @@ gsm_status GlobalRenderer::ensurePartitionBuffers(uint32_t numSlabs) {
         ScheduleSet t;
         st = alloc((void**)&t.unitCost, (size_t)tileCount_ * 4 * sizeof(uint16_t));
         if (st == GSM_OK) st = alloc((void**)&t.unitOrder, (size_t)tileCount_ * 4 * sizeof(uint32_t));
-        if (st == GSM_OK) st = alloc((void**)&t.costMax, (kCostMaxSlots + 1) * sizeof(uint32_t));
+        if (st == GSM_OK) st = alloc((void**)&t.costMax, (kCostMaxSlots + 2) * sizeof(uint32_t));
         if (st == GSM_OK && (hipMemset(t.unitCost, 0, (size_t)tileCount_ * 4 * sizeof(uint16_t)) != hipSuccess ||
-                             hipMemset(t.costMax, 0, (kCostMaxSlots + 1) * sizeof(uint32_t)) != hipSuccess ||
+                             hipMemset(t.costMax, 0, (kCostMaxSlots + 2) * sizeof(uint32_t)) != hipSuccess ||
                              hipDeviceSynchronize() != hipSuccess))
             st = GSM_ERR_FAILED_TO_ALLOCATE_BUFFER;
         if (st == GSM_OK) sched_[1] = t;
@@ -368,6 +368,7 @@ gsm_status GlobalRenderer::partitionCounts(hipStream_t s, const gsm_gaussian_inp
     if (st != GSM_OK) return st;
     // the blend units of this renderer's rows (its slab), ordered by one extra workgroup of the launch
     f.a.schedUnits = orderUnits ? scheduleUnits(s, width, height) : 0u;
+    f.a.pairBucket = tuning_.blendPairs ? (uint32_t)std::max(1, tuning_.pairBucket) : kUoBuckets;
     launch_partition_counts(f.half, f.deg, f.world, f.harm, f.a, f.slabs, part_, arena_.sincosTable, sendCounts,
                             arena_, publish ? *publish : CountPublish{}, s);
     partCount_ = count;
@@ -397,7 +398,7 @@ uint32_t GlobalRenderer::scheduleUnits(hipStream_t s, uint32_t width, uint32_t h
         for (const ScheduleSet& t : sched_) {
             if (!t.unitCost) continue;
             hipMemsetAsync(t.unitCost, 0, (size_t)units * sizeof(uint16_t), s);
-            hipMemsetAsync(t.costMax, 0, (kCostMaxSlots + 1) * sizeof(uint32_t), s);
+            hipMemsetAsync(t.costMax, 0, (kCostMaxSlots + 2) * sizeof(uint32_t), s);
         }
         schedKey_ = key;
     }
@@ -433,7 +434,8 @@ gsm_status GlobalRenderer::runFrame(hipStream_t s, const ProjectArgs& a, uint32_
     const uint32_t units = preOrdered ? 0u : scheduleUnits(s, width, height);
     const bool costOrder = preOrdered ? tuning_.costOrder : units > 0;
     fa.schedUnits = units;
-    fa.pairBucket = tuning_.blendPairs ? (uint32_t)std::max(1, tuning_.pairBucket) : 0u;  // (1: no single)
+    // (written on every scheduled frame: the blend's remaining-walk priorities read the longest walk too)
+    fa.pairBucket = tuning_.blendPairs ? (uint32_t)std::max(1, tuning_.pairBucket) : kUoBuckets;
 
     hipEvent_t* ev = (prof || blendOnly) ? frameEvents(profFrames_) : nullptr;
     if (prof) hipEventRecord(ev[0], s);

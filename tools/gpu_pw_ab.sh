@@ -17,12 +17,11 @@ b() {  # label cfg env...
   [ $rc -eq 0 ] || { echo "bench $label rc=$rc"; tail -n 5 $O/bench_$label.log; exit $rc; }
   grep '"metric"' $O/bench_$label.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); o=d.get('orbit') or {}; print('$label', round(d['value'],1), 'parity', d.get('parity_vs_oracle'), 'blend_us', round(d['stages_ms']['blend_timed_region']*1e3,1), 'orbit', round(o.get('value',0),1), round((o.get('blend_ms') or 0)*1e3,1), o.get('parity_last_frame'))"
 }
-for sp in ${SPLITS:-64 96 128 160 192}; do
-  b pw${sp}_cfg2 cfg2_1m_sh3_1080p_f16 GSM_BLEND_PAIRS=1 GSM_BLEND_PAIR_SPLIT=$sp
+for v in ${CFG2_VARIANTS:-}; do  # label:ENV=a,ENV=b
+  b ${v%%:*}_cfg2 cfg2_1m_sh3_1080p_f16 $(echo ${v#*:} | tr ',' ' ')
 done
 b px_cfg2 cfg2_1m_sh3_1080p_f16 GSM_BLEND_PAIRS=0
-for sp in ${SPLITS3:-16 32 64}; do
-  b pw${sp}_cfg3 cfg3_5m_sh3_4k_f16 GSM_BLEND_PAIRS=1 GSM_BLEND_PAIR_SPLIT=$sp
+for v in ${CFG3_VARIANTS:-}; do
+  b ${v%%:*}_cfg3 cfg3_5m_sh3_4k_f16 $(echo ${v#*:} | tr ',' ' ')
 done
-b px_cfg3 cfg3_5m_sh3_4k_f16 GSM_BLEND_PAIRS=0
 echo done

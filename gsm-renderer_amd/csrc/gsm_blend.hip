@@ -852,13 +852,13 @@ void launch_blend(const FrameGeometry& g, const DeviceArena& A, void* color,
                      (depth == nullptr || ((((uintptr_t)depth) & 7u) == 0 && (depthPitch & 7u) == 0)))
                         ? 1
                         : 0;
-    // GSM_BLEND_PRIO=lrpt[:a,b,c] (A/B): remaining-walk priorities at a / b / c of the longest walk
+    // GSM_BLEND_PRIO=lrpt[:a/b/c] (A/B): remaining-walk priorities at a / b / c of the longest walk
     static const char* pv = getenv("GSM_BLEND_PRIO");
     static const bool lrptMode = pv && !strncmp(pv, "lrpt", 4);
     static float4 prioFrac = [] {
         float4 f = make_float4(0.6f, 0.35f, 0.15f, 0.0f);
         const char* p = getenv("GSM_BLEND_PRIO");
-        if (p && p[0] && p[4] == ':') sscanf(p + 5, "%f,%f,%f", &f.x, &f.y, &f.z);
+        if (p && p[0] && p[4] == ':') sscanf(p + 5, "%f/%f/%f", &f.x, &f.y, &f.z);
         return f;
     }();
     const int flags = vec | 2 | (costOrder ? 4 : 0) | ((colorFormat & 15) << 4) | ((claim & 3) << 8) |

@@ -104,7 +104,7 @@ def parse():
     p.add_argument("--traffic-json", default=None,
                    help="blend PMC numbers per launch (tools/traffic.py), used when measured on --config; "
                         "default profiles/PMC_TAG_pmc_blend_<cfgN>.json")
-    p.add_argument("--pmc-tag", default="r04", help="round tag of the default PMC files in profiles/")
+    p.add_argument("--pmc-tag", default="r05", help="round tag of the default PMC files in profiles/")
     p.add_argument("--stereo-path", choices=("depthfirst", "global"), default="depthfirst",
                    help="stereo configs: DepthFirst semantics (SURVEY 8f rank 1) or two Global views")
     p.add_argument("--df-max-gaussians", type=int, default=6_000_000,
@@ -442,8 +442,12 @@ def main():
     # outnumber 8 waves x CUs, quadrants otherwise; every unit reads the tile's whole list
     n_cus = torch.cuda.get_device_properties(dev).multi_processor_count
     units_per_tile = 2 if T > 8 * n_cus else 4
+    # the blend kernel (gsm_blend.hip launch_blend): the pair walk k_blend_pw for half-tile frames of >= 6
+    # units per wave slot at 16 waves per CU (config 3), k_blend_px otherwise (GSM_BLEND_PAIRS=0: always)
+    blend_kernel = ("k_blend_pw" if units_per_tile == 2 and T * 2 >= 6 * n_cus * 16 and world_size == 1
+                    and os.environ.get("GSM_BLEND_PAIRS", "1") != "0" else "k_blend_px")
     traffic = valu_insts = traffic_note = valu_mix = None
-    tj = load_pmc(args.traffic_json, args.config, world_size, "k_blend_px")
+    tj = load_pmc(args.traffic_json, args.config, world_size, blend_kernel)
     if tj:
         raw_fetch = tj["fetch_size_kib"] * 1024
         write = tj["write_size_kib"] * 1024
@@ -535,14 +539,14 @@ def main():
                                       if native_multi else
                                       ("all-to-all of projected records" if alltoall else "projection replicas")))
                                   if world_size > 1 else "single GPU"},
-        "roofline": {"bound": "hbm", "kernel": "k_blend_px", "achieved": achieved, "peak": HBM_PEAK_GBS,
+        "roofline": {"bound": "hbm", "kernel": blend_kernel, "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "traffic_over_algorithmic": (traffic / b_blend) if traffic else None,
                      "traffic_note": traffic_note,
                      "algorithmic_bytes": b_blend, "launch_timing": f"HIP events around the blend on every {BLEND_EVENT_PERIOD}th frame of the timed region", "avg_launch_ms": blend_ms_timed,
                      "note": "blend is bound by packed-fp16 VALU issue (roofline_valu); HBM fraction "
                              "reported per the metric"},
-        "roofline_valu": valu_roofline("k_blend_px", valu_insts, valu_mix, t_blend),
+        "roofline_valu": valu_roofline(blend_kernel, valu_insts, valu_mix, t_blend),
         "roofline_frame": {"bound": "hbm", "achieved": b_frame / (ms_per_step * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
                            "unit": "GB/s", "frac": b_frame / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS,
                            "algorithmic_bytes": b_frame,

@@ -24,7 +24,7 @@ CFGS=${CFGS:-cfg2_1m_sh3_1080p_f16 cfg3_5m_sh3_4k_f16 cfg5_1m_sh2_stereo_2x1440x
 if [ "${PMC:-1}" = 1 ]; then
   for cfg in $CFGS; do
     c=${cfg%%_*}
-    kern=k_blend_px; [ $c = cfg5 ] && kern=k_df_blend_eye
+    kern=k_blend_px; [ $c = cfg5 ] && kern=k_df_blend_eye; [ $c = cfg3 ] && kern=k_blend_pw
     CMD="python bench.py --config $cfg --steps 5 --warmup 2 --cpu-baseline 0 --parity 0 --orbit-steps 0 --inflight-steps 0 --virtual-ranks 0"
     i=0
     for set in "FETCH_SIZE" "WRITE_SIZE" \

@@ -53,6 +53,24 @@ __device__ __forceinline__ uint32_t pw_bperm(uint32_t srcLane, uint32_t v) {
 }
 __device__ __forceinline__ h2 pw_bperm(uint32_t srcLane, h2 v) { return as_h2(pw_bperm(srcLane, as_u32(v))); }
 
+// A/B switches of the table gathers (LDS bank conflicts): GSM_PW_PCLAMP -- p above the last
+// nonzero entry reads the one zero entry 0x5056 (v_pk_minimum3_f16 keeps negative p and NaN);
+// GSM_PW_DEADX -- dead groups' columns moved to x = 65504
+#ifndef GSM_PW_PCLAMP
+#define GSM_PW_PCLAMP 0
+#endif
+#ifndef GSM_PW_DEADX
+#define GSM_PW_DEADX 0
+#endif
+__device__ __forceinline__ uint32_t pw_tbl_bits(h2 p) {
+#if GSM_PW_PCLAMP
+    const h2 c = {(h1)34.6875f, (h1)34.6875f};
+    return as_u32(__builtin_elementwise_minimum(p, c));
+#else
+    return as_u32(p);
+#endif
+}
+
 struct PwTarget {
     uint8_t* color;
     size_t colorPitch;
@@ -157,6 +175,8 @@ __global__ __launch_bounds__(NT) void k_blend_pw(
     const bool agePrio = (flags & 2) != 0, split = (flags & 4) != 0;
     const h2 ONE = {(h1)1.0f, (h1)1.0f};
     const h2 ZERO = {(h1)0.0f, (h1)0.0f};
+    const h2 FAR = {(h1)65504.0f, (h1)65504.0f};  // (GSM_PW_DEADX)
+    (void)FAR;
     const uint32_t thrBits = (uint32_t)__builtin_bit_cast(uint16_t, (h1)(1.0f / 255.0f));
     const h1 c099 = (h1)0.99;
     const h2 C099 = {c099, c099};
@@ -359,7 +379,7 @@ __global__ __launch_bounds__(NT) void k_blend_pw(
                     bdc[k] = LB[hb + k];
 #pragma unroll
                     for (int q = 0; q < NP; ++q) {
-                        const uint32_t pb = as_u32(pq[q]);
+                        const uint32_t pb = pw_tbl_bits(pq[q]);
                         const h2 ek = as_h2((uint32_t)tbl[pb & 0xFFFFu] | ((uint32_t)tbl[pb >> 16] << 16));
                         // a = min(opacity * exp(-0.5h * p), 0.99h) (GlobalShaders.metal:1124-1131)
                         ac[k][q] = __builtin_elementwise_min(splat_hi(as_h2(ra.z)) * ek, C099);
@@ -389,7 +409,7 @@ __global__ __launch_bounds__(NT) void k_blend_pw(
                                 bdn[k] = LB[nb + k];
 #pragma unroll
                                 for (int q = 0; q < NP; ++q) {
-                                    const uint32_t pb = as_u32(pq[q]);
+                                    const uint32_t pb = pw_tbl_bits(pq[q]);
                                     en[k][q].x = tbl[pb & 0xFFFFu];
                                     en[k][q].y = tbl[pb >> 16];
                                 }
@@ -458,6 +478,11 @@ __global__ __launch_bounds__(NT) void k_blend_pw(
                                 else if (e == 320u && !split) __builtin_amdgcn_s_setprio(3);
                             }
                             hb = (e - b0 == 0u) ? laneSlot() : hb + 16u;
+#if GSM_PW_DEADX
+                            // a dead group's lanes walk on with their columns at x = 65504: p = +-inf or NaN,
+                            // three table words, instead of scattered live-looking gathers (bank conflicts)
+                            if (!alive) X0 = X1 = FAR;
+#endif
                         }
                         // stage 3: the next group's alphas
 #pragma unroll

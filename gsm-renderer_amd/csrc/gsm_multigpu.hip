@@ -202,6 +202,19 @@ class MultiGpu {
     // from the slab render on; phase 1's push still runs when phase 0 published this rank's counts)
     gsm_status finishFrame(hipStream_t s);
     // gsm_multigpu_wait_event: the next phase 0 waits for `ev` on the stream its projection runs on
+    // gsm_multigpu_debug_set_epoch: the barrier epoch of the next frame - 1 (every rank alike, no frame
+    // pending or in flight): this rank's flag words are set to it, as if every peer had reached it
+    gsm_status debugSetEpoch(uint32_t epoch) {
+        if (nextPhase_ != 0) return GSM_ERR_PHASE_ORDER;
+        epoch &= kEpochMask;
+        if (epoch == 0) epoch = 1;
+        if (hipSetDevice(device_) != hipSuccess || hipDeviceSynchronize() != hipSuccess) return GSM_ERR_RENDER_FAILED;
+        uint32_t f[kBarriers * kMaxSlabs];
+        for (uint32_t& w : f) w = epoch;
+        if (hipMemcpy(ctl() + kFlagWords, f, sizeof(f), hipMemcpyHostToDevice) != hipSuccess) return GSM_ERR_RENDER_FAILED;
+        frame_ = epoch;
+        return GSM_OK;
+    }
     gsm_status waitEvent(hipEvent_t ev) {
         inputEvent_ = ev;
         return GSM_OK;
@@ -782,6 +795,11 @@ gsm_status gsm_multigpu_render_phase(gsm_multigpu* m, int phase, void* stream, c
 gsm_status gsm_multigpu_finish_frame(gsm_multigpu* m, void* stream) {
     if (!m || !m->impl) return GSM_ERR_INVALID_ARGUMENT;
     return m->impl->finishFrame((hipStream_t)stream);
+}
+
+gsm_status gsm_multigpu_debug_set_epoch(gsm_multigpu* m, uint32_t epoch) {
+    if (!m || !m->impl) return GSM_ERR_INVALID_ARGUMENT;
+    return m->impl->debugSetEpoch(epoch);
 }
 
 gsm_status gsm_multigpu_wait_event(gsm_multigpu* m, void* event) {

@@ -259,6 +259,7 @@ _SIGNATURES = {
     "gsm_multigpu_errors": ([C.c_void_p, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.c_int], C.c_int),
     "gsm_multigpu_finish_frame": ([C.c_void_p, C.c_void_p], C.c_int),
     "gsm_multigpu_wait_event": ([C.c_void_p, C.c_void_p], C.c_int),
+    "gsm_multigpu_debug_set_epoch": ([C.c_void_p, C.c_uint32], C.c_int),
 }
 
 SPLAT_RECORD_BYTES = 48  # include/gsm_multigpu.h GSM_SPLAT_RECORD_BYTES
@@ -746,6 +747,10 @@ class MultiGpuRenderer:
         """gsm_multigpu_finish_frame: the phases a caller left unfinished (barrier steps; the slab is
         abandoned from phase 2 on), so the ranks stay in step; a no-op when no frame is pending."""
         _check(_lib().gsm_multigpu_finish_frame(self._h, _stream_handle(stream)), "gsm_multigpu_finish_frame")
+
+    def debug_set_epoch(self, epoch: int):
+        """gsm_multigpu_debug_set_epoch (tests: reach the 2^31 epoch wrap in a few frames)."""
+        _check(_lib().gsm_multigpu_debug_set_epoch(self._h, int(epoch) & 0xFFFFFFFF), "gsm_multigpu_debug_set_epoch")
 
     def wait_event(self, event):
         """gsm_multigpu_wait_event: the next frame's projection (phase 0) waits for `event` (a

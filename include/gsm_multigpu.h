@@ -173,6 +173,12 @@ gsm_status gsm_multigpu_debug_copy_exchange(gsm_multigpu *multigpu, void *host_d
 /* The last frame's world x world record counts (row = source rank, column = slab), synchronous. */
 gsm_status gsm_multigpu_debug_counts(gsm_multigpu *multigpu, uint32_t *host_counts);
 
+/* Test surface (r05): the barrier epoch of the last frame becomes `epoch` (taken modulo 2^31, 0 -> 1) and
+ * this rank's flag words are set as if every peer had reached it -- so a test reaches the epoch wrap
+ * (2^31 - 1 -> 1) in a few frames.  Every rank alike, with no frame pending or in flight (synchronous);
+ * GSM_ERR_PHASE_ORDER while a frame is pending. */
+gsm_status gsm_multigpu_debug_set_epoch(gsm_multigpu *multigpu, uint32_t epoch);
+
 /* gsm_multigpu_render in four phases (0: projection + counts + barrier; 1: records + barrier;
  * 2: slab render + the gather signal; 3: rank 0's gather wait + copy); render = phases 0..3, each
  * called even after an earlier phase of the frame returned an error.  A phase called out of order

@@ -354,3 +354,44 @@ def test_virtual_ranks_phase_order_and_finish_frame(gsm, cuda, oracle):
         m.close()
     for r in rends:
         r.close()
+
+
+@pytest.mark.parametrize("pipelined", ["0", "1"])
+def test_virtual_ranks_epoch_wrap(gsm, cuda, oracle, monkeypatch, pipelined):
+    """the barrier epochs are frame numbers masked to 31 bits (0 skipped); the flags are compared
+    modulo 2^31 and the frame parity (count matrix, receive buffers, schedules, pipelined gathered frames)
+    alternates in a counter of its own.  Three ranks start at epoch 2^31 - 4 and render six frames across
+    the wrap 2^31 - 1 -> 1 -> 2, serial and pipelined: every frame bit-exact, no barrier timeout."""
+    from gsm_amd import scenes
+    monkeypatch.setenv("GSM_MG_PIPELINE", pipelined)
+    world, n, w, h, sh, prec = 3, 30_000, 640, 360, 16, 1
+    world_np, harm_np, cam0 = scenes.gen_scene(n, w, h, sh, prec, seed=23)
+    wt = cuda.from_numpy(world_np.view(np.uint8).reshape(-1).copy()).cuda()
+    ht = cuda.from_numpy(harm_np.view(np.uint8).reshape(-1).copy()).cuda()
+    inp = gsm.GaussianInput(wt, ht, n, sh)
+    cfg = gsm.RendererConfig(max_gaussians=n, max_width=w, max_height=h, precision=prec, gaussian_color_space=0)
+    rends = [gsm.GlobalRenderer(device=0, config=cfg) for _ in range(world)]
+    pre = [gsm.MultiGpuRenderer.prepare(r, k, world) for k, r in enumerate(rends)]
+    mgs = [m.connect_handles([hd for _, hd in pre]) for m, _ in pre]
+    for m in mgs:
+        m.debug_set_epoch(2**31 - 4)
+    stream = cuda.cuda.current_stream()
+    cams = [cam0, scenes.orbit_camera(w, h, 5.0)] * 3
+    colors = [cuda.full((h, w, 4), float("nan"), dtype=cuda.float16, device="cuda") for _ in cams]
+    for f, cam in enumerate(cams):
+        cp = gsm.CameraParams.from_dict(cam)
+        for ph in range(4):
+            for k, m in enumerate(mgs):
+                m.render_phases([ph], colors[f] if k == 0 else None, None, inp, cp, w, h, gather=True, stream=stream,
+                                gather_depth=False)
+    cuda.cuda.synchronize()
+    assert [m.errors() for m in mgs] == [(0, 0)] * world
+    refs = [oracle.render(world_np, harm_np, sh, c, w, h, max_gaussians=n)["color"] for c in cams[:2]]
+    for f in range(len(cams)):
+        got = colors[f].view(cuda.int16).cpu().numpy().view(np.uint16)
+        bad = np.nonzero(np.any(got != refs[f % 2], axis=(1, 2)))[0]
+        assert len(bad) == 0, f"frame {f}: {len(bad)} rows differ, first {bad[:16].tolist()}"
+    for m in mgs:
+        m.close()
+    for r in rends:
+        r.close()

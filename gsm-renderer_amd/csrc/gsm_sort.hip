@@ -73,11 +73,36 @@ __device__ __forceinline__ uint32_t wave_rank(uint32_t* cnt, uint32_t d, bool va
     }
 }
 
+// Scanless narrow passes (the default; GSM_SORT_SCAN=kernel restores k_radix_scan): the upsweep also
+// adds each block's digit counts into its super-group's row (kSuperGroup consecutive blocks share a
+// row of 256 words; device-scope atomics, at most kSuperGroup deep per word), and every downsweep
+// block derives its digit bases itself -- digit totals = the sum of all rows, its prefix = the rows of
+// the earlier super-groups plus the earlier blocks of its own group (< kSuperGroup + grid/kSuperGroup
+// reads per digit, spread over 256 / R threads).  One launch less per pass, no extra pass over the keys.
+// Two row sets: a sort call of an even number of narrow passes alternates them, pass i on set i & 1,
+// and each upsweep zeroes the other set (its last reader, the previous pass, has finished), so every
+// call starts and ends with set 0 zero; calls of an odd number of narrow passes keep k_radix_scan.
+// (A ticket taken by the downsweep's last block to zero the rows costs more than the scan it replaces:
+// a single ticket serializes at ~36 ns an atomic, and an agent-scope fence per block writes back the
+// XCD's L2 -- +35 us a pass, measured.)
+constexpr uint32_t kSuperGroup = 32;
+constexpr uint32_t kSuperRows = 1024 / kSuperGroup;  // radix_grid_for_capacity caps the grid at 1024
+constexpr size_t kSuperSetWords = (size_t)kSuperRows * 256;
+constexpr size_t kSuperWords = 2 * kSuperSetWords;
+static_assert(kRadixBlock == 256 && kRadixBlock / 64 == 4, "the scanless base reduction assumes 4 waves");
+
+static bool scanless_sort() {
+    static const bool v = !(getenv("GSM_SORT_SCAN") && strcmp(getenv("GSM_SORT_SCAN"), "kernel") == 0);
+    return v;
+}
+
 template <int BITS>
 __global__ __launch_bounds__(kRadixBlock) void k_radix_upsweep(const uint32_t* __restrict__ keys,
                                                                const uint32_t* __restrict__ nPtr,
                                                                uint32_t shift,
-                                                               uint32_t* __restrict__ hist) {
+                                                               uint32_t* __restrict__ hist,
+                                                               uint32_t* __restrict__ super,
+                                                               uint32_t* __restrict__ superClear) {
     constexpr uint32_t R = 1u << BITS;
     // GSM_UPSWEEP_COPIES counter copies per wave (lane & (copies - 1) picks one), rows padded by a
     // word so one digit's copies sit in different LDS banks: fewer same-address collisions among
@@ -87,6 +112,9 @@ __global__ __launch_bounds__(kRadixBlock) void k_radix_upsweep(const uint32_t* _
     const uint32_t wave = threadIdx.x >> 6;
     const uint32_t row = wave * CP + (threadIdx.x & (CP - 1u));
     for (int i = threadIdx.x; i < (int)(kWaves * CP * RS); i += kRadixBlock) (&cnt[0][0])[i] = 0;
+    if (superClear)  // scanless: the previous pass's row set, for the next pass
+        for (uint32_t i = blockIdx.x * kRadixBlock + threadIdx.x; i < (uint32_t)kSuperSetWords; i += gridDim.x * kRadixBlock)
+            superClear[i] = 0u;
     __syncthreads();
     uint32_t begin, end;
     block_range(*nPtr, gridDim.x, blockIdx.x, &begin, &end);
@@ -127,6 +155,7 @@ __global__ __launch_bounds__(kRadixBlock) void k_radix_upsweep(const uint32_t* _
 #pragma unroll
         for (uint32_t w = 0; w < kWaves * CP; ++w) s += cnt[w][d];
         hist[(size_t)d * gridDim.x + blockIdx.x] = s;
+        if (super && s) atomicAdd(&super[(blockIdx.x / kSuperGroup) * 256u + d], s);
     }
 }
 
@@ -196,7 +225,8 @@ template <int BITS, bool BALLOT, bool STARTS>
 __global__ __launch_bounds__(kRadixBlock) void k_radix_downsweep(
     const uint32_t* __restrict__ keysIn, const uint32_t* __restrict__ valsIn,
     uint32_t* __restrict__ keysOut, uint32_t* __restrict__ valsOut, const uint32_t* __restrict__ nPtr,
-    uint32_t shift, const uint32_t* __restrict__ hist, const uint32_t* __restrict__ binTotals, TileStarts ts) {
+    uint32_t shift, const uint32_t* __restrict__ hist, const uint32_t* __restrict__ binTotals, TileStarts ts,
+    const uint32_t* __restrict__ super) {
     constexpr uint32_t R = 1u << BITS;
     __shared__ uint32_t binBase[256];
     __shared__ uint32_t localStart[256];
@@ -224,7 +254,48 @@ __global__ __launch_bounds__(kRadixBlock) void k_radix_downsweep(
 
     // global base of every digit for this block: exclusive scan over digits + block column offset
     {
-        const uint32_t t = tid < R ? binTotals[tid] : 0u;
+        uint32_t t, pre;
+        if (super) {  // scanless: totals and this block's prefix from the super-group rows
+            constexpr uint32_t SPLIT = (256u / R) < 4u ? (256u / R) : 4u;
+            const uint32_t d = tid % R, q = tid / R, b = blockIdx.x, g = b / kSuperGroup;
+            const uint32_t rows = (gridDim.x + kSuperGroup - 1u) / kSuperGroup;
+            uint32_t tq = 0, pq = 0;
+            if (q < SPLIT) {  // fixed trip counts, unrolled: every load in flight at once
+                constexpr uint32_t NR = kSuperRows / SPLIT, NB = kSuperGroup / SPLIT;
+                uint32_t rv[NR], bv[NB];
+#pragma unroll
+                for (uint32_t i = 0; i < NR; ++i) {
+                    const uint32_t r = q + i * SPLIT;
+                    rv[i] = r < rows ? super[r * 256u + d] : 0u;
+                }
+#pragma unroll
+                for (uint32_t i = 0; i < NB; ++i) {
+                    const uint32_t bb = g * kSuperGroup + q + i * SPLIT;
+                    bv[i] = bb < b ? hist[(size_t)d * gridDim.x + bb] : 0u;
+                }
+#pragma unroll
+                for (uint32_t i = 0; i < NR; ++i) {
+                    tq += rv[i];
+                    pq += q + i * SPLIT < g ? rv[i] : 0u;
+                }
+#pragma unroll
+                for (uint32_t i = 0; i < NB; ++i) pq += bv[i];
+                sKeys[q * 256u + d] = tq;
+                waveCnt[q][d] = pq;
+            }
+            __syncthreads();
+            t = 0u;
+            pre = 0u;
+            if (tid < R)
+#pragma unroll
+                for (uint32_t i = 0; i < SPLIT; ++i) {
+                    t += sKeys[i * 256u + tid];
+                    pre += waveCnt[i][tid];
+                }
+        } else {
+            t = tid < R ? binTotals[tid] : 0u;
+            pre = tid < R ? hist[(size_t)tid * gridDim.x + blockIdx.x] : 0u;
+        }
         uint32_t inc = t;
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) {
@@ -237,7 +308,7 @@ __global__ __launch_bounds__(kRadixBlock) void k_radix_downsweep(
 #pragma unroll
         for (int w = 0; w < kWaves; ++w)
             if ((uint32_t)w < wave) off += part[w];
-        binBase[tid] = off + inc - t + (tid < R ? hist[(size_t)tid * gridDim.x + blockIdx.x] : 0u);
+        binBase[tid] = off + inc - t + pre;
         // first pass of radix_sort_tiles: its digits are the last pass's buckets
         if (!STARTS && ts.bucketStartOut && blockIdx.x == 0 && tid < R) ts.bucketStartOut[tid] = off + inc - t;
 #pragma unroll
@@ -797,6 +868,7 @@ static void wide_pass(uint32_t* kin, uint32_t* vin, uint32_t* kout, uint32_t* vo
                       uint32_t grid, uint32_t shift, uint32_t base, int bits, uint32_t* hist, uint32_t* binTotals,
                       hipStream_t s, bool ballot, bool starts, uint32_t* tileStart, uint32_t numTiles,
                       uint32_t allTiles) {
+    hist += kSuperWords;  // (radix_workspace_bytes: the narrow passes' super-group rows come first)
 #define GSM_WIDE_DOWN(B, BAL, S)                                                                              \
     if (B == kWide12Bits)                                                                                     \
         hipLaunchKernelGGL((k_wide12_downsweep<BAL, S>), dim3(grid), dim3(kRadixBlock), 0, s, kin, vin, kout, \
@@ -825,9 +897,9 @@ static void wide_pass(uint32_t* kin, uint32_t* vin, uint32_t* kout, uint32_t* vo
 }
 
 size_t radix_workspace_bytes(uint32_t capacity) {
-    // per-block digit counts: <= 1024 blocks x 256 digits (narrow), x 2048 digits (wide)
+    // the scanless super-group row sets (zero at allocation; see kSuperGroup), then the per-block digit counts: <= 1024 blocks x 256 digits (narrow), x 2048 (wide)
     const size_t wide = (size_t)(kWide12Bins + kWideRowPad) * radix_grid_for_capacity(capacity) * sizeof(uint32_t);
-    return wide > (size_t)256 * 1024 * 4 ? wide : (size_t)256 * 1024 * sizeof(uint32_t);
+    return kSuperWords * sizeof(uint32_t) + (wide > (size_t)256 * 1024 * 4 ? wide : (size_t)256 * 1024 * sizeof(uint32_t));
 }
 
 uint32_t radix_grid_for_capacity(uint32_t capacity) {
@@ -842,17 +914,23 @@ uint32_t radix_grid_for_capacity(uint32_t capacity) {
 // starts = true -- the tile starts)
 static void radix_pass(uint32_t* kin, uint32_t* vin, uint32_t* kout, uint32_t* vout, const uint32_t* nPtr,
                        uint32_t grid, uint32_t shift, int bits, uint32_t* hist, uint32_t* binTotals,
-                       hipStream_t s, bool ballot, const TileStarts* ts = nullptr, bool starts = false) {
+                       hipStream_t s, bool ballot, const TileStarts* ts = nullptr, bool starts = false,
+                       int superSet = -1) {
     const TileStarts t = ts ? *ts : TileStarts{};
+    // scanless (superSet 0 or 1): the row sets sit in front of the block counts
+    uint32_t* super = superSet >= 0 ? hist + (size_t)superSet * kSuperSetWords : nullptr;
+    uint32_t* superClear = superSet >= 0 ? hist + (size_t)(superSet ^ 1) * kSuperSetWords : nullptr;
+    hist += kSuperWords;
 #define GSM_RADIX_PASS(B, S)                                                                                \
-    hipLaunchKernelGGL(k_radix_upsweep<B>, dim3(grid), dim3(kRadixBlock), 0, s, kin, nPtr, shift, hist);    \
-    hipLaunchKernelGGL(k_radix_scan, dim3(1u << B), dim3(256), 0, s, hist, grid, binTotals);               \
+    hipLaunchKernelGGL(k_radix_upsweep<B>, dim3(grid), dim3(kRadixBlock), 0, s, kin, nPtr, shift, hist, super, \
+                       superClear);                                                                         \
+    if (!super) hipLaunchKernelGGL(k_radix_scan, dim3(1u << B), dim3(256), 0, s, hist, grid, binTotals);  \
     if (ballot)                                                                                             \
         hipLaunchKernelGGL((k_radix_downsweep<B, true, S>), dim3(grid), dim3(kRadixBlock), 0, s, kin, vin, kout, \
-                           vout, nPtr, shift, hist, binTotals, t);                                          \
+                           vout, nPtr, shift, hist, binTotals, t, super);                                   \
     else                                                                                                    \
         hipLaunchKernelGGL((k_radix_downsweep<B, false, S>), dim3(grid), dim3(kRadixBlock), 0, s, kin, vin, kout, \
-                           vout, nPtr, shift, hist, binTotals, t)
+                           vout, nPtr, shift, hist, binTotals, t, super)
 #define GSM_RADIX_BITS(S)                    \
     switch (bits) {                          \
         case 4: GSM_RADIX_PASS(4, S); break; \
@@ -875,9 +953,10 @@ int radix_sort_pairs(uint32_t* keys[2], uint32_t* vals[2], const uint32_t* nPtr,
                      hipStream_t s, bool ballot) {
     const uint32_t grid = radix_grid_for_capacity(capacity);
     int cur = 0;
+    const bool scanless = scanless_sort() && numDigits % 2 == 0;
     for (int dgt = firstDigit; dgt < firstDigit + numDigits; ++dgt) {
         radix_pass(keys[cur], vals[cur], keys[cur ^ 1], vals[cur ^ 1], nPtr, grid, (uint32_t)dgt * 8u, 8, hist,
-                   binTotals, s, ballot);
+                   binTotals, s, ballot, nullptr, false, scanless ? (dgt - firstDigit) & 1 : -1);
         cur ^= 1;
     }
     return cur;
@@ -892,6 +971,7 @@ int radix_sort_bits(uint32_t* keys[2], uint32_t* vals[2], const uint32_t* nPtr, 
     // wide digits where they save a whole pass (32-bit keys: 3 passes of 11/11/10 bits instead of 4)
     const bool useWide = wide && widePasses < narrowPasses;
     const uint32_t passes = useWide ? widePasses : narrowPasses;
+    const bool scanless = !useWide && scanless_sort() && passes % 2 == 0;
     int cur = 0;
     uint32_t done = 0;
     for (uint32_t p = 0; p < passes; ++p) {
@@ -904,7 +984,7 @@ int radix_sort_bits(uint32_t* keys[2], uint32_t* vals[2], const uint32_t* nPtr, 
         } else {
             if (b < 4) b = 4;
             radix_pass(keys[cur], vals[cur], keys[cur ^ 1], vals[cur ^ 1], nPtr, grid, shift + done, (int)b, hist,
-                       binTotals, s, ballot);
+                       binTotals, s, ballot, nullptr, false, scanless ? (int)(p & 1u) : -1);
         }
         done += b;
         cur ^= 1;
@@ -947,12 +1027,13 @@ int radix_sort_tiles(uint32_t* keys[2], uint32_t* vals[2], const uint32_t* nPtr,
     const uint32_t hi = bits - lo < 4u ? 4u : bits - lo;  // (a digit wider than the bits left reads zeros)
     TileStarts first{};
     first.bucketStartOut = binTotals + 512;
+    const bool scanless = scanless_sort();
     radix_pass(keys[0], vals[0], keys[1], vals[1], nPtr, grid, shift, (int)lo, hist, binTotals + 256, s, ballot,
-               &first, false);
+               &first, false, scanless ? 0 : -1);
     ts.bucketStart = binTotals + 512;
     ts.lowBits = lo;
     radix_pass(keys[1], vals[1], keys[0], vals[0], nPtr, grid, shift + lo, (int)hi, hist, binTotals, s, ballot, &ts,
-               true);
+               true, scanless ? 1 : -1);
     return 0;
 }
 

@@ -194,8 +194,8 @@ gsm_status gsm_sort_pairs_u32(void* keys, void* values, uint32_t n, uint32_t key
         const int digits = (int)((key_bits + 7) / 8);
         int dev = 0;
         hipGetDevice(&dev);
-        const bool ballot = gsm::tuning_from_env(dev).ballotRank;  // read per call: no renderer here
-        int res = gsm::radix_sort_pairs(kb, vb, np, n, 0, digits, hist, bins, s, ballot);
+        const gsm::Tuning tn = gsm::tuning_from_env(dev);  // read per call: no renderer here
+        int res = gsm::radix_sort_pairs(kb, vb, np, n, 0, digits, hist, bins, s, tn.ballotRank, tn.sortScanless);
         if (res == 1) {
             hipMemcpyAsync(keys, k2, (size_t)n * 4, hipMemcpyDeviceToDevice, s);
             hipMemcpyAsync(values, v2, (size_t)n * 4, hipMemcpyDeviceToDevice, s);

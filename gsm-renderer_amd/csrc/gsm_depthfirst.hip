@@ -259,7 +259,8 @@ gsm_status DepthFirstRenderer::renderStereoSbs(hipStream_t s, const gsm_gaussian
     // DepthRadixSortEncoder, 32-bit keys (DepthFirstRenderer.swift:664-681): stable LSD
     // (3 wide passes of 11/11/10 bits unless GSM_SORT_WIDE=0: the same stable order)
     const int dc = radix_sort_bits(A_.dkeys, A_.dvals, &A_.visHdr->totalAssignments, maxGaussians_, 0, 32,
-                                   A_.radixHist, A_.radixBinTotals, s, tuning_.ballotRank, tuning_.wideSort);
+                                   A_.radixHist, A_.radixBinTotals, s, tuning_.ballotRank, tuning_.wideSort,
+                                   tuning_.sortScanless);
     if (prof) hipEventRecord(ev[2], s);
     df_launch_instance_counts(A_.dvals[dc], a, A_, s);
     launch_scan_sums(A_.instSums, nb, maxInstances_, A_.instHdr, A_.queue, s);
@@ -269,7 +270,7 @@ gsm_status DepthFirstRenderer::renderStereoSbs(hipStream_t s, const gsm_gaussian
     // the last pass also writes the tile ranges' starts (radix_sort_tiles: no pass over the instances)
     const int ic = radix_sort_tiles(A_.ikeys, A_.ivals, &A_.instHdr->totalAssignments, maxInstances_, 0, A_.radixHist,
                                     A_.radixBinTotals, A_.starts, 0u, a.tileCount, a.tileCount, s, tuning_.ballotRank,
-                                    0, tuning_.wideSort);
+                                    0, tuning_.wideSort, false, tuning_.sortScanless);
     // Blend schedule: (tile, eye) units handed out longest first by the walk lengths the previous
     // frame of the same geometry measured (the image does not depend on the order, only the load
     // balance does).  Tuning::costOrder false (GSM_BLEND_SCHED=0 at create): index order.

@@ -209,6 +209,7 @@ struct Tuning {
     int tileLoBits = 0;       // GSM_SORT_LOBITS=4..8: width of the first tile pass (0: half the tile field)
     int blendClaim = 1;       // GSM_BLEND_CLAIM=early|late|auto (0/1/2): when a blend wave claims its next unit
     bool wideSort = true;     // GSM_SORT_WIDE=0: narrow passes only (no wide 9..11-bit tile or depth passes)
+    bool sortScanless = true; // GSM_SORT_SCAN=kernel: narrow passes with the k_radix_scan launch (r05 default: none)
     bool mgPixelsWB = true;   // a gathered multi-GPU frame's blend stores its pixels plainly and the last
                               // exiting wave of each workgroup writes the XCD's L2 back at system scope
                               // before arriving; GSM_MG_PIXELS=wt: write-through pixel stores instead
@@ -316,20 +317,22 @@ uint32_t blend_units_per_tile(uint32_t numTiles, int numCUs);
 // ballot: ranks from ballot matches (Tuning::ballotRank) instead of lane-ordered LDS atomics.
 int radix_sort_pairs(uint32_t* keys[2], uint32_t* vals[2], const uint32_t* nPtr, uint32_t capacity,
                      int firstDigit, int numDigits, uint32_t* hist, uint32_t* binTotals,
-                     hipStream_t stream, bool ballot);
+                     hipStream_t stream, bool ballot, bool scanless = true);
 // Stable LSD radix sort by bits [shift, shift + bits) only, in ceil(bits / 8) passes of
 // near-equal digit widths (4..8 bits), or -- `wide` and where that saves a pass -- ceil(bits / 11)
 // passes of 9..11 bits.  binTotals: kSortTotalsWords words.  Returns the ping-pong index of the result.
 int radix_sort_bits(uint32_t* keys[2], uint32_t* vals[2], const uint32_t* nPtr, uint32_t capacity,
                     uint32_t shift, uint32_t bits, uint32_t* hist, uint32_t* binTotals, hipStream_t stream,
-                    bool ballot, bool wide = false);
+                    bool ballot, bool wide = false, bool scanless = true);
 // the frame sort's tile field (tiles [tileBase, tileBase + numTiles) of allTiles, bits <= 16) with
 // the tile starts written by its last pass (tileStart[0..allTiles], lower bounds for empty tiles);
 // one wide pass relative to tileBase when numTiles <= 2048 and `wide`; binTotals: kSortTotalsWords words
 int radix_sort_tiles(uint32_t* keys[2], uint32_t* vals[2], const uint32_t* nPtr, uint32_t capacity, uint32_t shift,
                      uint32_t* hist, uint32_t* binTotals, uint32_t* tileStart, uint32_t tileBase, uint32_t numTiles,
                      uint32_t allTiles, hipStream_t stream, bool ballot, int loBits = 0, bool wide = true,
-                     bool wide12 = false);
+                     bool wide12 = false, bool scanless = true);
+// scanless: narrow passes without the k_radix_scan launch (super-group digit rows, gsm_sort.hip;
+// Tuning::sortScanless) -- the same order either way
 uint32_t radix_grid_for_capacity(uint32_t capacity);
 // bytes of the sort workspace (`hist` argument above) for a capacity; zero it once at allocation
 size_t radix_workspace_bytes(uint32_t capacity);

@@ -478,7 +478,7 @@ gsm_status GlobalRenderer::runFrame(hipStream_t s, const ProjectArgs& a, uint32_
         const int res = radix_sort_tiles(kb, vb, &arena_.header->totalAssignments, maxAssignments_, 16,
                                          arena_.radixHist, arena_.radixBinTotals, arena_.tileStart, 0u, localTiles,
                                          tileCount_, s, ballot, tuning_.tileLoBits, tuning_.wideSort,
-                                         tuning_.wideSort && tuning_.wide12);
+                                         tuning_.wideSort && tuning_.wide12, tuning_.sortScanless);
         tile_depth_sort(kb[res], vb[res], kb[res ^ 1], vb[res ^ 1], arena_.tileStart, 0u, localTiles, s, ballot,
                         arena_.halfVals[0], arena_.halfVals[1],
                         arena_.halfCount, tileCount_, capture, numCUs_);
@@ -486,7 +486,8 @@ gsm_status GlobalRenderer::runFrame(hipStream_t s, const ProjectArgs& a, uint32_
         sortedVals_ = capture ? vb[res ^ 1] : nullptr;
     } else {
         const int res = radix_sort_pairs(kb, vb, &arena_.header->totalAssignments, maxAssignments_, 0,
-                                         sortPassCount(), arena_.radixHist, arena_.radixBinTotals, s, ballot);
+                                         sortPassCount(), arena_.radixHist, arena_.radixBinTotals, s, ballot,
+                                         tuning_.sortScanless);
         sortedKeys_ = kb[res];
         sortedVals_ = vb[res];
     }

@@ -73,7 +73,7 @@ __device__ __forceinline__ uint32_t wave_rank(uint32_t* cnt, uint32_t d, bool va
     }
 }
 
-// Scanless narrow passes (the default; GSM_SORT_SCAN=kernel restores k_radix_scan): the upsweep also
+// Scanless narrow passes (the default; Tuning::sortScanless, GSM_SORT_SCAN=kernel restores k_radix_scan): the upsweep also
 // adds each block's digit counts into its super-group's row (kSuperGroup consecutive blocks share a
 // row of 256 words; device-scope atomics, at most kSuperGroup deep per word), and every downsweep
 // block derives its digit bases itself -- digit totals = the sum of all rows, its prefix = the rows of
@@ -91,10 +91,6 @@ constexpr size_t kSuperSetWords = (size_t)kSuperRows * 256;
 constexpr size_t kSuperWords = 2 * kSuperSetWords;
 static_assert(kRadixBlock == 256 && kRadixBlock / 64 == 4, "the scanless base reduction assumes 4 waves");
 
-static bool scanless_sort() {
-    static const bool v = !(getenv("GSM_SORT_SCAN") && strcmp(getenv("GSM_SORT_SCAN"), "kernel") == 0);
-    return v;
-}
 
 template <int BITS>
 __global__ __launch_bounds__(kRadixBlock) void k_radix_upsweep(const uint32_t* __restrict__ keys,
@@ -950,10 +946,10 @@ static void radix_pass(uint32_t* kin, uint32_t* vin, uint32_t* kout, uint32_t* v
 
 int radix_sort_pairs(uint32_t* keys[2], uint32_t* vals[2], const uint32_t* nPtr, uint32_t capacity,
                      int firstDigit, int numDigits, uint32_t* hist, uint32_t* binTotals,
-                     hipStream_t s, bool ballot) {
+                     hipStream_t s, bool ballot, bool scanlessOn) {
     const uint32_t grid = radix_grid_for_capacity(capacity);
     int cur = 0;
-    const bool scanless = scanless_sort() && numDigits % 2 == 0;
+    const bool scanless = scanlessOn && numDigits % 2 == 0;
     for (int dgt = firstDigit; dgt < firstDigit + numDigits; ++dgt) {
         radix_pass(keys[cur], vals[cur], keys[cur ^ 1], vals[cur ^ 1], nPtr, grid, (uint32_t)dgt * 8u, 8, hist,
                    binTotals, s, ballot, nullptr, false, scanless ? (dgt - firstDigit) & 1 : -1);
@@ -964,14 +960,14 @@ int radix_sort_pairs(uint32_t* keys[2], uint32_t* vals[2], const uint32_t* nPtr,
 
 int radix_sort_bits(uint32_t* keys[2], uint32_t* vals[2], const uint32_t* nPtr, uint32_t capacity,
                     uint32_t shift, uint32_t bits, uint32_t* hist, uint32_t* binTotals, hipStream_t s,
-                    bool ballot, bool wide) {
+                    bool ballot, bool wide, bool scanlessOn) {
     const uint32_t grid = radix_grid_for_capacity(capacity);
     const uint32_t narrowPasses = (bits + 7) / 8;
     const uint32_t widePasses = (bits + kWideMaxBits - 1) / kWideMaxBits;
     // wide digits where they save a whole pass (32-bit keys: 3 passes of 11/11/10 bits instead of 4)
     const bool useWide = wide && widePasses < narrowPasses;
     const uint32_t passes = useWide ? widePasses : narrowPasses;
-    const bool scanless = !useWide && scanless_sort() && passes % 2 == 0;
+    const bool scanless = !useWide && scanlessOn && passes % 2 == 0;
     int cur = 0;
     uint32_t done = 0;
     for (uint32_t p = 0; p < passes; ++p) {
@@ -1000,7 +996,8 @@ int radix_sort_bits(uint32_t* keys[2], uint32_t* vals[2], const uint32_t* nPtr, 
 // first pass's at +256, its bucket starts at +512 (narrow); the wide pass's 2048 totals.
 int radix_sort_tiles(uint32_t* keys[2], uint32_t* vals[2], const uint32_t* nPtr, uint32_t capacity, uint32_t shift,
                      uint32_t* hist, uint32_t* binTotals, uint32_t* tileStart, uint32_t tileBase, uint32_t numTiles,
-                     uint32_t allTiles, hipStream_t s, bool ballot, int loBits, bool wide, bool wide12) {
+                     uint32_t allTiles, hipStream_t s, bool ballot, int loBits, bool wide, bool wide12,
+                     bool scanlessOn) {
     const uint32_t grid = radix_grid_for_capacity(capacity);
     auto bitsFor = [](uint32_t tiles) {
         uint32_t b = 1;
@@ -1027,7 +1024,7 @@ int radix_sort_tiles(uint32_t* keys[2], uint32_t* vals[2], const uint32_t* nPtr,
     const uint32_t hi = bits - lo < 4u ? 4u : bits - lo;  // (a digit wider than the bits left reads zeros)
     TileStarts first{};
     first.bucketStartOut = binTotals + 512;
-    const bool scanless = scanless_sort();
+    const bool scanless = scanlessOn;
     radix_pass(keys[0], vals[0], keys[1], vals[1], nPtr, grid, shift, (int)lo, hist, binTotals + 256, s, ballot,
                &first, false, scanless ? 0 : -1);
     ts.bucketStart = binTotals + 512;
@@ -1426,6 +1423,8 @@ Tuning tuning_from_env(int device) {
     t.blendClaim = !cv ? 1 : std::strcmp(cv, "early") == 0 ? 0 : std::strcmp(cv, "auto") == 0 ? 2 : 1;
     const char* ws = getenv("GSM_SORT_WIDE");
     t.wideSort = !(ws && ws[0] == '0');
+    const char* sc = getenv("GSM_SORT_SCAN");
+    t.sortScanless = !(sc && std::strcmp(sc, "kernel") == 0);
     const char* mp = getenv("GSM_MG_PIXELS");
     t.mgPixelsWB = !(mp && std::strcmp(mp, "wt") == 0);
     const char* mpg = getenv("GSM_MG_PUSH_GRID");

@@ -180,6 +180,35 @@ def test_radix_sort_variants(gsm, cuda, variant, monkeypatch):
             np.testing.assert_array_equal(v.cpu().numpy(), np.argsort(keys, kind="stable"))
 
 
+@pytest.mark.parametrize("scan", ["none", "kernel"])
+def test_radix_sort_scanless_and_scan_kernel(gsm, cuda, oracle, scan, monkeypatch):
+    """Narrow passes with (GSM_SORT_SCAN=kernel) and without (default, r05) the k_radix_scan launch give
+    the same stable order: stand-alone sorts of 1..4 digits (even digit counts take the alternating
+    super-group row sets, odd ones the scan; repeated sorts find the rows zeroed again), and a 1080p
+    frame (two narrow tile passes) rendered bit for bit three times on one renderer."""
+    monkeypatch.setenv("GSM_SORT_SCAN", scan)
+    rng = np.random.default_rng(17)
+    for n, bits in [(3, 32), (4096, 8), (70_000, 16), (1_000_003, 24), (2_500_000, 32), (4_194_304, 32)]:
+        keys = rng.integers(0, 2 ** bits, n, dtype=np.uint64).astype(np.uint32)
+        keys[: n // 5] = keys[n // 2]
+        for _ in range(2):
+            k = cuda.from_numpy(keys.view(np.int32).copy()).cuda()
+            v = cuda.arange(n, dtype=cuda.int32, device="cuda")
+            gsm.sort_pairs_u32(k, v, key_bits=bits)
+            np.testing.assert_array_equal(k.cpu().numpy().view(np.uint32), np.sort(keys, kind="stable"))
+            np.testing.assert_array_equal(v.cpu().numpy(), np.argsort(keys, kind="stable"))
+    case = _synth(200_000, 1920, 1080, 4, 1, 29)
+    r = oracle_render(oracle, case)
+    g = gpu_render(gsm, cuda, case, keep=False)
+    monkeypatch.delenv("GSM_SORT_SCAN")
+    assert_frame_equal(g, r)
+    for _ in range(2):
+        g2 = gpu_render(gsm, cuda, case, renderer=g["renderer"], keep=False)
+        assert np.array_equal(g["color"], g2["color"])
+        assert np.array_equal(g["depth"], g2["depth"])
+    g["renderer"].close()
+
+
 def _synth(n, w, h, sh, prec, seed, **kw):
     from gsm_amd import scenes
     world, harm, cam = scenes.gen_scene(n, w, h, sh, prec, seed=seed, **kw)

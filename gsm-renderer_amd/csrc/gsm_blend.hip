@@ -13,6 +13,7 @@
 #include <cstring>
 
 #include "../../include/gsm_renderer.h"
+#include "gsm_blend_exact.h"
 #include "gsm_detmath.h"
 #include "gsm_internal.h"
 #include "gsm_types.h"
@@ -348,6 +349,8 @@ __global__ __launch_bounds__(NT) void k_blend_px(
             T[k] = ONE;
             R[k] = G[k] = B[k] = D[k] = ZERO;
         }
+        // the unit met a record of inf / NaN fp16 depth: walked again exactly at its end (gsm_blend_exact.h)
+        bool exactD = false;
         if (count > 0) {
             h2 X[P], Yv;  // Yv: the lane's (up to) two rows
 #pragma unroll
@@ -382,6 +385,7 @@ __global__ __launch_bounds__(NT) void k_blend_px(
                 nA = pad;
                 nB = 0u;
             }
+            exactD = blend_exact::batch_depth_nonfinite(bB) || blend_exact::batch_depth_nonfinite(nB);
 
             h2 ac[U][P], om[U][P];
             uint32_t rgc[U], bdc[U], rgn[U], bdn[U], opn[U];
@@ -435,6 +439,7 @@ __global__ __launch_bounds__(NT) void k_blend_px(
                             lrecA[wv][lane] = nA;
                             lrecB[wv][lane] = nB;
                             blend_wave_sync();
+                            exactD = exactD || blend_exact::batch_depth_nonfinite(nB);
                         }
 #pragma unroll
                         for (uint32_t k = 0; k < U; ++k) {
@@ -606,6 +611,7 @@ __global__ __launch_bounds__(NT) void k_blend_px(
                     mA = *(const uint4*)(rec + nI);
                     mB = rec[nI].b;
                     nI = lst[min(base + 256u + lane, last)];
+                    exactD = exactD || blend_exact::batch_depth_nonfinite(nB);
                 };
                 uint32_t e = eC, bb = b0C;
                 ncomp = eC;
@@ -650,6 +656,7 @@ __global__ __launch_bounds__(NT) void k_blend_px(
                             lrecA[wv][lane] = nA;
                             lrecB[wv][lane] = nB;
                             blend_wave_sync();
+                            exactD = exactD || blend_exact::batch_depth_nonfinite(nB);
                         }
 #pragma unroll
                         for (uint32_t k = 0; k < U1; ++k) {
@@ -741,6 +748,9 @@ __global__ __launch_bounds__(NT) void k_blend_px(
         for (int q = 0; q < P; ++q)
             write_pair(ux + offX[q], uy + offY[q], (full > 0) ? (ONE - T[q]) : ONE, R[q], G[q], B[q], D[q]);
     unit_end:
+        if (exactD)  // (rare: a record of inf / NaN fp16 depth; every pixel of the unit is written again)
+            blend_exact::walk_unit_exact<P>((hsel ? half1 : half0) + start, count, rec, tbl, lrecA[wv], lrecB[wv], ux,
+                                            uy, thrBits, write_pair);
         if (wt && depth) {
             // every pixel pair of the unit was staged by the writes above (each exactly once); rows
             // past H were not, and are not stored

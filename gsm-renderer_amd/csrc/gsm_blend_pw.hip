@@ -22,6 +22,7 @@
 #include <type_traits>
 
 #include "../../include/gsm_renderer.h"
+#include "gsm_blend_exact.h"
 #include "gsm_detmath.h"
 #include "gsm_internal.h"
 #include "gsm_types.h"
@@ -271,6 +272,9 @@ __global__ __launch_bounds__(NT) void k_blend_pw(
             layout = 4;
         }
         bool alive = (ku ? CNT1 : CNT0) > 0u;
+        // the job met a record of inf / NaN fp16 depth: its units are walked again exactly at its end
+        // (gsm_blend_exact.h; one ballot per staged batch)
+        bool exactD = false;
 
         if (maxCnt > 0u) {
             // ---- record batches: BS entries per unit and batch (32 for pairs: lanes 0-31 unit 0, 32-63
@@ -307,6 +311,7 @@ __global__ __launch_bounds__(NT) void k_blend_pw(
                 LA[lane] = A0;
                 LB[lane] = B0;
                 pw_wave_sync();
+                exactD = blend_exact::batch_depth_nonfinite(B0) || blend_exact::batch_depth_nonfinite(B1);
             }
             // the batch at b0 + BS goes into LDS (neutral records past the lane's list); the registers
             // move one batch on
@@ -315,6 +320,7 @@ __global__ __launch_bounds__(NT) void k_blend_pw(
                 LA[lane] = make_uint4(in ? A1.x : padL.x, in ? A1.y : 0u, in ? A1.z : 0u, in ? A1.w : 0u);
                 LB[lane] = in ? B1 : 0u;
                 pw_wave_sync();
+                exactD = exactD || blend_exact::batch_depth_nonfinite(in ? B1 : 0u);
                 A1 = *(const uint4*)(rec + I2);
                 B1 = rec[I2].b;
                 I2 = gidx(b0 + 3u * BS + lo);
@@ -591,6 +597,11 @@ __global__ __launch_bounds__(NT) void k_blend_pw(
             } else {
                 pw_write_pair(tg, px, py, fullL ? ONE - T[0] : ONE, R[0], G[0], B[0], D[0]);
             }
+        }
+        if (exactD) {  // (rare) every pixel of the job's units written again
+            auto wr = [&](uint32_t x, uint32_t y, h2 A, h2 r, h2 g, h2 b, h2 d) { pw_write_pair(tg, x, y, A, r, g, b, d); };
+            if (CNT0) blend_exact::walk_unit_exact<2>(LST0, CNT0, rec, tbl, LA, LB, UX0, UY0, thrBits, wr);
+            if (pair && CNT1) blend_exact::walk_unit_exact<2>(LST1, CNT1, rec, tbl, LA, LB, UX1, UY1, thrBits, wr);
         }
         auto finishUnit = [&](uint32_t uu, uint32_t cnt, bool done, uint32_t walk) {
             const uint32_t wk = min(cnt ? (done ? walk : (cnt + 15u) / 16u * 16u) : 0u, 65535u);

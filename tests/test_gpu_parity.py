@@ -250,6 +250,55 @@ def test_edge_cases(gsm, cuda, oracle):
     assert_frame_equal(g, r)
 
 
+@pytest.mark.parametrize("env", [{}, {"GSM_BLEND_WAVES": "16"}, {"GSM_BLEND_PAIRS": "0"}])
+def test_far_gaussians_in_a_full_frame(gsm, cuda, oracle, monkeypatch, env):
+    """test_far_gaussian_fp16_depth_overflow's record (fp16 depth inf) among 60k ordinary gaussians of a
+    1080p frame: the half-tile walk and its compaction phase (k_blend_px), and at 16 waves the pair walk's
+    three layouts (k_blend_pw), all switch to the exact depth test from the batch holding it."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    case = _synth(60_000, 1920, 1080, 1, 0, 7)
+    far = np.zeros(4, case["world"].dtype)
+    far["rot"][:, 3] = 1.0
+    for i, (x, y) in enumerate([(0.0, 0.0), (30000.0, 9000.0), (-40000.0, -12000.0), (0.0, 20000.0)]):
+        far[i]["px"], far[i]["py"], far[i]["pz"], far[i]["opacity"] = x, y, 80000.0 + 5000.0 * i, 0.8
+        far[i]["sx"], far[i]["sy"], far[i]["sz"] = 3000.0, 2200.0, 3000.0
+    case["world"] = np.concatenate([case["world"][:30_000], far, case["world"][30_000:]])
+    h = case["harm"].reshape(-1, 3)
+    case["harm"] = np.concatenate([h[:30_000], np.tile([[0.2, 0.1, -0.3]], (4, 1)).astype(h.dtype), h[30_000:]]).reshape(-1)
+    case["max_gaussians"] = len(case["world"])
+    r = oracle_render(oracle, case)
+    assert all(r["mask"][30_000:30_004] == 1)
+    g = gpu_render(gsm, cuda, case, keep=False)
+    for k in env:
+        monkeypatch.delenv(k)
+    assert_frame_equal(g, r)
+    g["renderer"].close()
+
+
+def test_far_gaussian_fp16_depth_overflow(gsm, cuda, oracle):
+    """A gaussian whose view depth overflows fp16 (record depth +inf; the Global path has no far-plane
+    cull): where its alphas are nonzero the reference's depth becomes inf / NaN (inf * 0), and a 4x2
+    group whose alphas are all zero skips the entry (GlobalShaders.metal:1133) and keeps its depth."""
+    from gsm_amd.types import WORLD32
+    w = np.zeros(3, WORLD32)
+    w["rot"][:, 3] = 1.0
+    # 0: near, small; 1: at depth 80000 (fp16 inf), wide enough to cover ~60 px; 2: near, large
+    w[0]["px"], w[0]["py"], w[0]["pz"], w[0]["opacity"] = 0.1, 0.05, 3.0, 0.6
+    w[0]["sx"], w[0]["sy"], w[0]["sz"] = 0.05, 0.04, 0.05
+    w[1]["px"], w[1]["py"], w[1]["pz"], w[1]["opacity"] = 0.0, 0.0, 80000.0, 0.9
+    w[1]["sx"], w[1]["sy"], w[1]["sz"] = 3000.0, 2500.0, 3000.0
+    w[2]["px"], w[2]["py"], w[2]["pz"], w[2]["opacity"] = -0.2, 0.1, 4.0, 0.3
+    w[2]["sx"], w[2]["sy"], w[2]["sz"] = 0.5, 0.3, 0.2
+    harm = np.tile(np.array([0.3, -0.2, 0.8], np.float32), 3)
+    cam = oracle.make_camera(640, 360)
+    case = dict(world=w, harm=harm, sh=1, cam=cam, width=640, height=360, max_gaussians=3)
+    r = oracle_render(oracle, case)
+    assert r["mask"][1] == 1
+    g = gpu_render(gsm, cuda, case)
+    assert_frame_equal(g, r)
+
+
 def test_frame_smaller_than_max_and_reuse(gsm, cuda, oracle):
     """width/height < maxWidth/maxHeight (tile grid from the max dims, GlobalRenderer.swift:25-51),
     then a second, different frame on the same renderer (no stale state)."""

@@ -245,6 +245,24 @@ def test_df_sort_switches(gsm, cuda, oracle, monkeypatch, env):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("kind,n,w,h,sh,seed", [("f16", 30_000, 360, 400, 9, 21), ("f32", 20_000, 250, 170, 1, 22),
+                                                 ("f16", 40_000, 640, 480, 16, 23)])
+def test_df_adversarial_scenes_bit_exact(gsm, cuda, oracle, kind, n, w, h, sh, seed):
+    """The Global path's adversarial inputs (tests/adversarial.py: zero / extreme / inf / NaN scales,
+    positions and quaternions, opacities around the cull and outside [0, 1], huge / NaN SH) through the
+    DepthFirst stereo frame: every intermediate and the side-by-side target bit for bit."""
+    import adversarial
+    case = adversarial.scene(kind, n, w, h, sh, seed)
+    L, R = _cams(w, h)
+    mg = case["max_gaussians"]  # (4 n: room for the large splats' instances, 4 x max_gaussians)
+    r = oracle.df_render_stereo(case["world"], case["harm"], sh, L, R, w, h, max_gaussians=mg)
+    assert r["status"] == 0 and r["overflow"] == 0
+    g = gpu_df(gsm, cuda, case["world"], case["harm"], sh, L, R, w, h, max_gaussians=mg)
+    assert_df_equal(g, r)
+    g["renderer"].close()
+
+
+@pytest.mark.gpu
 def test_df_scene_transform(gsm, cuda, oracle):
     n, w, h = 15000, 240, 200
     world, harm = _scene(n, w, h, 9, 1, 12)

@@ -276,6 +276,32 @@ def test_far_gaussians_in_a_full_frame(gsm, cuda, oracle, monkeypatch, env):
     g["renderer"].close()
 
 
+@pytest.mark.parametrize("kind,n,w,h,sh,seed,env", [
+    ("f32", 20_000, 640, 360, 16, 5, {}), ("f16", 20_000, 640, 360, 16, 6, {}),
+    ("f32", 40_000, 1920, 1080, 1, 7, {}), ("f16", 60_000, 1920, 1080, 9, 8, {}),
+    ("f16", 60_000, 1920, 1080, 16, 9, {"GSM_BLEND_WAVES": "16"}),
+    ("f32", 30_000, 1280, 720, 4, 10, {"GSM_SORT_SCAN": "kernel"}),
+    ("f16", 60_000, 1920, 1080, 9, 11, {"overflow": True}),
+])
+def test_adversarial_scenes_bit_exact(gsm, cuda, oracle, monkeypatch, kind, n, w, h, sh, seed, env):
+    """Ordinary gaussians with a quarter of them given edge values (tests/adversarial.py: zero / extreme /
+    inf / NaN scales, positions and quaternions, opacities around the 0.005 cull and outside [0, 1],
+    huge / NaN SH coefficients, a few large close splats): every intermediate bit for bit."""
+    import adversarial
+    env = dict(env)
+    overflow = env.pop("overflow", False)  # (max_gaussians = n: the assignments pass the 4 n cap)
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    case = adversarial.scene(kind, n, w, h, sh, seed, overflow)
+    r = oracle_render(oracle, case)
+    assert r["overflow"] == (1 if overflow else 0)
+    g = gpu_render(gsm, cuda, case)
+    for k in env:
+        monkeypatch.delenv(k)
+    assert_frame_equal(g, r)
+    g["renderer"].close()
+
+
 def test_far_gaussian_fp16_depth_overflow(gsm, cuda, oracle):
     """A gaussian whose view depth overflows fp16 (record depth +inf; the Global path has no far-plane
     cull): where its alphas are nonzero the reference's depth becomes inf / NaN (inf * 0), and a 4x2
@@ -374,23 +400,30 @@ def test_tile_row_slabs_compose_to_full_frame(gsm, cuda, oracle):
     rend.close()
 
 
-@pytest.mark.parametrize("world,n,w,h,prec", [(2, 40_000, 640, 360, 1), (3, 60_000, 1280, 720, 1),
-                                              (8, 50_000, 640, 360, 0)])
-def test_partitioned_frame_matches_single_gpu(gsm, cuda, oracle, world, n, w, h, prec):
+@pytest.mark.parametrize("world,n,w,h,prec,adv", [(2, 40_000, 640, 360, 1, False), (3, 60_000, 1280, 720, 1, False),
+                                                  (8, 50_000, 640, 360, 0, False), (4, 40_000, 1280, 720, 1, True),
+                                                  (3, 30_000, 640, 360, 0, True)])
+def test_partitioned_frame_matches_single_gpu(gsm, cuda, oracle, world, n, w, h, prec, adv):
     """All-to-all slab partition (include/gsm_multigpu.h) over `world` virtual
     ranks on one GPU: every rank projects its id range once, records are exchanged in
     source-rank order (gsm_amd.exchange.emulate = the order the real all_to_all delivers,
     checked with gloo in test_exchange_distributed), every slab is rendered from its
     records.  The composed frame equals the single-GPU frame and the oracle bit for bit."""
     from gsm_amd import exchange
-    case = _synth(n, w, h, 16 if prec else 4, prec, 77)
+    if adv:  # tests/adversarial.py's edge values (test_adversarial_scenes_bit_exact) through the partition
+        import adversarial
+        case = adversarial.scene("f16" if prec else "f32", n, w, h, 16 if prec else 4, 31 + world)
+    else:
+        case = _synth(n, w, h, 16 if prec else 4, prec, 77)
+    mg = case["max_gaussians"]
     r = oracle_render(oracle, case)
+    assert r["overflow"] == 0
     full = gpu_render(gsm, cuda, case, keep=False)
     full["renderer"].close()
     assert np.array_equal(full["color"], r["color"])
     tiles_y = r["tiles_y"]
     rows = exchange.slab_rows(tiles_y, h, world)
-    cfg = gsm.RendererConfig(max_gaussians=n, max_width=w, max_height=h, precision=prec, gaussian_color_space=0)
+    cfg = gsm.RendererConfig(max_gaussians=mg, max_width=w, max_height=h, precision=prec, gaussian_color_space=0)
     ranks = [gsm.GlobalRenderer(config=cfg) for _ in range(world)]
     wt, ht = to_dev(cuda, case["world"]), to_dev(cuda, case["harm"])
     inp = gsm.GaussianInput(wt, ht, n, case["sh"])

@@ -302,6 +302,63 @@ def test_adversarial_scenes_bit_exact(gsm, cuda, oracle, monkeypatch, kind, n, w
     g["renderer"].close()
 
 
+def _random_camera(w, h, seed):
+    """make_camera's projection with a random orientation (QR of a normal matrix) at a random point
+    within 8 units of the scene's centre (0, 0, 5.5) -- views from inside the cloud, from behind it,
+    rolled, looking away."""
+    from gsm_amd import scenes
+    rng = np.random.default_rng(seed)
+    pos = (np.array([0, 0, 5.5]) + rng.normal(size=3) * 3.0).astype(np.float32)
+    if seed % 3 == 0:  # any orientation (often looking away from most of the cloud)
+        q, r = np.linalg.qr(rng.normal(size=(3, 3)))
+        R = q * np.sign(np.diag(r))
+        if np.linalg.det(R) < 0:
+            R[:, 0] = -R[:, 0]
+    else:  # towards a point near the centre, rolled (camera looks along +z of its frame)
+        fwd = np.array([0, 0, 5.5]) + rng.normal(size=3) * 1.5 - pos
+        fwd /= np.linalg.norm(fwd)
+        right = np.cross([0.0, 1.0, 0.0], fwd)
+        right /= np.linalg.norm(right)
+        up = np.cross(fwd, right)
+        a = rng.uniform(-np.pi, np.pi)
+        R = np.stack([np.cos(a) * right + np.sin(a) * up, -np.sin(a) * right + np.cos(a) * up, fwd], axis=1)
+    R = R.astype(np.float32)
+    V = np.eye(4, dtype=np.float32)
+    V[:3, :3] = R.T
+    V[:3, 3] = -(R.T @ pos)
+    cam = scenes.make_camera(w, h)
+    cam["view"] = V.T.reshape(-1).astype(np.float32)
+    cam["position"] = pos
+    return cam
+
+
+@pytest.mark.parametrize("seed,w,h,maxw,maxh,sh,prec,cs", [
+    (1, 1000, 555, 1024, 600, 16, 1, 0), (2, 333, 777, 333, 777, 9, 0, 1), (3, 1921, 1081, 1921, 1081, 4, 1, 1),
+    (4, 97, 45, 640, 360, 1, 0, 0), (5, 1280, 720, 1920, 1080, 16, 1, 0), (6, 2000, 300, 2000, 300, 9, 1, 1),
+])
+def test_random_cameras_ragged_frames(gsm, cuda, oracle, seed, w, h, maxw, maxh, sh, prec, cs):
+    """Random camera poses over ragged frame sizes (not multiples of the 32x16 tile, frames smaller than
+    the renderer's maximum, 97x45 to 2000x300), every SH degree, both input precisions, sRGB input --
+    every intermediate bit for bit."""
+    case = _synth(80_000, w, h, sh, prec, 100 + seed, spread=1.5)
+    case.update(cam=_random_camera(w, h, seed), max_width=maxw, max_height=maxh, color_space=cs)
+    r = oracle_render(oracle, case)
+    g = gpu_render(gsm, cuda, case)
+    assert_frame_equal(g, r)
+    g["renderer"].close()
+
+
+@pytest.mark.parametrize("n", [8192 * 256, 8192 * 256 + 1])
+def test_fused_scan_threshold(gsm, cuda, oracle, n):
+    """The last frame size whose block counts the scatter workgroups add up themselves (8192 projection
+    blocks, kFusedScanMaxBlocks) and the first one that takes the k_scan_blocks launch: both bit-exact."""
+    case = _synth(n, 320, 180, 1, 1, 41, scale_px=0.6)
+    r = oracle_render(oracle, case)
+    g = gpu_render(gsm, cuda, case, keep=False)
+    assert_frame_equal(g, r)
+    g["renderer"].close()
+
+
 def test_far_gaussian_fp16_depth_overflow(gsm, cuda, oracle):
     """A gaussian whose view depth overflows fp16 (record depth +inf; the Global path has no far-plane
     cull): where its alphas are nonzero the reference's depth becomes inf / NaN (inf * 0), and a 4x2

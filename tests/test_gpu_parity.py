@@ -348,6 +348,26 @@ def test_random_cameras_ragged_frames(gsm, cuda, oracle, seed, w, h, maxw, maxh,
     g["renderer"].close()
 
 
+@pytest.mark.parametrize("w,h", [
+    (512, 256),    # 256 tiles: one narrow tile pass
+    (544, 256),    # 272 tiles: two passes / one wide pass
+    (2048, 512),   # 2048 tiles: the last quadrant-unit frame and the last one-wide-pass field
+    (1600, 656),   # 2050 tiles: half-tile units, two narrow tile passes
+    (2048, 768),   # 3072 tiles = 6144 half-tile units: the 12-wave blend's first frame
+    (2016, 768),   # 3024 tiles: 8 waves
+    (4096, 1536),  # 12288 tiles = 24576 units: the 16-wave pair-walk blend's first frame
+])
+def test_kernel_shape_thresholds(gsm, cuda, oracle, w, h):
+    """Frames on both sides of every size rule that changes the kernels (one vs two narrow tile passes,
+    the wide pass's 2048 tiles, quadrant vs half-tile blend units at 8 tiles per CU, 8 / 12 / 16 blend
+    waves and the pair walk at 2 / 6 units per wave slot on 256 CUs): every intermediate bit for bit."""
+    case = _synth(60_000, w, h, 4, 1, 43, spread=1.2)
+    r = oracle_render(oracle, case)
+    g = gpu_render(gsm, cuda, case, keep=False)
+    assert_frame_equal(g, r)
+    g["renderer"].close()
+
+
 @pytest.mark.parametrize("n", [8192 * 256, 8192 * 256 + 1])
 def test_fused_scan_threshold(gsm, cuda, oracle, n):
     """The last frame size whose block counts the scatter workgroups add up themselves (8192 projection

@@ -616,6 +616,30 @@ def test_create_time_switches_frames_match(gsm, cuda, oracle, monkeypatch, env):
     g["renderer"].close()
 
 
+@pytest.mark.parametrize("fused", ["1", "0"])
+def test_scan_modes_frame_sequence(gsm, cuda, oracle, monkeypatch, fused):
+    """The block-count scan (GSM_SCAN_FUSED, read at create): the scatter adding up every earlier block
+    count (default up to 8192 blocks) or the k_scan_blocks launch.  One renderer renders a sequence of
+    different frames -- several sizes, an empty frame in between (no projection blocks: the scan kernel
+    writes its header) -- each bit for bit against the oracle."""
+    monkeypatch.setenv("GSM_SCAN_FUSED", fused)
+    cases = [_synth(200_000, 1280, 720, 16, 1, 51), _synth(40_000, 1280, 720, 4, 1, 52),
+             _synth(200_000, 1280, 720, 16, 1, 53), _synth(9_000, 1280, 720, 9, 1, 54)]
+    for c in cases:
+        c["max_gaussians"] = 300_000
+    empty = dict(cases[1])
+    empty["count"] = 0
+    seq = [cases[0], cases[1], empty, cases[2], cases[3], empty, cases[0]]
+    renderer = None
+    for c in seq:
+        r = oracle_render(oracle, c)
+        g = gpu_render(gsm, cuda, c, renderer=renderer, keep=False)
+        renderer = g["renderer"]
+        monkeypatch.delenv("GSM_SCAN_FUSED", raising=False)
+        assert_frame_equal(g, r)
+    renderer.close()
+
+
 @pytest.mark.parametrize("env", [{"GSM_BLEND_WAVES": "16"}, {"GSM_BLEND_WAVES": "16", "GSM_BLEND_PAIR_SPLIT": "1"},
                                  {"GSM_BLEND_WAVES": "16", "GSM_BLEND_PAIR_SPLIT": "256"},
                                  {"GSM_BLEND_WAVES": "16", "GSM_BLEND_PAIR_SPLIT": "200"},

@@ -442,6 +442,25 @@ __global__ __launch_bounds__(kRadixBlock) void k_radix_downsweep(
 }
 
 // ---------------------------------------------------------------------------
+// Wide passes take chunks of kWideChunk keys (GSM_WIDE_ITEMS per thread): their per-chunk digit
+// bookkeeping is heavier, so their blocks are fewer per CU.
+#ifndef GSM_WIDE_ITEMS
+#define GSM_WIDE_ITEMS 16
+#endif
+constexpr int kWideItems = GSM_WIDE_ITEMS;
+constexpr int kWideChunk = kRadixBlock * kWideItems;
+static_assert(kWideItems % 4 == 0 && kWideItems <= kRadixItems, "wide chunks: 16-B loads, <= the narrow chunk");
+__device__ __forceinline__ void block_range_w(uint32_t n, uint32_t grid, uint32_t b, uint32_t* begin, uint32_t* end) {
+    uint32_t per = (n + grid - 1) / grid;
+    per = (per + kWideChunk - 1) / kWideChunk * kWideChunk;
+    uint64_t bb = (uint64_t)per * b;
+    uint64_t ee = bb + per;
+    if (bb > n) bb = n;
+    if (ee > n) ee = n;
+    *begin = (uint32_t)bb;
+    *end = (uint32_t)ee;
+}
+
 // Wide digits (9..11 bits, up to 2048 bins): one pass where the narrow kernels need two -- the tile
 // field of a frame with <= 2048 tiles in its rows (a multi-GPU slab, keys counted relative to the
 // slab's first tile), and the DepthFirst depth sort's 32-bit keys (3 passes of 11/11/10 bits).
@@ -464,27 +483,27 @@ __global__ __launch_bounds__(kRadixBlock) void k_wide_upsweep(const uint32_t* __
     // one counter array: a histogram needs no order, and 2^BITS bins spread the atomics
     __shared__ uint32_t cnt[R];
     uint32_t begin, end;
-    block_range(*nPtr, gridDim.x, blockIdx.x, &begin, &end);
+    block_range_w(*nPtr, gridDim.x, blockIdx.x, &begin, &end);
     if (begin >= end) return;  // no row: k_wide_scan reads the active blocks' rows only
     for (uint32_t i = threadIdx.x; i < R; i += kRadixBlock) cnt[i] = 0;
     __syncthreads();
-    auto load_chunk = [&](uint32_t cbase, uint4 (&q)[kRadixItems / 4]) {
+    auto load_chunk = [&](uint32_t cbase, uint4 (&q)[kWideItems / 4]) {
 #pragma unroll
-        for (int i = 0; i < kRadixItems / 4; ++i) {
+        for (int i = 0; i < kWideItems / 4; ++i) {
             const uint32_t idx = cbase + (uint32_t)(i * kRadixBlock + threadIdx.x) * 4u;
             q[i] = idx + 3u < end ? *(const uint4*)(keys + idx)
                                   : make_uint4(idx < end ? keys[idx] : 0u, idx + 1u < end ? keys[idx + 1u] : 0u,
                                                idx + 2u < end ? keys[idx + 2u] : 0u, 0u);
         }
     };
-    uint4 q[kRadixItems / 4];
+    uint4 q[kWideItems / 4];
     if (begin < end) load_chunk(begin, q);
-    for (uint32_t cbase = begin; cbase < end; cbase += kRadixChunk) {
-        uint4 nq[kRadixItems / 4];
-        const bool more = cbase + kRadixChunk < end;
-        if (more) load_chunk(cbase + kRadixChunk, nq);
+    for (uint32_t cbase = begin; cbase < end; cbase += kWideChunk) {
+        uint4 nq[kWideItems / 4];
+        const bool more = cbase + kWideChunk < end;
+        if (more) load_chunk(cbase + kWideChunk, nq);
 #pragma unroll
-        for (int i = 0; i < kRadixItems / 4; ++i) {
+        for (int i = 0; i < kWideItems / 4; ++i) {
             const uint32_t idx = cbase + (uint32_t)(i * kRadixBlock + threadIdx.x) * 4u;
             const uint32_t kk[4] = {q[i].x, q[i].y, q[i].z, q[i].w};
 #pragma unroll
@@ -493,7 +512,7 @@ __global__ __launch_bounds__(kRadixBlock) void k_wide_upsweep(const uint32_t* __
         }
         if (more) {
 #pragma unroll
-            for (int i = 0; i < kRadixItems / 4; ++i) q[i] = nq[i];
+            for (int i = 0; i < kWideItems / 4; ++i) q[i] = nq[i];
         }
     }
     __syncthreads();
@@ -516,7 +535,7 @@ __global__ __launch_bounds__(256) void k_wide_scan(uint32_t* __restrict__ hist, 
     // active blocks, as block_range splits n: block b holds keys iff b * per < n
     const uint32_t n = *nPtr;
     uint32_t per = (n + grid - 1) / grid;
-    per = (per + kRadixChunk - 1) / kRadixChunk * kRadixChunk;
+    per = (per + kWideChunk - 1) / kWideChunk * kWideChunk;
     const uint32_t active = per ? min(grid, (n + per - 1) / per) : 0u;
     const uint32_t j = threadIdx.x % kWideScanDigits, sg = threadIdx.x / kWideScanDigits;
     const uint32_t d = blockIdx.x * kWideScanDigits + j;
@@ -595,13 +614,13 @@ __global__ __launch_bounds__(kRadixBlock) void k_wide_downsweep(
     static_assert(DPT >= 2 && DPT <= 8, "wide digits: 9..11 bits (12: k_wide12_downsweep)");
     __shared__ __attribute__((aligned(16))) uint32_t waveCnt[kWaves][RP];  // ranks, then each wave's LDS start per digit
     __shared__ uint32_t adj[RP];               // per digit: global destination minus LDS start
-    __shared__ uint32_t sKeys[kRadixChunk];
-    __shared__ uint32_t sVals[kRadixChunk];
+    __shared__ uint32_t sKeys[kWideChunk];
+    __shared__ uint32_t sVals[kWideChunk];
     __shared__ uint32_t part[kWaves];
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
     const uint32_t n = *nPtr;
     uint32_t begin, end;
-    block_range(n, gridDim.x, blockIdx.x, &begin, &end);
+    block_range_w(n, gridDim.x, blockIdx.x, &begin, &end);
     const uint32_t d0 = tid * DPT;  // this thread's digits
     auto zero_counters = [&]() {    // 16-byte stores
         static_assert((kWaves * RP) % (4 * kRadixBlock) == 0, "counter rows in whole uint4 rounds");
@@ -640,18 +659,18 @@ __global__ __launch_bounds__(kRadixBlock) void k_wide_downsweep(
     }
 
     const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-    for (uint32_t cbase = begin; cbase < end; cbase += kRadixChunk) {
-        uint32_t k[kRadixItems], v[kRadixItems], rank[kRadixItems];
+    for (uint32_t cbase = begin; cbase < end; cbase += kWideChunk) {
+        uint32_t k[kWideItems], v[kWideItems], rank[kWideItems];
 #pragma unroll
-        for (int j = 0; j < kRadixItems; ++j) {
-            const uint32_t idx = cbase + wave * (64 * kRadixItems) + j * 64 + lane;
+        for (int j = 0; j < kWideItems; ++j) {
+            const uint32_t idx = cbase + wave * (64 * kWideItems) + j * 64 + lane;
             const bool valid = idx < end;
             k[j] = valid ? keysIn[idx] : 0u;
             v[j] = valid ? valsIn[idx] : 0u;
         }
 #pragma unroll
-        for (int j = 0; j < kRadixItems; ++j) {
-            const uint32_t idx = cbase + wave * (64 * kRadixItems) + j * 64 + lane;
+        for (int j = 0; j < kWideItems; ++j) {
+            const uint32_t idx = cbase + wave * (64 * kWideItems) + j * 64 + lane;
             const bool valid = idx < end;
             const uint32_t d = ((k[j] >> shift) - base) & (R - 1u);
             if constexpr (BALLOT) {
@@ -693,8 +712,8 @@ __global__ __launch_bounds__(kRadixBlock) void k_wide_downsweep(
         }
         __syncthreads();
 #pragma unroll
-        for (int j = 0; j < kRadixItems; ++j) {
-            const uint32_t idx = cbase + wave * (64 * kRadixItems) + j * 64 + lane;
+        for (int j = 0; j < kWideItems; ++j) {
+            const uint32_t idx = cbase + wave * (64 * kWideItems) + j * 64 + lane;
             if (idx < end) {
                 const uint32_t pos = waveCnt[wave][wide_pad(((k[j] >> shift) - base) & (R - 1u))] + rank[j];
                 sKeys[pos] = k[j];
@@ -703,7 +722,7 @@ __global__ __launch_bounds__(kRadixBlock) void k_wide_downsweep(
         }
         __syncthreads();
         zero_counters();
-        const uint32_t cn = min((uint32_t)kRadixChunk, end - cbase);
+        const uint32_t cn = min((uint32_t)kWideChunk, end - cbase);
         for (uint32_t p = tid; p < cn; p += kRadixBlock) {
             const uint32_t key = sKeys[p];
             const uint32_t dst = adj[wide_pad(((key >> shift) - base) & (R - 1u))] + p;
@@ -730,16 +749,16 @@ __global__ __launch_bounds__(kRadixBlock) void k_wide12_downsweep(
     constexpr uint32_t RWP = (R / 2 + R / 16 + 255u) / 256u * 256u;           // padded words per wave: 2304
     static_assert(kWaves * RWP >= R + R / 8, "the digits' offsets fit over the counters");
     static_assert((kWaves * RWP) % (4 * kRadixBlock) == 0, "counter rows in whole uint4 rounds");
-    static_assert(kRadixItems * 64 < 65536, "a wave's count of one digit fits 16 bits");
+    static_assert(kWideItems * 64 < 65536, "a wave's count of one digit fits 16 bits");
     __shared__ __attribute__((aligned(16))) uint32_t cnt[kWaves][RWP];
-    __shared__ uint32_t sKeys[kRadixChunk];
-    __shared__ uint32_t sVals[kRadixChunk];
+    __shared__ uint32_t sKeys[kWideChunk];
+    __shared__ uint32_t sVals[kWideChunk];
     __shared__ uint32_t part[kWaves];
     uint32_t* adj = &cnt[0][0];  // after the LDS scatter: digit d's global destination minus LDS start, at wide_pad(d)
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
     const uint32_t n = *nPtr;
     uint32_t begin, end;
-    block_range(n, gridDim.x, blockIdx.x, &begin, &end);
+    block_range_w(n, gridDim.x, blockIdx.x, &begin, &end);
     const uint32_t d0 = tid * DPT, w0 = tid * WPT;  // this thread's digits and counter words
     auto zero_counters = [&]() {
         uint4* z = (uint4*)&cnt[0][0];
@@ -773,18 +792,18 @@ __global__ __launch_bounds__(kRadixBlock) void k_wide12_downsweep(
         __syncthreads();
     }
     const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-    for (uint32_t cbase = begin; cbase < end; cbase += kRadixChunk) {
-        uint32_t k[kRadixItems], v[kRadixItems], rank[kRadixItems];
+    for (uint32_t cbase = begin; cbase < end; cbase += kWideChunk) {
+        uint32_t k[kWideItems], v[kWideItems], rank[kWideItems];
 #pragma unroll
-        for (int j = 0; j < kRadixItems; ++j) {
-            const uint32_t idx = cbase + wave * (64 * kRadixItems) + j * 64 + lane;
+        for (int j = 0; j < kWideItems; ++j) {
+            const uint32_t idx = cbase + wave * (64 * kWideItems) + j * 64 + lane;
             const bool valid = idx < end;
             k[j] = valid ? keysIn[idx] : 0u;
             v[j] = valid ? valsIn[idx] : 0u;
         }
 #pragma unroll
-        for (int j = 0; j < kRadixItems; ++j) {
-            const uint32_t idx = cbase + wave * (64 * kRadixItems) + j * 64 + lane;
+        for (int j = 0; j < kWideItems; ++j) {
+            const uint32_t idx = cbase + wave * (64 * kWideItems) + j * 64 + lane;
             const bool valid = idx < end;
             const uint32_t d = ((k[j] >> shift) - base) & (R - 1u);
             uint32_t* word = &cnt[wave][wide_pad(d >> 1)];
@@ -834,8 +853,8 @@ __global__ __launch_bounds__(kRadixBlock) void k_wide12_downsweep(
         }
         __syncthreads();
 #pragma unroll
-        for (int j = 0; j < kRadixItems; ++j) {
-            const uint32_t idx = cbase + wave * (64 * kRadixItems) + j * 64 + lane;
+        for (int j = 0; j < kWideItems; ++j) {
+            const uint32_t idx = cbase + wave * (64 * kWideItems) + j * 64 + lane;
             if (idx < end) {
                 const uint32_t d = ((k[j] >> shift) - base) & (R - 1u);
                 const uint32_t pos = ((cnt[wave][wide_pad(d >> 1)] >> ((d & 1u) * 16u)) & 0xFFFFu) + rank[j];
@@ -847,7 +866,7 @@ __global__ __launch_bounds__(kRadixBlock) void k_wide12_downsweep(
 #pragma unroll
         for (uint32_t i = 0; i < DPT; ++i) adj[wide_pad(d0 + i)] = adjR[i];
         __syncthreads();
-        const uint32_t cn = min((uint32_t)kRadixChunk, end - cbase);
+        const uint32_t cn = min((uint32_t)kWideChunk, end - cbase);
         for (uint32_t p = tid; p < cn; p += kRadixBlock) {
             const uint32_t key = sKeys[p];
             const uint32_t dst = adj[wide_pad(((key >> shift) - base) & (R - 1u))] + p;
@@ -858,6 +877,13 @@ __global__ __launch_bounds__(kRadixBlock) void k_wide12_downsweep(
         zero_counters();
         __syncthreads();
     }
+}
+
+static uint32_t wide_grid_for_capacity(uint32_t capacity) {
+    uint32_t g = (capacity + kWideChunk - 1) / kWideChunk;  // (<= 1024 rows: radix_workspace_bytes)
+    if (g > 1024) g = 1024;
+    if (g < 1) g = 1;
+    return g;
 }
 
 static void wide_pass(uint32_t* kin, uint32_t* vin, uint32_t* kout, uint32_t* vout, const uint32_t* nPtr,
@@ -894,7 +920,8 @@ static void wide_pass(uint32_t* kin, uint32_t* vin, uint32_t* kout, uint32_t* vo
 
 size_t radix_workspace_bytes(uint32_t capacity) {
     // the scanless super-group row sets (zero at allocation; see kSuperGroup), then the per-block digit counts: <= 1024 blocks x 256 digits (narrow), x 2048 (wide)
-    const size_t wide = (size_t)(kWide12Bins + kWideRowPad) * radix_grid_for_capacity(capacity) * sizeof(uint32_t);
+    const uint32_t g = std::max(radix_grid_for_capacity(capacity), wide_grid_for_capacity(capacity));
+    const size_t wide = (size_t)(kWide12Bins + kWideRowPad) * g * sizeof(uint32_t);
     return kSuperWords * sizeof(uint32_t) + (wide > (size_t)256 * 1024 * 4 ? wide : (size_t)256 * 1024 * sizeof(uint32_t));
 }
 
@@ -975,7 +1002,7 @@ int radix_sort_bits(uint32_t* keys[2], uint32_t* vals[2], const uint32_t* nPtr, 
         uint32_t b = (bits - done + (passes - p) - 1) / (passes - p);
         if (useWide) {
             if (b < 9) b = 9;
-            wide_pass(keys[cur], vals[cur], keys[cur ^ 1], vals[cur ^ 1], nPtr, grid, shift + done, 0u, (int)b, hist,
+            wide_pass(keys[cur], vals[cur], keys[cur ^ 1], vals[cur ^ 1], nPtr, wide_grid_for_capacity(capacity), shift + done, 0u, (int)b, hist,
                       binTotals, s, ballot, false, nullptr, 0u, 0u);
         } else {
             if (b < 4) b = 4;
@@ -1007,7 +1034,7 @@ int radix_sort_tiles(uint32_t* keys[2], uint32_t* vals[2], const uint32_t* nPtr,
     uint32_t bits = bitsFor(allTiles);
     const uint32_t localBits = bitsFor(numTiles);
     if (wide && bits > 8 && (localBits <= kWideMaxBits || (wide12 && localBits == kWide12Bits))) {
-        wide_pass(keys[0], vals[0], keys[1], vals[1], nPtr, grid, shift, tileBase, (int)(localBits < 9 ? 9 : localBits),
+        wide_pass(keys[0], vals[0], keys[1], vals[1], nPtr, wide_grid_for_capacity(capacity), shift, tileBase, (int)(localBits < 9 ? 9 : localBits),
                   hist, binTotals, s, ballot, true, tileStart, numTiles, allTiles);
         return 1;
     }

@@ -25,6 +25,11 @@
 #ifndef GSM_DF_EXEC_ALIVE
 #define GSM_DF_EXEC_ALIVE 1
 #endif
+// the blend's wave-uniform "every alpha is 0" test: 0 = integer range test (df_all_cut), 1 = packed
+// minimum and two compares (df_some_uncut)
+#ifndef GSM_DF_CUT_TEST
+#define GSM_DF_CUT_TEST 1
+#endif
 
 namespace gsm {
 
@@ -436,6 +441,15 @@ __device__ __forceinline__ bool df_all_cut(h2 p0, h2 p1) {
     const df_u16x2 m = __builtin_elementwise_max(d0, d1);
     return max((uint32_t)m.x, (uint32_t)m.y) <= 0x7C00u - 0x4881u;
 }
+// the converse, in fewer instructions: some p of the 2x2 group is <= 9, negative or NaN.  p > 9 holds
+// exactly for the bits in [0x4881, 0x7C00]; IEEE-754-2019 minimum (v_pk_minimum3_f16) keeps NaN, so
+// min(p0, p1) > 9 in both halves <=> all four p > 9 (one packed min and two ordered compares)
+// -- as the wave's lane mask: one ballot per compare, so each compare's mask is used as it is
+__device__ __forceinline__ uint64_t df_some_uncut_mask(h2 p0, h2 p1) {
+    const h2 m = __builtin_elementwise_minimum(p0, p1);
+    const h1 nine = (h1)9.0f;
+    return __builtin_amdgcn_ballot_w64(!(m.x > nine)) | __builtin_amdgcn_ballot_w64(!(m.y > nine));
+}
 
 // one list entry for one eye of a lane (depthFirstStereoRender :1872-1913 / :1915-1956) from the
 // quadratic forms: alpha = min(opacity * exp(-0.5 p), 0.99) with the r^2 cutoff folded into the
@@ -589,6 +603,8 @@ __global__ __launch_bounds__(NW * 64) void k_df_blend_eye(const uint32_t* __rest
         E.T[0] = E.T[1] = ONE;
         E.Cr[0] = E.Cr[1] = E.Cg[0] = E.Cg[1] = E.Cb[0] = E.Cb[1] = df_h2(0u);
         bool done = false;
+        bool alive = true;  // the lane's max T >= 1/255 (df_alive; T = 1 at the start)
+        uint64_t aliveM = __builtin_amdgcn_ballot_w64(true);  // ... as the wave's lane mask
         uint32_t walked = hd.y;  // entries this unit walked (its cost for the next frame's order)
         uint32_t nValid = 0, nBlend = 0;  // STATS: entries with a real mean / with a blend step
         // Loads run one batch ahead: while batch k blends, the records of batch k + 1 and the ids of
@@ -642,20 +658,29 @@ __global__ __launch_bounds__(NW * 64) void k_df_blend_eye(const uint32_t* __rest
 #pragma unroll
                 for (uint32_t jj = 0; jj < 4; ++jj) {
                     const uint32_t j = j0 + jj;
-                    const bool alive = df_alive(E, thrBits);
-                    if (__builtin_amdgcn_ballot_w64(alive) == 0) {  // every lane of this eye is done
-                        done = true;
-                        break;
-                    }
                     const uint4 ra = sA[j];
                     const uint32_t mw = __builtin_amdgcn_readfirstlane(ra.x);
                     if (df_mean_valid(mw)) {  // uniform
                         h2 p0, p1;
                         df_quadform(df_h2(mw), df_h2(ra.y), df_h2(ra.z), PX, PY, p0, p1);
                         if (STATS) nValid++;
-                        if (__builtin_amdgcn_ballot_w64(alive && !df_all_cut(p0, p1)) != 0) {
+#if GSM_DF_CUT_TEST == 0
+                        const uint64_t some = __builtin_amdgcn_ballot_w64(!df_all_cut(p0, p1));
+#else
+                        const uint64_t some = df_some_uncut_mask(p0, p1);
+#endif
+                        if ((some & aliveM) != 0) {
                             df_blend_eye_w(E, alive, p0, p1, ra.z, ra.w, sB[j], tbl);
+                            // T changes only here, so the per-eye test (:1872 / :1915) of the next
+                            // entry is the test of the updated T (a done lane's T is unchanged and
+                            // stays below 1/255); the wave leaves once every lane is done
+                            alive = df_alive(E, thrBits);
+                            aliveM = __builtin_amdgcn_ballot_w64(alive);
                             if (STATS) nBlend++;
+                            if (aliveM == 0) {
+                                done = true;
+                                break;
+                            }
                         }
                     }
                 }

@@ -25,6 +25,11 @@
 #ifndef GSM_DF_EXEC_ALIVE
 #define GSM_DF_EXEC_ALIVE 1
 #endif
+// GSM_DF_MEAN_TEST 1: the blend tests every staged entry's mean (df_mean_valid, scalar) and pads a
+// batch to a multiple of 4 with mean -inf; 0: the kept entries' means are valid by construction
+#ifndef GSM_DF_MEAN_TEST
+#define GSM_DF_MEAN_TEST 0
+#endif
 // the blend's wave-uniform "every alpha is 0" test: 0 = integer range test (df_all_cut), 1 = packed
 // minimum and two compares (df_some_uncut)
 #ifndef GSM_DF_CUT_TEST
@@ -631,12 +636,13 @@ __global__ __launch_bounds__(NW * 64) void k_df_blend_eye(const uint32_t* __rest
                 else if (b0 == 320u && !split) __builtin_amdgcn_s_setprio(3);
             }
             // the batch's entries not flagged for this eye (k_df_expand), compacted in list order (the
-            // flagged ones are identity steps); padded with mean -inf to a multiple of 4
+            // flagged ones are identity steps)
             const uint32_t gw = gwA;
             const uint4 rc = rcA;
             const bool keep = lane < n && !((gw >> (kDfSkipShift + eye)) & 1u);
             const uint64_t km = __builtin_amdgcn_ballot_w64(keep);
-            const uint32_t nk = (uint32_t)__popcll(km);
+            // (two 32-bit counts: the batch-end tests below then stay scalar compares)
+            const uint32_t nk = (uint32_t)__builtin_popcount((uint32_t)km) + (uint32_t)__builtin_popcount((uint32_t)(km >> 32));
             // next batch's records, and the ids of the one after
             {
                 const uint32_t* w = (const uint32_t*)(rd + (gwB & kDfGidMask));
@@ -652,15 +658,25 @@ __global__ __launch_bounds__(NW * 64) void k_df_blend_eye(const uint32_t* __rest
                                      (uint32_t)div255[c & 0xFFu] | ((uint32_t)div255[(c >> 8) & 0xFFu] << 16));
                 sB[pos] = (uint32_t)div255[(c >> 16) & 0xFFu];
             }
+#if GSM_DF_MEAN_TEST
             if (lane < 4u && nk + lane < ((nk + 3u) & ~3u)) sA[nk + lane] = make_uint4(0xFC00FC00u, 0u, 0u, 0u);
+#endif
             df_wave_sync();
             for (uint32_t j0 = 0; j0 < nk; j0 += 4) {
 #pragma unroll
                 for (uint32_t jj = 0; jj < 4; ++jj) {
                     const uint32_t j = j0 + jj;
                     const uint4 ra = sA[j];
+#if GSM_DF_MEAN_TEST
                     const uint32_t mw = __builtin_amdgcn_readfirstlane(ra.x);
                     if (df_mean_valid(mw)) {  // uniform
+#else
+                    // a kept entry's mean passes the reference's mean test (gMean.x >= -60000): an
+                    // eye whose mean fails it is flagged by k_df_expand (quad_bound_setup mode 1), so
+                    // the only test left is the batch's end (uniform, no pad records)
+                    const uint32_t mw = ra.x;
+                    if (j < nk) {
+#endif
                         h2 p0, p1;
                         df_quadform(df_h2(mw), df_h2(ra.y), df_h2(ra.z), PX, PY, p0, p1);
                         if (STATS) nValid++;

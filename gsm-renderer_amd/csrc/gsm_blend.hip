@@ -21,6 +21,11 @@
 #ifndef GSM_COMPACT_LDS
 #define GSM_COMPACT_LDS 1
 #endif
+// entries between the walks' exit / compaction checkpoints (a multiple of 4: the compacted walk's groups)
+#ifndef GSM_BLEND_EXIT
+#define GSM_BLEND_EXIT 16
+#endif
+static_assert(GSM_BLEND_EXIT == 4 || GSM_BLEND_EXIT == 8 || GSM_BLEND_EXIT == 16 || GSM_BLEND_EXIT == 32, "exit interval");
 #ifndef GSM_BLEND_P1_TILES_PER_CU
 #define GSM_BLEND_P1_TILES_PER_CU 8u
 #endif
@@ -129,7 +134,7 @@ __global__ __launch_bounds__(NT) void k_blend_px(
     static_assert(!COMPACT || P == 2, "compaction: half tiles");
     constexpr uint32_t U = 4 / P;  // entries per pipeline group
     constexpr uint32_t NG = 64 / U;      // groups per 64-entry batch
-    constexpr uint32_t EXITG = 16 / U;   // exit test every 16 entries
+    constexpr uint32_t EXITG = GSM_BLEND_EXIT / U;  // exit test every GSM_BLEND_EXIT entries
     constexpr uint32_t UPT = 4 / P;      // units per tile
     constexpr uint32_t NW = NT / 64;
     constexpr uint32_t UNROLL = NG;
@@ -519,7 +524,9 @@ __global__ __launch_bounds__(NT) void k_blend_px(
                             goto unit_done;
                         }
                         // at most 16 of the 32 groups alive: continue them one pixel pair per lane
-                        if (COMPACT && __popcll(am & 0x5555555555555555ull) <= 16) {
+                        // (two 32-bit counts: a 64-bit popcount's compare goes to the VALU)
+                        if (COMPACT && (uint32_t)__builtin_popcount((uint32_t)am & 0x55555555u) +
+                                               (uint32_t)__builtin_popcount((uint32_t)(am >> 32) & 0x55555555u) <= 16u) {
                             eC = g1;
                             b0C = b0;
                             goto compact_phase;
@@ -714,7 +721,7 @@ __global__ __launch_bounds__(NT) void k_blend_px(
                         }
                     }
                     e += U1;
-                    if ((e & 15u) == 0) {
+                    if ((e & (GSM_BLEND_EXIT - 1u)) == 0) {
                         if (e >= count || __ballot(alive1) == 0) break;
 #if GSM_BLEND_DEADX
                         X1 = alive1 ? X1 : FAR;

@@ -26,6 +26,11 @@
 #define GSM_BLEND_EXIT 16
 #endif
 static_assert(GSM_BLEND_EXIT == 4 || GSM_BLEND_EXIT == 8 || GSM_BLEND_EXIT == 16 || GSM_BLEND_EXIT == 32, "exit interval");
+// waves per workgroup that take the schedule's longest units first, at the top priority (waves map
+// to SIMDs round-robin: 4 = one per SIMD)
+#ifndef GSM_BLEND_NTOP
+#define GSM_BLEND_NTOP 4
+#endif
 #ifndef GSM_BLEND_P1_TILES_PER_CU
 #define GSM_BLEND_P1_TILES_PER_CU 8u
 #endif
@@ -293,7 +298,7 @@ __global__ __launch_bounds__(NT) void k_blend_px(
     // long walk issues nearly as fast as a wave alone (the makespan is the longest walk's).
     const uint32_t wv = threadIdx.x >> 6;
     const bool split = (flags & 4) != 0;
-    constexpr uint32_t NTOP = 4;  // one top-priority wave per SIMD
+    constexpr uint32_t NTOP = GSM_BLEND_NTOP;  // one top-priority wave per SIMD (A/B: 0, 8)
     uint32_t qi = !split ? blockIdx.x * NW + wv
                          : (wv < NTOP ? blockIdx.x * NTOP + wv
                                       : gridDim.x * NTOP + blockIdx.x * (NW - NTOP) + (wv - NTOP));

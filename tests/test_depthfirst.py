@@ -263,6 +263,31 @@ def test_df_adversarial_scenes_bit_exact(gsm, cuda, oracle, kind, n, w, h, sh, s
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("seed", [31, 35, 37, 41])
+def test_df_wide_baseline_ragged_frames(gsm, cuda, oracle, seed):
+    """Eyes far apart (a baseline of 2-4 scene units instead of 0.064) on ragged frame sizes: many
+    gaussians are on screen in one eye only, so the other eye's mean fails the reference's mean test
+    (gMean.x >= -60000) and k_df_expand flags that eye for every instance -- the blend walks only the
+    unflagged entries and takes their means as valid without testing them.  Every
+    intermediate and the side-by-side target bit for bit."""
+    rng = np.random.default_rng(seed)
+    w, h = int(rng.integers(97, 400)), int(rng.integers(61, 300))
+    n = int(rng.integers(8000, 25000))
+    sh = int(rng.choice([1, 4, 9, 16]))
+    prec = int(rng.integers(0, 2))
+    world, harm = _scene(n, w, h, sh, prec, seed)
+    L, R = _cams(w, h, ipd=float(rng.uniform(2.0, 4.0)))
+    r = oracle.df_render_stereo(world, harm, sh, L, R, w, h, max_gaussians=4 * n)
+    assert r["status"] == 0 and r["overflow"] == 0
+    # one-eye gaussians exist (mean -1e10 -> fp16 -inf in the eye the gaussian misses)
+    rd = r["render_data"].view(np.uint16).reshape(-1, 16)[r["touched"] > 0]
+    assert ((rd[:, 0] == 0xFC00) != (rd[:, 6] == 0xFC00)).sum() > 100
+    g = gpu_df(gsm, cuda, world, harm, sh, L, R, w, h, max_gaussians=4 * n)
+    assert_df_equal(g, r)
+    g["renderer"].close()
+
+
+@pytest.mark.gpu
 def test_df_scene_transform(gsm, cuda, oracle):
     n, w, h = 15000, 240, 200
     world, harm = _scene(n, w, h, 9, 1, 12)

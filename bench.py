@@ -338,6 +338,9 @@ def main():
     stage_ms = renderer.stage_times_ms()
     stage_ms["blend_timed_region"] = blend_ms_timed
     counters = renderer.counters()
+    # the blend kernel the library launched for this frame (not re-derived here, so a
+    # GSM_BLEND_WAVES / GSM_BLEND_PAIRS override is attributed to the kernel that actually ran)
+    blend_kernel = renderer.blend_kernel() or "k_blend_px"
     ms_per_step = elapsed / args.steps * 1e3
     fps = 1e3 / ms_per_step
     # two frames in flight (single GPU, mono): a second renderer handle on a second stream, frames
@@ -442,10 +445,6 @@ def main():
     # outnumber 8 waves x CUs, quadrants otherwise; every unit reads the tile's whole list
     n_cus = torch.cuda.get_device_properties(dev).multi_processor_count
     units_per_tile = 2 if T > 8 * n_cus else 4
-    # the blend kernel (gsm_blend.hip launch_blend): the pair walk k_blend_pw for half-tile frames of >= 6
-    # units per wave slot at 16 waves per CU (config 3), k_blend_px otherwise (GSM_BLEND_PAIRS=0: always)
-    blend_kernel = ("k_blend_pw" if units_per_tile == 2 and T * 2 >= 6 * n_cus * 16 and world_size == 1
-                    and os.environ.get("GSM_BLEND_PAIRS", "1") != "0" else "k_blend_px")
     traffic = valu_insts = traffic_note = valu_mix = None
     tj = load_pmc(args.traffic_json, args.config, world_size, blend_kernel)
     if tj:

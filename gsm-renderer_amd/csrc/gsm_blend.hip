@@ -12,30 +12,23 @@
 #include <cstdlib>
 #include <cstring>
 
+#include "../../include/gsm_debug.h"
 #include "../../include/gsm_renderer.h"
 #include "gsm_blend_exact.h"
 #include "gsm_detmath.h"
 #include "gsm_internal.h"
 #include "gsm_types.h"
 
-#ifndef GSM_COMPACT_LDS
-#define GSM_COMPACT_LDS 1
-#endif
-// entries between the walks' exit / compaction checkpoints (a multiple of 4: the compacted walk's groups)
-#ifndef GSM_BLEND_EXIT
-#define GSM_BLEND_EXIT 16
-#endif
-static_assert(GSM_BLEND_EXIT == 4 || GSM_BLEND_EXIT == 8 || GSM_BLEND_EXIT == 16 || GSM_BLEND_EXIT == 32, "exit interval");
-// waves per workgroup that take the schedule's longest units first, at the top priority (waves map
-// to SIMDs round-robin: 4 = one per SIMD)
-#ifndef GSM_BLEND_NTOP
-#define GSM_BLEND_NTOP 4
-#endif
-#ifndef GSM_BLEND_P1_TILES_PER_CU
-#define GSM_BLEND_P1_TILES_PER_CU 8u
-#endif
-
 namespace gsm {
+
+// entries between the walks' exit / compaction checkpoints (a multiple of 4: the compacted walk's groups;
+// 4 and 8 measured no faster)
+constexpr uint32_t kBlendExit = 16;
+// waves per workgroup that take the schedule's longest units first, at the top priority (waves map
+// to SIMDs round-robin: 4 = one per SIMD; 0 and 8 measured slower)
+constexpr uint32_t kBlendTopWaves = 4;
+// quadrant units (P = 1) up to this many tiles per CU, half tiles beyond
+constexpr uint32_t kBlendP1TilesPerCu = 8;
 
 typedef _Float16 h1;
 typedef _Float16 h2 __attribute__((ext_vector_type(2)));
@@ -54,37 +47,16 @@ __device__ __forceinline__ uint32_t as_u32(h2 v) { return __builtin_bit_cast(uin
 __device__ __forceinline__ h2 splat_lo(h2 v) { return h2{v.x, v.x}; }
 __device__ __forceinline__ h2 splat_hi(h2 v) { return h2{v.y, v.y}; }
 
-// The table index of a packed pair of quadratic forms.  GSM_BLEND_PCLAMP: every p above 34.65625 (the
-// largest p with a nonzero entry, +inf included) reads the one zero entry of 34.6875 (0x5056), so the
-// lanes of a gaussian's far field broadcast one LDS word instead of gathering scattered zeros
-// (bank conflicts); v_pk_minimum3_f16 (IEEE 754-2019 minimum) keeps negative p and NaN p (whose entries
-// are NaN) -- the entry read is the same value for every p.
-#ifndef GSM_BLEND_PCLAMP
-#define GSM_BLEND_PCLAMP 0
-#endif
-// GSM_BLEND_DEADX: a lane whose group broke walks on with its columns moved to x = 65504, so its p is
-// +-inf or NaN (one of three table words) instead of a live-looking scattered index
-#ifndef GSM_BLEND_DEADX
-#define GSM_BLEND_DEADX 0
-#endif
-// GSM_BLEND_DUPTBL (attribution builds only): every table read of the walk issued twice, the second
-// result folded into nothing observable -- the difference of SQ_LDS_BANK_CONFLICT to the plain build
-// is the conflict count of the table reads themselves
+// The table index of a packed pair of quadratic forms: its fp16 bits.  (The far-field clamp and the
+// dead-lane columns that cut the gathers' bank conflicts, and the duplicate-read attribution build, are
+// kept as tools/exp/rejected_variants.patch: bit-exact, no faster)
 // GSM_BLEND_ZSTATS (statistics builds only): the trace's t[3] holds per unit the entries on which no
 // live pixel has a nonzero alpha and the sum over entries of the live pixels; t[0]'s top 16 bits ncomp
 #ifndef GSM_BLEND_ZSTATS
 #define GSM_BLEND_ZSTATS 0
 #endif
-#ifndef GSM_BLEND_DUPTBL
-#define GSM_BLEND_DUPTBL 0
-#endif
 __device__ __forceinline__ uint32_t tbl_bits(h2 p) {
-#if GSM_BLEND_PCLAMP
-    const h2 c = {(h1)34.6875f, (h1)34.6875f};
-    return as_u32(__builtin_elementwise_minimum(p, c));
-#else
     return as_u32(p);
-#endif
 }
 
 // exp table lookup for a packed pair of quadratic forms: the table is indexed by the fp16 bits
@@ -134,37 +106,21 @@ __global__ __launch_bounds__(NT) void k_blend_px(
     const uint32_t* __restrict__ order, uint16_t* __restrict__ unitCost,
     unsigned long long* __restrict__ trace, const uint32_t* __restrict__ half0,
     const uint32_t* __restrict__ half1, const uint32_t* __restrict__ halfCount, uint32_t tileCount,
-    uint32_t* __restrict__ costMax, uint32_t rowBegin, uint32_t rowStride, MgArrive arrive, float4 prioFrac) {
+    uint32_t* __restrict__ costMax, uint32_t rowBegin, uint32_t rowStride, MgArrive arrive) {
     static_assert(P == 1 || P == 2, "pairs per lane: quadrant or half-tile units (half-tile lists)");
     static_assert(!COMPACT || P == 2, "compaction: half tiles");
     constexpr uint32_t U = 4 / P;  // entries per pipeline group
     constexpr uint32_t NG = 64 / U;      // groups per 64-entry batch
-    constexpr uint32_t EXITG = GSM_BLEND_EXIT / U;  // exit test every GSM_BLEND_EXIT entries
+    constexpr uint32_t EXITG = kBlendExit / U;  // exit test every kBlendExit entries
     constexpr uint32_t UPT = 4 / P;      // units per tile
     constexpr uint32_t NW = NT / 64;
     constexpr uint32_t UNROLL = NG;
     const bool agePrio = (flags & 2) != 0;
-    // flags bit 12 (GSM_BLEND_PRIO=lrpt): priority by the unit's predicted REMAINING walk (last frame's
-    // walk minus the entries done), levels at prioT[0..2] x the longest walk of last frame -- longest
-    // remaining processing time first; otherwise the age priority below
-    const bool lrpt = (flags & 8192) != 0 && unitCost != nullptr;
-    uint32_t prioT3 = 0, prioT2 = 0, prioT1 = 0;
-    if (lrpt) {
-        const uint32_t M = __builtin_amdgcn_readfirstlane(costMax[kCostMaxSlots + 1]);
-        prioT3 = (uint32_t)((float)M * prioFrac.x);
-        prioT2 = (uint32_t)((float)M * prioFrac.y);
-        prioT1 = (uint32_t)((float)M * prioFrac.z);
-    }
     __shared__ __attribute__((aligned(16))) uint16_t tbl[65536];
     __shared__ uint32_t cscr[NW][16];  // compaction: the alive groups of each wave, in order
     __shared__ __attribute__((aligned(16))) uint4 lrecA[NW][64];  // current batch records
     __shared__ uint32_t lrecB[NW][64];
-    // a gathered multi-GPU frame (flags bit 10): the unit's r16f depth staged per wave, stored at the
-    // unit's end as 16-B write-through stores (2-B write-through stores cost ~12x a 16-B store per
-    // byte on gfx950: MI355X_MICROARCH.md, store flavours)
-    constexpr uint32_t UH = (P == 1) ? 8u : 16u;  // unit rows (units are 16 pixels wide)
-    __shared__ __attribute__((aligned(16))) uint32_t dstage[NW][UH * 8];
-    __shared__ uint32_t exitCount;  // GSM_MG_PIXELS=wb: waves of this workgroup past their last unit
+    __shared__ uint32_t exitCount;  // a gathered multi-GPU frame: waves of this workgroup past their last unit
     if (threadIdx.x == 0) exitCount = 0;
     {
         const uint4* src = (const uint4*)expTable;
@@ -177,27 +133,12 @@ __global__ __launch_bounds__(NT) void k_blend_px(
     // write (GlobalShaders.metal:1152-1186): one pixel pair (px, py), (px + 1, py) in the target's
     // format (flags bits 4-7, gsm_color_format; conversion rules in include/gsm_renderer.h)
     const int colorFmt = (flags >> 4) & 15;
-    // flags bit 10: the targets are rank 0's gathered frame of a multi-GPU frame -- every pixel store
-    // system-coherent write-through (gsm_internal.h: the wave's arrival at the end then only drains)
-    const bool wt = (flags & 1024) != 0;
-    const uint32_t colorBytes = (uint32_t)(colorPitch * H), depthBytes = (uint32_t)(depthPitch * H);
-    uint32_t* const dst = dstage[threadIdx.x >> 6];
-    auto st128 = [&](uint8_t* p, uint4 v) {
-        if (wt) st_sys128_at(color, colorBytes, (uint32_t)(p - color), v);
-        else *(uint4*)p = v;
-    };
-    auto st32 = [&](uint8_t* p, uint32_t v) {
-        if (wt) st_sys32_at(color, colorBytes, (uint32_t)(p - color), v);
-        else *(uint32_t*)p = v;
-    };
-    auto std32 = [&](uint8_t* p, uint32_t v) {
-        if (wt) st_sys32_at(depth, depthBytes, (uint32_t)(p - depth), v);
-        else *(uint32_t*)p = v;
-    };
-    auto std16 = [&](uint8_t* p, uint16_t v) {
-        if (wt) st_sys16_at(depth, depthBytes, (uint32_t)(p - depth), v);
-        else *(uint16_t*)p = v;
-    };
+    // plain stores, also into rank 0's gathered frame of a multi-GPU frame (flags bit 12: released by the
+    // workgroup's L2 write-back at its exit; write-through pixel stores measured slower)
+    auto st128 = [&](uint8_t* p, uint4 v) { *(uint4*)p = v; };
+    auto st32 = [&](uint8_t* p, uint32_t v) { *(uint32_t*)p = v; };
+    auto std32 = [&](uint8_t* p, uint32_t v) { *(uint32_t*)p = v; };
+    auto std16 = [&](uint8_t* p, uint16_t v) { *(uint16_t*)p = v; };
     auto write_pair = [&](uint32_t px, uint32_t py, h2 Av, h2 Rq, h2 Gq, h2 Bq, h2 Dq) {
         if (py >= H) return;
         uint8_t* crow = color + (size_t)py * colorPitch;
@@ -253,9 +194,7 @@ __global__ __launch_bounds__(NT) void k_blend_px(
                 st32(crow + (size_t)(px + i) * 4, px32);
             }
         }
-        if (depth && wt) {
-            dst[((py & (UH - 1u)) * 16u + (px & 15u)) >> 1] = ud;  // (flush_depth at the unit's end)
-        } else if (depth) {
+        if (depth) {
             if ((flags & 1) && px + 1 < W) {
                 std32(depth + (size_t)py * depthPitch + (size_t)px * 2, ud);
             } else {
@@ -281,11 +220,6 @@ __global__ __launch_bounds__(NT) void k_blend_px(
     }
     const h2 ONE = {(h1)1.0f, (h1)1.0f};
     const h2 ZERO = {(h1)0.0f, (h1)0.0f};
-    const h2 FAR = {(h1)65504.0f, (h1)65504.0f};  // (GSM_BLEND_DEADX)
-    (void)FAR;
-#if GSM_BLEND_DUPTBL
-    uint32_t dupSink = 0;
-#endif
     const uint32_t thrBits = (uint32_t)__builtin_bit_cast(uint16_t, (h1)(1.0f / 255.0f));
     const h1 c099 = (h1)0.99;
     const h2 C099 = {c099, c099};
@@ -298,7 +232,7 @@ __global__ __launch_bounds__(NT) void k_blend_px(
     // long walk issues nearly as fast as a wave alone (the makespan is the longest walk's).
     const uint32_t wv = threadIdx.x >> 6;
     const bool split = (flags & 4) != 0;
-    constexpr uint32_t NTOP = GSM_BLEND_NTOP;  // one top-priority wave per SIMD (A/B: 0, 8)
+    constexpr uint32_t NTOP = kBlendTopWaves;
     uint32_t qi = !split ? blockIdx.x * NW + wv
                          : (wv < NTOP ? blockIdx.x * NTOP + wv
                                       : gridDim.x * NTOP + blockIdx.x * (NW - NTOP) + (wv - NTOP));
@@ -337,15 +271,7 @@ __global__ __launch_bounds__(NT) void k_blend_px(
         uint32_t nextQ = 0;
         bool claimed = false;
         // claimMode 2: the walk this unit made last frame (before this frame's walk overwrites it)
-        const uint32_t expWalk = ((claimMode == 2 || lrpt) && unitCost) ? __builtin_amdgcn_readfirstlane((uint32_t)unitCost[u]) : 0u;
-        auto lrptPrio = [&](uint32_t done) {  // (flags bit 12)
-            const uint32_t rem = expWalk > done ? expWalk - done : 0u;
-            if (rem >= prioT3) __builtin_amdgcn_s_setprio(3);
-            else if (rem >= prioT2) __builtin_amdgcn_s_setprio(2);
-            else if (rem >= prioT1) __builtin_amdgcn_s_setprio(1);
-            else __builtin_amdgcn_s_setprio(0);
-        };
-        if (lrpt) lrptPrio(0u);
+        const uint32_t expWalk = (claimMode == 2 && unitCost) ? __builtin_amdgcn_readfirstlane((uint32_t)unitCost[u]) : 0u;
         auto claim = [&]() {
             if (!claimed) {
                 if (lane == 0) nextQ = atomicAdd(myQueue, 1u);
@@ -467,10 +393,6 @@ __global__ __launch_bounds__(NT) void k_blend_px(
                                 const uint32_t pb = tbl_bits(pq[q]);
                                 en[k][q].x = tbl[pb & 0xFFFFu];
                                 en[k][q].y = tbl[pb >> 16];
-#if GSM_BLEND_DUPTBL
-                                dupSink ^= (uint32_t)((volatile uint16_t*)tbl)[pb & 0xFFFFu] ^
-                                           ((uint32_t)((volatile uint16_t*)tbl)[pb >> 16] << 16);
-#endif
                             }
                         }
                     }
@@ -536,10 +458,6 @@ __global__ __launch_bounds__(NT) void k_blend_px(
                             b0C = b0;
                             goto compact_phase;
                         }
-#if GSM_BLEND_DEADX
-#pragma unroll
-                        for (int k = 0; k < P; ++k) X[k] = alive ? X[k] : FAR;
-#endif
                     }
                     // stage 3: the next group's alphas
 #pragma unroll
@@ -554,9 +472,7 @@ __global__ __launch_bounds__(NT) void k_blend_px(
                         bdc[k] = bdn[k];
                     }
                 }
-                if (lrpt) {
-                    lrptPrio(b0 + 64u);
-                } else if (topPrio) {
+                if (topPrio) {
                     if (b0 == 0) __builtin_amdgcn_s_setprio(3);
                 } else if (agePrio) {
                     if (b0 == 0) __builtin_amdgcn_s_setprio(1);
@@ -601,9 +517,6 @@ __global__ __launch_bounds__(NT) void k_blend_px(
                 h2 B1 = pick(B[0], B[1]), D1 = pick(D[0], D[1]);
                 const uint32_t px1 = ux + (sg & 3u) * 4u + 2u * kk, py1 = uy + (sg >> 2) * 2u + rr;
                 h2 X1 = h2{(h1)(float)px1, (h1)(float)(px1 + 1u)};
-#if GSM_BLEND_DEADX
-                if (!valid1) X1 = FAR;
-#endif
                 const h2 Y1 = h2{(h1)(float)py1, (h1)(float)py1};
                 bool alive1 = valid1;
                 // the same per-pixel operations as the half-tile walk (quadform above)
@@ -636,24 +549,17 @@ __global__ __launch_bounds__(NT) void k_blend_px(
                 uint32_t rgc1[U1], bdc1[U1], rgn1[U1], bdn1[U1], opn1[U1];
                 u16x2 en1[U1];
                 // The records come from the LDS stage of the current batch (uniform-address reads, as
-                // in the half-tile walk; GSM_COMPACT_LDS) -- it holds batch bb here: the walk staged it,
+                // in the half-tile walk) -- it holds batch bb here: the walk staged it,
                 // or staged the next one and the rotation above made that batch bb -- instead of five
                 // v_readlane per entry from the batch registers.
 #pragma unroll
                 for (uint32_t k = 0; k < U1; ++k) {  // prime the group at e
                     const uint32_t j = e - bb + k;
-#if GSM_COMPACT_LDS
                     const uint4 ra = lrecA[wv][j];
                     const uint32_t r2 = ra.z;
                     const h2 pq = quad1(ra.x, ra.y, r2);
                     rgc1[k] = ra.w;
                     bdc1[k] = lrecB[wv][j];
-#else
-                    const uint32_t r2 = __builtin_amdgcn_readlane(bA.z, j);
-                    const h2 pq = quad1(__builtin_amdgcn_readlane(bA.x, j), __builtin_amdgcn_readlane(bA.y, j), r2);
-                    rgc1[k] = __builtin_amdgcn_readlane(bA.w, j);
-                    bdc1[k] = __builtin_amdgcn_readlane(bB, j);
-#endif
                     ac1[k] = __builtin_elementwise_min(splat_hi(as_h2(r2)) * lookup2(tbl, pq), C099);
                     om1[k] = ONE - ac1[k];
                 }
@@ -663,7 +569,6 @@ __global__ __launch_bounds__(NT) void k_blend_px(
                     {
                         const uint32_t jn = e + U1 - bb;  // 4..64
                         const bool nb = jn >= 64u;
-#if GSM_COMPACT_LDS
                         if (nb) {  // the next group opens the next batch: stage it (this batch is all read)
                             lrecA[wv][lane] = nA;
                             lrecB[wv][lane] = nB;
@@ -681,27 +586,7 @@ __global__ __launch_bounds__(NT) void k_blend_px(
                             const uint32_t pb = tbl_bits(pq);
                             en1[k].x = tbl[pb & 0xFFFFu];
                             en1[k].y = tbl[pb >> 16];
-#if GSM_BLEND_DUPTBL
-                            dupSink ^= (uint32_t)((volatile uint16_t*)tbl)[pb & 0xFFFFu] ^
-                                       ((uint32_t)((volatile uint16_t*)tbl)[pb >> 16] << 16);
-#endif
                         }
-#else
-                        const uint32_t sx = nb ? nA.x : bA.x, sy = nb ? nA.y : bA.y;
-                        const uint32_t sz = nb ? nA.z : bA.z, sw = nb ? nA.w : bA.w;
-                        const uint32_t sb = nb ? nB : bB;
-#pragma unroll
-                        for (uint32_t k = 0; k < U1; ++k) {
-                            const uint32_t j = (jn + k) & 63u;
-                            opn1[k] = __builtin_amdgcn_readlane(sz, j);
-                            const h2 pq = quad1(__builtin_amdgcn_readlane(sx, j), __builtin_amdgcn_readlane(sy, j), opn1[k]);
-                            rgn1[k] = __builtin_amdgcn_readlane(sw, j);
-                            bdn1[k] = __builtin_amdgcn_readlane(sb, j);
-                            const uint32_t pb = as_u32(pq);
-                            en1[k].x = tbl[pb & 0xFFFFu];
-                            en1[k].y = tbl[pb >> 16];
-                        }
-#endif
                     }
                     // stage 2: blend the current group
 #pragma unroll
@@ -726,11 +611,8 @@ __global__ __launch_bounds__(NT) void k_blend_px(
                         }
                     }
                     e += U1;
-                    if ((e & (GSM_BLEND_EXIT - 1u)) == 0) {
+                    if ((e & (kBlendExit - 1u)) == 0) {
                         if (e >= count || __ballot(alive1) == 0) break;
-#if GSM_BLEND_DEADX
-                        X1 = alive1 ? X1 : FAR;
-#endif
                     }
                     // stage 3: the next group's alphas
 #pragma unroll
@@ -744,7 +626,6 @@ __global__ __launch_bounds__(NT) void k_blend_px(
                     if (e - bb == 64u) {
                         rotate(bb);
                         bb += 64u;
-                        if (lrpt) lrptPrio(e);
                     }
                 }
                 nproc = e;
@@ -763,30 +644,6 @@ __global__ __launch_bounds__(NT) void k_blend_px(
         if (exactD)  // (rare: a record of inf / NaN fp16 depth; every pixel of the unit is written again)
             blend_exact::walk_unit_exact<P>((hsel ? half1 : half0) + start, count, rec, tbl, lrecA[wv], lrecB[wv], ux,
                                             uy, thrBits, write_pair);
-        if (wt && depth) {
-            // every pixel pair of the unit was staged by the writes above (each exactly once); rows
-            // past H were not, and are not stored
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-            if (lane < UH * 2u) {
-                const uint32_t r = lane >> 1, hx = (lane & 1u) * 8u;
-                const uint32_t py = uy + r, px = ux + hx;
-                const uint4 v = *(const uint4*)&dst[r * 8u + (hx >> 1)];
-                if (py < H) {
-                    const uint32_t off = (uint32_t)((size_t)py * depthPitch + (size_t)px * 2u);
-                    if ((flags & 2048) && px + 8u <= W) {
-                        st_sys128_at(depth, depthBytes, off, v);
-                    } else {
-                        const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-                        for (uint32_t i = 0; i < 8; ++i)
-                            if (px + i < W) st_sys16_at(depth, depthBytes, off + 2u * i, (uint16_t)(w4[i >> 1] >> (16u * (i & 1u))));
-                    }
-                }
-            }
-            __builtin_amdgcn_wave_barrier();  // the next unit's staging writes after these reads
-        }
         if (unitCost && lane == 0) unitCost[u] = (uint16_t)min(nproc, 65535u);
         waveMax = max(waveMax, min(nproc, 65535u));
         if (trace && lane == 0) {
@@ -803,33 +660,23 @@ __global__ __launch_bounds__(NT) void k_blend_px(
             t[3] = (xcc << 48) | ((unsigned long long)(ncomp & 0xFFFFu) << 32) |
                    (unsigned long long)__builtin_amdgcn_s_getreg(4 | (31 << 11));
         }
-        if (agePrio || topPrio || lrpt) __builtin_amdgcn_s_setprio(0);
+        if (agePrio || topPrio) __builtin_amdgcn_s_setprio(0);
         topPrio = false;
         claim();  // (no-op when claimed during the walk)
         qi = gridWaves + stripe + stripes * __builtin_amdgcn_readfirstlane(nextQ);
     }
-#if GSM_BLEND_DUPTBL
-    if (dupSink == 0x9E3779B9u && flags == -1) queue[0] = dupSink;  // keeps the duplicate reads alive
-#endif
     if (unitCost && lane == 0 && waveMax) atomicMax(&costMax[(blockIdx.x * NW + wv) % kCostMaxSlots], waveMax);
-    // multi-GPU frame gathered on rank 0 (gsm_multigpu.hip): the pixels this wave stored into rank
-    // 0's frame (write-through, flags bit 10) are drained and the wave arrives at barrier 2 (the last
-    // one raises the flags) -- every wave of the grid arrives exactly once, here
+    // multi-GPU frame gathered on rank 0 (gsm_multigpu.hip): the pixels were plain stores; the
+    // workgroup's last exiting wave writes the XCD's L2 back at system scope (covering every wave of the
+    // workgroup: each drained its stores before its count) and arrives at barrier 2 for the workgroup
     if (arrive.done) {
-        if (flags & 4096) {
-            // GSM_MG_PIXELS=wb: plain pixel stores; the workgroup's last exiting wave writes the XCD's
-            // L2 back at system scope (covering every wave of the workgroup: each drained its stores
-            // before its count) and arrives for the workgroup
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        uint32_t old = 0;
+        if (lane == 0) old = __hip_atomic_fetch_add(&exitCount, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (__builtin_amdgcn_readfirstlane(old) == NW - 1u) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            uint32_t old = 0;
-            if (lane == 0) old = __hip_atomic_fetch_add(&exitCount, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            if (__builtin_amdgcn_readfirstlane(old) == NW - 1u) {
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                mg_arrive_unit(arrive, blockIdx.x);
-            }
-        } else {
-            mg_arrive_unit(arrive, blockIdx.x * NW + (threadIdx.x >> 6));
+            mg_arrive_unit(arrive, blockIdx.x);
         }
     }
 }
@@ -841,7 +688,7 @@ int blend_pairs_per_lane(uint32_t numTiles, int numCUs) {
     // or a slab of a multi-GPU frame has fewer units than slots, its blend time is its longest
     // unit's walk, and quadrant units (1 pair per lane, ~38 instead of ~61 VALU per entry)
     // shorten that (measured on 1/2, 1/4, 1/8 of the 1080p rows: 149/130/118 -> 138/105/96 us)
-    return numTiles <= (uint32_t)numCUs * GSM_BLEND_P1_TILES_PER_CU ? 1 : 2;
+    return numTiles <= (uint32_t)numCUs * kBlendP1TilesPerCu ? 1 : 2;
 }
 
 uint32_t blend_units_per_tile(uint32_t numTiles, int numCUs) {
@@ -863,30 +710,19 @@ static int blend_waves_per_wg(uint32_t numTiles, int numCUs) {
 // Measured schedule choices: units longest-first by last frame's walk (costOrder;
 // 1080p 8 waves 293 -> 248 us, 4K 16 waves 703 -> 660), the longest on one top-priority wave per
 // SIMD (flags bit 2), later units' priority rising with the age of their walk (flags bit 1).
-void launch_blend(const FrameGeometry& g, const DeviceArena& A, void* color,
+int launch_blend(const FrameGeometry& g, const DeviceArena& A, void* color,
                   size_t colorPitch, void* depth, size_t depthPitch, int numCUs, bool costOrder, int colorFormat,
-                  hipStream_t s, int wavesOverride, int claim, const MgArrive* arrive, bool arriveWB, bool pairs) {
+                  hipStream_t s, int wavesOverride, int claim, const MgArrive* arrive, bool pairs) {
     // local tile ids: tile t = k * tilesX + tx of the renderer's row k (pixel row rowBegin + k * rowStride)
     const uint32_t numTiles = g.rowCount * g.tilesX;
-    if (numTiles == 0) return;
+    if (numTiles == 0) return 0;
     const uint32_t t0 = 0;
     const int vec = ((((uintptr_t)color) & 15u) == 0 && (colorPitch & 15u) == 0 &&
                      (depth == nullptr || ((((uintptr_t)depth) & 7u) == 0 && (depthPitch & 7u) == 0)))
                         ? 1
                         : 0;
-    // GSM_BLEND_PRIO=lrpt[:a/b/c] (A/B): remaining-walk priorities at a / b / c of the longest walk
-    static const char* pv = getenv("GSM_BLEND_PRIO");
-    static const bool lrptMode = pv && !strncmp(pv, "lrpt", 4);
-    static float4 prioFrac = [] {
-        float4 f = make_float4(0.6f, 0.35f, 0.15f, 0.0f);
-        const char* p = getenv("GSM_BLEND_PRIO");
-        if (p && p[0] && p[4] == ':') sscanf(p + 5, "%f/%f/%f", &f.x, &f.y, &f.z);
-        return f;
-    }();
     const int flags = vec | 2 | (costOrder ? 4 : 0) | ((colorFormat & 15) << 4) | ((claim & 3) << 8) |
-                      ((lrptMode && costOrder) ? 8192 : 0) |
-                      (arrive ? (arriveWB ? 4096 : 1024) : 0) |  // (a gathered multi-GPU frame: write-through
-                                                                 // pixel stores, or the L2 write-back at exit)
+                      (arrive ? 4096 : 0) |  // (a gathered multi-GPU frame: the L2 write-back at exit)
                       ((depth && (((uintptr_t)depth) & 15u) == 0 && (depthPitch & 15u) == 0) ? 2048 : 0);
     // A.tileQueue was zeroed by k_scan_blocks earlier in the frame
     const int P = blend_pairs_per_lane(numTiles, numCUs);
@@ -895,10 +731,9 @@ void launch_blend(const FrameGeometry& g, const DeviceArena& A, void* color,
     // per wave (r05, k_blend_pw).  The pairs cut the VALU work (-10 %) but halve the waves walking: a gain
     // where the walk is VALU-bound (config 3: blend 370 -> 327 us), a loss where it is bound by its
     // longest units and latency (config 2: 121 -> 129-147 us at every split tried).
-    static const bool forcePairs = getenv("GSM_BLEND_PAIRS") && getenv("GSM_BLEND_PAIRS")[0] == '2';  // (A/B)
-    if (pairs && P == 2 && !arrive && (waves == 16 || forcePairs)) {
+    if (pairs && P == 2 && !arrive && waves == 16) {
         launch_blend_pw(g, A, color, colorPitch, depth, depthPitch, numCUs, costOrder, colorFormat, s, waves);
-        return;
+        return GSM_BLEND_KERNEL_PAIR_WALK;
     }
     const uint32_t units = numTiles * (4u / (uint32_t)P);
     uint32_t grid = (units + (uint32_t)waves - 1) / (uint32_t)waves;
@@ -907,14 +742,14 @@ void launch_blend(const FrameGeometry& g, const DeviceArena& A, void* color,
     MgArrive ar{};
     if (arrive) {
         ar = *arrive;
-        ar.total = arriveWB ? grid : grid * (uint32_t)waves;  // every wave (workgroup) arrives once, at its exit
+        ar.total = grid;  // every workgroup arrives once, at its exit
     }
 #define GSM_LAUNCH_BLEND(NTH, PP, CMP)                                                                       \
     hipLaunchKernelGGL((k_blend_px<NTH, PP, CMP>), dim3(grid), dim3(NTH), 0, s, A.tileStart, A.rec, \
                        A.expTable, A.tileQueue, t0, numTiles, g.tilesX, g.width, g.height,          \
                        (uint8_t*)color, colorPitch, (uint8_t*)depth, depthPitch, flags, order, A.unitCost,  \
                        A.blendTrace, A.halfVals[0], A.halfVals[1], A.halfCount, g.tileCount, A.costMax, \
-                       g.rowBegin, g.rowStride, ar, prioFrac)
+                       g.rowBegin, g.rowStride, ar)
     // half tiles compact to one pair per lane once <= 16 of their 32 groups are alive
     if (P == 1) {
         if (waves == 16) GSM_LAUNCH_BLEND(1024, 1, false);
@@ -926,6 +761,7 @@ void launch_blend(const FrameGeometry& g, const DeviceArena& A, void* color,
         else GSM_LAUNCH_BLEND(512, 2, true);
     }
 #undef GSM_LAUNCH_BLEND
+    return P == 1 ? GSM_BLEND_KERNEL_QUADRANT : GSM_BLEND_KERNEL_HALF_TILE;
 }
 
 }  // namespace gsm

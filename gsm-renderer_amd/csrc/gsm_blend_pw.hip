@@ -54,22 +54,10 @@ __device__ __forceinline__ uint32_t pw_bperm(uint32_t srcLane, uint32_t v) {
 }
 __device__ __forceinline__ h2 pw_bperm(uint32_t srcLane, h2 v) { return as_h2(pw_bperm(srcLane, as_u32(v))); }
 
-// A/B switches of the table gathers (LDS bank conflicts): GSM_PW_PCLAMP -- p above the last
-// nonzero entry reads the one zero entry 0x5056 (v_pk_minimum3_f16 keeps negative p and NaN);
-// GSM_PW_DEADX -- dead groups' columns moved to x = 65504
-#ifndef GSM_PW_PCLAMP
-#define GSM_PW_PCLAMP 0
-#endif
-#ifndef GSM_PW_DEADX
-#define GSM_PW_DEADX 0
-#endif
+// the table index of a packed pair of quadratic forms: its fp16 bits (the far-field clamp / dead-column
+// variants: tools/exp/rejected_variants.patch)
 __device__ __forceinline__ uint32_t pw_tbl_bits(h2 p) {
-#if GSM_PW_PCLAMP
-    const h2 c = {(h1)34.6875f, (h1)34.6875f};
-    return as_u32(__builtin_elementwise_minimum(p, c));
-#else
     return as_u32(p);
-#endif
 }
 
 struct PwTarget {
@@ -157,7 +145,7 @@ __global__ __launch_bounds__(NT) void k_blend_pw(
     PwTarget tg, const uint32_t* __restrict__ order, uint16_t* __restrict__ unitCost,
     unsigned long long* __restrict__ trace, const uint32_t* __restrict__ half0, const uint32_t* __restrict__ half1,
     const uint32_t* __restrict__ halfCount, uint32_t tileCount, uint32_t* __restrict__ costMax, uint32_t rowBegin,
-    uint32_t rowStride, int flags, uint32_t tailSingles, int staticSingles) {
+    uint32_t rowStride, int flags) {
     constexpr uint32_t NW = NT / 64;
     constexpr uint32_t NTOP = 4;  // one top-priority single unit per SIMD (the schedule's longest)
     static_assert(NW > NTOP, "pairs need waves beyond the top-priority ones");
@@ -176,8 +164,6 @@ __global__ __launch_bounds__(NT) void k_blend_pw(
     const bool agePrio = (flags & 2) != 0, split = (flags & 4) != 0;
     const h2 ONE = {(h1)1.0f, (h1)1.0f};
     const h2 ZERO = {(h1)0.0f, (h1)0.0f};
-    const h2 FAR = {(h1)65504.0f, (h1)65504.0f};  // (GSM_PW_DEADX)
-    (void)FAR;
     const uint32_t thrBits = (uint32_t)__builtin_bit_cast(uint16_t, (h1)(1.0f / 255.0f));
     const h1 c099 = (h1)0.99;
     const h2 C099 = {c099, c099};
@@ -194,9 +180,7 @@ __global__ __launch_bounds__(NT) void k_blend_pw(
     // after a job ends).
     const uint32_t gridWaves = gridDim.x * NW;
     uint32_t NS = order ? min(__builtin_amdgcn_readfirstlane(costMax[kCostMaxSlots]), numUnits) : 0u;
-    if (staticSingles) NS = min(max(NS, gridWaves), numUnits);  // (A/B: every wave's first job alone)
-    // (A/B: the last tailSingles positions -- the shortest walks -- alone again)
-    const uint32_t PE = max(NS, numUnits > tailSingles ? numUnits - tailSingles : 0u);
+    const uint32_t PE = numUnits;
     const uint32_t NPJ = (PE - NS + 1u) / 2u;
     uint32_t job = !split ? blockIdx.x * NW + wv
                           : (wv < NTOP ? blockIdx.x * NTOP + wv : gridDim.x * NTOP + blockIdx.x * (NW - NTOP) + (wv - NTOP));
@@ -484,11 +468,6 @@ __global__ __launch_bounds__(NT) void k_blend_pw(
                                 else if (e == 320u && !split) __builtin_amdgcn_s_setprio(3);
                             }
                             hb = (e - b0 == 0u) ? laneSlot() : hb + 16u;
-#if GSM_PW_DEADX
-                            // a dead group's lanes walk on with their columns at x = 65504: p = +-inf or NaN,
-                            // three table words, instead of scattered live-looking gathers (bank conflicts)
-                            if (!alive) X0 = X1 = FAR;
-#endif
                         }
                         // stage 3: the next group's alphas
 #pragma unroll
@@ -632,10 +611,6 @@ __global__ __launch_bounds__(NT) void k_blend_pw(
 // the pair walk for a frame of half-tile units on one GPU (no multi-GPU gather); `waves` per workgroup
 void launch_blend_pw(const FrameGeometry& g, const DeviceArena& A, void* color, size_t colorPitch, void* depth,
                      size_t depthPitch, int numCUs, bool costOrder, int colorFormat, hipStream_t s, int waves) {
-    // A/B knobs (read per launch, experiments only): GSM_BLEND_PAIR_TAIL=k -- the k shortest units alone;
-    // GSM_BLEND_PAIR_STATIC=1 -- every wave's first job alone
-    static const uint32_t tailSingles = getenv("GSM_BLEND_PAIR_TAIL") ? (uint32_t)atoi(getenv("GSM_BLEND_PAIR_TAIL")) : 0u;
-    static const int staticSingles = getenv("GSM_BLEND_PAIR_STATIC") ? atoi(getenv("GSM_BLEND_PAIR_STATIC")) : 0;
     const uint32_t numTiles = g.rowCount * g.tilesX;
     if (numTiles == 0) return;
     const int vec = ((((uintptr_t)color) & 15u) == 0 && (colorPitch & 15u) == 0 &&
@@ -654,7 +629,7 @@ void launch_blend_pw(const FrameGeometry& g, const DeviceArena& A, void* color, 
 #define GSM_LAUNCH_PW(NTH)                                                                                          \
     hipLaunchKernelGGL((k_blend_pw<NTH>), dim3(grid), dim3(NTH), 0, s, A.tileStart, A.rec, A.expTable, A.tileQueue, \
                        numTiles, g.tilesX, tg, order, A.unitCost, A.blendTrace, A.halfVals[0], A.halfVals[1],      \
-                       A.halfCount, g.tileCount, A.costMax, g.rowBegin, g.rowStride, flags, tailSingles, staticSingles)
+                       A.halfCount, g.tileCount, A.costMax, g.rowBegin, g.rowStride, flags)
     if (waves >= 16) GSM_LAUNCH_PW(1024);
     else if (waves >= 12) GSM_LAUNCH_PW(768);
     else GSM_LAUNCH_PW(512);

@@ -154,6 +154,12 @@ gsm_status gsm_global_debug_counters(gsm_renderer* r, gsm_debug_counters* out) {
     return r->impl->counters(out);
 }
 
+gsm_status gsm_global_debug_blend_kernel(gsm_renderer* r, int* kind) {
+    if (!r || !r->impl || !kind) return GSM_ERR_INVALID_ARGUMENT;
+    *kind = r->impl->lastBlendKernel();
+    return GSM_OK;
+}
+
 gsm_status gsm_global_debug_copy(gsm_renderer* r, int which, void* dst, size_t bytes, size_t* needed) {
     if (!r || !r->impl) return GSM_ERR_INVALID_ARGUMENT;
     return r->impl->debugCopy(which, dst, bytes, needed);
@@ -172,6 +178,15 @@ gsm_status gsm_global_stage_times(gsm_renderer* r, float* ms, int n) {
 gsm_status gsm_global_set_tile_rows(gsm_renderer* r, uint32_t b, uint32_t e) {
     if (!r || !r->impl) return GSM_ERR_INVALID_ARGUMENT;
     return r->impl->setTileRows(b, e);
+}
+
+size_t gsm_debug_sort_workspace_bytes(uint32_t capacity) { return gsm::radix_workspace_bytes(capacity); }
+
+gsm_status gsm_debug_sort_plan_fits(uint32_t capacity, uint32_t key_bits, int wide, size_t hist_bytes) {
+    if (key_bits == 0 || key_bits > 32) return GSM_ERR_INVALID_ARGUMENT;
+    // (placeholder pointers: the plan only compares footprints, nothing is dereferenced or launched)
+    const gsm::SortSpace ws{(uint32_t*)(uintptr_t)16, hist_bytes, (uint32_t*)(uintptr_t)16, gsm::kSortTotalsWords};
+    return gsm::sort_bits_plan_fits(capacity, key_bits, wide != 0, ws) ? GSM_OK : GSM_ERR_INVALID_ASSIGNMENT_CAPACITY;
 }
 
 gsm_status gsm_sort_pairs_u32(void* keys, void* values, uint32_t n, uint32_t key_bits, void* stream) {
@@ -195,7 +210,9 @@ gsm_status gsm_sort_pairs_u32(void* keys, void* values, uint32_t n, uint32_t key
         int dev = 0;
         hipGetDevice(&dev);
         const gsm::Tuning tn = gsm::tuning_from_env(dev);  // read per call: no renderer here
-        int res = gsm::radix_sort_pairs(kb, vb, np, n, 0, digits, hist, bins, s, tn.ballotRank, tn.sortScanless);
+        const gsm::SortSpace ws{hist, gsm::radix_workspace_bytes(n), bins, 256};
+        int res = gsm::radix_sort_pairs(kb, vb, np, n, 0, digits, ws, s, tn.ballotRank, tn.sortScanless);
+        if (res == gsm::kSortNoSpace) st = GSM_ERR_INVALID_ASSIGNMENT_CAPACITY;
         if (res == 1) {
             hipMemcpyAsync(keys, k2, (size_t)n * 4, hipMemcpyDeviceToDevice, s);
             hipMemcpyAsync(values, v2, (size_t)n * 4, hipMemcpyDeviceToDevice, s);

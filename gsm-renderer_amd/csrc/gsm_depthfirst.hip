@@ -141,7 +141,8 @@ gsm_status DepthFirstRenderer::create(const gsm_renderer_config& cfg, int hipDev
         GSM_DF_ALLOC(A.ikeys[i], cap * 4);
         GSM_DF_ALLOC(A.ivals[i], cap * 4);
     }
-    GSM_DF_ALLOC(A.radixHist, radix_workspace_bytes(r->maxInstances_ > r->maxGaussians_ ? r->maxInstances_ : r->maxGaussians_));
+    A.radixHistBytes = radix_workspace_bytes(r->maxInstances_ > r->maxGaussians_ ? r->maxInstances_ : r->maxGaussians_);
+    GSM_DF_ALLOC(A.radixHist, A.radixHistBytes);
     if (st == GSM_OK &&
         hipMemset(A.radixHist, 0, radix_workspace_bytes(r->maxInstances_ > r->maxGaussians_ ? r->maxInstances_ : r->maxGaussians_)) != hipSuccess)
         st = GSM_ERR_FAILED_TO_ALLOCATE_BUFFER;
@@ -259,8 +260,9 @@ gsm_status DepthFirstRenderer::renderStereoSbs(hipStream_t s, const gsm_gaussian
     // DepthRadixSortEncoder, 32-bit keys (DepthFirstRenderer.swift:664-681): stable LSD
     // (3 wide passes of 11/11/10 bits unless GSM_SORT_WIDE=0: the same stable order)
     const int dc = radix_sort_bits(A_.dkeys, A_.dvals, &A_.visHdr->totalAssignments, maxGaussians_, 0, 32,
-                                   A_.radixHist, A_.radixBinTotals, s, tuning_.ballotRank, tuning_.wideSort,
+                                   sort_space(A_), s, tuning_.ballotRank, tuning_.wideSort,
                                    tuning_.sortScanless);
+    if (dc == kSortNoSpace) return GSM_ERR_INVALID_ASSIGNMENT_CAPACITY;  // (nothing of the sort launched)
     if (prof) hipEventRecord(ev[2], s);
     df_launch_instance_counts(A_.dvals[dc], a, A_, s);
     launch_scan_sums(A_.instSums, nb, maxInstances_, A_.instHdr, A_.queue, s);
@@ -268,9 +270,10 @@ gsm_status DepthFirstRenderer::renderStereoSbs(hipStream_t s, const gsm_gaussian
     if (prof) hipEventRecord(ev[3], s);
     // TileSortEncoder (DepthFirstRenderer.swift:683-768): stable sort by the 16-bit tile id
     // the last pass also writes the tile ranges' starts (radix_sort_tiles: no pass over the instances)
-    const int ic = radix_sort_tiles(A_.ikeys, A_.ivals, &A_.instHdr->totalAssignments, maxInstances_, 0, A_.radixHist,
-                                    A_.radixBinTotals, A_.starts, 0u, a.tileCount, a.tileCount, s, tuning_.ballotRank,
-                                    0, tuning_.wideSort, false, tuning_.sortScanless);
+    const int ic = radix_sort_tiles(A_.ikeys, A_.ivals, &A_.instHdr->totalAssignments, maxInstances_, 0, sort_space(A_),
+                                    A_.starts, 0u, a.tileCount, a.tileCount, s, tuning_.ballotRank,
+                                    tuning_.wideSort, tuning_.sortScanless);
+    if (ic == kSortNoSpace) return GSM_ERR_INVALID_ASSIGNMENT_CAPACITY;
     // Blend schedule: (tile, eye) units handed out longest first by the walk lengths the previous
     // frame of the same geometry measured (the image does not depend on the order, only the load
     // balance does).  Tuning::costOrder false (GSM_BLEND_SCHED=0 at create): index order.

@@ -167,29 +167,18 @@ __device__ __forceinline__ float load_harm(const void* __restrict__ h, size_t i)
     }
 }
 
-#ifndef GSM_SH_FMAMIX
-#define GSM_SH_FMAMIX 1
-#endif
 // fp32(h) * b for the fp16 in the low / high half of w: one v_fma_mix_f32 (the fp16 operand widened
 // exactly inside the instruction, fma(h, b, -0) = the correctly rounded product) instead of a
 // v_cvt_f32_f16 and a v_mul_f32 -- the same bits as the contract's convert-then-multiply
 __device__ __forceinline__ float mul_h_lo(uint32_t w, float b) {
-#if GSM_SH_FMAMIX
     float r;
     asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel_hi:[1,0,0]" : "=v"(r) : "v"(w), "v"(b), "v"(-0.0f));
     return r;
-#else
-    return hbits_to_f((uint16_t)(w & 0xFFFFu)) * b;
-#endif
 }
 __device__ __forceinline__ float mul_h_hi(uint32_t w, float b) {
-#if GSM_SH_FMAMIX
     float r;
     asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "=v"(r) : "v"(w), "v"(b), "v"(-0.0f));
     return r;
-#else
-    return hbits_to_f((uint16_t)(w >> 16)) * b;
-#endif
 }
 
 // computeSHColor (GaussianShared.h:38-116) specialised by degree like the

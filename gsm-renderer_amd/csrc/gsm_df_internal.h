@@ -49,6 +49,7 @@ struct DfArena {
     uint32_t* ikeys[2] = {nullptr, nullptr};      // [maxInstances] tile ids
     uint32_t* ivals[2] = {nullptr, nullptr};      // [maxInstances] gaussian ids
     uint32_t* radixHist = nullptr;
+    size_t radixHistBytes = 0;
     uint32_t* radixBinTotals = nullptr;
     uint32_t* starts = nullptr;                   // [tileCount + 1] first instance of each tile
     uint32_t* queue = nullptr;                    // blend work counter
@@ -59,6 +60,7 @@ struct DfArena {
     unsigned long long* blendStats = nullptr;     // [4] profiling bit 1: entries walked / with a real
                                                   // mean / blended, list entries (null: not counted)
 };
+inline SortSpace sort_space(const DfArena& A) { return SortSpace{A.radixHist, A.radixHistBytes, A.radixBinTotals, kSortTotalsWords}; }
 
 constexpr int kDfBlock = 256;
 // instance values: gaussian id in bits 0-29 (max_gaussians <= 30M < 2^30); bit 30 + e set when eye e

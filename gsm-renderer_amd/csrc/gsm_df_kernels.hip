@@ -22,19 +22,8 @@
 #include "gsm_internal.h"
 #include "gsm_types.h"
 
-#ifndef GSM_DF_EXEC_ALIVE
-#define GSM_DF_EXEC_ALIVE 1
-#endif
-// GSM_DF_MEAN_TEST 1: the blend tests every staged entry's mean (df_mean_valid, scalar) and pads a
-// batch to a multiple of 4 with mean -inf; 0: the kept entries' means are valid by construction
-#ifndef GSM_DF_MEAN_TEST
-#define GSM_DF_MEAN_TEST 0
-#endif
-// the blend's wave-uniform "every alpha is 0" test: 0 = integer range test (df_all_cut), 1 = packed
-// minimum and two compares (df_some_uncut)
-#ifndef GSM_DF_CUT_TEST
-#define GSM_DF_CUT_TEST 1
-#endif
+// The blend's kept entries' means are valid by construction (the per-entry mean test and the integer
+// "every alpha is 0" test it replaced: tools/exp/rejected_variants.patch)
 
 namespace gsm {
 
@@ -438,15 +427,7 @@ __device__ __forceinline__ void df_quadform(h2 mean, h2 cc, h2 cxy, h2 PX, h2 PY
     p1 = (ax + df_hi(by)) + (dx * df_hi(dy)) * c2;
 }
 
-// every alpha of the 2x2 group is 0 when each p is in (9, +inf] (the r^2 cutoff; NaN and negative p
-// are not): (bits - 0x4881) mod 2^16 <= 0x7C00 - 0x4881
-__device__ __forceinline__ bool df_all_cut(h2 p0, h2 p1) {
-    const df_u16x2 k = {(unsigned short)0x4881u, (unsigned short)0x4881u};
-    const df_u16x2 d0 = __builtin_bit_cast(df_u16x2, p0) - k, d1 = __builtin_bit_cast(df_u16x2, p1) - k;
-    const df_u16x2 m = __builtin_elementwise_max(d0, d1);
-    return max((uint32_t)m.x, (uint32_t)m.y) <= 0x7C00u - 0x4881u;
-}
-// the converse, in fewer instructions: some p of the 2x2 group is <= 9, negative or NaN.  p > 9 holds
+// some p of the 2x2 group is <= 9, negative or NaN (not every alpha is 0: the r^2 cutoff).  p > 9 holds
 // exactly for the bits in [0x4881, 0x7C00]; IEEE-754-2019 minimum (v_pk_minimum3_f16) keeps NaN, so
 // min(p0, p1) > 9 in both halves <=> all four p > 9 (one packed min and two ordered compares)
 // -- as the wave's lane mask: one ballot per compare, so each compare's mask is used as it is
@@ -496,11 +477,9 @@ __device__ __forceinline__ void df_blend_eye_w(DfEyeState& st, bool alive, h2 p0
     const h2 ONE = {(h1)1.0f, (h1)1.0f};
     const h1 c099 = (h1)0.99;
     const h2 C099 = {c099, c099};
-#if GSM_DF_EXEC_ALIVE
     // a lane whose eye is done keeps C and T (alpha 0 would leave the same bits: C + c * 0 == C,
     // T * 1 == T): its updates run under an EXEC mask of the live lanes instead of zeroing its alphas
     if (!alive) return;
-#endif
     const uint32_t b0 = df_u32(p0), b1 = df_u32(p1);
     df_u16x2 e0, e1;
     e0.x = tbl[b0 & 0xFFFFu];
@@ -510,12 +489,6 @@ __device__ __forceinline__ void df_blend_eye_w(DfEyeState& st, bool alive, h2 p0
     const h2 op = df_hi(df_h2(zw));
     h2 a0 = __builtin_elementwise_min(op * __builtin_bit_cast(h2, e0), C099);
     h2 a1 = __builtin_elementwise_min(op * __builtin_bit_cast(h2, e1), C099);
-#if !GSM_DF_EXEC_ALIVE
-    if (!alive) {
-        a0 = df_h2(0u);
-        a1 = df_h2(0u);
-    }
-#endif
     const h2 w0 = a0 * st.T[0], w1 = a1 * st.T[1];
     const h2 r = df_lo(df_h2(rg)), g = df_hi(df_h2(rg)), b = df_lo(df_h2(bw));
     st.Cr[0] = df_acc(st.Cr[0], r, w0);
@@ -526,13 +499,6 @@ __device__ __forceinline__ void df_blend_eye_w(DfEyeState& st, bool alive, h2 p0
     st.Cb[1] = df_acc(st.Cb[1], b, w1);
     st.T[0] = st.T[0] * (ONE - a0);
     st.T[1] = st.T[1] * (ONE - a1);
-}
-
-// gMean.x >= -60000.0h on the fp16 bits of a uniform word (integer compares, so the test stays on
-// the scalar unit): +0..+inf, or -0..-60000 (0xFB53); NaN and -inf fail
-__device__ __forceinline__ bool df_mean_valid(uint32_t meanWord) {
-    const uint32_t x = meanWord & 0xFFFFu;
-    return x <= 0x7C00u || (x >= 0x8000u && x <= 0xFB53u);
 }
 
 // max transmittance of a lane's 4 pixels >= fp16(1/255); T >= 0, so fp16 order is bit order
@@ -658,33 +624,21 @@ __global__ __launch_bounds__(NW * 64) void k_df_blend_eye(const uint32_t* __rest
                                      (uint32_t)div255[c & 0xFFu] | ((uint32_t)div255[(c >> 8) & 0xFFu] << 16));
                 sB[pos] = (uint32_t)div255[(c >> 16) & 0xFFu];
             }
-#if GSM_DF_MEAN_TEST
-            if (lane < 4u && nk + lane < ((nk + 3u) & ~3u)) sA[nk + lane] = make_uint4(0xFC00FC00u, 0u, 0u, 0u);
-#endif
             df_wave_sync();
             for (uint32_t j0 = 0; j0 < nk; j0 += 4) {
 #pragma unroll
                 for (uint32_t jj = 0; jj < 4; ++jj) {
                     const uint32_t j = j0 + jj;
                     const uint4 ra = sA[j];
-#if GSM_DF_MEAN_TEST
-                    const uint32_t mw = __builtin_amdgcn_readfirstlane(ra.x);
-                    if (df_mean_valid(mw)) {  // uniform
-#else
                     // a kept entry's mean passes the reference's mean test (gMean.x >= -60000): an
                     // eye whose mean fails it is flagged by k_df_expand (quad_bound_setup mode 1), so
                     // the only test left is the batch's end (uniform, no pad records)
                     const uint32_t mw = ra.x;
                     if (j < nk) {
-#endif
                         h2 p0, p1;
                         df_quadform(df_h2(mw), df_h2(ra.y), df_h2(ra.z), PX, PY, p0, p1);
                         if (STATS) nValid++;
-#if GSM_DF_CUT_TEST == 0
-                        const uint64_t some = __builtin_amdgcn_ballot_w64(!df_all_cut(p0, p1));
-#else
                         const uint64_t some = df_some_uncut_mask(p0, p1);
-#endif
                         if ((some & aliveM) != 0) {
                             df_blend_eye_w(E, alive, p0, p1, ra.z, ra.w, sB[j], tbl);
                             // T changes only here, so the per-eye test (:1872 / :1915) of the next

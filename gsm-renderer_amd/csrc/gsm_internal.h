@@ -169,6 +169,18 @@ __device__ __forceinline__ void st_sys128_at(void* base, uint32_t bytes, uint32_
 }
 
 // Device buffers of one renderer (the GlobalViewResources analogue, GlobalResources.swift:6-362).
+// A sort's device workspace and its sizes.  Every sort below plans its passes first and launches
+// nothing (returns kSortNoSpace) when one pass's per-block digit counts, super-group rows or digit
+// totals would not fit -- a knob or a grid rule changed without the allocation (the r05 wide-pass
+// A/B fault class); callers report GSM_ERR_INVALID_ASSIGNMENT_CAPACITY.
+struct SortSpace {
+    uint32_t* hist = nullptr;      // radix_workspace_bytes(capacity) bytes, zeroed once at allocation
+    size_t histBytes = 0;
+    uint32_t* binTotals = nullptr;  // digit totals (+ the tile passes' bucket starts)
+    size_t binWords = 0;
+};
+constexpr int kSortNoSpace = -1;
+
 struct DeviceArena {
     GaussianRenderData* renderData = nullptr;  // [maxG]
     short4* bounds = nullptr;                  // [maxG]
@@ -183,7 +195,8 @@ struct DeviceArena {
     uint32_t* valsKeep = nullptr;
     unsigned long long* blendTrace = nullptr;  // [4 * tiles * 4] (profiling bit 2 only)
     uint32_t* costMax = nullptr;               // [kCostMaxSlots] longest walk of the last blend
-    uint32_t* radixHist = nullptr;             // [256 * radixGrid]
+    uint32_t* radixHist = nullptr;             // radix_workspace_bytes(maxAssignments) bytes
+    size_t radixHistBytes = 0;
     uint32_t* radixBinTotals = nullptr;        // [kSortTotalsWords] (radix_sort_tiles)
     uint32_t* tileStart = nullptr;             // [tileCount + 1] first sorted entry of each tile
     uint32_t* tileQueue = nullptr;             // [kQueueStripes * kQueueStride] blend work counters
@@ -206,18 +219,9 @@ struct Tuning {
                               // or forced by GSM_SORT_RANK=ballot
     bool costOrder = true;    // GSM_BLEND_SCHED=0: blend units in index order instead of last frame's walks
     int blendWaves = 0;       // GSM_BLEND_WAVES=8|12|16: waves per blend workgroup (0: by frame size)
-    int tileLoBits = 0;       // GSM_SORT_LOBITS=4..8: width of the first tile pass (0: half the tile field)
     int blendClaim = 1;       // GSM_BLEND_CLAIM=early|late|auto (0/1/2): when a blend wave claims its next unit
     bool wideSort = true;     // GSM_SORT_WIDE=0: narrow passes only (no wide 9..11-bit tile or depth passes)
     bool sortScanless = true; // GSM_SORT_SCAN=kernel: narrow passes with the k_radix_scan launch (r05 default: none)
-    bool mgPixelsWB = true;   // a gathered multi-GPU frame's blend stores its pixels plainly and the last
-                              // exiting wave of each workgroup writes the XCD's L2 back at system scope
-                              // before arriving; GSM_MG_PIXELS=wt: write-through pixel stores instead
-                              // (config 4 / W = 8 slab blend 96 -> 75 us with wb: DESIGN.md 7)
-    int mgPushPerCU = 4;      // GSM_MG_PUSH_GRID=k: the push (k_part_copy) runs k workgroups per CU over the
-                              // runs (0: one workgroup per 256-id block)
-    bool wide12 = false;      // GSM_SORT_WIDE12=1: a 12-bit tile field (2049..4096 tiles) in one 12-bit
-                              // wide pass instead of two narrow passes (measured slower: DESIGN.md 4)
     bool blendPairs = true;   // half-tile frames on one GPU: two units per blend wave (k_blend_pw, r05);
                               // GSM_BLEND_PAIRS=0: one unit per wave (k_blend_px)
     int pairBucket = 128;     // GSM_BLEND_PAIR_SPLIT=b (0..256): the units whose last walk exceeds (256 - b) / 256
@@ -246,18 +250,14 @@ constexpr float kBlendZeroP = 34.65625f;
 
 constexpr int kProjectBlock = 256;
 constexpr int kRadixBlock = 256;
-#ifndef GSM_RADIX_ITEMS
-#define GSM_RADIX_ITEMS 16
-#endif
-constexpr int kRadixItems = GSM_RADIX_ITEMS;  // keys per thread per chunk (4096-key chunks)
+constexpr int kRadixItems = 16;  // keys per thread per chunk (4096-key chunks)
 constexpr int kRadixChunk = kRadixBlock * kRadixItems;
 // wide radix digits (gsm_sort.hip): up to 11 bits, 2048 bins
 constexpr uint32_t kWideMaxBits = 11, kWideBins = 1u << kWideMaxBits;
-// one 12-bit pass for a tile field of 2049..4096 tiles (1080p: 4080) -- Tuning::wide12
-constexpr uint32_t kWide12Bits = 12, kWide12Bins = 1u << kWide12Bits;
 // radix_sort_tiles' workspace beside the histogram: two passes' digit totals + the bucket starts
 // (narrow passes, 768 words), or one wide pass's 2048 digit totals
-constexpr size_t kSortTotalsWords = kWide12Bins;
+constexpr size_t kSortTotalsWords = kWideBins;
+inline SortSpace sort_space(const DeviceArena& A) { return SortSpace{A.radixHist, A.radixHistBytes, A.radixBinTotals, kSortTotalsWords}; }
 
 // project + cull + SH + tile count + per-block count sums (GlobalShaders.metal:19-123, 563-616)
 void launch_project(bool halfInput, uint32_t shDegree, const void* world, const void* harmonics,
@@ -300,11 +300,12 @@ void launch_half_lists(const uint32_t* sortedVals, uint32_t tileBegin, uint32_t 
 // per-tile binary search headers (GlobalShaders.metal:304-363), tiles of rows [rowBegin,rowEnd)
 void launch_headers(const uint32_t* sortedKeys, const FrameGeometry& geo, const DeviceArena& A,
                     hipStream_t stream);
-// front-to-back fp16 blend + clear (GlobalShaders.metal:140-154, 1030-1187)
-void launch_blend(const FrameGeometry& geo, const DeviceArena& A,
+// front-to-back fp16 blend + clear (GlobalShaders.metal:140-154, 1030-1187); returns the kernel it
+// launched (gsm_blend_kernel, include/gsm_debug.h; 0 for an empty frame)
+int launch_blend(const FrameGeometry& geo, const DeviceArena& A,
                   void* color, size_t colorPitch, void* depth, size_t depthPitch, int numCUs,
                   bool costOrder, int colorFormat, hipStream_t stream, int waves = 0, int claim = 1,
-                  const MgArrive* arrive = nullptr, bool arriveWB = false, bool pairs = false);
+                  const MgArrive* arrive = nullptr, bool pairs = false);
 // k_blend_pw (gsm_blend_pw.hip): two half-tile units per wave, one GPU's frame
 void launch_blend_pw(const FrameGeometry& g, const DeviceArena& A, void* color, size_t colorPitch, void* depth,
                      size_t depthPitch, int numCUs, bool costOrder, int colorFormat, hipStream_t s, int waves);
@@ -313,24 +314,27 @@ int blend_pairs_per_lane(uint32_t numTiles, int numCUs);
 uint32_t blend_units_per_tile(uint32_t numTiles, int numCUs);
 
 // Stable LSD radix sort of (key, value) pairs; n read from device memory *nPtr.
-// Returns the index (0/1) of the ping-pong buffer holding the result.
+// Returns the index (0/1) of the ping-pong buffer holding the result (or kSortNoSpace).
 // ballot: ranks from ballot matches (Tuning::ballotRank) instead of lane-ordered LDS atomics.
 int radix_sort_pairs(uint32_t* keys[2], uint32_t* vals[2], const uint32_t* nPtr, uint32_t capacity,
-                     int firstDigit, int numDigits, uint32_t* hist, uint32_t* binTotals,
+                     int firstDigit, int numDigits, const SortSpace& ws,
                      hipStream_t stream, bool ballot, bool scanless = true);
 // Stable LSD radix sort by bits [shift, shift + bits) only, in ceil(bits / 8) passes of
 // near-equal digit widths (4..8 bits), or -- `wide` and where that saves a pass -- ceil(bits / 11)
 // passes of 9..11 bits.  binTotals: kSortTotalsWords words.  Returns the ping-pong index of the result.
 int radix_sort_bits(uint32_t* keys[2], uint32_t* vals[2], const uint32_t* nPtr, uint32_t capacity,
-                    uint32_t shift, uint32_t bits, uint32_t* hist, uint32_t* binTotals, hipStream_t stream,
+                    uint32_t shift, uint32_t bits, const SortSpace& ws, hipStream_t stream,
                     bool ballot, bool wide = false, bool scanless = true);
 // the frame sort's tile field (tiles [tileBase, tileBase + numTiles) of allTiles, bits <= 16) with
 // the tile starts written by its last pass (tileStart[0..allTiles], lower bounds for empty tiles);
 // one wide pass relative to tileBase when numTiles <= 2048 and `wide`; binTotals: kSortTotalsWords words
 int radix_sort_tiles(uint32_t* keys[2], uint32_t* vals[2], const uint32_t* nPtr, uint32_t capacity, uint32_t shift,
-                     uint32_t* hist, uint32_t* binTotals, uint32_t* tileStart, uint32_t tileBase, uint32_t numTiles,
-                     uint32_t allTiles, hipStream_t stream, bool ballot, int loBits = 0, bool wide = true,
-                     bool wide12 = false, bool scanless = true);
+                     const SortSpace& ws, uint32_t* tileStart, uint32_t tileBase, uint32_t numTiles,
+                     uint32_t allTiles, hipStream_t stream, bool ballot, bool wide = true, bool scanless = true);
+// the workspace footprint of one pass (words of `hist`, incl. the super-group rows in front), and
+// whether every pass radix_sort_bits plans fits `ws` (host only: no launch)
+size_t sort_pass_hist_words(bool wide, int bits, uint32_t grid);
+bool sort_bits_plan_fits(uint32_t capacity, uint32_t bits, bool wide, const SortSpace& ws);
 // scanless: narrow passes without the k_radix_scan launch (super-group digit rows, gsm_sort.hip;
 // Tuning::sortScanless) -- the same order either way
 uint32_t radix_grid_for_capacity(uint32_t capacity);
@@ -404,14 +408,21 @@ __device__ __forceinline__ void unit_order_block(const uint16_t* __restrict__ co
             if (lane >= (uint32_t)o) inc += v;
         }
         const uint32_t e = inc - local;
-        *(uint4*)(base + lane * 4u) = make_uint4(e, e + c.x, e + c.x + c.y, e + c.x + c.y + c.z);
+        const uint4 starts = make_uint4(e, e + c.x, e + c.x + c.y, e + c.x + c.y + c.z);
+        *(uint4*)(base + lane * 4u) = starts;
+        // the pair walk's split: the units of buckets [0, splitBucket) -- the longest walks -- run alone.
+        // Taken here, from the lane that owns bucket splitBucket's start, before the ordering loop below
+        // advances base[] (read after the barrier it raced with other waves' atomics).
+        if (splitBucket) {
+            if (splitBucket >= kUoBuckets) {
+                if (lane == 0) costMax[kCostMaxSlots] = n;
+            } else if (lane == splitBucket / 4u) {
+                const uint32_t q = splitBucket & 3u;
+                costMax[kCostMaxSlots] = q == 0 ? starts.x : q == 1 ? starts.y : q == 2 ? starts.z : starts.w;
+            }
+        }
     }
     __syncthreads();
-    // the pair walk's split: the units of buckets [0, splitBucket) -- the longest walks -- run alone
-    if (splitBucket && t == 0) {
-        costMax[kCostMaxSlots] = splitBucket >= kUoBuckets ? n : base[splitBucket];
-        costMax[kCostMaxSlots + 1] = mx;
-    }
 
     for (uint32_t b0 = 0; b0 < n; b0 += (uint32_t)NT * UN) {
         uint32_t c[UN];

@@ -12,9 +12,6 @@
 #include "gsm_internal.h"
 #include "gsm_types.h"
 
-#ifndef GSM_SCAN_RUNS
-#define GSM_SCAN_RUNS 1
-#endif
 // Stage attribution of k_project (A/B builds only, tools/gpu_proj_stages.sh): GSM_PROJ_STOP = k ends the
 // projection after stage k (1 loads + view / clip + the early culls, 2 + the 3D covariance, 3 + the 2D
 // covariance and its stabilisation, 4 + theta / sigmas, 5 + the radius / ink / screen culls and the OBB,
@@ -856,7 +853,7 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_blocks(uint32_t* __restri
     // contiguous run of `per` sums (16-byte loads, all in flight), then ONE block scan of the run
     // totals -- instead of one block scan per 4096-sum row (config 3: 5)
     const uint32_t per = ((nb + kScanThreads - 1) / kScanThreads + 3u) & ~3u;
-    if (GSM_SCAN_RUNS && nb > kRow && per <= 32u) {
+    if (nb > kRow && per <= 32u) {
         constexpr uint32_t kV = 8;
         uint4 v[kV];
         const uint32_t b0 = threadIdx.x * per;

@@ -316,6 +316,7 @@ class MultiGpu {
     Targets frameT_{};         // phase 0's targets (gathering or not: the barrier steps of finishFrame)
     hipEvent_t inputEvent_ = nullptr;  // gsm_multigpu_wait_event (one-shot, the next phase 0)
     gsm_status frameErr_ = GSM_OK;  // this rank's error of the current frame (barrier-only phases after it)
+    bool launchFailed_ = false;     // the last run() saw a failed launch (finishFrame's status)
     bool interleave_ = false;  // slab rows interleaved (GSM_MG_ROWS=interleaved at prepare)
     // Pipelined (GSM_MG_PIPELINE=1 at prepare, every rank alike): phases 0-1 on the library's own stream
     // (front_), phases 2-3 on the caller's, joined by events -- frame f + 1's projection and push run
@@ -560,10 +561,12 @@ gsm_status MultiGpu::finishFrame(hipStream_t s) {
         const int p = nextPhase_;
         // phase 1 needs no caller argument: the push runs when phase 0 published this rank's counts (the
         // owners expect those records); from phase 2 on the frame is abandoned -- barrier steps only,
-        // a failed arrival at barrier 2 when gathering
+        // a failed arrival at barrier 2 when gathering.  The first real failure of any phase is returned
+        // (phase 1's push status, or a launch that failed in any phase: ADVICE r05), not the abandonment.
         if (p >= 2 && frameErr_ == GSM_OK) frameErr_ = GSM_ERR_RENDER_FAILED;
+        launchFailed_ = false;
         const gsm_status st = run(p, s, nullptr, nullptr, 0, 0, frameT_, 0, nullptr, 0, nullptr);
-        if (first == GSM_OK && p == 1) first = st;
+        if (first == GSM_OK && (launchFailed_ || p == 1)) first = launchFailed_ ? GSM_ERR_RENDER_FAILED : st;
     }
     return first;
 }
@@ -684,7 +687,10 @@ gsm_status MultiGpu::run(int p, hipStream_t s, const gsm_gaussian_input* in, con
             break;
         }
     }
-    if (hipGetLastError() != hipSuccess) return GSM_ERR_RENDER_FAILED;
+    if (hipGetLastError() != hipSuccess) {
+        launchFailed_ = true;
+        return GSM_ERR_RENDER_FAILED;
+    }
     return frameErr_;
 }
 

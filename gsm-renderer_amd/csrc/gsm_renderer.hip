@@ -111,7 +111,8 @@ gsm_status GlobalRenderer::create(const gsm_renderer_config& cfg, int hipDevice,
     GSM_ALLOC(A.keys[1], cap * sizeof(uint32_t));
     GSM_ALLOC(A.vals[0], cap * sizeof(uint32_t));
     GSM_ALLOC(A.vals[1], cap * sizeof(uint32_t));
-    GSM_ALLOC(A.radixHist, radix_workspace_bytes(r->maxAssignments_));
+    A.radixHistBytes = radix_workspace_bytes(r->maxAssignments_);
+    GSM_ALLOC(A.radixHist, A.radixHistBytes);
     if (st == GSM_OK && hipMemset(A.radixHist, 0, radix_workspace_bytes(r->maxAssignments_)) != hipSuccess)
         st = GSM_ERR_FAILED_TO_ALLOCATE_BUFFER;
     GSM_ALLOC(A.radixBinTotals, kSortTotalsWords * sizeof(uint32_t));  // radix_sort_tiles: totals + block table
@@ -384,7 +385,7 @@ gsm_status GlobalRenderer::partitionPush(hipStream_t s, uint32_t world, uint32_t
     a.count = partCount_;
     if (world != partSlabs_.n) return GSM_ERR_INVALID_ARGUMENT;  // one slab per rank, as partitionCounts split
     launch_partition_push(a, world, rank, part_, counts, peers, recvCount, partSlabs_, arrive, s,
-                          tuning_.mgPushPerCU > 0 ? (uint32_t)(tuning_.mgPushPerCU * numCUs_) : 0u);
+                          (uint32_t)(4 * numCUs_));  // 4 workgroups per CU looping over the runs
     if (hipGetLastError() != hipSuccess) return GSM_ERR_RENDER_FAILED;
     return GSM_OK;
 }
@@ -476,9 +477,9 @@ gsm_status GlobalRenderer::runFrame(hipStream_t s, const ProjectArgs& a, uint32_
         // (multi-GPU) takes one wide pass
         const uint32_t localTiles = rowCount() * tilesX_;
         const int res = radix_sort_tiles(kb, vb, &arena_.header->totalAssignments, maxAssignments_, 16,
-                                         arena_.radixHist, arena_.radixBinTotals, arena_.tileStart, 0u, localTiles,
-                                         tileCount_, s, ballot, tuning_.tileLoBits, tuning_.wideSort,
-                                         tuning_.wideSort && tuning_.wide12, tuning_.sortScanless);
+                                         sort_space(arena_), arena_.tileStart, 0u, localTiles,
+                                         tileCount_, s, ballot, tuning_.wideSort, tuning_.sortScanless);
+        if (res == kSortNoSpace) return GSM_ERR_INVALID_ASSIGNMENT_CAPACITY;  // (nothing of the sort launched)
         tile_depth_sort(kb[res], vb[res], kb[res ^ 1], vb[res ^ 1], arena_.tileStart, 0u, localTiles, s, ballot,
                         arena_.halfVals[0], arena_.halfVals[1],
                         arena_.halfCount, tileCount_, capture, numCUs_);
@@ -486,8 +487,9 @@ gsm_status GlobalRenderer::runFrame(hipStream_t s, const ProjectArgs& a, uint32_
         sortedVals_ = capture ? vb[res ^ 1] : nullptr;
     } else {
         const int res = radix_sort_pairs(kb, vb, &arena_.header->totalAssignments, maxAssignments_, 0,
-                                         sortPassCount(), arena_.radixHist, arena_.radixBinTotals, s, ballot,
+                                         sortPassCount(), sort_space(arena_), s, ballot,
                                          tuning_.sortScanless);
+        if (res == kSortNoSpace) return GSM_ERR_INVALID_ASSIGNMENT_CAPACITY;
         sortedKeys_ = kb[res];
         sortedVals_ = vb[res];
     }
@@ -502,9 +504,9 @@ gsm_status GlobalRenderer::runFrame(hipStream_t s, const ProjectArgs& a, uint32_
     arena_.blendTrace = (profiling_ & 4) ? traceBuf_ : nullptr;
     // the schedule from the walks the previous frame's blend recorded (same stream: no join)
     if (prof || blendOnly) hipEventRecord(ev[5], s);
-    launch_blend(g, arena_, color, colorPitch, depth, depthPitch, numCUs_, costOrder,
+    lastBlendKernel_ = launch_blend(g, arena_, color, colorPitch, depth, depthPitch, numCUs_, costOrder,
                  (int)config_.color_format, s, tuning_.blendWaves, tuning_.blendClaim, blendArrive,
-                 tuning_.mgPixelsWB, tuning_.blendPairs);
+                 tuning_.blendPairs);
     if (prof || blendOnly) hipEventRecord(ev[6], s);
     if (prof || blendOnly) profFrames_++;
     haveTimes_ = profFrames_ > 0;

@@ -69,6 +69,7 @@ class GlobalRenderer {
     bool halfPrecision() const { return config_.precision == GSM_PRECISION_FLOAT16; }
 
     gsm_status counters(gsm_debug_counters* out);
+    int lastBlendKernel() const { return lastBlendKernel_; }
     gsm_status debugCopy(int which, void* dst, size_t bytes, size_t* needed);
     gsm_status setProfiling(int flags);  // bit0: stage events, bit1: keep unsorted keys
     gsm_status stageTimes(float* ms, int n);
@@ -131,6 +132,7 @@ class GlobalRenderer {
     uint32_t sampleFrame_ = 0;  // frames since setProfiling (blend-event sampling)
     hipEvent_t* frameEvents(uint32_t frame) { return &events_[(frame % kEventRing) * (GSM_STAGE_COUNT + 1)]; }
     int profiling_ = 0;
+    int lastBlendKernel_ = 0;  // gsm_blend_kernel of the last enqueued frame (gsm_global_debug_blend_kernel)
     bool keptRenderData_ = false;  // the last frame wrote GaussianRenderData for readback
     bool haveTimes_ = false;
     uint32_t lastCount_ = 0, lastWidth_ = 0, lastHeight_ = 0;

@@ -23,9 +23,6 @@
 namespace gsm {
 
 constexpr int kWaves = kRadixBlock / 64;
-#ifndef GSM_UPSWEEP_COPIES
-#define GSM_UPSWEEP_COPIES 4
-#endif
 
 __device__ __forceinline__ void block_range(uint32_t n, uint32_t grid, uint32_t b, uint32_t* begin,
                                             uint32_t* end) {
@@ -100,10 +97,10 @@ __global__ __launch_bounds__(kRadixBlock) void k_radix_upsweep(const uint32_t* _
                                                                uint32_t* __restrict__ super,
                                                                uint32_t* __restrict__ superClear) {
     constexpr uint32_t R = 1u << BITS;
-    // GSM_UPSWEEP_COPIES counter copies per wave (lane & (copies - 1) picks one), rows padded by a
+    // CP counter copies per wave (lane & (copies - 1) picks one), rows padded by a
     // word so one digit's copies sit in different LDS banks: fewer same-address collisions among
     // the 64 lanes of one ds_add
-    constexpr uint32_t CP = GSM_UPSWEEP_COPIES, RS = R + (CP > 1 ? 1u : 0u);
+    constexpr uint32_t CP = 4, RS = R + (CP > 1 ? 1u : 0u);
     __shared__ uint32_t cnt[kWaves * CP][RS];
     const uint32_t wave = threadIdx.x >> 6;
     const uint32_t row = wave * CP + (threadIdx.x & (CP - 1u));
@@ -442,12 +439,9 @@ __global__ __launch_bounds__(kRadixBlock) void k_radix_downsweep(
 }
 
 // ---------------------------------------------------------------------------
-// Wide passes take chunks of kWideChunk keys (GSM_WIDE_ITEMS per thread): their per-chunk digit
+// Wide passes take chunks of kWideChunk keys (kWideItems per thread; 8 measured slower): their per-chunk digit
 // bookkeeping is heavier, so their blocks are fewer per CU.
-#ifndef GSM_WIDE_ITEMS
-#define GSM_WIDE_ITEMS 16
-#endif
-constexpr int kWideItems = GSM_WIDE_ITEMS;
+constexpr int kWideItems = 16;
 constexpr int kWideChunk = kRadixBlock * kWideItems;
 static_assert(kWideItems % 4 == 0 && kWideItems <= kRadixItems, "wide chunks: 16-B loads, <= the narrow chunk");
 __device__ __forceinline__ void block_range_w(uint32_t n, uint32_t grid, uint32_t b, uint32_t* begin, uint32_t* end) {
@@ -611,7 +605,7 @@ __global__ __launch_bounds__(kRadixBlock) void k_wide_downsweep(
     constexpr uint32_t R = 1u << BITS;
     constexpr uint32_t DPT = R / kRadixBlock;  // digits per thread
     constexpr uint32_t RP = (R + R / 8 + 255u) / 256u * 256u;  // padded counter rows (whole uint4 zeroing rounds)
-    static_assert(DPT >= 2 && DPT <= 8, "wide digits: 9..11 bits (12: k_wide12_downsweep)");
+    static_assert(DPT >= 2 && DPT <= 8, "wide digits: 9..11 bits");
     __shared__ __attribute__((aligned(16))) uint32_t waveCnt[kWaves][RP];  // ranks, then each wave's LDS start per digit
     __shared__ uint32_t adj[RP];               // per digit: global destination minus LDS start
     __shared__ uint32_t sKeys[kWideChunk];
@@ -733,152 +727,6 @@ __global__ __launch_bounds__(kRadixBlock) void k_wide_downsweep(
     }
 }
 
-// 12-bit wide downsweep (a tile field of 2049..4096 tiles: 1080p's 4080): k_wide_downsweep's
-// algorithm with the per-wave digit counters packed two 16-bit halves per word (a wave ranks at most
-// 1024 keys of a chunk, so a half never carries into its neighbour; lanes of one ds_add_rtn_u32 on the
-// same word are still served in lane order, so a lane's old half is its stable rank), and the
-// per-digit global offsets written over the counters once the chunk sits in LDS: 69 KB of LDS, two
-// workgroups per CU (the unpacked layout needs 125 KB: one).
-template <bool BALLOT, bool STARTS>
-__global__ __launch_bounds__(kRadixBlock) void k_wide12_downsweep(
-    const uint32_t* __restrict__ keysIn, const uint32_t* __restrict__ valsIn, uint32_t* __restrict__ keysOut,
-    uint32_t* __restrict__ valsOut, const uint32_t* __restrict__ nPtr, uint32_t shift, uint32_t base,
-    const uint32_t* __restrict__ hist, const uint32_t* __restrict__ binTotals, uint32_t* __restrict__ tileStart,
-    uint32_t numTiles, uint32_t allTiles) {
-    constexpr uint32_t R = kWide12Bins, DPT = R / kRadixBlock, WPT = DPT / 2;  // 16 digits, 8 words per thread
-    constexpr uint32_t RWP = (R / 2 + R / 16 + 255u) / 256u * 256u;           // padded words per wave: 2304
-    static_assert(kWaves * RWP >= R + R / 8, "the digits' offsets fit over the counters");
-    static_assert((kWaves * RWP) % (4 * kRadixBlock) == 0, "counter rows in whole uint4 rounds");
-    static_assert(kWideItems * 64 < 65536, "a wave's count of one digit fits 16 bits");
-    __shared__ __attribute__((aligned(16))) uint32_t cnt[kWaves][RWP];
-    __shared__ uint32_t sKeys[kWideChunk];
-    __shared__ uint32_t sVals[kWideChunk];
-    __shared__ uint32_t part[kWaves];
-    uint32_t* adj = &cnt[0][0];  // after the LDS scatter: digit d's global destination minus LDS start, at wide_pad(d)
-    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
-    const uint32_t n = *nPtr;
-    uint32_t begin, end;
-    block_range_w(n, gridDim.x, blockIdx.x, &begin, &end);
-    const uint32_t d0 = tid * DPT, w0 = tid * WPT;  // this thread's digits and counter words
-    auto zero_counters = [&]() {
-        uint4* z = (uint4*)&cnt[0][0];
-#pragma unroll
-        for (uint32_t i = 0; i < kWaves * RWP / 4 / kRadixBlock; ++i) z[i * kRadixBlock + tid] = make_uint4(0u, 0u, 0u, 0u);
-    };
-    uint32_t gbase[DPT];
-    {
-        uint32_t run = 0;
-#pragma unroll
-        for (uint32_t i = 0; i < DPT; ++i) {
-            gbase[i] = run;
-            run += binTotals[d0 + i];
-        }
-        uint32_t tot;
-        const uint32_t off = wide_block_scan(run, part, &tot);
-#pragma unroll
-        for (uint32_t i = 0; i < DPT; ++i) gbase[i] += off;
-        if (STARTS && blockIdx.x == 0) {
-            for (uint32_t t = tid; t < base; t += kRadixBlock) tileStart[t] = 0u;
-#pragma unroll
-            for (uint32_t i = 0; i < DPT; ++i)
-                if (d0 + i < numTiles) tileStart[base + d0 + i] = gbase[i];
-            for (uint32_t t = base + numTiles + tid; t <= allTiles; t += kRadixBlock) tileStart[t] = n;
-        }
-        if (begin >= end) return;
-        const uint32_t* row = hist + (size_t)blockIdx.x * (R + kWideRowPad) + d0;  // block-major (k_wide_scan)
-#pragma unroll
-        for (uint32_t i = 0; i < DPT; ++i) gbase[i] += row[i];
-        zero_counters();
-        __syncthreads();
-    }
-    const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-    for (uint32_t cbase = begin; cbase < end; cbase += kWideChunk) {
-        uint32_t k[kWideItems], v[kWideItems], rank[kWideItems];
-#pragma unroll
-        for (int j = 0; j < kWideItems; ++j) {
-            const uint32_t idx = cbase + wave * (64 * kWideItems) + j * 64 + lane;
-            const bool valid = idx < end;
-            k[j] = valid ? keysIn[idx] : 0u;
-            v[j] = valid ? valsIn[idx] : 0u;
-        }
-#pragma unroll
-        for (int j = 0; j < kWideItems; ++j) {
-            const uint32_t idx = cbase + wave * (64 * kWideItems) + j * 64 + lane;
-            const bool valid = idx < end;
-            const uint32_t d = ((k[j] >> shift) - base) & (R - 1u);
-            uint32_t* word = &cnt[wave][wide_pad(d >> 1)];
-            const uint32_t sh = (d & 1u) * 16u;
-            if constexpr (BALLOT) {
-                const uint64_t peers = match_digit<kWide12Bits>(d, valid);
-                const uint32_t before = (*word >> sh) & 0xFFFFu;
-                // one leader per digit; the two digits of a word add to different halves
-                if (valid && (peers & lt) == 0) atomicAdd(word, (uint32_t)__popcll(peers) << sh);
-                rank[j] = before + (uint32_t)__popcll(peers & lt);
-            } else {
-                rank[j] = valid ? ((atomicAdd(word, 1u << sh) >> sh) & 0xFFFFu) : 0u;
-            }
-        }
-        __syncthreads();
-        // per digit: chunk total, its LDS start (scan over digits), each wave's start within it
-        uint32_t adjR[DPT];
-        {
-            uint32_t x[WPT][kWaves], run = 0;
-#pragma unroll
-            for (uint32_t i = 0; i < WPT; ++i)
-#pragma unroll
-                for (int w = 0; w < kWaves; ++w) {
-                    x[i][w] = cnt[w][wide_pad(w0 + i)];
-                    run += (x[i][w] & 0xFFFFu) + (x[i][w] >> 16);
-                }
-            uint32_t all;
-            uint32_t ls = wide_block_scan(run, part, &all);
-#pragma unroll
-            for (uint32_t i = 0; i < WPT; ++i) {
-                uint32_t lo[kWaves], hi[kWaves];
-#pragma unroll
-                for (int h = 0; h < 2; ++h) {  // digit d0 + 2i + h
-                    const uint32_t dd = 2u * i + (uint32_t)h;
-                    adjR[dd] = gbase[dd] - ls;
-#pragma unroll
-                    for (int w = 0; w < kWaves; ++w) {
-                        const uint32_t c = h ? (x[i][w] >> 16) : (x[i][w] & 0xFFFFu);
-                        (h ? hi : lo)[w] = ls;
-                        ls += c;
-                        gbase[dd] += c;
-                    }
-                }
-#pragma unroll
-                for (int w = 0; w < kWaves; ++w) cnt[w][wide_pad(w0 + i)] = lo[w] | (hi[w] << 16);
-            }
-        }
-        __syncthreads();
-#pragma unroll
-        for (int j = 0; j < kWideItems; ++j) {
-            const uint32_t idx = cbase + wave * (64 * kWideItems) + j * 64 + lane;
-            if (idx < end) {
-                const uint32_t d = ((k[j] >> shift) - base) & (R - 1u);
-                const uint32_t pos = ((cnt[wave][wide_pad(d >> 1)] >> ((d & 1u) * 16u)) & 0xFFFFu) + rank[j];
-                sKeys[pos] = k[j];
-                sVals[pos] = v[j];
-            }
-        }
-        __syncthreads();
-#pragma unroll
-        for (uint32_t i = 0; i < DPT; ++i) adj[wide_pad(d0 + i)] = adjR[i];
-        __syncthreads();
-        const uint32_t cn = min((uint32_t)kWideChunk, end - cbase);
-        for (uint32_t p = tid; p < cn; p += kRadixBlock) {
-            const uint32_t key = sKeys[p];
-            const uint32_t dst = adj[wide_pad(((key >> shift) - base) & (R - 1u))] + p;
-            keysOut[dst] = key;
-            valsOut[dst] = sVals[p];
-        }
-        __syncthreads();
-        zero_counters();
-        __syncthreads();
-    }
-}
-
 static uint32_t wide_grid_for_capacity(uint32_t capacity) {
     uint32_t g = (capacity + kWideChunk - 1) / kWideChunk;  // (<= 1024 rows: radix_workspace_bytes)
     if (g > 1024) g = 1024;
@@ -892,12 +740,8 @@ static void wide_pass(uint32_t* kin, uint32_t* vin, uint32_t* kout, uint32_t* vo
                       uint32_t allTiles) {
     hist += kSuperWords;  // (radix_workspace_bytes: the narrow passes' super-group rows come first)
 #define GSM_WIDE_DOWN(B, BAL, S)                                                                              \
-    if (B == kWide12Bits)                                                                                     \
-        hipLaunchKernelGGL((k_wide12_downsweep<BAL, S>), dim3(grid), dim3(kRadixBlock), 0, s, kin, vin, kout, \
-                           vout, nPtr, shift, base, hist, binTotals, tileStart, numTiles, allTiles);          \
-    else                                                                                                      \
-        hipLaunchKernelGGL((k_wide_downsweep<(B < 12 ? B : 11), BAL, S>), dim3(grid), dim3(kRadixBlock), 0, s, kin, vin, \
-                           kout, vout, nPtr, shift, base, hist, binTotals, tileStart, numTiles, allTiles)
+    hipLaunchKernelGGL((k_wide_downsweep<B, BAL, S>), dim3(grid), dim3(kRadixBlock), 0, s, kin, vin, kout, vout, \
+                       nPtr, shift, base, hist, binTotals, tileStart, numTiles, allTiles)
 #define GSM_WIDE_PASS(B)                                                                                         \
     hipLaunchKernelGGL(k_wide_upsweep<B>, dim3(grid), dim3(kRadixBlock), 0, s, kin, nPtr, shift, base, hist);    \
     hipLaunchKernelGGL(k_wide_scan<B>, dim3((1u << B) / kWideScanDigits), dim3(256), 0, s, hist, grid, nPtr, binTotals); \
@@ -911,18 +755,34 @@ static void wide_pass(uint32_t* kin, uint32_t* vin, uint32_t* kout, uint32_t* vo
     switch (bits) {
         case 9: GSM_WIDE_PASS(9); break;
         case 10: GSM_WIDE_PASS(10); break;
-        case 12: GSM_WIDE_PASS(12); break;
         default: GSM_WIDE_PASS(11); break;
     }
 #undef GSM_WIDE_PASS
 #undef GSM_WIDE_DOWN
 }
 
+size_t sort_pass_hist_words(bool wide, int bits, uint32_t grid) {
+    // narrow: digit-major counts hist[d][block] (k_radix_upsweep / k_radix_scan); wide: block-major rows
+    // of 2^bits + kWideRowPad words (k_wide_upsweep); both behind the scanless super-group row sets
+    const size_t rows = wide ? ((size_t)1 << bits) + kWideRowPad : ((size_t)1 << bits);
+    return kSuperWords + rows * grid;
+}
+
 size_t radix_workspace_bytes(uint32_t capacity) {
-    // the scanless super-group row sets (zero at allocation; see kSuperGroup), then the per-block digit counts: <= 1024 blocks x 256 digits (narrow), x 2048 (wide)
-    const uint32_t g = std::max(radix_grid_for_capacity(capacity), wide_grid_for_capacity(capacity));
-    const size_t wide = (size_t)(kWide12Bins + kWideRowPad) * g * sizeof(uint32_t);
-    return kSuperWords * sizeof(uint32_t) + (wide > (size_t)256 * 1024 * 4 ? wide : (size_t)256 * 1024 * sizeof(uint32_t));
+    // the scanless super-group row sets (zero at allocation; see kSuperGroup), then the per-block digit
+    // counts of the widest pass any sort of this capacity plans: 256 digits (narrow) or 2^kWideMaxBits
+    const size_t narrow = sort_pass_hist_words(false, 8, radix_grid_for_capacity(capacity));
+    const size_t wide = sort_pass_hist_words(true, (int)kWideMaxBits, wide_grid_for_capacity(capacity));
+    return std::max(narrow, wide) * sizeof(uint32_t);
+}
+
+// the passes' footprints against the workspace (nothing is launched for a plan that does not fit)
+static bool pass_fits(const SortSpace& ws, bool wide, int bits, uint32_t grid, size_t binWords) {
+    if (!ws.hist || !ws.binTotals) return false;
+    if (sort_pass_hist_words(wide, bits, grid) * sizeof(uint32_t) > ws.histBytes) return false;
+    // narrow passes read <= 1024 blocks' rows (k_radix_scan's column in registers, the super rows)
+    if (!wide && grid > kSuperRows * kSuperGroup) return false;
+    return binWords <= ws.binWords;
 }
 
 uint32_t radix_grid_for_capacity(uint32_t capacity) {
@@ -972,43 +832,59 @@ static void radix_pass(uint32_t* kin, uint32_t* vin, uint32_t* kout, uint32_t* v
 }
 
 int radix_sort_pairs(uint32_t* keys[2], uint32_t* vals[2], const uint32_t* nPtr, uint32_t capacity,
-                     int firstDigit, int numDigits, uint32_t* hist, uint32_t* binTotals,
-                     hipStream_t s, bool ballot, bool scanlessOn) {
+                     int firstDigit, int numDigits, const SortSpace& ws, hipStream_t s, bool ballot, bool scanlessOn) {
     const uint32_t grid = radix_grid_for_capacity(capacity);
+    if (!pass_fits(ws, false, 8, grid, 256)) return kSortNoSpace;
     int cur = 0;
     const bool scanless = scanlessOn && numDigits % 2 == 0;
     for (int dgt = firstDigit; dgt < firstDigit + numDigits; ++dgt) {
-        radix_pass(keys[cur], vals[cur], keys[cur ^ 1], vals[cur ^ 1], nPtr, grid, (uint32_t)dgt * 8u, 8, hist,
-                   binTotals, s, ballot, nullptr, false, scanless ? (dgt - firstDigit) & 1 : -1);
+        radix_pass(keys[cur], vals[cur], keys[cur ^ 1], vals[cur ^ 1], nPtr, grid, (uint32_t)dgt * 8u, 8, ws.hist,
+                   ws.binTotals, s, ballot, nullptr, false, scanless ? (dgt - firstDigit) & 1 : -1);
         cur ^= 1;
     }
     return cur;
 }
 
+bool sort_bits_plan_fits(uint32_t capacity, uint32_t bits, bool wide, const SortSpace& ws) {
+    const uint32_t grid = radix_grid_for_capacity(capacity), wgrid = wide_grid_for_capacity(capacity);
+    const uint32_t narrowPasses = (bits + 7) / 8, widePasses = (bits + kWideMaxBits - 1) / kWideMaxBits;
+    const bool useWide = wide && widePasses < narrowPasses;
+    const uint32_t passes = useWide ? widePasses : narrowPasses;
+    for (uint32_t p = 0, done = 0; p < passes; ++p) {
+        uint32_t b = (bits - done + (passes - p) - 1) / (passes - p);
+        b = useWide ? (b < 9 ? 9u : b) : (b < 4 ? 4u : b);
+        if (!pass_fits(ws, useWide, (int)b, useWide ? wgrid : grid, (size_t)1 << b)) return false;
+        done += b;
+    }
+    return true;
+}
+
 int radix_sort_bits(uint32_t* keys[2], uint32_t* vals[2], const uint32_t* nPtr, uint32_t capacity,
-                    uint32_t shift, uint32_t bits, uint32_t* hist, uint32_t* binTotals, hipStream_t s,
+                    uint32_t shift, uint32_t bits, const SortSpace& ws, hipStream_t s,
                     bool ballot, bool wide, bool scanlessOn) {
-    const uint32_t grid = radix_grid_for_capacity(capacity);
+    const uint32_t grid = radix_grid_for_capacity(capacity), wgrid = wide_grid_for_capacity(capacity);
     const uint32_t narrowPasses = (bits + 7) / 8;
     const uint32_t widePasses = (bits + kWideMaxBits - 1) / kWideMaxBits;
     // wide digits where they save a whole pass (32-bit keys: 3 passes of 11/11/10 bits instead of 4)
     const bool useWide = wide && widePasses < narrowPasses;
     const uint32_t passes = useWide ? widePasses : narrowPasses;
     const bool scanless = !useWide && scanlessOn && passes % 2 == 0;
+    // near-equal digit widths; a digit wider than the bits left reads zero bits above the field
+    auto width = [&](uint32_t p, uint32_t done) {
+        const uint32_t b = (bits - done + (passes - p) - 1) / (passes - p);
+        return useWide ? (b < 9 ? 9u : b) : (b < 4 ? 4u : b);
+    };
+    if (!sort_bits_plan_fits(capacity, bits, wide, ws)) return kSortNoSpace;  // the plan fits, or no launch
     int cur = 0;
     uint32_t done = 0;
     for (uint32_t p = 0; p < passes; ++p) {
-        // near-equal digit widths; a digit wider than the bits left reads zero bits above the field
-        uint32_t b = (bits - done + (passes - p) - 1) / (passes - p);
-        if (useWide) {
-            if (b < 9) b = 9;
-            wide_pass(keys[cur], vals[cur], keys[cur ^ 1], vals[cur ^ 1], nPtr, wide_grid_for_capacity(capacity), shift + done, 0u, (int)b, hist,
-                      binTotals, s, ballot, false, nullptr, 0u, 0u);
-        } else {
-            if (b < 4) b = 4;
-            radix_pass(keys[cur], vals[cur], keys[cur ^ 1], vals[cur ^ 1], nPtr, grid, shift + done, (int)b, hist,
-                       binTotals, s, ballot, nullptr, false, scanless ? (int)(p & 1u) : -1);
-        }
+        const uint32_t b = width(p, done);
+        if (useWide)
+            wide_pass(keys[cur], vals[cur], keys[cur ^ 1], vals[cur ^ 1], nPtr, wgrid, shift + done, 0u, (int)b, ws.hist,
+                      ws.binTotals, s, ballot, false, nullptr, 0u, 0u);
+        else
+            radix_pass(keys[cur], vals[cur], keys[cur ^ 1], vals[cur ^ 1], nPtr, grid, shift + done, (int)b, ws.hist,
+                       ws.binTotals, s, ballot, nullptr, false, scanless ? (int)(p & 1u) : -1);
         done += b;
         cur ^= 1;
     }
@@ -1022,9 +898,8 @@ int radix_sort_bits(uint32_t* keys[2], uint32_t* vals[2], const uint32_t* nPtr, 
 // one or two passes).  binTotals holds kSortTotalsWords words: the last pass's digit totals, the
 // first pass's at +256, its bucket starts at +512 (narrow); the wide pass's 2048 totals.
 int radix_sort_tiles(uint32_t* keys[2], uint32_t* vals[2], const uint32_t* nPtr, uint32_t capacity, uint32_t shift,
-                     uint32_t* hist, uint32_t* binTotals, uint32_t* tileStart, uint32_t tileBase, uint32_t numTiles,
-                     uint32_t allTiles, hipStream_t s, bool ballot, int loBits, bool wide, bool wide12,
-                     bool scanlessOn) {
+                     const SortSpace& ws, uint32_t* tileStart, uint32_t tileBase, uint32_t numTiles,
+                     uint32_t allTiles, hipStream_t s, bool ballot, bool wide, bool scanlessOn) {
     const uint32_t grid = radix_grid_for_capacity(capacity);
     auto bitsFor = [](uint32_t tiles) {
         uint32_t b = 1;
@@ -1033,31 +908,36 @@ int radix_sort_tiles(uint32_t* keys[2], uint32_t* vals[2], const uint32_t* nPtr,
     };
     uint32_t bits = bitsFor(allTiles);
     const uint32_t localBits = bitsFor(numTiles);
-    if (wide && bits > 8 && (localBits <= kWideMaxBits || (wide12 && localBits == kWide12Bits))) {
-        wide_pass(keys[0], vals[0], keys[1], vals[1], nPtr, wide_grid_for_capacity(capacity), shift, tileBase, (int)(localBits < 9 ? 9 : localBits),
-                  hist, binTotals, s, ballot, true, tileStart, numTiles, allTiles);
+    if (wide && bits > 8 && localBits <= kWideMaxBits) {
+        const uint32_t wb = localBits < 9 ? 9 : localBits, wgrid = wide_grid_for_capacity(capacity);
+        if (!pass_fits(ws, true, (int)wb, wgrid, (size_t)1 << wb)) return kSortNoSpace;
+        wide_pass(keys[0], vals[0], keys[1], vals[1], nPtr, wgrid, shift, tileBase, (int)wb, ws.hist, ws.binTotals, s,
+                  ballot, true, tileStart, numTiles, allTiles);
         return 1;
     }
     TileStarts ts{};
     ts.numTiles = allTiles;
     ts.tileStart = tileStart;
     if (bits <= 8) {  // one pass, one bucket
-        radix_pass(keys[0], vals[0], keys[1], vals[1], nPtr, grid, shift, (int)(bits < 4 ? 4 : bits), hist,
-                   binTotals, s, ballot, &ts, true);
+        const int b = (int)(bits < 4 ? 4 : bits);
+        if (!pass_fits(ws, false, b, grid, 256)) return kSortNoSpace;
+        radix_pass(keys[0], vals[0], keys[1], vals[1], nPtr, grid, shift, b, ws.hist, ws.binTotals, s, ballot, &ts, true);
         return 1;
     }
-    uint32_t lo = (bits + 1u) / 2u;  // radix_sort_bits' digit widths unless a create-time width is set
-    if (loBits >= 4 && loBits <= 8 && bits - (uint32_t)loBits >= 1u && bits - (uint32_t)loBits <= 8u) lo = (uint32_t)loBits;
+    // radix_sort_bits' digit widths (balanced: 6 + 8 / 8 + 6 at 4K and 5 + 7 / 7 + 5 at 1080p measured slower)
+    const uint32_t lo = (bits + 1u) / 2u;
     const uint32_t hi = bits - lo < 4u ? 4u : bits - lo;  // (a digit wider than the bits left reads zeros)
+    // totals of the last pass at 0, the first pass's at +256, its bucket starts at +512 (<= 256 each)
+    if (!pass_fits(ws, false, (int)lo, grid, 768) || !pass_fits(ws, false, (int)hi, grid, 768)) return kSortNoSpace;
     TileStarts first{};
-    first.bucketStartOut = binTotals + 512;
+    first.bucketStartOut = ws.binTotals + 512;
     const bool scanless = scanlessOn;
-    radix_pass(keys[0], vals[0], keys[1], vals[1], nPtr, grid, shift, (int)lo, hist, binTotals + 256, s, ballot,
+    radix_pass(keys[0], vals[0], keys[1], vals[1], nPtr, grid, shift, (int)lo, ws.hist, ws.binTotals + 256, s, ballot,
                &first, false, scanless ? 0 : -1);
-    ts.bucketStart = binTotals + 512;
+    ts.bucketStart = ws.binTotals + 512;
     ts.lowBits = lo;
-    radix_pass(keys[1], vals[1], keys[0], vals[0], nPtr, grid, shift + lo, (int)hi, hist, binTotals, s, ballot, &ts,
-               true, scanless ? 1 : -1);
+    radix_pass(keys[1], vals[1], keys[0], vals[0], nPtr, grid, shift + lo, (int)hi, ws.hist, ws.binTotals, s, ballot,
+               &ts, true, scanless ? 1 : -1);
     return 0;
 }
 
@@ -1444,20 +1324,12 @@ Tuning tuning_from_env(int device) {
     const char* wv = getenv("GSM_BLEND_WAVES");
     const int w = wv ? atoi(wv) : 0;
     t.blendWaves = (w == 8 || w == 12 || w == 16) ? w : 0;
-    const char* lb = getenv("GSM_SORT_LOBITS");
-    t.tileLoBits = lb ? atoi(lb) : 0;
     const char* cv = getenv("GSM_BLEND_CLAIM");
     t.blendClaim = !cv ? 1 : std::strcmp(cv, "early") == 0 ? 0 : std::strcmp(cv, "auto") == 0 ? 2 : 1;
     const char* ws = getenv("GSM_SORT_WIDE");
     t.wideSort = !(ws && ws[0] == '0');
     const char* sc = getenv("GSM_SORT_SCAN");
     t.sortScanless = !(sc && std::strcmp(sc, "kernel") == 0);
-    const char* mp = getenv("GSM_MG_PIXELS");
-    t.mgPixelsWB = !(mp && std::strcmp(mp, "wt") == 0);
-    const char* mpg = getenv("GSM_MG_PUSH_GRID");
-    t.mgPushPerCU = mpg ? atoi(mpg) : 4;
-    const char* w12 = getenv("GSM_SORT_WIDE12");
-    t.wide12 = w12 && w12[0] == '1';
     const char* bp = getenv("GSM_BLEND_PAIRS");
     t.blendPairs = !(bp && bp[0] == '0');
     const char* ps = getenv("GSM_BLEND_PAIR_SPLIT");

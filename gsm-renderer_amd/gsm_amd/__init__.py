@@ -98,6 +98,8 @@ class BufferId(enum.IntEnum):  # include/gsm_debug.h gsm_buffer_id
 
 
 STAGES = ("project", "scan", "scatter", "sort", "headers", "blend")
+# gsm_blend_kernel (include/gsm_debug.h) -> the kernel's name in rocprofv3 traces
+BLEND_KERNELS = {0: None, 1: "k_blend_px", 2: "k_blend_px", 3: "k_blend_pw"}
 
 
 @dataclass
@@ -205,6 +207,9 @@ _SIGNATURES = {
     "gsm_global_debug_read_total_assignments": ([C.c_void_p], C.c_uint32),
     "gsm_global_last_gpu_time": ([C.c_void_p, C.POINTER(C.c_double)], C.c_int),
     "gsm_global_debug_counters": ([C.c_void_p, C.POINTER(_Counters)], C.c_int),
+    "gsm_global_debug_blend_kernel": ([C.c_void_p, C.POINTER(C.c_int)], C.c_int),
+    "gsm_debug_sort_workspace_bytes": ([C.c_uint32], C.c_size_t),
+    "gsm_debug_sort_plan_fits": ([C.c_uint32, C.c_uint32, C.c_int, C.c_size_t], C.c_int),
     "gsm_global_debug_copy": ([C.c_void_p, C.c_int, C.c_void_p, C.c_size_t, C.POINTER(C.c_size_t)],
                               C.c_int),
     "gsm_global_set_profiling": ([C.c_void_p, C.c_int], C.c_int),
@@ -469,6 +474,12 @@ class GlobalRenderer:
 
     def set_tile_rows(self, begin: int, end: int):
         _check(_lib().gsm_global_set_tile_rows(self._h, int(begin), int(end)), "gsm_global_set_tile_rows")
+
+    def blend_kernel(self) -> str:
+        """The blend kernel the last enqueued frame launched (gsm_global_debug_blend_kernel)."""
+        k = C.c_int(0)
+        _check(_lib().gsm_global_debug_blend_kernel(self._h, C.byref(k)), "gsm_global_debug_blend_kernel")
+        return BLEND_KERNELS[k.value]
 
     def counters(self) -> dict:
         c = _Counters()

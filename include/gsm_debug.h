@@ -46,6 +46,18 @@ typedef enum {
 } gsm_buffer_id;
 
 gsm_status gsm_global_debug_counters(gsm_renderer *renderer, gsm_debug_counters *out);
+
+/* The blend kernel the last enqueued frame launched (host-side choice, no sync): k_blend_px with
+ * 16x8 quadrant units (small frames and multi-GPU slabs), k_blend_px with 16x16 half-tile units, or
+ * the pair walk k_blend_pw (>= 6 half-tile units per wave slot on one GPU).  The benchmark attributes
+ * its blend roofline and PMC counters to this kernel. */
+typedef enum {
+    GSM_BLEND_KERNEL_NONE = 0,
+    GSM_BLEND_KERNEL_QUADRANT = 1,
+    GSM_BLEND_KERNEL_HALF_TILE = 2,
+    GSM_BLEND_KERNEL_PAIR_WALK = 3
+} gsm_blend_kernel;
+gsm_status gsm_global_debug_blend_kernel(gsm_renderer *renderer, int *kind);
 /* Copies up to `bytes` of buffer `which` into host memory; *needed receives the full size. */
 gsm_status gsm_global_debug_copy(gsm_renderer *renderer, int which, void *host_dst, size_t bytes,
                                  size_t *needed);
@@ -88,6 +100,15 @@ gsm_status gsm_sort_pairs_u32(void *keys, void *values, uint32_t n, uint32_t key
  * ballot matches).  GSM_SORT_RANK=ballot in the environment at create forces the ballot ranks.
  * Cached per device and process; no reference counterpart (a gfx950 design choice). */
 gsm_status gsm_debug_sort_rank_probe(int hip_device, int *lane_ordered);
+
+/* The sorts' workspace guard (host only, no device call): the digit-count workspace bytes every
+ * renderer allocates for a sort of `capacity` keys, and whether the passes the LSD sort plans for
+ * `key_bits` bits (wide 9..11-bit digits allowed or not) fit `hist_bytes` of it -- GSM_OK, or
+ * GSM_ERR_INVALID_ASSIGNMENT_CAPACITY, the status a frame whose sort would overrun its workspace
+ * returns before launching any of its passes (an undersized histogram workspace faulted an r05
+ * A/B build). */
+size_t gsm_debug_sort_workspace_bytes(uint32_t capacity);
+gsm_status gsm_debug_sort_plan_fits(uint32_t capacity, uint32_t key_bits, int wide, size_t hist_bytes);
 
 /* The device steps of gsm_multigpu_render (gsm_multigpu.h) without RCCL, so W virtual ranks can run
  * the native exchange in one process on one GPU (tests): the caller plays the collectives --

@@ -112,3 +112,23 @@ def test_null_handle_arguments(gsm):
         gsm.Status.INVALID_ARGUMENT
     assert L.gsm_global_debug_read_total_assignments(None) == 0
     L.gsm_global_destroy(None)
+
+
+@pytest.mark.parametrize("capacity", [1, 4096, 4096 * 1024 + 1, 4_000_000, 20_000_000, 24_000_000])
+def test_sort_workspace_guard(gsm, capacity):
+    """every pass a sort plans is checked against its digit-count workspace before
+    anything launches.  The renderers' own allocation (gsm_debug_sort_workspace_bytes) fits every plan
+    they make -- 32-bit depth keys in 3 wide or 4 narrow passes, the 16-bit tile field in 2 narrow
+    passes, one 9..11-bit wide pass -- and a workspace one word short of the widest pass is refused
+    with GSM_ERR_INVALID_ASSIGNMENT_CAPACITY (host only: no GPU)."""
+    L = gsm._lib()
+    ws = L.gsm_debug_sort_workspace_bytes(capacity)
+    plans = [(32, 1), (32, 0), (16, 0), (12, 0), (11, 1), (9, 1), (8, 0)]
+    for bits, wide in plans:
+        assert L.gsm_debug_sort_plan_fits(capacity, bits, wide, ws) == 0, (bits, wide)
+    # the widest pass of this capacity is the one radix_workspace_bytes was sized for
+    short = [L.gsm_debug_sort_plan_fits(capacity, bits, wide, ws - 4) for bits, wide in plans]
+    assert gsm.Status.INVALID_ASSIGNMENT_CAPACITY in short
+    for bits, wide in plans:
+        assert L.gsm_debug_sort_plan_fits(capacity, bits, wide, 0) == gsm.Status.INVALID_ASSIGNMENT_CAPACITY
+    assert L.gsm_debug_sort_plan_fits(capacity, 0, 0, ws) == gsm.Status.INVALID_ARGUMENT

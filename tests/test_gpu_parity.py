@@ -690,18 +690,16 @@ def test_full_size_config_bit_exact(gsm, cuda, oracle, cfg_name, precision):
     g["renderer"].close()
 
 
-@pytest.mark.parametrize("wide12,rank", [("1", "atomic"), ("1", "ballot"), ("0", "atomic")])
-def test_1080p_tile_field_one_12bit_pass(gsm, cuda, oracle, monkeypatch, wide12, rank):
-    """A 1080p frame's 4080 tiles (a 12-bit tile field): one 12-bit wide radix pass with packed 16-bit
-    digit counters writing the tile starts (GSM_SORT_WIDE12=1, measured slower: DESIGN.md 4;
-    lane-ordered atomic or ballot ranks) or two narrow 6-bit passes (default) -- the same frame as the
-    oracle's, every intermediate bit for bit, first and second frame."""
-    monkeypatch.setenv("GSM_SORT_WIDE12", wide12)
+@pytest.mark.parametrize("rank", ["atomic", "ballot"])
+def test_1080p_tile_field_two_narrow_passes(gsm, cuda, oracle, monkeypatch, rank):
+    """A 1080p frame's 4080 tiles (a 12-bit tile field): two narrow 6-bit passes writing the tile starts
+    (lane-ordered atomic or ballot ranks; the one-pass 12-bit variant measured slower and lives in
+    tools/exp/rejected_variants.patch) -- the same frame as the oracle's, every intermediate bit for bit,
+    first and second frame."""
     monkeypatch.setenv("GSM_SORT_RANK", rank)
     case = _synth(200_000, 1920, 1080, 4, 1, 61)
     r = oracle_render(oracle, case)
     g = gpu_render(gsm, cuda, case)
-    monkeypatch.delenv("GSM_SORT_WIDE12")
     monkeypatch.delenv("GSM_SORT_RANK")
     assert r["tiles_y"] * ((1920 + 31) // 32) == 4080
     assert_frame_equal(g, r)

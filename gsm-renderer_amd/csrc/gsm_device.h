@@ -575,7 +575,9 @@ __device__ __forceinline__ BandSkip band_skip_setup(uint32_t meanW, uint32_t ccW
     const float det = b.cxx * b.cyy - 0.25f * cxy * cxy;
     if (!(det > 0.0f)) return b;
     // det >= (1 - rho^2) cxx cyy > 0.12 cxx cyy: no cancellation worth more than the relative margin
-    b.ex = __builtin_sqrtf(L * b.cyy * __builtin_amdgcn_rcpf(det)) * (1.0f + 1e-5f) + 1e-4f;
+    // hardware square root (v_sqrt_f32, ~1 ulp; r06): inside the 1e-5 relative margin like rsq / rcp above
+    // (the argument is >= L / cxx > 5e-4: never subnormal); the flags only drop entries, the image is the same
+    b.ex = __builtin_amdgcn_sqrtf(L * b.cyy * __builtin_amdgcn_rcpf(det)) * (1.0f + 1e-5f) + 1e-4f;
     b.valid = __builtin_isfinite(b.ex);
     return b;
 }

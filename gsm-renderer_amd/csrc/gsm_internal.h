@@ -168,7 +168,6 @@ __device__ __forceinline__ void st_sys128_at(void* base, uint32_t bytes, uint32_
     __builtin_amdgcn_raw_buffer_store_b128(w, sys_rsrc(base, bytes), (int)off, 0, kSysCoherent);
 }
 
-// Device buffers of one renderer (the GlobalViewResources analogue, GlobalResources.swift:6-362).
 // A sort's device workspace and its sizes.  Every sort below plans its passes first and launches
 // nothing (returns kSortNoSpace) when one pass's per-block digit counts, super-group rows or digit
 // totals would not fit -- a knob or a grid rule changed without the allocation (the r05 wide-pass
@@ -181,6 +180,7 @@ struct SortSpace {
 };
 constexpr int kSortNoSpace = -1;
 
+// Device buffers of one renderer (the GlobalViewResources analogue, GlobalResources.swift:6-362).
 struct DeviceArena {
     GaussianRenderData* renderData = nullptr;  // [maxG]
     short4* bounds = nullptr;                  // [maxG]

@@ -15,7 +15,8 @@
 // Stage attribution of k_project (A/B builds only, tools/gpu_proj_stages.sh): GSM_PROJ_STOP = k ends the
 // projection after stage k (1 loads + view / clip + the early culls, 2 + the 3D covariance, 3 + the 2D
 // covariance and its stabilisation, 4 + theta / sigmas, 5 + the radius / ink / screen culls and the OBB,
-// 6 + the SH colour, 7 the whole projection without the tile tests); the stage's values are folded into
+// 6 + the SH colour, 7 the whole projection without the tile tests, 8 everything but the skip band); the
+// stage's values are folded into
 // the bounds word so nothing is dropped by the compiler, and every later stage (tile tests, records) is
 // skipped.  0 (default): the product kernel.
 #ifndef GSM_PROJ_STOP
@@ -236,6 +237,11 @@ __device__ __forceinline__ RowSet rows_of(const ProjectArgs& P) {
 // row indices [*k0, *k1] of the set inside tile rows [y0, y1] (empty when *k0 > *k1)
 __device__ __forceinline__ void rows_within(const RowSet& R, int y0, int y1, int* k0, int* k1) {
     const int lo = max(y0, R.b), hi = min(y1, R.e - 1);
+    if (R.s == 1) {  // contiguous rows (one GPU, contiguous slabs): no integer divisions (r06)
+        *k0 = lo - R.b;
+        *k1 = hi < R.b ? -1 : hi - R.b;
+        return;
+    }
     *k0 = (lo - R.b + R.s - 1) / R.s;
     *k1 = hi < R.b ? -1 : (hi - R.b) / R.s;
 }
@@ -399,7 +405,11 @@ __global__ __launch_bounds__(kProjectBlock) void k_project(
         const uint32_t mask = sMask[tid];
         ntiles = (uint32_t)__builtin_popcount(mask) + sMore[tid];
         masks[gid] = mask;
+#if GSM_PROJ_STOP == 8  // (attribution: the tile tests without the skip band)
+        const float2 band = make_float2(0.f, -1.f);
+#else
         const float2 band = ntiles ? band_of(o.ra, o.bounds, rows_of(P)) : make_float2(0.f, -1.f);
+#endif
         uint4* rp = (uint4*)(outRec + gid);
         rp[0] = make_uint4(o.ra.x, o.ra.y, o.ra.z, o.ra.w);
         rp[1] = make_uint4(o.rb, __float_as_uint(band.x), __float_as_uint(band.y), 0u);

@@ -40,6 +40,7 @@
 #include <rccl/rccl.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
@@ -57,7 +58,12 @@ struct Rccl {
     decltype(&ncclAllGather) allGather = nullptr;
     decltype(&ncclCommCount) commCount = nullptr;
     decltype(&ncclCommUserRank) userRank = nullptr;
+    decltype(&ncclSend) send = nullptr;  // the RCCL transport's frame (GSM_MG_TRANSPORT_RCCL)
+    decltype(&ncclRecv) recv = nullptr;
+    decltype(&ncclGroupStart) groupStart = nullptr;
+    decltype(&ncclGroupEnd) groupEnd = nullptr;
     bool ok = false;
+    bool p2p = false;
 };
 
 const Rccl& rccl() {
@@ -72,6 +78,11 @@ const Rccl& rccl() {
         R.commCount = (decltype(R.commCount))dlsym(h, "ncclCommCount");
         R.userRank = (decltype(R.userRank))dlsym(h, "ncclCommUserRank");
         R.ok = R.allGather && R.commCount && R.userRank;
+        R.send = (decltype(R.send))dlsym(h, "ncclSend");
+        R.recv = (decltype(R.recv))dlsym(h, "ncclRecv");
+        R.groupStart = (decltype(R.groupStart))dlsym(h, "ncclGroupStart");
+        R.groupEnd = (decltype(R.groupEnd))dlsym(h, "ncclGroupEnd");
+        R.p2p = R.ok && R.send && R.recv && R.groupStart && R.groupEnd;
     });
     return R;
 }
@@ -82,12 +93,15 @@ constexpr size_t kFlagWords = 0;      // u32 flag[kBarriers][kMaxSlabs]: [b][src
 constexpr size_t kStatusWord = 64;    // u32 [0] barrier timeouts, [1] failed peer arrivals, [2] epoch of the last timeout
 constexpr size_t kCountsWord = 256;   // u32 counts[2][kMaxSlabs * kMaxSlabs] (frame parity; row = source)
 constexpr size_t kRecordsOff = 4096;  // SplatRecord[2][capacity] (frame parity)
+constexpr size_t kProbeWord = 768;    // u32 probe[kMaxSlabs]: word src of the connect-time check (MultiGpu::probe)
+constexpr size_t kCtlZeroWords = kProbeWord;  // control words zeroed at prepare (flags, status, counts)
+static_assert(kCountsWord + 2 * kMaxSlabs * kMaxSlabs <= kProbeWord, "counts before the probe words");
 static_assert(kFlagWords + kBarriers * kMaxSlabs <= kStatusWord, "flags before the status word");
 constexpr uint32_t kFailBit = 0x80000000u;  // a flag's epoch with this bit: that rank's frame failed
 constexpr uint32_t kEpochMask = 0x7FFFFFFFu;
 constexpr uint32_t kSyncWaitBlocks = 32;    // workgroups of a wait: >= 4 per XCD (blocks are dealt round robin)
 constexpr uint32_t kHandleMagic = 0x58534D47u;  // "GMSX"
-constexpr uint32_t kHandleVersion = 3;
+constexpr uint32_t kHandleVersion = 4;
 
 struct ExchangeFields {
     uint32_t magic, version;
@@ -101,7 +115,8 @@ struct ExchangeFields {
     uint64_t depthOff;  // rank 0: the gathered r16f depth frame; 0 elsewhere
     uint32_t interleave;  // slab rows interleaved (GSM_MG_ROWS=interleaved): every rank must agree
     uint32_t memKind;     // exchange memory kind (0 fine-grained, 2 device)
-    uint32_t pipelined;   // GSM_MG_PIPELINE=1 (rank 0 holds two gathered frames): every rank must agree
+    uint32_t pipelined;   // options.pipelined (rank 0 holds two gathered frames): every rank must agree
+    uint32_t transport;   // gsm_multigpu_transport: every rank must agree
     char busId[32];
     hipIpcMemHandle_t ipc;
 };
@@ -172,6 +187,50 @@ __global__ __launch_bounds__(64) void k_mg_sync(SyncPeers peers, uint32_t* __res
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
 }
 
+// The control words of a fresh exchange allocation zeroed with system-coherent write-through stores
+// (at prepare, before any peer can hold a handle): no dirty line of a cached memset can linger in an
+// XCD's L2 and be written back over a flag or a count later (r06).
+__global__ __launch_bounds__(256) void k_mg_zero_ctl(uint32_t* __restrict__ mem, uint32_t words) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i < words) __hip_atomic_store(mem + i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// Connect-time check of every mapping this rank stores into or polls (r06): one word
+// per 4 KiB page of each mapping -- page 0: probe word `src` of the control page (no peer writes it), page
+// g > 0: word `src` of the page (records / frames: scratch until the first frame's barrier 0, which needs
+// this rank's arrival) -- stored with the flags' store form (a relaxed system-scope atomic store) or, with
+// `check`, polled with the barrier's load form (ld_sys32) until it holds `value` or `spinTicks` pass (then
+// counted in *fails).  `rot` rotates the item -> workgroup assignment so that each word is read by another
+// workgroup (CU, XCD) than the one that stored it.
+struct ProbeMaps {
+    uint32_t* base[kMaxSlabs];
+    uint32_t pages[kMaxSlabs];
+    uint32_t n;
+};
+__global__ __launch_bounds__(64) void k_mg_probe(ProbeMaps maps, uint32_t total, uint32_t src, uint32_t value,
+                                                 uint32_t rot, int check, uint32_t* __restrict__ fails,
+                                                 unsigned long long spinTicks) {
+    for (uint32_t t = blockIdx.x * 64u + threadIdx.x; t < total; t += gridDim.x * 64u) {
+        uint32_t i = t + rot;
+        if (i >= total) i -= total;
+        uint32_t m = 0;
+        while (m + 1u < maps.n && i >= maps.pages[m]) i -= maps.pages[m++];
+        uint32_t* w = maps.base[m] + (size_t)i * 1024u + (i == 0 ? kProbeWord + src : src);
+        if (!check) {
+            __hip_atomic_store(w, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            continue;
+        }
+        const unsigned long long t0 = wall_clock64();
+        while (ld_sys32(w) != value) {
+            if (wall_clock64() - t0 > spinTicks) {
+                atomicAdd(fails, 1u);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+    }
+}
+
 // rank 0's copy of the gathered frame into the caller's target (rows of `rowBytes`, a multiple of 2):
 // system-coherent loads (the peers stored the frame over xGMI), 4-byte words where aligned
 __global__ __launch_bounds__(256) void k_mg_copy2d(uint8_t* __restrict__ dst, size_t dpitch, const uint8_t* src,
@@ -192,7 +251,8 @@ __global__ __launch_bounds__(256) void k_mg_copy2d(uint8_t* __restrict__ dst, si
 
 class MultiGpu {
    public:
-    static gsm_status prepare(GlobalRenderer* r, int rank, int world, MultiGpu** out, void* handle);
+    static gsm_status prepare(GlobalRenderer* r, int rank, int world, const gsm_multigpu_options& o, MultiGpu** out,
+                              void* handle);
     gsm_status connect(const void* all);
     ~MultiGpu() { release(); }
     gsm_status phase(int p, hipStream_t s, const gsm_gaussian_input& in, const gsm_camera_params& cam, uint32_t width,
@@ -206,6 +266,7 @@ class MultiGpu {
     // pending or in flight): this rank's flag words are set to it, as if every peer had reached it
     gsm_status debugSetEpoch(uint32_t epoch) {
         if (nextPhase_ != 0) return GSM_ERR_PHASE_ORDER;
+        if (!mem_) return GSM_ERR_UNSUPPORTED;  // (no flag words with the RCCL transport)
         epoch &= kEpochMask;
         if (epoch == 0) epoch = 1;
         if (hipSetDevice(device_) != hipSuccess || hipDeviceSynchronize() != hipSuccess) return GSM_ERR_RENDER_FAILED;
@@ -237,6 +298,7 @@ class MultiGpu {
     }
     gsm_status counts(uint32_t* hostCounts);  // world x world, after the frame's stream work
     gsm_status copyExchange(void* dst, size_t bytes) {
+        if (!mem_) return GSM_ERR_UNSUPPORTED;  // (the RCCL transport has no exchange allocation)
         hipSetDevice(device_);
         return hipMemcpy(dst, mem_, bytes < memBytes_ ? bytes : memBytes_, hipMemcpyDeviceToHost) == hipSuccess
                    ? GSM_OK
@@ -272,6 +334,13 @@ class MultiGpu {
     char* depthBuf(uint32_t par) const { return depth0_ ? depth0_ + (pipelined_ ? par * depthStride_ : 0) : nullptr; }
     gsm_status run(int p, hipStream_t s, const gsm_gaussian_input* in, const gsm_camera_params* cam, uint32_t width,
                    uint32_t height, Targets t, size_t colorPitch, void* depth, size_t depthPitch, void* gatherColor);
+    // the same phases over RCCL (GSM_MG_TRANSPORT_RCCL): no exchange memory, no device barrier
+    gsm_status runRccl(int p, hipStream_t s, const gsm_gaussian_input* in, const gsm_camera_params* cam, uint32_t width,
+                       uint32_t height, Targets t, size_t colorPitch, void* depth, size_t depthPitch, void* gatherColor);
+    // connect's check of the mappings (peer-stores transport): GSM_OK or GSM_ERR_DEVICE_NOT_AVAILABLE
+    gsm_status probe(char* const* base, const size_t* bytes);
+    // slab rows [*y0, *y1) of pixel rows of tile-row index k of rank q's slab (contiguous: k = 0 only)
+    bool slabPixelRows(uint32_t q, uint32_t k, uint32_t height, uint32_t* y0, uint32_t* y1) const;
     bool libraryFrame(const void* p) const {
         return p && (p == frame0_ || p == depth0_ || (pipelined_ && (p == frame0_ + frameStride_ || p == depth0_ + depthStride_)));
     }
@@ -314,10 +383,24 @@ class MultiGpu {
     uint32_t par_ = 0;         // the frame's parity, alternating every frame (also across the epoch's wrap)
     int nextPhase_ = 0;        // phases run in order 0..3
     Targets frameT_{};         // phase 0's targets (gathering or not: the barrier steps of finishFrame)
+    uint32_t frameW_ = 0, frameH_ = 0;  // phase 0's frame size (the RCCL transport's gather rows)
     hipEvent_t inputEvent_ = nullptr;  // gsm_multigpu_wait_event (one-shot, the next phase 0)
     gsm_status frameErr_ = GSM_OK;  // this rank's error of the current frame (barrier-only phases after it)
     bool launchFailed_ = false;     // the last run() saw a failed launch (finishFrame's status)
-    bool interleave_ = false;  // slab rows interleaved (GSM_MG_ROWS=interleaved at prepare)
+    bool interleave_ = false;  // slab rows interleaved (options.rows)
+    // GSM_MG_TRANSPORT_RCCL: the communicator, this rank's packed send records (slab after slab), its
+    // receive buffer, the W x W count matrix (device, and pinned host), the records received this frame,
+    // and (ranks != 0, gathering) the full-frame colour / depth targets the slab renders into
+    uint32_t transport_ = GSM_MG_TRANSPORT_PEER_STORES;
+    void* comm_ = nullptr;
+    SplatRecord* sendRec_ = nullptr;
+    SplatRecord* recvRec_ = nullptr;
+    uint64_t sendCap_ = 0;
+    uint32_t* countMat_ = nullptr;
+    uint32_t* hostCounts_ = nullptr;
+    uint32_t recvTotal_ = 0;
+    char* ownFrame_ = nullptr;  // the RCCL transport's frames: rank 0's gathered frame, or a rank's staging
+    char* ownDepth_ = nullptr;
     // Pipelined (GSM_MG_PIPELINE=1 at prepare, every rank alike): phases 0-1 on the library's own stream
     // (front_), phases 2-3 on the caller's, joined by events -- frame f + 1's projection and push run
     // beside frame f's slab render.  front_ starts frame f only after the caller's stream finished frame
@@ -338,8 +421,13 @@ void MultiGpu::release() {
     if (front_) hipStreamSynchronize(front_);
     for (void* p : opened_) hipIpcCloseMemHandle(p);
     opened_.clear();
-    for (void* p : {(void*)mem_, (void*)sendCounts_, (void*)recvCount_, (void*)done_})
+    for (void* p : {(void*)mem_, (void*)sendCounts_, (void*)recvCount_, (void*)done_, (void*)sendRec_, (void*)recvRec_,
+                    (void*)countMat_, (void*)ownFrame_, (void*)ownDepth_})
         if (p) hipFree(p);
+    if (hostCounts_) hipHostFree(hostCounts_);
+    sendRec_ = recvRec_ = nullptr;
+    countMat_ = hostCounts_ = nullptr;
+    ownFrame_ = ownDepth_ = nullptr;
     for (hipEvent_t& e : evFront_)
         if (e) hipEventDestroy(e), e = nullptr;
     for (hipEvent_t& e : evEnd_)
@@ -349,12 +437,19 @@ void MultiGpu::release() {
     sendCounts_ = recvCount_ = done_ = nullptr;
 }
 
-gsm_status MultiGpu::prepare(GlobalRenderer* r, int rank, int world, MultiGpu** out, void* handle) {
+gsm_status MultiGpu::prepare(GlobalRenderer* r, int rank, int world, const gsm_multigpu_options& o, MultiGpu** out,
+                             void* handle) {
     *out = nullptr;
     if (!handle || world < 1 || world > (int)kMaxSlabs || rank < 0 || rank >= world) return GSM_ERR_INVALID_ARGUMENT;
+    if (o.struct_bytes != sizeof(gsm_multigpu_options) || (o.rows != GSM_MG_ROWS_CONTIGUOUS && o.rows != GSM_MG_ROWS_INTERLEAVED) ||
+        (o.transport != GSM_MG_TRANSPORT_PEER_STORES && o.transport != GSM_MG_TRANSPORT_RCCL) || (o.pipelined & ~1))
+        return GSM_ERR_INVALID_ARGUMENT;
+    const bool rcclT = o.transport == GSM_MG_TRANSPORT_RCCL;
+    if (rcclT && (o.pipelined || !o.nccl_comm)) return o.pipelined ? GSM_ERR_UNSUPPORTED : GSM_ERR_INVALID_ARGUMENT;
+    if (rcclT && !rccl().p2p) return GSM_ERR_UNSUPPORTED;
     if (hipSetDevice(r->device()) != hipSuccess) return GSM_ERR_DEVICE_NOT_AVAILABLE;
-    // exchange memory kind (create-time): fine-grained device memory (default) or ordinary
-    // device memory (GSM_MG_MEM=cached, one GPU only)
+    // exchange memory kind: fine-grained device memory; GSM_MG_MEM=cached (ordinary device
+    // memory, one GPU only) is an A/B override of the environment
     const char* mode = getenv("GSM_MG_MEM");
     // uncached exchange memory renders wrong slabs on MI355X: refused; the A/B script
     // (tools/exp/mg_memkind_ab.py) reaches it as "uncached-ab"
@@ -368,38 +463,61 @@ gsm_status MultiGpu::prepare(GlobalRenderer* r, int rank, int world, MultiGpu** 
     m->capacity_ = r->maxGaussians();
     m->bpp_ = r->colorBytesPerPixel();
     m->memKind_ = mode && !strcmp(mode, "cached") ? 2u : (mode && !strcmp(mode, "uncached-ab") ? 1u : 0u);
+    m->transport_ = (uint32_t)o.transport;
+    m->comm_ = o.nccl_comm;
     int khz = 0;
     if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, m->device_) == hipSuccess && khz > 0)
         m->wallKHz_ = (uint32_t)khz;
-    m->timeoutTicks_ = 10000ull * m->wallKHz_;
-    const char* rv = getenv("GSM_MG_ROWS");  // every rank must agree: checked at connect (the handle)
-    m->interleave_ = rv && std::strcmp(rv, "interleaved") == 0;
-    const char* pv = getenv("GSM_MG_PIPELINE");  // every rank must agree: checked at connect (the handle)
-    m->pipelined_ = pv && pv[0] == '1';
-    // two frame parities of the receive buffer (a source pushes frame f + 2 into the parity of frame f
-    // only after its barrier 0 of frame f + 2, which needs this rank's arrival there -- made after this
-    // rank finished reading frame f's records: in stream order, or, pipelined, after evEnd_)
-    const size_t recBytes = 2 * recv_parity_bytes(m->capacity_);
+    m->timeoutTicks_ = (unsigned long long)(o.timeout_ms ? o.timeout_ms : 10000u) * m->wallKHz_;
+    m->interleave_ = o.rows == GSM_MG_ROWS_INTERLEAVED;  // every rank must agree: checked at connect (the handle)
+    m->pipelined_ = o.pipelined != 0;
     m->framePitch_ = align_up((size_t)r->maxWidth() * m->bpp_, 16);
     m->depthPitch0_ = align_up((size_t)r->maxWidth() * 2u, 16);
     m->frameStride_ = align_up(m->framePitch_ * r->maxHeight(), 4096);
     m->depthStride_ = align_up(m->depthPitch0_ * r->maxHeight(), 4096);
-    const size_t nFrames = m->pipelined_ ? 2 : 1;
-    m->frameOff_ = rank == 0 ? align_up(kRecordsOff + recBytes, 4096) : 0;
-    m->depthOff_ = rank == 0 ? m->frameOff_ + nFrames * m->frameStride_ : 0;
-    m->memBytes_ = rank == 0 ? m->depthOff_ + nFrames * m->depthStride_ : kRecordsOff + recBytes;
-    hipError_t ae = m->memKind_ == 2u ? hipMalloc((void**)&m->mem_, m->memBytes_)
-                                      : hipExtMallocWithFlags((void**)&m->mem_, m->memBytes_,
-                                                              m->memKind_ == 1u ? hipDeviceMallocUncached
-                                                                                : hipDeviceMallocFinegrained);
-    // the partition buffers now, so that no frame can fail on an allocation
-    bool ok = ae == hipSuccess && r->ensurePartitionBuffers((uint32_t)world) == GSM_OK &&
-              (!getenv("GSM_MG_POISON") || hipMemset(m->mem_, 0xAB, m->memBytes_) == hipSuccess) &&
-              hipMemset(m->mem_, 0, kRecordsOff) == hipSuccess &&
+    bool ok = r->ensurePartitionBuffers((uint32_t)world) == GSM_OK &&
               hipMalloc(&m->sendCounts_, kMaxSlabs * 4) == hipSuccess && hipMalloc(&m->recvCount_, 8) == hipSuccess &&
               hipMalloc(&m->done_, kBarriers * kArriveWordsPerBarrier * 4) == hipSuccess &&
               hipMemset(m->sendCounts_, 0, kMaxSlabs * 4) == hipSuccess && hipMemset(m->recvCount_, 0, 8) == hipSuccess &&
-              hipMemset(m->done_, 0, kBarriers * kArriveWordsPerBarrier * 4) == hipSuccess && hipDeviceSynchronize() == hipSuccess;
+              hipMemset(m->done_, 0, kBarriers * kArriveWordsPerBarrier * 4) == hipSuccess;
+    if (ok && rcclT) {
+        // RCCL transport: ordinary device memory only -- packed send records (a rank's ceil(N / W) ids, each
+        // in at most W slabs: at most N + W - 1 records), the receive buffer (a slab receives every id at most
+        // once), the count matrix, and full-frame colour / depth targets (rank 0: the gathered frame)
+        m->sendCap_ = (uint64_t)m->capacity_ + kMaxSlabs;
+        ok = hipMalloc((void**)&m->sendRec_, m->sendCap_ * sizeof(SplatRecord)) == hipSuccess &&
+             hipMalloc((void**)&m->recvRec_, ((size_t)m->capacity_ + 1) * sizeof(SplatRecord)) == hipSuccess &&
+             hipMalloc((void**)&m->countMat_, kMaxSlabs * kMaxSlabs * 4) == hipSuccess &&
+             hipHostMalloc((void**)&m->hostCounts_, kMaxSlabs * kMaxSlabs * 4, hipHostMallocDefault) == hipSuccess &&
+             hipMalloc((void**)&m->ownFrame_, m->frameStride_) == hipSuccess &&
+             hipMalloc((void**)&m->ownDepth_, m->depthStride_) == hipSuccess;
+        if (ok) std::memset(m->hostCounts_, 0, kMaxSlabs * kMaxSlabs * 4);
+        if (ok && rank == 0) {
+            m->frame0_ = m->ownFrame_;
+            m->depth0_ = m->ownDepth_;
+        }
+    } else if (ok) {
+        // two frame parities of the receive buffer (a source pushes frame f + 2 into the parity of frame f
+        // only after its barrier 0 of frame f + 2, which needs this rank's arrival there -- made after this
+        // rank finished reading frame f's records: in stream order, or, pipelined, after evEnd_)
+        const size_t recBytes = 2 * recv_parity_bytes(m->capacity_);
+        const size_t nFrames = m->pipelined_ ? 2 : 1;
+        m->frameOff_ = rank == 0 ? align_up(kRecordsOff + recBytes, 4096) : 0;
+        m->depthOff_ = rank == 0 ? m->frameOff_ + nFrames * m->frameStride_ : 0;
+        m->memBytes_ = rank == 0 ? m->depthOff_ + nFrames * m->depthStride_ : kRecordsOff + recBytes;
+        hipError_t ae = m->memKind_ == 2u ? hipMalloc((void**)&m->mem_, m->memBytes_)
+                                          : hipExtMallocWithFlags((void**)&m->mem_, m->memBytes_,
+                                                                  m->memKind_ == 1u ? hipDeviceMallocUncached
+                                                                                    : hipDeviceMallocFinegrained);
+        ok = ae == hipSuccess && (!getenv("GSM_MG_POISON") || hipMemset(m->mem_, 0xAB, m->memBytes_) == hipSuccess) &&
+             hipDeviceSynchronize() == hipSuccess;
+        if (ok) {  // the control words: write-through zeros, not a cached memset (k_mg_zero_ctl)
+            hipLaunchKernelGGL(k_mg_zero_ctl, dim3((kCtlZeroWords + 255) / 256), dim3(256), 0, 0, (uint32_t*)m->mem_,
+                               (uint32_t)kCtlZeroWords);
+            ok = hipGetLastError() == hipSuccess;
+        }
+    }
+    if (ok) ok = hipDeviceSynchronize() == hipSuccess;
     if (ok && m->pipelined_)
         ok = hipStreamCreateWithFlags(&m->front_, hipStreamNonBlocking) == hipSuccess &&
              hipEventCreateWithFlags(&m->evFront_[0], hipEventDisableTiming) == hipSuccess &&
@@ -408,7 +526,7 @@ gsm_status MultiGpu::prepare(GlobalRenderer* r, int rank, int world, MultiGpu** 
              hipEventCreateWithFlags(&m->evEnd_[1], hipEventDisableTiming) == hipSuccess;
     ExchangeHandle h;
     std::memset(&h, 0, sizeof(h));
-    if (ok) ok = hipIpcGetMemHandle(&h.ipc, m->mem_) == hipSuccess;
+    if (ok && !rcclT) ok = hipIpcGetMemHandle(&h.ipc, m->mem_) == hipSuccess;
     if (ok) ok = hipDeviceGetPCIBusId(h.busId, (int)sizeof(h.busId) - 1, m->device_) == hipSuccess;
     if (!ok) {
         (void)hipGetLastError();
@@ -432,6 +550,7 @@ gsm_status MultiGpu::prepare(GlobalRenderer* r, int rank, int world, MultiGpu** 
     h.interleave = m->interleave_ ? 1u : 0u;
     h.memKind = m->memKind_;
     h.pipelined = m->pipelined_ ? 1u : 0u;
+    h.transport = m->transport_;
     std::memcpy(handle, &h, sizeof(h));
     *out = m;
     return GSM_OK;
@@ -444,22 +563,30 @@ gsm_status MultiGpu::connect(const void* all) {
     std::vector<ExchangeHandle> hs((size_t)world_);
     std::memcpy(hs.data(), all, sizeof(ExchangeHandle) * (size_t)world_);
     uint32_t minCap = 0xFFFFFFFFu;
+    const bool rcclT = transport_ == GSM_MG_TRANSPORT_RCCL;
     for (int p = 0; p < world_; ++p) {
         const ExchangeHandle& h = hs[(size_t)p];
-        // the ranks agree on the world, the frame limits and the row layout (a rank with another
-        // GSM_MG_ROWS would send records with the wrong slab masks: refused here)
+        // the ranks agree on the world, the frame limits and the options (a rank with another row layout
+        // would send records with the wrong slab masks: refused here)
         if (h.magic != kHandleMagic || h.version != kHandleVersion || h.rank != p || h.world != world_ ||
             h.maxWidth != r_->maxWidth() || h.maxHeight != r_->maxHeight() || h.bytesPerPixel != bpp_ ||
-            h.interleave != (interleave_ ? 1u : 0u) || h.pipelined != (pipelined_ ? 1u : 0u))
+            h.interleave != (interleave_ ? 1u : 0u) || h.pipelined != (pipelined_ ? 1u : 0u) || h.transport != transport_)
             return GSM_ERR_INVALID_ARGUMENT;
-        if (p == 0 && (h.frameOff == 0 || h.depthOff == 0)) return GSM_ERR_INVALID_ARGUMENT;
+        if (!rcclT && p == 0 && (h.frameOff == 0 || h.depthOff == 0)) return GSM_ERR_INVALID_ARGUMENT;
         if (h.capacity < minCap) minCap = h.capacity;
     }
     if (hs[(size_t)rank_].base != (uint64_t)(uintptr_t)mem_) return GSM_ERR_INVALID_ARGUMENT;  // not our handle
+    if (rcclT) {  // no mappings: every frame's data moves through the communicator
+        minCap_ = minCap;
+        connected_ = true;
+        return GSM_OK;
+    }
     const int32_t pid = (int32_t)getpid();
     char* base[kMaxSlabs] = {};
+    size_t bytes[kMaxSlabs] = {};
     for (int p = 0; p < world_; ++p) {
         const ExchangeHandle& h = hs[(size_t)p];
+        bytes[p] = h.bytes;
         if (p == rank_) {
             base[p] = mem_;
         } else if (h.pid == pid) {  // a rank of this process (virtual ranks): the pointer itself
@@ -486,11 +613,67 @@ gsm_status MultiGpu::connect(const void* all) {
         recs_.recv[p] = (SplatRecord*)(base[p] + kRecordsOff);
         recs_.cap[p] = h.capacity;
     }
+    // every mapping this rank will store into or poll, checked before the first frame relies on it
+    const gsm_status pst = probe(base, bytes);
+    if (pst != GSM_OK) return pst;
     frame0_ = base[0] + hs[0].frameOff;
     depth0_ = base[0] + hs[0].depthOff;
     minCap_ = minCap;
     connected_ = true;
     return GSM_OK;
+}
+
+// Connect-time check of the mappings (r06).  r05's diagnosis: the first frame
+// whose exchange allocation reused the address range of a freed *uncached* allocation lost flag stores
+// (every wait of that frame timed out) or read wrong record words, while counts and records stored into the
+// same pages were right and every later frame was clean -- state of the old mapping served the first
+// accesses of the new one.  Before the first frame, this rank makes exactly those accesses: one word per 4
+// KiB page of every mapping (own and peers', this rank's own word of each page), twice -- stored with the
+// flags' store form by one set of workgroups, polled with the barrier's load form by another (each word read
+// on another CU / XCD than the one that stored it, a bounded spin of 50 ms), and the control page's word
+// compared through the host -- so the frame's first stores and polls no longer meet that state, and a
+// mapping that still does not show a stored word refuses the connect (GSM_ERR_DEVICE_NOT_AVAILABLE) instead
+// of a frame timing out.
+gsm_status MultiGpu::probe(char* const* base, const size_t* bytes) {
+    ProbeMaps maps{};
+    uint32_t total = 0;
+    for (int p = 0; p < world_; ++p) {
+        maps.base[p] = (uint32_t*)base[p];
+        maps.pages[p] = (uint32_t)((bytes[p] + 4095) / 4096);
+        total += maps.pages[p];
+    }
+    maps.n = (uint32_t)world_;
+    uint32_t* fails = nullptr;
+    hipStream_t s = nullptr;
+    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess || hipMalloc(&fails, 4) != hipSuccess ||
+        hipMemsetAsync(fails, 0, 4, s) != hipSuccess) {
+        if (fails) hipFree(fails);
+        if (s) hipStreamDestroy(s);
+        (void)hipGetLastError();
+        return GSM_ERR_FAILED_TO_ALLOCATE_BUFFER;
+    }
+    const uint32_t grid = std::min<uint32_t>(2048u, (total + 63u) / 64u);
+    const unsigned long long spin = 50ull * wallKHz_;
+    bool ok = true;
+    for (uint32_t round = 0; round < 2 && ok; ++round) {
+        const uint32_t value = 0x5EED0000u | ((uint32_t)rank_ << 8) | (round + 1u);
+        const uint32_t rotStore = round * (total / 3u), rotCheck = rotStore + total / 2u + 64u;
+        hipLaunchKernelGGL(k_mg_probe, dim3(grid), dim3(64), 0, s, maps, total, (uint32_t)rank_, value,
+                           rotStore % total, 0, fails, spin);
+        hipLaunchKernelGGL(k_mg_probe, dim3(grid), dim3(64), 0, s, maps, total, (uint32_t)rank_, value,
+                           rotCheck % total, 1, fails, spin);
+        uint32_t nf = 1;
+        ok = hipMemcpyAsync(&nf, fails, 4, hipMemcpyDeviceToHost, s) == hipSuccess && hipStreamSynchronize(s) == hipSuccess &&
+             nf == 0;
+        for (int p = 0; ok && p < world_; ++p) {  // the control page's word through the host's own path
+            uint32_t w = 0;
+            ok = hipMemcpy(&w, maps.base[p] + kProbeWord + rank_, 4, hipMemcpyDeviceToHost) == hipSuccess && w == value;
+        }
+    }
+    hipFree(fails);
+    hipStreamDestroy(s);
+    if (hipGetLastError() != hipSuccess) ok = false;
+    return ok ? GSM_OK : GSM_ERR_DEVICE_NOT_AVAILABLE;
 }
 
 // Everything any phase of this rank's frame could refuse, before anything is enqueued.
@@ -506,9 +689,12 @@ gsm_status MultiGpu::check(const gsm_gaussian_input& in, uint32_t width, uint32_
         return GSM_ERR_INVALID_DIMENSIONS;
     if (in.gaussian_count > 0 && (!in.gaussians || !in.harmonics)) return GSM_ERR_MISSING_REQUIRED_BUFFER;
     if (t->gather) {
-        t->color = frame0_;
+        // the slab render's targets: rank 0's gathered frame (peer stores: every rank's blend writes into it
+        // through the mapping; RCCL: each rank renders into its own frame, sent to rank 0 in phase 3)
+        const bool rcclT = transport_ == GSM_MG_TRANSPORT_RCCL;
+        t->color = rcclT ? ownFrame_ : frame0_;
         t->colorPitch = framePitch_;
-        t->depth = t->gatherDepth ? (void*)depth0_ : nullptr;
+        t->depth = t->gatherDepth ? (void*)(rcclT ? ownDepth_ : depth0_) : nullptr;
         t->depthPitch = depthPitch0_;
         if (rank_ == 0) {  // the copies of phase 3 into the caller's targets
             // pipelined: the library frames alternate and a peer may be writing the other one
@@ -549,6 +735,12 @@ gsm_status MultiGpu::phase(int p, hipStream_t s, const gsm_gaussian_input& in, c
     } else if (frameErr_ == GSM_OK) {
         frameErr_ = cst;  // (the same arguments as phase 0's for a caller that follows the protocol)
     }
+    if (p == 0) {
+        frameW_ = width;
+        frameH_ = height;
+    }
+    if (transport_ == GSM_MG_TRANSPORT_RCCL)
+        return runRccl(p, s, &in, &cam, width, height, t, colorPitch, depth, depthPitch, gatherColor);
     return run(p, s, &in, &cam, width, height, t, colorPitch, depth, depthPitch, gatherColor);
 }
 
@@ -565,7 +757,9 @@ gsm_status MultiGpu::finishFrame(hipStream_t s) {
         // (phase 1's push status, or a launch that failed in any phase: ADVICE r05), not the abandonment.
         if (p >= 2 && frameErr_ == GSM_OK) frameErr_ = GSM_ERR_RENDER_FAILED;
         launchFailed_ = false;
-        const gsm_status st = run(p, s, nullptr, nullptr, 0, 0, frameT_, 0, nullptr, 0, nullptr);
+        const gsm_status st = transport_ == GSM_MG_TRANSPORT_RCCL
+                                  ? runRccl(p, s, nullptr, nullptr, frameW_, frameH_, frameT_, 0, nullptr, 0, nullptr)
+                                  : run(p, s, nullptr, nullptr, 0, 0, frameT_, 0, nullptr, 0, nullptr);
         if (first == GSM_OK && (launchFailed_ || p == 1)) first = launchFailed_ ? GSM_ERR_RENDER_FAILED : st;
     }
     return first;
@@ -695,6 +889,11 @@ gsm_status MultiGpu::run(int p, hipStream_t s, const gsm_gaussian_input* in, con
 }
 
 gsm_status MultiGpu::status(uint32_t* timeouts, uint32_t* peerErrors, bool clear) {
+    if (!mem_) {  // the RCCL transport has no device barrier: nothing times out
+        if (timeouts) *timeouts = 0;
+        if (peerErrors) *peerErrors = 0;
+        return GSM_OK;
+    }
     hipSetDevice(device_);
     uint32_t w[2] = {0, 0};
     if (hipMemcpy(w, ctl() + kStatusWord, 8, hipMemcpyDeviceToHost) != hipSuccess) return GSM_ERR_RENDER_FAILED;
@@ -704,7 +903,166 @@ gsm_status MultiGpu::status(uint32_t* timeouts, uint32_t* peerErrors, bool clear
     return GSM_OK;
 }
 
+bool MultiGpu::slabPixelRows(uint32_t q, uint32_t k, uint32_t height, uint32_t* y0, uint32_t* y1) const {
+    const uint32_t tilesY = r_->tilesY(), W = (uint32_t)world_;
+    uint32_t t0, t1;
+    if (interleave_) {  // tile row q + k W
+        t0 = q + k * W;
+        t1 = t0 + 1u;
+    } else {  // rows [q p, (q + 1) p) in one piece
+        if (k > 0) return false;
+        const uint32_t per = (tilesY + W - 1u) / W;
+        t0 = std::min(q * per, tilesY);
+        t1 = std::min(t0 + per, tilesY);
+    }
+    if (t0 >= tilesY || t0 >= t1) return false;
+    *y0 = std::min(t0 * 16u, height);
+    *y1 = std::min(t1 * 16u, height);
+    return *y1 > *y0;
+}
+
+// The frame over RCCL (GSM_MG_TRANSPORT_RCCL; SURVEY.md 8e's exchange): the same
+// projection and per-slab runs as the peer-stores frame, moved by the communicator instead of the producing
+// kernels' peer stores.  Every rank performs every collective of every phase -- a refused frame with zero
+// counts -- so the ranks' collectives always match.
+//   0  projection of the rank's ids, runs packed slab after slab into sendRec_ (k_part_copy), the per-slab
+//      counts into sendCounts_ (gsm_global_project_partition's path);
+//   1  ncclAllGather of the count rows -> the W x W matrix, copied to the host (the frame's one host
+//      synchronisation), then one group of ncclSend / ncclRecv: slab q's records to rank q, rank q's records
+//      for this slab into recvRec_ at the offset of the ranks before q (source-rank order = ascending id,
+//      the stable sort's tie order); this rank's own records by a device copy;
+//   2  the slab render from the received records (count known on the host), into rank 0's gathered frame
+//      (rank 0), this rank's staging frame (gathering) or the caller's targets;
+//   3  gathering: one group of sends of every slab's pixel rows (colour, and depth when gathered) to rank 0,
+//      which receives them in place; then rank 0's copy into the caller's targets.
+gsm_status MultiGpu::runRccl(int p, hipStream_t s, const gsm_gaussian_input* in, const gsm_camera_params* cam,
+                             uint32_t width, uint32_t height, Targets t, size_t colorPitch, void* depth,
+                             size_t depthPitch, void* gatherColor) {
+    nextPhase_ = (p + 1) & 3;
+    const Rccl& R = rccl();
+    const ncclComm_t comm = (ncclComm_t)comm_;
+    const uint32_t world = (uint32_t)world_, rank = (uint32_t)rank_;
+    const uint32_t tilesY = r_->tilesY();
+    const uint32_t perRows = (tilesY + world - 1) / world;
+    uint32_t rows[kMaxSlabs + 1];
+    for (uint32_t i = 0; i <= world; ++i)
+        rows[i] = interleave_ ? (i < world ? (i < tilesY ? i : tilesY) : tilesY) : (i * perRows < tilesY ? i * perRows : tilesY);
+    const bool mine = interleave_ ? rank < tilesY : rows[rank] < rows[rank + 1];
+    auto setRows = [&]() {
+        return interleave_ ? r_->setTileRows(rank, tilesY, world) : r_->setTileRows(rows[rank], rows[rank + 1]);
+    };
+    // the slab render's targets: rank 0's gathered frame, this rank's staging frame, or the caller's
+    char* const colorT = t.gather ? ownFrame_ : (char*)t.color;
+    char* const depthT = t.gather ? (t.gatherDepth ? ownDepth_ : nullptr) : (char*)t.depth;
+    const size_t colorP = t.gather ? framePitch_ : t.colorPitch, depthP = t.gather ? depthPitch0_ : t.depthPitch;
+    gsm_status st = GSM_OK;
+    bool collOk = true;
+    switch (p) {
+        case 0: {
+            if (frameErr_ == GSM_OK) {
+                const uint32_t N = in->gaussian_count;
+                const uint32_t perIds = (N + world - 1) / world;
+                const uint32_t first = rank * perIds < N ? rank * perIds : N;
+                const uint32_t cnt = perIds < N - first ? perIds : N - first;
+                r_->selectSchedule(0);
+                if ((st = r_->projectPartition(s, *in, *cam, width, height, first, cnt, rows, world, sendRec_, sendCap_,
+                                               sendCounts_, interleave_)) != GSM_OK)
+                    frameErr_ = st;  // (refused before any launch)
+            }
+            if (frameErr_ != GSM_OK) hipMemsetAsync(sendCounts_, 0, world * sizeof(uint32_t), s);
+            break;
+        }
+        case 1: {
+            collOk = R.allGather(sendCounts_, countMat_, world, ncclUint32, comm, s) == ncclSuccess &&
+                     hipMemcpyAsync(hostCounts_, countMat_, (size_t)world * world * 4, hipMemcpyDeviceToHost, s) == hipSuccess &&
+                     hipStreamSynchronize(s) == hipSuccess;
+            if (!collOk) break;
+            // (recvTotal <= N <= the smallest capacity: a slab receives every id at most once)
+            uint64_t sendOff = 0, recvOff = 0;
+            uint32_t recvTotal = 0;
+            for (uint32_t q = 0; q < world; ++q) recvTotal += hostCounts_[q * world + rank];
+            // this rank's own records first (a device copy), then one group for every peer
+            for (uint32_t q = 0; q < rank; ++q) sendOff += hostCounts_[rank * world + q];
+            for (uint32_t q = 0; q < rank; ++q) recvOff += hostCounts_[q * world + rank];
+            const uint32_t self = hostCounts_[rank * world + rank];
+            if (self)
+                hipMemcpyAsync(recvRec_ + recvOff, sendRec_ + sendOff, (size_t)self * sizeof(SplatRecord),
+                               hipMemcpyDeviceToDevice, s);
+            collOk = R.groupStart() == ncclSuccess;
+            sendOff = recvOff = 0;
+            for (uint32_t q = 0; q < world && collOk; ++q) {
+                const uint32_t ns = hostCounts_[rank * world + q], nr = hostCounts_[q * world + rank];
+                if (q != rank) {
+                    if (ns) collOk = R.send(sendRec_ + sendOff, (size_t)ns * sizeof(SplatRecord), ncclUint8, (int)q, comm, s) == ncclSuccess;
+                    if (nr && collOk)
+                        collOk = R.recv(recvRec_ + recvOff, (size_t)nr * sizeof(SplatRecord), ncclUint8, (int)q, comm, s) ==
+                                 ncclSuccess;
+                }
+                sendOff += ns;
+                recvOff += nr;
+            }
+            if (R.groupEnd() != ncclSuccess) collOk = false;
+            recvTotal_ = recvTotal;
+            break;
+        }
+        case 2: {
+            if (frameErr_ == GSM_OK && mine) {
+                if ((st = setRows()) == GSM_OK) {
+                    r_->selectSchedule(0);
+                    st = r_->renderRecords(s, recvRec_, recvTotal_, width, height, colorT, colorP, depthT, depthP);
+                }
+                if (st != GSM_OK) frameErr_ = st;
+            }
+            break;
+        }
+        case 3: {
+            if (t.gather && world > 1) {  // every slab's pixel rows to rank 0 (sent even by a failed rank)
+                collOk = R.groupStart() == ncclSuccess;
+                for (uint32_t q = 1; q < world && collOk; ++q) {
+                    if (rank != 0 && rank != q) continue;
+                    uint32_t y0, y1;
+                    for (uint32_t k = 0; collOk && slabPixelRows(q, k, height, &y0, &y1); ++k) {
+                        const size_t cOff = (size_t)y0 * framePitch_, cBytes = (size_t)(y1 - y0) * framePitch_;
+                        const size_t dOff = (size_t)y0 * depthPitch0_, dBytes = (size_t)(y1 - y0) * depthPitch0_;
+                        if (rank == 0) {
+                            collOk = R.recv(ownFrame_ + cOff, cBytes, ncclUint8, (int)q, comm, s) == ncclSuccess &&
+                                     (!t.gatherDepth || R.recv(ownDepth_ + dOff, dBytes, ncclUint8, (int)q, comm, s) == ncclSuccess);
+                        } else {
+                            collOk = R.send(ownFrame_ + cOff, cBytes, ncclUint8, 0, comm, s) == ncclSuccess &&
+                                     (!t.gatherDepth || R.send(ownDepth_ + dOff, dBytes, ncclUint8, 0, comm, s) == ncclSuccess);
+                        }
+                    }
+                }
+                if (R.groupEnd() != ncclSuccess) collOk = false;
+            }
+            if (t.gather && rank == 0 && frameErr_ == GSM_OK && gatherColor) {  // the caller's targets
+                const size_t rowBytes = (size_t)width * bpp_;
+                if (gatherColor != ownFrame_)
+                    hipMemcpy2DAsync(gatherColor, colorPitch, ownFrame_, framePitch_, rowBytes, height, hipMemcpyDeviceToDevice, s);
+                if (t.gatherDepth && depth && depth != ownDepth_)
+                    hipMemcpy2DAsync(depth, depthPitch, ownDepth_, depthPitch0_, (size_t)width * 2u, height,
+                                     hipMemcpyDeviceToDevice, s);
+            }
+            break;
+        }
+    }
+    if (!collOk) {
+        if (frameErr_ == GSM_OK) frameErr_ = GSM_ERR_RENDER_FAILED;
+        launchFailed_ = true;
+        return GSM_ERR_RENDER_FAILED;
+    }
+    if (hipGetLastError() != hipSuccess) {
+        launchFailed_ = true;
+        return GSM_ERR_RENDER_FAILED;
+    }
+    return frameErr_;
+}
+
 gsm_status MultiGpu::counts(uint32_t* hostCounts) {
+    if (transport_ == GSM_MG_TRANSPORT_RCCL) {  // (the last frame's matrix, copied to the host in its phase 1)
+        std::memcpy(hostCounts, hostCounts_, (size_t)world_ * world_ * 4);
+        return GSM_OK;
+    }
     hipSetDevice(device_);
     const uint32_t* c = ctl() + kCountsWord + par_ * kMaxSlabs * kMaxSlabs;
     if (hipMemcpy(hostCounts, c, (size_t)world_ * world_ * 4, hipMemcpyDeviceToHost) != hipSuccess)
@@ -720,12 +1078,33 @@ struct gsm_multigpu {
 
 extern "C" {
 
-gsm_status gsm_multigpu_prepare(gsm_renderer* renderer, int rank, int world_size, gsm_multigpu** out, void* handle) {
+void gsm_multigpu_default_options(gsm_multigpu_options* o) {
+    if (!o) return;
+    std::memset(o, 0, sizeof(*o));
+    o->struct_bytes = sizeof(gsm_multigpu_options);
+    o->rows = GSM_MG_ROWS_CONTIGUOUS;
+    o->transport = GSM_MG_TRANSPORT_PEER_STORES;
+    o->timeout_ms = 10000;
+}
+
+// the options of the entry points without them: the defaults with the environment's test overrides
+static gsm_multigpu_options env_options() {
+    gsm_multigpu_options o;
+    gsm_multigpu_default_options(&o);
+    const char* rv = getenv("GSM_MG_ROWS");
+    if (rv && std::strcmp(rv, "interleaved") == 0) o.rows = GSM_MG_ROWS_INTERLEAVED;
+    const char* pv = getenv("GSM_MG_PIPELINE");
+    if (pv && pv[0] == '1') o.pipelined = 1;
+    return o;
+}
+
+gsm_status gsm_multigpu_prepare_with_options(gsm_renderer* renderer, int rank, int world_size,
+                                             const gsm_multigpu_options* options, gsm_multigpu** out, void* handle) {
     if (!out) return GSM_ERR_INVALID_ARGUMENT;
     *out = nullptr;
-    if (!renderer || !renderer->impl) return GSM_ERR_INVALID_ARGUMENT;
+    if (!renderer || !renderer->impl || !options) return GSM_ERR_INVALID_ARGUMENT;
     gsm::MultiGpu* m = nullptr;
-    gsm_status st = gsm::MultiGpu::prepare(renderer->impl, rank, world_size, &m, handle);
+    gsm_status st = gsm::MultiGpu::prepare(renderer->impl, rank, world_size, *options, &m, handle);
     if (st != GSM_OK) return st;
     gsm_multigpu* h = new (std::nothrow) gsm_multigpu{m};
     if (!h) {
@@ -736,16 +1115,21 @@ gsm_status gsm_multigpu_prepare(gsm_renderer* renderer, int rank, int world_size
     return GSM_OK;
 }
 
+gsm_status gsm_multigpu_prepare(gsm_renderer* renderer, int rank, int world_size, gsm_multigpu** out, void* handle) {
+    const gsm_multigpu_options o = env_options();
+    return gsm_multigpu_prepare_with_options(renderer, rank, world_size, &o, out, handle);
+}
+
 gsm_status gsm_multigpu_connect(gsm_multigpu* m, const void* all_handles) {
     if (!m || !m->impl) return GSM_ERR_INVALID_ARGUMENT;
     return m->impl->connect(all_handles);
 }
 
-gsm_status gsm_multigpu_create(gsm_renderer* renderer, void* nccl_comm, int rank, int world_size,
-                               gsm_multigpu** out) {
+gsm_status gsm_multigpu_create_with_options(gsm_renderer* renderer, void* nccl_comm, int rank, int world_size,
+                                            const gsm_multigpu_options* options, gsm_multigpu** out) {
     if (!out) return GSM_ERR_INVALID_ARGUMENT;
     *out = nullptr;
-    if (!renderer || !renderer->impl) return GSM_ERR_INVALID_ARGUMENT;
+    if (!renderer || !renderer->impl || !options) return GSM_ERR_INVALID_ARGUMENT;
     const gsm::Rccl& R = gsm::rccl();
     if (!R.ok) return GSM_ERR_UNSUPPORTED;
     if (!nccl_comm || world_size < 1 || world_size > (int)gsm::kMaxSlabs || rank < 0 || rank >= world_size)
@@ -754,11 +1138,15 @@ gsm_status gsm_multigpu_create(gsm_renderer* renderer, void* nccl_comm, int rank
     if (R.commCount((ncclComm_t)nccl_comm, &n) != ncclSuccess || R.userRank((ncclComm_t)nccl_comm, &me) != ncclSuccess ||
         n != world_size || me != rank)
         return GSM_ERR_INVALID_ARGUMENT;
+    gsm_multigpu_options o = *options;
+    if (o.struct_bytes != sizeof(gsm_multigpu_options)) return GSM_ERR_INVALID_ARGUMENT;
+    if (o.transport == GSM_MG_TRANSPORT_RCCL) o.nccl_comm = nccl_comm;  // the frames' collectives run on it
     std::vector<uint8_t> all((size_t)world_size * GSM_MULTIGPU_HANDLE_BYTES);
     gsm_multigpu* h = nullptr;
-    gsm_status st = gsm_multigpu_prepare(renderer, rank, world_size, &h, all.data() + (size_t)rank * GSM_MULTIGPU_HANDLE_BYTES);
+    gsm_status st = gsm_multigpu_prepare_with_options(renderer, rank, world_size, &o, &h,
+                                                      all.data() + (size_t)rank * GSM_MULTIGPU_HANDLE_BYTES);
     if (st != GSM_OK) return st;
-    // the handles over the communicator (once, at set-up; the frame itself uses no collective)
+    // the handles over the communicator (once, at set-up; the peer-stores frame itself uses no collective)
     uint8_t* d = nullptr;
     hipStream_t s = nullptr;
     bool ok = hipStreamCreate(&s) == hipSuccess && hipMalloc(&d, all.size()) == hipSuccess &&
@@ -781,6 +1169,12 @@ gsm_status gsm_multigpu_create(gsm_renderer* renderer, void* nccl_comm, int rank
     }
     *out = h;
     return GSM_OK;
+}
+
+gsm_status gsm_multigpu_create(gsm_renderer* renderer, void* nccl_comm, int rank, int world_size,
+                               gsm_multigpu** out) {
+    const gsm_multigpu_options o = env_options();
+    return gsm_multigpu_create_with_options(renderer, nccl_comm, rank, world_size, &o, out);
 }
 
 void gsm_multigpu_destroy(gsm_multigpu* m) {

@@ -348,10 +348,10 @@ gsm_status GlobalRenderer::projectPartition(hipStream_t s, const gsm_gaussian_in
                                             const gsm_camera_params& camp, uint32_t width, uint32_t height,
                                             uint32_t first, uint32_t count, const uint32_t* slabRows,
                                             uint32_t numSlabs, void* send, uint64_t capacity,
-                                            uint32_t* sendCounts) {
+                                            uint32_t* sendCounts, bool interleave) {
     PartitionFrame f;
     gsm_status st = preparePartition(in, camp, width, height, first, count, slabRows, numSlabs, true, send,
-                                     sendCounts, &f);
+                                     sendCounts, &f, interleave);
     if (st != GSM_OK) return st;
     launch_partition(f.half, f.deg, f.world, f.harm, f.a, f.slabs, part_, arena_.sincosTable, send, capacity,
                      sendCounts, s);

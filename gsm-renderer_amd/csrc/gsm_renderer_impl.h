@@ -27,7 +27,7 @@ class GlobalRenderer {
     gsm_status projectPartition(hipStream_t stream, const gsm_gaussian_input& input,
                                 const gsm_camera_params& camera, uint32_t width, uint32_t height,
                                 uint32_t first, uint32_t count, const uint32_t* slabRows, uint32_t numSlabs,
-                                void* send, uint64_t capacity, uint32_t* sendCounts);
+                                void* send, uint64_t capacity, uint32_t* sendCounts, bool interleave = false);
     // the same projection for the direct exchange: per-slab counts first, then the records written
     // into every slab owner's receive buffer once the count matrix is on the device (gsm_multigpu.hip)
     // orderUnits: the launch also orders the blend units of the renderer's own rows (set_tile_rows) for a

@@ -245,6 +245,12 @@ _SIGNATURES = {
                                                C.c_uint32, C.c_uint32, C.c_void_p, C.c_size_t, C.c_void_p,
                                                C.c_size_t], C.c_int),
     "gsm_multigpu_create": ([C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_void_p)], C.c_int),
+    # (options structs passed as pointers: _MgOptions, gsm_multigpu_options)
+    "gsm_multigpu_default_options": ([C.c_void_p], None),
+    "gsm_multigpu_prepare_with_options": ([C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.POINTER(C.c_void_p),
+                                           C.c_void_p], C.c_int),
+    "gsm_multigpu_create_with_options": ([C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_void_p,
+                                          C.POINTER(C.c_void_p)], C.c_int),
     "gsm_multigpu_destroy": ([C.c_void_p], None),
     "gsm_multigpu_render": ([C.c_void_p, C.c_void_p, C.POINTER(_Input), C.POINTER(_Camera), C.c_uint32,
                              C.c_uint32, C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t, C.c_void_p], C.c_int),
@@ -631,6 +637,37 @@ def sort_pairs_u32(keys, values, key_bits: int = 32, stream=None):
            "gsm_sort_pairs_u32")
 
 
+class _MgOptions(C.Structure):
+    _fields_ = [("struct_bytes", C.c_uint32), ("rows", C.c_int32), ("pipelined", C.c_int32),
+                ("transport", C.c_int32), ("timeout_ms", C.c_uint32), ("reserved", C.c_uint32),
+                ("nccl_comm", C.c_void_p)]
+
+
+MG_ROWS = {"contiguous": 0, "interleaved": 1}
+MG_TRANSPORT = {"peer_stores": 0, "rccl": 1}
+
+
+@dataclass
+class MultiGpuOptions:
+    """gsm_multigpu_options (include/gsm_multigpu.h): row layout, pipelining, transport, barrier
+    timeout, and the RCCL transport's communicator (ncclComm_t as an int)."""
+    rows: str = "contiguous"
+    pipelined: bool = False
+    transport: str = "peer_stores"
+    timeout_ms: int = 10000
+    nccl_comm: Optional[int] = None
+
+    def _c(self) -> "_MgOptions":
+        o = _MgOptions()
+        _lib().gsm_multigpu_default_options(C.byref(o))
+        o.rows = MG_ROWS[self.rows]
+        o.pipelined = 1 if self.pipelined else 0
+        o.transport = MG_TRANSPORT[self.transport]
+        o.timeout_ms = int(self.timeout_ms)
+        o.nccl_comm = C.c_void_p(int(self.nccl_comm)) if self.nccl_comm else None
+        return o
+
+
 class MultiGpuRenderer:
     """gsm_multigpu_* (include/gsm_multigpu.h): one frame of a GlobalRenderer split by tile-row slab
     across the ranks of a node -- counts, records and slab pixels written straight into the owners'
@@ -645,7 +682,10 @@ class MultiGpuRenderer:
                                                           allgather(bytes) -> list of every rank's
                                                           bytes (e.g. torch.distributed over gloo)."""
 
-    def __init__(self, renderer: "GlobalRenderer", comm: Optional[int], rank: int, world_size: int, _handle=None):
+    def __init__(self, renderer: "GlobalRenderer", comm: Optional[int], rank: int, world_size: int, _handle=None,
+                 options: Optional["MultiGpuOptions"] = None):
+        """options None: gsm_multigpu_create (defaults + the environment's test overrides); otherwise
+        gsm_multigpu_create_with_options."""
         self.renderer = renderer
         self.rank = int(rank)
         self.world_size = int(world_size)
@@ -653,17 +693,30 @@ class MultiGpuRenderer:
             self._h = _handle
             return
         h = C.c_void_p()
-        _check(_lib().gsm_multigpu_create(renderer._h, C.c_void_p(int(comm)), int(rank), int(world_size), C.byref(h)),
-               "gsm_multigpu_create")
+        if options is None:
+            _check(_lib().gsm_multigpu_create(renderer._h, C.c_void_p(int(comm)), int(rank), int(world_size),
+                                              C.byref(h)), "gsm_multigpu_create")
+        else:
+            o = options._c()
+            _check(_lib().gsm_multigpu_create_with_options(renderer._h, C.c_void_p(int(comm)), int(rank),
+                                                           int(world_size), C.byref(o), C.byref(h)),
+                   "gsm_multigpu_create_with_options")
         self._h = h
 
     @classmethod
-    def prepare(cls, renderer: "GlobalRenderer", rank: int, world_size: int):
-        """gsm_multigpu_prepare: (unconnected renderer, this rank's handle bytes)."""
+    def prepare(cls, renderer: "GlobalRenderer", rank: int, world_size: int,
+                options: Optional["MultiGpuOptions"] = None):
+        """gsm_multigpu_prepare (options None) or gsm_multigpu_prepare_with_options: (unconnected
+        renderer, this rank's handle bytes)."""
         h = C.c_void_p()
         buf = C.create_string_buffer(MULTIGPU_HANDLE_BYTES)
-        _check(_lib().gsm_multigpu_prepare(renderer._h, int(rank), int(world_size), C.byref(h), buf),
-               "gsm_multigpu_prepare")
+        if options is None:
+            _check(_lib().gsm_multigpu_prepare(renderer._h, int(rank), int(world_size), C.byref(h), buf),
+                   "gsm_multigpu_prepare")
+        else:
+            o = options._c()
+            _check(_lib().gsm_multigpu_prepare_with_options(renderer._h, int(rank), int(world_size), C.byref(o),
+                                                            C.byref(h), buf), "gsm_multigpu_prepare_with_options")
         return cls(renderer, None, rank, world_size, _handle=h), bytes(buf.raw)
 
     def connect_handles(self, handles):
@@ -675,8 +728,9 @@ class MultiGpuRenderer:
         return self
 
     @classmethod
-    def connect(cls, renderer: "GlobalRenderer", rank: int, world_size: int, allgather):
-        mg, mine = cls.prepare(renderer, rank, world_size)
+    def connect(cls, renderer: "GlobalRenderer", rank: int, world_size: int, allgather,
+                options: Optional["MultiGpuOptions"] = None):
+        mg, mine = cls.prepare(renderer, rank, world_size, options)
         try:
             return mg.connect_handles(allgather(mine))
         except Exception:

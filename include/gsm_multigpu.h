@@ -84,8 +84,16 @@ gsm_status gsm_global_render_records(gsm_renderer *renderer, void *stream, const
  *   (caller)               all-gathers the handles: all[r * GSM_MULTIGPU_HANDLE_BYTES] = rank r's;
  *   gsm_multigpu_connect   opens every peer's exchange memory (hipIpcOpenMemHandle; a handle
  *                          from the same process is used directly) and checks that the ranks
- *                          agree on the world, the frame limits and the row layout
- *                          (GSM_MG_ROWS): GSM_ERR_INVALID_ARGUMENT otherwise.
+ *                          agree on the world, the frame limits and the options (row layout,
+ *                          pipelining, transport): GSM_ERR_INVALID_ARGUMENT otherwise.  It then
+ *                          checks every mapping it will store into or poll (own and peers'): one
+ *                          word per 4 KiB page written with the frame's system-coherent store form
+ *                          from workgroups spread over every XCD, read back with the barrier's poll
+ *                          form from other workgroups and through the host, twice with different
+ *                          values, and finally re-zeroes the control words with write-through stores
+ *                          (never a cached memset) -- GSM_ERR_DEVICE_NOT_AVAILABLE when a word was
+ *                          not seen (r06: a range last mapped uncached by any library of the process
+ *                          and reused lost flag stores in r05).
  * The frame capacity is the smallest max_gaussians of all ranks (a slab receives every id at
  * most once): a frame with more gaussians returns GSM_ERR_INVALID_GAUSSIAN_COUNT on every rank
  * alike, before anything is enqueued.
@@ -95,8 +103,49 @@ gsm_status gsm_global_render_records(gsm_renderer *renderer, void *stream, const
  * GSM_ERR_INVALID_ARGUMENT when rank / world_size do not match the communicator or
  * world_size > GSM_MAX_SLABS. */
 typedef struct gsm_multigpu gsm_multigpu;
+
+/* Per-renderer choices of the partitioned frame (r06), every rank alike (checked at
+ * connect; GSM_ERR_INVALID_ARGUMENT otherwise).  gsm_multigpu_default_options fills the defaults; the
+ * entry points without options use them, with the environment variables GSM_MG_ROWS=interleaved and
+ * GSM_MG_PIPELINE=1 applied on top as test overrides (explicit options ignore the environment). */
+typedef enum {
+    GSM_MG_ROWS_CONTIGUOUS = 0,  /* rank r owns tile rows [r ceil(tiles_y / W), +ceil(tiles_y / W)): each
+                                    record travels to the fewest ranks (faster on centred content) */
+    GSM_MG_ROWS_INTERLEAVED = 1  /* rank r owns rows r, r + W, ...: balanced on off-centre content
+                                    (the heaviest contiguous rank can sort 2.8x the mean) */
+} gsm_multigpu_rows;
+typedef enum {
+    GSM_MG_TRANSPORT_PEER_STORES = 0, /* the producing kernels store counts, records and pixels straight
+                                         into the peers' fine-grained exchange memory (IPC mappings) and
+                                         meet at device flag barriers: no collective, no host sync */
+    GSM_MG_TRANSPORT_RCCL = 1         /* the same per-slab runs moved by RCCL over `nccl_comm`: the count
+                                         rows all-gathered and copied to the host once per frame, the
+                                         records by grouped ncclSend / ncclRecv into each owner's receive
+                                         buffer at the count matrix's offsets (source-rank order), the
+                                         slab rows of colour and depth by grouped send / recv to rank 0.
+                                         No IPC and no device barrier: for nodes where peer mappings
+                                         cannot be opened (SURVEY.md 8e's all-to-all) */
+} gsm_multigpu_transport;
+typedef struct {
+    uint32_t struct_bytes; /* sizeof(gsm_multigpu_options): set by gsm_multigpu_default_options */
+    int32_t rows;          /* gsm_multigpu_rows */
+    int32_t pipelined;     /* 1: phases 0-1 on a stream of the library's own, overlapping the previous
+                              frame's slab render (peer-stores transport only; GSM_ERR_UNSUPPORTED with
+                              RCCL) -- rank 0 then holds two alternating gathered frames */
+    int32_t transport;     /* gsm_multigpu_transport */
+    uint32_t timeout_ms;   /* device barrier timeout (peer stores), 0 = 10000 */
+    uint32_t reserved;
+    void *nccl_comm;       /* transport RCCL: the ncclComm_t the frames run their collectives on
+                              (gsm_multigpu_create_with_options: its own argument) */
+} gsm_multigpu_options;
+void gsm_multigpu_default_options(gsm_multigpu_options *options);
 gsm_status gsm_multigpu_prepare(gsm_renderer *renderer, int rank, int world_size, gsm_multigpu **out,
                                 void *handle);
+gsm_status gsm_multigpu_prepare_with_options(gsm_renderer *renderer, int rank, int world_size,
+                                             const gsm_multigpu_options *options, gsm_multigpu **out,
+                                             void *handle);
+gsm_status gsm_multigpu_create_with_options(gsm_renderer *renderer, void *nccl_comm, int rank, int world_size,
+                                            const gsm_multigpu_options *options, gsm_multigpu **out);
 gsm_status gsm_multigpu_connect(gsm_multigpu *multigpu, const void *all_handles);
 gsm_status gsm_multigpu_create(gsm_renderer *renderer, void *nccl_comm, int rank, int world_size,
                                gsm_multigpu **out);

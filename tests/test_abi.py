@@ -65,6 +65,25 @@ def test_struct_sizes_match_headers(gsm, tmp_path):
                      C.sizeof(gsm._Counters)]
 
 
+def test_multigpu_options_layout_and_defaults(gsm, tmp_path):
+    """gsm_multigpu_options (include/gsm_multigpu.h, r06): the C struct and the ctypes mirror agree, and
+    gsm_multigpu_default_options (host only) fills the defaults the mirror relies on."""
+    prog = tmp_path / "mgo.c"
+    prog.write_text('#include "gsm_multigpu.h"\n#include <stdio.h>\n#include <stddef.h>\n'
+                    'int main(void){printf("%zu %zu %zu\\n", sizeof(gsm_multigpu_options),'
+                    ' offsetof(gsm_multigpu_options, timeout_ms), offsetof(gsm_multigpu_options, nccl_comm));return 0;}\n')
+    exe = tmp_path / "mgo"
+    subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(prog), "-o", str(exe)], check=True)
+    sizes = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()]
+    assert sizes == [C.sizeof(gsm._MgOptions), gsm._MgOptions.timeout_ms.offset, gsm._MgOptions.nccl_comm.offset]
+    o = gsm._MgOptions()
+    gsm._lib().gsm_multigpu_default_options(C.byref(o))
+    assert (o.struct_bytes, o.rows, o.pipelined, o.transport, o.timeout_ms) == (C.sizeof(o), 0, 0, 0, 10000)
+    assert not o.nccl_comm
+    c = gsm.MultiGpuOptions(rows="interleaved", transport="rccl", timeout_ms=5)._c()
+    assert (c.rows, c.transport, c.timeout_ms) == (1, 1, 5)
+
+
 def test_status_strings_and_defaults(gsm):
     L = gsm._lib()
     assert L.gsm_abi_version() == 1

@@ -130,7 +130,7 @@ def test_processes_refuse_a_frame_over_the_smallest_capacity(tmp_path):
     assert all(s["refused"] for s in st)
 
 
-def _virtual_frame(gsm, cuda, world, n, w, h, sh, prec, seed, cams):
+def _virtual_frame(gsm, cuda, world, n, w, h, sh, prec, seed, cams, options=None):
     from gsm_amd import scenes
     world_np, harm_np, cam_d = scenes.gen_scene(n, w, h, sh, prec, seed=seed)
     wt = cuda.from_numpy(world_np.view(np.uint8).reshape(-1).copy()).cuda()
@@ -139,7 +139,7 @@ def _virtual_frame(gsm, cuda, world, n, w, h, sh, prec, seed, cams):
     inp = gsm.GaussianInput(wt, ht, n, sh)
     cfg = gsm.RendererConfig(max_gaussians=n, max_width=w, max_height=h, precision=prec, gaussian_color_space=0)
     rends = [gsm.GlobalRenderer(device=0, config=cfg) for _ in range(world)]
-    pre = [gsm.MultiGpuRenderer.prepare(r, k, world) for k, r in enumerate(rends)]
+    pre = [gsm.MultiGpuRenderer.prepare(r, k, world, options) for k, r in enumerate(rends)]
     handles = [hd for _, hd in pre]
     mgs = [m.connect_handles(handles) for m, _ in pre]
     frame_ptr, _ = mgs[0].frame()
@@ -170,15 +170,16 @@ def _virtual_frame(gsm, cuda, world, n, w, h, sh, prec, seed, cams):
                                                    (3, 60_000, 1280, 720, 1, "interleaved"),
                                                    (8, 50_000, 640, 360, 0, "interleaved"),
                                                    (16, 30_000, 640, 360, 1, "interleaved")])
-def test_virtual_ranks_product_path(gsm, cuda, oracle, monkeypatch, world, n, w, h, prec, rows):
+def test_virtual_ranks_product_path(gsm, cuda, oracle, world, n, w, h, prec, rows):
     """W ranks of one process through the product kernels (barriers, pushes, gather into rank 0's
     frame), two cameras: the second frame reuses the parity-double-buffered count matrix.  Rows in
-    contiguous blocks (the default) or interleaved over the ranks (GSM_MG_ROWS=interleaved)."""
+    contiguous blocks (the default) or interleaved over the ranks, chosen through the C ABI's
+    gsm_multigpu_options (r06; the environment's GSM_MG_ROWS is only a test override)."""
     from gsm_amd import scenes
-    monkeypatch.setenv("GSM_MG_ROWS", rows)
     sh = 16 if prec else 4
     cams = [scenes.make_camera(w, h), scenes.orbit_camera(w, h, 5.0)]
-    frames, counts, timeouts, depths = _virtual_frame(gsm, cuda, world, n, w, h, sh, prec, 78, cams)
+    opts = gsm.MultiGpuOptions(rows=rows, timeout_ms=20000)
+    frames, counts, timeouts, depths = _virtual_frame(gsm, cuda, world, n, w, h, sh, prec, 78, cams, opts)
     assert timeouts == [0] * world
     world_np, harm_np, _ = scenes.gen_scene(n, w, h, sh, prec, seed=78)
     for i, (got, gd, cam) in enumerate(zip(frames, depths, cams)):
@@ -218,14 +219,13 @@ def test_uncached_exchange_memory_is_refused(gsm, cuda, monkeypatch):
 
 
 @pytest.mark.parametrize("world,n,w,h,prec", [(3, 60_000, 1280, 720, 1), (8, 50_000, 640, 360, 0)])
-def test_virtual_ranks_pipelined(gsm, cuda, oracle, monkeypatch, world, n, w, h, prec):
-    """GSM_MG_PIPELINE=1: every rank runs phases 0-1 on the library's own stream and phases 2-3 on
+def test_virtual_ranks_pipelined(gsm, cuda, oracle, world, n, w, h, prec):
+    """options.pipelined (gsm_multigpu_options, r06): every rank runs phases 0-1 on the library's own stream and phases 2-3 on
     the caller's, so frame f + 1's projection and push overlap frame f's slab render; four frames
     (three views) are issued back to back with no host synchronisation, each gathered into its own
     caller tensors, and every frame's colour and depth are bit-exact with the oracle (the receive
     buffers, receive counts, blend schedules and rank 0's gathered frames alternate by frame parity)."""
     from gsm_amd import scenes
-    monkeypatch.setenv("GSM_MG_PIPELINE", "1")
     sh = 16 if prec else 4
     world_np, harm_np, cam0 = scenes.gen_scene(n, w, h, sh, prec, seed=91)
     cams = [cam0, scenes.orbit_camera(w, h, 5.0), scenes.orbit_camera(w, h, 10.0), cam0]
@@ -234,7 +234,8 @@ def test_virtual_ranks_pipelined(gsm, cuda, oracle, monkeypatch, world, n, w, h,
     inp = gsm.GaussianInput(wt, ht, n, sh)
     cfg = gsm.RendererConfig(max_gaussians=n, max_width=w, max_height=h, precision=prec, gaussian_color_space=0)
     rends = [gsm.GlobalRenderer(device=0, config=cfg) for _ in range(world)]
-    pre = [gsm.MultiGpuRenderer.prepare(r, k, world) for k, r in enumerate(rends)]
+    opts = gsm.MultiGpuOptions(pipelined=True)
+    pre = [gsm.MultiGpuRenderer.prepare(r, k, world, opts) for k, r in enumerate(rends)]
     mgs = [m.connect_handles([hd for _, hd in pre]) for m, _ in pre]
     stream = cuda.cuda.current_stream()
     colors = [cuda.full((h, w, 4), float("nan"), dtype=cuda.float16, device="cuda") for _ in cams]
@@ -395,3 +396,57 @@ def test_virtual_ranks_epoch_wrap(gsm, cuda, oracle, monkeypatch, pipelined):
         m.close()
     for r in rends:
         r.close()
+
+
+def test_options_must_agree_across_ranks(gsm, cuda):
+    """gsm_multigpu_options are checked at connect like the old environment switches: ranks prepared
+    with another row layout, pipelining or transport refuse the connect (GSM_ERR_INVALID_ARGUMENT); a
+    malformed options struct (unknown row layout) is refused at prepare; the RCCL transport without a
+    communicator is refused at prepare, and pipelined RCCL is unsupported."""
+    cfg = gsm.RendererConfig(max_gaussians=4096, max_width=256, max_height=128)
+    rends = [gsm.GlobalRenderer(device=0, config=cfg) for _ in range(2)]
+    for other in (gsm.MultiGpuOptions(rows="interleaved"), gsm.MultiGpuOptions(pipelined=True)):
+        a, ha = gsm.MultiGpuRenderer.prepare(rends[0], 0, 2, gsm.MultiGpuOptions())
+        b, hb = gsm.MultiGpuRenderer.prepare(rends[1], 1, 2, other)
+        for m in (a, b):
+            with pytest.raises(gsm.RendererError) as e:
+                m.connect_handles([ha, hb])
+            assert e.value.status == gsm.Status.INVALID_ARGUMENT
+            m.close()
+    bad = gsm.MultiGpuOptions()
+    bad.rows = "interleaved"
+    o = bad._c()
+    o.rows = 7
+    import ctypes as C
+    h = C.c_void_p()
+    buf = C.create_string_buffer(gsm.MULTIGPU_HANDLE_BYTES)
+    st = gsm._lib().gsm_multigpu_prepare_with_options(rends[0]._h, 0, 2, C.byref(o), C.byref(h), buf)
+    assert st == gsm.Status.INVALID_ARGUMENT
+    with pytest.raises(gsm.RendererError) as e:
+        gsm.MultiGpuRenderer.prepare(rends[0], 0, 1, gsm.MultiGpuOptions(transport="rccl"))
+    assert e.value.status == gsm.Status.INVALID_ARGUMENT
+    with pytest.raises(gsm.RendererError) as e:
+        gsm.MultiGpuRenderer.prepare(rends[0], 0, 1, gsm.MultiGpuOptions(transport="rccl", pipelined=True, nccl_comm=1))
+    assert e.value.status == gsm.Status.UNSUPPORTED
+    for r in rends:
+        r.close()
+
+
+def test_fine_exchange_after_freed_uncached_allocations(tmp_path):
+    """r05's barrier timeouts came from the first frame of a fine-grained exchange whose
+    allocations reused the address ranges of freed *uncached* ones.  A child process (tests/mg_uc_reuse.py)
+    replays that sequence twice -- virtual-rank frames over uncached exchange memory (the A/B kind) plus raw
+    uncached allocations of the same sizes, all freed, then a fine-grained exchange of the same shape -- and
+    the fine-grained exchange must either render both frames bit-exact with zero barrier timeouts, or refuse
+    at connect (the mapping check, GSM_ERR_DEVICE_NOT_AVAILABLE).  The barrier timeout is 2 s, so a lost flag
+    costs seconds, not a hang."""
+    out = tmp_path / "uc.json"
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    env.pop("GSM_MG_MEM", None)
+    r = subprocess.run([sys.executable, os.path.join(os.path.dirname(__file__), "mg_uc_reuse.py"), str(out)], env=env,
+                       capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    res = json.loads(out.read_text())
+    assert res["cases"], res
+    for c in res["cases"]:
+        assert c["refused"] or (c["timeouts"] == 0 and c["bad_rows"] == [0, 0]), c

@@ -118,3 +118,37 @@ def test_native_exchange_virtual_ranks(gsm, cuda, oracle, world, n, w, h, prec):
     assert np.array_equal(depth.view(cuda.int16).cpu().numpy().view(np.uint16), ref["depth"])
     for rend in ranks:
         rend.close()
+
+
+@pytest.mark.parametrize("rows,gather", [("contiguous", True), ("interleaved", True), ("contiguous", False)])
+def test_world1_rccl_transport_frame(gsm, cuda, oracle, nccl_world1, rows, gather):
+    """GSM_MG_TRANSPORT_RCCL (gsm_multigpu_options, r06): the same per-slab runs moved by
+    RCCL inside the library -- count rows all-gathered and read on the host, the records by grouped
+    ncclSend / ncclRecv (a device copy for the rank's own slab), the slab pixels by send / recv to rank 0 --
+    over a world-1 communicator from torch.distributed.  Two frames, gathered into the caller's tensors (or
+    rendered into them directly), equal the oracle bit for bit, and the counts the frame read are the
+    single-GPU frame's."""
+    from gsm_amd import scenes
+    n, w, h, sh, prec = 60_000, 640, 360, 16, 1
+    world, harm, cam = scenes.gen_scene(n, w, h, sh, prec, seed=5)
+    wt = cuda.from_numpy(world.view(np.uint8).reshape(-1).copy()).cuda()
+    ht = cuda.from_numpy(harm.view(np.uint8).reshape(-1).copy()).cuda()
+    inp = gsm.GaussianInput(wt, ht, n, sh)
+    cams = [cam, scenes.orbit_camera(w, h, 5.0)]
+    cfg = gsm.RendererConfig(max_gaussians=n, max_width=w, max_height=h, precision=prec, gaussian_color_space=0)
+    rend = gsm.GlobalRenderer(device=0, config=cfg)
+    opts = gsm.MultiGpuOptions(rows=rows, transport="rccl")
+    mg = gsm.MultiGpuRenderer(rend, gsm.MultiGpuRenderer.torch_comm(0), 0, 1, options=opts)
+    for c in cams:
+        color = cuda.full((h, w, 4), float("nan"), dtype=cuda.float16, device="cuda")
+        depth = cuda.full((h, w), float("nan"), dtype=cuda.float16, device="cuda")
+        mg.render(color, depth, inp, gsm.CameraParams.from_dict(c), w, h, gather=gather)
+        cuda.cuda.synchronize()
+        ref = oracle.render(world, harm, sh, c, w, h, max_gaussians=n)
+        assert np.array_equal(color.view(cuda.int16).cpu().numpy().view(np.uint16), ref["color"])
+        assert np.array_equal(depth.view(cuda.int16).cpu().numpy().view(np.uint16), ref["depth"])
+        counts = mg.counts()
+        assert counts.shape == (1, 1) and int(np.count_nonzero(ref["tile_counts"])) <= counts[0, 0] <= n
+    assert mg.status() == 0
+    mg.close()
+    rend.close()

@@ -4,7 +4,7 @@
 set -eu
 cd "$(dirname "$0")/../gsm-renderer_amd"
 make -s -j8
-for k in ${STOPS:-1 2 3 4 5 6 7}; do
+for k in ${STOPS:-1 2 3 4 5 6 7 8}; do
   rm -rf build_ps$k lib_ps$k; mkdir -p build_ps$k
   cp -p build/*.o build_ps$k/; rm build_ps$k/gsm_kernels.o
   make -s BUILD=build_ps$k LIB=lib_ps$k EXTRA=-DGSM_PROJ_STOP=$k &

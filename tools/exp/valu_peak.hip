@@ -40,7 +40,7 @@ __global__ void k_peak(unsigned* out, unsigned long long* clk) {
     if (OP == 8) asm volatile("v_pk_fma_f32 %0, %0, %1, %2" : "+v"(p##i) : "v"(pm), "v"(pc));               \
     if (OP == 9) asm volatile("v_add_f16 %0, %0, %1" : "+v"(a##i) : "v"(m));                                 \
     if (OP == 10) asm volatile("v_perm_b32 %0, %0, %1, %2" : "+v"(a##i) : "v"(m), "v"(c));                   \
-    if (OP == 11) asm volatile("v_cndmask_b32 %0, %0, %1, vcc" : "+v"(a##i) : "v"(m));                       \
+    if (OP == 11) asm volatile("v_cndmask_b32 %0, %0, %1, vcc" : "+v"(a##i) : "v"(m));  /* VCC never written */ \
     if (OP == 12) asm volatile("v_mov_b32_dpp %0, %0 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf" : "+v"(a##i)); \
     if (OP == 13) asm volatile("v_cvt_f32_f16 %0, %0" : "+v"(a##i));                                          \
     if (OP == 14) asm volatile("v_exp_f32 %0, %0" : "+v"(a##i));                                              \
@@ -53,7 +53,14 @@ __global__ void k_peak(unsigned* out, unsigned long long* clk) {
     if (OP == 21) asm volatile("v_fma_mix_f32 %0, %0, %1, %2 op_sel_hi:[0,1,0]" : "+v"(a##i) : "v"(m), "v"(c)); \
     if (OP == 22) asm volatile("v_cvt_f16_f32 %0, %0" : "+v"(a##i));                                          \
     if (OP == 23) asm volatile("v_cndmask_b32 %0, %0, %1, s[0:1]" : "+v"(a##i) : "v"(m) : "s0", "s1");        \
-    if (OP == 24) asm volatile("v_cmp_gt_f32 s[0:1], %0, %1" : : "v"(a##i), "v"(m) : "s0", "s1");
+    if (OP == 24) asm volatile("v_cmp_gt_f32 s[0:1], %0, %1" : : "v"(a##i), "v"(m) : "s0", "s1");             \
+    if (OP == 25) asm volatile("v_cndmask_b32_e64 %0, %0, %1, vcc" : "+v"(a##i) : "v"(m));                   \
+    if (OP == 26) asm volatile("v_cmp_gt_f32_e32 vcc, %0, %1\n v_cndmask_b32_e32 %0, %0, %1, vcc" : "+v"(a##i) : "v"(m) : "vcc"); \
+    if (OP == 27) asm volatile("v_cmp_gt_f32_e64 s[" #i "*2+16:" #i "*2+17], %0, %1\n v_cndmask_b32_e64 %0, %0, %1, s[" #i "*2+16:" #i "*2+17]" \
+                               : "+v"(a##i) : "v"(m) : "s16", "s17", "s18", "s19", "s20", "s21", "s22", "s23", "s24", "s25", "s26", "s27", "s28", "s29", "s30", "s31"); \
+    if (OP == 28) asm volatile("v_sub_f32 %0, %0, %1\n v_cndmask_b32_e64 %0, %0, %1, s[0:1]" : "+v"(a##i) : "v"(m) : "s0", "s1"); \
+    if (OP == 29) asm volatile("v_cmp_class_f32_e64 s[" #i "*2+16:" #i "*2+17], %0, %1" : : "v"(a##i), "v"(m) \
+                               : "s16", "s17", "s18", "s19", "s20", "s21", "s22", "s23", "s24", "s25", "s26", "s27", "s28", "s29", "s30", "s31");
             REP8(ACC)
 #undef ACC
         }
@@ -69,7 +76,7 @@ __global__ void k_peak(unsigned* out, unsigned long long* clk) {
 }
 
 template <int OP>
-static void run(const char* name, int cus, unsigned* out, unsigned long long* clk) {
+static void run(const char* name, int cus, unsigned* out, unsigned long long* clk, int perAcc = 1) {
     for (int wps = 1; wps <= 8; wps *= 2) {
         // waves per CU = 4 * wps, in workgroups of at most 1024 threads
         const int threads = 64 * 4 * wps;
@@ -97,7 +104,7 @@ static void run(const char* name, int cus, unsigned* out, unsigned long long* cl
             hipEventDestroy(a);
             hipEventDestroy(b);
         }
-        const double waveInstr = (double)grid.x * (block / 64) * ITERS * 16.0;
+        const double waveInstr = (double)grid.x * (block / 64) * ITERS * 16.0 * perAcc;
         const double perNs = waveInstr / (best * 1e6);
         const double simds = cus * 4.0;
         // cycles per wave-instruction per SIMD at the in-kernel clock
@@ -141,5 +148,10 @@ int main() {
     run<22>("v_cvt_f16_f32", cus, out, clk);
     run<23>("v_cndmask_b32_sgpr", cus, out, clk);
     run<24>("v_cmp_gt_f32", cus, out, clk);
+    run<25>("v_cndmask_e64_vcc", cus, out, clk);
+    run<26>("cmp_e32+cndmask_vcc", cus, out, clk, 2);
+    run<27>("cmp_e64+cndmask_sN", cus, out, clk, 2);
+    run<28>("sub+cndmask_s01", cus, out, clk, 2);
+    run<29>("v_cmp_class_e64", cus, out, clk);
     return 0;
 }

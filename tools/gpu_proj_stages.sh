@@ -1,11 +1,14 @@
 #!/bin/bash
 # Stage attribution of k_project: kernel traces of the GSM_PROJ_STOP builds
 # (gsm-renderer_amd/lib_ps<k>, tools/build_proj_stages.sh) at configs 2 and 3, one PMC pass per build at
-# config 2, and the VALU issue probe (tools/exp/valu_peak).  Output: gpurun_out/ps/.
+# config 2, and the VALU issue probe (tools/exp/valu_peak).  Output: gpurun_out/ps/.  SCHED=0 runs every
+# build with GSM_BLEND_SCHED=0: no blend-schedule workgroup in the projection launch (block 0, which
+# otherwise sets a floor under the truncated builds' duration).
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-OUT=gpurun_out/ps
+[ "${SCHED:-1}" = 0 ] && export GSM_BLEND_SCHED=0
+OUT=gpurun_out/${OUTDIR:-ps}
 mkdir -p $OUT
 LIBDIR=gsm-renderer_amd/lib
 cp $LIBDIR/libgsm_amd.so /tmp/libgsm_amd_A.so
@@ -15,7 +18,7 @@ if [ "${PEAK:-1}" = 1 ]; then
   echo "valu_peak done"
 fi
 BENCH="bench.py --steps 20 --warmup 3 --cpu-baseline 0 --parity 0 --orbit-steps 0 --inflight-steps 0 --virtual-ranks 0"
-for v in A ${VARIANTS:-ps1 ps2 ps3 ps4 ps5 ps6 ps7}; do
+for v in A ${VARIANTS:-ps1 ps2 ps3 ps4 ps5 ps6 ps7 ps8}; do
   use $v
   for cfg in ${CFGS:-cfg2_1m_sh3_1080p_f16 cfg3_5m_sh3_4k_f16}; do
     c=${cfg%%_*}

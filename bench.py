@@ -13,8 +13,9 @@ N>1 (torch.distributed.run, one rank per GPU), --multi:
       are stored into every rank's count matrix by the scan kernel, each 48-byte record is written
       straight into its slab owner's receive buffer over xGMI, every rank renders its band of tile
       rows into rank 0's frame, ordered by device-side flag barriers the producing kernels arrive
-      at themselves; if any rank cannot create that frame, every rank falls back to
-      the RCCL all-to-all of gsm_amd.exchange ("multi_fallback" in the line);
+      at themselves; if any rank cannot create that frame, every rank takes the
+      library's RCCL transport (grouped send / recv of the same runs, "multi_transport": "rccl"),
+      and only without an NCCL backend the torch all-to-all of gsm_amd.exchange ("multi_fallback");
   replicas: every rank projects all gaussians and keeps its band's assignments.
 Either way the bands are gathered on rank 0 inside the timed step.  The frame is fixed as N
 grows -> "scaling": "strong".  The line also carries "config4": BASELINE configs[3], the 4K
@@ -260,30 +261,19 @@ def main():
     # blends, device flag barriers -- no host round trip and no collective in a frame (the exchange
     # handles travel once, at set-up, over torch.distributed with any backend).
     native_multi = alltoall
-    multi_fallback = None
-    if native_multi and args.mg_pipeline:
-        os.environ["GSM_MG_PIPELINE"] = "1"  # read by gsm_multigpu_prepare on every rank
+    multi_fallback = multi_transport = None
     gtargets = (None, None)
     if native_multi:
-        mg = None
-        try:  # exchange handles over torch.distributed (any backend); the frame needs no collective
-            mg = gsm_amd.MultiGpuRenderer.connect(renderer, rank, world_size, gsm_amd.MultiGpuRenderer.torch_allgather)
+        mg, multi_transport, multi_fallback = connect_multi(gsm_amd, renderer, rank, world_size, backend, dev, args)
+        if mg is None:
+            native_multi = False
+            print(f"bench: native multi-GPU frame unavailable ({multi_fallback}); "
+                  "records move through gsm_amd.exchange (torch all-to-all, host-read counts)", file=sys.stderr)
+        else:
             frame_ptr = mg.frame()[0]  # rank 0: the gathered frame (library memory, zero copy)
             if args.mg_pipeline and rank == 0:  # pipelined: the library frames alternate, gather into ours
                 gtargets = (torch.empty((H, W, 4), dtype=torch.float16, device=dev),
                             torch.empty((H, W), dtype=torch.float16, device=dev))
-        except gsm_amd.RendererError as e:  # e.g. exchange memory that cannot be opened on this node
-            multi_fallback = f"rank {rank}: {e}"
-        # create is collective: every rank takes the native frame or none does
-        ok = torch.tensor([0 if mg is None else 1], dtype=torch.int32, device=dev if backend == "nccl" else "cpu")
-        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
-        if int(ok.item()) == 0:
-            if mg is not None:
-                mg.close()
-            native_multi = False
-            multi_fallback = multi_fallback or "another rank's gsm_multigpu_create failed"
-            print(f"bench: native multi-GPU frame unavailable ({multi_fallback}); "
-                  "records move through gsm_amd.exchange (RCCL all-to-all, host-read counts)", file=sys.stderr)
     if alltoall and not native_multi:
         first, cnt = exchange.id_range(n, world_size, rank)
         rows = exchange.slab_rows(tiles_y, H, world_size)
@@ -561,6 +551,8 @@ def main():
     }
     if multi_fallback:
         out["multi_fallback"] = multi_fallback
+    if multi_transport:
+        out["multi_transport"] = multi_transport
     if barrier_timeouts is not None:
         out["barrier_timeouts"] = barrier_timeouts
         out["mg_pipelined"] = bool(args.mg_pipeline)
@@ -590,18 +582,10 @@ def multi_extra_frame(args, gsm_amd, scenes, dev, gpu, rank, world_size, backend
     cfg = gsm_amd.RendererConfig(max_gaussians=n, max_width=W, max_height=H, precision=prec,
                                  gaussian_color_space=gsm_amd.GaussianColorSpace.LINEAR)
     r = gsm_amd.GlobalRenderer(device=dev.index, config=cfg)
-    mg, err = None, None
-    try:
-        mg = gsm_amd.MultiGpuRenderer.connect(r, rank, world_size, gsm_amd.MultiGpuRenderer.torch_allgather)
-    except gsm_amd.RendererError as e:
-        err = f"rank {rank}: {e}"
-    ok = torch.tensor([0 if mg is None else 1], dtype=torch.int32, device=dev if backend == "nccl" else "cpu")
-    torch.distributed.all_reduce(ok, op=torch.distributed.ReduceOp.MIN)  # collective: all or none
-    if int(ok.item()) == 0:
-        if mg is not None:
-            mg.close()
+    mg, transport, err = connect_multi(gsm_amd, r, rank, world_size, backend, dev, args)
+    if mg is None:
         r.close()
-        return {"error": err or "another rank's gsm_multigpu_create failed"}
+        return {"error": err}
     frame_ptr = mg.frame()[0]
     inp = gsm_amd.GaussianInput(world, harm, n, sh)
     cam = gsm_amd.CameraParams.from_dict(cam_d)
@@ -627,9 +611,49 @@ def multi_extra_frame(args, gsm_amd, scenes, dev, gpu, rank, world_size, backend
     mg.close()
     r.close()
     return {"value": steps / elapsed, "unit": "frames/s", "n_gpus": world_size, "steps": steps, "warmup": 3,
-            "barrier_timeouts": timeouts,
+            "barrier_timeouts": timeouts, "transport": transport,
             "ms_per_step": elapsed / steps * 1e3, "workload": f"{args.multi_extra_config}: {n} gaussians "
             f"{W}x{H} partitioned by tile-row slab over {world_size} GPUs (BASELINE config 4)"}
+
+
+def connect_multi(gsm_amd, renderer, rank, world_size, backend, dev, args):
+    """The partitioned frame inside libgsm_amd (gsm_multigpu_options, include/gsm_multigpu.h): the peer-stores
+    transport first (exchange handles all-gathered over torch.distributed, any backend; no collective in a
+    frame); if any rank cannot open it (e.g. exchange memory that cannot be mapped on this node, or the
+    connect-time mapping check refusing), the in-library RCCL transport over torch's NCCL communicator
+    (grouped send / recv, host-read counts).  Collective: every rank takes the same transport.  Returns
+    (MultiGpuRenderer or None, transport name, reason of the fallback or None)."""
+    import torch
+    import torch.distributed as dist
+
+    def agree(mg):  # create is collective: every rank takes this transport or none does
+        ok = torch.tensor([0 if mg is None else 1], dtype=torch.int32, device=dev if backend == "nccl" else "cpu")
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        if int(ok.item()) == 0 and mg is not None:
+            mg.close()
+        return int(ok.item()) == 1
+    reason = None
+    mg = None
+    try:
+        opts = gsm_amd.MultiGpuOptions(pipelined=bool(args.mg_pipeline))
+        mg = gsm_amd.MultiGpuRenderer.connect(renderer, rank, world_size, gsm_amd.MultiGpuRenderer.torch_allgather,
+                                              options=opts)
+    except gsm_amd.RendererError as e:
+        reason = f"peer stores, rank {rank}: {e}"
+    if agree(mg):
+        return mg, "peer_stores", None
+    reason = reason or "peer stores: another rank's connect failed"
+    if backend != "nccl":
+        return None, None, reason
+    mg = None
+    try:
+        mg = gsm_amd.MultiGpuRenderer(renderer, gsm_amd.MultiGpuRenderer.torch_comm(dev.index), rank, world_size,
+                                      options=gsm_amd.MultiGpuOptions(transport="rccl"))
+    except gsm_amd.RendererError as e:
+        reason += f"; rccl, rank {rank}: {e}"
+    if agree(mg):
+        return mg, "rccl", reason
+    return None, None, reason + "; rccl: unavailable"
 
 
 def timed_loop(steps, step, renderer, world_size, dev, backend="nccl"):

@@ -23,6 +23,29 @@ __device__ __forceinline__ float clampf(float v, float lo, float hi) {
 }
 
 // ---------------------------------------------------------------------------
+// Cheaper sequences with the numeric contract's results (r06).  Checked bit for bit
+// against the compiler's correctly rounded sequences (-fhip-fp32-correctly-rounded-divide-sqrt) over EVERY
+// 32-bit input on gfx950 (tools/exp/crmath_check.hip, profiles/r06_crmath_check.txt):
+//  * sqrt_cr: v_sqrt_f32 and the IEEE sequence's two-neighbour residual test, without its tiny-input scaling
+//    and its special-class select (9 instead of 15 VALU) -- the same bits as __builtin_sqrtf for every
+//    x >= 4.6e-32 (the largest input that differs is 0x0b6e9372 = 4.59e-32), +0, -0, +inf and NaN;
+//    callers pass x >= 1e-16 by construction (a max with a positive constant, or a sum of squares of a
+//    term beyond 1e-8);
+//  * rcp_cr: v_rcp_f32 and one fma Newton step (3 instead of 9 VALU and the denormal-mode switches) -- the
+//    same bits as 1.0f / b for every b in [2^-126, 2^126] (b above 2^126: 1/b subnormal, differs).
+__device__ __forceinline__ float sqrt_cr(float x) {
+    const float s = __builtin_amdgcn_sqrtf(x);
+    const float sd = __uint_as_float(__float_as_uint(s) - 1u), su = __uint_as_float(__float_as_uint(s) + 1u);
+    const float rd = __builtin_fmaf(-sd, s, x), ru = __builtin_fmaf(-su, s, x);
+    const float r = rd <= 0.0f ? sd : s;
+    return ru > 0.0f ? su : r;
+}
+__device__ __forceinline__ float rcp_cr(float b) {
+    const float r = __builtin_amdgcn_rcpf(b);
+    return __builtin_fmaf(__builtin_fmaf(-b, r, 1.0f), r, r);
+}
+
+// ---------------------------------------------------------------------------
 // Correctly rounded a[k] / b for K numerators over one divisor -- bit for bit the IEEE a[k] / b of the
 // oracle -- at one division's cost: y = RN(1 / b), then per numerator q = RN(a y), r = RN(a - b q) (exact
 // by the fma), q' = RN(q + r y): Markstein's correction, correctly rounded when y is the correctly
@@ -47,7 +70,7 @@ __device__ __forceinline__ void div_many(float (&a)[K], float b) {
         for (int k = 0; k < K; ++k) a[k] = a[k] / b;
         return;
     }
-    const float y = 1.0f / b;
+    const float y = rcp_cr(b);  // = 1.0f / b: b in [2^-29, 2^29] here
 #pragma unroll
     for (int k = 0; k < K; ++k) {
         const float q = a[k] * y;
@@ -105,8 +128,11 @@ __device__ __forceinline__ Conic conic_from_quant(const float2* __restrict__ sin
     float s = sc.x, c = sc.y;
     float sig1 = __builtin_fmaxf(sigma1, 1e-4f);
     float sig2 = __builtin_fmaxf(sigma2, 1e-4f);
-    float iv1 = 1.0f / (sig1 * sig1);
-    float iv2 = 1.0f / (sig2 * sig2);
+    // sig^2 is in [1e-8, 65504^2] or +inf (an fp16 sigma >= 1e-4: inf when the fp32 sigma passed 65504 --
+    // adversarial scales reach it, tests/adversarial.py): rcp_cr's exact range, and IEEE 1 / inf = +0
+    const float q1 = sig1 * sig1, q2 = sig2 * sig2;
+    float iv1 = q1 < __builtin_inff() ? rcp_cr(q1) : 0.0f;
+    float iv2 = q2 < __builtin_inff() ? rcp_cr(q2) : 0.0f;
     float cc = c * c, ss = s * s, cs = c * s;
     Conic k;
     k.A = cc * iv1 + ss * iv2;
@@ -285,7 +311,7 @@ __device__ __forceinline__ M3 build_cov3d(const float scale[3], const float rot[
         float d = q[0] * q[0] + q[1] * q[1];
         d = d + q[2] * q[2];
         d = d + q[3] * q[3];
-        float nrm = __builtin_sqrtf(__builtin_fmaxf(d, 1e-8f));
+        float nrm = sqrt_cr(__builtin_fmaxf(d, 1e-8f));
         if (nrm < 1e-8f) {
             q[0] = 1.0f; q[1] = 0.0f; q[2] = 0.0f; q[3] = 0.0f;
         } else {
@@ -374,7 +400,7 @@ __device__ __forceinline__ Cov2 stabilize_cov2d(Cov2 cov, float maxEig) {
     float v1x, v1y;
     if (__builtin_fabsf(b) > 1e-8f) {
         float vx = b, vy = l1 - a;
-        float dn = __builtin_fmaxf(__builtin_sqrtf(vx * vx + vy * vy), 1e-8f);
+        float dn = __builtin_fmaxf(sqrt_cr(vx * vx + vy * vy), 1e-8f);  // (|vx| > 1e-8: the sum >= 1e-16)
         float v2[2] = {vx, vy};
         div_many(v2, dn);
         v1x = v2[0];
@@ -409,7 +435,7 @@ __device__ __forceinline__ bool theta_sigmas(const Cov2& cov, float* theta, floa
     float v1x, v1y;
     if (__builtin_fabsf(b) > 1e-8f) {
         float tx = b, ty = l1 - a;
-        float nn = __builtin_sqrtf(tx * tx + ty * ty);
+        float nn = sqrt_cr(tx * tx + ty * ty);  // (|tx| > 1e-8: the sum >= 1e-16)
         float v2[2] = {tx, ty};
         div_many(v2, nn);
         v1x = v2[0];
@@ -424,8 +450,8 @@ __device__ __forceinline__ bool theta_sigmas(const Cov2& cov, float* theta, floa
     if (th < 0.0f) th = th + kPiF;
     if (th >= kPiF) th = th - kPiF;
     *theta = th;
-    *s1 = __builtin_sqrtf(l1);
-    *s2 = __builtin_sqrtf(l2);
+    *s1 = sqrt_cr(l1);  // (l1, l2 >= 1e-8)
+    *s2 = sqrt_cr(l2);
     return __builtin_isfinite(th) && __builtin_isfinite(*s1) && __builtin_isfinite(*s2);
 }
 
@@ -434,15 +460,15 @@ __device__ __forceinline__ void obb_extents(const Cov2& cov, float* ex, float* e
     float a = cov.a, b = cov.b, d = cov.d;
     float det = a * d - b * b;
     float mid = 0.5f * (a + d);
-    float sq = __builtin_sqrtf(__builtin_fmaxf(mid * mid - det, 1e-6f));
+    float sq = sqrt_cr(__builtin_fmaxf(mid * mid - det, 1e-6f));
     float l1 = mid + sq;
     float l2 = __builtin_fmaxf(mid - sq, 1e-6f);
-    float e1 = 3.0f * __builtin_sqrtf(__builtin_fmaxf(l1, 1e-6f));
-    float e2 = 3.0f * __builtin_sqrtf(__builtin_fmaxf(l2, 1e-6f));
+    float e1 = 3.0f * sqrt_cr(__builtin_fmaxf(l1, 1e-6f));
+    float e2 = 3.0f * sqrt_cr(__builtin_fmaxf(l2, 1e-6f));
     float v1x, v1y;
     if (__builtin_fabsf(b) > 1e-6f) {
         float vx = b, vy = l1 - a;
-        float dn = __builtin_fmaxf(__builtin_sqrtf(vx * vx + vy * vy), 1e-6f);
+        float dn = __builtin_fmaxf(sqrt_cr(vx * vx + vy * vy), 1e-6f);  // (|vx| > 1e-6: the sum >= 1e-12)
         float v2[2] = {vx, vy};
         div_many(v2, dn);
         v1x = v2[0];

@@ -109,7 +109,9 @@ __device__ __forceinline__ ProjOut project_gaussian(const void* __restrict__ wor
         }
         float sx = 0.f, sy = 0.f;
         if (vis) {
-            float ndcx = clip[0] / clip[3], ndcy = clip[1] / clip[3];
+            float ndc[2] = {clip[0], clip[1]};
+            div_many(ndc, clip[3]);  // clip / w, each correctly rounded (w > near > 0)
+            const float ndcx = ndc[0], ndcy = ndc[1];
             sx = ((ndcx + 1.0f) * cam.width - 1.0f) * 0.5f;  // ndcToScreenCentered
             sy = ((ndcy + 1.0f) * cam.height - 1.0f) * 0.5f;
             if (opacity < P.bin.alphaThreshold) vis = false;
@@ -135,7 +137,7 @@ __device__ __forceinline__ ProjOut project_gaussian(const void* __restrict__ wor
         if (vis && P.bin.totalInkThreshold > 0.0f) {  // cullByTotalInkFromCov
             float a = cov.a, b = 0.5f * (cov.b + cov.c), d = cov.d;
             float det = a * d - b * b;
-            float ink = opacity * 6.283185f * __builtin_sqrtf(__builtin_fmaxf(det, 1e-12f));
+            float ink = opacity * 6.283185f * sqrt_cr(__builtin_fmaxf(det, 1e-12f));
             float s = clampf((P.adjFar - clip[3]) / P.adjDen, 0.0f, 1.0f);
             float depthFactor = 1.0f - s * s;
             if (ink < depthFactor * P.bin.totalInkThreshold) vis = false;
@@ -786,7 +788,14 @@ __global__ __launch_bounds__(kProjectBlock) void k_records_in(
         r.bounds = __builtin_bit_cast(short4, make_uint2(w2.x, w2.y));
         r.rb = w2.z;
         r.pad = w2.w;
-        const int rw = (int)r.bounds.y - (int)r.bounds.x + 1;
+        // a received record addresses only the frame's tile grid (r06): computeTileBounds already clamps a
+        // projected gaussian's rect to it, so this changes nothing for a valid record, and a corrupt one --
+        // e.g. words that never arrived over a stale mapping -- cannot send the scatter or the sort outside it
+        r.bounds.x = (short)max((int)r.bounds.x, 0);
+        r.bounds.y = (short)min((int)r.bounds.y, (int)P.bin.tilesX - 1);
+        r.bounds.z = (short)max((int)r.bounds.z, 0);
+        r.bounds.w = (short)min((int)r.bounds.w, (int)P.bin.tilesY - 1);
+        const int rw = max((int)r.bounds.y - (int)r.bounds.x + 1, 0);
         const RowSet R = rows_of(P);
         int k0, k1;
         rows_within(R, (int)r.bounds.z, (int)r.bounds.w, &k0, &k1);
@@ -795,9 +804,10 @@ __global__ __launch_bounds__(kProjectBlock) void k_records_in(
         uint4* rp = (uint4*)(outRec + gid);
         rp[0] = make_uint4(r.ra.x, r.ra.y, r.ra.z, r.ra.w);
         uint32_t mask;
-        if (((int)r.bounds.w - (int)r.bounds.z + 1) * rw <= kMaskTiles) {
-            // the sender's answers for this slab's rows (slab_tile_mask)
-            mask = r.pad;
+        const int area = max((int)r.bounds.w - (int)r.bounds.z + 1, 0) * rw;
+        if (area <= kMaskTiles) {
+            // the sender's answers for this slab's rows (slab_tile_mask), never past the rect
+            mask = area >= kMaskTiles ? r.pad : (r.pad & ((1u << area) - 1u));
             ntiles = (uint32_t)__builtin_popcount(mask);
         } else {
             // a rect of more than 32 tiles: the values k_project had in registers, rebuilt from the

@@ -41,6 +41,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
@@ -93,9 +94,12 @@ constexpr size_t kFlagWords = 0;      // u32 flag[kBarriers][kMaxSlabs]: [b][src
 constexpr size_t kStatusWord = 64;    // u32 [0] barrier timeouts, [1] failed peer arrivals, [2] epoch of the last timeout
 constexpr size_t kCountsWord = 256;   // u32 counts[2][kMaxSlabs * kMaxSlabs] (frame parity; row = source)
 constexpr size_t kRecordsOff = 4096;  // SplatRecord[2][capacity] (frame parity)
-constexpr size_t kProbeWord = 768;    // u32 probe[kMaxSlabs]: word src of the connect-time check (MultiGpu::probe)
+constexpr size_t kProbeWord = 768;    // u32 probe[kMaxSlabs][8]: words 8 src .. 8 src + 7 of the connect-time check
+                                      // (MultiGpu::probe); in every later page of an allocation the same words
+                                      // from its start
 constexpr size_t kCtlZeroWords = kProbeWord;  // control words zeroed at prepare (flags, status, counts)
 static_assert(kCountsWord + 2 * kMaxSlabs * kMaxSlabs <= kProbeWord, "counts before the probe words");
+static_assert(kProbeWord + 8 * kMaxSlabs <= 1024, "probe words inside the control page");
 static_assert(kFlagWords + kBarriers * kMaxSlabs <= kStatusWord, "flags before the status word");
 constexpr uint32_t kFailBit = 0x80000000u;  // a flag's epoch with this bit: that rank's frame failed
 constexpr uint32_t kEpochMask = 0x7FFFFFFFu;
@@ -215,7 +219,7 @@ __global__ __launch_bounds__(64) void k_mg_probe(ProbeMaps maps, uint32_t total,
         if (i >= total) i -= total;
         uint32_t m = 0;
         while (m + 1u < maps.n && i >= maps.pages[m]) i -= maps.pages[m++];
-        uint32_t* w = maps.base[m] + (size_t)i * 1024u + (i == 0 ? kProbeWord + src : src);
+        uint32_t* w = maps.base[m] + (size_t)i * 1024u + (i == 0 ? kProbeWord : 0) + 8u * src;
         if (!check) {
             __hip_atomic_store(w, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             continue;
@@ -229,6 +233,20 @@ __global__ __launch_bounds__(64) void k_mg_probe(ProbeMaps maps, uint32_t total,
             __builtin_amdgcn_s_sleep(1);
         }
     }
+}
+
+// The same words written with the gathered pixels' store form: plain stores, then each workgroup's
+// system-scope release (the blend's L2 write-back, gsm_blend.hip) -- read back by the host.  Workgroups
+// 8c .. 8c + 7 take pages 64c .. 64c + 63 (lane = page), workgroup 8c + j writing word 8 src + j of each,
+// so that every page is stored from workgroups of all eight XCDs (dealt round robin).
+__global__ __launch_bounds__(64) void k_mg_probe_plain(ProbeMaps maps, uint32_t total, uint32_t src, uint32_t value) {
+    const uint32_t j = blockIdx.x & 7u;
+    for (uint32_t t = (blockIdx.x >> 3) * 64u + threadIdx.x; t < total; t += (gridDim.x >> 3) * 64u) {
+        uint32_t i = t, m = 0;
+        while (m + 1u < maps.n && i >= maps.pages[m]) i -= maps.pages[m++];
+        maps.base[m][(size_t)i * 1024u + (i == 0 ? kProbeWord : 0) + 8u * src + j] = value + j;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // (as a gathering blend workgroup at its exit)
 }
 
 // rank 0's copy of the gathered frame into the caller's target (rows of `rowBytes`, a multiple of 2):
@@ -653,9 +671,16 @@ gsm_status MultiGpu::probe(char* const* base, const size_t* bytes) {
         return GSM_ERR_FAILED_TO_ALLOCATE_BUFFER;
     }
     const uint32_t grid = std::min<uint32_t>(2048u, (total + 63u) / 64u);
+    const uint32_t gridPlain = 8u * std::min<uint32_t>(512u, (total + 63u) / 64u);
     const unsigned long long spin = 50ull * wallKHz_;
+    uint32_t maxPages = 0;
+    for (int p = 0; p < world_; ++p) maxPages = std::max(maxPages, maps.pages[p]);
+    std::vector<uint32_t> host((size_t)maxPages * 8);
     bool ok = true;
+    uint32_t badPlain = 0, firstMap = 0, firstPage = 0, firstGot = 0, firstWant = 0;
     for (uint32_t round = 0; round < 2 && ok; ++round) {
+        // (a) the counts' / records' / flags' forms: write-through stores, polled with system-coherent loads
+        //     by other workgroups
         const uint32_t value = 0x5EED0000u | ((uint32_t)rank_ << 8) | (round + 1u);
         const uint32_t rotStore = round * (total / 3u), rotCheck = rotStore + total / 2u + 64u;
         hipLaunchKernelGGL(k_mg_probe, dim3(grid), dim3(64), 0, s, maps, total, (uint32_t)rank_, value,
@@ -665,9 +690,35 @@ gsm_status MultiGpu::probe(char* const* base, const size_t* bytes) {
         uint32_t nf = 1;
         ok = hipMemcpyAsync(&nf, fails, 4, hipMemcpyDeviceToHost, s) == hipSuccess && hipStreamSynchronize(s) == hipSuccess &&
              nf == 0;
-        for (int p = 0; ok && p < world_; ++p) {  // the control page's word through the host's own path
-            uint32_t w = 0;
-            ok = hipMemcpy(&w, maps.base[p] + kProbeWord + rank_, 4, hipMemcpyDeviceToHost) == hipSuccess && w == value;
+        // (b) the gathered pixels' form: plain stores from every XCD released at the workgroups' exit, read
+        //     back by the host (one 32-B run per page) -- r06's reuse test saw such stores stay in an L2 past
+        //     the release on a range last mapped uncached (the host read the connect's own probe words)
+        const uint32_t pv = 0x9A5E0000u | ((uint32_t)rank_ << 8) | ((round + 1u) << 4);
+        hipLaunchKernelGGL(k_mg_probe_plain, dim3(gridPlain), dim3(64), 0, s, maps, total, (uint32_t)rank_, pv);
+        ok = ok && hipStreamSynchronize(s) == hipSuccess;
+        for (int p = 0; ok && p < world_; ++p) {
+            const char* b = (const char*)maps.base[p];
+            const size_t off = 32u * (uint32_t)rank_;
+            ok = hipMemcpy(host.data(), b + kProbeWord * 4 + off, 32, hipMemcpyDeviceToHost) == hipSuccess;
+            if (ok && maps.pages[p] > 1)
+                ok = hipMemcpy2D(host.data() + 8, 32, b + 4096 + off, 4096, 32, maps.pages[p] - 1, hipMemcpyDeviceToHost) ==
+                     hipSuccess;
+            for (size_t i = 0; ok && i < (size_t)maps.pages[p] * 8; ++i)
+                if (host[i] != pv + (uint32_t)(i & 7u)) {
+                    if (badPlain++ == 0) {
+                        firstMap = (uint32_t)p;
+                        firstPage = (uint32_t)(i / 8);
+                        firstGot = host[i];
+                        firstWant = pv + (uint32_t)(i & 7u);
+                    }
+                }
+            ok = ok && badPlain == 0;
+        }
+        if (!ok) {  // (the refusal's evidence, on stderr)
+            fprintf(stderr,
+                    "gsm_multigpu_connect: rank %d refuses its mappings (round %u): %u polled words not seen in 50 ms, "
+                    "%u plain-stored words wrong through the host (first: mapping %u page %u holds 0x%08x, stored 0x%08x)\n",
+                    rank_, round, nf, badPlain, firstMap, firstPage, firstGot, firstWant);
         }
     }
     hipFree(fails);

@@ -1,11 +1,13 @@
 """Child process of tests/test_multigpu_ipc.py::test_fine_exchange_after_freed_uncached_allocations (GPU).
 
 Replays the r05 sequence behind the barrier timeouts (profiles/r05_mg_uncached_diag_nokeep.log)
-in one process: per case, virtual-rank frames over *uncached* exchange memory (GSM_MG_MEM=uncached-ab, the A/B
-kind the product refuses) plus raw uncached allocations of the exchange sizes, everything freed, then a
-fine-grained exchange of the same shape -- whose allocations can land on the freed uncached ranges.  The fine
-exchange either refuses at connect (its mapping check) or renders two frames that are compared with the
-oracle; barrier timeout 2 s.  Writes {"cases": [{case, refused, timeouts, bad_rows}]} to argv[1].
+in one process: per case, virtual-rank exchanges over *uncached* memory (GSM_MG_MEM=uncached-ab, the A/B kind
+the product refuses; prepared and connected -- the connect's mapping check writes every page -- but no frame is
+rendered on it: records read from it can be garbage, r03-r05) plus raw uncached allocations of the exchange
+sizes, everything freed, then a fine-grained exchange of the same shape -- whose allocations can land on the
+freed uncached ranges.  The fine exchange either refuses at connect (its mapping check) or renders two frames
+that are compared with the oracle; barrier timeout 2 s.  Writes {"cases": [{case, refused, timeouts,
+bad_rows}]} to argv[1].
 
 usage: python tests/mg_uc_reuse.py OUT.json"""
 import ctypes as C
@@ -41,7 +43,7 @@ def raw_uncached(sizes):
     HIP.hipDeviceSynchronize()
 
 
-def frames(world, n, w, h, sh, prec, cams, inp, opts, kind):
+def frames(world, n, w, h, sh, prec, cams, inp, opts, kind, render=True):
     if kind == "uncached":
         os.environ["GSM_MG_MEM"] = "uncached-ab"
     else:
@@ -59,6 +61,10 @@ def frames(world, n, w, h, sh, prec, cams, inp, opts, kind):
         out["refused"] = True
         for m, _ in pre:
             m.close()
+    if mgs and not render:
+        for m in mgs:
+            m.close()
+        mgs = []
     if mgs:
         frame_ptr, _ = mgs[0].frame()
         stream = torch.cuda.current_stream()
@@ -93,7 +99,7 @@ def main():
         refs = [O.render(world_np, harm_np, sh, c, w, h, max_gaussians=n)["color"] for c in cams]
         opts = gsm.MultiGpuOptions(timeout_ms=2000)
         for rep in range(2):
-            uc = frames(world, n, w, h, sh, prec, cams, inp, opts, "uncached")  # (its pixels are not judged)
+            uc = frames(world, n, w, h, sh, prec, cams, inp, opts, "uncached", render=False)
             rec = 2 * ((n * 48 + 4095) // 4096 * 4096) + 4096
             raw_uncached([rec] * world + [w * h * 8, w * h * 2])
             fine = frames(world, n, w, h, sh, prec, cams, inp, opts, "fine")

@@ -188,6 +188,7 @@ gsm_status DepthFirstRenderer::renderStereoSbs(hipStream_t s, const gsm_gaussian
                                                const gsm_camera_params& left, const gsm_camera_params& right,
                                                const float* scene, uint32_t width, uint32_t height, void* color,
                                                size_t pitch) {
+    (void)hipGetLastError();  // (an error left by an earlier call of the process is not this call's: the launches below are checked)
     // encodeStereoPipeline guards (DepthFirstRenderer.swift:478, 607) -- errors, not a silent skip
     if (in.gaussian_count > maxGaussians_) return GSM_ERR_INVALID_GAUSSIAN_COUNT;
     if (width == 0 || height == 0 || width > maxWidth_ || height > maxHeight_) return GSM_ERR_INVALID_DIMENSIONS;

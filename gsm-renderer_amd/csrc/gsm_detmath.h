@@ -101,6 +101,12 @@ GSM_HD float det_exp2f(float x) {
 // fast::powr(x, y), x > 0 (GaussianShared.h:120).
 GSM_HD float det_powrf(float x, float y) { return det_exp2f(y * det_log2f(x)); }
 
+// gaussianComputePower (GaussianShared.h:595-597).
+GSM_HD float det_compute_power(float opacity) {
+    const float LN2 = 0.693147180559945f;
+    return LN2 * 8.0f + LN2 * det_log2f(__builtin_fmaxf(opacity, 1e-6f));
+}
+
 // ---- host-side table builders (double series, no libm) ----
 inline double det_sin_series(double x) {
     double x2 = x * x, term = x, sum = x;
@@ -208,6 +214,15 @@ inline uint16_t double_to_half_bits(double d) {
     return (uint16_t)(sign | (uint16_t)(he << 10) | (uint16_t)((int)r - 1024));
 }
 inline uint16_t float_to_half_bits(float f) { return double_to_half_bits((double)f); }
+
+// The projection's table of the u8 channel values c = 0..255 (k_project, stored behind the 65536 sincos
+// entries): x = the tile-test level 2 computePower(c) of an opacity byte (tileCountIndirectKernel,
+// GlobalShaders.metal:563-616), y = the bits of fp16(float(c) / 255) (getColor/getOpacity,
+// GlobalShaders.metal:9-15) -- the same single IEEE operations the kernels evaluated per gaussian before r06.
+inline void det_byte_lut_entry(uint32_t c, float* level, uint32_t* div255) {
+    *level = 2.0f * det_compute_power((float)c);
+    *div255 = float_to_half_bits((float)c / 255.0f);
+}
 // e^x for fp16 x: one rounding of the double series.
 inline uint16_t det_exp_half_bits(uint16_t xb) {
     float x = half_bits_to_float(xb);

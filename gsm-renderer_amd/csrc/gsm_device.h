@@ -141,11 +141,8 @@ __device__ __forceinline__ Conic conic_from_quant(const float2* __restrict__ sin
     return k;
 }
 
-// gaussianComputePower (GaussianShared.h:595-597).
-__device__ __forceinline__ float compute_power(float opacity) {
-    const float LN2 = 0.693147180559945f;
-    return LN2 * 8.0f + LN2 * det_log2f(__builtin_fmaxf(opacity, 1e-6f));
-}
+// gaussianComputePower (GaussianShared.h:595-597; gsm_detmath.h).
+__device__ __forceinline__ float compute_power(float opacity) { return det_compute_power(opacity); }
 
 // gaussianSegmentIntersectEllipse .. intersectsTile (GaussianShared.h:599-653).
 __device__ __forceinline__ bool seg_ellipse(float a, float b, float c, float d, float l, float r) {

@@ -206,7 +206,7 @@ struct DeviceArena {
                                                  // skip flag for that half is clear, from the tile's start
     uint32_t* halfCount = nullptr;             // [2 * tileCount] entries of each half list (half-major)
     uint16_t* expTable = nullptr;              // [65536]
-    float2* sincosTable = nullptr;             // [65536]
+    float2* sincosTable = nullptr;             // [kSincosEntries + 256]: sin/cos, then the byte table (det_byte_lut_entry)
 };
 
 // A/B switches of the frame pipeline.  Read ONCE, when a renderer is created (tuning_from_env),
@@ -249,6 +249,8 @@ constexpr uint32_t kGidMask = (1u << kHalfSkipShift) - 1u;
 constexpr float kBlendZeroP = 34.65625f;
 
 constexpr int kProjectBlock = 256;
+// entries of the sincos table (one per quantised angle); the 256 byte-table entries follow (gsm_detmath.h)
+constexpr uint32_t kSincosEntries = 65536;
 constexpr int kRadixBlock = 256;
 constexpr int kRadixItems = 16;  // keys per thread per chunk (4096-key chunks)
 constexpr int kRadixChunk = kRadixBlock * kRadixItems;

@@ -41,11 +41,20 @@ struct ProjOut {
     bool vis, countable;
 };
 
-// fp16(float(c) / 255) for c = 0..255 (getColor/getOpacity, GlobalShaders.metal:9-15), one
-// entry per thread of the block; callers use it after the barrier
-static_assert(kProjectBlock == 256, "one div255 entry per thread");
-__device__ __forceinline__ void fill_div255(uint16_t* div255) {
-    div255[threadIdx.x] = f_to_hbits((float)threadIdx.x / 255.0f);
+// The per-block byte table: fp16(float(c) / 255) (getColor/getOpacity, GlobalShaders.metal:9-15) and the
+// tile-test level 2 computePower(c) (tileCountIndirectKernel, GlobalShaders.metal:563-616) of every u8
+// channel value c, one entry per thread of the block, copied from the host-built entries behind the sincos
+// table (det_byte_lut_entry; r06: the per-gaussian division and log2 they replace were ~3% of k_project's
+// VALU).  Callers use it after the barrier.
+static_assert(kProjectBlock == 256, "one byte-table entry per thread");
+struct ByteLut {
+    uint16_t div255[256];
+    float level[256];
+};
+__device__ __forceinline__ void fill_byte_lut(ByteLut& L, const float2* __restrict__ sincos) {
+    const uint2 e = ((const uint2*)(sincos + kSincosEntries))[threadIdx.x];
+    L.level[threadIdx.x] = __uint_as_float(e.x);
+    L.div255[threadIdx.x] = (uint16_t)e.y;
     __syncthreads();
 }
 
@@ -68,7 +77,7 @@ __device__ __forceinline__ ProjOut project_gaussian(const void* __restrict__ wor
                                                     const void* __restrict__ harm, uint32_t gid,
                                                     const ProjectArgs& P,
                                                     const float2* __restrict__ sincos,
-                                                    const uint16_t* div255) {
+                                                    const ByteLut& lut) {
     ProjOut o;
     o.vis = false;
     o.countable = false;
@@ -200,10 +209,10 @@ __device__ __forceinline__ ProjOut project_gaussian(const void* __restrict__ wor
             float cmx = hbits_to_f(hmx), cmy = hbits_to_f(hmy);
             Conic k = conic_from_quant(sincos, thq, hbits_to_f(hs1), hbits_to_f(hs2));
             uint16_t hcxx = f_to_hbits(k.A), hcyy = f_to_hbits(k.C), hcxy2 = f_to_hbits(2.0f * k.B);
-            // fp16(float(c) / 255) for the u8 channels: the block's 256-entry table
-            uint16_t hop = div255[cO];
-            uint16_t hr = div255[cR], hg = div255[cG];
-            uint16_t hb = div255[cB];
+            // fp16(float(c) / 255) for the u8 channels: the block's byte table
+            uint16_t hop = lut.div255[cO];
+            uint16_t hr = lut.div255[cR], hg = lut.div255[cG];
+            uint16_t hb = lut.div255[cB];
             BlendRecordA ra;
             ra.x = rdw.x;
             ra.y = (uint32_t)hcxx | ((uint32_t)hcyy << 16);
@@ -219,7 +228,7 @@ __device__ __forceinline__ ProjOut project_gaussian(const void* __restrict__ wor
             // tileCountIndirectKernel (GlobalShaders.metal:563-616): alpha is the u8 opacity
             const float alpha = (float)cO;
             o.countable = alpha >= 1e-4f && minTX <= maxTX && minTY <= maxTY;
-            o.w = o.countable ? 2.0f * compute_power(alpha) : 0.0f;
+            o.w = o.countable ? lut.level[cO] : 0.0f;  // = 2 computePower(alpha)
 #if GSM_PROJ_STOP == 7
             o.countable = o.w == 12345.0f;  // (never) keeps the level alive; no tile tests
 #endif
@@ -307,7 +316,7 @@ __global__ __launch_bounds__(kProjectBlock) void k_project(
     uint32_t* __restrict__ masks, uint32_t* __restrict__ blockSums, const float2* __restrict__ sincos,
     const uint16_t* __restrict__ unitCost, uint32_t* __restrict__ unitOrder, uint32_t* __restrict__ costMax) {
     __shared__ uint32_t lds[kProjectBlock / 64];
-    __shared__ uint16_t div255[256];
+    __shared__ ByteLut lut;
     // block 0 of a scheduled launch orders the blend's units from the previous frame's walks while
     // the other blocks project (no launch, no second stream, no join before the blend)
     if (P.schedUnits) {
@@ -326,11 +335,12 @@ __global__ __launch_bounds__(kProjectBlock) void k_project(
     __shared__ uint32_t sMask[kProjectBlock];
     __shared__ uint32_t sMore[kProjectBlock];  // hits among candidates >= 32 (large rects)
     // the block's first kCandCap candidates: owner << 8 | k for rects of <= kCandRect tiles,
-    // kSearch for the candidates of larger rects (their owner comes from a binary search)
+    // kSearch for the candidates of larger rects (their owner comes from a binary search).  (r06: 8 waves
+    // per SIMD -- 3072 candidates and a 64-VGPR cap -- measured no faster than 7, profiles/r06_proj_ab.txt)
     constexpr uint32_t kCandCap = 4096, kCandRect = 64;
     constexpr uint16_t kSearch = 0xFFFFu;
     __shared__ uint16_t sCand[kCandCap];
-    fill_div255(div255);
+    fill_byte_lut(lut, sincos);
     const uint32_t tid = threadIdx.x;
     const uint32_t gid = blk * kProjectBlock + tid;
     ProjOut o;
@@ -340,7 +350,7 @@ __global__ __launch_bounds__(kProjectBlock) void k_project(
     uint32_t area = 0;
     int ty0 = 0;
     if (gid < P.count) {
-        o = project_gaussian<HALF, DEG>(world, harm, gid, P, sincos, div255);
+        o = project_gaussian<HALF, DEG>(world, harm, gid, P, sincos, lut);
         outBounds[gid] = o.bounds;
         if (o.vis) {
             // GaussianRenderData: the frame itself only reads it for rects the scatter re-tests
@@ -435,7 +445,8 @@ __global__ __launch_bounds__(kProjectBlock) void k_project(
 // hit(lo, k, ty) is called for every candidate k (ty-major, tx-minor over the rect) of gaussian
 // lo whose ellipse meets tile row ty.  Ends with a barrier.
 struct TileTestLds {
-    static constexpr uint32_t kCandCap = 4096, kCandRect = 64;
+    // (2560: k_project_part's LDS under 20 KiB; its 72 VGPRs then allow 7 waves per SIMD, r06)
+    static constexpr uint32_t kCandCap = 2560, kCandRect = 64;
     static constexpr uint16_t kSearch = 0xFFFFu;
     float4 ell[kProjectBlock];   // cmx, cmy, conic A, conic B
     float2 ell2[kProjectBlock];  // conic C, level w
@@ -539,7 +550,7 @@ __global__ __launch_bounds__(kProjectBlock) void k_project_part(
     const uint32_t blk = blockIdx.x - (P.schedUnits ? 1u : 0u);
     __shared__ uint32_t wcnt[kProjectBlock / 64][kMaxSlabs];
     __shared__ uint64_t wbal[kProjectBlock / 64][kMaxSlabs];  // the wave's ballot of each slab
-    __shared__ uint16_t div255[256];
+    __shared__ ByteLut lut;
     __shared__ TileTestLds L;
     __shared__ uint32_t sTile[kProjectBlock];  // answers of candidates < 32
     __shared__ uint32_t sSlab[kProjectBlock];  // slabs with a hit
@@ -548,7 +559,7 @@ __global__ __launch_bounds__(kProjectBlock) void k_project_part(
     // over the slab bounds (contiguous) or a division (interleaved)
     constexpr uint32_t kRowTab = 512;
     __shared__ uint8_t sRowSlab[kRowTab];
-    fill_div255(div255);
+    fill_byte_lut(lut, sincos);
     const uint32_t tid = threadIdx.x;
     const uint32_t gid = blk * kProjectBlock + tid;
     const uint32_t lane = tid & 63, wave = tid >> 6;
@@ -571,7 +582,7 @@ __global__ __launch_bounds__(kProjectBlock) void k_project_part(
     o.bounds = make_short4(0, -1, 0, -1);
     uint32_t area = 0;
     if (gid < P.count) {
-        o = project_gaussian<HALF, DEG>(world, harm, gid, P, sincos, div255);
+        o = project_gaussian<HALF, DEG>(world, harm, gid, P, sincos, lut);
         if (o.vis && o.countable)
             area = (uint32_t)(((int)o.bounds.w - (int)o.bounds.z + 1) * ((int)o.bounds.y - (int)o.bounds.x + 1));
     }

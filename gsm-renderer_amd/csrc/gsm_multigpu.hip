@@ -199,33 +199,36 @@ __global__ __launch_bounds__(256) void k_mg_zero_ctl(uint32_t* __restrict__ mem,
     if (i < words) __hip_atomic_store(mem + i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// Connect-time check of every mapping this rank stores into or polls (r06): one word
-// per 4 KiB page of each mapping -- page 0: probe word `src` of the control page (no peer writes it), page
-// g > 0: word `src` of the page (records / frames: scratch until the first frame's barrier 0, which needs
-// this rank's arrival) -- stored with the flags' store form (a relaxed system-scope atomic store) or, with
-// `check`, polled with the barrier's load form (ld_sys32) until it holds `value` or `spinTicks` pass (then
-// counted in *fails).  `rot` rotates the item -> workgroup assignment so that each word is read by another
-// workgroup (CU, XCD) than the one that stored it.
+// The mapping check (r06) of every mapping this rank stores into or polls:
+// one word per 4 KiB page of each mapping -- page 0: probe word 8 src + j of the control page (no peer
+// writes it), page g > 0: word 8 src + j of the page (records / frames: scratch until the first frame's
+// barrier 0, which needs this rank's arrival).  Workgroups 8c .. 8c + 7 take pages 64c .. 64c + 63 (lane =
+// page), workgroup 8c + j (dealt round robin to the eight XCDs) on word j: stored with the flags' store
+// form (a relaxed system-scope atomic store: write-through) or, with `check`, polled with the barrier's
+// load form (ld_sys32) on word (j + 3) & 7 -- stored from another XCD -- until it holds value + that index
+// or `spinTicks` pass (then counted in *fails).  So every page is stored from all eight XCDs and checked
+// across XCDs, as a frame's flags and records are.
 struct ProbeMaps {
     uint32_t* base[kMaxSlabs];
     uint32_t pages[kMaxSlabs];
     uint32_t n;
 };
-__global__ __launch_bounds__(64) void k_mg_probe(ProbeMaps maps, uint32_t total, uint32_t src, uint32_t value,
-                                                 uint32_t rot, int check, uint32_t* __restrict__ fails,
-                                                 unsigned long long spinTicks) {
-    for (uint32_t t = blockIdx.x * 64u + threadIdx.x; t < total; t += gridDim.x * 64u) {
-        uint32_t i = t + rot;
-        if (i >= total) i -= total;
-        uint32_t m = 0;
-        while (m + 1u < maps.n && i >= maps.pages[m]) i -= maps.pages[m++];
-        uint32_t* w = maps.base[m] + (size_t)i * 1024u + (i == 0 ? kProbeWord : 0) + 8u * src;
+__device__ __forceinline__ uint32_t* probe_word(const ProbeMaps& maps, uint32_t t, uint32_t src, uint32_t j) {
+    uint32_t i = t, m = 0;
+    while (m + 1u < maps.n && i >= maps.pages[m]) i -= maps.pages[m++];
+    return maps.base[m] + (size_t)i * 1024u + (i == 0 ? kProbeWord : 0) + 8u * src + j;
+}
+__global__ __launch_bounds__(64) void k_mg_probe(ProbeMaps maps, uint32_t total, uint32_t src, uint32_t value, int check,
+                                                 uint32_t* __restrict__ fails, unsigned long long spinTicks) {
+    const uint32_t j = check ? ((blockIdx.x + 3u) & 7u) : (blockIdx.x & 7u);
+    for (uint32_t t = (blockIdx.x >> 3) * 64u + threadIdx.x; t < total; t += (gridDim.x >> 3) * 64u) {
+        uint32_t* w = probe_word(maps, t, src, j);
         if (!check) {
-            __hip_atomic_store(w, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(w, value + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             continue;
         }
         const unsigned long long t0 = wall_clock64();
-        while (ld_sys32(w) != value) {
+        while (ld_sys32(w) != value + j) {
             if (wall_clock64() - t0 > spinTicks) {
                 atomicAdd(fails, 1u);
                 break;
@@ -241,11 +244,8 @@ __global__ __launch_bounds__(64) void k_mg_probe(ProbeMaps maps, uint32_t total,
 // so that every page is stored from workgroups of all eight XCDs (dealt round robin).
 __global__ __launch_bounds__(64) void k_mg_probe_plain(ProbeMaps maps, uint32_t total, uint32_t src, uint32_t value) {
     const uint32_t j = blockIdx.x & 7u;
-    for (uint32_t t = (blockIdx.x >> 3) * 64u + threadIdx.x; t < total; t += (gridDim.x >> 3) * 64u) {
-        uint32_t i = t, m = 0;
-        while (m + 1u < maps.n && i >= maps.pages[m]) i -= maps.pages[m++];
-        maps.base[m][(size_t)i * 1024u + (i == 0 ? kProbeWord : 0) + 8u * src + j] = value + j;
-    }
+    for (uint32_t t = (blockIdx.x >> 3) * 64u + threadIdx.x; t < total; t += (gridDim.x >> 3) * 64u)
+        *probe_word(maps, t, src, j) = value + j;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // (as a gathering blend workgroup at its exit)
 }
 
@@ -355,8 +355,8 @@ class MultiGpu {
     // the same phases over RCCL (GSM_MG_TRANSPORT_RCCL): no exchange memory, no device barrier
     gsm_status runRccl(int p, hipStream_t s, const gsm_gaussian_input* in, const gsm_camera_params* cam, uint32_t width,
                        uint32_t height, Targets t, size_t colorPitch, void* depth, size_t depthPitch, void* gatherColor);
-    // connect's check of the mappings (peer-stores transport): GSM_OK or GSM_ERR_DEVICE_NOT_AVAILABLE
-    gsm_status probe(char* const* base, const size_t* bytes);
+    // the mapping check of n mappings (peer-stores transport): GSM_OK or GSM_ERR_DEVICE_NOT_AVAILABLE
+    gsm_status probe(char* const* base, const size_t* bytes, int n, const char* who);
     // slab rows [*y0, *y1) of pixel rows of tile-row index k of rank q's slab (contiguous: k = 0 only)
     bool slabPixelRows(uint32_t q, uint32_t k, uint32_t height, uint32_t* y0, uint32_t* y1) const;
     bool libraryFrame(const void* p) const {
@@ -431,6 +431,14 @@ class MultiGpu {
     uint32_t wallKHz_ = 100000;
     unsigned long long timeoutTicks_ = 0;
     std::vector<void*> opened_;  // IPC mappings of peer allocations
+    // exchange allocations that failed the prepare-time mapping check, kept until destroy so that their
+    // ranges are not handed out again (r06)
+    std::vector<char*> heldBack_;
+    uint32_t heldBackCount_ = 0;
+    static constexpr int kAllocAttempts = 4;
+
+   public:
+    uint32_t heldBack() const { return heldBackCount_; }
 };
 
 void MultiGpu::release() {
@@ -439,6 +447,8 @@ void MultiGpu::release() {
     if (front_) hipStreamSynchronize(front_);
     for (void* p : opened_) hipIpcCloseMemHandle(p);
     opened_.clear();
+    for (char* p : heldBack_) hipFree(p);
+    heldBack_.clear();
     for (void* p : {(void*)mem_, (void*)sendCounts_, (void*)recvCount_, (void*)done_, (void*)sendRec_, (void*)recvRec_,
                     (void*)countMat_, (void*)ownFrame_, (void*)ownDepth_})
         if (p) hipFree(p);
@@ -493,6 +503,7 @@ gsm_status MultiGpu::prepare(GlobalRenderer* r, int rank, int world, const gsm_m
     m->depthPitch0_ = align_up((size_t)r->maxWidth() * 2u, 16);
     m->frameStride_ = align_up(m->framePitch_ * r->maxHeight(), 4096);
     m->depthStride_ = align_up(m->depthPitch0_ * r->maxHeight(), 4096);
+    gsm_status failSt = GSM_ERR_FAILED_TO_ALLOCATE_BUFFER;
     bool ok = r->ensurePartitionBuffers((uint32_t)world) == GSM_OK &&
               hipMalloc(&m->sendCounts_, kMaxSlabs * 4) == hipSuccess && hipMalloc(&m->recvCount_, 8) == hipSuccess &&
               hipMalloc(&m->done_, kBarriers * kArriveWordsPerBarrier * 4) == hipSuccess &&
@@ -523,16 +534,35 @@ gsm_status MultiGpu::prepare(GlobalRenderer* r, int rank, int world, const gsm_m
         m->frameOff_ = rank == 0 ? align_up(kRecordsOff + recBytes, 4096) : 0;
         m->depthOff_ = rank == 0 ? m->frameOff_ + nFrames * m->frameStride_ : 0;
         m->memBytes_ = rank == 0 ? m->depthOff_ + nFrames * m->depthStride_ : kRecordsOff + recBytes;
-        hipError_t ae = m->memKind_ == 2u ? hipMalloc((void**)&m->mem_, m->memBytes_)
-                                          : hipExtMallocWithFlags((void**)&m->mem_, m->memBytes_,
-                                                                  m->memKind_ == 1u ? hipDeviceMallocUncached
-                                                                                    : hipDeviceMallocFinegrained);
-        ok = ae == hipSuccess && (!getenv("GSM_MG_POISON") || hipMemset(m->mem_, 0xAB, m->memBytes_) == hipSuccess) &&
-             hipDeviceSynchronize() == hipSuccess;
-        if (ok) {  // the control words: write-through zeros, not a cached memset (k_mg_zero_ctl)
-            hipLaunchKernelGGL(k_mg_zero_ctl, dim3((kCtlZeroWords + 255) / 256), dim3(256), 0, 0, (uint32_t*)m->mem_,
-                               (uint32_t)kCtlZeroWords);
-            ok = hipGetLastError() == hipSuccess;
+        // The allocation passes the mapping check before its handle exists (MultiGpu::probe): an allocation
+        // that fails it -- r06: one that reused the range of a freed uncached allocation -- is kept (so its
+        // range is not handed out again) and another is made; connect checks the peers' mappings the same way
+        for (int attempt = 0; ok; ++attempt) {
+            hipError_t ae = m->memKind_ == 2u ? hipMalloc((void**)&m->mem_, m->memBytes_)
+                                              : hipExtMallocWithFlags((void**)&m->mem_, m->memBytes_,
+                                                                      m->memKind_ == 1u ? hipDeviceMallocUncached
+                                                                                        : hipDeviceMallocFinegrained);
+            ok = ae == hipSuccess && (!getenv("GSM_MG_POISON") || hipMemset(m->mem_, 0xAB, m->memBytes_) == hipSuccess) &&
+                 hipDeviceSynchronize() == hipSuccess;
+            if (ok) {  // the control words: write-through zeros, not a cached memset (k_mg_zero_ctl)
+                (void)hipGetLastError();  // (only this launch's error counts below)
+                hipLaunchKernelGGL(k_mg_zero_ctl, dim3((kCtlZeroWords + 255) / 256), dim3(256), 0, 0, (uint32_t*)m->mem_,
+                                   (uint32_t)kCtlZeroWords);
+                ok = hipGetLastError() == hipSuccess && hipDeviceSynchronize() == hipSuccess;
+            }
+            if (!ok) break;
+            const gsm_status pst = m->probe(&m->mem_, &m->memBytes_, 1, "gsm_multigpu_prepare");
+            if (pst == GSM_OK) break;
+            if (pst != GSM_ERR_DEVICE_NOT_AVAILABLE || attempt + 1 >= kAllocAttempts) {
+                ok = false;
+                failSt = pst;
+                break;
+            }
+            fprintf(stderr, "gsm_multigpu_prepare: rank %d: exchange allocation %p (%zu B) held back, allocating another\n",
+                    rank, (void*)m->mem_, m->memBytes_);
+            m->heldBack_.push_back(m->mem_);
+            m->mem_ = nullptr;
+            ++m->heldBackCount_;
         }
     }
     if (ok) ok = hipDeviceSynchronize() == hipSuccess;
@@ -549,7 +579,7 @@ gsm_status MultiGpu::prepare(GlobalRenderer* r, int rank, int world, const gsm_m
     if (!ok) {
         (void)hipGetLastError();
         delete m;
-        return GSM_ERR_FAILED_TO_ALLOCATE_BUFFER;
+        return failSt;
     }
     h.magic = kHandleMagic;
     h.version = kHandleVersion;
@@ -632,7 +662,7 @@ gsm_status MultiGpu::connect(const void* all) {
         recs_.cap[p] = h.capacity;
     }
     // every mapping this rank will store into or poll, checked before the first frame relies on it
-    const gsm_status pst = probe(base, bytes);
+    const gsm_status pst = probe(base, bytes, world_, "gsm_multigpu_connect");
     if (pst != GSM_OK) return pst;
     frame0_ = base[0] + hs[0].frameOff;
     depth0_ = base[0] + hs[0].depthOff;
@@ -641,26 +671,27 @@ gsm_status MultiGpu::connect(const void* all) {
     return GSM_OK;
 }
 
-// Connect-time check of the mappings (r06).  r05's diagnosis: the first frame
-// whose exchange allocation reused the address range of a freed *uncached* allocation lost flag stores
-// (every wait of that frame timed out) or read wrong record words, while counts and records stored into the
-// same pages were right and every later frame was clean -- state of the old mapping served the first
-// accesses of the new one.  Before the first frame, this rank makes exactly those accesses: one word per 4
-// KiB page of every mapping (own and peers', this rank's own word of each page), twice -- stored with the
-// flags' store form by one set of workgroups, polled with the barrier's load form by another (each word read
-// on another CU / XCD than the one that stored it, a bounded spin of 50 ms), and the control page's word
-// compared through the host -- so the frame's first stores and polls no longer meet that state, and a
-// mapping that still does not show a stored word refuses the connect (GSM_ERR_DEVICE_NOT_AVAILABLE) instead
-// of a frame timing out.
-gsm_status MultiGpu::probe(char* const* base, const size_t* bytes) {
+// The mapping check (r06).  r05: the first frame whose exchange allocation
+// reused the address range of a freed *uncached* allocation lost flag stores (every wait of that frame timed
+// out) or read wrong record words.  r06 (profiles/r06_mg_uc_reuse.log): on such a range, words stored by
+// some workgroups are not seen by others nor by the host -- the accesses of different CUs / XCDs and of the
+// host go to different memory, as through stale translations of the freed range.  So before a frame relies
+// on a mapping, this rank makes the frame's own accesses to one word of every 4 KiB page of it: stored with
+// the flags' write-through store from all eight XCDs and polled across XCDs with the barrier's load (a
+// bounded spin of 50 ms), then stored with the gathered pixels' plain stores and release and read back by
+// the host -- twice.  GSM_OK, or GSM_ERR_DEVICE_NOT_AVAILABLE with the evidence on stderr (`who`).
+gsm_status MultiGpu::probe(char* const* base, const size_t* bytes, int n, const char* who) {
     ProbeMaps maps{};
     uint32_t total = 0;
-    for (int p = 0; p < world_; ++p) {
+    for (int p = 0; p < n; ++p) {
         maps.base[p] = (uint32_t*)base[p];
         maps.pages[p] = (uint32_t)((bytes[p] + 4095) / 4096);
         total += maps.pages[p];
     }
-    maps.n = (uint32_t)world_;
+    maps.n = (uint32_t)n;
+    // an error left by an earlier call of the process (another library's, or the caller's) is not this
+    // check's: only the calls below decide (r06: a failed call of the reuse test's own once read as a refusal)
+    (void)hipGetLastError();
     uint32_t* fails = nullptr;
     hipStream_t s = nullptr;
     if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess || hipMalloc(&fails, 4) != hipSuccess ||
@@ -670,33 +701,28 @@ gsm_status MultiGpu::probe(char* const* base, const size_t* bytes) {
         (void)hipGetLastError();
         return GSM_ERR_FAILED_TO_ALLOCATE_BUFFER;
     }
-    const uint32_t grid = std::min<uint32_t>(2048u, (total + 63u) / 64u);
-    const uint32_t gridPlain = 8u * std::min<uint32_t>(512u, (total + 63u) / 64u);
+    const uint32_t grid = 8u * std::min<uint32_t>(512u, (total + 63u) / 64u);
     const unsigned long long spin = 50ull * wallKHz_;
     uint32_t maxPages = 0;
-    for (int p = 0; p < world_; ++p) maxPages = std::max(maxPages, maps.pages[p]);
+    for (int p = 0; p < n; ++p) maxPages = std::max(maxPages, maps.pages[p]);
     std::vector<uint32_t> host((size_t)maxPages * 8);
     bool ok = true;
-    uint32_t badPlain = 0, firstMap = 0, firstPage = 0, firstGot = 0, firstWant = 0;
+    uint32_t nf = 0, badPlain = 0, firstMap = 0, firstPage = 0, firstGot = 0, firstWant = 0;
     for (uint32_t round = 0; round < 2 && ok; ++round) {
         // (a) the counts' / records' / flags' forms: write-through stores, polled with system-coherent loads
-        //     by other workgroups
-        const uint32_t value = 0x5EED0000u | ((uint32_t)rank_ << 8) | (round + 1u);
-        const uint32_t rotStore = round * (total / 3u), rotCheck = rotStore + total / 2u + 64u;
-        hipLaunchKernelGGL(k_mg_probe, dim3(grid), dim3(64), 0, s, maps, total, (uint32_t)rank_, value,
-                           rotStore % total, 0, fails, spin);
-        hipLaunchKernelGGL(k_mg_probe, dim3(grid), dim3(64), 0, s, maps, total, (uint32_t)rank_, value,
-                           rotCheck % total, 1, fails, spin);
-        uint32_t nf = 1;
+        //     by workgroups of other XCDs
+        const uint32_t value = 0x5EED0000u | ((uint32_t)rank_ << 8) | ((round + 1u) << 4);
+        hipLaunchKernelGGL(k_mg_probe, dim3(grid), dim3(64), 0, s, maps, total, (uint32_t)rank_, value, 0, fails, spin);
+        hipLaunchKernelGGL(k_mg_probe, dim3(grid), dim3(64), 0, s, maps, total, (uint32_t)rank_, value, 1, fails, spin);
+        nf = 1;
         ok = hipMemcpyAsync(&nf, fails, 4, hipMemcpyDeviceToHost, s) == hipSuccess && hipStreamSynchronize(s) == hipSuccess &&
              nf == 0;
         // (b) the gathered pixels' form: plain stores from every XCD released at the workgroups' exit, read
-        //     back by the host (one 32-B run per page) -- r06's reuse test saw such stores stay in an L2 past
-        //     the release on a range last mapped uncached (the host read the connect's own probe words)
+        //     back by the host (one 32-B run per page)
         const uint32_t pv = 0x9A5E0000u | ((uint32_t)rank_ << 8) | ((round + 1u) << 4);
-        hipLaunchKernelGGL(k_mg_probe_plain, dim3(gridPlain), dim3(64), 0, s, maps, total, (uint32_t)rank_, pv);
+        hipLaunchKernelGGL(k_mg_probe_plain, dim3(grid), dim3(64), 0, s, maps, total, (uint32_t)rank_, pv);
         ok = ok && hipStreamSynchronize(s) == hipSuccess;
-        for (int p = 0; ok && p < world_; ++p) {
+        for (int p = 0; ok && p < n; ++p) {
             const char* b = (const char*)maps.base[p];
             const size_t off = 32u * (uint32_t)rank_;
             ok = hipMemcpy(host.data(), b + kProbeWord * 4 + off, 32, hipMemcpyDeviceToHost) == hipSuccess;
@@ -714,20 +740,22 @@ gsm_status MultiGpu::probe(char* const* base, const size_t* bytes) {
                 }
             ok = ok && badPlain == 0;
         }
-        if (!ok) {  // (the refusal's evidence, on stderr)
+        if (!ok)  // (the evidence, on stderr)
             fprintf(stderr,
-                    "gsm_multigpu_connect: rank %d refuses its mappings (round %u): %u polled words not seen in 50 ms, "
-                    "%u plain-stored words wrong through the host (first: mapping %u page %u holds 0x%08x, stored 0x%08x)\n",
-                    rank_, round, nf, badPlain, firstMap, firstPage, firstGot, firstWant);
-        }
+                    "%s: rank %d: mapping check failed (round %u): %u polled words not seen in 50 ms, %u plain-stored "
+                    "words wrong through the host (first: mapping %u page %u holds 0x%08x, stored 0x%08x)\n",
+                    who, rank_, round, nf, badPlain, firstMap, firstPage, firstGot, firstWant);
     }
+    const hipError_t launchErr = hipGetLastError();  // (the probe kernels' launches)
     hipFree(fails);
     hipStreamDestroy(s);
-    if (hipGetLastError() != hipSuccess) ok = false;
+    if (launchErr != hipSuccess) {
+        fprintf(stderr, "%s: rank %d: mapping check failed to run (%s)\n", who, rank_, hipGetErrorString(launchErr));
+        ok = false;
+    }
     return ok ? GSM_OK : GSM_ERR_DEVICE_NOT_AVAILABLE;
 }
 
-// Everything any phase of this rank's frame could refuse, before anything is enqueued.
 gsm_status MultiGpu::check(const gsm_gaussian_input& in, uint32_t width, uint32_t height, void* color,
                            size_t colorPitch, void* depth, size_t depthPitch, void* gatherColor, Targets* t) const {
     // which barrier steps the frame has (gather, and so barrier 2) follows from the arguments alone:
@@ -819,6 +847,7 @@ gsm_status MultiGpu::finishFrame(hipStream_t s) {
 gsm_status MultiGpu::run(int p, hipStream_t s, const gsm_gaussian_input* in, const gsm_camera_params* cam,
                          uint32_t width, uint32_t height, Targets t, size_t colorPitch, void* depth,
                          size_t depthPitch, void* gatherColor) {
+    (void)hipGetLastError();  // (an error left by an earlier call of the process is not this call's: the launches below are checked)
     nextPhase_ = (p + 1) & 3;
     const uint32_t world = (uint32_t)world_, rank = (uint32_t)rank_;
     const uint32_t par = par_;  // the frame's parity: count matrix, receive buffer, schedule set
@@ -989,6 +1018,7 @@ bool MultiGpu::slabPixelRows(uint32_t q, uint32_t k, uint32_t height, uint32_t* 
 gsm_status MultiGpu::runRccl(int p, hipStream_t s, const gsm_gaussian_input* in, const gsm_camera_params* cam,
                              uint32_t width, uint32_t height, Targets t, size_t colorPitch, void* depth,
                              size_t depthPitch, void* gatherColor) {
+    (void)hipGetLastError();  // (an error left by an earlier call of the process is not this call's: the launches below are checked)
     nextPhase_ = (p + 1) & 3;
     const Rccl& R = rccl();
     const ncclComm_t comm = (ncclComm_t)comm_;

@@ -30,17 +30,22 @@ HIP_UNCACHED = 0x3  # hipDeviceMallocUncached
 
 
 def raw_uncached(sizes):
-    """Allocate, write and free uncached device memory of the given sizes (their ranges become free)."""
-    ptrs = []
+    """Allocate, write and free uncached device memory of the given sizes (their ranges become free).
+    Returns the HIP status of every allocation (and leaves no error behind for the next HIP call)."""
+    ptrs, st = [], []
     for b in sizes:
         p = C.c_void_p()
-        if HIP.hipExtMallocWithFlags(C.byref(p), C.c_size_t(b), C.c_uint(HIP_UNCACHED)) == 0:
+        rc = HIP.hipExtMallocWithFlags(C.byref(p), C.c_size_t(b), C.c_uint(HIP_UNCACHED))
+        st.append(int(rc))
+        if rc == 0:
             HIP.hipMemset(p, 0x5A, C.c_size_t(b))
             ptrs.append(p)
     HIP.hipDeviceSynchronize()
     for p in ptrs:
         HIP.hipFree(p)
     HIP.hipDeviceSynchronize()
+    HIP.hipGetLastError()
+    return st
 
 
 def frames(world, n, w, h, sh, prec, cams, inp, opts, kind, render=True):
@@ -50,15 +55,16 @@ def frames(world, n, w, h, sh, prec, cams, inp, opts, kind, render=True):
         os.environ.pop("GSM_MG_MEM", None)
     cfg = gsm.RendererConfig(max_gaussians=n, max_width=w, max_height=h, precision=prec, gaussian_color_space=0)
     rends = [gsm.GlobalRenderer(device=0, config=cfg) for _ in range(world)]
-    pre = [gsm.MultiGpuRenderer.prepare(r, k, world, opts) for k, r in enumerate(rends)]
     out = {"refused": False, "timeouts": 0, "pix": []}
-    mgs = []
-    try:
+    pre, mgs = [], []
+    try:  # prepare checks (and, failing, replaces) the rank's own allocation; connect checks every mapping
+        for k, r in enumerate(rends):
+            pre.append(gsm.MultiGpuRenderer.prepare(r, k, world, opts))
         mgs = [m.connect_handles([hd for _, hd in pre]) for m, _ in pre]
     except gsm.RendererError as e:
         if e.status != gsm.Status.DEVICE_NOT_AVAILABLE:
             raise
-        out["refused"] = True
+        out["refused"] = "connect" if len(pre) == world else "prepare"
         for m, _ in pre:
             m.close()
     if mgs and not render:
@@ -101,11 +107,12 @@ def main():
         for rep in range(2):
             uc = frames(world, n, w, h, sh, prec, cams, inp, opts, "uncached", render=False)
             rec = 2 * ((n * 48 + 4095) // 4096 * 4096) + 4096
-            raw_uncached([rec] * world + [w * h * 8, w * h * 2])
+            alloc = raw_uncached([rec] * world + [w * h * 8, w * h * 2])
             fine = frames(world, n, w, h, sh, prec, cams, inp, opts, "fine")
             bad = [int(np.count_nonzero(np.any(p != r, axis=(1, 2)))) for p, r in zip(fine["pix"], refs)]
             c = {"case": [world, n, w, h, prec, rep], "refused": fine["refused"], "timeouts": fine["timeouts"],
-                 "bad_rows": bad, "uncached_refused": uc["refused"], "uncached_timeouts": uc["timeouts"]}
+                 "bad_rows": bad, "uncached_refused": uc["refused"], "uncached_timeouts": uc["timeouts"],
+                 "raw_alloc_status": alloc}
             detail = []
             for p, r in zip(fine["pix"], refs):  # where and what the wrong pixels are
                 rows = np.nonzero(np.any(p != r, axis=(1, 2)))[0]

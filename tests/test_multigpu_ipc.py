@@ -438,8 +438,10 @@ def test_fine_exchange_after_freed_uncached_allocations(tmp_path):
     replays that sequence twice -- virtual-rank frames over uncached exchange memory (the A/B kind) plus raw
     uncached allocations of the same sizes, all freed, then a fine-grained exchange of the same shape -- and
     the fine-grained exchange must either render both frames bit-exact with zero barrier timeouts, or refuse
-    at connect (the mapping check, GSM_ERR_DEVICE_NOT_AVAILABLE).  The barrier timeout is 2 s, so a lost flag
-    costs seconds, not a hang."""
+    (the mapping check, GSM_ERR_DEVICE_NOT_AVAILABLE, with its evidence on stderr).  r06: gsm_multigpu_prepare
+    checks each rank's own allocation and replaces one that fails (held back until destroy), so the
+    virtual-rank exchange renders instead of refusing.  The barrier timeout is 2 s, so a lost flag costs
+    seconds, not a hang."""
     out = tmp_path / "uc.json"
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
     env.pop("GSM_MG_MEM", None)
@@ -448,5 +450,11 @@ def test_fine_exchange_after_freed_uncached_allocations(tmp_path):
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     res = json.loads(out.read_text())
     assert res["cases"], res
+    refusals = r.stderr.count("mapping check failed (")
     for c in res["cases"]:
         assert c["refused"] or (c["timeouts"] == 0 and c["bad_rows"] == [0, 0]), c
+    # a refusal is the mapping check's, with its evidence on stderr -- not an error left by another call
+    # (r06: an error of the child's own raw allocations once read as one)
+    assert refusals >= sum(1 for c in res["cases"] if c["refused"]), (res, r.stderr[-3000:])
+    assert "mapping check failed to run" not in r.stderr, r.stderr[-3000:]
+    print(json.dumps(res["cases"]), "held back:", r.stderr.count("held back"))

@@ -125,7 +125,7 @@ gsm_status GlobalRenderer::create(const gsm_renderer_config& cfg, int hipDevice,
     GSM_ALLOC(A.halfVals[1], cap * sizeof(uint32_t));
     GSM_ALLOC(A.halfCount, (size_t)r->tileCount_ * 2 * sizeof(uint32_t));
     GSM_ALLOC(A.expTable, 65536 * sizeof(uint16_t));
-    GSM_ALLOC(A.sincosTable, 65536 * sizeof(float2));
+    GSM_ALLOC(A.sincosTable, (kSincosEntries + 256) * sizeof(float2));
 #undef GSM_ALLOC
     if (st != GSM_OK) {
         delete r;
@@ -135,10 +135,15 @@ gsm_status GlobalRenderer::create(const gsm_renderer_config& cfg, int hipDevice,
     // numeric-contract tables (gsm_detmath.h)
     std::vector<uint16_t> expt(65536);
     for (uint32_t i = 0; i < 65536; ++i) expt[i] = blend_exp_table_entry((uint16_t)i);
-    std::vector<float2> sc(65536);
-    for (uint32_t i = 0; i < 65536; ++i) det_sincos_table_entry(i, &sc[i].x, &sc[i].y);
+    std::vector<float2> sc(kSincosEntries + 256);
+    for (uint32_t i = 0; i < kSincosEntries; ++i) det_sincos_table_entry(i, &sc[i].x, &sc[i].y);
+    for (uint32_t c = 0; c < 256; ++c) {
+        uint32_t d;
+        det_byte_lut_entry(c, &sc[kSincosEntries + c].x, &d);
+        std::memcpy(&sc[kSincosEntries + c].y, &d, 4);  // (bits, not a value)
+    }
     if (hipMemcpy(A.expTable, expt.data(), 65536 * sizeof(uint16_t), hipMemcpyHostToDevice) != hipSuccess ||
-        hipMemcpy(A.sincosTable, sc.data(), 65536 * sizeof(float2), hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(A.sincosTable, sc.data(), sc.size() * sizeof(float2), hipMemcpyHostToDevice) != hipSuccess ||
         hipMemset(A.header, 0, sizeof(TileAssignmentHeader)) != hipSuccess ||
         hipMemset(A.tileStart, 0, ((size_t)r->tileCount_ + 1) * sizeof(uint32_t)) != hipSuccess ||
         hipMemset(A.unitCost, 0, (size_t)r->tileCount_ * 4 * sizeof(uint16_t)) != hipSuccess ||
@@ -279,6 +284,7 @@ gsm_status GlobalRenderer::preparePartition(const gsm_gaussian_input& in, const 
                                             const uint32_t* slabRows, uint32_t numSlabs, bool needSend,
                                             const void* send, const uint32_t* sendCounts, PartitionFrame* f,
                                             bool interleave) {
+    (void)hipGetLastError();  // (an error left by an earlier call of the process is not this call's: the launches below are checked)
     if ((uint64_t)first + count > in.gaussian_count || count > maxGaussians_)
         return GSM_ERR_INVALID_GAUSSIAN_COUNT;
     if (width == 0 || height == 0 || width > maxWidth_ || height > maxHeight_)
@@ -380,6 +386,7 @@ gsm_status GlobalRenderer::partitionCounts(hipStream_t s, const gsm_gaussian_inp
 
 gsm_status GlobalRenderer::partitionPush(hipStream_t s, uint32_t world, uint32_t rank, const uint32_t* counts,
                                          const SlabPeers& peers, uint32_t* recvCount, const MgArrive& arrive) {
+    (void)hipGetLastError();  // (an error left by an earlier call of the process is not this call's: the launches below are checked)
     ProjectArgs a;
     std::memset(&a, 0, sizeof(a));
     a.count = partCount_;
@@ -411,6 +418,7 @@ gsm_status GlobalRenderer::runFrame(hipStream_t s, const ProjectArgs& a, uint32_
                                     void* color, size_t colorPitch, void* depth, size_t depthPitch,
                                     Front&& front, const uint32_t* devCount, bool preOrdered,
                                     const MgArrive* blendArrive) {
+    (void)hipGetLastError();  // (an error left by an earlier call of the process is not this call's: the launches below are checked)
     const bool prof = (profiling_ & 1) != 0;         // every stage bracketed by events
     // only the blend (2 events per frame), on every frame or every period-th (bits 8-15)
     const uint32_t period = ((uint32_t)profiling_ >> 8) & 0xFFu;

@@ -23,6 +23,7 @@
 #define GSM_PROJ_STOP 0
 #endif
 
+
 namespace gsm {
 
 // ---------------------------------------------------------------------------
@@ -1071,7 +1072,13 @@ __global__ __launch_bounds__(kProjectBlock) void k_scatter(
         }
     }
     if (blockIdx.x * kProjectBlock >= n) return;  // (uniform; the scan stopped at the count too)
-    uint32_t c = (gid < n) ? counts[gid] : 0u;  // (in flight while the block counts are added up)
+    // The scatter's once-read inputs (counts, bounds, the records' band half, masks) are streaming loads
+    // (nt): they no longer displace the keys and values this kernel writes from the 256 MiB infinity
+    // cache, which the first tile pass reads next -- config 3: that pass 64.4-66.1 -> 59.6-61.3 us, nothing
+    // else slower (r06, VERDICT r05 item 4: profiles/r06_nt_loads_ab.txt)
+    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+#define GSM_SLD(p) __builtin_nontemporal_load(p)
+    uint32_t c = (gid < n) ? GSM_SLD(counts + gid) : 0u;  // (in flight while the block counts are added up)
     uint32_t base;
     if (fusedScan) {
         const uint64_t before = blockIdx.x ? block_sum_prefix(blockOffsets, blockIdx.x, lds64) : 0ull;
@@ -1088,8 +1095,10 @@ __global__ __launch_bounds__(kProjectBlock) void k_scatter(
     uint32_t mask = 0;
     float2 band = make_float2(0.0f, -1.0f);
     if (c != 0) {
-        r = bounds[gid];
-        const uint4 r1 = ((const uint4*)(rec + gid))[1];  // the band k_project left in the padding
+        const unsigned long long rb = GSM_SLD((const unsigned long long*)(bounds + gid));
+        r = __builtin_bit_cast(short4, rb);
+        const u32x4 r1v = GSM_SLD((const u32x4*)(rec + gid) + 1);  // the band k_project left in the padding
+        const uint4 r1 = make_uint4(r1v.x, r1v.y, r1v.z, r1v.w);
         band = make_float2(__uint_as_float(r1.y), __uint_as_float(r1.z));
         // the key's depth: the fp16 depth bits of the blend record (b = colB | depth << 16, the same
         // bits as GaussianRenderData.depth), so the scatter reads one 16-B slot per gaussian
@@ -1099,7 +1108,7 @@ __global__ __launch_bounds__(kProjectBlock) void k_scatter(
         rows_within(rows_of(P), (int)r.z, (int)r.w, &ty0, &ty1);
         const int rw = (int)r.y - (int)r.x + 1;
         large = (ty1 - ty0 + 1) * rw > kMaskTiles;
-        if (!large) mask = masks[gid];
+        if (!large) mask = GSM_SLD(masks + gid);
         sRect[threadIdx.x] = ((uint32_t)(int)r.x & 0xFFFFu) | ((uint32_t)rw << 16);
         // 2^16 / rw is a power of two (v_rcp_f32 exact) or >= 1/rw >= 1/32 away from an integer, and the
         // 1-ulp reciprocal moves it by <= 2^16 * 2^-23 < 0.008: the ceiling is exact.  With inv = ceil(2^16

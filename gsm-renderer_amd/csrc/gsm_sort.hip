@@ -230,7 +230,7 @@ __global__ __launch_bounds__(kRadixBlock) void k_radix_downsweep(
     __shared__ uint32_t part[kWaves];
 
     // STARTS: the chunk's keys per digit before a bucket start (1 << BITS words: with the arrays
-    // above, 4 blocks per CU still fit for BITS <= 7)
+    // above, 4 blocks per CU still fit for BITS <= 7 -- radix_pass limits every narrow downsweep to 3)
     __shared__ uint32_t sCntB[1u << BITS];
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint32_t n = *nPtr;
@@ -804,15 +804,19 @@ static void radix_pass(uint32_t* kin, uint32_t* vin, uint32_t* kout, uint32_t* v
     uint32_t* super = superSet >= 0 ? hist + (size_t)superSet * kSuperSetWords : nullptr;
     uint32_t* superClear = superSet >= 0 ? hist + (size_t)(superSet ^ 1) * kSuperSetWords : nullptr;
     hist += kSuperWords;
+    // 1 KiB of dynamic LDS on the downsweeps without tile starts: > 40 KiB a block, 3 blocks per CU like
+    // the STARTS pass -- the first 4K tile pass at 4 blocks per CU measured 2.5 us slower (64.4-65.9
+    // against 62.2-62.4 us; 1080p unchanged; r06, profiles/r06_sort_occupancy_ab.txt)
+    const uint32_t ldsPad = starts ? 0u : 1024u;
 #define GSM_RADIX_PASS(B, S)                                                                                \
     hipLaunchKernelGGL(k_radix_upsweep<B>, dim3(grid), dim3(kRadixBlock), 0, s, kin, nPtr, shift, hist, super, \
                        superClear);                                                                         \
     if (!super) hipLaunchKernelGGL(k_radix_scan, dim3(1u << B), dim3(256), 0, s, hist, grid, binTotals);  \
     if (ballot)                                                                                             \
-        hipLaunchKernelGGL((k_radix_downsweep<B, true, S>), dim3(grid), dim3(kRadixBlock), 0, s, kin, vin, kout, \
+        hipLaunchKernelGGL((k_radix_downsweep<B, true, S>), dim3(grid), dim3(kRadixBlock), ldsPad, s, kin, vin, kout, \
                            vout, nPtr, shift, hist, binTotals, t, super);                                   \
     else                                                                                                    \
-        hipLaunchKernelGGL((k_radix_downsweep<B, false, S>), dim3(grid), dim3(kRadixBlock), 0, s, kin, vin, kout, \
+        hipLaunchKernelGGL((k_radix_downsweep<B, false, S>), dim3(grid), dim3(kRadixBlock), ldsPad, s, kin, vin, kout, \
                            vout, nPtr, shift, hist, binTotals, t, super)
 #define GSM_RADIX_BITS(S)                    \
     switch (bits) {                          \

@@ -7,7 +7,8 @@ crossing xGMI.  HIP events bracket each rank's phase; the renderers' stage event
 render (records in, scan, scatter, sort, gap, blend).
 
 Prints JSON: per-phase times per rank, and device_frame_ms = max phase 0 + max phase 1 + max phase 2
-(+ phase 3), the device part of one N-GPU frame without the fabric.
+(+ phase 3), the device part of one N-GPU frame without the fabric.  Each timed frame is enqueued while
+the GPU spins (--hold-cycles), so no event pair times the host's enqueue of a phase.
 
 usage: python tools/exp_virtual_ranks.py [--config cfg3_5m_sh3_4k_f16] [--world 8] [--frames 5]
 """
@@ -33,6 +34,8 @@ def main():
     ap.add_argument("--trace-rank", type=int, default=-1,
                     help="per-unit blend trace of this rank's slab (profiling bit 2) -> gpurun_out/vr_trace_*.npz")
     ap.add_argument("--depth", type=int, default=1, help="gather the r16f depth frame too (product default)")
+    ap.add_argument("--hold-cycles", type=float, default=6e6,
+                    help="spin the GPU this many cycles (~2.5 ms) before each timed frame while the host enqueues it")
     ap.add_argument("--interval", type=int, default=0,
                     help="also time N frames issued back to back (no events between phases): the group's frame "
                          "interval; run with GSM_MG_PIPELINE=1 in the environment for the pipelined frame")
@@ -61,6 +64,12 @@ def main():
     ph = np.zeros((a.frames, 4, W))
 
     def frame(record):
+        # (r06) the GPU waits behind a short spin while the host enqueues the frame's 4 x W phases: each
+        # event pair then brackets device work only.  Before, rank 0's phase 0 began on an idle GPU, so
+        # its pair also timed the host's enqueue of that phase (~35 us: phase 0 0.085 ms for rank 0
+        # against 0.049-0.050 for the others, profiles/r06_virtual_ranks_kernel_trace.txt)
+        if record:
+            torch.cuda._sleep(int(a.hold_cycles))
         marks = []
         for p in range(4):
             for k, m in enumerate(mgs):

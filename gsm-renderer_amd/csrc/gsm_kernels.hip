@@ -12,16 +12,6 @@
 #include "gsm_internal.h"
 #include "gsm_types.h"
 
-// Stage attribution of k_project (A/B builds only, tools/gpu_proj_stages.sh): GSM_PROJ_STOP = k ends the
-// projection after stage k (1 loads + view / clip + the early culls, 2 + the 3D covariance, 3 + the 2D
-// covariance and its stabilisation, 4 + theta / sigmas, 5 + the radius / ink / screen culls and the OBB,
-// 6 + the SH colour, 7 the whole projection without the tile tests, 8 everything but the skip band); the
-// stage's values are folded into
-// the bounds word so nothing is dropped by the compiler, and every later stage (tile tests, records) is
-// skipped.  0 (default): the product kernel.
-#ifndef GSM_PROJ_STOP
-#define GSM_PROJ_STOP 0
-#endif
 
 
 namespace gsm {
@@ -59,19 +49,6 @@ __device__ __forceinline__ void fill_byte_lut(ByteLut& L, const float2* __restri
     __syncthreads();
 }
 
-#if GSM_PROJ_STOP
-__device__ __forceinline__ short4 stop_fold(float a, float b = 0.f, float c = 0.f, float d = 0.f) {
-    const uint32_t h = __float_as_uint(a) ^ (__float_as_uint(b) * 3u) ^ (__float_as_uint(c) * 5u) ^ (__float_as_uint(d) * 7u);
-    return make_short4((short)(h & 0x7FFF), (short)-1, (short)(h >> 17), (short)-1);
-}
-#define GSM_STOP_AT(k, ...)                                       \
-    if constexpr (GSM_PROJ_STOP == k) {                           \
-        if (vis) o.bounds = stop_fold(__VA_ARGS__);               \
-        return o;                                                 \
-    }
-#else
-#define GSM_STOP_AT(k, ...)
-#endif
 
 template <bool HALF, int DEG>
 __device__ __forceinline__ ProjOut project_gaussian(const void* __restrict__ world,
@@ -126,20 +103,16 @@ __device__ __forceinline__ ProjOut project_gaussian(const void* __restrict__ wor
             sy = ((ndcy + 1.0f) * cam.height - 1.0f) * 0.5f;
             if (opacity < P.bin.alphaThreshold) vis = false;
         }
-        GSM_STOP_AT(1, sx, sy, clip[3], scale[0] + rot[0])
         Cov2 cov;
         float theta = 0.f, s1 = 0.f, s2 = 0.f;
         if (vis) {
             // buildCovariance3D, projectCovariance2D, stabilizeCovariance2D, covarianceToThetaSigmas
             // (GaussianShared.h:289-324, 326-375, 655-714, 446-488; gsm_device.h)
             const M3 C3 = build_cov3d(scale, rot);
-            GSM_STOP_AT(2, C3.m[0][0] + C3.m[1][1], C3.m[2][2] + C3.m[0][1], C3.m[0][2] + C3.m[1][2], sx + sy)
             cov = project_cov2d(C3, vp, cam.view, P.limX, P.limY, P.focalX, P.focalY);
             cov = stabilize_cov2d(cov, P.maxEig);
-            GSM_STOP_AT(3, cov.a, cov.b, cov.d, sx + sy)
             if (!theta_sigmas(cov, &theta, &s1, &s2)) vis = false;
         }
-        GSM_STOP_AT(4, theta, s1, s2, sx + sy)
         if (vis) {
             float radius = 3.0f * __builtin_fmaxf(s1, s2);
             if (radius < 0.5f) vis = false;  // cullByRadius
@@ -159,7 +132,6 @@ __device__ __forceinline__ ProjOut project_gaussian(const void* __restrict__ wor
             if (sx + ex < 0.0f || sx - ex > cam.width || sy + ey < 0.0f || sy - ey > cam.height)
                 vis = false;
         }
-        GSM_STOP_AT(5, ex, ey, theta + s1, sx + sy)
         if (vis) {
             float col[3];
             sh_color<HALF, DEG>(harm, gid, pos, cam.cameraCenter, cam.shComponents, col);
@@ -171,7 +143,6 @@ __device__ __forceinline__ ProjOut project_gaussian(const void* __restrict__ wor
                 col[1] = srgb_to_linear(col[1]);
                 col[2] = srgb_to_linear(col[2]);
             }
-            GSM_STOP_AT(6, col[0], col[1], col[2], ex + ey + theta + s1 + s2)
             // pack GaussianRenderData (GlobalShaders.metal:106-117), packThetaPi (GaussianShared.h:434-440)
             float th = fmod_pi(theta);
             if (th < 0.0f) th = th + kPiF;
@@ -230,9 +201,6 @@ __device__ __forceinline__ ProjOut project_gaussian(const void* __restrict__ wor
             const float alpha = (float)cO;
             o.countable = alpha >= 1e-4f && minTX <= maxTX && minTY <= maxTY;
             o.w = o.countable ? lut.level[cO] : 0.0f;  // = 2 computePower(alpha)
-#if GSM_PROJ_STOP == 7
-            o.countable = o.w == 12345.0f;  // (never) keeps the level alive; no tile tests
-#endif
         }
     }
     return o;
@@ -418,11 +386,7 @@ __global__ __launch_bounds__(kProjectBlock) void k_project(
         const uint32_t mask = sMask[tid];
         ntiles = (uint32_t)__builtin_popcount(mask) + sMore[tid];
         masks[gid] = mask;
-#if GSM_PROJ_STOP == 8  // (attribution: the tile tests without the skip band)
-        const float2 band = make_float2(0.f, -1.f);
-#else
         const float2 band = ntiles ? band_of(o.ra, o.bounds, rows_of(P)) : make_float2(0.f, -1.f);
-#endif
         uint4* rp = (uint4*)(outRec + gid);
         rp[0] = make_uint4(o.ra.x, o.ra.y, o.ra.z, o.ra.w);
         rp[1] = make_uint4(o.rb, __float_as_uint(band.x), __float_as_uint(band.y), 0u);

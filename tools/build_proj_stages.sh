@@ -3,6 +3,8 @@
 # objects: only gsm_kernels.hip is recompiled per variant.
 set -eu
 cd "$(dirname "$0")/../gsm-renderer_amd"
+# the stop macros live in a patch (not in the product): git apply tools/exp/proj_stop.patch first
+grep -q GSM_PROJ_STOP csrc/gsm_kernels.hip || { echo "apply tools/exp/proj_stop.patch first (git apply)"; exit 1; }
 make -s -j8
 for k in ${STOPS:-1 2 3 4 5 6 7 8}; do
   rm -rf build_ps$k lib_ps$k; mkdir -p build_ps$k

@@ -50,11 +50,6 @@ __device__ __forceinline__ h2 splat_hi(h2 v) { return h2{v.y, v.y}; }
 // The table index of a packed pair of quadratic forms: its fp16 bits.  (The far-field clamp and the
 // dead-lane columns that cut the gathers' bank conflicts, and the duplicate-read attribution build, are
 // kept as tools/exp/rejected_variants.patch: bit-exact, no faster)
-// GSM_BLEND_ZSTATS (statistics builds only): the trace's t[3] holds per unit the entries on which no
-// live pixel has a nonzero alpha and the sum over entries of the live pixels; t[0]'s top 16 bits ncomp
-#ifndef GSM_BLEND_ZSTATS
-#define GSM_BLEND_ZSTATS 0
-#endif
 __device__ __forceinline__ uint32_t tbl_bits(h2 p) {
     return as_u32(p);
 }
@@ -265,9 +260,6 @@ __global__ __launch_bounds__(NT) void k_blend_px(
         if (trace) tStart = __builtin_amdgcn_s_memrealtime();
         uint32_t nproc = 0;
         uint32_t ncomp = 0;  // entry at which the unit moved to one pair per lane (trace only)
-#if GSM_BLEND_ZSTATS
-        uint32_t zeroEntries = 0, alivePx = 0;  // (statistics build: entries no live pixel takes, live pixels)
-#endif
         uint32_t nextQ = 0;
         bool claimed = false;
         // claimMode 2: the walk this unit made last frame (before this frame's walk overwrites it)
@@ -397,9 +389,6 @@ __global__ __launch_bounds__(NT) void k_blend_px(
                         }
                     }
                     // stage 2: blend the current group
-#if GSM_BLEND_ZSTATS
-                    const uint32_t g1s = b0 + gi * U;
-#endif
 #pragma unroll
                     for (uint32_t k = 0; k < U; ++k) {
                         // group break (GlobalShaders.metal:1086-1088): max T of the 4x2 group
@@ -416,17 +405,6 @@ __global__ __launch_bounds__(NT) void k_blend_px(
                             gm = max(gm, o);
                         }
                         alive = alive && !(gm < thrBits);  // T >= 0: fp16 order == bit order
-#if GSM_BLEND_ZSTATS
-                        {
-                            uint32_t nz = 0;
-#pragma unroll
-                            for (int q = 0; q < P; ++q) nz |= as_u32(ac[k][q]);
-                            if (g1s + k < count) {
-                                zeroEntries += __ballot(alive && nz != 0) == 0 ? 1u : 0u;
-                                alivePx += (uint32_t)__popcll(__ballot(alive)) * (2u * P);
-                            }
-                        }
-#endif
                         const h2 rgv = as_h2(rgc[k]), bdv = as_h2(bdc[k]);
                         // a dead lane keeps T and C (alpha 0 would give the same bits: C + c*0 == C,
                         // T*1 == T): the updates run under an EXEC mask of the live lanes
@@ -594,12 +572,6 @@ __global__ __launch_bounds__(NT) void k_blend_px(
                         const uint32_t tb = as_u32(T1);
                         const uint32_t gm = quad_max_u32(max(tb & 0xFFFFu, tb >> 16));
                         alive1 = alive1 && !(gm < thrBits);
-#if GSM_BLEND_ZSTATS
-                        if (e + k < count) {
-                            zeroEntries += __ballot(alive1 && as_u32(ac1[k]) != 0) == 0 ? 1u : 0u;
-                            alivePx += (uint32_t)__popcll(__ballot(alive1)) * 2u;
-                        }
-#endif
                         if (alive1) {
                             const h2 rgv = as_h2(rgc1[k]), bdv = as_h2(bdc1[k]);
                             const h2 w = ac1[k] * T1;  // (GlobalShaders.metal:1137-1149)
@@ -652,11 +624,6 @@ __global__ __launch_bounds__(NT) void k_blend_px(
             t[1] = __builtin_amdgcn_s_memrealtime();
             t[2] = ((unsigned long long)count << 32) | nproc;
             const unsigned long long xcc = (unsigned long long)__builtin_amdgcn_s_getreg(20 | (3 << 11));  // XCC_ID
-#if GSM_BLEND_ZSTATS
-            t[0] = ((unsigned long long)ncomp << 48) | (tStart & 0xFFFFFFFFFFFFull);
-            t[3] = ((unsigned long long)alivePx << 32) | zeroEntries;
-            if (false)
-#endif
             t[3] = (xcc << 48) | ((unsigned long long)(ncomp & 0xFFFFu) << 32) |
                    (unsigned long long)__builtin_amdgcn_s_getreg(4 | (31 << 11));
         }

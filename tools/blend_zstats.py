@@ -1,4 +1,4 @@
-"""Walk statistics of the Global blend from a GSM_BLEND_ZSTATS=1 library build (the per-unit trace's
+"""(r06: the switch lives in tools/exp/blend_zstats.patch -- `git apply` it before that build.)  Walk statistics of the Global blend from a GSM_BLEND_ZSTATS=1 library build (the per-unit trace's
 t[3] = live pixels summed over entries << 32 | entries on which no live pixel has a nonzero alpha;
 t[0] >> 48 = the entry at which the unit compacted).  Prints, per camera angle, the walked entries,
 the all-zero entries and the live-pixel fraction of the walk's pixel slots.

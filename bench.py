@@ -180,7 +180,9 @@ def virtual_ranks_entry(world: int):
             "modelled_speedup_with_xgmi": (round(d["one_gpu_frame_ms"] / d["xgmi_model"]["modelled_frame_ms"], 3)
                                            if d.get("one_gpu_frame_ms") and d.get("xgmi_model") else None),
             "note": "each rank's phases run alone on this GPU (an upper bound for a rank's own GPU); the pushes "
-                    "and the gathered pixels stay local (no xGMI time); device_speedup = one-renderer frame / "
+                    "and the gathered pixels stay local (no xGMI time); each timed frame is enqueued while the GPU "
+                    "spins, so the per-phase event pairs time device work only (r06: before, rank 0's phase 0 also "
+                    "timed the host's enqueue, ~35 us); device_speedup = one-renderer frame / "
                     "per-rank device frame (one-frame latency); interval_*: the group's frame interval / world "
                     "for frames issued back to back under a moving camera, serial and pipelined (GSM_MG_PIPELINE=1)"}
 

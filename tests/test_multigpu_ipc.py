@@ -206,6 +206,23 @@ def test_config4_virtual_ranks_full_size(gsm, cuda, oracle):
     assert counts.sum() >= int(np.count_nonzero(ref["tile_counts"]))
 
 
+def test_virtual_ranks_over_poisoned_exchange_memory(gsm, cuda, oracle, monkeypatch):
+    """GSM_MG_POISON (the diagnosis switch of tools/exp/mg_uncached_diag.py): the exchange memory is filled
+    with 0xAB bytes at prepare, before the write-through zeroing of its control words.  Nothing of a frame may
+    read a word it did not write first: three virtual ranks, two views, bit-exact, no timeout."""
+    from gsm_amd import scenes
+    monkeypatch.setenv("GSM_MG_POISON", "1")
+    n, w, h, prec, sh = 30_000, 640, 360, 1, 16
+    cams = [scenes.make_camera(w, h), scenes.orbit_camera(w, h, 5.0)]
+    frames, _, timeouts, depths = _virtual_frame(gsm, cuda, 3, n, w, h, sh, prec, 91, cams,
+                                                 gsm.MultiGpuOptions(timeout_ms=5000))
+    assert timeouts == [0] * 3
+    world_np, harm_np, _ = scenes.gen_scene(n, w, h, sh, prec, seed=91)
+    for got, gd, cam in zip(frames, depths, cams):
+        ref = oracle.render(world_np, harm_np, sh, cam, w, h, max_gaussians=n)
+        assert np.array_equal(got, ref["color"]) and np.array_equal(gd, ref["depth"])
+
+
 def test_uncached_exchange_memory_is_refused(gsm, cuda, monkeypatch):
     """GSM_MG_MEM=uncached: refused at gsm_multigpu_prepare (GSM_ERR_UNSUPPORTED) -- uncached memory
     renders wrong virtual-rank slabs on MI355X even with write-through stores and system-coherent

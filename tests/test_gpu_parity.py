@@ -370,9 +370,9 @@ def test_kernel_shape_thresholds(gsm, cuda, oracle, w, h):
 
 @pytest.mark.parametrize("n", [64 * 256, 64 * 256 + 1, 8192 * 256, 8192 * 256 + 1])
 def test_fused_scan_threshold(gsm, cuda, oracle, n):
-    """The scatter workgroups' bases from the block-sum groups (r06, kSumGroup = 64 projection blocks per
-    group) at one full group, one block past it, and around r05's old limit of the fused scan (8192
-    blocks, beyond which k_scan_blocks ran): all bit-exact."""
+    """Frame sizes of 64 and 65 projection blocks (small fused scans), the last size whose block counts the
+    scatter workgroups add up themselves (8192 blocks, kFusedScanMaxBlocks) and the first one that takes
+    the k_scan_blocks launch: all bit-exact."""
     case = _synth(n, 320, 180, 1, 1, 41, scale_px=0.6)
     r = oracle_render(oracle, case)
     g = gpu_render(gsm, cuda, case, keep=False)
@@ -619,11 +619,10 @@ def test_create_time_switches_frames_match(gsm, cuda, oracle, monkeypatch, env):
 
 @pytest.mark.parametrize("fused", ["1", "0"])
 def test_scan_modes_frame_sequence(gsm, cuda, oracle, monkeypatch, fused):
-    """The block-count scan (GSM_SCAN_FUSED, read at create): the scatter adding up the block-sum groups
-    and block counts before its own (default, r06: any size; the groups alternate by frame parity and are
-    zeroed by the next frame's projection) or the k_scan_blocks launch.  One renderer renders a sequence of
-    different frames -- several sizes, an empty frame in between (no projection blocks: the parity does not
-    flip and the scan kernel writes its header) -- each bit for bit against the oracle."""
+    """The block-count scan (GSM_SCAN_FUSED, read at create): the scatter adding up every earlier block
+    count (default up to 8192 blocks) or the k_scan_blocks launch.  One renderer renders a sequence of
+    different frames -- several sizes, an empty frame in between (no projection blocks: the scan kernel
+    writes its header) -- each bit for bit against the oracle."""
     monkeypatch.setenv("GSM_SCAN_FUSED", fused)
     cases = [_synth(200_000, 1280, 720, 16, 1, 51), _synth(40_000, 1280, 720, 4, 1, 52),
              _synth(200_000, 1280, 720, 16, 1, 53), _synth(9_000, 1280, 720, 9, 1, 54)]

@@ -42,6 +42,19 @@ struct ByteLut {
     uint16_t div255[256];
     float level[256];
 };
+// fp16 input: the gaussian's 32-B world record loaded before the byte table's load and barrier, so the
+// two memory round trips overlap (r06)
+template <bool HALF>
+__device__ __forceinline__ void preload_world(const void* __restrict__ world, uint32_t gid, uint32_t count, uint4 (&w)[2]) {
+    w[0] = w[1] = make_uint4(0u, 0u, 0u, 0u);
+    if constexpr (HALF) {
+        if (gid < count) {
+            const uint4* wp = (const uint4*)((const PackedWorldGaussianHalf*)world + gid);
+            w[0] = wp[0];
+            w[1] = wp[1];
+        }
+    }
+}
 __device__ __forceinline__ void fill_byte_lut(ByteLut& L, const float2* __restrict__ sincos) {
     const uint2 e = ((const uint2*)(sincos + kSincosEntries))[threadIdx.x];
     L.level[threadIdx.x] = __uint_as_float(e.x);
@@ -55,7 +68,7 @@ __device__ __forceinline__ ProjOut project_gaussian(const void* __restrict__ wor
                                                     const void* __restrict__ harm, uint32_t gid,
                                                     const ProjectArgs& P,
                                                     const float2* __restrict__ sincos,
-                                                    const ByteLut& lut) {
+                                                    const ByteLut& lut, const uint4* preWorld = nullptr) {
     ProjOut o;
     o.vis = false;
     o.countable = false;
@@ -64,8 +77,15 @@ __device__ __forceinline__ ProjOut project_gaussian(const void* __restrict__ wor
         const CameraUniforms& cam = P.cam;
         float pos[3], scale[3], rot[4], opacity;
         if constexpr (HALF) {
-            const uint4* wp = (const uint4*)((const PackedWorldGaussianHalf*)world + gid);
-            uint4 w0 = wp[0], w1 = wp[1];
+            uint4 w0, w1;
+            if (preWorld) {  // loaded by the kernel before the byte table's barrier
+                w0 = preWorld[0];
+                w1 = preWorld[1];
+            } else {
+                const uint4* wp = (const uint4*)((const PackedWorldGaussianHalf*)world + gid);
+                w0 = wp[0];
+                w1 = wp[1];
+            }
             pos[0] = __builtin_bit_cast(float, w0.x);
             pos[1] = __builtin_bit_cast(float, w0.y);
             pos[2] = __builtin_bit_cast(float, w0.z);
@@ -309,6 +329,8 @@ __global__ __launch_bounds__(kProjectBlock) void k_project(
     constexpr uint32_t kCandCap = 4096, kCandRect = 64;
     constexpr uint16_t kSearch = 0xFFFFu;
     __shared__ uint16_t sCand[kCandCap];
+    uint4 preW[2];
+    preload_world<HALF>(world, blk * kProjectBlock + threadIdx.x, P.count, preW);
     fill_byte_lut(lut, sincos);
     const uint32_t tid = threadIdx.x;
     const uint32_t gid = blk * kProjectBlock + tid;
@@ -319,7 +341,7 @@ __global__ __launch_bounds__(kProjectBlock) void k_project(
     uint32_t area = 0;
     int ty0 = 0;
     if (gid < P.count) {
-        o = project_gaussian<HALF, DEG>(world, harm, gid, P, sincos, lut);
+        o = project_gaussian<HALF, DEG>(world, harm, gid, P, sincos, lut, HALF ? preW : nullptr);
         outBounds[gid] = o.bounds;
         if (o.vis) {
             // GaussianRenderData: the frame itself only reads it for rects the scatter re-tests
@@ -524,6 +546,8 @@ __global__ __launch_bounds__(kProjectBlock) void k_project_part(
     // over the slab bounds (contiguous) or a division (interleaved)
     constexpr uint32_t kRowTab = 512;
     __shared__ uint8_t sRowSlab[kRowTab];
+    uint4 preW[2];
+    preload_world<HALF>(world, blk * kProjectBlock + threadIdx.x, P.count, preW);
     fill_byte_lut(lut, sincos);
     const uint32_t tid = threadIdx.x;
     const uint32_t gid = blk * kProjectBlock + tid;
@@ -547,7 +571,7 @@ __global__ __launch_bounds__(kProjectBlock) void k_project_part(
     o.bounds = make_short4(0, -1, 0, -1);
     uint32_t area = 0;
     if (gid < P.count) {
-        o = project_gaussian<HALF, DEG>(world, harm, gid, P, sincos, lut);
+        o = project_gaussian<HALF, DEG>(world, harm, gid, P, sincos, lut, HALF ? preW : nullptr);
         if (o.vis && o.countable)
             area = (uint32_t)(((int)o.bounds.w - (int)o.bounds.z + 1) * ((int)o.bounds.y - (int)o.bounds.x + 1));
     }

@@ -19,7 +19,7 @@ for l in open(sys.argv[3]):
     if l.startswith("{") and '"metric"' in l: fps = json.loads(l)["value"]
 print(f"{sys.argv[2]:28s} k_project {pick('void gsm::k_project<'):7.1f}  down1 {pick('void gsm::k_radix_downsweep<7, false, false>') if 'cfg3' in sys.argv[2] else pick('void gsm::k_radix_downsweep<6, false, false>'):6.1f}"
       f"  down2 {pick('void gsm::k_radix_downsweep<7, false, true>') if 'cfg3' in sys.argv[2] else pick('void gsm::k_radix_downsweep<6, false, true>'):6.1f}  tile_sort {pick('void gsm::k_tile_sort<'):6.1f}"
-      f"  scatter {pick('gsm::k_scatter'):6.1f}  blend {pick('void gsm::k_blend'):6.1f}  fps {fps:7.1f}")
+      f"  scatter {pick('gsm::k_scatter'):6.1f}  blend {pick('void gsm::k_blend'):6.1f}  wide_down {pick('void gsm::k_wide_downsweep'):6.1f}  fps {fps:7.1f}")
 PY
 }
 run() {  # label lib cfg [env...]
@@ -32,7 +32,7 @@ run() {  # label lib cfg [env...]
 for rep in $(seq 1 ${REPS:-2}); do
   for v in ${VARIANTS:-cur}; do
     if [ $v = cur ]; then lib=$PWD/gsm-renderer_amd/lib/libgsm_amd.so; else lib=$PWD/gsm-renderer_amd/lib_ab_$v/libgsm_amd.so; fi
-    for cfg in cfg2_1m_sh3_1080p_f16 cfg3_5m_sh3_4k_f16; do
+    for cfg in ${CFGS:-cfg2_1m_sh3_1080p_f16 cfg3_5m_sh3_4k_f16}; do
       run ${v}_${cfg%%_*}_r$rep $lib $cfg || exit 1
     done
   done

@@ -350,6 +350,30 @@ void tile_depth_sort(uint32_t* keysIn, uint32_t* valsIn, uint32_t* keysOut, uint
                      bool ballot, uint32_t* half0, uint32_t* half1, uint32_t* halfCount, uint32_t tileCount,
                      bool full, int numCUs);
 
+// Unpredicated loads of 4-word groups p[i, i + 4) (i % 4 == 0) ending at n.  A load under a condition
+// whose value is used under the same condition is issued alone and waited for before the next one (the
+// compiler's diamond per group: r06, every k_scan_blocks / upsweep / tile-sort / schedule load was its own
+// memory round trip).  Here the 16-B load's index is clamped to the last whole group and the ragged group
+// at n & ~3 comes from `t` (three uniform loads, once per thread), so all loads go out before any wait.
+// Words at and past n are unspecified (callers mask them).  Needs n >= 1 and 16 readable bytes at p.
+struct Tail4 {
+    uint32_t n4, last4, t[3];
+};
+__device__ __forceinline__ Tail4 tail4_load(const uint32_t* __restrict__ p, uint32_t n) {
+    Tail4 T;
+    T.n4 = n & ~3u;
+    T.last4 = T.n4 >= 4u ? T.n4 - 4u : 0u;
+#pragma unroll
+    for (uint32_t j = 0; j < 3; ++j) T.t[j] = p[min(T.n4 + j, n - 1u)];
+    return T;
+}
+__device__ __forceinline__ uint4 load4_clamped(const uint32_t* __restrict__ p, uint32_t i, const Tail4& T) {
+    return *(const uint4*)(p + min(i, T.last4));
+}
+__device__ __forceinline__ uint4 fix4(uint4 q, uint32_t i, const Tail4& T) {
+    return i == T.n4 ? make_uint4(T.t[0], T.t[1], T.t[2], 0u) : q;
+}
+
 // Blend schedule (the blend's unit order): the units in descending order of the walk each made
 // in the previous frame (longest-processing-time-first list scheduling on the blend's persistent
 // waves), as a counting sort into kUoBuckets buckets of walk length (bucket width = max walk /
@@ -374,12 +398,9 @@ __device__ __forceinline__ void unit_order_block(const uint16_t* __restrict__ co
     static_assert(NT >= (int)kUoBuckets && NT % 64 == 0, "one thread per bucket");
     constexpr uint32_t UN = 8;
     const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
-    auto load = [&](uint32_t b0, uint32_t (&c)[UN]) {
+    auto load = [&](uint32_t b0, uint32_t (&c)[UN]) {  // (b0 < n; unpredicated, clamped: see Tail4)
 #pragma unroll
-        for (uint32_t k = 0; k < UN; ++k) {
-            const uint32_t i = b0 + k * (uint32_t)NT + t;
-            c[k] = i < n ? (uint32_t)cost[i] : 0u;
-        }
+        for (uint32_t k = 0; k < UN; ++k) c[k] = (uint32_t)cost[min(b0 + k * (uint32_t)NT + t, n - 1u)];
     };
     // the longest walk: the previous frame's blend left each wave's longest in one of kCostMaxSlots
     // words (atomicMax at its exit); read them and clear them for this frame's blend

@@ -856,6 +856,13 @@ __device__ __forceinline__ uint64_t scan_exact64(uint64_t v, uint32_t* lds, uint
     *total = ((uint64_t)hiTot << 16) + loTot;
     return ((uint64_t)hiOff << 16) + loOff;
 }
+// sums[i, i + 4) with zeros at and past nb, from unpredicated loads (Tail4, gsm_internal.h: conditional
+// loads made config 3's 19.5K sums five memory round trips, r06)
+__device__ __forceinline__ uint4 pick_sums4(uint4 q, uint32_t i, uint32_t nb, const Tail4& T) {
+    if (i >= nb) return make_uint4(0u, 0u, 0u, 0u);
+    if (i != T.n4) return q;
+    return make_uint4(T.t[0], i + 1u < nb ? T.t[1] : 0u, i + 2u < nb ? T.t[2] : 0u, 0u);
+}
 __global__ __launch_bounds__(kScanThreads) void k_scan_blocks(uint32_t* __restrict__ sums,
                                                               uint32_t nb, uint32_t maxAssignments,
                                                               TileAssignmentHeader* __restrict__ hdr,
@@ -877,13 +884,13 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_blocks(uint32_t* __restri
         constexpr uint32_t kV = 8;
         uint4 v[kV];
         const uint32_t b0 = threadIdx.x * per;
+        const Tail4 T = tail4_load(sums, nb);
+#pragma unroll
+        for (uint32_t r = 0; r < kV; ++r) v[r] = load4_clamped(sums, b0 + 4u * r, T);
 #pragma unroll
         for (uint32_t r = 0; r < kV; ++r) {
             const uint32_t i = b0 + 4u * r;
-            v[r] = (4u * r < per && i + 3u < nb) ? *(const uint4*)(sums + i)
-                   : (4u * r < per ? make_uint4(i < nb ? sums[i] : 0u, i + 1u < nb ? sums[i + 1u] : 0u,
-                                                i + 2u < nb ? sums[i + 2u] : 0u, 0u)
-                                   : make_uint4(0u, 0u, 0u, 0u));
+            v[r] = 4u * r < per ? pick_sums4(v[r], i, nb, T) : make_uint4(0u, 0u, 0u, 0u);
         }
         uint64_t local = 0;
 #pragma unroll
@@ -912,15 +919,13 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_blocks(uint32_t* __restri
         carry = tot;
         nb = 0;  // (the row loop below has nothing left)
     }
+    const Tail4 T = tail4_load(sums, nb > 0u ? nb : 1u);
     for (uint32_t base = 0; base < nb; base += kScanRows * kRow) {
         uint4 v[kScanRows];
 #pragma unroll
-        for (uint32_t r = 0; r < kScanRows; ++r) {
-            const uint32_t i = base + r * kRow + t4;
-            v[r] = i + 3u < nb ? *(const uint4*)(sums + i)
-                               : make_uint4(i < nb ? sums[i] : 0u, i + 1u < nb ? sums[i + 1u] : 0u,
-                                            i + 2u < nb ? sums[i + 2u] : 0u, 0u);
-        }
+        for (uint32_t r = 0; r < kScanRows; ++r) v[r] = load4_clamped(sums, base + r * kRow + t4, T);
+#pragma unroll
+        for (uint32_t r = 0; r < kScanRows; ++r) v[r] = pick_sums4(v[r], base + r * kRow + t4, nb, T);
 #pragma unroll
         for (uint32_t r = 0; r < kScanRows; ++r) {
             const uint32_t row0 = base + r * kRow;

@@ -16,6 +16,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
+#include <type_traits>
 #include <unordered_map>
 
 #include "gsm_internal.h"
@@ -114,14 +115,13 @@ __global__ __launch_bounds__(kRadixBlock) void k_radix_upsweep(const uint32_t* _
     // a chunk's keys are all loaded before any is counted (16 loads in flight per thread), and the
     // next chunk's loads are issued before this chunk's counting starts (its LDS atomics hide them);
     // order does not matter for a histogram, so they come as 16-byte vectors
+    // (unpredicated, the ragged end from T: see Tail4; keys at and past `end` are not counted)
+    const Tail4 T = tail4_load(keys, end > 0u ? end : 1u);
     auto load_chunk = [&](uint32_t cbase, uint4 (&q)[kRadixItems / 4]) {
 #pragma unroll
-        for (int i = 0; i < kRadixItems / 4; ++i) {
-            const uint32_t idx = cbase + (uint32_t)(i * kRadixBlock + threadIdx.x) * 4u;
-            q[i] = idx + 3u < end ? *(const uint4*)(keys + idx)
-                                  : make_uint4(idx < end ? keys[idx] : 0u, idx + 1u < end ? keys[idx + 1u] : 0u,
-                                               idx + 2u < end ? keys[idx + 2u] : 0u, 0u);
-        }
+        for (int i = 0; i < kRadixItems / 4; ++i) q[i] = load4_clamped(keys, cbase + (uint32_t)(i * kRadixBlock + threadIdx.x) * 4u, T);
+#pragma unroll
+        for (int i = 0; i < kRadixItems / 4; ++i) q[i] = fix4(q[i], cbase + (uint32_t)(i * kRadixBlock + threadIdx.x) * 4u, T);
     };
     uint4 q[kRadixItems / 4];
     if (begin < end) load_chunk(begin, q);
@@ -481,14 +481,13 @@ __global__ __launch_bounds__(kRadixBlock) void k_wide_upsweep(const uint32_t* __
     if (begin >= end) return;  // no row: k_wide_scan reads the active blocks' rows only
     for (uint32_t i = threadIdx.x; i < R; i += kRadixBlock) cnt[i] = 0;
     __syncthreads();
+    // (unpredicated, the ragged end from T: see Tail4; keys at and past `end` are not counted)
+    const Tail4 T = tail4_load(keys, end);
     auto load_chunk = [&](uint32_t cbase, uint4 (&q)[kWideItems / 4]) {
 #pragma unroll
-        for (int i = 0; i < kWideItems / 4; ++i) {
-            const uint32_t idx = cbase + (uint32_t)(i * kRadixBlock + threadIdx.x) * 4u;
-            q[i] = idx + 3u < end ? *(const uint4*)(keys + idx)
-                                  : make_uint4(idx < end ? keys[idx] : 0u, idx + 1u < end ? keys[idx + 1u] : 0u,
-                                               idx + 2u < end ? keys[idx + 2u] : 0u, 0u);
-        }
+        for (int i = 0; i < kWideItems / 4; ++i) q[i] = load4_clamped(keys, cbase + (uint32_t)(i * kRadixBlock + threadIdx.x) * 4u, T);
+#pragma unroll
+        for (int i = 0; i < kWideItems / 4; ++i) q[i] = fix4(q[i], cbase + (uint32_t)(i * kRadixBlock + threadIdx.x) * 4u, T);
     };
     uint4 q[kWideItems / 4];
     if (begin < end) load_chunk(begin, q);
@@ -1147,14 +1146,30 @@ __global__ __launch_bounds__(kTsThreads) void k_tile_sort(
     const uint32_t E = (n + kTsThreads - 1) / kTsThreads;  // items per thread
     const uint32_t seg = wave * 64u * E;                    // this wave's segment of the run
     uint32_t x[kTsItems], pos[kTsItems];
-    // all of the run's keys and values in flight at once (one memory latency per tile); word =
-    // depth << 16 | position in the run; the values wait in LDS for the sorted positions
+    // all of the run's keys and values in flight at once (one memory latency per tile): unpredicated loads
+    // at clamped indices for the first 2, 4 or 8 items (E is uniform), masked afterwards -- a load under
+    // `i < n` whose value was used under it went out alone with its own wait (one round trip per item,
+    // r06).  Word = depth << 16 | position in the run; the values wait in LDS for the sorted positions.
+    auto load_run = [&](auto ne) {
+        constexpr uint32_t NE = decltype(ne)::value;
+#pragma unroll
+        for (uint32_t j = 0; j < NE; ++j) {
+            const uint32_t i = min(seg + j * 64u + lane, n - 1u);
+            x[j] = kin[i];
+            pos[j] = vin[i];
+        }
+#pragma unroll
+        for (uint32_t j = NE; j < kTsItems; ++j) x[j] = pos[j] = 0u;
+    };
+    if (E <= 2u) load_run(std::integral_constant<uint32_t, 2>{});
+    else if (E <= 4u) load_run(std::integral_constant<uint32_t, 4>{});
+    else load_run(std::integral_constant<uint32_t, kTsItems>{});
 #pragma unroll
     for (uint32_t j = 0; j < kTsItems; ++j) {
         const uint32_t i = seg + j * 64u + lane;
         const bool ok = j < E && i < n;
-        x[j] = ok ? ((kin[i] & 0xFFFFu) << 16) | i : 0u;
-        pos[j] = ok ? vin[i] : 0u;
+        x[j] = ok ? ((x[j] & 0xFFFFu) << 16) | i : 0u;
+        pos[j] = ok ? pos[j] : 0u;
     }
 #pragma unroll
     for (uint32_t j = 0; j < kTsItems; ++j) {

@@ -19,7 +19,8 @@ for l in open(sys.argv[3]):
     if l.startswith("{") and '"metric"' in l: fps = json.loads(l)["value"]
 print(f"{sys.argv[2]:28s} k_project {pick('void gsm::k_project<'):7.1f}  down1 {pick('void gsm::k_radix_downsweep<7, false, false>') if 'cfg3' in sys.argv[2] else pick('void gsm::k_radix_downsweep<6, false, false>'):6.1f}"
       f"  down2 {pick('void gsm::k_radix_downsweep<7, false, true>') if 'cfg3' in sys.argv[2] else pick('void gsm::k_radix_downsweep<6, false, true>'):6.1f}  tile_sort {pick('void gsm::k_tile_sort<'):6.1f}"
-      f"  scatter {pick('gsm::k_scatter'):6.1f}  blend {pick('void gsm::k_blend'):6.1f}  wide_down {pick('void gsm::k_wide_downsweep'):6.1f}  fps {fps:7.1f}")
+      f"  scatter {pick('gsm::k_scatter'):6.1f}  blend {pick('void gsm::k_blend'):6.1f}  wide_down {pick('void gsm::k_wide_downsweep'):6.1f}"
+      f"  up {pick('void gsm::k_radix_upsweep'):5.1f}  scan {pick('gsm::k_scan_blocks'):5.1f}  fps {fps:7.1f}")
 PY
 }
 run() {  # label lib cfg [env...]

@@ -638,9 +638,8 @@ __device__ __forceinline__ void store_color_px(int fmt, char* dst, uint32_t rg, 
 template <int BLOCK>
 __device__ __forceinline__ uint32_t block_reduce_add(uint32_t v, uint32_t* lds) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    if (lane == 0) lds[wave] = v;
+    v = wave_scan_incl(v);  // (DPP; lane 63 holds the wave's sum)
+    if (lane == 63) lds[wave] = v;
     __syncthreads();
     uint32_t s = 0;
 #pragma unroll
@@ -649,15 +648,7 @@ __device__ __forceinline__ uint32_t block_reduce_add(uint32_t v, uint32_t* lds) 
 }
 
 // Inclusive scan inside a wave of 64 lanes.
-__device__ __forceinline__ uint32_t wave_inclusive_scan(uint32_t v) {
-    const int lane = threadIdx.x & 63;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        uint32_t t = __shfl_up(v, o, 64);
-        if (lane >= o) v += t;
-    }
-    return v;
-}
+__device__ __forceinline__ uint32_t wave_inclusive_scan(uint32_t v) { return wave_scan_incl(v); }
 // Exclusive scan over a block; returns the block total in *total.
 template <int BLOCK>
 __device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t v, uint32_t* lds, uint32_t* total) {

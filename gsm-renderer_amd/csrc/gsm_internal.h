@@ -350,6 +350,27 @@ void tile_depth_sort(uint32_t* keysIn, uint32_t* valsIn, uint32_t* keysOut, uint
                      bool ballot, uint32_t* half0, uint32_t* half1, uint32_t* halfCount, uint32_t tileCount,
                      bool full, int numCUs);
 
+// Inclusive prefix sum over the 64 lanes of a wave by DPP (row_shr 1/2/4/8 within rows of 16, then
+// row_bcast 15 / 31 across rows): six VALU adds with their operand moved by the DPP unit, where a
+// __shfl_up step is a ds_bpermute (an LDS round trip; six of them per scan -- r06: the sorts' digit
+// scans and the block scans).  All 64 lanes must be active.
+__device__ __forceinline__ uint32_t wave_scan_incl(uint32_t v) {
+#if defined(GSM_AB_SHFL_SCAN)
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t t = __shfl_up(v, o, 64);
+        if ((threadIdx.x & 63u) >= (uint32_t)o) v += t;
+    }
+    return v;
+#endif
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, true);   // row_shr:1
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, true);   // row_shr:2
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, true);   // row_shr:4
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, true);   // row_shr:8
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);  // row_bcast:15 -> rows 1, 3
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false);  // row_bcast:31 -> rows 2, 3
+    return v;
+}
+
 // Unpredicated loads of 4-word groups p[i, i + 4) (i % 4 == 0) ending at n.  A load under a condition
 // whose value is used under the same condition is issued alone and waited for before the next one (the
 // compiler's diamond per group: r06, every k_scan_blocks / upsweep / tile-sort / schedule load was its own
@@ -425,11 +446,7 @@ __device__ __forceinline__ void unit_order_block(const uint16_t* __restrict__ co
     if (w == 0) {
         const uint4 c = *(const uint4*)(base + lane * 4u);
         const uint32_t local = c.x + c.y + c.z + c.w;
-        uint32_t inc = local;
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t v = __shfl_up(inc, o, 64);
-            if (lane >= (uint32_t)o) inc += v;
-        }
+        const uint32_t inc = wave_scan_incl(local);
         const uint32_t e = inc - local;
         const uint4 starts = make_uint4(e, e + c.x, e + c.x + c.y, e + c.x + c.y + c.z);
         *(uint4*)(base + lane * 4u) = starts;

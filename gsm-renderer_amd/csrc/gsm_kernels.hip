@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdlib>
+#include <type_traits>
 
 #include "gsm_device.h"
 #include "gsm_detmath.h"
@@ -997,22 +998,56 @@ __device__ __forceinline__ uint64_t block_sum_prefix(const uint32_t* __restrict_
     uint64_t v = 0;
     const uint32_t n4 = n & ~3u;
     constexpr uint32_t kStep = kProjectBlock * 4u;
-    uint32_t i = threadIdx.x * 4u;
-    for (; i + 3u * kStep < n4; i += 4u * kStep) {  // four 16-B loads in flight per thread
-        uint4 q[4];
+    // up to 8 * kStep sums (the fused scan's kFusedScanMaxBlocks): 1, 2, 4 or 8 unpredicated 16-B loads per
+    // thread, up to four in flight at once, the ragged end from Tail4 and the words past n masked (r06: the
+    // loop below waited for each of its tail loads in turn -- up to four round trips before a scatter
+    // workgroup knew its base)
+    // (whole groups below n & ~3 from the clamped loads, the ragged end -- uniform loads -- added by thread 0;
+    // at most 4 loads in flight, so k_scatter keeps its 58 VGPRs and 8 waves per SIMD)
+    auto sum_groups = [&](auto ng) {
+        constexpr uint32_t NG = decltype(ng)::value, NR = NG < 4u ? NG : 4u;
+        const Tail4 T = tail4_load(sums, n);
 #pragma unroll
-        for (uint32_t k = 0; k < 4; ++k) q[k] = *(const uint4*)(sums + i + k * kStep);
+        for (uint32_t r = 0; r < NG; r += NR) {
+            uint4 q[NR];
 #pragma unroll
-        for (uint32_t k = 0; k < 4; ++k) v += (uint64_t)q[k].x + q[k].y + q[k].z + q[k].w;
+            for (uint32_t k = 0; k < NR; ++k) q[k] = load4_clamped(sums, threadIdx.x * 4u + (r + k) * kStep, T);
+#pragma unroll
+            for (uint32_t k = 0; k < NR; ++k)
+                if (threadIdx.x * 4u + (r + k) * kStep < T.n4) v += (uint64_t)q[k].x + q[k].y + q[k].z + q[k].w;
+        }
+        if (threadIdx.x == 0)
+            v += (uint64_t)(T.n4 < n ? T.t[0] : 0u) + (T.n4 + 1u < n ? T.t[1] : 0u) + (T.n4 + 2u < n ? T.t[2] : 0u);
+    };
+    if (n == 0u) {
+    } else if (n <= kStep) {
+        sum_groups(std::integral_constant<uint32_t, 1>{});
+    } else if (n <= 2u * kStep) {
+        sum_groups(std::integral_constant<uint32_t, 2>{});
+    } else if (n <= 4u * kStep) {
+        sum_groups(std::integral_constant<uint32_t, 4>{});
+    } else if (n <= 8u * kStep) {
+        sum_groups(std::integral_constant<uint32_t, 8>{});
+    } else {
+        uint32_t i = threadIdx.x * 4u;
+        for (; i + 3u * kStep < n4; i += 4u * kStep) {  // four 16-B loads in flight per thread
+            uint4 q[4];
+#pragma unroll
+            for (uint32_t k = 0; k < 4; ++k) q[k] = *(const uint4*)(sums + i + k * kStep);
+#pragma unroll
+            for (uint32_t k = 0; k < 4; ++k) v += (uint64_t)q[k].x + q[k].y + q[k].z + q[k].w;
+        }
+        for (; i < n4; i += kStep) {
+            const uint4 q = *(const uint4*)(sums + i);
+            v += (uint64_t)q.x + q.y + q.z + q.w;
+        }
+        if (threadIdx.x < n - n4) v += sums[n4 + threadIdx.x];
     }
-    for (; i < n4; i += kStep) {
-        const uint4 q = *(const uint4*)(sums + i);
-        v += (uint64_t)q.x + q.y + q.z + q.w;
-    }
-    if (threadIdx.x < n - n4) v += sums[n4 + threadIdx.x];
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += (uint64_t)__shfl_xor((unsigned long long)v, o, 64);
-    if ((threadIdx.x & 63u) == 0) lds64[threadIdx.x >> 6] = v;
+    // the wave's sum exactly in two 32-bit DPP scans: v < 2^52 (< 2^20 words per thread), so the 64 lanes'
+    // low 26-bit parts and their high parts each add up below 2^32
+    const uint32_t lo = wave_scan_incl((uint32_t)(v & 0x3FFFFFFull)), hi = wave_scan_incl((uint32_t)(v >> 26));
+    v = ((uint64_t)hi << 26) + lo;
+    if ((threadIdx.x & 63u) == 63u) lds64[threadIdx.x >> 6] = v;
     __syncthreads();
     uint64_t t = 0;
 #pragma unroll
@@ -1250,12 +1285,7 @@ __global__ __launch_bounds__(kHlThreads) void k_half_lists(const uint32_t* __res
         }
         // exclusive scans of the two keep counts over the block (thread order = list order)
         const uint32_t packed = k0 | (k1 << 16);
-        uint32_t inc = packed;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t x = __shfl_up(inc, o, 64);
-            if (lane >= (uint32_t)o) inc += x;
-        }
+        uint32_t inc = wave_scan_incl(packed);
         if (lane == 63) {
             part[0][wave] = inc & 0xFFFFu;
             part[1][wave] = inc >> 16;

@@ -165,12 +165,7 @@ __global__ __launch_bounds__(256) void k_radix_scan(uint32_t* __restrict__ hist,
     for (int i = 0; i < 4; ++i) v[i] = b0 + i < grid ? row[b0 + i] : 0u;
     const uint32_t local = v[0] + v[1] + v[2] + v[3];
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    uint32_t inc = local;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t t = __shfl_up(inc, o, 64);
-        if (lane >= (uint32_t)o) inc += t;
-    }
+    uint32_t inc = wave_scan_incl(local);
     if (lane == 63) part[wave] = inc;
     __syncthreads();
     uint32_t off = 0, tot = 0;
@@ -289,12 +284,7 @@ __global__ __launch_bounds__(kRadixBlock) void k_radix_downsweep(
             t = tid < R ? binTotals[tid] : 0u;
             pre = tid < R ? hist[(size_t)tid * gridDim.x + blockIdx.x] : 0u;
         }
-        uint32_t inc = t;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            uint32_t v = __shfl_up(inc, o, 64);
-            if (lane >= (uint32_t)o) inc += v;
-        }
+        uint32_t inc = wave_scan_incl(t);
         if (lane == 63) part[wave] = inc;
         __syncthreads();
         uint32_t off = 0;
@@ -361,12 +351,7 @@ __global__ __launch_bounds__(kRadixBlock) void k_radix_downsweep(
                 tot += c;
             }
             chunkTotal[tid] = tot;
-            uint32_t inc = tot;
-#pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {
-                uint32_t x = __shfl_up(inc, o, 64);
-                if (lane >= (uint32_t)o) inc += x;
-            }
+            uint32_t inc = wave_scan_incl(tot);
             if (lane == 63) part[wave] = inc;
             __syncthreads();
             uint32_t off = 0;
@@ -574,12 +559,7 @@ __global__ __launch_bounds__(256) void k_wide_scan(uint32_t* __restrict__ hist, 
 // Exclusive scan over the block of one value per thread (4 waves); returns this thread's offset.
 __device__ __forceinline__ uint32_t wide_block_scan(uint32_t x, uint32_t* part, uint32_t* total) {
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
-    uint32_t inc = x;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t t = __shfl_up(inc, o, 64);
-        if (lane >= (uint32_t)o) inc += t;
-    }
+    uint32_t inc = wave_scan_incl(x);
     if (lane == 63) part[wave] = inc;
     __syncthreads();
     uint32_t off = 0, tot = 0;
@@ -980,12 +960,7 @@ __device__ __forceinline__ void ts_offsets(uint32_t (*wcnt)[256], uint32_t* part
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
     const uint32_t c0 = wcnt[0][tid], c1 = wcnt[1][tid], c2 = wcnt[2][tid], c3 = wcnt[3][tid];
     const uint32_t tot = c0 + c1 + c2 + c3;
-    uint32_t inc = tot;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t t = __shfl_up(inc, o, 64);
-        if (lane >= (uint32_t)o) inc += t;
-    }
+    uint32_t inc = wave_scan_incl(tot);
     if (lane == 63) part[wave] = inc;
     __syncthreads();
     uint32_t off = 0;

@@ -355,13 +355,6 @@ void tile_depth_sort(uint32_t* keysIn, uint32_t* valsIn, uint32_t* keysOut, uint
 // __shfl_up step is a ds_bpermute (an LDS round trip; six of them per scan -- r06: the sorts' digit
 // scans and the block scans).  All 64 lanes must be active.
 __device__ __forceinline__ uint32_t wave_scan_incl(uint32_t v) {
-#if defined(GSM_AB_SHFL_SCAN)
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t t = __shfl_up(v, o, 64);
-        if ((threadIdx.x & 63u) >= (uint32_t)o) v += t;
-    }
-    return v;
-#endif
     v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, true);   // row_shr:1
     v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, true);   // row_shr:2
     v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, true);   // row_shr:4

@@ -635,8 +635,10 @@ __global__ __launch_bounds__(1024) void k_part_scan(uint32_t* __restrict__ block
         const uint32_t i0 = base + threadIdx.x * IT;
         uint32_t v[IT], sum = 0;
 #pragma unroll
+        for (uint32_t k = 0; k < IT; ++k) v[k] = row[min(i0 + k, numBlocks - 1u)];  // (unpredicated: Tail4 note)
+#pragma unroll
         for (uint32_t k = 0; k < IT; ++k) {
-            v[k] = i0 + k < numBlocks ? row[i0 + k] : 0u;
+            v[k] = i0 + k < numBlocks ? v[k] : 0u;
             sum += v[k];
         }
         uint32_t tot;
@@ -674,23 +676,45 @@ __global__ __launch_bounds__(kProjectBlock) void k_part_copy(
     const uint32_t* __restrict__ counts, SlabPeers peers, uint32_t* __restrict__ recvCount, MgArrive arrive,
     SplatRecord* __restrict__ send, uint64_t capacity) {
     __shared__ uint32_t sBase[kMaxSlabs], sTotal[kMaxSlabs];
+    // the count matrix (PUSH: world x world words, system-coherent loads) or the slab totals, one word per
+    // thread in a single round of loads (r06: each thread summed its column in a loop -- one load round
+    // trip after another, up to world of them for the last rank, and world more for block 0's receive count)
+    __shared__ uint32_t sCnt[kMaxSlabs * kMaxSlabs];
+    // (PUSH: the peers' receive buffers and capacities too -- indexed by slab, the kernel-argument arrays
+    // were two dependent memory round trips per run)
+    __shared__ SplatRecord* sRecv[kMaxSlabs];
+    __shared__ uint32_t sCap[kMaxSlabs];
+    const uint32_t nCnt = PUSH ? numSlabs * numSlabs : numSlabs;
+    static_assert(kMaxSlabs * kMaxSlabs <= kProjectBlock, "one count-matrix word per thread");
+    {  // (loads unpredicated at clamped indices, all before the first LDS store: one round trip)
+        const uint32_t tc = min((uint32_t)threadIdx.x, nCnt - 1u), ts = min((uint32_t)threadIdx.x, numSlabs - 1u);
+        const uint32_t cv = PUSH ? ld_sys32(counts + tc) : totals[tc];
+        SplatRecord* const rv = PUSH ? peers.recv[ts] : nullptr;
+        const uint32_t capv = PUSH ? peers.cap[ts] : 0u;
+        if (threadIdx.x < nCnt) sCnt[threadIdx.x] = cv;
+        if (PUSH && threadIdx.x < numSlabs) {
+            sRecv[threadIdx.x] = rv;
+            sCap[threadIdx.x] = capv;
+        }
+    }
+    __syncthreads();
     if (threadIdx.x < numSlabs) {
         const uint32_t sl = threadIdx.x;
         uint32_t base = 0;
         if constexpr (PUSH) {
-            for (uint32_t r = 0; r < rank; ++r) base += ld_sys32(counts + r * numSlabs + sl);
-            sTotal[sl] = ld_sys32(counts + rank * numSlabs + sl);
+            for (uint32_t r = 0; r < rank; ++r) base += sCnt[r * numSlabs + sl];
+            sTotal[sl] = sCnt[rank * numSlabs + sl];
         } else {
-            for (uint32_t t = 0; t < sl; ++t) base += totals[t];
-            sTotal[sl] = totals[sl];
+            for (uint32_t t = 0; t < sl; ++t) base += sCnt[t];
+            sTotal[sl] = sCnt[sl];
         }
         sBase[sl] = base;
     }
     if constexpr (PUSH) {
         if (blockIdx.x == 0 && threadIdx.x == 0) {
             uint32_t mine = 0;
-            for (uint32_t r = 0; r < numSlabs; ++r) mine += ld_sys32(counts + r * numSlabs + rank);
-            *recvCount = min(mine, peers.cap[rank]);
+            for (uint32_t r = 0; r < numSlabs; ++r) mine += sCnt[r * numSlabs + rank];
+            *recvCount = min(mine, sCap[rank]);
         }
     }
     __syncthreads();
@@ -719,15 +743,27 @@ __global__ __launch_bounds__(kProjectBlock) void k_part_copy(
             const uint32_t b = k / numSlabs, sl = k - b * numSlabs;
             const uint4* src = (const uint4*)(runs + (size_t)sl * runStride + (size_t)b * kProjectBlock);
             const uint64_t at = (uint64_t)sBase[sl] + off;  // the run's first record at the destination
-            if constexpr (PUSH) {
-                const uint64_t cap = peers.cap[sl];
-                const uint32_t m = at >= cap ? 0u : (uint32_t)min((uint64_t)n, cap - at);  // never past it
-                uint4* d = (uint4*)(peers.recv[sl] + at);
-                for (uint32_t w = lane; w < 3u * m; w += 64u) st_sys128(d, 3u * m * 16u, w, src[w]);
-            } else {
-                const uint32_t m = at >= capacity ? 0u : (uint32_t)min((uint64_t)n, capacity - at);
-                uint4* d = (uint4*)(send + at);
-                for (uint32_t w = lane; w < 3u * m; w += 64u) d[w] = src[w];
+            // four 16-B words per lane in flight before the stores (unpredicated loads at clamped indices;
+            // a load-store pair per word was one round trip per 1 KiB of the run, r06)
+            const uint64_t cap = PUSH ? (uint64_t)sCap[sl] : capacity;
+            const uint32_t m = at >= cap ? 0u : (uint32_t)min((uint64_t)n, cap - at);  // never past it
+            // Stores at clamped indices too: a word past the run rewrites the run's last word with its own
+            // value, so no store (and no load sunk into it) sits under a condition.  The destination is
+            // made wave-uniform explicitly (a buffer descriptor from VGPRs costs a waterfall loop per store).
+            const uint32_t words = (uint32_t)__builtin_amdgcn_readfirstlane((int)(3u * m));
+            const uint64_t dA = (uint64_t)(uintptr_t)(PUSH ? (void*)(sRecv[sl] + at) : (void*)(send + at));
+            uint4* d = (uint4*)(uintptr_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(dA >> 32)) << 32) |
+                                           (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)dA));
+            for (uint32_t w0 = lane; w0 < words; w0 += 256u) {
+                uint4 v[4];
+#pragma unroll
+                for (uint32_t q = 0; q < 4; ++q) v[q] = src[min(w0 + 64u * q, words - 1u)];
+#pragma unroll
+                for (uint32_t q = 0; q < 4; ++q) {
+                    const uint32_t w = min(w0 + 64u * q, words - 1u);
+                    if constexpr (PUSH) st_sys128(d, words * 16u, w, v[q]);
+                    else d[w] = v[q];
+                }
             }
         }
     }

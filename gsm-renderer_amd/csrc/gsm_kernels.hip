@@ -806,11 +806,13 @@ __global__ __launch_bounds__(kProjectBlock) void k_records_in(
         // peers' k_part_copy over xGMI; no L1 / L2 line of an earlier frame may answer
         const uint32_t words = 3u * (min(n - blk * kProjectBlock, (uint32_t)kProjectBlock));
         const SplatRecord* src = in + (size_t)blk * kProjectBlock;
+        // (unconditional: a word past the block's records is outside the buffer descriptor's range and
+        // reads as 0 -- a load under `i < words` went out alone with its own wait, r06)
+        uint4 t[3];
 #pragma unroll
-        for (uint32_t j = 0; j < 3; ++j) {
-            const uint32_t i = threadIdx.x + j * kProjectBlock;
-            if (i < words) sIn[i] = ld_sys128(src, words * 16u, i);
-        }
+        for (uint32_t j = 0; j < 3; ++j) t[j] = ld_sys128(src, words * 16u, threadIdx.x + j * kProjectBlock);
+#pragma unroll
+        for (uint32_t j = 0; j < 3; ++j) sIn[threadIdx.x + j * kProjectBlock] = t[j];
     }
     __syncthreads();
     uint32_t ntiles = 0;

@@ -117,11 +117,7 @@ __global__ __launch_bounds__(NT) void k_blend_px(
     __shared__ uint32_t lrecB[NW][64];
     __shared__ uint32_t exitCount;  // a gathered multi-GPU frame: waves of this workgroup past their last unit
     if (threadIdx.x == 0) exitCount = 0;
-    {
-        const uint4* src = (const uint4*)expTable;
-        uint4* dst = (uint4*)tbl;
-        for (int i = threadIdx.x; i < 65536 * 2 / 16; i += NT) dst[i] = src[i];
-    }
+    GSM_EXP_TABLE_TO_LDS(NT, expTable, tbl);
     __syncthreads();
 
     const uint32_t lane = threadIdx.x & 63;

@@ -153,11 +153,7 @@ __global__ __launch_bounds__(NT) void k_blend_pw(
     __shared__ uint32_t cscr[NW][32];                                // layout changes: the live groups
     __shared__ __attribute__((aligned(16))) uint4 lrecA[NW][64];   // staged records: unit k at 32 k (pairs)
     __shared__ uint32_t lrecB[NW][64];
-    {
-        const uint4* src = (const uint4*)expTable;
-        uint4* dst = (uint4*)tbl;
-        for (int i = threadIdx.x; i < 65536 * 2 / 16; i += NT) dst[i] = src[i];
-    }
+    GSM_EXP_TABLE_TO_LDS(NT, expTable, tbl);
     __syncthreads();
 
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;

@@ -532,6 +532,8 @@ __global__ __launch_bounds__(NW * 64) void k_df_blend_eye(const uint32_t* __rest
     __shared__ __attribute__((aligned(16))) uint32_t stageB[NW][kDfEyeBatch];
     __shared__ uint16_t div255[256];
     {
+        // (a loop of load / wait / store per 16 B here: GSM_EXP_TABLE_TO_LDS's batched fill measured slower
+        // for this kernel, 333.5 -> 340.5 us at config 5, profiles/r06_exp_table_fill_ab.txt)
         const uint4* src = (const uint4*)expTable;
         uint4* dst = (uint4*)tbl;
         for (int i = threadIdx.x; i < 65536 * 2 / 16; i += NW * 64) dst[i] = src[i];

@@ -388,6 +388,23 @@ __device__ __forceinline__ uint4 fix4(uint4 q, uint32_t i, const Tail4& T) {
     return i == T.n4 ? make_uint4(T.t[0], T.t[1], T.t[2], 0u) : q;
 }
 
+// The blends' 128 KiB exp table from global memory into the workgroup's LDS copy: every load of a thread
+// in flight at once (unpredicated, clamped), then the 16-B LDS stores.  (A `dst[i] = src[i]` loop over
+// i += NT compiled to load / wait / store per iteration: 8-16 memory round trips, one after another, before
+// any wave could blend -- r06.)
+#define GSM_EXP_TABLE_TO_LDS(NTHREADS, expTable, tbl)                                                        \
+    do {                                                                                                     \
+        constexpr uint32_t kVec_ = 65536u * 2u / 16u, kPer_ = (kVec_ + (NTHREADS) - 1u) / (NTHREADS);        \
+        const uint4* src_ = (const uint4*)(expTable);                                                        \
+        uint4 t_[kPer_];                                                                                     \
+        _Pragma("unroll") for (uint32_t k_ = 0; k_ < kPer_; ++k_)                                            \
+            t_[k_] = src_[min((uint32_t)threadIdx.x + k_ * (uint32_t)(NTHREADS), kVec_ - 1u)];                \
+        _Pragma("unroll") for (uint32_t k_ = 0; k_ < kPer_; ++k_) {                                          \
+            const uint32_t i_ = (uint32_t)threadIdx.x + k_ * (uint32_t)(NTHREADS);                           \
+            if (i_ < kVec_) ((uint4*)(tbl))[i_] = t_[k_];                                                    \
+        }                                                                                                    \
+    } while (0)
+
 // Blend schedule (the blend's unit order): the units in descending order of the walk each made
 // in the previous frame (longest-processing-time-first list scheduling on the blend's persistent
 // waves), as a counting sort into kUoBuckets buckets of walk length (bucket width = max walk /

@@ -450,8 +450,11 @@ gsm_status GlobalRenderer::runFrame(hipStream_t s, const ProjectArgs& a, uint32_
     if (prof) hipEventRecord(ev[0], s);
     front(fa);  // the projection (or records) launch; its block 0 orders the blend units (fa.schedUnits)
     if (prof) hipEventRecord(ev[1], s);
-    // (a frame of few blocks: the scatter's workgroups add up the block counts themselves)
-    const bool fusedScan = tuning_.fusedScan && nb > 0 && nb <= kFusedScanMaxBlocks;
+    // (a frame of few blocks: the scatter's workgroups add up the block counts themselves).  The records path
+    // (devCount: a multi-GPU slab) sizes its grids for the receive capacity but adds up only the blocks of
+    // the records received -- at 8 ranks ~1/8 of a frame's gaussians -- so it takes the fused scan up to 4x
+    // the block count (a slab that receives more than 2M records pays a longer prefix instead of the launch)
+    const bool fusedScan = tuning_.fusedScan && nb > 0 && nb <= (devCount ? 4u : 1u) * kFusedScanMaxBlocks;
     if (!fusedScan) launch_scan_blocks(nb, a, arena_, s, devCount);
     if (prof) hipEventRecord(ev[2], s);
     launch_scatter(a, arena_, s, devCount, fusedScan);
